@@ -1,0 +1,199 @@
+/*
+ * srt.h -- C ABI of the MI355X-native Shadow routing-table build ("srt").
+ *
+ * This is the drop-in boundary behind Shadow's Rust network-graph API.  Each
+ * entry point names the reference interface it replaces (paths relative to the
+ * Shadow v3.1.0 tree, see INTEGRATION.md for the Rust-side binding):
+ *
+ *   srt_compute_shortest_paths  <- NetworkGraph::compute_shortest_paths
+ *                                  src/main/network/graph/mod.rs:183-228
+ *   srt_get_direct_paths        <- NetworkGraph::get_direct_paths
+ *                                  src/main/network/graph/mod.rs:230-252
+ *   min_latency_ns out-params   <- RoutingInfo::get_smallest_latency_ns
+ *                                  src/main/network/graph/mod.rs:474-476
+ *   srt_packet_batch            <- Worker::send_packet decision
+ *                                  src/main/core/worker.rs:326-410 (+ :539-553)
+ *   srt_gml_parse               <- NetworkGraph::parse / gml_parser::parse
+ *                                  src/main/network/graph/mod.rs:134-181
+ *
+ * Conventions (mirroring the reference's FFI: plain C types, no exceptions
+ * across the boundary, caller-owned outputs):
+ *   - All pointers in srt_csr / outputs are HOST pointers unless a function
+ *     says "device".  Inputs are borrowed for the duration of the call.
+ *   - Node references are petgraph NodeIndex values (0..n_nodes-1, GML order).
+ *   - out[i*n + j] is the path nodes[i] -> nodes[j] (row-major over the
+ *     caller's in-use node list, which may be in any order).
+ *   - Every function returns an srt_status and fills *err (may be NULL) with
+ *     the reference's error text for NO_EDGE / MULTI_EDGE.
+ *   - Library functions are thread-compatible: concurrent calls on different
+ *     srt_plan objects are fine; one plan is used by one thread at a time.
+ */
+#ifndef SRT_H
+#define SRT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SRT_ABI_VERSION 1
+
+typedef enum {
+    SRT_OK = 0,
+    SRT_ERR_NO_EDGE = 1,      /* "No edge connecting node {a} to {b}"   (mod.rs:267-268) */
+    SRT_ERR_MULTI_EDGE = 2,   /* "More than one edge connecting node {a} to {b}" (:270-274) */
+    SRT_ERR_DISCONNECTED = 3, /* reference panics: assert_eq!(paths.len(), n^2) (:219) */
+    SRT_ERR_INVALID = 4,      /* bad arguments / parse error */
+    SRT_ERR_HIP = 5,          /* HIP runtime failure */
+    SRT_ERR_OOM = 6,
+    SRT_ERR_UNSUPPORTED = 7,
+    SRT_ERR_COMM = 8, /* RCCL failure */
+} srt_status;
+
+typedef struct {
+    int32_t code;
+    uint32_t a_id; /* GML ids named in NO_EDGE / MULTI_EDGE messages */
+    uint32_t b_id;
+    char msg[256];
+} srt_err;
+
+/* The graph as petgraph holds it: for every NodeIndex u, the EdgeReferences of
+ * graph.edges(u) (directed: outgoing; undirected: all incident edges, the far
+ * endpoint as `col`, self-loops once).  Parallel edges are allowed. */
+typedef struct {
+    uint32_t n_nodes;
+    uint32_t directed;        /* informational; adjacency already encodes it */
+    uint64_t n_adj;           /* number of adjacency entries */
+    const uint64_t *row_ptr;  /* n_nodes + 1 */
+    const uint32_t *col;      /* n_adj */
+    const uint64_t *lat_ns;   /* n_adj, latency already converted to ns (mod.rs:336) */
+    const float *loss;        /* n_adj, packet_loss in [0,1] */
+    const uint32_t *node_ids; /* n_nodes GML ids (error text); NULL = use NodeIndex */
+} srt_csr;
+
+/* #[repr(C)] mirror of PathProperties (mod.rs:296-303), 16 bytes */
+typedef struct {
+    uint64_t latency_ns;
+    float packet_loss;
+    uint32_t _pad;
+} srt_path;
+
+typedef enum { SRT_ALGO_AUTO = 0, SRT_ALGO_FW = 1, SRT_ALGO_SSSP = 2 } srt_algo;
+
+typedef struct {
+    uint32_t algo;   /* srt_algo */
+    int32_t device;  /* HIP device ordinal, -1 = current */
+    uint32_t flags;  /* reserved, 0 */
+    uint32_t reserved;
+} srt_opts;
+
+/* ------------------------------------------------------------------ info */
+int srt_abi_version(void);
+/* number of visible HIP devices (0 when no GPU); never fails */
+int srt_device_count(void);
+
+/* ------------------------------------------------------ one-shot host API */
+/* compute_shortest_paths over the in-use nodes.  out: n*n entries (caller
+ * allocated).  *min_latency_ns (may be NULL) = get_smallest_latency_ns() of the
+ * resulting table, diagonal included. */
+srt_status srt_compute_shortest_paths(const srt_csr *g, const uint32_t *nodes, uint32_t n,
+                                      srt_path *out, uint64_t *min_latency_ns,
+                                      const srt_opts *opts, srt_err *err);
+
+/* get_direct_paths: table = the unique edge between every ordered pair. */
+srt_status srt_get_direct_paths(const srt_csr *g, const uint32_t *nodes, uint32_t n,
+                                srt_path *out, uint64_t *min_latency_ns, const srt_opts *opts,
+                                srt_err *err);
+
+/* ---------------------------------------------- device-resident plan API */
+/* A plan holds the graph and the routing table in HBM so a caller (bench,
+ * multi-GPU driver, the packet stage) can time or chain the build without
+ * PCIe copies.  Table layout in HBM: SoA, row-major n*n: u64 latency_ns and
+ * f32 packet_loss. */
+typedef struct srt_plan srt_plan;
+
+/* Uploads the graph, validates self-loops of the in-use nodes (mod.rs:210-217)
+ * and chooses the kernel family; no shortest-path work yet. */
+srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
+                           const srt_opts *opts, srt_plan **plan, srt_err *err);
+/* Full routing build on the plan's stream; blocks until done. */
+srt_status srt_plan_run(srt_plan *plan, srt_err *err);
+/* Same, enqueue only (caller synchronises with srt_plan_sync). */
+srt_status srt_plan_run_async(srt_plan *plan, srt_err *err);
+srt_status srt_plan_sync(srt_plan *plan, srt_err *err);
+/* Post-run: connectivity check + min latency; copies the table out if out != NULL. */
+srt_status srt_plan_fetch(srt_plan *plan, srt_path *out, uint64_t *min_latency_ns,
+                          srt_err *err);
+/* device pointers of the table (valid until srt_plan_destroy) */
+srt_status srt_plan_table(srt_plan *plan, uint64_t **d_latency_ns, float **d_packet_loss,
+                          uint32_t *n);
+/* human-readable kernel/representation choice, e.g. "fw:packed64 g=1000000 qb=38 s=30" */
+const char *srt_plan_describe(const srt_plan *plan);
+/* hipStream_t of the plan (as void*) */
+void *srt_plan_stream(srt_plan *plan);
+/* Timing of the last run's dominant kernel family (phase-3 of FW or the SSSP
+ * sweep): total ms and number of launches, measured with HIP events on the
+ * plan's stream. */
+srt_status srt_plan_kernel_stats(const srt_plan *plan, double *dominant_ms,
+                                 uint64_t *dominant_launches, double *total_ms);
+void srt_plan_destroy(srt_plan *plan);
+
+/* -------------------------------------------------------- multi-GPU (RCCL) */
+/* One process per GPU.  Rank 0 calls srt_comm_unique_id, ships the 128 bytes
+ * to the other ranks (e.g. torch.distributed broadcast), then every rank calls
+ * srt_comm_init on its device.  A plan bound to a communicator computes only
+ * its own source rows and all-gathers the table over xGMI. */
+typedef struct srt_comm srt_comm;
+srt_status srt_comm_unique_id(uint8_t out[128], srt_err *err);
+srt_status srt_comm_init(const uint8_t id[128], int nranks, int rank, int device,
+                         srt_comm **comm, srt_err *err);
+void srt_comm_destroy(srt_comm *comm);
+srt_status srt_plan_bind_comm(srt_plan *plan, srt_comm *comm, srt_err *err);
+
+/* ------------------------------------------------------- packet delivery */
+/* One outgoing inter-host packet, in the source host's send order. */
+typedef struct {
+    uint32_t src_host; /* index of the source host's RNG state */
+    uint32_t src_row;  /* table row of the source host's node */
+    uint32_t dst_row;  /* table column of the destination host's node */
+    uint32_t payload_size;
+    uint64_t t_ns; /* emulated time at send */
+} srt_pkt;
+
+enum { SRT_PDS_NONE = 0, SRT_PDS_INET_SENT = 1u << 8, SRT_PDS_INET_DROPPED = 1u << 9 };
+
+typedef struct {
+    uint64_t round_end_ns;
+    uint64_t bootstrap_end_ns;
+    uint64_t sim_end_ns;
+} srt_round;
+
+/* Batched Worker::send_packet decision for one scheduling round, on the device.
+ * All pointers are DEVICE pointers on the plan's device.  Packets must be
+ * grouped by source host: host_pkt_ptr[h]..host_pkt_ptr[h+1] are host h's
+ * packets in send order (n_hosts + 1 entries).  rng: 4 x u64 xoshiro256++ state
+ * per host, advanced in place by one draw per non-completed packet.
+ * flags/deliver: per packet.  counters (may be NULL): n*n u64 per-path packet
+ * counts (RoutingInfo::increment_packet_count).  stats (device, 2 x u64):
+ * [0] = min latency of sent packets (runahead), [1] = min deliver time
+ * (next event time); both UINT64_MAX when nothing was sent, and they are
+ * min-combined with their previous contents (initialise to UINT64_MAX). */
+srt_status srt_packet_batch(srt_plan *plan, const srt_pkt *d_pkts, const uint32_t *d_host_pkt_ptr,
+                            uint32_t n_hosts, uint64_t n_pkts, uint64_t *d_rng,
+                            const srt_round *round, uint32_t *d_flags, uint64_t *d_deliver,
+                            uint64_t *d_counters, uint64_t *d_stats, srt_err *err);
+
+/* --------------------------------------------------------------- GML ingest */
+/* Parses Shadow GML text (gml-parser grammar + NetworkGraph validation) into a
+ * library-owned graph; srt_gml_csr exposes its petgraph adjacency. */
+typedef struct srt_gml srt_gml;
+srt_status srt_gml_parse(const char *text, size_t len, srt_gml **out, srt_err *err);
+srt_status srt_gml_csr(const srt_gml *g, srt_csr *csr);
+void srt_gml_free(srt_gml *g);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SRT_H */

@@ -1,0 +1,100 @@
+// srt_internal.h -- shared declarations of the gfx950 routing-table build.
+// Not part of the ABI (include/srt.h is).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/srt.h"
+
+namespace srt {
+
+// Path key for the dense min-plus closure.
+//
+// The reference orders paths lexicographically by (latency_ns, packet_loss)
+// (graph/mod.rs:305-313) and folds loss as 1-(1-a)(1-b) (mod.rs:322-331).  We
+// carry loss as its additive form -ln(1-loss) in fixed point, so a path key is
+//     key = (latency / g) << qb  |  round(-ln(reliability) * 2^s)
+// and lexicographic (latency, loss) order == unsigned integer order of keys,
+// while "+" of two paths == integer "+" of keys.  The host proves that no
+// candidate sum can carry out of the loss field nor reach KEY_INF (see
+// choose_key_params in srt_api.cpp), so latency is bit-exact and the loss
+// field only decides ties among equal-latency paths.
+constexpr uint64_t KEY_INF = 1ull << 62;  // INF + INF < 2^64: no wrap in the closure
+
+struct KeyParams {
+    uint64_t g;        // latency unit (gcd of all edge latencies, ns)
+    uint32_t qb;       // bits of the loss field
+    int32_t s;         // loss scale exponent (fixed point 2^-s)
+    double scale;      // 2^s
+    double inv_scale;  // 2^-s
+    double nlr_cap;    // -ln(reliability) clamp (loss ~ 1)
+    uint64_t q_cap;    // clamp in key units
+};
+
+// FW tile geometry: B x B blocks, one block-row/column per round.
+constexpr int FW_B = 64;
+
+struct FwTimers {
+    std::vector<hipEvent_t> ev;  // 2 per phase-3 launch
+    int used = 0;
+};
+
+}  // namespace srt
+
+struct srt_comm;
+
+struct srt_plan {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    uint32_t V = 0;   // graph nodes
+    uint32_t Vp = 0;  // padded to FW_B
+    uint32_t n = 0;   // in-use nodes
+    uint64_t n_adj = 0;
+    int algo = SRT_ALGO_FW;
+    srt::KeyParams kp{};
+    std::string desc;
+    bool identity_nodes = false;
+
+    // device buffers
+    uint64_t *d_row_ptr = nullptr;
+    uint32_t *d_col = nullptr;
+    uint64_t *d_lat = nullptr;
+    float *d_loss = nullptr;
+    uint32_t *d_nodes = nullptr;
+    uint64_t *d_D = nullptr;  // Vp*Vp path keys
+    uint64_t *d_out_lat = nullptr;
+    float *d_out_loss = nullptr;
+    uint64_t *d_sl_lat = nullptr;
+    float *d_sl_loss = nullptr;
+    unsigned long long *d_stats = nullptr;  // [0] min latency, [1] unreachable pairs
+    srt_path *d_pack = nullptr;             // AoS staging for fetch
+    uint64_t *d_draws = nullptr;            // packet stage: one RNG draw per packet
+    uint64_t draws_cap = 0;
+
+    // host copies needed after create
+    std::vector<uint32_t> nodes;
+    std::vector<uint32_t> node_ids;
+
+    // timing of the last run
+    std::vector<hipEvent_t> ev;  // pairs around each phase-3 launch
+    hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+    uint64_t p3_launches = 0;
+    double p3_ms = 0.0, total_ms = 0.0;
+    bool ran = false;
+
+    // multi-GPU
+    srt_comm *comm = nullptr;
+};
+
+namespace srt {
+// kernels (srt_fw.hip)
+void fw_init(srt_plan *p);
+void fw_rounds(srt_plan *p);
+void fw_extract(srt_plan *p);
+void pack_paths(srt_plan *p);
+}  // namespace srt

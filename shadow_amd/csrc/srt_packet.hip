@@ -1,0 +1,157 @@
+// srt_packet.hip -- batched Worker::send_packet decision for one round.
+//
+// Reference: src/main/core/worker.rs:326-410 (+ WorkerShared::latency /
+// reliability :539-553, RoutingInfo::increment_packet_count mod.rs:449-456,
+// Worker::update_lowest_used_latency :291-300, update_next_event_time :314-322).
+// Per packet, in the source host's send order:
+//   completed  = t >= sim_end            -> nothing, and NO RNG draw (:336-339)
+//   chance     = host_rng.gen::<f64>()   = (next_u64 >> 11) * 2^-53 (rand 0.8.5)
+//   reliability= (1.0f32 - loss) as f64  (f32 subtraction, then widened)
+//   drop iff !(t < bootstrap_end) && chance >= reliability && payload > 0
+//   else: delay = latency; counter++; SENT; deliver = max(t + delay, round_end)
+//
+// Two kernels: (A) one lane per host walks its packets and advances its
+// xoshiro256++ state -- the only sequential part, ~20 integer ops per draw;
+// (B) one lane per packet does the table gather and the decision, HBM-bound.
+#include <cstring>
+
+#include "srt_internal.h"
+
+namespace {
+
+__device__ __forceinline__ uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+
+// rand_xoshiro 0.6.0 Xoshiro256PlusPlus::next_u64
+__device__ __forceinline__ uint64_t xoshiro_next(uint64_t &s0, uint64_t &s1, uint64_t &s2,
+                                                 uint64_t &s3) {
+    const uint64_t r = rotl(s0 + s3, 23) + s0;
+    const uint64_t t = s1 << 17;
+    s2 ^= s0;
+    s3 ^= s1;
+    s1 ^= s2;
+    s0 ^= s3;
+    s2 ^= t;
+    s3 = rotl(s3, 45);
+    return r;
+}
+
+__global__ void draw_kernel(const srt_pkt *__restrict__ pkts, const uint32_t *__restrict__ host_ptr,
+                            uint32_t n_hosts, uint64_t *__restrict__ rng, uint64_t sim_end,
+                            uint64_t *__restrict__ draws) {
+    const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= n_hosts) return;
+    uint64_t s0 = rng[4 * (uint64_t)h], s1 = rng[4 * (uint64_t)h + 1];
+    uint64_t s2 = rng[4 * (uint64_t)h + 2], s3 = rng[4 * (uint64_t)h + 3];
+    const uint32_t b = host_ptr[h], e = host_ptr[h + 1];
+    for (uint32_t p = b; p < e; ++p) {
+        if (pkts[p].t_ns >= sim_end) continue;  // completed: no draw
+        draws[p] = xoshiro_next(s0, s1, s2, s3);
+    }
+    rng[4 * (uint64_t)h] = s0;
+    rng[4 * (uint64_t)h + 1] = s1;
+    rng[4 * (uint64_t)h + 2] = s2;
+    rng[4 * (uint64_t)h + 3] = s3;
+}
+
+__global__ void decide_kernel(const srt_pkt *__restrict__ pkts, uint64_t n_pkts,
+                              const uint64_t *__restrict__ draws,
+                              const uint64_t *__restrict__ lat, const float *__restrict__ loss,
+                              uint32_t n, srt_round r, uint32_t *__restrict__ flags,
+                              uint64_t *__restrict__ deliver, unsigned long long *counters,
+                              unsigned long long *stats) {
+    unsigned long long min_lat = ~0ull, min_deliver = ~0ull;
+    for (uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; p < n_pkts;
+         p += (uint64_t)gridDim.x * blockDim.x) {
+        const srt_pkt k = pkts[p];
+        uint32_t f = SRT_PDS_NONE;
+        uint64_t d = 0;
+        if (k.t_ns < r.sim_end_ns) {
+            const uint64_t o = (uint64_t)k.src_row * n + k.dst_row;
+            const float rel32 = 1.0f - loss[o];
+            const double reliability = (double)rel32;
+            const double chance = (double)(draws[p] >> 11) * 0x1.0p-53;
+            const bool bootstrapping = k.t_ns < r.bootstrap_end_ns;
+            if (!bootstrapping && chance >= reliability && k.payload_size > 0) {
+                f = SRT_PDS_INET_DROPPED;
+            } else {
+                const uint64_t delay = lat[o];
+                f = SRT_PDS_INET_SENT;
+                d = k.t_ns + delay;
+                if (d < r.round_end_ns) d = r.round_end_ns;
+                if (counters) atomicAdd(&counters[o], 1ull);
+                min_lat = delay < min_lat ? delay : min_lat;
+                min_deliver = d < min_deliver ? d : min_deliver;
+            }
+        }
+        flags[p] = f;
+        deliver[p] = d;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long a = __shfl_xor(min_lat, off), b = __shfl_xor(min_deliver, off);
+        min_lat = a < min_lat ? a : min_lat;
+        min_deliver = b < min_deliver ? b : min_deliver;
+    }
+    if ((threadIdx.x & 63) == 0 && stats) {
+        if (min_lat != ~0ull) atomicMin(&stats[0], min_lat);
+        if (min_deliver != ~0ull) atomicMin(&stats[1], min_deliver);
+    }
+}
+
+}  // namespace
+
+extern "C" srt_status srt_packet_batch(srt_plan *plan, const srt_pkt *d_pkts,
+                                       const uint32_t *d_host_pkt_ptr, uint32_t n_hosts,
+                                       uint64_t n_pkts, uint64_t *d_rng, const srt_round *round,
+                                       uint32_t *d_flags, uint64_t *d_deliver,
+                                       uint64_t *d_counters, uint64_t *d_stats, srt_err *err) {
+    if (err) std::memset(err, 0, sizeof *err);
+    if (!plan || !round || (n_pkts && (!d_pkts || !d_flags || !d_deliver)) || !d_host_pkt_ptr ||
+        (n_hosts && !d_rng)) {
+        if (err) {
+            err->code = SRT_ERR_INVALID;
+            std::snprintf(err->msg, sizeof err->msg, "null argument");
+        }
+        return SRT_ERR_INVALID;
+    }
+    if (!plan->ran) {
+        if (err) {
+            err->code = SRT_ERR_INVALID;
+            std::snprintf(err->msg, sizeof err->msg, "routing table not built (run the plan first)");
+        }
+        return SRT_ERR_INVALID;
+    }
+    if (hipSetDevice(plan->device) != hipSuccess) return SRT_ERR_HIP;
+    if (n_pkts > plan->draws_cap) {
+        if (plan->d_draws) (void)hipFree(plan->d_draws);
+        plan->d_draws = nullptr;
+        plan->draws_cap = 0;
+        if (hipMalloc(&plan->d_draws, n_pkts * sizeof(uint64_t)) != hipSuccess) {
+            if (err) {
+                err->code = SRT_ERR_OOM;
+                std::snprintf(err->msg, sizeof err->msg, "hipMalloc(draws) failed");
+            }
+            return SRT_ERR_OOM;
+        }
+        plan->draws_cap = n_pkts;
+    }
+    hipStream_t s = plan->stream;
+    if (n_hosts)
+        hipLaunchKernelGGL(draw_kernel, dim3((n_hosts + 255) / 256), dim3(256), 0, s, d_pkts,
+                           d_host_pkt_ptr, n_hosts, d_rng, round->sim_end_ns, plan->d_draws);
+    if (n_pkts) {
+        uint64_t blocks = (n_pkts + 255) / 256;
+        if (blocks > 8192) blocks = 8192;
+        hipLaunchKernelGGL(decide_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, d_pkts, n_pkts,
+                           plan->d_draws, plan->d_out_lat, plan->d_out_loss, plan->n, *round,
+                           d_flags, d_deliver, (unsigned long long *)d_counters,
+                           (unsigned long long *)d_stats);
+    }
+    if (hipGetLastError() != hipSuccess) {
+        if (err) {
+            err->code = SRT_ERR_HIP;
+            std::snprintf(err->msg, sizeof err->msg, "packet kernel launch failed");
+        }
+        return SRT_ERR_HIP;
+    }
+    return SRT_OK;
+}

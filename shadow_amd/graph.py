@@ -1,0 +1,278 @@
+"""Host-side mirror of Shadow's network-graph API (src/main/network/graph/mod.rs)
+over the gfx950 routing build in libsrt.so.
+
+Names, argument meaning and error behaviour follow the reference:
+
+  reference (mod.rs)                          here
+  ------------------------------------------  ------------------------------------
+  PathProperties {latency_ns, packet_loss}    PathProperties (+, ordering: 296-331)
+  NetworkGraph::parse(text)        :134       NetworkGraph.parse(text)
+  NetworkGraph::node_id_to_index   :126       NetworkGraph.node_id_to_index
+  NetworkGraph::node_index_to_id   :130       NetworkGraph.node_index_to_id
+  compute_shortest_paths(&[NodeIndex]) :183   NetworkGraph.compute_shortest_paths
+  get_direct_paths(&[NodeIndex])   :230       NetworkGraph.get_direct_paths
+  IpAssignment                     :352-420   IpAssignment
+  RoutingInfo                      :428-477   RoutingInfo
+  Err(Box<dyn Error>) / panic      :219       NetGraphError (code = srt_status)
+
+The HashMap<(NodeIndex, NodeIndex), PathProperties> result becomes a dense
+`PathTable` (row-major u64 latency + f32 loss over the caller's node list) that
+also answers `table[(a, b)]` like the map did.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import ipaddress
+from dataclasses import dataclass
+from typing import Dict, Iterable, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import SrtError as NetGraphError
+
+
+@dataclass(frozen=True)
+class PathProperties:
+    """mod.rs:296-340. Ordered by latency, then loss; `+` folds loss as
+    1 - (1 - a)(1 - b) in f32."""
+
+    latency_ns: int = 0
+    packet_loss: float = 0.0
+
+    def __add__(self, other: "PathProperties") -> "PathProperties":
+        one = np.float32(1.0)
+        a, b = np.float32(self.packet_loss), np.float32(other.packet_loss)
+        loss = one - (one - a) * (one - b)
+        return PathProperties((self.latency_ns + other.latency_ns) & (2**64 - 1), float(np.float32(loss)))
+
+    def _key(self):
+        return (self.latency_ns, self.packet_loss)
+
+    def __lt__(self, o):
+        return self._key() < o._key()
+
+    def __le__(self, o):
+        return self._key() <= o._key()
+
+
+def _csr_from_edges(n_nodes: int, src, dst, lat_ns, loss, directed: bool):
+    """petgraph adjacency (Graph::edges semantics) as CSR: directed -> outgoing;
+    undirected -> every edge from both endpoints, self-loops once."""
+    src = np.asarray(src, np.uint32)
+    dst = np.asarray(dst, np.uint32)
+    lat_ns = np.asarray(lat_ns, np.uint64)
+    loss = np.asarray(loss, np.float32)
+    if directed:
+        rows, cols, lats, losses = src, dst, lat_ns, loss
+    else:
+        back = src != dst
+        rows = np.concatenate([src, dst[back]])
+        cols = np.concatenate([dst, src[back]])
+        lats = np.concatenate([lat_ns, lat_ns[back]])
+        losses = np.concatenate([loss, loss[back]])
+    order = np.argsort(rows, kind="stable")
+    counts = np.bincount(rows, minlength=n_nodes).astype(np.uint64)
+    row_ptr = np.zeros(n_nodes + 1, np.uint64)
+    np.cumsum(counts, out=row_ptr[1:])
+    return (row_ptr, np.ascontiguousarray(cols[order], np.uint32), np.ascontiguousarray(lats[order], np.uint64),
+            np.ascontiguousarray(losses[order], np.float32))
+
+
+class PathTable:
+    """Dense result of compute_shortest_paths / get_direct_paths over `nodes`
+    (NodeIndex values): latency_ns[i, j], packet_loss[i, j] = nodes[i] -> nodes[j]."""
+
+    def __init__(self, nodes: np.ndarray, latency_ns: np.ndarray, packet_loss: np.ndarray, min_latency_ns: int):
+        self.nodes = nodes
+        self.latency_ns = latency_ns
+        self.packet_loss = packet_loss
+        self.min_latency_ns = min_latency_ns
+        self._pos = {int(v): i for i, v in enumerate(nodes)}
+
+    def __len__(self):
+        return len(self.nodes) ** 2
+
+    def __getitem__(self, key: Tuple[int, int]) -> PathProperties:
+        i, j = self._pos[int(key[0])], self._pos[int(key[1])]
+        return PathProperties(int(self.latency_ns[i, j]), float(self.packet_loss[i, j]))
+
+    def get(self, key, default=None):
+        try:
+            return self[key]
+        except KeyError:
+            return default
+
+    def items(self):
+        for i, a in enumerate(self.nodes):
+            for j, b in enumerate(self.nodes):
+                yield (int(a), int(b)), PathProperties(int(self.latency_ns[i, j]), float(self.packet_loss[i, j]))
+
+
+class NetworkGraph:
+    """A parsed network graph: petgraph adjacency in CSR plus the GML id map."""
+
+    def __init__(self, n_nodes, node_ids, row_ptr, col, lat_ns, loss, directed, _owner=None):
+        self.n_nodes = int(n_nodes)
+        self.node_ids = np.ascontiguousarray(node_ids, np.uint32)
+        self.row_ptr = np.ascontiguousarray(row_ptr, np.uint64)
+        self.col = np.ascontiguousarray(col, np.uint32)
+        self.lat_ns = np.ascontiguousarray(lat_ns, np.uint64)
+        self.loss = np.ascontiguousarray(loss, np.float32)
+        self.directed = bool(directed)
+        self._owner = _owner
+        # HashMap::insert semantics: a repeated GML id maps to the last node
+        self._id_to_index: Dict[int, int] = {int(v): i for i, v in enumerate(self.node_ids)}
+
+    # ---------------------------------------------------------------- build
+    @classmethod
+    def from_edges(cls, n_nodes: int, src, dst, lat_ns, loss=None, directed: bool = False,
+                   node_ids: Optional[Sequence[int]] = None) -> "NetworkGraph":
+        """Graph from a GML-order edge list with NodeIndex endpoints."""
+        if loss is None:
+            loss = np.zeros(len(src), np.float32)
+        row_ptr, col, lat, los = _csr_from_edges(n_nodes, src, dst, lat_ns, loss, directed)
+        ids = np.arange(n_nodes, dtype=np.uint32) if node_ids is None else node_ids
+        return cls(n_nodes, ids, row_ptr, col, lat, los, directed)
+
+    @classmethod
+    def parse(cls, graph_text: str) -> "NetworkGraph":
+        """NetworkGraph::parse (mod.rs:134-181) via the C++ GML ingest in libsrt."""
+        L = _lib.lib()
+        b = graph_text.encode()
+        h = C.c_void_p()
+        err = _lib.SrtErr()
+        _lib.check(L.srt_gml_parse(b, len(b), C.byref(h), C.byref(err)), err)
+        try:
+            csr = _lib.SrtCsr()
+            L.srt_gml_csr(h, C.byref(csr))
+            n, m = csr.n_nodes, csr.n_adj
+            as_np = np.ctypeslib.as_array
+            row_ptr = as_np(csr.row_ptr, (n + 1,)).copy()
+            col = as_np(csr.col, (m,)).copy() if m else np.zeros(0, np.uint32)
+            lat = as_np(csr.lat_ns, (m,)).copy() if m else np.zeros(0, np.uint64)
+            loss = as_np(csr.loss, (m,)).copy() if m else np.zeros(0, np.float32)
+            ids = as_np(csr.node_ids, (n,)).copy() if n else np.zeros(0, np.uint32)
+            return cls(n, ids, row_ptr, col, lat, loss, bool(csr.directed))
+        finally:
+            L.srt_gml_free(h)
+
+    # ---------------------------------------------------------------- ids
+    def node_id_to_index(self, gml_id: int) -> Optional[int]:
+        return self._id_to_index.get(int(gml_id))
+
+    def node_index_to_id(self, index: int) -> Optional[int]:
+        return int(self.node_ids[index]) if 0 <= index < self.n_nodes else None
+
+    # ---------------------------------------------------------------- ABI
+    def csr(self) -> _lib.SrtCsr:
+        c = _lib.SrtCsr()
+        c.n_nodes = self.n_nodes
+        c.directed = int(self.directed)
+        c.n_adj = len(self.col)
+        c.row_ptr = self.row_ptr.ctypes.data_as(C.POINTER(C.c_uint64))
+        c.col = self.col.ctypes.data_as(C.POINTER(C.c_uint32))
+        c.lat_ns = self.lat_ns.ctypes.data_as(C.POINTER(C.c_uint64))
+        c.loss = self.loss.ctypes.data_as(C.POINTER(C.c_float))
+        c.node_ids = self.node_ids.ctypes.data_as(C.POINTER(C.c_uint32))
+        return c
+
+    def _run(self, fn_name: str, nodes, algo: int, device: int) -> PathTable:
+        L = _lib.lib()
+        _lib.require_device()
+        nodes = np.ascontiguousarray(np.asarray(list(nodes) if not isinstance(nodes, np.ndarray) else nodes),
+                                     np.uint32)
+        n = len(nodes)
+        out = (_lib.SrtPath * max(n * n, 1))()
+        mn = C.c_uint64()
+        opts = _lib.SrtOpts(algo, device, 0, 0)
+        err = _lib.SrtErr()
+        csr = self.csr()
+        rc = getattr(L, fn_name)(C.byref(csr), nodes.ctypes.data_as(C.POINTER(C.c_uint32)), n, out, C.byref(mn),
+                                 C.byref(opts), C.byref(err))
+        _lib.check(rc, err)
+        raw = np.frombuffer(out, dtype=np.dtype([("lat", "<u8"), ("loss", "<f4"), ("pad", "<u4")]), count=n * n)
+        return PathTable(nodes, raw["lat"].reshape(n, n).copy(), raw["loss"].reshape(n, n).copy(), mn.value)
+
+    def compute_shortest_paths(self, nodes: Iterable[int], algo: int = _lib.SRT_ALGO_AUTO,
+                               device: int = -1) -> PathTable:
+        """mod.rs:183-228 on the GPU. Raises NetGraphError(code=NO_EDGE/MULTI_EDGE)
+        for a missing/duplicate self-loop and code=DISCONNECTED where the
+        reference panics on an unreachable pair."""
+        return self._run("srt_compute_shortest_paths", nodes, algo, device)
+
+    def get_direct_paths(self, nodes: Iterable[int], device: int = -1) -> PathTable:
+        """mod.rs:230-252 on the GPU."""
+        return self._run("srt_get_direct_paths", nodes, _lib.SRT_ALGO_AUTO, device)
+
+
+class IpAssignment:
+    """mod.rs:352-420: IP <-> node id; auto-assignment from 11.0.0.1 upward,
+    skipping addresses ending in .0 or .255."""
+
+    def __init__(self):
+        self._map: Dict[ipaddress.IPv4Address, int] = {}
+        self._last = ipaddress.IPv4Address("11.0.0.0")
+
+    @staticmethod
+    def _increment(addr: ipaddress.IPv4Address) -> ipaddress.IPv4Address:
+        x = int(addr)
+        while True:
+            x += 1
+            if x & 0xFF not in (0, 255):
+                return ipaddress.IPv4Address(x)
+
+    def assign(self, node_id: int) -> ipaddress.IPv4Address:
+        while True:
+            ip = self._increment(self._last)
+            self._last = ip
+            if ip not in self._map:
+                self._map[ip] = node_id
+                return ip
+
+    def assign_ip(self, node_id: int, ip) -> None:
+        ip = ipaddress.IPv4Address(ip)
+        if ip in self._map:
+            raise ValueError("IP address has already been assigned")
+        self._map[ip] = node_id
+
+    def get_node(self, ip) -> Optional[int]:
+        return self._map.get(ipaddress.IPv4Address(ip))
+
+    def get_nodes(self) -> set:
+        return set(self._map.values())
+
+
+class RoutingInfo:
+    """mod.rs:428-477 over a dense table keyed by GML ids: path() is an index
+    lookup; packet counters are a dense array (no global RwLock)."""
+
+    def __init__(self, table: PathTable, gml_ids: np.ndarray):
+        self.table = table
+        self._row = {int(gml_ids[int(v)]): i for i, v in enumerate(table.nodes)}
+        n = len(table.nodes)
+        self.packet_counters = np.zeros((n, n), np.uint64)
+
+    def path(self, start: int, end: int) -> Optional[PathProperties]:
+        i, j = self._row.get(int(start)), self._row.get(int(end))
+        if i is None or j is None:
+            return None
+        return PathProperties(int(self.table.latency_ns[i, j]), float(self.table.packet_loss[i, j]))
+
+    def row_of(self, gml_id: int) -> Optional[int]:
+        return self._row.get(int(gml_id))
+
+    def increment_packet_count(self, start: int, end: int) -> None:
+        i, j = self._row[int(start)], self._row[int(end)]
+        if self.packet_counters[i, j] != np.uint64(2**64 - 1):
+            self.packet_counters[i, j] += np.uint64(1)
+
+    def get_smallest_latency_ns(self) -> Optional[int]:
+        return int(self.table.min_latency_ns) if len(self.table.nodes) else None
+
+
+def generate_routing_info(graph: NetworkGraph, node_ids: set, use_shortest_paths: bool = True) -> RoutingInfo:
+    """sim_config.rs:424-461: GML ids of in-use nodes -> NodeIndex list -> table."""
+    nodes = np.array([graph.node_id_to_index(x) for x in node_ids], np.uint32)
+    table = graph.compute_shortest_paths(nodes) if use_shortest_paths else graph.get_direct_paths(nodes)
+    return RoutingInfo(table, graph.node_ids)

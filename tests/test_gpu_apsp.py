@@ -1,0 +1,169 @@
+"""GPU parity of the routing build (libsrt.so on gfx950) against the oracle.
+
+Bar (BASELINE.json north_star): latency bit-exact; packet_loss within 1e-6
+absolute (LOSS_TOL below); min latency exact; error codes/texts as the
+reference.  All calls go through the C ABI (shadow_amd.graph -> libsrt.so).
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from shadow_amd import NetworkGraph, _lib, synth
+
+pytestmark = pytest.mark.gpu
+
+LOSS_TOL = 1e-6  # north_star: "packet_loss within 1e-6 absolute"
+
+GOLDEN_DIRECTED = [[3333, 3, 7], [5, 5555, 12], [16, 11, 7777]]
+GOLDEN_UNDIRECTED = [[3333, 3, 7], [3, 5555, 10], [7, 10, 7777]]
+
+
+def _three(directed):
+    from tests.test_oracle import THREE_NODE
+    return THREE_NODE.format(d=directed)
+
+
+def _check(graph_edges, nodes, directed, n_nodes, node_ids=None, algo=_lib.SRT_ALGO_AUTO):
+    src, dst, lat, loss = graph_edges
+    ids = np.arange(n_nodes) if node_ids is None else node_ids
+    og = O.Graph(directed, ids, src, dst, lat, loss)
+    elat, eloss = O.compute_shortest_paths(og, nodes)
+    g = NetworkGraph.from_edges(n_nodes, src, dst, lat, loss, directed=directed, node_ids=ids)
+    t = g.compute_shortest_paths(nodes, algo=algo)
+    assert np.array_equal(t.latency_ns, elat), "latency must be bit-exact"
+    err = np.abs(t.packet_loss.astype(np.float64) - eloss.astype(np.float64))
+    assert err.max() <= LOSS_TOL, f"max loss error {err.max()}"
+    # diagonal is the raw self-loop edge, bit-exact (mod.rs:210-217)
+    assert np.array_equal(np.diag(t.packet_loss).view(np.uint32), np.diag(eloss).view(np.uint32))
+    assert t.min_latency_ns == int(elat.min())
+    return t
+
+
+@pytest.mark.parametrize("directed", [1, 0])
+def test_reference_golden_three_node(directed):
+    g = NetworkGraph.parse(_three(directed))
+    nodes = [g.node_id_to_index(0), g.node_id_to_index(1), g.node_id_to_index(2)]
+    t = g.compute_shortest_paths(nodes)
+    assert t.latency_ns.tolist() == (GOLDEN_DIRECTED if directed else GOLDEN_UNDIRECTED)
+    assert t.min_latency_ns == 3
+    assert t[(nodes[2], nodes[0])].latency_ns == (16 if directed else 7)
+
+
+@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("directed", [False, True])
+def test_random_tie_heavy(seed, directed):
+    n = 70 + 13 * seed  # crosses the 64-node block boundary, ragged padding
+    e = synth.random_graph(n, seed, p_edge=0.15, directed=directed, lat_range_ns=(1, 4), loss_max=0.05)
+    nodes = np.random.default_rng(seed).permutation(n).astype(np.uint32)
+    _check(e, nodes, directed, n)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_subset_in_use(seed):
+    # intermediates may be any graph node; sources/destinations only in-use nodes (mod.rs:203)
+    n = 150
+    e = synth.random_graph(n, 100 + seed, p_edge=0.05, directed=True, lat_range_ns=(1, 30))
+    nodes = np.random.default_rng(seed).choice(n, 37, replace=False).astype(np.uint32)
+    _check(e, nodes, True, n)
+
+
+def test_complete_c1_slice_through_gml():
+    n = 256
+    src, dst, lat, loss = synth.complete_graph(n, 1)
+    text = synth.gml_text(n, src, dst, lat, loss)
+    g = NetworkGraph.parse(text)
+    og = O.gml_parse(text)
+    nodes = np.arange(n, dtype=np.uint32)
+    elat, eloss = O.compute_shortest_paths(og, nodes)
+    t = g.compute_shortest_paths(nodes)
+    assert np.array_equal(t.latency_ns, elat)
+    assert np.abs(t.packet_loss.astype(np.float64) - eloss).max() <= LOSS_TOL
+
+
+def test_loss_free_graph_exact_zero_loss():
+    n = 90
+    src, dst, lat, loss = synth.random_graph(n, 5, p_edge=0.1, loss_max=0.0)
+    t = _check((src, dst, lat, loss), np.arange(n, dtype=np.uint32), False, n)
+    assert not t.packet_loss.any()
+
+
+def test_single_node():
+    g = NetworkGraph.from_edges(1, [0], [0], [42], [0.25], directed=False, node_ids=[9])
+    t = g.compute_shortest_paths([0])
+    assert t.latency_ns.tolist() == [[42]] and t.packet_loss[0, 0] == np.float32(0.25)
+
+
+def test_high_loss_and_loss_one_edges():
+    n = 40
+    src, dst, lat, loss = synth.random_graph(n, 11, p_edge=0.2, lat_range_ns=(1, 3), loss_max=0.9)
+    loss[::7] = 1.0
+    _check((src, dst, lat, loss), np.arange(n, dtype=np.uint32), False, n)
+
+
+def test_disconnected_raises():
+    g = NetworkGraph.from_edges(3, [0, 1, 2, 0], [0, 1, 2, 1], [5, 5, 5, 3], directed=True)
+    with pytest.raises(_lib.SrtError) as e:
+        g.compute_shortest_paths([0, 1, 2])
+    assert e.value.code == _lib.SRT_ERR_DISCONNECTED
+
+
+def test_missing_selfloop_error_text():
+    g = NetworkGraph.from_edges(2, [0, 0], [0, 1], [5, 5], directed=False, node_ids=[4, 8])
+    with pytest.raises(_lib.SrtError) as e:
+        g.compute_shortest_paths([0, 1])
+    assert e.value.code == _lib.SRT_ERR_NO_EDGE and str(e.value) == "No edge connecting node 8 to 8"
+
+
+def test_direct_paths_parity():
+    n = 33
+    src, dst, lat, loss = synth.complete_graph(n, 9)
+    og = O.Graph(False, np.arange(n) + 1000, src, dst, lat, loss)
+    nodes = np.random.default_rng(1).permutation(n).astype(np.uint32)
+    elat, eloss = O.get_direct_paths(og, nodes)
+    g = NetworkGraph.from_edges(n, src, dst, lat, loss, directed=False, node_ids=np.arange(n) + 1000)
+    t = g.get_direct_paths(nodes)
+    assert np.array_equal(t.latency_ns, elat)
+    assert np.array_equal(t.packet_loss.view(np.uint32), eloss.view(np.uint32))  # verbatim edge values
+    assert t.min_latency_ns == int(elat.min())
+
+
+def test_direct_paths_errors_in_reference_order():
+    n = 6
+    src, dst, lat, loss = synth.complete_graph(n, 2)
+    keep = ~((src == 2) & (dst == 4))
+    g = NetworkGraph.from_edges(n, src[keep], dst[keep], lat[keep], loss[keep], node_ids=np.arange(n) + 50)
+    with pytest.raises(_lib.SrtError) as e:
+        g.get_direct_paths([0, 4, 2, 1])
+    assert str(e.value) == "No edge connecting node 54 to 52"
+    src2 = np.concatenate([src, [1]]).astype(np.uint32)
+    dst2 = np.concatenate([dst, [3]]).astype(np.uint32)
+    g2 = NetworkGraph.from_edges(n, src2, dst2, np.concatenate([lat, [lat[0]]]), np.concatenate([loss, [0]]),
+                                 node_ids=np.arange(n) + 50)
+    with pytest.raises(_lib.SrtError) as e:
+        g2.get_direct_paths([3, 1])
+    assert str(e.value) == "More than one edge connecting node 53 to 51"
+
+
+def test_c2_scale_row_sample():
+    """4096-node complete graph (config C2): full GPU table vs oracle rows for a
+    seeded sample of sources, plus size-independent properties."""
+    n = 4096
+    src, dst, lat, loss = synth.complete_graph(n, 2)
+    g = NetworkGraph.from_edges(n, src, dst, lat, loss)
+    t = g.compute_shortest_paths(np.arange(n, dtype=np.uint32))
+    L = t.latency_ns
+    # symmetric for an undirected graph, and <= the direct edge
+    assert np.array_equal(L, L.T)
+    og = O.Graph(False, np.arange(n), src, dst, lat, loss)
+    rows = np.random.default_rng(0).choice(n, 16, replace=False)
+    nodes = np.concatenate([rows, np.setdiff1d(np.arange(n), rows)]).astype(np.uint32)
+    elat, eloss = O.compute_shortest_paths(og, nodes, src_count=16)
+    for i, r in enumerate(rows):
+        exp_lat = np.empty(n, np.uint64)
+        exp_lat[nodes] = elat[i]
+        exp_loss = np.empty(n, np.float32)
+        exp_loss[nodes] = eloss[i]
+        exp_lat[r] = L[r, r]
+        exp_loss[r] = t.packet_loss[r, r]
+        assert np.array_equal(L[r], exp_lat)
+        assert np.abs(t.packet_loss[r].astype(np.float64) - exp_loss).max() <= LOSS_TOL

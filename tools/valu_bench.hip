@@ -1,0 +1,149 @@
+// valu_bench.hip -- measured VALU issue rates on gfx950 for the instructions a
+// min-plus relaxation can be built from (to pick the path-key representation
+// and to state the roofline peak from measurement, not from a datasheet).
+//
+//   hipcc -O3 --offload-arch=gfx950 tools/valu_bench.hip -o tools/valu_bench && ./tools/valu_bench
+//
+// Each kernel runs 8 independent chains of one instruction kind in inline asm,
+// ITER iterations, on a full grid (2048 x 256 threads); reported as wave64
+// instructions per CU per cycle-equivalent and as lane-ops/s.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+#define ITER 4096
+
+
+#define V32(i) unsigned a##i = seed + i + threadIdx.x;
+#define DECL32 V32(0) V32(1) V32(2) V32(3) V32(4) V32(5) V32(6) V32(7) unsigned b = seed * 3u;
+#define SINK32 unsigned sink = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7
+
+#define ASM8(op)                                                        \
+    asm volatile(op " %0, %0, %1" : "+v"(a0) : "v"(b));                \
+    asm volatile(op " %0, %0, %1" : "+v"(a1) : "v"(b));                \
+    asm volatile(op " %0, %0, %1" : "+v"(a2) : "v"(b));                \
+    asm volatile(op " %0, %0, %1" : "+v"(a3) : "v"(b));                \
+    asm volatile(op " %0, %0, %1" : "+v"(a4) : "v"(b));                \
+    asm volatile(op " %0, %0, %1" : "+v"(a5) : "v"(b));                \
+    asm volatile(op " %0, %0, %1" : "+v"(a6) : "v"(b));                \
+    asm volatile(op " %0, %0, %1" : "+v"(a7) : "v"(b));
+
+
+// plain 32-bit ops
+#define K32(kname, op)                                                           \
+    __global__ __launch_bounds__(256) void kname(unsigned *out, unsigned seed) { \
+        DECL32;                                                                  \
+        for (int it = 0; it < ITER; ++it) { ASM8(op) }                           \
+        SINK32;                                                                  \
+        if (seed == 12345u) out[threadIdx.x] = sink;                             \
+    }
+K32(k_add_u32, "v_add_u32")
+K32(k_min_u32, "v_min_u32")
+K32(k_pk_add_u16, "v_pk_add_u16")
+K32(k_pk_min_u16, "v_pk_min_u16")
+
+#define ASM8_3(op)                                                              \
+    asm volatile(op " %0, %0, %1, %2" : "+v"(a0) : "v"(b), "v"(a7));           \
+    asm volatile(op " %0, %0, %1, %2" : "+v"(a1) : "v"(b), "v"(a0));           \
+    asm volatile(op " %0, %0, %1, %2" : "+v"(a2) : "v"(b), "v"(a1));           \
+    asm volatile(op " %0, %0, %1, %2" : "+v"(a3) : "v"(b), "v"(a2));           \
+    asm volatile(op " %0, %0, %1, %2" : "+v"(a4) : "v"(b), "v"(a3));           \
+    asm volatile(op " %0, %0, %1, %2" : "+v"(a5) : "v"(b), "v"(a4));           \
+    asm volatile(op " %0, %0, %1, %2" : "+v"(a6) : "v"(b), "v"(a5));           \
+    asm volatile(op " %0, %0, %1, %2" : "+v"(a7) : "v"(b), "v"(a6));
+#define K32_3(kname, op)                                                         \
+    __global__ __launch_bounds__(256) void kname(unsigned *out, unsigned seed) { \
+        DECL32;                                                                  \
+        for (int it = 0; it < ITER; ++it) { ASM8_3(op) }                         \
+        SINK32;                                                                  \
+        if (seed == 12345u) out[threadIdx.x] = sink;                             \
+    }
+K32_3(k_min3_u32, "v_min3_u32")
+
+// 64-bit ops
+#define V64(i) unsigned long long a##i = (unsigned long long)(seed + i + threadIdx.x) << 20;
+#define DECL64 V64(0) V64(1) V64(2) V64(3) V64(4) V64(5) V64(6) V64(7) unsigned long long b = seed * 3ull;
+#define SINK64 unsigned sink = (unsigned)(a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7)
+#define ASM8_64(op)                                                             \
+    asm volatile(op : "+v"(a0) : "v"(b));                                       \
+    asm volatile(op : "+v"(a1) : "v"(b));                                       \
+    asm volatile(op : "+v"(a2) : "v"(b));                                       \
+    asm volatile(op : "+v"(a3) : "v"(b));                                       \
+    asm volatile(op : "+v"(a4) : "v"(b));                                       \
+    asm volatile(op : "+v"(a5) : "v"(b));                                       \
+    asm volatile(op : "+v"(a6) : "v"(b));                                       \
+    asm volatile(op : "+v"(a7) : "v"(b));
+#define K64(kname, op)                                                           \
+    __global__ __launch_bounds__(256) void kname(unsigned *out, unsigned seed) { \
+        DECL64;                                                                  \
+        for (int it = 0; it < ITER; ++it) { ASM8_64(op) }                        \
+        SINK64;                                                                  \
+        if (seed == 12345u) out[threadIdx.x] = sink;                             \
+    }
+K64(k_lshl_add_u64, "v_lshl_add_u64 %0, %0, 0, %1")
+K64(k_add_f64, "v_add_f64 %0, %0, %1")
+K64(k_min_f64, "v_min_f64 %0, %0, %1")
+
+// the full packed-key relaxation as the compiler emits it: c = min(c, a + b)
+__global__ __launch_bounds__(256) void k_relax_u64(unsigned *out, unsigned seed) {
+    DECL64;
+    unsigned long long c0 = ~0ull >> 2, c1 = c0, c2 = c0, c3 = c0, c4 = c0, c5 = c0, c6 = c0, c7 = c0;
+    for (int it = 0; it < ITER; ++it) {
+#define R(i) { unsigned long long t = a##i + b; c##i = t < c##i ? t : c##i; asm volatile("" : "+v"(a##i), "+v"(c##i)); }
+        R(0) R(1) R(2) R(3) R(4) R(5) R(6) R(7)
+#undef R
+    }
+    unsigned sink = (unsigned)(c0 ^ c1 ^ c2 ^ c3 ^ c4 ^ c5 ^ c6 ^ c7);
+    if (seed == 12345u) out[threadIdx.x] = sink;
+}
+
+__global__ __launch_bounds__(256) void k_relax_u32sat(unsigned *out, unsigned seed) {
+    DECL32;
+    unsigned c0 = ~0u, c1 = c0, c2 = c0, c3 = c0, c4 = c0, c5 = c0, c6 = c0, c7 = c0;
+    for (int it = 0; it < ITER; ++it) {
+#define R(i) { unsigned t = __builtin_elementwise_add_sat(a##i, b); c##i = t < c##i ? t : c##i; asm volatile("" : "+v"(a##i), "+v"(c##i)); }
+        R(0) R(1) R(2) R(3) R(4) R(5) R(6) R(7)
+#undef R
+    }
+    unsigned sink = c0 ^ c1 ^ c2 ^ c3 ^ c4 ^ c5 ^ c6 ^ c7;
+    if (seed == 12345u) out[threadIdx.x] = sink;
+}
+
+typedef void (*kfn)(unsigned *, unsigned);
+
+static void run(const char *name, kfn k, int instr_per_iter, unsigned *d) {
+    const int grid = 2048, block = 256;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(block), 0, 0, d, 1u);  // warm
+    hipDeviceSynchronize();
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipEventRecord(a);
+    const int reps = 5;
+    for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k, dim3(grid), dim3(block), 0, 0, d, 1u);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    const double lane_ops = (double)reps * grid * block * ITER * instr_per_iter;
+    const double rate = lane_ops / (ms * 1e-3);
+    printf("%-16s %8.3f ms  %7.2f Tlane-ops/s  (%.3f of 78.6)\n", name, ms / reps, rate / 1e12,
+           rate / 78.6e12);
+}
+
+int main() {
+    unsigned *d;
+    hipMalloc(&d, 4096);
+    run("v_add_u32", k_add_u32, 8, d);
+    run("v_min_u32", k_min_u32, 8, d);
+    run("v_min3_u32", k_min3_u32, 8, d);
+    run("v_pk_add_u16", k_pk_add_u16, 8, d);
+    run("v_pk_min_u16", k_pk_min_u16, 8, d);
+    run("v_lshl_add_u64", k_lshl_add_u64, 8, d);
+    run("v_add_f64", k_add_f64, 8, d);
+    run("v_min_f64", k_min_f64, 8, d);
+    run("relax_u64(x1)", k_relax_u64, 8, d);  // reported per relaxation
+    run("relax_u32sat(x1)", k_relax_u32sat, 8, d);
+    hipFree(d);
+    return 0;
+}
