@@ -26,10 +26,13 @@ sys.path.insert(0, ROOT)
 # MI355X constants (/opt/skills/guides/MI355X_MICROARCH.md): 256 CUs x 4 SIMD-32,
 # one wave64 VALU op per 2 cycles per SIMD -> 128 int32 lane-ops/clk/CU at 2.4 GHz.
 VALU_LANE_OPS_PEAK = 256 * 128 * 2.4e9  # 78.6e12 int32 lane-ops/s
-# One lexicographic (latency, loss) relaxation on a packed 64-bit key is 4 VALU
-# ops on gfx950: v_lshl_add_u64 (add), v_cmp_lt_u64, 2 x v_cndmask_b32 (min).
-OPS_PER_RELAX = 4
-RELAX_PEAK = VALU_LANE_OPS_PEAK / OPS_PER_RELAX
+# FP64 VALU ops (v_add_f64, v_min_f64) issue at half that rate (spec: FP64 vector
+# 78.6 TF vs FP32 157.3 TF; tools/valu_bench measured 36.5e12 lane-ops/s).  One
+# lexicographic (latency, loss) relaxation on the f64-encoded path key is one
+# v_add_f64 + one v_min_f64.
+F64_LANE_OPS_PEAK = VALU_LANE_OPS_PEAK / 2  # 39.3e12
+OPS_PER_RELAX = 2
+RELAX_PEAK = F64_LANE_OPS_PEAK / OPS_PER_RELAX  # 19.66e12 relaxations/s
 
 
 def parse_args():
@@ -96,7 +99,7 @@ def main():
     del row_ptr, col, lat, loss, g
     if world > 1:
         from shadow_amd import dist as sdist
-        sdist.bind(plan, rank, world, local_rank)
+        sdist.bind(plan, rank, world, local_rank, transport=os.environ.get("SRT_COMM", "rccl"))
 
     def barrier():
         if world > 1:
@@ -128,17 +131,19 @@ def main():
         ms_per_step = elapsed * 1e3 / args.steps
         pairs = n * n
         value = pairs / (elapsed / args.steps)
-        # dominant kernel: FW phase 3 -- (nblk-1)^2 blocks x 64^3 relaxations per launch
-        B = 64
+        # dominant kernel: FW phase 3 -- (nblk-1)^2 tiles x B^3 relaxations per launch
+        import re
+        B = int(re.search(r"B=(\d+)", plan.describe()).group(1))
         nblk = (n + B - 1) // B
         relax_per_launch = (nblk - 1) ** 2 * B ** 3
         avg_launch_s = (p3_ms / 1e3) / max(p3_launches, 1)
         achieved = relax_per_launch / avg_launch_s
         roofline = {"bound": "valu", "achieved": achieved / 1e12, "peak": RELAX_PEAK / 1e12, "unit": "Trelax/s",
                     "frac": achieved / RELAX_PEAK, "traffic": None,
-                    "kernel": "fw_phase3_kernel", "avg_launch_ms": avg_launch_s * 1e3,
+                    "kernel": "minplus_tile_kernel<double, 0> (FW phase 3)", "avg_launch_ms": avg_launch_s * 1e3,
                     "relax_per_launch": relax_per_launch,
-                    "peak_basis": f"{VALU_LANE_OPS_PEAK / 1e12:.1f}e12 int32 VALU lane-ops/s / {OPS_PER_RELAX} ops"}
+                    "peak_basis": f"{F64_LANE_OPS_PEAK / 1e12:.1f}e12 f64 VALU lane-ops/s / {OPS_PER_RELAX} ops "
+                                  f"(v_add_f64 + v_min_f64) per relaxation"}
         cpu = None
         if args.cpu_baseline and world == 1:
             cpu = cpu_baseline(n, args.seed, args.cpu_threads, args.cpu_sources)
@@ -146,7 +151,7 @@ def main():
             "metric": "APSP pairs/sec (routing-table build, 16k-node graph)",
             "value": value, "unit": "pairs/s", "n_gpus": n_gpus, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
-            "dtype": "u64", "data": "synthetic (seeded complete graph, latency U{1..300} ms, loss U[0,0.01])",
+            "dtype": "f64" if "f64key" in plan.describe() else "u64", "data": "synthetic (seeded complete graph, latency U{1..300} ms, loss U[0,0.01])",
             "config": {"workload": f"C3: {n}-node complete undirected GML graph, use_shortest_path=true, "
                                    f"blocked Floyd-Warshall", "nodes": n, "pairs": pairs,
                        "parallelism": f"rows{n_gpus}" if n_gpus > 1 else "single",

@@ -150,6 +150,21 @@ srt_status srt_comm_unique_id(uint8_t out[128], srt_err *err);
 srt_status srt_comm_init(const uint8_t id[128], int nranks, int rank, int device,
                          srt_comm **comm, srt_err *err);
 void srt_comm_destroy(srt_comm *comm);
+/* Host-callback transport with the same semantics (used to run the sharded
+ * build over any host-side collective, e.g. torch.distributed/gloo in tests).
+ * Each callback is invoked with the plan's stream idle and must have completed
+ * the collective on the DEVICE buffer before returning 0.
+ *   bcast:     d_buf[0..bytes) from rank `root` to all ranks;
+ *   allgather: in place, rank r contributes d_buf[r*bytes_per_rank ..). */
+typedef int (*srt_bcast_fn)(void *user, void *d_buf, uint64_t bytes, int root);
+typedef int (*srt_allgather_fn)(void *user, void *d_buf, uint64_t bytes_per_rank);
+srt_status srt_comm_init_callbacks(int nranks, int rank, srt_bcast_fn bcast,
+                                   srt_allgather_fn allgather, void *user, srt_comm **comm,
+                                   srt_err *err);
+/* Binds the plan to a communicator: from now on srt_plan_run computes only
+ * this rank's block-rows of the closure, broadcasts each round's pivot
+ * block-row from its owner and all-gathers the path keys at the end, so every
+ * rank holds the full table.  The communicator must outlive the plan. */
 srt_status srt_plan_bind_comm(srt_plan *plan, srt_comm *comm, srt_err *err);
 
 /* ------------------------------------------------------- packet delivery */

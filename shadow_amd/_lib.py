@@ -64,6 +64,9 @@ class SrtError(RuntimeError):
 
 _lib = None
 
+BCAST_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_int)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64)
+
 # name -> (restype, argtypes): the full exported surface of include/srt.h
 _vp = C.c_void_p
 _u64p, _u32p, _f32p = C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.POINTER(C.c_float)
@@ -88,6 +91,7 @@ SIGNATURES = {
     "srt_comm_unique_id": (C.c_int, [C.c_void_p, _errp]),
     "srt_comm_init": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(_vp), _errp]),
     "srt_comm_destroy": (None, [_vp]),
+    "srt_comm_init_callbacks": (C.c_int, [C.c_int, C.c_int, _vp, _vp, _vp, C.POINTER(_vp), _errp]),
     "srt_plan_bind_comm": (C.c_int, [_vp, _vp, _errp]),
     "srt_packet_batch": (C.c_int, [_vp, _vp, _vp, C.c_uint32, C.c_uint64, _vp, C.POINTER(SrtRound), _vp, _vp, _vp,
                                    _vp, _errp]),
@@ -101,6 +105,14 @@ def lib():
     """Load libsrt.so (raises if it was not built: there is no fallback)."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: torch ships its own libamdhip64.so.7.  If
+        # libsrt.so were dlopen'd first, the system copy would load and torch
+        # would later bring a second runtime that finds no GPU.  Importing torch
+        # first makes libsrt bind to the already-loaded runtime (same SONAME).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise SrtError(SRT_ERR_UNSUPPORTED,
                            f"{LIB_PATH} not built: run __graft_entry__.build() (make -C shadow_amd/csrc)")

@@ -89,32 +89,24 @@ int bits_for(unsigned __int128 x) {  // number of bits to represent x
     return b;
 }
 
-// Choose the packed-key representation (see KeyParams).  Bounds: every FW
-// stored value is a simple path (<= V-1 hops) and a candidate is the sum of
-// two, so <= 2(V-1) edges.  Latency field must hold 2(V-1)*max(lat/g) and the
-// whole key must stay below KEY_INF = 2^62; the loss field must hold
-// 2(V-1)*max edge q without carrying into the latency field.
-bool choose_key_params(const srt_csr *g, KeyParams *kp, std::string *why) {
-    uint64_t gcd = 0, maxlat = 0;
-    double max_nl = 0.0;
-    const double NLR_CAP = 40.0;  // reliability < e^-40 ~ 4e-18: loss == 1.0f in f32
-    for (uint64_t k = 0; k < g->n_adj; ++k) {
-        gcd = std::gcd(gcd, g->lat_ns[k]);
-        maxlat = std::max(maxlat, g->lat_ns[k]);
-        const double nl = -std::log1p(-(double)g->loss[k]);
-        max_nl = std::max(max_nl, std::min(nl, NLR_CAP));
-    }
-    if (gcd == 0) gcd = 1;
-    const unsigned __int128 hops = 2 * (unsigned __int128)(g->n_nodes ? g->n_nodes - 1 : 0) + 1;
-    const unsigned __int128 latfield = hops * (maxlat / gcd) + 1;
-    const int lbits = bits_for(latfield);
-    kp->g = gcd;
-    kp->nlr_cap = NLR_CAP;
-    if (lbits > 62) {
-        *why = "latency range exceeds the 62-bit packed key";
-        return false;
-    }
-    if (max_nl == 0.0) {  // loss-free graph: key = latency units
+// Choose the packed-key representation (see KeyParams) and prove it exact.
+//
+// Every value the closure stores is the key of a simple path whose latency is
+// at most Lmax (units of g), and every candidate is the sum of two stored
+// values.  Lmax = max edge latency when every ordered pair of graph nodes has
+// an edge (the initial matrix is finite and values only decrease), else
+// (V-1) * max edge latency.  A stored path has at most H = min(V-1,
+// Lmax / min_edge_latency) hops.  So with W usable bits (53 for f64 keys, 62
+// for u64 keys):
+//   latency field: 2*Lmax (+1) must fit in W - qb bits;
+//   loss field:    2*H*max_q must stay < 2^qb (no carry into the latency);
+// then key sums are exact integers and lexicographic (latency, loss) order is
+// plain numeric order.  s (the loss resolution) must be >= 24, i.e. loss
+// quantisation <= 2^-25 per hop; otherwise the next wider key is tried.
+bool fit_width(int W, unsigned __int128 lat_field, unsigned __int128 hops2, double max_nl, KeyParams *kp) {
+    const int lbits = bits_for(lat_field);
+    if (lbits > W) return false;
+    if (max_nl == 0.0) {  // loss-free graph: key = latency units, loss field empty
         kp->qb = 0;
         kp->s = 0;
         kp->scale = 1.0;
@@ -122,21 +114,67 @@ bool choose_key_params(const srt_csr *g, KeyParams *kp, std::string *why) {
         kp->q_cap = 0;
         return true;
     }
-    const int qb = 62 - lbits;
-    // largest s with hops * max_nl * 2^s < 2^qb
-    const double room = std::ldexp(1.0, qb) / ((double)hops * max_nl);
+    const int qb = W - lbits;
+    const double room = std::ldexp(1.0, qb) / ((double)hops2 * max_nl);
     int s = (int)std::floor(std::log2(room)) - 1;  // one bit of margin for rounding
     s = std::min(s, 52);
-    if (s < 24) {
-        *why = "loss field too narrow for 2^-24 resolution (" + std::to_string(s) + " bits)";
-        return false;
-    }
+    if (s < 24) return false;
     kp->qb = (uint32_t)qb;
     kp->s = s;
     kp->scale = std::ldexp(1.0, s);
     kp->inv_scale = std::ldexp(1.0, -s);
-    kp->q_cap = (uint64_t)std::llrint(NLR_CAP * kp->scale);
+    kp->q_cap = (uint64_t)std::llrint(kp->nlr_cap * kp->scale);
     return true;
+}
+
+bool choose_key_params(const srt_csr *g, KeyParams *kp, bool *f64, std::string *why) {
+    uint64_t gcd = 0, maxlat = 0, minlat = ~0ull;
+    double max_nl = 0.0;
+    const double NLR_CAP = 40.0;  // reliability < e^-40 ~ 4e-18: loss == 1.0f in f32
+    for (uint64_t k = 0; k < g->n_adj; ++k) {
+        const uint64_t l = g->lat_ns[k];
+        gcd = std::gcd(gcd, l);
+        maxlat = std::max(maxlat, l);
+        minlat = std::min(minlat, l);
+        const double nl = -std::log1p(-(double)g->loss[k]);
+        max_nl = std::max(max_nl, std::min(nl, NLR_CAP));
+    }
+    if (gcd == 0) gcd = 1;
+    kp->g = gcd;
+    kp->nlr_cap = NLR_CAP;
+    const uint64_t V = g->n_nodes;
+    // complete: every node has an edge to every other node
+    bool complete = V > 0;
+    {
+        std::vector<uint32_t> stamp(V, 0);
+        for (uint64_t u = 0; u < V && complete; ++u) {
+            uint64_t distinct = 0;
+            for (uint64_t k = g->row_ptr[u]; k < g->row_ptr[u + 1]; ++k) {
+                const uint32_t v = g->col[k];
+                if (v != u && stamp[v] != u + 1) {
+                    stamp[v] = (uint32_t)(u + 1);
+                    ++distinct;
+                }
+            }
+            complete = distinct == V - 1;
+        }
+    }
+    const uint64_t maxu = maxlat / gcd, minu = std::max<uint64_t>(minlat / gcd, 1);
+    const unsigned __int128 Lmax = complete ? (unsigned __int128)maxu : (unsigned __int128)(V ? V - 1 : 0) * maxu;
+    unsigned __int128 H = V ? V - 1 : 0;
+    if (minlat != ~0ull && Lmax / minu < H) H = Lmax / minu;
+    const unsigned __int128 lat_field = 2 * Lmax + 1;
+    const unsigned __int128 hops2 = 2 * H + 1;
+    if (fit_width(53, lat_field, hops2, max_nl, kp)) {
+        *f64 = true;
+        return true;
+    }
+    if (fit_width(62, lat_field, hops2, max_nl, kp)) {
+        *f64 = false;
+        return true;
+    }
+    *why = "latency range and loss resolution do not fit a 62-bit exact key";
+    return false;
 }
 
 template <typename T>
@@ -213,6 +251,8 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     p->V = g->n_nodes;
     p->Vp = ((g->n_nodes + srt::FW_B - 1) / srt::FW_B) * srt::FW_B;
     if (p->Vp == 0) p->Vp = srt::FW_B;
+    p->rb0 = 0;
+    p->rb1 = p->Vp / srt::FW_B;
     p->n = n;
     p->n_adj = g->n_adj;
     p->nodes.assign(nodes, nodes + n);
@@ -221,15 +261,15 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     if (g->node_ids) p->node_ids.assign(g->node_ids, g->node_ids + g->n_nodes);
 
     std::string why;
-    if (!choose_key_params(g, &p->kp, &why)) {
+    if (!choose_key_params(g, &p->kp, &p->key_f64, &why)) {
         delete p;
         set_err(err, SRT_ERR_UNSUPPORTED, ("packed key unavailable: " + why).c_str());
         return SRT_ERR_UNSUPPORTED;
     }
     p->algo = SRT_ALGO_FW;
     char d[160];
-    std::snprintf(d, sizeof d, "fw:packed64 B=%d g=%llu qb=%u s=%d V=%u n=%u", srt::FW_B,
-                  (unsigned long long)p->kp.g, p->kp.qb, p->kp.s, p->V, n);
+    std::snprintf(d, sizeof d, "fw:%s B=%d g=%llu qb=%u s=%d V=%u n=%u", p->key_f64 ? "f64key" : "u64key",
+                  srt::FW_B, (unsigned long long)p->kp.g, p->kp.qb, p->kp.s, p->V, n);
     p->desc = d;
 
     int dev = opts && opts->device >= 0 ? opts->device : -1;
@@ -300,7 +340,8 @@ srt_status srt_plan_run_async(srt_plan *p, srt_err *err) {
     HIP_TRY(hipSetDevice(p->device), "hipSetDevice");
     hipEventRecord(p->ev_begin, p->stream);
     srt::fw_init(p);
-    srt::fw_rounds(p);
+    srt_status st = srt::fw_rounds(p, err);
+    if (st != SRT_OK) return st;
     srt::fw_extract(p);
     hipEventRecord(p->ev_end, p->stream);
     HIP_TRY(hipGetLastError(), "kernel launch");
@@ -400,6 +441,35 @@ void srt_plan_destroy(srt_plan *p) {
     if (p->ev_end) hipEventDestroy(p->ev_end);
     if (p->own_stream && p->stream) hipStreamDestroy(p->stream);
     delete p;
+}
+
+srt_status srt_plan_bind_comm(srt_plan *p, srt_comm *comm, srt_err *err) {
+    clear_err(err);
+    if (!p || !comm) {
+        set_err(err, SRT_ERR_INVALID, "null plan or communicator");
+        return SRT_ERR_INVALID;
+    }
+    HIP_TRY(hipSetDevice(p->device), "hipSetDevice");
+    // pad the node range so every rank owns the same number of block-rows
+    // (equal all-gather chunks); padded nodes are isolated and never in use
+    const uint32_t unit = (uint32_t)srt::FW_B * (uint32_t)comm->nranks;
+    const uint32_t Vp = std::max<uint32_t>(((p->V + unit - 1) / unit) * unit, unit);
+    if (Vp != p->Vp) {
+        void *ptr = nullptr;
+        hipError_t e = hipMalloc(&ptr, (size_t)Vp * Vp * sizeof(uint64_t));
+        if (e != hipSuccess) return hip_fail(err, e, "hipMalloc(D)");
+        HIP_TRY(hipFree(p->d_D), "hipFree");
+        p->d_D = (uint64_t *)ptr;
+        p->Vp = Vp;
+    }
+    const uint32_t nblk = p->Vp / srt::FW_B, per = nblk / (uint32_t)comm->nranks;
+    p->comm = comm;
+    p->rb0 = per * (uint32_t)comm->rank;
+    p->rb1 = p->rb0 + per;
+    char d[64];
+    std::snprintf(d, sizeof d, " ranks=%d rows=[%u,%u)", comm->nranks, p->rb0 * srt::FW_B, p->rb1 * srt::FW_B);
+    p->desc += d;
+    return SRT_OK;
 }
 
 srt_status srt_compute_shortest_paths(const srt_csr *g, const uint32_t *nodes, uint32_t n,

@@ -2,33 +2,68 @@
 //
 // Replaces NetworkGraph::compute_shortest_paths (src/main/network/graph/mod.rs:183-228):
 // instead of one petgraph Dijkstra per in-use source on a rayon pool, the whole
-// graph is closed in HBM with a three-phase blocked Floyd-Warshall:
-//   round kb:  phase 1+2 (one launch): close the B x B pivot block, then relax
-//              the pivot block-row and block-column through it;
-//              phase 3: every other block C(i,j) = min(C, A(i,kb) (+) B(kb,j)),
-//              a min-plus rank-B update -- the N^3 hot loop.
-// Keys are u64 (see KeyParams in srt_internal.h): integer add + unsigned min
-// implement the lexicographic (latency, loss) algebra of PathProperties.
+// graph is closed in HBM with a three-phase blocked Floyd-Warshall, B = 128:
+//   round kb:  phase 1: close the B x B pivot block P in LDS (one workgroup);
+//              phase 2: pivot block-row    R <- P* (x) R,
+//                       pivot block-column Q <- Q (x) P*      (min-plus products:
+//                       with the closed P* the in-block sequential sweep of FW
+//                       collapses to one product);
+//              phase 3: every other block C <- min(C, Q(i) (x) R(j)) -- the N^3
+//                       hot loop, a min-plus "GEMM" with K = B.
+// Phases 2 and 3 run the same tile kernel (minplus_tile_kernel).
+//
+// Path keys (see KeyParams, srt_internal.h) are exact integers packed as
+//   key = (latency/g) << qb | round(-ln(1-loss) * 2^s)
+// carried either as f64 (< 2^53, the fast path: v_add_f64 + v_min_f64 = 2 VALU
+// ops per relaxation) or as u64 (< 2^62: v_lshl_add_u64 + v_cmp_lt_u64 +
+// 2 v_cndmask = 4 ops).  Both give bit-identical tables; the host picks f64
+// whenever its bound proof fits in 53 bits.
+#include <type_traits>
+
 #include "srt_internal.h"
 
 namespace srt {
 
 namespace {
 
-constexpr int B = FW_B;       // 64
-constexpr int NT = 256;       // threads per workgroup (4 waves)
-constexpr int TPR = 16;       // threads per row of the 16x16 thread grid
-constexpr int RPT = B / TPR;  // 4 rows / cols per thread
+constexpr int B = FW_B;  // 128: pivot block / tile edge
+constexpr int KC = 32;   // k-chunk staged in LDS per step of the tile kernel
+constexpr int NT3 = 256; // tile kernel: 4 waves; 66 KB LDS -> 2 workgroups per CU
+constexpr int TR = 8;    // rows per thread   (128 / 16 row-threads)
+constexpr int TC = 8;    // cols per thread   (128 / 16 col-threads)
 
-__device__ __forceinline__ uint64_t kmin(uint64_t a, uint64_t b) { return a < b ? a : b; }
+template <typename K>
+struct KeyOps;
+
+template <>
+struct KeyOps<uint64_t> {
+    static __device__ __forceinline__ uint64_t inf() { return KEY_INF; }
+    static __device__ __forceinline__ uint64_t zero() { return 0ull; }
+    static __device__ __forceinline__ uint64_t kmin(uint64_t a, uint64_t b) { return a < b ? a : b; }
+    static __device__ __forceinline__ uint64_t from_int(uint64_t v) { return v; }
+    static __device__ __forceinline__ bool is_inf(uint64_t k) { return k >= KEY_INF; }
+    static __device__ __forceinline__ uint64_t to_int(uint64_t k) { return k; }
+};
+
+template <>
+struct KeyOps<double> {
+    static __device__ __forceinline__ double inf() { return __builtin_huge_val(); }
+    static __device__ __forceinline__ double zero() { return 0.0; }
+    // keys are never NaN: v_min_f64 directly (no canonicalisation needed)
+    static __device__ __forceinline__ double kmin(double a, double b) { return __builtin_fmin(a, b); }
+    static __device__ __forceinline__ double from_int(uint64_t v) { return (double)v; }
+    static __device__ __forceinline__ bool is_inf(double k) { return !(k < 9007199254740992.0); }
+    static __device__ __forceinline__ uint64_t to_int(double k) { return (uint64_t)k; }
+};
 
 // ------------------------------------------------------------------ init
-__global__ void fill_kernel(uint64_t *__restrict__ D, uint32_t Vp) {
+template <typename K>
+__global__ void fill_kernel(K *__restrict__ D, uint32_t Vp) {
     const uint64_t total = (uint64_t)Vp * Vp;
     for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < total;
          e += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t r = (uint32_t)(e / Vp), c = (uint32_t)(e % Vp);
-        D[e] = (r == c) ? 0ull : KEY_INF;
+        D[e] = (r == c) ? KeyOps<K>::zero() : KeyOps<K>::inf();
     }
 }
 
@@ -36,16 +71,17 @@ __device__ __forceinline__ uint64_t edge_key(uint64_t lat, float loss, const Key
     const uint64_t lq = lat / kp.g;
     uint64_t q = 0;
     if (kp.qb) {
-        const double nl = -log1p(-(double)loss);  // -ln(1 - loss) >= 0
+        const double nl = -log1p(-(double)loss);  // -ln(1 - loss) >= 0; loss 1 -> +inf
         q = (nl >= kp.nlr_cap) ? kp.q_cap : (uint64_t)llrint(nl * kp.scale);
     }
     return (lq << kp.qb) | q;
 }
 
-// One wave per graph node row: D[u][v] = min over parallel edges u->v.  The
-// diagonal keeps 0 (a self-loop never shortens a path; it is written into the
-// table verbatim by the extract kernel, mod.rs:210-217).
-__global__ void scatter_edges_kernel(uint64_t *__restrict__ D, uint32_t Vp,
+// D[u][v] = min over parallel edges u->v (one wave per graph row).  The
+// diagonal keeps 0: a self-loop never shortens a path, and the table's
+// diagonal is the raw self-loop written by the extract kernel (mod.rs:210-217).
+template <typename K>
+__global__ void scatter_edges_kernel(K *__restrict__ D, uint32_t Vp,
                                      const uint64_t *__restrict__ row_ptr,
                                      const uint32_t *__restrict__ col,
                                      const uint64_t *__restrict__ lat,
@@ -58,161 +94,219 @@ __global__ void scatter_edges_kernel(uint64_t *__restrict__ D, uint32_t Vp,
         for (uint64_t k = b + lane; k < e; k += 64) {
             const uint32_t v = col[k];
             if (v == u) continue;
-            atomicMin((unsigned long long *)&D[(uint64_t)u * Vp + v],
-                      (unsigned long long)edge_key(lat[k], loss[k], kp));
+            // integer key order == f64 order for exact integers: atomicMin on the
+            // u64 value works for both representations (f64 bits of non-negative
+            // doubles order like the doubles)
+            const uint64_t key = edge_key(lat[k], loss[k], kp);
+            uint64_t bits;
+            if constexpr (std::is_same<K, double>::value) {
+                const double d = (double)key;
+                bits = __builtin_bit_cast(uint64_t, d);
+            } else {
+                bits = key;
+            }
+            atomicMin((unsigned long long *)&D[(uint64_t)u * Vp + v], (unsigned long long)bits);
         }
     }
 }
 
-// ------------------------------------------------------- phase 1 + phase 2
-// Block 0 closes the pivot block and writes it back; every other block closes
-// the pivot block redundantly in LDS (64 short steps, far cheaper than an extra
-// launch) and then relaxes one block of the pivot row (blockIdx < nblk) or
-// pivot column through it.
-__global__ __launch_bounds__(NT) void fw_phase12_kernel(uint64_t *__restrict__ D, uint32_t Vp,
-                                                        uint32_t kb, uint32_t nblk) {
-    __shared__ uint64_t P[B][B + 1];  // pivot block
-    __shared__ uint64_t O[B][B + 1];  // own block
-    const int tid = threadIdx.x, tx = tid % TPR, ty = tid / TPR;
-    const uint64_t kb0 = (uint64_t)kb * B;
-
-    for (int e = tid; e < B * B; e += NT) {
-        const int r = e / B, c = e % B;
-        P[r][c] = D[(kb0 + r) * Vp + kb0 + c];
+// ------------------------------------------------------------- phase 1
+// Close the 128x128 pivot block: 1024 threads; thread (c = tid % 128,
+// r0 = tid / 128) keeps P[r0 + 8i][c] (i < 16) in registers.  Step k only needs
+// row k and column k of P, published through two small double-buffered LDS
+// vectors by their owners: one barrier per step.
+template <typename K>
+__global__ __launch_bounds__(1024) void fw_phase1_kernel(K *__restrict__ D, uint32_t Vp, uint32_t kb) {
+    __shared__ K rowbuf[2][B];
+    __shared__ K colbuf[2][B];
+    const int tid = threadIdx.x;
+    const int c = tid % B, r0 = tid / B;
+    const uint64_t k0 = (uint64_t)kb * B;
+    K p[B / 8];
+#pragma unroll
+    for (int i = 0; i < B / 8; ++i) p[i] = D[(k0 + r0 + 8 * i) * Vp + k0 + c];
+    // publish step 0
+    if (r0 == 0) rowbuf[0][c] = p[0];
+    if (c == 0) {
+#pragma unroll
+        for (int i = 0; i < B / 8; ++i) colbuf[0][r0 + 8 * i] = p[i];
     }
     __syncthreads();
     for (int k = 0; k < B; ++k) {
+        const int cur = k & 1, nxt = cur ^ 1;
+        const K pkc = rowbuf[cur][c];
 #pragma unroll
-        for (int i = 0; i < RPT; ++i)
+        for (int i = 0; i < B / 8; ++i) p[i] = KeyOps<K>::kmin(p[i], colbuf[cur][r0 + 8 * i] + pkc);
+        // owners of row k+1 / column k+1 publish their (now final for step k) values
+        const int kn = k + 1;
+        if (kn < B) {
+            if (r0 == (kn & 7)) {
 #pragma unroll
-            for (int j = 0; j < RPT; ++j) {
-                const int r = ty + TPR * i, c = tx + TPR * j;
-                P[r][c] = kmin(P[r][c], P[r][k] + P[k][c]);
+                for (int i = 0; i < B / 8; ++i)
+                    if (i == (kn >> 3)) rowbuf[nxt][c] = p[i];
             }
-        __syncthreads();
-    }
-    if (blockIdx.x == 0) {
-        for (int e = tid; e < B * B; e += NT) {
-            const int r = e / B, c = e % B;
-            D[(kb0 + r) * Vp + kb0 + c] = P[r][c];
+            if (c == kn) {
+#pragma unroll
+                for (int i = 0; i < B / 8; ++i) colbuf[nxt][r0 + 8 * i] = p[i];
+            }
         }
-        return;
-    }
-    // which block: 1..nblk-1 -> row blocks (skipping kb), nblk..2*nblk-2 -> column blocks
-    uint32_t idx = blockIdx.x - 1;
-    const bool is_row = idx < nblk - 1;
-    if (!is_row) idx -= nblk - 1;
-    const uint32_t other = idx < kb ? idx : idx + 1;
-    const uint64_t r0 = is_row ? kb0 : (uint64_t)other * B;
-    const uint64_t c0 = is_row ? (uint64_t)other * B : kb0;
-    for (int e = tid; e < B * B; e += NT) {
-        const int r = e / B, c = e % B;
-        O[r][c] = D[(r0 + r) * Vp + c0 + c];
-    }
-    __syncthreads();
-    for (int k = 0; k < B; ++k) {
-#pragma unroll
-        for (int i = 0; i < RPT; ++i)
-#pragma unroll
-            for (int j = 0; j < RPT; ++j) {
-                const int r = ty + TPR * i, c = tx + TPR * j;
-                const uint64_t cand = is_row ? P[r][k] + O[k][c] : O[r][k] + P[k][c];
-                O[r][c] = kmin(O[r][c], cand);
-            }
         __syncthreads();
     }
-    for (int e = tid; e < B * B; e += NT) {
-        const int r = e / B, c = e % B;
-        D[(r0 + r) * Vp + c0 + c] = O[r][c];
-    }
+#pragma unroll
+    for (int i = 0; i < B / 8; ++i) D[(k0 + r0 + 8 * i) * Vp + k0 + c] = p[i];
 }
 
-// ------------------------------------------------------------- phase 3
-// C(i,j) = min(C(i,j), min_k A(i,k) + B(k,j)) for all blocks i,j != kb.
-// grid = (nblk-1)^2 blocks; the pivot row/column are skipped by index remap.
-__global__ __launch_bounds__(NT) void fw_phase3_kernel(uint64_t *__restrict__ D, uint32_t Vp,
-                                                       uint32_t kb, uint32_t nblk) {
-    __shared__ uint64_t As[B][B + 1];  // As[r][k] = D[i-block row r][pivot col k]
-    __shared__ uint64_t Bs[B][B];      // Bs[k][c] = D[pivot row k][j-block col c]
-    const int tid = threadIdx.x, tx = tid % TPR, ty = tid / TPR;
+// ------------------------------------------------------ phases 2 and 3
+// One 128x128 output tile C per workgroup: C <- min(C, A (x) Bm), A = 128 x 128
+// (rows of C, pivot columns), Bm = 128 x 128 (pivot rows, columns of C).
+// MODE 0 (phase 3): tiles (bi, bj), bi, bj != kb, XCD-grouped by rows.
+// MODE 1 (phase 2): tiles of the pivot row (A = P*) and pivot column (Bm = P*).
+// A or Bm may alias C in MODE 1: both are fully staged in LDS before C is
+// written, and every tile is owned by exactly one workgroup.
+template <typename K, int MODE>
+__global__ __launch_bounds__(NT3) void minplus_tile_kernel(K *__restrict__ D, uint32_t Vp,
+                                                           uint32_t kb, uint32_t nblk,
+                                                           uint32_t rb0, uint32_t rb1) {
+    __shared__ K As[B][KC + 1];  // As[row][k]
+    __shared__ K Bs[KC][B];      // Bs[k][col]
+    // local block-rows [rb0, rb1) without the pivot row kb
+    const bool kb_local = kb >= rb0 && kb < rb1;
+    const uint32_t mr = (rb1 - rb0) - (kb_local ? 1u : 0u);
     const uint32_t m = nblk - 1;
-    uint32_t bi = blockIdx.x / m, bj = blockIdx.x % m;
-    bi += bi >= kb;
-    bj += bj >= kb;
+    auto local_row = [&](uint32_t idx) {
+        uint32_t bi = rb0 + idx;
+        return (kb_local && bi >= kb) ? bi + 1 : bi;
+    };
+    uint32_t bi, bj;
+    if (MODE == 0) {
+        // phase 3.  XCD-aware bijective remap: blocks b and b+8 share an XCD
+        // (round-robin dispatch); each XCD gets a contiguous run of row-major
+        // tiles, so A-panel rows and many B-panel columns stay in its L2.
+        const uint32_t nwg = mr * m, orig = blockIdx.x;
+        const uint32_t q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
+        const uint32_t t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+        bi = local_row(t / m);
+        bj = t % m;
+        bj += bj >= kb;
+    } else {
+        uint32_t t = blockIdx.x;
+        const bool row_tile = (MODE == 1) || (MODE == 3 && t < m);
+        if (MODE == 3 && !row_tile) t -= m;
+        if (row_tile) {  // pivot block-row: C = R(bj), A = P*
+            bi = kb;
+            bj = t + (t >= kb);
+        } else {  // pivot block-column of a local row: C = Q(bi), Bm = P*
+            bi = local_row(t);
+            bj = kb;
+        }
+    }
     const uint64_t i0 = (uint64_t)bi * B, j0 = (uint64_t)bj * B, k0 = (uint64_t)kb * B;
+    const int tid = threadIdx.x;
+    const int tx = tid % 16, ty = tid / 16;  // 16 column-threads x 16 row-threads
 
-    for (int e = tid; e < B * B; e += NT) {
-        const int r = e / B, c = e % B;
-        As[r][c] = D[(i0 + r) * Vp + k0 + c];
-        Bs[r][c] = D[(k0 + r) * Vp + j0 + c];
+    // C sub-tile: rows ty*8 .. ty*8+7 (A reads: 4 distinct rows per wave, broadcast),
+    // cols tx + 16 j (B reads and C stores: 16 consecutive keys per wave row)
+    K acc[TR][TC];
+#pragma unroll
+    for (int i = 0; i < TR; ++i) {
+        const K *src = D + (i0 + ty * TR + i) * Vp + j0 + tx;
+#pragma unroll
+        for (int j = 0; j < TC; ++j) acc[i][j] = src[16 * j];
     }
-    uint64_t acc[RPT][RPT];
+    for (int kc = 0; kc < B; kc += KC) {
+        // stage A[i0.., k0+kc..] and Bm[k0+kc.., j0..]
+        for (int e = tid; e < B * KC; e += NT3) {
+            const int r = e / KC, c = e % KC;
+            As[r][c] = D[(i0 + r) * Vp + k0 + kc + c];
+        }
+        for (int e = tid; e < KC * B; e += NT3) {
+            const int r = e / B, c = e % B;
+            Bs[r][c] = D[(k0 + kc + r) * Vp + j0 + c];
+        }
+        __syncthreads();
+#pragma unroll 2
+        for (int k = 0; k < KC; ++k) {
+            K a[TR], b[TC];
 #pragma unroll
-    for (int i = 0; i < RPT; ++i)
+            for (int i = 0; i < TR; ++i) a[i] = As[ty * TR + i][k];
 #pragma unroll
-        for (int j = 0; j < RPT; ++j) acc[i][j] = D[(i0 + ty + TPR * i) * Vp + j0 + tx + TPR * j];
-    __syncthreads();
-#pragma unroll 4
-    for (int k = 0; k < B; ++k) {
-        uint64_t a[RPT], b[RPT];
+            for (int j = 0; j < TC; ++j) b[j] = Bs[k][tx + 16 * j];
 #pragma unroll
-        for (int i = 0; i < RPT; ++i) a[i] = As[ty + TPR * i][k];
+            for (int i = 0; i < TR; ++i)
 #pragma unroll
-        for (int j = 0; j < RPT; ++j) b[j] = Bs[k][tx + TPR * j];
-#pragma unroll
-        for (int i = 0; i < RPT; ++i)
-#pragma unroll
-            for (int j = 0; j < RPT; ++j) acc[i][j] = kmin(acc[i][j], a[i] + b[j]);
+                for (int j = 0; j < TC; ++j) acc[i][j] = KeyOps<K>::kmin(acc[i][j], a[i] + b[j]);
+        }
+        __syncthreads();
     }
 #pragma unroll
-    for (int i = 0; i < RPT; ++i)
+    for (int i = 0; i < TR; ++i) {
+        K *dst = D + (i0 + ty * TR + i) * Vp + j0 + tx;
 #pragma unroll
-        for (int j = 0; j < RPT; ++j) D[(i0 + ty + TPR * i) * Vp + j0 + tx + TPR * j] = acc[i][j];
+        for (int j = 0; j < TC; ++j) dst[16 * j] = acc[i][j];
+    }
 }
 
 // ------------------------------------------------------------- extract
 // table[i][j] = decode(D[nodes[i]][nodes[j]]); diagonal = the raw self-loop
 // edge (mod.rs:210-217); min latency over the whole table (mod.rs:474-476);
 // count of unreachable pairs (the reference's assert at mod.rs:219).
-__global__ void extract_kernel(const uint64_t *__restrict__ D, uint32_t Vp,
-                               const uint32_t *__restrict__ nodes, uint32_t n, KeyParams kp,
-                               const uint64_t *__restrict__ sl_lat,
-                               const float *__restrict__ sl_loss, uint64_t *__restrict__ out_lat,
-                               float *__restrict__ out_loss, unsigned long long *stats) {
-    const uint32_t cb = (n + blockDim.x - 1) / blockDim.x;  // column blocks per row
-    const uint32_t i = blockIdx.x / cb;
-    const uint32_t j = (blockIdx.x % cb) * blockDim.x + threadIdx.x;
-    uint64_t lat = ~0ull;
-    unsigned unreach = 0;
-    if (j < n) {
-        float loss;
-        if (i == j) {
-            lat = sl_lat[i];
-            loss = sl_loss[i];
-        } else {
-            const uint64_t k = D[(uint64_t)nodes[i] * Vp + nodes[j]];
-            if (k >= KEY_INF) {
-                unreach = 1;
-                lat = ~0ull;
-                loss = 1.0f;
+template <typename K>
+__global__ __launch_bounds__(256) void extract_kernel(const K *__restrict__ D, uint32_t Vp,
+                                                      const uint32_t *__restrict__ nodes, uint32_t n,
+                                                      KeyParams kp, const uint64_t *__restrict__ sl_lat,
+                                                      const float *__restrict__ sl_loss,
+                                                      uint64_t *__restrict__ out_lat,
+                                                      float *__restrict__ out_loss,
+                                                      unsigned long long *stats) {
+    // grid-stride over rows; one block-level reduction and 2 atomics per block
+    __shared__ unsigned long long red_min[4], red_cnt[4];
+    uint64_t mn = ~0ull;
+    unsigned long long unreach = 0;
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const K *row = D + (uint64_t)nodes[i] * Vp;
+        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
+            uint64_t lat;
+            float loss;
+            if (i == j) {
+                lat = sl_lat[i];
+                loss = sl_loss[i];
             } else {
-                lat = (k >> kp.qb) * kp.g;
-                const uint64_t q = kp.qb ? (k & ((1ull << kp.qb) - 1)) : 0ull;
-                loss = (float)(-expm1(-(double)q * kp.inv_scale));
+                const K kk = row[nodes[j]];
+                if (KeyOps<K>::is_inf(kk)) {
+                    ++unreach;
+                    lat = ~0ull;
+                    loss = 1.0f;
+                } else {
+                    const uint64_t k = KeyOps<K>::to_int(kk);
+                    lat = (k >> kp.qb) * kp.g;
+                    const uint64_t q = kp.qb ? (k & ((1ull << kp.qb) - 1)) : 0ull;
+                    loss = q ? (float)(-expm1(-(double)q * kp.inv_scale)) : 0.0f;
+                }
             }
+            out_lat[(uint64_t)i * n + j] = lat;
+            out_loss[(uint64_t)i * n + j] = loss;
+            mn = lat < mn ? lat : mn;
         }
-        out_lat[(uint64_t)i * n + j] = lat;
-        out_loss[(uint64_t)i * n + j] = loss;
     }
-    // wave reductions then one atomic per wave
     for (int off = 32; off > 0; off >>= 1) {
-        const uint64_t o = __shfl_xor(lat, off);
-        lat = o < lat ? o : lat;
+        const uint64_t o = __shfl_xor(mn, off);
+        mn = o < mn ? o : mn;
         unreach += __shfl_xor(unreach, off);
     }
+    const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
-        atomicMin(&stats[0], (unsigned long long)lat);
-        if (unreach) atomicAdd(&stats[1], (unsigned long long)unreach);
+        red_min[w] = mn;
+        red_cnt[w] = unreach;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long m = red_min[0], c = red_cnt[0];
+        for (int k = 1; k < (int)(blockDim.x >> 6); ++k) {
+            m = red_min[k] < m ? red_min[k] : m;
+            c += red_cnt[k];
+        }
+        atomicMin(&stats[0], m);
+        if (c) atomicAdd(&stats[1], c);
     }
 }
 
@@ -233,16 +327,21 @@ __global__ void pack_kernel(const uint64_t *__restrict__ lat, const float *__res
     }
 }
 
-}  // namespace
-
-void fw_init(srt_plan *p) {
-    hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, p->stream, p->d_D, p->Vp);
-    hipLaunchKernelGGL(scatter_edges_kernel, dim3(2048), dim3(256), 0, p->stream, p->d_D, p->Vp,
+template <typename K>
+void fw_init_t(srt_plan *p) {
+    K *D = reinterpret_cast<K *>(p->d_D);
+    hipLaunchKernelGGL(fill_kernel<K>, dim3(4096), dim3(256), 0, p->stream, D, p->Vp);
+    hipLaunchKernelGGL(scatter_edges_kernel<K>, dim3(2048), dim3(256), 0, p->stream, D, p->Vp,
                        p->d_row_ptr, p->d_col, p->d_lat, p->d_loss, p->V, p->kp);
 }
 
-void fw_rounds(srt_plan *p) {
+template <typename K>
+srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
+    K *D = reinterpret_cast<K *>(p->d_D);
     const uint32_t nblk = p->Vp / B;
+    const uint32_t rb0 = p->rb0, rb1 = p->rb1;
+    const bool sharded = p->comm != nullptr;  // a 1-rank comm runs the same schedule (tested)
+    const uint32_t per_rank = sharded ? nblk / p->comm->nranks : nblk;
     p->p3_launches = 0;
     const size_t need = 2 * (size_t)nblk;
     while (p->ev.size() < need) {
@@ -251,25 +350,60 @@ void fw_rounds(srt_plan *p) {
         p->ev.push_back(e);
     }
     for (uint32_t kb = 0; kb < nblk; ++kb) {
-        hipLaunchKernelGGL(fw_phase12_kernel, dim3(nblk > 1 ? 2 * nblk - 1 : 1), dim3(NT), 0,
-                           p->stream, p->d_D, p->Vp, kb, nblk);
-        if (nblk > 1) {
-            hipEventRecord(p->ev[2 * kb], p->stream);
-            hipLaunchKernelGGL(fw_phase3_kernel, dim3((nblk - 1) * (nblk - 1)), dim3(NT), 0,
-                               p->stream, p->d_D, p->Vp, kb, nblk);
-            hipEventRecord(p->ev[2 * kb + 1], p->stream);
-            p->p3_launches++;
+        const bool own = kb >= rb0 && kb < rb1;
+        const uint32_t mr = (rb1 - rb0) - (own ? 1u : 0u);
+        if (own) hipLaunchKernelGGL(fw_phase1_kernel<K>, dim3(1), dim3(1024), 0, p->stream, D, p->Vp, kb);
+        if (nblk == 1) break;
+        if (!sharded) {
+            hipLaunchKernelGGL((minplus_tile_kernel<K, 3>), dim3(2 * (nblk - 1)), dim3(NT3), 0, p->stream,
+                               D, p->Vp, kb, nblk, rb0, rb1);
+        } else {
+            if (own)
+                hipLaunchKernelGGL((minplus_tile_kernel<K, 1>), dim3(nblk - 1), dim3(NT3), 0, p->stream, D,
+                                   p->Vp, kb, nblk, rb0, rb1);
+            // the pivot block-row sits at the same offset on every rank
+            srt_status st = comm_bcast(p->comm, D + (uint64_t)kb * B * p->Vp,
+                                       (size_t)B * p->Vp * sizeof(K), (int)(kb / per_rank), p->stream, err);
+            if (st != SRT_OK) return st;
+            if (mr)
+                hipLaunchKernelGGL((minplus_tile_kernel<K, 2>), dim3(mr), dim3(NT3), 0, p->stream, D, p->Vp,
+                                   kb, nblk, rb0, rb1);
         }
+        if (mr == 0) continue;
+        hipEventRecord(p->ev[2 * p->p3_launches], p->stream);
+        hipLaunchKernelGGL((minplus_tile_kernel<K, 0>), dim3(mr * (nblk - 1)), dim3(NT3), 0, p->stream, D,
+                           p->Vp, kb, nblk, rb0, rb1);
+        hipEventRecord(p->ev[2 * p->p3_launches + 1], p->stream);
+        p->p3_launches++;
     }
+    if (sharded)
+        return comm_allgather_inplace(p->comm, D, (size_t)per_rank * B * p->Vp * sizeof(K), p->stream, err);
+    return SRT_OK;
+}
+
+template <typename K>
+void fw_extract_t(srt_plan *p) {
+    hipLaunchKernelGGL(init_stats_kernel, dim3(1), dim3(1), 0, p->stream, p->d_stats);
+    const uint32_t blocks = p->n < 4096 ? (p->n ? p->n : 1) : 4096;
+    hipLaunchKernelGGL(extract_kernel<K>, dim3(blocks), dim3(256), 0, p->stream,
+                       reinterpret_cast<const K *>(p->d_D), p->Vp, p->d_nodes, p->n, p->kp,
+                       p->d_sl_lat, p->d_sl_loss, p->d_out_lat, p->d_out_loss, p->d_stats);
+}
+
+}  // namespace
+
+void fw_init(srt_plan *p) {
+    if (p->key_f64) fw_init_t<double>(p);
+    else fw_init_t<uint64_t>(p);
+}
+
+srt_status fw_rounds(srt_plan *p, srt_err *err) {
+    return p->key_f64 ? fw_rounds_t<double>(p, err) : fw_rounds_t<uint64_t>(p, err);
 }
 
 void fw_extract(srt_plan *p) {
-    hipLaunchKernelGGL(init_stats_kernel, dim3(1), dim3(1), 0, p->stream, p->d_stats);
-    const uint32_t cb = (p->n + 255) / 256;
-    dim3 grid(cb * p->n);
-    hipLaunchKernelGGL(extract_kernel, grid, dim3(256), 0, p->stream, p->d_D, p->Vp, p->d_nodes,
-                       p->n, p->kp, p->d_sl_lat, p->d_sl_loss, p->d_out_lat, p->d_out_loss,
-                       p->d_stats);
+    if (p->key_f64) fw_extract_t<double>(p);
+    else fw_extract_t<uint64_t>(p);
 }
 
 void pack_paths(srt_plan *p) {

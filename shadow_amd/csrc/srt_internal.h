@@ -36,7 +36,7 @@ struct KeyParams {
 };
 
 // FW tile geometry: B x B blocks, one block-row/column per round.
-constexpr int FW_B = 64;
+constexpr int FW_B = 128;
 
 struct FwTimers {
     std::vector<hipEvent_t> ev;  // 2 per phase-3 launch
@@ -45,7 +45,14 @@ struct FwTimers {
 
 }  // namespace srt
 
-struct srt_comm;
+struct srt_comm {
+    int nranks = 1;
+    int rank = 0;
+    void *nccl = nullptr;  // ncclComm_t when the RCCL transport is used
+    srt_bcast_fn bcast = nullptr;
+    srt_allgather_fn allgather = nullptr;
+    void *user = nullptr;
+};
 
 struct srt_plan {
     int device = 0;
@@ -57,6 +64,7 @@ struct srt_plan {
     uint64_t n_adj = 0;
     int algo = SRT_ALGO_FW;
     srt::KeyParams kp{};
+    bool key_f64 = false;  // f64-encoded keys (exact integers < 2^53)
     std::string desc;
     bool identity_nodes = false;
 
@@ -87,14 +95,19 @@ struct srt_plan {
     double p3_ms = 0.0, total_ms = 0.0;
     bool ran = false;
 
-    // multi-GPU
+    // multi-GPU: this rank computes block-rows [rb0, rb1) of the closure
     srt_comm *comm = nullptr;
+    uint32_t rb0 = 0, rb1 = 0;
 };
 
 namespace srt {
+// collectives (srt_comm.cpp)
+srt_status comm_bcast(srt_comm *c, void *buf, size_t bytes, int root, hipStream_t s, srt_err *err);
+srt_status comm_allgather_inplace(srt_comm *c, void *buf, size_t bytes_per_rank, hipStream_t s,
+                                  srt_err *err);
 // kernels (srt_fw.hip)
 void fw_init(srt_plan *p);
-void fw_rounds(srt_plan *p);
+srt_status fw_rounds(srt_plan *p, srt_err *err);
 void fw_extract(srt_plan *p);
 void pack_paths(srt_plan *p);
 }  // namespace srt

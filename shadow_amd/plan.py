@@ -84,6 +84,10 @@ class RoutingPlan:
         if self._h:
             _lib.lib().srt_plan_destroy(self._h)
             self._h = C.c_void_p()
+        comm = getattr(self, "_comm", None)
+        if comm is not None:  # the plan referenced it: destroy after the plan
+            comm.close()
+            self._comm = None
 
     def __del__(self):
         try:

@@ -1,0 +1,54 @@
+"""One rank of the sharded routing build (spawned by tests/test_gpu_dist.py).
+
+usage: dist_worker.py RANK WORLD PORT N SEED TRANSPORT
+All ranks share cuda:0 (the box has one GPU); collectives go through
+torch.distributed/gloo via the callback transport, which exercises exactly the
+same per-round schedule as the RCCL transport.  Exit code 0 = table matches
+the oracle (rank 0 checks; every rank checks its own table equals rank 0's
+via a checksum).
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    rank, world, port, n, seed = (int(x) for x in sys.argv[1:6])
+    transport = sys.argv[6]
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from shadow_amd import NetworkGraph, synth
+    from shadow_amd import dist as sdist
+    from shadow_amd.plan import RoutingPlan
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    src, dst, lat, loss = synth.random_graph(n, seed, p_edge=0.08, directed=True, lat_range_ns=(1, 9),
+                                             loss_max=0.05)
+    g = NetworkGraph.from_edges(n, src, dst, lat, loss, directed=True)
+    nodes = np.random.default_rng(seed).permutation(n).astype(np.uint32)
+    plan = RoutingPlan(g, nodes, device=0)
+    sdist.bind(plan, rank, world, 0, transport=transport)
+    plan.run()
+    t = plan.fetch()
+    ck = torch.tensor([int(np.bitwise_xor.reduce(t.latency_ns.reshape(-1) * np.uint64(2654435761))),
+                       int(np.bitwise_xor.reduce(t.packet_loss.view(np.uint32).reshape(-1)))], dtype=torch.int64)
+    all_ck = [torch.zeros_like(ck) for _ in range(world)]
+    dist.all_gather(all_ck, ck)
+    ok = all(bool((c == all_ck[0]).all()) for c in all_ck)
+    if rank == 0:
+        from oracle import oracle as O
+        elat, eloss = O.compute_shortest_paths(O.Graph(True, np.arange(n), src, dst, lat, loss), nodes)
+        ok = ok and np.array_equal(t.latency_ns, elat)
+        ok = ok and float(np.abs(t.packet_loss.astype(np.float64) - eloss).max()) <= 1e-6
+        print(f"rank0: {plan.describe()} ok={ok}", flush=True)
+    plan.close()
+    dist.destroy_process_group()
+    sys.exit(0 if ok else 1)
+
+
+if __name__ == "__main__":
+    main()
