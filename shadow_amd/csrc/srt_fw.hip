@@ -27,7 +27,7 @@ namespace srt {
 namespace {
 
 constexpr int B = FW_B;  // 128: pivot block / tile edge
-constexpr int KC = 32;   // k-chunk staged in LDS per step of the tile kernel
+constexpr int KC = 16;   // k-chunk staged in LDS per pipeline step of the tile kernel
 constexpr int NT3 = 256; // tile kernel: 4 waves; 66 KB LDS -> 2 workgroups per CU
 constexpr int TR = 8;    // rows per thread   (128 / 16 row-threads)
 constexpr int TC = 8;    // cols per thread   (128 / 16 col-threads)
@@ -49,12 +49,53 @@ template <>
 struct KeyOps<double> {
     static __device__ __forceinline__ double inf() { return __builtin_huge_val(); }
     static __device__ __forceinline__ double zero() { return 0.0; }
-    // keys are never NaN: v_min_f64 directly (no canonicalisation needed)
-    static __device__ __forceinline__ double kmin(double a, double b) { return __builtin_fmin(a, b); }
+    // Keys are never NaN, so v_min_f64 needs no IEEE-mode input quieting; with
+    // __builtin_fmin hipcc emits a v_max_f64 x,x,x canonicalisation per operand
+    // on loop-carried values (+50% VALU in the hot loop), hence the asm.
+    static __device__ __forceinline__ double kmin(double a, double b) {
+        double r;
+        asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+        return r;
+    }
     static __device__ __forceinline__ double from_int(uint64_t v) { return (double)v; }
     static __device__ __forceinline__ bool is_inf(double k) { return !(k < 9007199254740992.0); }
     static __device__ __forceinline__ uint64_t to_int(double k) { return (uint64_t)k; }
 };
+
+// One row of the register tile: acc[j] = min(acc[j], a + b[j]), j < 8.
+// f64: the 8 adds are issued before the 8 mins (dependency distance 8) -- left
+// to itself hipcc reuses one temporary and pairs every add with its min.
+template <typename K>
+__device__ __forceinline__ void relax_row8(K (&acc)[8], K a, const K (&b)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = KeyOps<K>::kmin(acc[j], a + b[j]);
+}
+
+template <>
+__device__ __forceinline__ void relax_row8<double>(double (&acc)[8], double a, const double (&b)[8]) {
+    double t0, t1, t2, t3, t4, t5, t6, t7;
+    asm("v_add_f64 %0, %16, %17\n\t"
+        "v_add_f64 %1, %16, %18\n\t"
+        "v_add_f64 %2, %16, %19\n\t"
+        "v_add_f64 %3, %16, %20\n\t"
+        "v_add_f64 %4, %16, %21\n\t"
+        "v_add_f64 %5, %16, %22\n\t"
+        "v_add_f64 %6, %16, %23\n\t"
+        "v_add_f64 %7, %16, %24\n\t"
+        "v_min_f64 %8, %8, %0\n\t"
+        "v_min_f64 %9, %9, %1\n\t"
+        "v_min_f64 %10, %10, %2\n\t"
+        "v_min_f64 %11, %11, %3\n\t"
+        "v_min_f64 %12, %12, %4\n\t"
+        "v_min_f64 %13, %13, %5\n\t"
+        "v_min_f64 %14, %14, %6\n\t"
+        "v_min_f64 %15, %15, %7"
+        : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "=&v"(t4), "=&v"(t5), "=&v"(t6), "=&v"(t7),
+          "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]),
+          "+v"(acc[6]), "+v"(acc[7])
+        : "v"(a), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]),
+          "v"(b[7]));
+}
 
 // ------------------------------------------------------------------ init
 template <typename K>
@@ -164,11 +205,11 @@ __global__ __launch_bounds__(1024) void fw_phase1_kernel(K *__restrict__ D, uint
 // A or Bm may alias C in MODE 1: both are fully staged in LDS before C is
 // written, and every tile is owned by exactly one workgroup.
 template <typename K, int MODE>
-__global__ __launch_bounds__(NT3) void minplus_tile_kernel(K *__restrict__ D, uint32_t Vp,
+__global__ __launch_bounds__(NT3, 2) void minplus_tile_kernel(K *__restrict__ D, uint32_t Vp,
                                                            uint32_t kb, uint32_t nblk,
                                                            uint32_t rb0, uint32_t rb1) {
-    __shared__ K As[B][KC + 1];  // As[row][k]
-    __shared__ K Bs[KC][B];      // Bs[k][col]
+    __shared__ K As[2][B][KC + 1];  // As[buf][row][k]  (double-buffered)
+    __shared__ K Bs[2][KC][B];      // Bs[buf][k][col]
     // local block-rows [rb0, rb1) without the pivot row kb
     const bool kb_local = kb >= rb0 && kb < rb1;
     const uint32_t mr = (rb1 - rb0) - (kb_local ? 1u : 0u);
@@ -213,29 +254,61 @@ __global__ __launch_bounds__(NT3) void minplus_tile_kernel(K *__restrict__ D, ui
 #pragma unroll
         for (int j = 0; j < TC; ++j) acc[i][j] = src[16 * j];
     }
-    for (int kc = 0; kc < B; kc += KC) {
-        // stage A[i0.., k0+kc..] and Bm[k0+kc.., j0..]
-        for (int e = tid; e < B * KC; e += NT3) {
-            const int r = e / KC, c = e % KC;
-            As[r][c] = D[(i0 + r) * Vp + k0 + kc + c];
+    // Two LDS buffers, one barrier per chunk.  With PREFETCH the next chunk is
+    // fetched into registers while the current one is consumed (needs 32 more
+    // VGPRs); without it the next chunk is staged into the other buffer before
+    // the current one is consumed and the 2 workgroups per CU overlap each
+    // other's staging.  Geometry (256 thr): A chunk 128 x KC, B chunk KC x 128.
+    constexpr int NA = B * KC / NT3, NB = KC * B / NT3;
+    constexpr bool PREFETCH = false;
+    K ra[NA], rb[NB];
+    auto fetch = [&](int kc) {
+#pragma unroll
+        for (int m2 = 0; m2 < NA; ++m2) {
+            const int e = tid + NT3 * m2, r = e / KC, c = e % KC;
+            ra[m2] = D[(i0 + r) * Vp + k0 + kc + c];
         }
-        for (int e = tid; e < KC * B; e += NT3) {
-            const int r = e / B, c = e % B;
-            Bs[r][c] = D[(k0 + kc + r) * Vp + j0 + c];
+#pragma unroll
+        for (int m2 = 0; m2 < NB; ++m2) {
+            const int e = tid + NT3 * m2, r = e / B, c = e % B;
+            rb[m2] = D[(k0 + kc + r) * Vp + j0 + c];
         }
-        __syncthreads();
+    };
+    auto stash = [&](int buf) {
+#pragma unroll
+        for (int m2 = 0; m2 < NA; ++m2) {
+            const int e = tid + NT3 * m2, r = e / KC, c = e % KC;
+            As[buf][r][c] = ra[m2];
+        }
+#pragma unroll
+        for (int m2 = 0; m2 < NB; ++m2) {
+            const int e = tid + NT3 * m2, r = e / B, c = e % B;
+            Bs[buf][r][c] = rb[m2];
+        }
+    };
+    fetch(0);
+    stash(0);
+    __syncthreads();
+    constexpr int NCH = B / KC;
+#pragma unroll 1
+    for (int ch = 0; ch < NCH; ++ch) {
+        const int cur = ch & 1;
+        if (PREFETCH && ch + 1 < NCH) fetch((ch + 1) * KC);
+        if (!PREFETCH && ch + 1 < NCH) {  // the other buffer's readers all passed the last barrier
+            fetch((ch + 1) * KC);
+            stash(cur ^ 1);
+        }
 #pragma unroll 2
         for (int k = 0; k < KC; ++k) {
             K a[TR], b[TC];
 #pragma unroll
-            for (int i = 0; i < TR; ++i) a[i] = As[ty * TR + i][k];
+            for (int i = 0; i < TR; ++i) a[i] = As[cur][ty * TR + i][k];
 #pragma unroll
-            for (int j = 0; j < TC; ++j) b[j] = Bs[k][tx + 16 * j];
+            for (int j = 0; j < TC; ++j) b[j] = Bs[cur][k][tx + 16 * j];
 #pragma unroll
-            for (int i = 0; i < TR; ++i)
-#pragma unroll
-                for (int j = 0; j < TC; ++j) acc[i][j] = KeyOps<K>::kmin(acc[i][j], a[i] + b[j]);
+            for (int i = 0; i < TR; ++i) relax_row8<K>(acc[i], a[i], b);
         }
+        if (PREFETCH && ch + 1 < NCH) stash(cur ^ 1);
         __syncthreads();
     }
 #pragma unroll
