@@ -74,6 +74,22 @@ def cpu_baseline(n, seed, threads, sources):
                       f"(oracle mode 0), {dt:.1f} s wall, extrapolated linearly to pairs/s"}
 
 
+def measured_traffic(n, kernel_tag="phase 3 rest"):
+    """HBM bytes per launch of the dominant kernel from the latest committed
+    PMC summary (profiles/rNN_pmc_traffic.json, FETCH_SIZE + WRITE_SIZE passes
+    of rocprofv3 on this same config), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    for f in reversed(files):
+        d = json.load(open(f))
+        if str(n) not in d.get("config", ""):
+            continue
+        for k, v in d.get("kernels", {}).items():
+            if kernel_tag in k:
+                return v["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
+    return None, None
+
+
 def main():
     args = parse_args()
     import torch
@@ -110,15 +126,16 @@ def main():
         plan.run()
     barrier()
     step_ms = []
-    p3_ms, p3_launches = 0.0, 0
+    p3_ms, p3_launches, p3_work = 0.0, 0, 0.0
     t_all0 = time.perf_counter()
     for _ in range(args.steps):
         t0 = time.perf_counter()
         plan.run()
         step_ms.append((time.perf_counter() - t0) * 1e3)
-        a, b, _ = plan.kernel_stats()
+        a, b, w, _ = plan.kernel_stats()
         p3_ms += a
         p3_launches += b
+        p3_work += w
     barrier()
     elapsed = time.perf_counter() - t_all0
     if world > 1:
@@ -131,16 +148,19 @@ def main():
         ms_per_step = elapsed * 1e3 / args.steps
         pairs = n * n
         value = pairs / (elapsed / args.steps)
-        # dominant kernel: FW phase 3 -- (nblk-1)^2 tiles x B^3 relaxations per launch
-        import re
-        B = int(re.search(r"B=(\d+)", plan.describe()).group(1))
-        nblk = (n + B - 1) // B
-        relax_per_launch = (nblk - 1) ** 2 * B ** 3
+        # dominant kernel: FW phase-3 "rest" launches; work = tiles x B^3 relaxations;
+        # its algorithmic HBM traffic = every tile read + written once (B^2 keys of
+        # 8 B each way per B^3 relaxations; the panels are L2/MALL-resident)
+        relax_per_launch = p3_work / max(p3_launches, 1)
+        B_TILE = 128
         avg_launch_s = (p3_ms / 1e3) / max(p3_launches, 1)
         achieved = relax_per_launch / avg_launch_s
+        traffic, traffic_src = measured_traffic(n)
         roofline = {"bound": "valu", "achieved": achieved / 1e12, "peak": RELAX_PEAK / 1e12, "unit": "Trelax/s",
-                    "frac": achieved / RELAX_PEAK, "traffic": None,
-                    "kernel": "minplus_tile_kernel<double, 0> (FW phase 3)", "avg_launch_ms": avg_launch_s * 1e3,
+                    "frac": achieved / RELAX_PEAK, "traffic": traffic, "traffic_unit": "HBM bytes per launch",
+                    "traffic_source": traffic_src,
+                    "algorithmic_hbm_bytes_per_launch": relax_per_launch / B_TILE * 2 * 8 if B_TILE else None,
+                    "kernel": "minplus_tile_kernel<double, 0> (FW phase 3, rest)", "avg_launch_ms": avg_launch_s * 1e3,
                     "relax_per_launch": relax_per_launch,
                     "peak_basis": f"{F64_LANE_OPS_PEAK / 1e12:.1f}e12 f64 VALU lane-ops/s / {OPS_PER_RELAX} ops "
                                   f"(v_add_f64 + v_min_f64) per relaxation"}

@@ -133,11 +133,13 @@ srt_status srt_plan_table(srt_plan *plan, uint64_t **d_latency_ns, float **d_pac
 const char *srt_plan_describe(const srt_plan *plan);
 /* hipStream_t of the plan (as void*) */
 void *srt_plan_stream(srt_plan *plan);
-/* Timing of the last run's dominant kernel family (phase-3 of FW or the SSSP
- * sweep): total ms and number of launches, measured with HIP events on the
- * plan's stream. */
+/* Timing of the last run's dominant kernel (FW phase-3 "rest" launches or the
+ * SSSP sweep): summed ms and number of launches, measured with HIP events on
+ * the plan's stream; dominant_work = relaxations those launches performed;
+ * total_ms = the whole build on the device. */
 srt_status srt_plan_kernel_stats(const srt_plan *plan, double *dominant_ms,
-                                 uint64_t *dominant_launches, double *total_ms);
+                                 uint64_t *dominant_launches, double *dominant_work,
+                                 double *total_ms);
 void srt_plan_destroy(srt_plan *plan);
 
 /* -------------------------------------------------------- multi-GPU (RCCL) */

@@ -289,8 +289,20 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         return hip_fail(err, e, "hipStreamCreate");
     }
     p->own_stream = true;
+    {
+        int lo = 0, hi = 0;
+        hipDeviceGetStreamPriorityRange(&lo, &hi);
+        e = hipStreamCreateWithPriority(&p->side_stream, hipStreamNonBlocking, hi);
+        if (e != hipSuccess) {
+            hipStreamDestroy(p->stream);
+            delete p;
+            return hip_fail(err, e, "hipStreamCreateWithPriority");
+        }
+    }
     hipEventCreate(&p->ev_begin);
     hipEventCreate(&p->ev_end);
+    hipEventCreateWithFlags(&p->ev_cross, hipEventDisableTiming);
+    hipEventCreateWithFlags(&p->ev_pivot, hipEventDisableTiming);
 
 #define PLAN_TRY(x)                \
     do {                           \
@@ -423,10 +435,11 @@ const char *srt_plan_describe(const srt_plan *p) { return p ? p->desc.c_str() : 
 void *srt_plan_stream(srt_plan *p) { return p ? (void *)p->stream : nullptr; }
 
 srt_status srt_plan_kernel_stats(const srt_plan *p, double *dominant_ms, uint64_t *launches,
-                                 double *total_ms) {
+                                 double *dominant_work, double *total_ms) {
     if (!p) return SRT_ERR_INVALID;
     if (dominant_ms) *dominant_ms = p->p3_ms;
     if (launches) *launches = p->p3_launches;
+    if (dominant_work) *dominant_work = p->p3_work;
     if (total_ms) *total_ms = p->total_ms;
     return SRT_OK;
 }
@@ -439,6 +452,12 @@ void srt_plan_destroy(srt_plan *p) {
     for (hipEvent_t e : p->ev) hipEventDestroy(e);
     if (p->ev_begin) hipEventDestroy(p->ev_begin);
     if (p->ev_end) hipEventDestroy(p->ev_end);
+    if (p->ev_cross) hipEventDestroy(p->ev_cross);
+    if (p->ev_pivot) hipEventDestroy(p->ev_pivot);
+    if (p->side_stream) {
+        hipStreamSynchronize(p->side_stream);
+        hipStreamDestroy(p->side_stream);
+    }
     if (p->own_stream && p->stream) hipStreamDestroy(p->stream);
     delete p;
 }

@@ -152,94 +152,123 @@ __global__ void scatter_edges_kernel(K *__restrict__ D, uint32_t Vp,
 }
 
 // ------------------------------------------------------------- phase 1
-// Close the 128x128 pivot block: 1024 threads; thread (c = tid % 128,
-// r0 = tid / 128) keeps P[r0 + 8i][c] (i < 16) in registers.  Step k only needs
-// row k and column k of P, published through two small double-buffered LDS
-// vectors by their owners: one barrier per step.
+// Close the 128x128 pivot block.  Same footprint as the tile kernel (256
+// threads, 8x8 keys per thread in registers) so that, under look-ahead, it can
+// take the slot of any retiring phase-3 workgroup.  Thread (tx, ty) holds rows
+// ty*8+i and cols tx*8+j.  Step k needs row k and column k; their owners
+// publish them (after their own step k-1 update) into double-buffered LDS
+// vectors: one barrier per step.  The k loop is unrolled by 8 so the owned
+// element index (k & 7) is static (a runtime index would send p to scratch).
 template <typename K>
-__global__ __launch_bounds__(1024) void fw_phase1_kernel(K *__restrict__ D, uint32_t Vp, uint32_t kb) {
+__global__ __launch_bounds__(NT3, 2) void fw_phase1_kernel(K *__restrict__ D, uint32_t Vp, uint32_t kb) {
     __shared__ K rowbuf[2][B];
     __shared__ K colbuf[2][B];
-    const int tid = threadIdx.x;
-    const int c = tid % B, r0 = tid / B;
+    const int tid = threadIdx.x, tx = tid % 16, ty = tid / 16;
     const uint64_t k0 = (uint64_t)kb * B;
-    K p[B / 8];
+    K p[TR][TC];
 #pragma unroll
-    for (int i = 0; i < B / 8; ++i) p[i] = D[(k0 + r0 + 8 * i) * Vp + k0 + c];
-    // publish step 0
-    if (r0 == 0) rowbuf[0][c] = p[0];
-    if (c == 0) {
+    for (int i = 0; i < TR; ++i) {
+        const K *src = D + (k0 + ty * TR + i) * Vp + k0 + tx * TC;
 #pragma unroll
-        for (int i = 0; i < B / 8; ++i) colbuf[0][r0 + 8 * i] = p[i];
+        for (int j = 0; j < TC; ++j) p[i][j] = src[j];
     }
-    __syncthreads();
-    for (int k = 0; k < B; ++k) {
-        const int cur = k & 1, nxt = cur ^ 1;
-        const K pkc = rowbuf[cur][c];
+    // owners of block index g = k >> 3 publish row/column k, e = k & 7 static
+    auto publish = [&](int g, int e, int buf) {
+        if (ty == g) {
 #pragma unroll
-        for (int i = 0; i < B / 8; ++i) p[i] = KeyOps<K>::kmin(p[i], colbuf[cur][r0 + 8 * i] + pkc);
-        // owners of row k+1 / column k+1 publish their (now final for step k) values
-        const int kn = k + 1;
-        if (kn < B) {
-            if (r0 == (kn & 7)) {
-#pragma unroll
-                for (int i = 0; i < B / 8; ++i)
-                    if (i == (kn >> 3)) rowbuf[nxt][c] = p[i];
-            }
-            if (c == kn) {
-#pragma unroll
-                for (int i = 0; i < B / 8; ++i) colbuf[nxt][r0 + 8 * i] = p[i];
-            }
+            for (int j = 0; j < TC; ++j) rowbuf[buf][tx * TC + j] = p[e][j];
         }
-        __syncthreads();
+        if (tx == g) {
+#pragma unroll
+            for (int i = 0; i < TR; ++i) colbuf[buf][ty * TR + i] = p[i][e];
+        }
+    };
+    publish(0, 0, 0);
+    __syncthreads();
+#pragma unroll 1
+    for (int g = 0; g < B / 8; ++g) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int cur = e & 1;  // k = 8g + e, parity of k == parity of e
+            K a[TR], b[TC];
+#pragma unroll
+            for (int i = 0; i < TR; ++i) a[i] = colbuf[cur][ty * TR + i];
+#pragma unroll
+            for (int j = 0; j < TC; ++j) b[j] = rowbuf[cur][tx * TC + j];
+#pragma unroll
+            for (int i = 0; i < TR; ++i) relax_row8<K>(p[i], a[i], b);
+            // publish step k+1 = 8g + e + 1
+            if (e < 7) publish(g, e + 1, cur ^ 1);
+            else if (g + 1 < B / 8) publish(g + 1, 0, cur ^ 1);
+            __syncthreads();
+        }
     }
 #pragma unroll
-    for (int i = 0; i < B / 8; ++i) D[(k0 + r0 + 8 * i) * Vp + k0 + c] = p[i];
+    for (int i = 0; i < TR; ++i) {
+        K *dst = D + (k0 + ty * TR + i) * Vp + k0 + tx * TC;
+#pragma unroll
+        for (int j = 0; j < TC; ++j) dst[j] = p[i][j];
+    }
 }
 
 // ------------------------------------------------------ phases 2 and 3
-// One 128x128 output tile C per workgroup: C <- min(C, A (x) Bm), A = 128 x 128
-// (rows of C, pivot columns), Bm = 128 x 128 (pivot rows, columns of C).
-// MODE 0 (phase 3): tiles (bi, bj), bi, bj != kb, XCD-grouped by rows.
-// MODE 1 (phase 2): tiles of the pivot row (A = P*) and pivot column (Bm = P*).
-// A or Bm may alias C in MODE 1: both are fully staged in LDS before C is
-// written, and every tile is owned by exactly one workgroup.
-template <typename K, int MODE>
+// Every min-plus update of a round is C(bi,bj) <- min(C, A(bi,kb) (x) Bm(kb,bj)):
+//   phase 2 row:  bi = kb  (A = P*, Bm aliases C);
+//   phase 2 col:  bj = kb  (Bm = P*, A aliases C);
+//   phase 3:      bi, bj != kb.
+// A launch covers up to two rectangles of tiles, each rows x cols where a
+// Span is [lo, hi) minus up to two skipped block indices.  Aliased operands
+// are fully staged in LDS before C is written and each tile has exactly one
+// owner workgroup, so phase-2 tiles are safe to update in place.  TAG only
+// gives each use its own kernel symbol (rocprof attribution).
+struct Span {
+    uint32_t lo, hi, s0, s1, n;  // s0 < s1, NONE = 0xffffffff
+};
+struct Rect {
+    Span r, c;
+};
+constexpr uint32_t NONE = 0xffffffffu;
+
+__host__ __device__ inline uint32_t span_at(const Span &s, uint32_t i) {
+    uint32_t v = s.lo + i;
+    if (v >= s.s0) ++v;
+    if (v >= s.s1) ++v;
+    return v;
+}
+
+inline Span make_span(uint32_t lo, uint32_t hi, uint32_t a = NONE, uint32_t b = NONE) {
+    uint32_t s0 = (a >= lo && a < hi) ? a : NONE, s1 = (b >= lo && b < hi) ? b : NONE;
+    if (s0 == s1) s1 = NONE;
+    if (s0 > s1) {
+        const uint32_t t = s0;
+        s0 = s1;
+        s1 = t;
+    }
+    const uint32_t n = (hi - lo) - (s0 != NONE) - (s1 != NONE);
+    return Span{lo, hi, s0, s1, n};
+}
+
+template <typename K, int TAG>
 __global__ __launch_bounds__(NT3, 2) void minplus_tile_kernel(K *__restrict__ D, uint32_t Vp,
-                                                           uint32_t kb, uint32_t nblk,
-                                                           uint32_t rb0, uint32_t rb1) {
+                                                           uint32_t kb, Rect r1, Rect r2) {
     __shared__ K As[2][B][KC + 1];  // As[buf][row][k]  (double-buffered)
     __shared__ K Bs[2][KC][B];      // Bs[buf][k][col]
-    // local block-rows [rb0, rb1) without the pivot row kb
-    const bool kb_local = kb >= rb0 && kb < rb1;
-    const uint32_t mr = (rb1 - rb0) - (kb_local ? 1u : 0u);
-    const uint32_t m = nblk - 1;
-    auto local_row = [&](uint32_t idx) {
-        uint32_t bi = rb0 + idx;
-        return (kb_local && bi >= kb) ? bi + 1 : bi;
-    };
-    uint32_t bi, bj;
-    if (MODE == 0) {
-        // phase 3.  XCD-aware bijective remap: blocks b and b+8 share an XCD
-        // (round-robin dispatch); each XCD gets a contiguous run of row-major
-        // tiles, so A-panel rows and many B-panel columns stay in its L2.
-        const uint32_t nwg = mr * m, orig = blockIdx.x;
-        const uint32_t q = nwg / 8, rr = nwg % 8, xcd = orig % 8;
-        const uint32_t t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
-        bi = local_row(t / m);
-        bj = t % m;
-        bj += bj >= kb;
-    } else {
-        uint32_t t = blockIdx.x;
-        const bool row_tile = (MODE == 1) || (MODE == 3 && t < m);
-        if (MODE == 3 && !row_tile) t -= m;
-        if (row_tile) {  // pivot block-row: C = R(bj), A = P*
-            bi = kb;
-            bj = t + (t >= kb);
-        } else {  // pivot block-column of a local row: C = Q(bi), Bm = P*
-            bi = local_row(t);
-            bj = kb;
+    const uint32_t n1 = r1.r.n * r1.c.n;
+    uint32_t t = blockIdx.x, bi, bj;
+    if (t < n1) {
+        if (gridDim.x == n1 && n1 >= 64) {
+            // XCD-aware bijective remap: blocks b and b+8 share an XCD (round-robin
+            // dispatch); each XCD gets a contiguous run of row-major tiles, so the
+            // A-panel rows and many B-panel columns stay in its 4 MB L2.
+            const uint32_t q = n1 / 8, rr = n1 % 8, xcd = t % 8;
+            t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + t / 8;
         }
+        bi = span_at(r1.r, t / r1.c.n);
+        bj = span_at(r1.c, t % r1.c.n);
+    } else {
+        t -= n1;
+        bi = span_at(r2.r, t / r2.c.n);
+        bj = span_at(r2.c, t % r2.c.n);
     }
     const uint64_t i0 = (uint64_t)bi * B, j0 = (uint64_t)bj * B, k0 = (uint64_t)kb * B;
     const int tid = threadIdx.x;
@@ -408,6 +437,22 @@ void fw_init_t(srt_plan *p) {
                        p->d_row_ptr, p->d_col, p->d_lat, p->d_loss, p->V, p->kp);
 }
 
+template <typename K, int TAG>
+void launch_tiles(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1, const Rect &r2) {
+    const uint32_t n = r1.r.n * r1.c.n + r2.r.n * r2.c.n;
+    if (!n) return;
+    hipLaunchKernelGGL((minplus_tile_kernel<K, TAG>), dim3(n), dim3(NT3), 0, s,
+                       reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2);
+}
+
+// Round schedule with one block of look-ahead, per rank (block-rows [rb0,rb1)):
+//   main stream M:  p2col(kb) | cross(kb) | rest(kb)
+//   side stream S:  (after cross(kb))  p1(kb+1), p2row(kb+1) on the owner of
+//                   kb+1, then the pivot-row broadcast of kb+1 (multi-GPU)
+// cross(kb) = the round-kb phase-3 tiles that round kb+1's pivot work needs
+// (column kb+1 of the local rows; row kb+1 on its owner), rest(kb) = all other
+// phase-3 tiles.  rest(kb) never touches block-row/column kb+1, so it runs
+// concurrently with S.  Single GPU = one rank, no broadcast.
 template <typename K>
 srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
     K *D = reinterpret_cast<K *>(p->d_D);
@@ -415,42 +460,65 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
     const uint32_t rb0 = p->rb0, rb1 = p->rb1;
     const bool sharded = p->comm != nullptr;  // a 1-rank comm runs the same schedule (tested)
     const uint32_t per_rank = sharded ? nblk / p->comm->nranks : nblk;
+    const size_t pivot_bytes = (size_t)B * p->Vp * sizeof(K);
+    hipStream_t M = p->stream, S = p->side_stream;
+    auto own = [&](uint32_t b) { return b >= rb0 && b < rb1; };
+    const Rect none{make_span(0, 0), make_span(0, 0)};
     p->p3_launches = 0;
-    const size_t need = 2 * (size_t)nblk;
+    p->p3_work = 0.0;
+    const size_t need = 2 * (size_t)nblk + 2;
     while (p->ev.size() < need) {
         hipEvent_t e;
-        hipEventCreate(&e);
+        hipEventCreateWithFlags(&e, 0);
         p->ev.push_back(e);
     }
+    srt_status st = SRT_OK;
+    // prologue: pivot 0
+    if (own(0)) {
+        hipLaunchKernelGGL(fw_phase1_kernel<K>, dim3(1), dim3(NT3), 0, M, D, p->Vp, 0u);
+        launch_tiles<K, 1>(p, M, 0, Rect{make_span(0, 1), make_span(0, nblk, 0)}, none);
+    }
+    if (sharded && (st = comm_bcast(p->comm, D, pivot_bytes, 0, M, err)) != SRT_OK) return st;
+    launch_tiles<K, 2>(p, M, 0, Rect{make_span(rb0, rb1, 0), make_span(0, 1)}, none);
+
     for (uint32_t kb = 0; kb < nblk; ++kb) {
-        const bool own = kb >= rb0 && kb < rb1;
-        const uint32_t mr = (rb1 - rb0) - (own ? 1u : 0u);
-        if (own) hipLaunchKernelGGL(fw_phase1_kernel<K>, dim3(1), dim3(1024), 0, p->stream, D, p->Vp, kb);
-        if (nblk == 1) break;
-        if (!sharded) {
-            hipLaunchKernelGGL((minplus_tile_kernel<K, 3>), dim3(2 * (nblk - 1)), dim3(NT3), 0, p->stream,
-                               D, p->Vp, kb, nblk, rb0, rb1);
-        } else {
-            if (own)
-                hipLaunchKernelGGL((minplus_tile_kernel<K, 1>), dim3(nblk - 1), dim3(NT3), 0, p->stream, D,
-                                   p->Vp, kb, nblk, rb0, rb1);
-            // the pivot block-row sits at the same offset on every rank
-            srt_status st = comm_bcast(p->comm, D + (uint64_t)kb * B * p->Vp,
-                                       (size_t)B * p->Vp * sizeof(K), (int)(kb / per_rank), p->stream, err);
-            if (st != SRT_OK) return st;
-            if (mr)
-                hipLaunchKernelGGL((minplus_tile_kernel<K, 2>), dim3(mr), dim3(NT3), 0, p->stream, D, p->Vp,
-                                   kb, nblk, rb0, rb1);
+        const bool nxt = kb + 1 < nblk;
+        const uint32_t k1 = kb + 1;
+        if (nxt) {
+            // cross(kb): column k1 of the local rows (+ row k1 on its owner)
+            Rect col{make_span(rb0, rb1, kb, k1), make_span(k1, k1 + 1)};
+            Rect row = own(k1) ? Rect{make_span(k1, k1 + 1), make_span(0, nblk, kb)} : none;
+            launch_tiles<K, 4>(p, M, kb, col, row);
+            hipEventRecord(p->ev_cross, M);
+            hipStreamWaitEvent(S, p->ev_cross, 0);
+            if (own(k1)) {
+                hipLaunchKernelGGL(fw_phase1_kernel<K>, dim3(1), dim3(NT3), 0, S, D, p->Vp, k1);
+                launch_tiles<K, 1>(p, S, k1, Rect{make_span(k1, k1 + 1), make_span(0, nblk, k1)}, none);
+            }
+            if (sharded &&
+                (st = comm_bcast(p->comm, D + (uint64_t)k1 * B * p->Vp, pivot_bytes, (int)(k1 / per_rank), S,
+                                 err)) != SRT_OK)
+                return st;
+            hipEventRecord(p->ev_pivot, S);
         }
-        if (mr == 0) continue;
-        hipEventRecord(p->ev[2 * p->p3_launches], p->stream);
-        hipLaunchKernelGGL((minplus_tile_kernel<K, 0>), dim3(mr * (nblk - 1)), dim3(NT3), 0, p->stream, D,
-                           p->Vp, kb, nblk, rb0, rb1);
-        hipEventRecord(p->ev[2 * p->p3_launches + 1], p->stream);
-        p->p3_launches++;
+        // rest(kb): local rows and all columns, minus kb and (look-ahead) k1
+        Rect rest{make_span(rb0, rb1, kb, nxt ? k1 : NONE), make_span(0, nblk, kb, nxt ? k1 : NONE)};
+        const uint32_t nt = rest.r.n * rest.c.n;
+        if (nt) {
+            hipEventRecord(p->ev[2 * p->p3_launches], M);
+            launch_tiles<K, 0>(p, M, kb, rest, none);
+            hipEventRecord(p->ev[2 * p->p3_launches + 1], M);
+            p->p3_launches++;
+            p->p3_work += (double)nt * B * B * B;
+        }
+        if (nxt) {
+            hipStreamWaitEvent(M, p->ev_pivot, 0);
+            // p2col(k1): column k1 of the local rows through P*(k1)
+            launch_tiles<K, 2>(p, M, k1, Rect{make_span(rb0, rb1, k1), make_span(k1, k1 + 1)}, none);
+        }
     }
     if (sharded)
-        return comm_allgather_inplace(p->comm, D, (size_t)per_rank * B * p->Vp * sizeof(K), p->stream, err);
+        return comm_allgather_inplace(p->comm, D, (size_t)per_rank * B * p->Vp * sizeof(K), M, err);
     return SRT_OK;
 }
 

@@ -89,9 +89,12 @@ struct srt_plan {
     std::vector<uint32_t> node_ids;
 
     // timing of the last run
-    std::vector<hipEvent_t> ev;  // pairs around each phase-3 launch
+    std::vector<hipEvent_t> ev;  // pairs around each phase-3 (rest) launch
     hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+    hipEvent_t ev_cross = nullptr, ev_pivot = nullptr;  // look-ahead hand-offs M <-> S
+    hipStream_t side_stream = nullptr;                  // high-priority pivot stream
     uint64_t p3_launches = 0;
+    double p3_work = 0.0;  // relaxations done by the timed launches
     double p3_ms = 0.0, total_ms = 0.0;
     bool ran = false;
 

@@ -62,10 +62,11 @@ class RoutingPlan:
         return _lib.lib().srt_plan_describe(self._h).decode()
 
     def kernel_stats(self):
-        """(dominant-kernel ms summed over launches, launches, total build ms) of the last run."""
-        a, b, c = C.c_double(), C.c_uint64(), C.c_double()
-        _lib.lib().srt_plan_kernel_stats(self._h, C.byref(a), C.byref(b), C.byref(c))
-        return a.value, b.value, c.value
+        """(dominant-kernel ms summed over its launches, launches, relaxations they
+        performed, whole-build device ms) of the last run."""
+        a, b, w, c = C.c_double(), C.c_uint64(), C.c_double(), C.c_double()
+        _lib.lib().srt_plan_kernel_stats(self._h, C.byref(a), C.byref(b), C.byref(w), C.byref(c))
+        return a.value, b.value, w.value, c.value
 
     def table_ptrs(self):
         lat, loss, n = C.c_void_p(), C.c_void_p(), C.c_uint32()
