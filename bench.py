@@ -1,12 +1,18 @@
 """Routing-table build benchmark (BASELINE.json metric: APSP pairs/sec +
 routing-table build wall-clock, 16k-node graph at 1/2/4/8 MI355X).
 
-One "step" = one full routing build of the 16,384-node complete undirected
-graph (config C3: latency U{1..300} ms, loss U[0,0.01], self-loops, seed 3):
-from the CSR resident in HBM to the n x n (latency, loss) table resident in
-HBM (all-gathered on every rank for N > 1).  value = n^2 pairs / step time.
+Default workload (--config c3): one "step" = one full routing build of the
+16,384-node complete undirected graph (config C3: latency U{1..300} ms, loss
+U[0,0.01], self-loops, seed 3), from the CSR resident in HBM to the n x n
+(latency, loss) table resident in HBM (all-gathered on every rank for N > 1).
+value = n^2 pairs / step time.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--nodes 16384]
+Other configs (not the headline line, same JSON shape):
+  --config c2   4,096-node complete graph (blocked Floyd-Warshall, 1 GPU)
+  --config c4   100,000-node Barabasi-Albert graph, m=4 (batched sparse sweep)
+  --config c5   1M packets/round send_packet decision on the C1 table (packets/s)
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3]
 Multi-GPU: launched by torch.distributed.run, one rank per GPU (RCCL).
 Prints one JSON line on rank 0.
 """
@@ -23,16 +29,22 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# MI355X constants (/opt/skills/guides/MI355X_MICROARCH.md): 256 CUs x 4 SIMD-32,
-# one wave64 VALU op per 2 cycles per SIMD -> 128 int32 lane-ops/clk/CU at 2.4 GHz.
-VALU_LANE_OPS_PEAK = 256 * 128 * 2.4e9  # 78.6e12 int32 lane-ops/s
-# FP64 VALU ops (v_add_f64, v_min_f64) issue at half that rate (spec: FP64 vector
-# 78.6 TF vs FP32 157.3 TF; tools/valu_bench measured 36.5e12 lane-ops/s).  One
-# lexicographic (latency, loss) relaxation on the f64-encoded path key is one
-# v_add_f64 + one v_min_f64.
-F64_LANE_OPS_PEAK = VALU_LANE_OPS_PEAK / 2  # 39.3e12
+# MI355X constants (/opt/skills/guides/MI355X_MICROARCH.md): FP64 vector peak
+# 78.6 TFLOP/s counts an FMA as 2 -> 39.3e12 f64 lane-ops/s (v_add_f64 and
+# v_min_f64 each one op; tools/valu_bench measured 36.5e12).  One lexicographic
+# (latency, loss) relaxation on the f64-encoded path key is one v_add_f64 + one
+# v_min_f64.
+F64_LANE_OPS_PEAK = 256 * 64 * 2.4e9  # 39.3e12
 OPS_PER_RELAX = 2
 RELAX_PEAK = F64_LANE_OPS_PEAK / OPS_PER_RELAX  # 19.66e12 relaxations/s
+HBM_PEAK = 8.0e12  # B/s
+
+CONFIGS = {
+    "c2": dict(kind="complete", nodes=4096, seed=2),
+    "c3": dict(kind="complete", nodes=16384, seed=3),
+    "c4": dict(kind="ba", nodes=100_000, seed=4, m=4),
+    "c5": dict(kind="packets", nodes=1000, seed=5, hosts=10_000, packets=1_000_000),
+}
 
 
 def parse_args():
@@ -40,8 +52,11 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--nodes", type=int, default=16384)
-    ap.add_argument("--seed", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--nodes", type=int, default=0, help="override the config's node count")
+    ap.add_argument("--in-use", dest="in_use", type=int, default=0,
+                    help="c4: number of in-use nodes (default: all)")
+    ap.add_argument("--seed", type=int, default=-1)
     ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -49,40 +64,39 @@ def parse_args():
     return ap.parse_args()
 
 
-def cpu_baseline(n, seed, threads, sources):
+def cpu_baseline(og, nodes, threads, sources, label, target_s=15.0):
     """The oracle's faithful restatement of compute_shortest_paths (hash-map
-    Dijkstra per source + rayon-style pool), timed on a bounded sample of
-    sources of the same graph; pairs/s extrapolated linearly (sources are
-    independent, mod.rs:190-208)."""
+    Dijkstra per source, the `nodes.contains` filter, per-source map, merged
+    map; rayon-style pool), timed on a bounded sample of sources of the same
+    graph; pairs/s extrapolated linearly (sources are independent,
+    mod.rs:190-208)."""
     from oracle import oracle as O
-    from shadow_amd import synth
 
-    src, dst, lat, loss = synth.complete_graph(n, seed)
-    g = O.Graph(False, np.arange(n), src, dst, lat, loss)
-    nodes = np.arange(n, dtype=np.uint32)
+    n = len(nodes)
     if sources <= 0:
-        # calibrate: one source per thread, then scale to ~15 s
+        # calibrate: one source per thread, then scale to ~target_s
         t0 = time.perf_counter()
-        O.compute_shortest_paths(g, nodes, threads=threads, mode=0, src_count=threads)
+        O.compute_shortest_paths(og, nodes, threads=threads, mode=0, src_count=threads)
         dt = time.perf_counter() - t0
-        sources = int(max(threads, min(n, threads * max(1, int(15.0 / max(dt, 1e-3))))))
+        sources = int(max(threads, min(n, threads * max(1, int(target_s / max(dt, 1e-3))))))
     t0 = time.perf_counter()
-    O.compute_shortest_paths(g, nodes, threads=threads, mode=0, src_count=sources)
+    O.compute_shortest_paths(og, nodes, threads=threads, mode=0, src_count=sources)
     dt = time.perf_counter() - t0
     return {"value": sources * n / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"{sources} of {n} sources of the same C3 graph, faithful hash-map Dijkstra "
+            "sample": f"{sources} of {n} sources of the same {label} graph, faithful hash-map Dijkstra "
                       f"(oracle mode 0), {dt:.1f} s wall, extrapolated linearly to pairs/s"}
 
 
-def measured_traffic(n, kernel_tag="phase 3 rest"):
+def measured_traffic(tag, kernel_tag):
     """HBM bytes per launch of the dominant kernel from the latest committed
-    PMC summary (profiles/rNN_pmc_traffic.json, FETCH_SIZE + WRITE_SIZE passes
-    of rocprofv3 on this same config), or None."""
+    PMC summary (profiles/rNN_pmc_traffic.json: FETCH_SIZE and WRITE_SIZE
+    passes of rocprofv3 on this same workload, gfx950 corrections applied), or
+    None."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
     for f in reversed(files):
         d = json.load(open(f))
-        if str(n) not in d.get("config", ""):
+        if tag not in d.get("config", ""):
             continue
         for k, v in d.get("kernels", {}).items():
             if kernel_tag in k:
@@ -90,100 +104,235 @@ def measured_traffic(n, kernel_tag="phase 3 rest"):
     return None, None
 
 
-def main():
-    args = parse_args()
-    import torch
-    import torch.distributed as dist
+class Dist:
+    def __init__(self, gpus):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.n_gpus = max(gpus, self.world)
+        if self.world > 1:
+            torch.cuda.set_device(self.local_rank)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local_rank))
+        self.dev = self.local_rank
 
-    from shadow_amd import NetworkGraph, synth
-    from shadow_amd.plan import RoutingPlan
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+        self.torch.cuda.synchronize(self.dev)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    n_gpus = max(args.gpus, world)
-    if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = local_rank
+    def max_over_ranks(self, x):
+        if self.world == 1:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=f"cuda:{self.dev}")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
 
-    n = args.nodes
-    row_ptr, col, lat, loss = synth.complete_csr(n, args.seed)
-    g = NetworkGraph(n, np.arange(n, dtype=np.uint32), row_ptr, col, lat, loss, directed=False)
-    nodes = np.arange(n, dtype=np.uint32)
-    plan = RoutingPlan(g, nodes, device=dev)
-    del row_ptr, col, lat, loss, g
-    if world > 1:
-        from shadow_amd import dist as sdist
-        sdist.bind(plan, rank, world, local_rank, transport=os.environ.get("SRT_COMM", "rccl"))
+    def close(self):
+        if self.world > 1:
+            self.dist.destroy_process_group()
 
-    def barrier():
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
 
-    for _ in range(args.warmup):
+def timed_builds(plan, D, steps, warmup):
+    for _ in range(warmup):
         plan.run()
-    barrier()
+    D.barrier()
     step_ms = []
-    p3_ms, p3_launches, p3_work = 0.0, 0, 0.0
+    k_ms, k_launches, k_work = 0.0, 0, 0.0
     t_all0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         t0 = time.perf_counter()
         plan.run()
         step_ms.append((time.perf_counter() - t0) * 1e3)
         a, b, w, _ = plan.kernel_stats()
-        p3_ms += a
-        p3_launches += b
-        p3_work += w
-    barrier()
-    elapsed = time.perf_counter() - t_all0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    plan.fetch(table=False)  # connectivity check + min latency (not timed)
+        k_ms += a
+        k_launches += b
+        k_work += w
+    D.barrier()
+    elapsed = D.max_over_ranks(time.perf_counter() - t_all0)
+    return elapsed, step_ms, k_ms, k_launches, k_work
 
-    if rank == 0:
-        ms_per_step = elapsed * 1e3 / args.steps
+
+def bench_graph(args, cfg, D):
+    from shadow_amd import NetworkGraph, synth
+    from shadow_amd.plan import RoutingPlan
+
+    n_nodes = args.nodes or cfg["nodes"]
+    seed = cfg["seed"] if args.seed < 0 else args.seed
+    if cfg["kind"] == "complete":
+        row_ptr, col, lat, loss = synth.complete_csr(n_nodes, seed)
+        g = NetworkGraph(n_nodes, np.arange(n_nodes, dtype=np.uint32), row_ptr, col, lat, loss, directed=False)
+        nodes = np.arange(n_nodes, dtype=np.uint32)
+        label = f"{args.config.upper()}: {n_nodes}-node complete undirected GML graph"
+        data = "synthetic (seeded complete graph, latency U{1..300} ms, loss U[0,0.01])"
+        og_args = None
+        del row_ptr, col, lat, loss
+    else:
+        src, dst, lat, loss = synth.barabasi_albert(n_nodes, cfg["m"], seed)
+        g = NetworkGraph.from_edges(n_nodes, src, dst, lat, loss, directed=False)
+        n = args.in_use or n_nodes
+        nodes = (np.arange(n_nodes, dtype=np.uint32) if n == n_nodes else
+                 np.sort(np.random.default_rng(seed).choice(n_nodes, n, replace=False)).astype(np.uint32))
+        label = (f"{args.config.upper()}: {n_nodes}-node Barabasi-Albert graph (m={cfg['m']}, avg degree "
+                 f"{2 * len(src) / n_nodes:.1f} incl. self-loops), {len(nodes)} in use")
+        data = "synthetic (seeded BA graph, latency U{1..300} ms, loss U[0,0.01])"
+        og_args = (src, dst, lat, loss)
+    plan = RoutingPlan(g, nodes, device=D.dev)
+    if D.world > 1:
+        from shadow_amd import dist as sdist
+        sdist.bind(plan, D.rank, D.world, D.local_rank, transport=os.environ.get("SRT_COMM", "rccl"))
+    desc = plan.describe()
+    elapsed, step_ms, k_ms, k_launches, k_work = timed_builds(plan, D, args.steps, args.warmup)
+    plan.fetch(table=False)  # connectivity check + min latency (not timed)
+    n = len(nodes)
+    out = None
+    if D.rank == 0:
         pairs = n * n
-        value = pairs / (elapsed / args.steps)
-        # dominant kernel: FW phase-3 "rest" launches; work = tiles x B^3 relaxations;
-        # its algorithmic HBM traffic = every tile read + written once (B^2 keys of
-        # 8 B each way per B^3 relaxations; the panels are L2/MALL-resident)
-        relax_per_launch = p3_work / max(p3_launches, 1)
-        B_TILE = 128
-        avg_launch_s = (p3_ms / 1e3) / max(p3_launches, 1)
-        achieved = relax_per_launch / avg_launch_s
-        traffic, traffic_src = measured_traffic(n)
-        roofline = {"bound": "valu", "achieved": achieved / 1e12, "peak": RELAX_PEAK / 1e12, "unit": "Trelax/s",
-                    "frac": achieved / RELAX_PEAK, "traffic": traffic, "traffic_unit": "HBM bytes per launch",
-                    "traffic_source": traffic_src,
-                    "algorithmic_hbm_bytes_per_launch": relax_per_launch / B_TILE * 2 * 8 if B_TILE else None,
-                    "kernel": "minplus_tile_kernel<double, 0> (FW phase 3, rest)", "avg_launch_ms": avg_launch_s * 1e3,
-                    "relax_per_launch": relax_per_launch,
-                    "peak_basis": f"{F64_LANE_OPS_PEAK / 1e12:.1f}e12 f64 VALU lane-ops/s / {OPS_PER_RELAX} ops "
-                                  f"(v_add_f64 + v_min_f64) per relaxation"}
+        ms_per_step = elapsed * 1e3 / args.steps
+        avg_launch_s = (k_ms / 1e3) / max(k_launches, 1)
+        work_per_launch = k_work / max(k_launches, 1)
+        if desc.startswith("fw"):
+            B_TILE = 128
+            achieved = work_per_launch / avg_launch_s
+            traffic, traffic_src = measured_traffic(str(n), "phase 3 rest")
+            roofline = {
+                "bound": "valu", "achieved": achieved / 1e12, "peak": RELAX_PEAK / 1e12, "unit": "Trelax/s",
+                "frac": achieved / RELAX_PEAK, "traffic": traffic, "traffic_unit": "HBM bytes per launch",
+                "traffic_source": traffic_src,
+                "algorithmic_hbm_bytes_per_launch": work_per_launch / B_TILE * 2 * 8,
+                "kernel": "minplus_tile_kernel<double, 0> (FW phase 3, rest)", "avg_launch_ms": avg_launch_s * 1e3,
+                "relax_per_launch": work_per_launch,
+                "peak_basis": f"{F64_LANE_OPS_PEAK / 1e12:.1f}e12 f64 VALU lane-ops/s / {OPS_PER_RELAX} ops "
+                              f"(v_add_f64 + v_min_f64) per relaxation; the SURVEY's INT-VALU basis (5 int32 ops "
+                              f"per u64 relaxation) would be 7.86 Trelax/s"}
+            algo = "blocked Floyd-Warshall"
+        else:
+            achieved = work_per_launch / avg_launch_s
+            traffic, traffic_src = measured_traffic(str(n), "sssp_sweep")
+            roofline = {
+                "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK, "traffic": traffic, "traffic_source": traffic_src,
+                "kernel": "sssp_sweep_kernel (all sweeps of one 64-source batch group)",
+                "avg_group_ms": avg_launch_s * 1e3, "groups_per_step": k_launches // max(args.steps, 1),
+                "algorithmic_bytes_per_group": work_per_launch,
+                "basis": "12 B x (E_in + V) per source (SURVEY.md 8(d)), E_in = in-edges without self-loops"}
+            algo = "batched sparse sweep"
         cpu = None
-        if args.cpu_baseline and world == 1:
-            cpu = cpu_baseline(n, args.seed, args.cpu_threads, args.cpu_sources)
+        if args.cpu_baseline and D.world == 1:
+            from oracle import oracle as O
+            if og_args is None:
+                og = O.Graph(False, np.arange(n_nodes), *synth.complete_graph(n_nodes, seed))
+            else:
+                og = O.Graph(False, np.arange(n_nodes), *og_args)
+            cpu = cpu_baseline(og, nodes, args.cpu_threads, args.cpu_sources, args.config.upper())
         out = {
-            "metric": "APSP pairs/sec (routing-table build, 16k-node graph)",
-            "value": value, "unit": "pairs/s", "n_gpus": n_gpus, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
-            "dtype": "f64" if "f64key" in plan.describe() else "u64", "data": "synthetic (seeded complete graph, latency U{1..300} ms, loss U[0,0.01])",
-            "config": {"workload": f"C3: {n}-node complete undirected GML graph, use_shortest_path=true, "
-                                   f"blocked Floyd-Warshall", "nodes": n, "pairs": pairs,
-                       "parallelism": f"rows{n_gpus}" if n_gpus > 1 else "single",
-                       "plan": plan.describe(), "step_ms": [round(x, 3) for x in step_ms],
-                       "build_wallclock_ms": ms_per_step},
+            "metric": f"APSP pairs/sec (routing-table build, {n_nodes // 1000 if n_nodes >= 1000 else n_nodes}"
+                      f"{'k' if n_nodes >= 1000 else ''}-node graph)",
+            "value": pairs / (elapsed / args.steps), "unit": "pairs/s", "n_gpus": D.n_gpus, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f64" if "f64key" in desc else ("u64" if desc.startswith("fw") else "u64"),
+            "data": data,
+            "config": {"workload": f"{label}, use_shortest_path=true, {algo}", "nodes": n_nodes, "in_use": n,
+                       "pairs": pairs, "parallelism": f"rows{D.n_gpus}" if D.n_gpus > 1 else "single",
+                       "plan": desc, "step_ms": [round(x, 3) for x in step_ms], "build_wallclock_ms": ms_per_step},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
-        print(json.dumps(out), flush=True)
     plan.close()
-    if world > 1:
-        dist.destroy_process_group()
+    return out
+
+
+def bench_packets(args, cfg, D):
+    """C5: one round = srt_packet_batch over 1M packets (10k hosts on the C1
+    nodes, loss U[0,0.25]), inputs resident in HBM; value = packets/s.
+    Replicas only: each rank runs its own round (per-host RNG streams shard by
+    source host, no exchange)."""
+    import torch
+
+    from oracle import oracle as O
+    from shadow_amd import NetworkGraph, synth
+    from shadow_amd.plan import RoutingPlan
+
+    n_nodes, hosts, n_pkts = cfg["nodes"], cfg["hosts"], cfg["packets"]
+    seed = cfg["seed"] if args.seed < 0 else args.seed
+    src, dst, lat, loss = synth.complete_graph(n_nodes, seed, loss_max=0.25)
+    g = NetworkGraph.from_edges(n_nodes, src, dst, lat, loss)
+    plan = RoutingPlan(g, np.arange(n_nodes, dtype=np.uint32), device=D.dev).run()
+    r0, r1 = 1_000_000_000, 1_000_000_000 + 5 * synth.MS
+    pk, host_ptr, _ = synth.packet_round(hosts, n_nodes, n_pkts, seed, r0, r1)
+    rng0 = synth.host_rng_states(hosts, general_seed=1)
+    dev = torch.device("cuda", D.dev)
+    t_pk = torch.from_numpy(pk.view(np.uint8).copy()).to(dev)
+    t_hp = torch.from_numpy(host_ptr.view(np.int32).copy()).to(dev)
+    t_rng = torch.from_numpy(rng0.view(np.int64).copy()).to(dev)
+    t_f = torch.zeros(n_pkts, dtype=torch.int32, device=dev)
+    t_d = torch.zeros(n_pkts, dtype=torch.int64, device=dev)
+    t_c = torch.zeros(n_nodes * n_nodes, dtype=torch.int64, device=dev)
+    t_s = torch.full((2,), -1, dtype=torch.int64, device=dev)
+    stream = torch.cuda.ExternalStream(plan.stream_ptr(), device=dev)
+
+    def one():
+        plan.packet_batch(t_pk, t_hp, t_rng, r1, 0, 2**62, t_f, t_d, t_c, t_s, sync=False)
+
+    for _ in range(args.warmup):
+        one()
+    plan.sync()
+    D.barrier()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        one()
+    ev1.record(stream)
+    plan.sync()
+    D.barrier()
+    elapsed = D.max_over_ranks(time.perf_counter() - t0)
+    dev_ms = ev0.elapsed_time(ev1) / args.steps
+    out = None
+    if D.rank == 0:
+        per_round = elapsed / args.steps
+        bytes_per_round = n_pkts * 52 + hosts * 64
+        cpu = None
+        if args.cpu_baseline and D.world == 1:
+            table = plan.fetch()
+            rng = rng0.copy()
+            t0 = time.perf_counter()
+            reps = 0
+            while time.perf_counter() - t0 < 10.0:
+                O.packet_batch(table.latency_ns, table.packet_loss, pk.view(O.PKT_DTYPE), rng, r1, 0, 2**62)
+                reps += 1
+            dt = time.perf_counter() - t0
+            cpu = {"value": reps * n_pkts / dt, "unit": "packets/s", "cores": 1, "kind": "port",
+                   "sample": f"{reps} rounds of the same 1M-packet batch through the oracle's sequential "
+                             f"send_packet restatement (one thread), {dt:.1f} s"}
+        out = {
+            "metric": "batched send_packet decisions/sec (1M packets/round)", "value": D.world * n_pkts / per_round,
+            "unit": "packets/s", "n_gpus": D.n_gpus, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": per_round * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u64", "data": "synthetic (seeded packet round, 10k hosts on the C1 nodes, loss U[0,0.25])",
+            "config": {"workload": "C5: 1M packets/round, latency lookup + per-host xoshiro256++ loss drops",
+                       "packets": n_pkts, "hosts": hosts, "parallelism": "replicas"},
+            "roofline": {"bound": "hbm", "achieved": bytes_per_round / (dev_ms / 1e3) / 1e9,
+                         "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                         "frac": bytes_per_round / (dev_ms / 1e3) / HBM_PEAK, "traffic": None,
+                         "kernel": "draw_kernel + decide_kernel (one round)", "device_ms_per_round": dev_ms,
+                         "basis": "52 B/packet + 64 B/host (SURVEY.md 8(d))"},
+            "cpu_baseline": cpu,
+        }
+    plan.close()
+    return out
+
+
+def main():
+    args = parse_args()
+    cfg = CONFIGS[args.config]
+    D = Dist(args.gpus)
+    out = bench_packets(args, cfg, D) if cfg["kind"] == "packets" else bench_graph(args, cfg, D)
+    if out is not None:
+        print(json.dumps(out), flush=True)
+    D.close()
 
 
 if __name__ == "__main__":

@@ -200,6 +200,61 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_stats);
     hipFree(p->d_pack);
     hipFree(p->d_draws);
+    hipFree(p->d_in_ptr);
+    hipFree(p->d_in_edge);
+    hipFree(p->d_sD);
+    hipFree(p->d_smask);
+    hipFree(p->d_sflag);
+    hipFree(p->d_rstats);
+    if (p->h_sflag) hipHostFree(p->h_sflag);
+}
+
+// Sparse SSSP key (srt_sssp.hip): latency in units of g in the high 32 bits.
+// A stored value is a simple path (<= V-1 edges) and a candidate adds one
+// edge, so V * max_edge_latency / g < 2^32 - 1 keeps every sum exact and
+// below the all-ones "unreached" key.
+bool sssp_params(const srt_csr *g, uint64_t *g_out, uint64_t *n_in, std::string *why) {
+    uint64_t gcd = 0, maxlat = 0, selfloops = 0;
+    for (uint32_t u = 0; u < g->n_nodes; ++u)
+        for (uint64_t k = g->row_ptr[u]; k < g->row_ptr[u + 1]; ++k) {
+            gcd = std::gcd(gcd, g->lat_ns[k]);
+            maxlat = std::max(maxlat, g->lat_ns[k]);
+            selfloops += g->col[k] == u;
+        }
+    if (gcd == 0) gcd = 1;
+    *g_out = gcd;
+    *n_in = g->n_adj - selfloops;
+    if ((unsigned __int128)g->n_nodes * (maxlat / gcd) >= 0xffffffffull) {
+        *why = "V * max edge latency exceeds the 32-bit latency field of the SSSP key";
+        return false;
+    }
+    return true;
+}
+
+// Pull-form adjacency for the sweep: for every v, the entries u -> v of every
+// row u (petgraph edges(u): directed outgoing / undirected incident), minus
+// self-loops (they never shorten a path; the diagonal is the raw self-loop).
+void build_in_edges(const srt_csr *g, uint64_t gunit, uint64_t n_in, std::vector<uint64_t> *ptr,
+                    std::vector<srt::InEdge> *edges) {
+    const uint32_t V = g->n_nodes;
+    ptr->assign((size_t)V + 1, 0);
+    for (uint32_t u = 0; u < V; ++u)
+        for (uint64_t k = g->row_ptr[u]; k < g->row_ptr[u + 1]; ++k)
+            if (g->col[k] != u) (*ptr)[g->col[k] + 1]++;
+    for (uint32_t v = 0; v < V; ++v) (*ptr)[v + 1] += (*ptr)[v];
+    edges->resize(std::max<uint64_t>(n_in, 1));
+    std::vector<uint64_t> fill(ptr->begin(), ptr->end() - 1);
+    for (uint32_t u = 0; u < V; ++u)
+        for (uint64_t k = g->row_ptr[u]; k < g->row_ptr[u + 1]; ++k) {
+            const uint32_t v = g->col[k];
+            if (v == u) continue;
+            srt::InEdge e;
+            e.u = u;
+            e.w = (uint32_t)(g->lat_ns[k] / gunit);
+            e.eb = 1.0f - g->loss[k];
+            e.pad = 0;
+            (*edges)[fill[v]++] = e;
+        }
 }
 
 }  // namespace
@@ -260,16 +315,55 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     for (uint32_t i = 0; i < n && p->identity_nodes; ++i) p->identity_nodes = nodes[i] == i;
     if (g->node_ids) p->node_ids.assign(g->node_ids, g->node_ids + g->n_nodes);
 
-    std::string why;
-    if (!choose_key_params(g, &p->kp, &p->key_f64, &why)) {
+    // Kernel family.  Dense closure (FW) costs Vp^3 relaxations at ~1.2e13/s;
+    // the batched sparse sweep costs ~n * (E_in + V) row gathers of 8 B with a
+    // few re-activations per row, priced at ~64 B per (source, in-edge) at
+    // ~3e12 B/s.  AUTO takes the cheaper representable one.
+    std::string why_fw, why_sssp;
+    const bool fw_ok = choose_key_params(g, &p->kp, &p->key_f64, &why_fw);
+    uint64_t n_in = 0;
+    const bool sssp_ok = sssp_params(g, &p->sssp_g, &n_in, &why_sssp);
+    const uint32_t want = opts ? opts->algo : (uint32_t)SRT_ALGO_AUTO;
+    int algo = -1;
+    if (want == SRT_ALGO_FW) {
+        if (fw_ok) algo = SRT_ALGO_FW;
+    } else if (want == SRT_ALGO_SSSP) {
+        if (sssp_ok) algo = SRT_ALGO_SSSP;
+    } else if (want == SRT_ALGO_AUTO) {
+        const double t_fw = fw_ok ? (double)p->Vp * p->Vp * p->Vp / 1.2e13 : 1e300;
+        const double t_sssp = sssp_ok ? (double)n * ((double)n_in + p->V) * 64.0 / 3e12 : 1e300;
+        if (fw_ok || sssp_ok) algo = t_sssp < t_fw ? SRT_ALGO_SSSP : SRT_ALGO_FW;
+    } else {
         delete p;
-        set_err(err, SRT_ERR_UNSUPPORTED, ("packed key unavailable: " + why).c_str());
+        set_err(err, SRT_ERR_INVALID, "unknown srt_opts.algo");
+        return SRT_ERR_INVALID;
+    }
+    if (algo < 0) {
+        delete p;
+        const std::string why = want == SRT_ALGO_SSSP ? why_sssp : want == SRT_ALGO_FW ? why_fw : why_fw + "; " + why_sssp;
+        set_err(err, SRT_ERR_UNSUPPORTED, ("no exact path key for this graph: " + why).c_str());
         return SRT_ERR_UNSUPPORTED;
     }
-    p->algo = SRT_ALGO_FW;
-    char d[160];
-    std::snprintf(d, sizeof d, "fw:%s B=%d g=%llu qb=%u s=%d V=%u n=%u", p->key_f64 ? "f64key" : "u64key",
-                  srt::FW_B, (unsigned long long)p->kp.g, p->kp.qb, p->kp.s, p->V, n);
+    p->algo = algo;
+    p->row0 = 0;
+    p->row1 = n;
+    p->rows_alloc = n;
+    char d[200];
+    if (algo == SRT_ALGO_FW) {
+        std::snprintf(d, sizeof d, "fw:%s B=%d g=%llu qb=%u s=%d V=%u n=%u", p->key_f64 ? "f64key" : "u64key",
+                      srt::FW_B, (unsigned long long)p->kp.g, p->kp.qb, p->kp.s, p->V, n);
+    } else {
+        // batches of 64 sources in flight: ~192 MB of path state (Infinity
+        // Cache sized), never more batches than the rows need
+        const uint64_t per_batch = (uint64_t)p->V * 64 * 8;
+        uint64_t nb = std::max<uint64_t>(1, (192ull << 20) / std::max<uint64_t>(per_batch, 1));
+        nb = std::min<uint64_t>(nb, std::max<uint32_t>(1, (n + 63) / 64));
+        nb = std::min<uint64_t>(nb, 1024);
+        p->sssp_nb = (uint32_t)nb;
+        p->n_in_edges = n_in;
+        std::snprintf(d, sizeof d, "sssp:lat32|f32 g=%llu V=%u n=%u E_in=%llu nb=%u",
+                      (unsigned long long)p->sssp_g, p->V, n, (unsigned long long)n_in, p->sssp_nb);
+    }
     p->desc = d;
 
     int dev = opts && opts->device >= 0 ? opts->device : -1;
@@ -317,12 +411,33 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     PLAN_TRY(dmalloc(&p->d_lat, g->n_adj, err));
     PLAN_TRY(dmalloc(&p->d_loss, g->n_adj, err));
     PLAN_TRY(dmalloc(&p->d_nodes, n, err));
-    PLAN_TRY(dmalloc(&p->d_D, (size_t)p->Vp * p->Vp, err));
+    if (algo == SRT_ALGO_FW) PLAN_TRY(dmalloc(&p->d_D, (size_t)p->Vp * p->Vp, err));
     PLAN_TRY(dmalloc(&p->d_out_lat, (size_t)n * n, err));
     PLAN_TRY(dmalloc(&p->d_out_loss, (size_t)n * n, err));
     PLAN_TRY(dmalloc(&p->d_sl_lat, n, err));
     PLAN_TRY(dmalloc(&p->d_sl_loss, n, err));
     PLAN_TRY(dmalloc(&p->d_stats, 2, err));
+    PLAN_TRY(dmalloc(&p->d_rstats, 2, err));
+    if (algo == SRT_ALGO_SSSP) {
+        std::vector<uint64_t> in_ptr;
+        std::vector<srt::InEdge> in_edge;
+        build_in_edges(g, p->sssp_g, n_in, &in_ptr, &in_edge);
+        PLAN_TRY(dmalloc(&p->d_in_ptr, in_ptr.size(), err));
+        PLAN_TRY(dmalloc(&p->d_in_edge, in_edge.size(), err));
+        PLAN_TRY(dmalloc(&p->d_sD, (size_t)p->sssp_nb * p->V * 64, err));
+        PLAN_TRY(dmalloc(&p->d_smask, (size_t)2 * p->sssp_nb * p->V, err));
+        PLAN_TRY(dmalloc(&p->d_sflag, (size_t)3 * p->sssp_nb, err));
+        if ((e = hipHostMalloc((void **)&p->h_sflag, (size_t)p->sssp_nb * sizeof(uint32_t), 0)) != hipSuccess) {
+            srt_plan_destroy(p);
+            return hip_fail(err, e, "hipHostMalloc");
+        }
+        if ((e = hipMemcpy(p->d_in_ptr, in_ptr.data(), in_ptr.size() * 8, hipMemcpyHostToDevice)) != hipSuccess ||
+            (e = hipMemcpy(p->d_in_edge, in_edge.data(), in_edge.size() * sizeof(srt::InEdge),
+                           hipMemcpyHostToDevice)) != hipSuccess) {
+            srt_plan_destroy(p);
+            return hip_fail(err, e, "upload in-edges");
+        }
+    }
 #undef PLAN_TRY
     auto up = [&](void *dst, const void *src, size_t bytes) -> hipError_t {
         if (!bytes) return hipSuccess;
@@ -351,10 +466,27 @@ srt_status srt_plan_run_async(srt_plan *p, srt_err *err) {
     }
     HIP_TRY(hipSetDevice(p->device), "hipSetDevice");
     hipEventRecord(p->ev_begin, p->stream);
-    srt::fw_init(p);
-    srt_status st = srt::fw_rounds(p, err);
-    if (st != SRT_OK) return st;
-    srt::fw_extract(p);
+    srt_status st;
+    if (p->algo == SRT_ALGO_SSSP) {
+        // rows [row0, row1) of this rank; every rank then holds the whole
+        // table after the row all-gather, and the stats of all ranks
+        const int rank = p->comm ? p->comm->rank : 0, nranks = p->comm ? p->comm->nranks : 1;
+        st = srt::sssp_run(p, p->d_rstats + 2 * rank, err);
+        if (st != SRT_OK) return st;
+        if (p->comm) {
+            const size_t per = (size_t)p->rows_alloc / nranks * p->n;
+            if ((st = srt::comm_allgather_inplace(p->comm, p->d_out_lat, per * 8, p->stream, err)) != SRT_OK ||
+                (st = srt::comm_allgather_inplace(p->comm, p->d_out_loss, per * 4, p->stream, err)) != SRT_OK ||
+                (st = srt::comm_allgather_inplace(p->comm, p->d_rstats, 16, p->stream, err)) != SRT_OK)
+                return st;
+        }
+        srt::reduce_rank_stats(p, nranks);
+    } else {
+        srt::fw_init(p);
+        st = srt::fw_rounds(p, err);
+        if (st != SRT_OK) return st;
+        srt::fw_extract(p);
+    }
     hipEventRecord(p->ev_end, p->stream);
     HIP_TRY(hipGetLastError(), "kernel launch");
     p->ran = true;
@@ -406,18 +538,23 @@ srt_status srt_plan_fetch(srt_plan *p, srt_path *out, uint64_t *min_latency_ns, 
     }
     if (min_latency_ns) *min_latency_ns = stats[0];
     if (out && p->n) {
-        const size_t total = (size_t)p->n * p->n;
+        // AoS staging in chunks of at most 64 Mi entries (1 GiB): the 100k-node
+        // table is 1e10 entries and must not be duplicated whole in HBM
+        const uint64_t total = (uint64_t)p->n * p->n;
+        const uint64_t chunk = std::min<uint64_t>(total, 1ull << 26);
         if (!p->d_pack) {
             void *ptr = nullptr;
-            hipError_t e = hipMalloc(&ptr, total * sizeof(srt_path));
+            hipError_t e = hipMalloc(&ptr, chunk * sizeof(srt_path));
             if (e != hipSuccess) return hip_fail(err, e, "hipMalloc(pack)");
             p->d_pack = (srt_path *)ptr;
         }
-        srt::pack_paths(p);
-        HIP_TRY(hipMemcpyAsync(out, p->d_pack, total * sizeof(srt_path), hipMemcpyDeviceToHost,
-                               p->stream),
-                "download");
-        HIP_TRY(hipStreamSynchronize(p->stream), "sync");
+        for (uint64_t off = 0; off < total; off += chunk) {
+            const uint64_t c = std::min<uint64_t>(chunk, total - off);
+            srt::pack_paths(p, off, c);
+            HIP_TRY(hipMemcpyAsync(out + off, p->d_pack, c * sizeof(srt_path), hipMemcpyDeviceToHost, p->stream),
+                    "download");
+            HIP_TRY(hipStreamSynchronize(p->stream), "sync");
+        }
     }
     return SRT_OK;
 }
@@ -469,6 +606,39 @@ srt_status srt_plan_bind_comm(srt_plan *p, srt_comm *comm, srt_err *err) {
         return SRT_ERR_INVALID;
     }
     HIP_TRY(hipSetDevice(p->device), "hipSetDevice");
+    if (p->algo == SRT_ALGO_SSSP) {
+        // sources shard with no exchange until the end: rank r owns table rows
+        // [r*per, (r+1)*per) (the last rank's tail past n is padding), and the
+        // table is allocated with per*nranks rows for an equal-chunk all-gather
+        const uint32_t W = (uint32_t)comm->nranks, per = (p->n + W - 1) / W;
+        const uint32_t rows_alloc = per * W;
+        if (rows_alloc > p->rows_alloc) {
+            void *a = nullptr, *b = nullptr;
+            hipError_t e = hipMalloc(&a, std::max<size_t>((size_t)rows_alloc * p->n, 1) * 8);
+            if (e == hipSuccess) e = hipMalloc(&b, std::max<size_t>((size_t)rows_alloc * p->n, 1) * 4);
+            if (e != hipSuccess) {
+                hipFree(a);
+                return hip_fail(err, e, "hipMalloc(table rows)");
+            }
+            hipFree(p->d_out_lat);
+            hipFree(p->d_out_loss);
+            p->d_out_lat = (uint64_t *)a;
+            p->d_out_loss = (float *)b;
+            p->rows_alloc = rows_alloc;
+        }
+        void *rs = nullptr;
+        hipError_t e = hipMalloc(&rs, 2 * sizeof(unsigned long long) * W);
+        if (e != hipSuccess) return hip_fail(err, e, "hipMalloc(rank stats)");
+        hipFree(p->d_rstats);
+        p->d_rstats = (unsigned long long *)rs;
+        p->comm = comm;
+        p->row0 = std::min<uint32_t>(per * (uint32_t)comm->rank, p->n);
+        p->row1 = std::min<uint32_t>(p->row0 + per, p->n);
+        char d[64];
+        std::snprintf(d, sizeof d, " ranks=%d rows=[%u,%u)", comm->nranks, p->row0, p->row1);
+        p->desc += d;
+        return SRT_OK;
+    }
     // pad the node range so every rank owns the same number of block-rows
     // (equal all-gather chunks); padded nodes are isolated and never in use
     const uint32_t unit = (uint32_t)srt::FW_B * (uint32_t)comm->nranks;

@@ -547,10 +547,9 @@ void fw_extract(srt_plan *p) {
     else fw_extract_t<uint64_t>(p);
 }
 
-void pack_paths(srt_plan *p) {
-    const uint64_t total = (uint64_t)p->n * p->n;
-    hipLaunchKernelGGL(pack_kernel, dim3(4096), dim3(256), 0, p->stream, p->d_out_lat,
-                       p->d_out_loss, p->d_pack, total);
+void pack_paths(srt_plan *p, uint64_t first, uint64_t count) {
+    hipLaunchKernelGGL(pack_kernel, dim3(4096), dim3(256), 0, p->stream, p->d_out_lat + first,
+                       p->d_out_loss + first, p->d_pack, count);
 }
 
 }  // namespace srt

@@ -38,9 +38,15 @@ struct KeyParams {
 // FW tile geometry: B x B blocks, one block-row/column per round.
 constexpr int FW_B = 128;
 
-struct FwTimers {
-    std::vector<hipEvent_t> ev;  // 2 per phase-3 launch
-    int used = 0;
+// In-edge of the sparse SSSP (srt_sssp.hip): the source vertex u of an
+// adjacency entry u -> v, its latency in units of g and 1 - loss rounded to f32
+// (the reference's `1f32 - other.packet_loss`, mod.rs:328).  16 B, one
+// global_load_dwordx4 per lane.
+struct InEdge {
+    uint32_t u;
+    uint32_t w;
+    float eb;
+    uint32_t pad;
 };
 
 }  // namespace srt
@@ -101,6 +107,22 @@ struct srt_plan {
     // multi-GPU: this rank computes block-rows [rb0, rb1) of the closure
     srt_comm *comm = nullptr;
     uint32_t rb0 = 0, rb1 = 0;
+
+    // sparse SSSP (algo == SRT_ALGO_SSSP, srt_sssp.hip)
+    uint64_t *d_in_ptr = nullptr;        // V + 1
+    srt::InEdge *d_in_edge = nullptr;    // n_in_edges (self-loops dropped)
+    uint64_t n_in_edges = 0;
+    uint64_t *d_sD = nullptr;            // sssp_nb * V * 64 keys
+    uint64_t *d_smask = nullptr;         // 2 * sssp_nb * V change masks
+    uint32_t *d_sflag = nullptr;         // 3 * sssp_nb convergence flags
+    uint32_t *h_sflag = nullptr;         // pinned host copy
+    uint32_t sssp_nb = 0;                // batches of 64 sources per group
+    uint64_t sssp_g = 1;                 // latency unit
+    uint64_t sssp_sweeps = 0;            // sweeps of the last run (all groups)
+    // table rows this rank computes ([0, n) single-GPU); the table is allocated
+    // with rows_alloc >= n rows so the row all-gather has equal chunks
+    uint32_t row0 = 0, row1 = 0, rows_alloc = 0;
+    unsigned long long *d_rstats = nullptr;  // 2 per rank: min latency, unreachable
 };
 
 namespace srt {
@@ -112,5 +134,9 @@ srt_status comm_allgather_inplace(srt_comm *c, void *buf, size_t bytes_per_rank,
 void fw_init(srt_plan *p);
 srt_status fw_rounds(srt_plan *p, srt_err *err);
 void fw_extract(srt_plan *p);
-void pack_paths(srt_plan *p);
+// table entries [first, first + count) -> d_pack[0, count) as srt_path
+void pack_paths(srt_plan *p, uint64_t first, uint64_t count);
+// kernels (srt_sssp.hip)
+srt_status sssp_run(srt_plan *p, unsigned long long *d_stats, srt_err *err);
+void reduce_rank_stats(srt_plan *p, int nranks);
 }  // namespace srt

@@ -68,6 +68,10 @@ class RoutingPlan:
         _lib.lib().srt_plan_kernel_stats(self._h, C.byref(a), C.byref(b), C.byref(w), C.byref(c))
         return a.value, b.value, w.value, c.value
 
+    def stream_ptr(self) -> int:
+        """hipStream_t the plan launches on (for HIP events on that stream)."""
+        return _lib.lib().srt_plan_stream(self._h)
+
     def table_ptrs(self):
         lat, loss, n = C.c_void_p(), C.c_void_p(), C.c_uint32()
         _lib.lib().srt_plan_table(self._h, C.byref(lat), C.byref(loss), C.byref(n))

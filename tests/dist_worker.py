@@ -1,6 +1,6 @@
 """One rank of the sharded routing build (spawned by tests/test_gpu_dist.py).
 
-usage: dist_worker.py RANK WORLD PORT N SEED TRANSPORT
+usage: dist_worker.py RANK WORLD PORT N SEED TRANSPORT [ALGO]
 All ranks share cuda:0 (the box has one GPU); collectives go through
 torch.distributed/gloo via the callback transport, which exercises exactly the
 same per-round schedule as the RCCL transport.  Exit code 0 = table matches
@@ -17,11 +17,12 @@ sys.path.insert(0, ROOT)
 def main():
     rank, world, port, n, seed = (int(x) for x in sys.argv[1:6])
     transport = sys.argv[6]
+    algo_name = sys.argv[7] if len(sys.argv) > 7 else "auto"
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    from shadow_amd import NetworkGraph, synth
+    from shadow_amd import NetworkGraph, _lib, synth
     from shadow_amd import dist as sdist
     from shadow_amd.plan import RoutingPlan
 
@@ -30,7 +31,8 @@ def main():
                                              loss_max=0.05)
     g = NetworkGraph.from_edges(n, src, dst, lat, loss, directed=True)
     nodes = np.random.default_rng(seed).permutation(n).astype(np.uint32)
-    plan = RoutingPlan(g, nodes, device=0)
+    algo = {"auto": _lib.SRT_ALGO_AUTO, "fw": _lib.SRT_ALGO_FW, "sssp": _lib.SRT_ALGO_SSSP}[algo_name]
+    plan = RoutingPlan(g, nodes, algo=algo, device=0)
     sdist.bind(plan, rank, world, 0, transport=transport)
     plan.run()
     t = plan.fetch()
@@ -43,7 +45,10 @@ def main():
         from oracle import oracle as O
         elat, eloss = O.compute_shortest_paths(O.Graph(True, np.arange(n), src, dst, lat, loss), nodes)
         ok = ok and np.array_equal(t.latency_ns, elat)
-        ok = ok and float(np.abs(t.packet_loss.astype(np.float64) - eloss).max()) <= 1e-6
+        if algo_name == "sssp":  # the sparse sweep's loss is bit-exact
+            ok = ok and np.array_equal(t.packet_loss.view(np.uint32), eloss.view(np.uint32))
+        else:
+            ok = ok and float(np.abs(t.packet_loss.astype(np.float64) - eloss).max()) <= 1e-6
         print(f"rank0: {plan.describe()} ok={ok}", flush=True)
     plan.close()
     dist.destroy_process_group()

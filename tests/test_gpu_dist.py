@@ -20,12 +20,13 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("world,n,seed", [(2, 300, 1), (3, 520, 2)])
-def test_sharded_build_matches_oracle(world, n, seed):
+@pytest.mark.parametrize("world,n,seed,algo", [(2, 300, 1, "fw"), (3, 520, 2, "fw"), (2, 301, 3, "sssp"),
+                                                (3, 200, 4, "sssp")])
+def test_sharded_build_matches_oracle(world, n, seed, algo):
     port = _port()
     env = dict(os.environ)
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker.py"), str(r), str(world), str(port),
-                               str(n), str(seed), "torch"], env=env, stdout=subprocess.PIPE,
+                               str(n), str(seed), "torch", algo], env=env, stdout=subprocess.PIPE,
                               stderr=subprocess.STDOUT, text=True) for r in range(world)]
     outs = []
     for p in procs:
@@ -40,7 +41,8 @@ def test_sharded_build_matches_oracle(world, n, seed):
         assert p.returncode == 0, out[-3000:]
 
 
-def test_rccl_transport_single_rank():
+@pytest.mark.parametrize("algo_name", ["fw", "sssp"])
+def test_rccl_transport_single_rank(algo_name):
     """Native RCCL communicator (1 rank on the box): runs the sharded schedule
     (owner phase 2 row launch, ncclBroadcast of each pivot block-row, column
     launch, ncclAllGather) and must reproduce the unsharded table exactly."""
@@ -55,14 +57,15 @@ def test_rccl_transport_single_rank():
     src, dst, lat, loss = synth.random_graph(n, 4, p_edge=0.05, directed=False, lat_range_ns=(1, 9))
     g = NetworkGraph.from_edges(n, src, dst, lat, loss)
     nodes = np.arange(n, dtype=np.uint32)
-    ref = RoutingPlan(g, nodes, device=0).run().fetch()
+    algo = _lib.SRT_ALGO_FW if algo_name == "fw" else _lib.SRT_ALGO_SSSP
+    ref = RoutingPlan(g, nodes, algo=algo, device=0).run().fetch()
     L = _lib.lib()
     err = _lib.SrtErr()
     uid = (C.c_uint8 * 128)()
     _lib.check(L.srt_comm_unique_id(uid, C.byref(err)), err)
     h = C.c_void_p()
     _lib.check(L.srt_comm_init(uid, 1, 0, 0, C.byref(h), C.byref(err)), err)
-    plan = RoutingPlan(g, nodes, device=0)
+    plan = RoutingPlan(g, nodes, algo=algo, device=0)
     plan.bind_comm(h)
     t = plan.run().fetch()
     assert "ranks=1" in plan.describe()

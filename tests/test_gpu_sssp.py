@@ -1,0 +1,154 @@
+"""GPU parity of the sparse routing build (srt_sssp.hip, SRT_ALGO_SSSP) against
+the oracle's restatement of petgraph's Dijkstra.
+
+Bar: latency bit-exact AND packet_loss bit-exact -- the sweep folds loss with
+the reference's own f32 Add (mod.rs:322-331), so unlike the dense closure no
+tolerance is needed; diagonal = raw self-loop; min latency exact; reference
+error codes.  All calls go through the C ABI (shadow_amd.graph -> libsrt.so).
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from shadow_amd import NetworkGraph, _lib, synth
+from shadow_amd.plan import RoutingPlan
+
+pytestmark = pytest.mark.gpu
+SSSP = _lib.SRT_ALGO_SSSP
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def _check(edges, nodes, directed, n_nodes, node_ids=None):
+    src, dst, lat, loss = edges
+    ids = np.arange(n_nodes) if node_ids is None else node_ids
+    elat, eloss = O.compute_shortest_paths(O.Graph(directed, ids, src, dst, lat, loss), nodes)
+    g = NetworkGraph.from_edges(n_nodes, src, dst, lat, loss, directed=directed, node_ids=ids)
+    t = g.compute_shortest_paths(nodes, algo=SSSP)
+    assert np.array_equal(t.latency_ns, elat), "latency must be bit-exact"
+    assert np.array_equal(_bits(t.packet_loss), _bits(eloss)), "loss must be bit-exact (reference f32 fold)"
+    assert t.min_latency_ns == int(elat.min())
+    return t
+
+
+@pytest.mark.parametrize("directed", [1, 0])
+def test_reference_golden_three_node(directed):
+    from tests.test_gpu_apsp import GOLDEN_DIRECTED, GOLDEN_UNDIRECTED, _three
+    g = NetworkGraph.parse(_three(directed))
+    nodes = [g.node_id_to_index(0), g.node_id_to_index(1), g.node_id_to_index(2)]
+    t = g.compute_shortest_paths(nodes, algo=SSSP)
+    assert t.latency_ns.tolist() == (GOLDEN_DIRECTED if directed else GOLDEN_UNDIRECTED)
+    assert t.min_latency_ns == 3
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("directed", [False, True])
+def test_random_tie_heavy(seed, directed):
+    # few distinct latencies -> many equal-latency paths: the loss tie-break decides
+    n = 60 + 37 * seed  # ragged batches of 64 sources
+    e = synth.random_graph(n, 20 + seed, p_edge=0.08, directed=directed, lat_range_ns=(1, 4), loss_max=0.05)
+    nodes = np.random.default_rng(seed).permutation(n).astype(np.uint32)
+    _check(e, nodes, directed, n)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_subset_in_use_intermediates(seed):
+    # sources/destinations only in-use nodes; any node is an intermediate (mod.rs:203)
+    n = 400
+    e = synth.random_graph(n, 200 + seed, p_edge=0.01, directed=True, lat_range_ns=(1, 30))
+    nodes = np.random.default_rng(seed).choice(n, 97, replace=False).astype(np.uint32)
+    _check(e, nodes, True, n)
+
+
+def test_high_loss_and_loss_one_edges():
+    n = 90
+    src, dst, lat, loss = synth.random_graph(n, 11, p_edge=0.05, lat_range_ns=(1, 3), loss_max=0.9)
+    loss[::7] = 1.0
+    _check((src, dst, lat, loss), np.arange(n, dtype=np.uint32), False, n)
+
+
+def test_ms_latencies_gcd_unit():
+    # latencies in whole ms: the key carries latency / gcd (1 ms) and must scale back exactly
+    n = 150
+    src, dst, lat, loss = synth.random_graph(n, 12, p_edge=0.04, lat_range_ns=(1, 300))
+    lat = lat * np.uint64(synth.MS)
+    _check((src, dst, lat, loss), np.arange(n, dtype=np.uint32), False, n)
+
+
+def test_single_node():
+    g = NetworkGraph.from_edges(1, [0], [0], [42], [0.25], directed=False, node_ids=[9])
+    t = g.compute_shortest_paths([0], algo=SSSP)
+    assert t.latency_ns.tolist() == [[42]] and t.packet_loss[0, 0] == np.float32(0.25)
+
+
+def test_disconnected_raises():
+    g = NetworkGraph.from_edges(3, [0, 1, 2, 0], [0, 1, 2, 1], [5, 5, 5, 3], directed=True)
+    with pytest.raises(_lib.SrtError) as e:
+        g.compute_shortest_paths([0, 1, 2], algo=SSSP)
+    assert e.value.code == _lib.SRT_ERR_DISCONNECTED
+
+
+def test_missing_selfloop_error_text():
+    g = NetworkGraph.from_edges(2, [0, 0], [0, 1], [5, 5], directed=False, node_ids=[4, 8])
+    with pytest.raises(_lib.SrtError) as e:
+        g.compute_shortest_paths([0, 1], algo=SSSP)
+    assert e.value.code == _lib.SRT_ERR_NO_EDGE and str(e.value) == "No edge connecting node 8 to 8"
+
+
+def test_latency_field_overflow_is_refused():
+    # V * max latency must fit the 32-bit latency field; otherwise SSSP is unsupported
+    n = 4
+    src = np.array([0, 1, 2, 3, 0, 1, 2], np.uint32)
+    dst = np.array([0, 1, 2, 3, 1, 2, 3], np.uint32)
+    lat = np.array([1, 1, 1, 1, 1, 1, 2**31], np.uint64)
+    g = NetworkGraph.from_edges(n, src, dst, lat, directed=False)
+    with pytest.raises(_lib.SrtError) as e:
+        g.compute_shortest_paths(np.arange(n), algo=SSSP)
+    assert e.value.code == _lib.SRT_ERR_UNSUPPORTED
+
+
+def test_auto_picks_sssp_for_sparse():
+    src, dst, lat, loss = synth.barabasi_albert(3000, 4, 4)
+    g = NetworkGraph.from_edges(3000, src, dst, lat, loss)
+    plan = RoutingPlan(g, np.arange(64, dtype=np.uint32))
+    assert plan.describe().startswith("sssp")
+    plan.close()
+
+
+def test_c4_graph_row_sample():
+    """Config C4's graph (100k-node Barabasi-Albert, m=4, seed 4): 2,048 in-use
+    nodes spread over the graph (every other node is an intermediate), several
+    source groups; oracle rows for a seeded sample, plus symmetry."""
+    V = 100_000
+    src, dst, lat, loss = synth.barabasi_albert(V, 4, 4)
+    g = NetworkGraph.from_edges(V, src, dst, lat, loss)
+    rng = np.random.default_rng(4)
+    nodes = rng.choice(V, 2048, replace=False).astype(np.uint32)
+    t = g.compute_shortest_paths(nodes)  # AUTO must pick the sparse path here
+    L = t.latency_ns
+    assert np.array_equal(L, L.T)  # undirected
+    og = O.Graph(False, np.arange(V), src, dst, lat, loss)
+    k = 12
+    rows = rng.choice(len(nodes), k, replace=False)
+    order = np.concatenate([rows, np.setdiff1d(np.arange(len(nodes)), rows)])
+    elat, eloss = O.compute_shortest_paths(og, nodes[order], src_count=k)
+    inv = np.argsort(order)
+    for i, r in enumerate(rows):
+        el, ep = elat[i][inv], eloss[i][inv]
+        el[r], ep[r] = L[r, r], t.packet_loss[r, r]  # diagonal: raw self-loop
+        assert np.array_equal(L[r], el)
+        assert np.array_equal(_bits(t.packet_loss[r]), _bits(ep))
+
+
+def test_fw_and_sssp_agree_on_latency():
+    # the dense closure (tolerance on loss) and the sparse sweep (exact loss) on one graph
+    n = 300
+    e = synth.random_graph(n, 77, p_edge=0.03, lat_range_ns=(1, 6), loss_max=0.02)
+    g = NetworkGraph.from_edges(n, *e)
+    nodes = np.arange(n, dtype=np.uint32)
+    a = g.compute_shortest_paths(nodes, algo=_lib.SRT_ALGO_FW)
+    b = g.compute_shortest_paths(nodes, algo=SSSP)
+    assert np.array_equal(a.latency_ns, b.latency_ns)
+    assert np.abs(a.packet_loss.astype(np.float64) - b.packet_loss).max() <= 1e-6
