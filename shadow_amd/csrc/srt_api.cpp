@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <numeric>
@@ -350,19 +351,32 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     p->rows_alloc = n;
     char d[200];
     if (algo == SRT_ALGO_FW) {
-        std::snprintf(d, sizeof d, "fw:%s B=%d g=%llu qb=%u s=%d V=%u n=%u", p->key_f64 ? "f64key" : "u64key",
-                      srt::FW_B, (unsigned long long)p->kp.g, p->kp.qb, p->kp.s, p->V, n);
+        // tuning knob (measurement only): SRT_FW_STAGE=reg selects register staging
+        if (const char *e = std::getenv("SRT_FW_STAGE")) p->fw_glds = std::strcmp(e, "reg") != 0;
+        std::snprintf(d, sizeof d, "fw:%s B=%d g=%llu qb=%u s=%d V=%u n=%u stage=%s",
+                      p->key_f64 ? "f64key" : "u64key", srt::FW_B, (unsigned long long)p->kp.g, p->kp.qb, p->kp.s,
+                      p->V, n, p->fw_glds ? "glds" : "reg");
     } else {
-        // batches of 64 sources in flight: ~192 MB of path state (Infinity
-        // Cache sized), never more batches than the rows need
-        const uint64_t per_batch = (uint64_t)p->V * 64 * 8;
-        uint64_t nb = std::max<uint64_t>(1, (192ull << 20) / std::max<uint64_t>(per_batch, 1));
-        nb = std::min<uint64_t>(nb, std::max<uint32_t>(1, (n + 63) / 64));
-        nb = std::min<uint64_t>(nb, 1024);
-        p->sssp_nb = (uint32_t)nb;
+        // R words of 64 sources per lane (one wave walks a vertex's in-edges
+        // once for 64*R sources), and as many groups in flight as ~256 MB of
+        // path state allows (Infinity Cache sized), never more than the rows need
+        const uint32_t words = std::max<uint32_t>(1, (n + 63) / 64);
+        // tuning knobs (measurement only): SRT_SSSP_R in {1,2,4}, SRT_SSSP_MB budget
+        uint32_t rmax = 1;
+        if (const char *e = std::getenv("SRT_SSSP_R")) rmax = (uint32_t)std::atoi(e);
+        uint64_t budget_mb = 192;
+        if (const char *e = std::getenv("SRT_SSSP_MB")) budget_mb = (uint64_t)std::atoll(e);
+        const uint32_t R = (rmax >= 4 && words >= 4) ? 4 : (rmax >= 2 && words >= 2) ? 2 : 1;
+        const uint64_t per_group = (uint64_t)p->V * 64 * 8 * R;
+        uint64_t G = std::max<uint64_t>(1, (budget_mb << 20) / std::max<uint64_t>(per_group, 1));
+        G = std::min<uint64_t>(G, (words + R - 1) / R);
+        G = std::min<uint64_t>(G, 256);
+        p->sssp_r = R;
+        p->sssp_nb = (uint32_t)(G * R);
         p->n_in_edges = n_in;
-        std::snprintf(d, sizeof d, "sssp:lat32|f32 g=%llu V=%u n=%u E_in=%llu nb=%u",
-                      (unsigned long long)p->sssp_g, p->V, n, (unsigned long long)n_in, p->sssp_nb);
+        std::snprintf(d, sizeof d, "sssp:lat32|f32 g=%llu V=%u n=%u E_in=%llu R=%u groups=%u",
+                      (unsigned long long)p->sssp_g, p->V, n, (unsigned long long)n_in, p->sssp_r,
+                      p->sssp_nb / p->sssp_r);
     }
     p->desc = d;
 

@@ -348,6 +348,102 @@ __global__ __launch_bounds__(NT3, 2) void minplus_tile_kernel(K *__restrict__ D,
     }
 }
 
+// Same tile and per-thread 8x8 register block as minplus_tile_kernel, but the
+// K-chunks are staged with LDS-DMA (global_load_lds_dwordx4: no VGPR round
+// trip, so the loads of chunk c+1 are issued before chunk c is consumed and
+// stay in flight under its 16 k-steps; -32 VGPRs of staging registers).
+// One __shared__ array holds both double-buffered images (a second __shared__
+// object can make hipcc drain vmcnt before every ds_read):
+//   A image [buf][128 rows][16 k], 128-B rows, lane-linear per 8-row piece; the
+//     k pairs of rows with (row>>3)&1 are XOR-swizzled by one pair (16 B) on the
+//     SOURCE side so the two row groups a half-wave reads hit different banks;
+//   B image [buf][16 k][128 cols], one 1-KiB wave-instruction per k row.
+template <typename K, int TAG>
+__global__ __launch_bounds__(NT3, 2) void minplus_glds_kernel(K *__restrict__ D, uint32_t Vp, uint32_t kb,
+                                                           Rect r1, Rect r2) {
+    static_assert(sizeof(K) == 8, "8-byte keys");
+    constexpr int AIMG = B * KC, BIMG = KC * B, BUF = AIMG + BIMG;  // elements
+    __shared__ K lds[2 * BUF];
+    const uint32_t n1 = r1.r.n * r1.c.n;
+    uint32_t t = blockIdx.x, bi, bj;
+    if (t < n1) {
+        if (gridDim.x == n1 && n1 >= 64) {  // XCD-aware bijective remap (see minplus_tile_kernel)
+            const uint32_t q = n1 / 8, rr = n1 % 8, xcd = t % 8;
+            t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + t / 8;
+        }
+        bi = span_at(r1.r, t / r1.c.n);
+        bj = span_at(r1.c, t % r1.c.n);
+    } else {
+        t -= n1;
+        bi = span_at(r2.r, t / r2.c.n);
+        bj = span_at(r2.c, t % r2.c.n);
+    }
+    const uint64_t i0 = (uint64_t)bi * B, j0 = (uint64_t)bj * B, k0 = (uint64_t)kb * B;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int tx = tid % 16, ty = tid / 16;
+
+    K acc[TR][TC];
+#pragma unroll
+    for (int i = 0; i < TR; ++i) {
+        const K *src = D + (i0 + ty * TR + i) * Vp + j0 + tx;
+#pragma unroll
+        for (int j = 0; j < TC; ++j) acc[i][j] = src[16 * j];
+    }
+    // 32 wave-instructions of 1 KiB per chunk, 8 per wave: 4 A pieces (8 rows
+    // each) and 4 B rows
+    auto stage = [&](int kc, int buf) {
+        K *img = lds + buf * BUF;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int r0 = (wave * 4 + q) * 8;             // A piece: rows r0..r0+7
+            const int row = r0 + lane / 8;
+            const int pair = (lane % 8) ^ ((r0 >> 3) & 1);  // source-side swizzle
+            const K *g = D + (i0 + row) * Vp + k0 + kc + pair * 2;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
+                                             (__attribute__((address_space(3))) void *)(img + r0 * KC), 16, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int kr = wave * 4 + q;  // B row
+            const K *g = D + (k0 + kc + kr) * Vp + j0 + lane * 2;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
+                                             (__attribute__((address_space(3))) void *)(img + AIMG + kr * B), 16,
+                                             0, 0);
+        }
+    };
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    constexpr int NCH = B / KC;
+    const int sw = (ty & 1) << 1;  // A read swizzle: rows ty*8+i all have (row>>3)&1 == ty&1
+#pragma unroll 1
+    for (int ch = 0; ch < NCH; ++ch) {
+        const int cur = ch & 1;
+        if (ch + 1 < NCH) stage((ch + 1) * KC, cur ^ 1);  // the other buffer's readers passed the last barrier
+        const K *As = lds + cur * BUF;
+        const K *Bs = As + AIMG;
+#pragma unroll 2
+        for (int k = 0; k < KC; ++k) {
+            K a[TR], b[TC];
+#pragma unroll
+            for (int i = 0; i < TR; ++i) a[i] = As[(ty * TR + i) * KC + (k ^ sw)];
+#pragma unroll
+            for (int j = 0; j < TC; ++j) b[j] = Bs[k * B + tx + 16 * j];
+#pragma unroll
+            for (int i = 0; i < TR; ++i) relax_row8<K>(acc[i], a[i], b);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < TR; ++i) {
+        K *dst = D + (i0 + ty * TR + i) * Vp + j0 + tx;
+#pragma unroll
+        for (int j = 0; j < TC; ++j) dst[16 * j] = acc[i][j];
+    }
+}
+
 // ------------------------------------------------------------- extract
 // table[i][j] = decode(D[nodes[i]][nodes[j]]); diagonal = the raw self-loop
 // edge (mod.rs:210-217); min latency over the whole table (mod.rs:474-476);
@@ -441,8 +537,12 @@ template <typename K, int TAG>
 void launch_tiles(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1, const Rect &r2) {
     const uint32_t n = r1.r.n * r1.c.n + r2.r.n * r2.c.n;
     if (!n) return;
-    hipLaunchKernelGGL((minplus_tile_kernel<K, TAG>), dim3(n), dim3(NT3), 0, s,
-                       reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2);
+    if (p->fw_glds)
+        hipLaunchKernelGGL((minplus_glds_kernel<K, TAG>), dim3(n), dim3(NT3), 0, s,
+                           reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2);
+    else
+        hipLaunchKernelGGL((minplus_tile_kernel<K, TAG>), dim3(n), dim3(NT3), 0, s,
+                           reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2);
 }
 
 // Round schedule with one block of look-ahead, per rank (block-rows [rb0,rb1)):

@@ -71,6 +71,7 @@ struct srt_plan {
     int algo = SRT_ALGO_FW;
     srt::KeyParams kp{};
     bool key_f64 = false;  // f64-encoded keys (exact integers < 2^53)
+    bool fw_glds = true;   // FW tiles staged by LDS-DMA (false: register staging)
     std::string desc;
     bool identity_nodes = false;
 
@@ -116,7 +117,8 @@ struct srt_plan {
     uint64_t *d_smask = nullptr;         // 2 * sssp_nb * V change masks
     uint32_t *d_sflag = nullptr;         // 3 * sssp_nb convergence flags
     uint32_t *h_sflag = nullptr;         // pinned host copy
-    uint32_t sssp_nb = 0;                // batches of 64 sources per group
+    uint32_t sssp_nb = 0;                // 64-source words in flight (groups x sssp_r)
+    uint32_t sssp_r = 1;                 // 64-source words per lane (group = 64 * sssp_r sources)
     uint64_t sssp_g = 1;                 // latency unit
     uint64_t sssp_sweeps = 0;            // sweeps of the last run (all groups)
     // table rows this rank computes ([0, n) single-GPU); the table is allocated

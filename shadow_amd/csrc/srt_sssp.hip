@@ -53,133 +53,164 @@ __device__ __forceinline__ uint64_t relax(uint64_t du, uint32_t w, float eb) {
     return ((uint64_t)lat << 32) | (uint64_t)__float_as_uint(loss);
 }
 
+// D, masks and flags of G groups of R batches (R*64 sources per group)
 __global__ void sssp_init_kernel(uint64_t *__restrict__ D, uint64_t *__restrict__ mask, uint32_t *flag,
-                                 uint32_t V, uint32_t nb) {
-    const uint64_t nD = (uint64_t)nb * V * 64, nM = 2ull * nb * V;
+                                 uint32_t V, uint32_t nbat, uint32_t G) {
+    const uint64_t nD = (uint64_t)nbat * V * 64, nM = 2ull * nbat * V;
     for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < nD;
          e += (uint64_t)gridDim.x * blockDim.x) {
         D[e] = SKEY_INF;
         if (e < nM) mask[e] = 0;
-        if (e < 3ull * nb) flag[e] = 0;
+        if (e < 3ull * G) flag[e] = 0;
     }
 }
 
-// batch b, lane s: source = nodes[row0 + b*64 + s] when that row is < row1
+// source row row0 + q (q = (g*R + r)*64 + s) -> group g, word r, lane s:
+// D[g][v][r][s], mask[g][v][r]
 __global__ void sssp_seed_kernel(uint64_t *__restrict__ D, uint64_t *__restrict__ mask,
                                  const uint32_t *__restrict__ nodes, uint32_t V, uint32_t row0,
-                                 uint32_t row1, uint32_t nb) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nb * 64) return;
-    const uint32_t b = t / 64, s = t % 64, r = row0 + t;
-    if (r >= row1) return;
-    const uint32_t src = nodes[r];
-    D[((uint64_t)b * V + src) * 64 + s] = 0ull;  // (0 ns, 0.0 loss): petgraph's zero score
-    mask[(uint64_t)b * V + src] = 1ull << s;     // sources within a batch are distinct nodes
+                                 uint32_t row1, uint32_t nbat, uint32_t R) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nbat * 64) return;
+    const uint32_t g = q / (64 * R), r = (q / 64) % R, s = q % 64;
+    if (row0 + q >= row1) return;
+    const uint32_t src = nodes[row0 + q];
+    const uint64_t row = (uint64_t)g * V + src;
+    D[(row * R + r) * 64 + s] = 0ull;  // (0 ns, 0.0 loss): petgraph's zero score
+    mask[row * R + r] = 1ull << s;     // sources within a word are distinct nodes
 }
 
+// Sweep t over G groups (blockIdx.y): one wave per target vertex v handles the
+// R*64 sources of its group.  Per chunk of 64 in-edges every lane loads one
+// edge and the R change masks of its source vertex; edges whose source changed
+// are walked 4 at a time with up to 4*R predicated gathers in flight.
+template <int R>
 __global__ __launch_bounds__(SWP_WAVES * 64) void sssp_sweep_kernel(
     const uint64_t *__restrict__ in_ptr, const InEdge *__restrict__ in_edge, uint32_t V,
     uint64_t *D, const uint64_t *__restrict__ mask_cur, uint64_t *__restrict__ mask_next,
     uint32_t *flag, uint32_t t) {
-    const uint32_t b = blockIdx.y, nb = gridDim.y;
-    if (blockIdx.x == 0 && threadIdx.x == 0) flag[((t + 1) % 3) * nb + b] = 0;  // for sweep t+1
-    if (t > 0 && flag[((t + 2) % 3) * nb + b] == 0) return;                     // converged
+    const uint32_t g = blockIdx.y, G = gridDim.y;
+    if (blockIdx.x == 0 && threadIdx.x == 0) flag[((t + 1) % 3) * G + g] = 0;  // for sweep t+1
+    if (t > 0 && flag[((t + 2) % 3) * G + g] == 0) return;                     // converged
     const int lane = threadIdx.x & 63;
     const uint32_t v = __builtin_amdgcn_readfirstlane(blockIdx.x * SWP_WAVES + (threadIdx.x >> 6));
     if (v >= V) return;
-    const uint64_t base = (uint64_t)b * V;
-    const uint64_t *Db = D + base * 64;
-    const uint64_t *mc = mask_cur + base;
-    uint64_t best = SKEY_INF;
+    const uint64_t base = (uint64_t)g * V;  // first vertex row of the group
+    const uint64_t *Dg = D + base * R * 64;
+    const uint64_t *mc = mask_cur + base * R;
+    uint64_t best[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) best[r] = SKEY_INF;
     const uint64_t e0 = in_ptr[v], e1 = in_ptr[v + 1];
     for (uint64_t c0 = e0; c0 < e1; c0 += 64) {
         const uint64_t k = c0 + lane;
         uint32_t eu = 0, ew = 0;
         float eeb = 0.f;
-        uint64_t em = 0;
+        uint64_t em[R];
+        bool any = false;
+#pragma unroll
+        for (int r = 0; r < R; ++r) em[r] = 0;
         if (k < e1) {
             const InEdge e = in_edge[k];
             eu = e.u;
             ew = e.w;
             eeb = e.eb;
-            em = mc[eu];
-        }
-        uint64_t act = __ballot(em != 0);
-        while (act) {
-            uint64_t du[8];
-            uint32_t w[8];
-            float eb[8];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                du[q] = SKEY_INF;
+            for (int r = 0; r < R; ++r) {
+                em[r] = mc[(uint64_t)eu * R + r];
+                any |= em[r] != 0;
+            }
+        }
+        uint64_t act = __ballot(any);
+        while (act) {
+            uint64_t du[4][R];
+            uint32_t w[4];
+            float eb[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
                 w[q] = 0;
                 eb[q] = 0.f;
+#pragma unroll
+                for (int r = 0; r < R; ++r) du[q][r] = SKEY_INF;
                 if (act) {
                     const int j = __builtin_ctzll(act);
                     act &= act - 1;
                     const uint32_t u = __builtin_amdgcn_readlane(eu, j);
-                    const uint32_t mlo = __builtin_amdgcn_readlane((uint32_t)em, j);
-                    const uint32_t mhi = __builtin_amdgcn_readlane((uint32_t)(em >> 32), j);
                     w[q] = __builtin_amdgcn_readlane(ew, j);
                     eb[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(eeb), j));
-                    const uint32_t bit = lane < 32 ? (mlo >> lane) : (mhi >> (lane - 32));
-                    if (bit & 1u) du[q] = Db[(uint64_t)u * 64 + lane];
+                    const uint64_t *Du = Dg + (uint64_t)u * R * 64 + lane;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const uint32_t mlo = __builtin_amdgcn_readlane((uint32_t)em[r], j);
+                        const uint32_t mhi = __builtin_amdgcn_readlane((uint32_t)(em[r] >> 32), j);
+                        const uint32_t bit = lane < 32 ? (mlo >> lane) : (mhi >> (lane - 32));
+                        if (bit & 1u) du[q][r] = Du[r * 64];
+                    }
                 }
             }
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                if (du[q] != SKEY_INF) {
-                    const uint64_t c = relax(du[q], w[q], eb[q]);
-                    best = c < best ? c : best;
+            for (int q = 0; q < 4; ++q) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if (du[q][r] != SKEY_INF) {
+                        const uint64_t c = relax(du[q][r], w[q], eb[q]);
+                        best[r] = c < best[r] ? c : best[r];
+                    }
                 }
             }
         }
     }
-    bool imp = false;
-    if (best != SKEY_INF) {
-        uint64_t *dv = D + (base + v) * 64 + lane;
-        if (best < *dv) {
-            *dv = best;
+    uint64_t *Dv = D + ((base + v) * R) * 64 + lane;
+    bool imp_any = false;
+    uint64_t m_out[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        bool imp = false;
+        if (best[r] != SKEY_INF && best[r] < Dv[r * 64]) {
+            Dv[r * 64] = best[r];
             imp = true;
         }
+        m_out[r] = __ballot(imp);
+        imp_any |= m_out[r] != 0;
     }
-    const uint64_t m_out = __ballot(imp);
     if (lane == 0) {
-        mask_next[base + v] = m_out;
-        if (m_out) flag[(t % 3) * nb + b] = 1;  // idempotent store, no atomic
+#pragma unroll
+        for (int r = 0; r < R; ++r) mask_next[(base + v) * R + r] = m_out[r];
+        if (imp_any) flag[(t % 3) * G + g] = 1;  // idempotent store, no atomic
     }
 }
 
-// Table rows of the group: row = row0 + b*64 + s for source lane s of batch b.
+// Table rows of the group: row = row0 + (g*R + r)*64 + s for lane s of word r.
 // A 64 x 64 (sources x columns) tile goes through LDS so both the gather from
 // D (64 sources of one vertex) and the row-major table stores are coalesced.
 // Diagonal = the raw self-loop (mod.rs:210-217); min latency (mod.rs:474-476)
 // and unreachable count (the assert at mod.rs:219) are block-reduced into
-// stats[0] (min) / stats[1] (count).
+// stats[0] (min) / stats[1] (count).  blockIdx.y = g*R + r.
 __global__ __launch_bounds__(256) void sssp_emit_kernel(
-    const uint64_t *__restrict__ D, uint32_t V, const uint32_t *__restrict__ nodes, uint32_t n, uint32_t row0,
-    uint32_t row1, uint64_t g, const uint64_t *__restrict__ sl_lat, const float *__restrict__ sl_loss,
-    uint64_t *__restrict__ out_lat, float *__restrict__ out_loss, unsigned long long *stats) {
+    const uint64_t *__restrict__ D, uint32_t V, uint32_t R, const uint32_t *__restrict__ nodes, uint32_t n,
+    uint32_t row0, uint32_t row1, uint64_t gunit, const uint64_t *__restrict__ sl_lat,
+    const float *__restrict__ sl_loss, uint64_t *__restrict__ out_lat, float *__restrict__ out_loss,
+    unsigned long long *stats) {
     __shared__ uint64_t tile[64][65];
     __shared__ unsigned long long red_min[4], red_cnt[4];
-    const uint32_t b = blockIdx.y, j0 = blockIdx.x * 64;
+    const uint32_t b = blockIdx.y, g = b / R, r = b % R, j0 = blockIdx.x * 64;
     const int tid = threadIdx.x;
-    const uint64_t *Db = D + (uint64_t)b * V * 64;
+    const uint64_t *Dg = D + (uint64_t)g * V * R * 64 + (uint64_t)r * 64;
     for (int idx = tid; idx < 64 * 64; idx += 256) {
         const int jj = idx / 64, s = idx % 64;
         const uint32_t j = j0 + jj;
-        tile[jj][s] = j < n ? Db[(uint64_t)nodes[j] * 64 + s] : SKEY_INF;
+        tile[jj][s] = j < n ? Dg[(uint64_t)nodes[j] * R * 64 + s] : SKEY_INF;
     }
     __syncthreads();
     uint64_t mn = ~0ull;
     unsigned long long unreach = 0;
     for (int idx = tid; idx < 64 * 64; idx += 256) {
         const int s = idx / 64, jj = idx % 64;
-        const uint32_t j = j0 + jj, r = row0 + b * 64 + s;
-        if (j >= n || r >= row1) continue;
+        const uint32_t j = j0 + jj, row = row0 + b * 64 + s;
+        if (j >= n || row >= row1) continue;
         uint64_t lat;
         float loss;
-        if (r == j) {
+        if (row == j) {
             lat = sl_lat[j];
             loss = sl_loss[j];
         } else {
@@ -189,12 +220,12 @@ __global__ __launch_bounds__(256) void sssp_emit_kernel(
                 lat = ~0ull;
                 loss = 1.0f;
             } else {
-                lat = (k >> 32) * g;
+                lat = (k >> 32) * gunit;
                 loss = __uint_as_float((uint32_t)k);
             }
         }
-        out_lat[(uint64_t)r * n + j] = lat;
-        out_loss[(uint64_t)r * n + j] = loss;
+        out_lat[(uint64_t)row * n + j] = lat;
+        out_loss[(uint64_t)row * n + j] = loss;
         mn = lat < mn ? lat : mn;
     }
     for (int off = 32; off > 0; off >>= 1) {
@@ -237,42 +268,53 @@ __global__ void reduce_rank_stats_kernel(const unsigned long long *rstats, int n
 
 }  // namespace
 
-// Whole build for this rank's table rows [row0, row1), group by group.  The
-// host polls the convergence flags after each chunk of sweeps, so this call
-// returns with the stream drained up to the last group's emit.
+template <int R>
+void launch_sweep(dim3 grid, hipStream_t s, srt_plan *p, uint64_t *mc, uint64_t *mn, uint32_t t) {
+    hipLaunchKernelGGL(sssp_sweep_kernel<R>, grid, dim3(SWP_WAVES * 64), 0, s, p->d_in_ptr, p->d_in_edge, p->V,
+                       p->d_sD, mc, mn, p->d_sflag, t);
+}
+
+// Whole build for this rank's table rows [row0, row1), G groups of R*64
+// sources at a time.  The host polls the convergence flags after each chunk
+// of sweeps, so this call returns with the stream drained up to the last
+// emit.
 srt_status sssp_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     hipStream_t M = p->stream;
-    const uint32_t V = p->V, NB = p->sssp_nb;
+    const uint32_t V = p->V, R = p->sssp_r, GMAX = p->sssp_nb / p->sssp_r;
+    const uint32_t per_launch = 64 * R * GMAX;
     p->p3_launches = 0;
     p->p3_work = 0.0;
     p->sssp_sweeps = 0;
     hipLaunchKernelGGL(sssp_stats_init_kernel, dim3(1), dim3(1), 0, M, d_stats);
-    const uint32_t groups = (p->row1 - p->row0 + 64 * NB - 1) / (64 * NB);
-    while (p->ev.size() < 2 * (size_t)groups) {
+    const uint32_t launches = (p->row1 - p->row0 + per_launch - 1) / per_launch;
+    while (p->ev.size() < 2 * (size_t)launches) {
         hipEvent_t e;
-        hipEventCreateWithFlags(&e, 0);
+        (void)hipEventCreateWithFlags(&e, 0);
         p->ev.push_back(e);
     }
     uint32_t chunk = 8;
-    for (uint32_t gi = 0; gi < groups; ++gi) {
-        const uint32_t g0 = p->row0 + gi * 64 * NB;
-        const uint32_t rows = std::min<uint32_t>(64 * NB, p->row1 - g0);
-        const uint32_t nb = (rows + 63) / 64;
-        hipLaunchKernelGGL(sssp_init_kernel, dim3(4096), dim3(256), 0, M, p->d_sD, p->d_smask, p->d_sflag, V, nb);
-        hipLaunchKernelGGL(sssp_seed_kernel, dim3((nb * 64 + 255) / 256), dim3(256), 0, M, p->d_sD, p->d_smask,
-                           p->d_nodes, V, g0, g0 + rows, nb);
-        hipEventRecord(p->ev[2 * gi], M);
-        const dim3 grid((V + SWP_WAVES - 1) / SWP_WAVES, nb);
+    for (uint32_t li = 0; li < launches; ++li) {
+        const uint32_t g0 = p->row0 + li * per_launch;
+        const uint32_t rows = std::min<uint32_t>(per_launch, p->row1 - g0);
+        const uint32_t nbat = (rows + 63) / 64;           // 64-source words with work
+        const uint32_t G = (nbat + R - 1) / R;            // groups in this launch
+        hipLaunchKernelGGL(sssp_init_kernel, dim3(4096), dim3(256), 0, M, p->d_sD, p->d_smask, p->d_sflag, V,
+                           G * R, G);
+        hipLaunchKernelGGL(sssp_seed_kernel, dim3((nbat * 64 + 255) / 256), dim3(256), 0, M, p->d_sD, p->d_smask,
+                           p->d_nodes, V, g0, g0 + rows, nbat, R);
+        (void)hipEventRecord(p->ev[2 * li], M);
+        const dim3 grid((V + SWP_WAVES - 1) / SWP_WAVES, G);
         uint32_t t = 0;
         for (;;) {
             for (uint32_t c = 0; c < chunk; ++c, ++t) {
-                uint64_t *mc = p->d_smask + (uint64_t)(t & 1) * nb * V;
-                uint64_t *mn = p->d_smask + (uint64_t)((t + 1) & 1) * nb * V;
-                hipLaunchKernelGGL(sssp_sweep_kernel, grid, dim3(SWP_WAVES * 64), 0, M, p->d_in_ptr, p->d_in_edge,
-                                   V, p->d_sD, mc, mn, p->d_sflag, t);
+                uint64_t *mc = p->d_smask + (uint64_t)(t & 1) * G * R * V;
+                uint64_t *mn = p->d_smask + (uint64_t)((t + 1) & 1) * G * R * V;
+                if (R == 4) launch_sweep<4>(grid, M, p, mc, mn, t);
+                else if (R == 2) launch_sweep<2>(grid, M, p, mc, mn, t);
+                else launch_sweep<1>(grid, M, p, mc, mn, t);
             }
             // flags of the last sweep (t-1): all zero == converged
-            hipError_t e = hipMemcpyAsync(p->h_sflag, p->d_sflag + ((t - 1) % 3) * nb, nb * sizeof(uint32_t),
+            hipError_t e = hipMemcpyAsync(p->h_sflag, p->d_sflag + ((t - 1) % 3) * G, G * sizeof(uint32_t),
                                           hipMemcpyDeviceToHost, M);
             if (e == hipSuccess) e = hipStreamSynchronize(M);
             if (e != hipSuccess) {
@@ -283,7 +325,7 @@ srt_status sssp_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
                 return SRT_ERR_HIP;
             }
             bool any = false;
-            for (uint32_t b = 0; b < nb; ++b) any |= p->h_sflag[b] != 0;
+            for (uint32_t b = 0; b < G; ++b) any |= p->h_sflag[b] != 0;
             if (!any) break;
             if (t > V + 2) {  // Bellman-Ford bound: cannot happen with positive latencies
                 if (err) {
@@ -294,13 +336,13 @@ srt_status sssp_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
             }
             chunk = 4;
         }
-        hipEventRecord(p->ev[2 * gi + 1], M);
+        (void)hipEventRecord(p->ev[2 * li + 1], M);
         p->p3_launches++;
         p->sssp_sweeps += t;
-        // the next group starts with as many sweeps as this one needed
+        // the next launch starts with as many sweeps as this one needed
         chunk = std::max<uint32_t>(t, 4);
-        hipLaunchKernelGGL(sssp_emit_kernel, dim3((p->n + 63) / 64, nb), dim3(256), 0, M, p->d_sD, V, p->d_nodes,
-                           p->n, g0, g0 + rows, p->sssp_g, p->d_sl_lat, p->d_sl_loss, p->d_out_lat,
+        hipLaunchKernelGGL(sssp_emit_kernel, dim3((p->n + 63) / 64, G * R), dim3(256), 0, M, p->d_sD, V, R,
+                           p->d_nodes, p->n, g0, g0 + rows, p->sssp_g, p->d_sl_lat, p->d_sl_loss, p->d_out_lat,
                            p->d_out_loss, d_stats);
     }
     // algorithmic bytes: 12 B per in-edge + 12 B per vertex, per source
