@@ -546,9 +546,10 @@ void launch_tiles(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1, const
 }
 
 // Round schedule with one block of look-ahead, per rank (block-rows [rb0,rb1)):
-//   main stream M:  p2col(kb) | cross(kb) | rest(kb)
+//   main stream M:  cross(kb) | rest(kb) | (wait S) cross(kb+1) | ...
 //   side stream S:  (after cross(kb))  p1(kb+1), p2row(kb+1) on the owner of
-//                   kb+1, then the pivot-row broadcast of kb+1 (multi-GPU)
+//                   kb+1, the pivot-row broadcast of kb+1 (multi-GPU), then
+//                   p2col(kb+1) for the local rows
 // cross(kb) = the round-kb phase-3 tiles that round kb+1's pivot work needs
 // (column kb+1 of the local rows; row kb+1 on its owner), rest(kb) = all other
 // phase-3 tiles.  rest(kb) never touches block-row/column kb+1, so it runs
@@ -599,6 +600,9 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
                 (st = comm_bcast(p->comm, D + (uint64_t)k1 * B * p->Vp, pivot_bytes, (int)(k1 / per_rank), S,
                                  err)) != SRT_OK)
                 return st;
+            // p2col(k1): column k1 of the local rows through P*(k1); rest(kb)
+            // never touches column k1, so this also overlaps rest(kb)
+            launch_tiles<K, 2>(p, S, k1, Rect{make_span(rb0, rb1, k1), make_span(k1, k1 + 1)}, none);
             hipEventRecord(p->ev_pivot, S);
         }
         // rest(kb): local rows and all columns, minus kb and (look-ahead) k1
@@ -611,11 +615,7 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
             p->p3_launches++;
             p->p3_work += (double)nt * B * B * B;
         }
-        if (nxt) {
-            hipStreamWaitEvent(M, p->ev_pivot, 0);
-            // p2col(k1): column k1 of the local rows through P*(k1)
-            launch_tiles<K, 2>(p, M, k1, Rect{make_span(rb0, rb1, k1), make_span(k1, k1 + 1)}, none);
-        }
+        if (nxt) hipStreamWaitEvent(M, p->ev_pivot, 0);
     }
     if (sharded)
         return comm_allgather_inplace(p->comm, D, (size_t)per_rank * B * p->Vp * sizeof(K), M, err);
