@@ -354,16 +354,85 @@ __global__ __launch_bounds__(NT3, 2) void minplus_tile_kernel(K *__restrict__ D,
 // stay in flight under its 16 k-steps; -32 VGPRs of staging registers).
 // One __shared__ array holds both double-buffered images (a second __shared__
 // object can make hipcc drain vmcnt before every ds_read):
-//   A image [buf][128 rows][16 k], 128-B rows, lane-linear per 8-row piece; the
-//     k pairs of rows with (row>>3)&1 are XOR-swizzled by one pair (16 B) on the
-//     SOURCE side so the two row groups a half-wave reads hit different banks;
+//   A image [buf][16 pieces][8 rows][16 k] + 16 B pad per piece: one 1-KiB
+//     lane-linear wave-instruction per piece; the pad puts the two pieces a
+//     half-wave reads (rows ty*8.., ty even / odd) on different banks;
 //   B image [buf][16 k][128 cols], one 1-KiB wave-instruction per k row.
+constexpr int APIECE = 8 * KC + 2;          // elements per padded A piece (1040 B)
+constexpr int AIMG = (B / 8) * APIECE;      // 2080
+constexpr int BIMG = KC * B;                // 2048
+constexpr int GBUF = AIMG + BIMG;           // elements per buffer
+
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+// Operands of one k-step: a[i] for the thread's 8 rows (as 4 pairs) and b[j]
+// for its 8 columns.
+struct StepOps {
+    f64x2 a[4];
+    double b[8];
+};
+
+// LDS reads of step k into o, by inline asm so hipcc neither merges steps nor
+// inserts waits: the caller waits with an explicit lgkmcnt.  abase = byte
+// address of the thread's A piece, bbase = of its first B column.
+template <int k>
+__device__ __forceinline__ void lds_step(StepOps &o, uint32_t abase, uint32_t bbase) {
+    asm volatile("ds_read2_b64 %0, %1 offset0:%2 offset1:%3" : "=v"(o.a[0]) : "v"(abase), "i"(k), "i"(16 + k));
+    asm volatile("ds_read2_b64 %0, %1 offset0:%2 offset1:%3" : "=v"(o.a[1]) : "v"(abase), "i"(32 + k), "i"(48 + k));
+    asm volatile("ds_read2_b64 %0, %1 offset0:%2 offset1:%3" : "=v"(o.a[2]) : "v"(abase), "i"(64 + k), "i"(80 + k));
+    asm volatile("ds_read2_b64 %0, %1 offset0:%2 offset1:%3" : "=v"(o.a[3]) : "v"(abase), "i"(96 + k), "i"(112 + k));
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(o.b[j]) : "v"(bbase), "i"(k * B * 8 + j * 128));
+}
+
+// acc[j] = min(acc[j], a + b[j]), j < 8, as one volatile asm block so it stays
+// in program order with the explicit waits.
+__device__ __forceinline__ void relax_row8_v(double (&acc)[8], double a, const double (&b)[8]) {
+    double t0, t1, t2, t3, t4, t5, t6, t7;
+    asm volatile(
+        "v_add_f64 %0, %16, %17\n\t"
+        "v_add_f64 %1, %16, %18\n\t"
+        "v_add_f64 %2, %16, %19\n\t"
+        "v_add_f64 %3, %16, %20\n\t"
+        "v_add_f64 %4, %16, %21\n\t"
+        "v_add_f64 %5, %16, %22\n\t"
+        "v_add_f64 %6, %16, %23\n\t"
+        "v_add_f64 %7, %16, %24\n\t"
+        "v_min_f64 %8, %8, %0\n\t"
+        "v_min_f64 %9, %9, %1\n\t"
+        "v_min_f64 %10, %10, %2\n\t"
+        "v_min_f64 %11, %11, %3\n\t"
+        "v_min_f64 %12, %12, %4\n\t"
+        "v_min_f64 %13, %13, %5\n\t"
+        "v_min_f64 %14, %14, %6\n\t"
+        "v_min_f64 %15, %15, %7"
+        : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "=&v"(t4), "=&v"(t5), "=&v"(t6), "=&v"(t7),
+          "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[6]),
+          "+v"(acc[7])
+        : "v"(a), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7]));
+}
+
+// Steps k .. KC-1 of a chunk: wait for step k's operands (issued during step
+// k-1), issue step k+1's reads into the other operand set, then 128 VALU ops.
+template <int k>
+__device__ __forceinline__ void chunk_steps(double (&acc)[TR][TC], StepOps (&o)[2], uint32_t abase,
+                                            uint32_t bbase) {
+    if constexpr (k < KC) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (k + 1 < KC) lds_step<k + 1>(o[(k + 1) & 1], abase, bbase);
+        const StepOps &c = o[k & 1];
+#pragma unroll
+        for (int i = 0; i < TR; ++i) relax_row8_v(acc[i], (i & 1) ? c.a[i >> 1].y : c.a[i >> 1].x, c.b);
+        chunk_steps<k + 1>(acc, o, abase, bbase);
+    }
+}
+
 template <typename K, int TAG>
 __global__ __launch_bounds__(NT3, 2) void minplus_glds_kernel(K *__restrict__ D, uint32_t Vp, uint32_t kb,
                                                            Rect r1, Rect r2) {
     static_assert(sizeof(K) == 8, "8-byte keys");
-    constexpr int AIMG = B * KC, BIMG = KC * B, BUF = AIMG + BIMG;  // elements
-    __shared__ K lds[2 * BUF];
+    __shared__ K lds[2 * GBUF];
     const uint32_t n1 = r1.r.n * r1.c.n;
     uint32_t t = blockIdx.x, bi, bj;
     if (t < n1) {
@@ -393,15 +462,14 @@ __global__ __launch_bounds__(NT3, 2) void minplus_glds_kernel(K *__restrict__ D,
     // 32 wave-instructions of 1 KiB per chunk, 8 per wave: 4 A pieces (8 rows
     // each) and 4 B rows
     auto stage = [&](int kc, int buf) {
-        K *img = lds + buf * BUF;
+        K *img = lds + buf * GBUF;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const int r0 = (wave * 4 + q) * 8;             // A piece: rows r0..r0+7
-            const int row = r0 + lane / 8;
-            const int pair = (lane % 8) ^ ((r0 >> 3) & 1);  // source-side swizzle
-            const K *g = D + (i0 + row) * Vp + k0 + kc + pair * 2;
+            const int piece = wave * 4 + q;  // rows piece*8 .. +7
+            const K *g = D + (i0 + piece * 8 + lane / 8) * Vp + k0 + kc + (lane % 8) * 2;
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
-                                             (__attribute__((address_space(3))) void *)(img + r0 * KC), 16, 0, 0);
+                                             (__attribute__((address_space(3))) void *)(img + piece * APIECE), 16,
+                                             0, 0);
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -416,22 +484,29 @@ __global__ __launch_bounds__(NT3, 2) void minplus_glds_kernel(K *__restrict__ D,
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     constexpr int NCH = B / KC;
-    const int sw = (ty & 1) << 1;  // A read swizzle: rows ty*8+i all have (row>>3)&1 == ty&1
 #pragma unroll 1
     for (int ch = 0; ch < NCH; ++ch) {
         const int cur = ch & 1;
         if (ch + 1 < NCH) stage((ch + 1) * KC, cur ^ 1);  // the other buffer's readers passed the last barrier
-        const K *As = lds + cur * BUF;
-        const K *Bs = As + AIMG;
+        const K *As = lds + cur * GBUF + ty * APIECE;     // the thread's A piece
+        const K *Bs = lds + cur * GBUF + AIMG + tx;       // the thread's first B column
+        if constexpr (std::is_same<K, double>::value) {
+            const uint32_t abase = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) K *)As;
+            const uint32_t bbase = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) K *)Bs;
+            StepOps o[2];
+            lds_step<0>(o[0], abase, bbase);
+            chunk_steps<0>(acc, o, abase, bbase);
+        } else {
 #pragma unroll 2
-        for (int k = 0; k < KC; ++k) {
-            K a[TR], b[TC];
+            for (int k = 0; k < KC; ++k) {
+                K a[TR], b[TC];
 #pragma unroll
-            for (int i = 0; i < TR; ++i) a[i] = As[(ty * TR + i) * KC + (k ^ sw)];
+                for (int i = 0; i < TR; ++i) a[i] = As[i * KC + k];
 #pragma unroll
-            for (int j = 0; j < TC; ++j) b[j] = Bs[k * B + tx + 16 * j];
+                for (int j = 0; j < TC; ++j) b[j] = Bs[k * B + 16 * j];
 #pragma unroll
-            for (int i = 0; i < TR; ++i) relax_row8<K>(acc[i], a[i], b);
+                for (int i = 0; i < TR; ++i) relax_row8<K>(acc[i], a[i], b);
+            }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
