@@ -1,18 +1,23 @@
 #!/bin/bash
-# Round profile: default bench (JSON line), rocprofv3 kernel-trace stats of the
-# same command, and HBM traffic PMC passes (FETCH_SIZE, WRITE_SIZE separately).
-# usage: bash tools/profile_round.sh rNN
+# Round profile of one bench config: the bench JSON line (with the CPU
+# baseline), rocprofv3 kernel-trace stats of the same command, and HBM-traffic
+# PMC passes (FETCH_SIZE and WRITE_SIZE in separate runs, MI355X_MICROARCH.md
+# HBM section).  Summarise with tools/summarize_profile.py.
+# usage: bash tools/profile_round.sh TAG [bench args...]
 set -o pipefail
 TAG=${1:-r01}
+shift
 export TMPDIR=/tmp
-R=$GRAFT_REPO_ROOT
+R=${GRAFT_REPO_ROOT:-$PWD}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
-timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err; echo "bench rc=$?"
-tail -1 $O/bench.json
+timeout -k 10 400 python -u bench.py "$@" > $O/bench.json 2> $O/bench.err; rc=$?
+echo "bench rc=$rc"; tail -1 $O/bench.json | cut -c1-400; [ $rc -eq 0 ] || exit $rc
 cd /tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $R/bench.py > $O/trace.log 2>&1; echo "trace rc=$?"
-timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > $O/pmc_fetch.log 2>&1; echo "fetch rc=$?"
-timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > $O/pmc_write.log 2>&1; echo "write rc=$?"
-ls -R $O | head -30
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $R/bench.py "$@" --no-cpu-baseline > $O/trace.log 2>&1; rc=$?
+echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- python3 $R/bench.py "$@" --steps 1 --warmup 0 --no-cpu-baseline > $O/pmc_fetch.log 2>&1; rc=$?
+echo "fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- python3 $R/bench.py "$@" --steps 1 --warmup 0 --no-cpu-baseline > $O/pmc_write.log 2>&1; rc=$?
+echo "write rc=$rc"

@@ -1,0 +1,87 @@
+"""Condense one tools/profile_round.sh output directory into the files kept
+under profiles/ (committed; gpurun_out/ is scratch):
+
+  profiles/<tag>_bench.json          the bench JSON line
+  profiles/<tag>_kernel_stats.csv    rocprofv3 --kernel-trace --stats summary
+  profiles/<tag>_pmc_traffic.json    FETCH_SIZE / WRITE_SIZE per dispatch of
+                                     every kernel (bench.py reads the dominant
+                                     kernel's entry as roofline.traffic)
+
+usage: python tools/summarize_profile.py gpurun_out/<tag> <tag> "<config text>"
+"""
+import csv
+import collections
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+LABELS = {
+    "minplus_glds_kernel<double, 0>": "phase 3 rest",
+    "minplus_glds_kernel<double, 4>": "phase 3 cross",
+    "minplus_glds_kernel<double, 1>": "phase 2 row",
+    "minplus_glds_kernel<double, 2>": "phase 2 col",
+    "minplus_tile_kernel<double, 0>": "phase 3 rest",
+    "sssp_sweep_kernel": "sssp_sweep",
+    "decide_kernel": "packet decide",
+    "draw_kernel": "packet draw",
+}
+
+
+def short(name):
+    n = name
+    for pre in ("(anonymous namespace)::", "void ", "srt::"):
+        n = n.replace(pre, "")
+    return n.split("(")[0].strip()
+
+
+def pmc(path, counter):
+    per = collections.defaultdict(float)
+    disp = collections.defaultdict(set)
+    for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            k = short(r["Kernel_Name"])
+            per[k] += float(r["Counter_Value"])
+            disp[k].add(r["Dispatch_Id"])
+    return {k: (v, len(disp[k])) for k, v in per.items()}
+
+
+def main():
+    src, tag, config = sys.argv[1], sys.argv[2], sys.argv[3]
+    out = os.path.join(ROOT, "profiles")
+    os.makedirs(out, exist_ok=True)
+    bench = open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1]
+    json.loads(bench)
+    open(os.path.join(out, f"{tag}_bench.json"), "w").write(bench + "\n")
+    stats = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)
+    if stats:
+        shutil.copy(stats[0], os.path.join(out, f"{tag}_kernel_stats.csv"))
+    fetch, write = pmc(os.path.join(src, "pmc_fetch"), "FETCH_SIZE"), pmc(os.path.join(src, "pmc_write"), "WRITE_SIZE")
+    kernels = {}
+    for k in sorted(set(fetch) | set(write)):
+        fkb, fn = fetch.get(k, (0.0, 1))
+        wkb, wn = write.get(k, (0.0, 1))
+        label = next((v for p, v in LABELS.items() if k.startswith(p)), None)
+        key = f"{k} ({label})" if label else k
+        kernels[key] = {"dispatches": max(fn, wn), "FETCH_SIZE_KB_per_launch": fkb / max(fn, 1),
+                        "WRITE_SIZE_KB_per_launch": wkb / max(wn, 1),
+                        "hbm_bytes_per_launch": 1024.0 * (fkb / max(fn, 1) + wkb / max(wn, 1))}
+    doc = {"round": tag, "config": config,
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (MI355X_MICROARCH.md "
+                     "HBM section), KB per dispatch averaged over the dispatches of each kernel.  Raw counter "
+                     "values: the guide's x2 FETCH_SIZE correction applies to 16-B/lane streams; the FW tile "
+                     "kernels' HBM reads are the 8-B/lane C-tile loads (calibrated 1:1 in r01: FETCH_SIZE of the "
+                     "rest kernel == 126^2 x 128 KB of C tiles) while their 16-B/lane LDS-DMA panel loads are "
+                     "served by L2 / Infinity Cache, so no correction is applied.",
+           "kernels": kernels}
+    json.dump(doc, open(os.path.join(out, f"{tag}_pmc_traffic.json"), "w"), indent=1)
+    print(json.dumps({k: round(v["hbm_bytes_per_launch"] / 1e6, 2) for k, v in kernels.items()}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
