@@ -361,10 +361,17 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         // once for 64*R sources), and as many groups in flight as ~256 MB of
         // path state allows (Infinity Cache sized), never more than the rows need
         const uint32_t words = std::max<uint32_t>(1, (n + 63) / 64);
-        // tuning knobs (measurement only): SRT_SSSP_R in {1,2,4}, SRT_SSSP_MB budget
-        uint32_t rmax = 1;
+        // Many groups in flight amortise each sweep's launch and latency chain
+        // and the convergence tail (C4, measured: 192 MB of path state 3.0 s,
+        // 1.6 GB 1.73 s, 6.4 GB 1.53 s, 12.8 GB 1.49 s), capped at 1/8 of the
+        // free HBM.  Tuning knobs (measurement only): SRT_SSSP_R in {1,2,4},
+        // SRT_SSSP_MB = path-state budget.
+        uint32_t rmax = 4;
         if (const char *e = std::getenv("SRT_SSSP_R")) rmax = (uint32_t)std::atoi(e);
-        uint64_t budget_mb = 192;
+        uint64_t budget_mb = 6400;
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b)
+            budget_mb = std::max<uint64_t>(64, std::min<uint64_t>(budget_mb, (free_b >> 20) / 8));
         if (const char *e = std::getenv("SRT_SSSP_MB")) budget_mb = (uint64_t)std::atoll(e);
         const uint32_t R = (rmax >= 4 && words >= 4) ? 4 : (rmax >= 2 && words >= 2) ? 2 : 1;
         const uint64_t per_group = (uint64_t)p->V * 64 * 8 * R;

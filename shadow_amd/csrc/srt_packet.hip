@@ -43,9 +43,17 @@ __global__ void draw_kernel(const srt_pkt *__restrict__ pkts, const uint32_t *__
     uint64_t s0 = rng[4 * (uint64_t)h], s1 = rng[4 * (uint64_t)h + 1];
     uint64_t s2 = rng[4 * (uint64_t)h + 2], s3 = rng[4 * (uint64_t)h + 3];
     const uint32_t b = host_ptr[h], e = host_ptr[h + 1];
-    for (uint32_t p = b; p < e; ++p) {
-        if (pkts[p].t_ns >= sim_end) continue;  // completed: no draw
-        draws[p] = xoshiro_next(s0, s1, s2, s3);
+    // send times are fetched 8 at a time (independent loads in flight) so the
+    // sequential state walk is not one memory latency per packet
+    for (uint32_t p0 = b; p0 < e; p0 += 8) {
+        uint64_t tt[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) tt[q] = p0 + q < e ? pkts[p0 + q].t_ns : 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            if (p0 + q >= e || tt[q] >= sim_end) continue;  // completed: no draw
+            draws[p0 + q] = xoshiro_next(s0, s1, s2, s3);
+        }
     }
     rng[4 * (uint64_t)h] = s0;
     rng[4 * (uint64_t)h + 1] = s1;
@@ -53,7 +61,9 @@ __global__ void draw_kernel(const srt_pkt *__restrict__ pkts, const uint32_t *__
     rng[4 * (uint64_t)h + 3] = s3;
 }
 
-__global__ void decide_kernel(const srt_pkt *__restrict__ pkts, uint64_t n_pkts,
+constexpr int DECIDE_THREADS = 256;
+
+__global__ __launch_bounds__(DECIDE_THREADS) void decide_kernel(const srt_pkt *__restrict__ pkts, uint64_t n_pkts,
                               const uint64_t *__restrict__ draws,
                               const uint64_t *__restrict__ lat, const float *__restrict__ loss,
                               uint32_t n, srt_round r, uint32_t *__restrict__ flags,
@@ -86,12 +96,25 @@ __global__ void decide_kernel(const srt_pkt *__restrict__ pkts, uint64_t n_pkts,
         flags[p] = f;
         deliver[p] = d;
     }
+    // wave, then block reduction: one pair of atomics per block (same-address
+    // atomics from every wave serialise at the memory-side atomic unit)
     for (int off = 32; off > 0; off >>= 1) {
         const unsigned long long a = __shfl_xor(min_lat, off), b = __shfl_xor(min_deliver, off);
         min_lat = a < min_lat ? a : min_lat;
         min_deliver = b < min_deliver ? b : min_deliver;
     }
-    if ((threadIdx.x & 63) == 0 && stats) {
+    __shared__ unsigned long long red[2][DECIDE_THREADS / 64];
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        red[0][w] = min_lat;
+        red[1][w] = min_deliver;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && stats) {
+        for (int k = 1; k < DECIDE_THREADS / 64; ++k) {
+            min_lat = red[0][k] < min_lat ? red[0][k] : min_lat;
+            min_deliver = red[1][k] < min_deliver ? red[1][k] : min_deliver;
+        }
         if (min_lat != ~0ull) atomicMin(&stats[0], min_lat);
         if (min_deliver != ~0ull) atomicMin(&stats[1], min_deliver);
     }
@@ -139,9 +162,9 @@ extern "C" srt_status srt_packet_batch(srt_plan *plan, const srt_pkt *d_pkts,
         hipLaunchKernelGGL(draw_kernel, dim3((n_hosts + 255) / 256), dim3(256), 0, s, d_pkts,
                            d_host_pkt_ptr, n_hosts, d_rng, round->sim_end_ns, plan->d_draws);
     if (n_pkts) {
-        uint64_t blocks = (n_pkts + 255) / 256;
-        if (blocks > 8192) blocks = 8192;
-        hipLaunchKernelGGL(decide_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, d_pkts, n_pkts,
+        uint64_t blocks = (n_pkts + DECIDE_THREADS - 1) / DECIDE_THREADS;
+        if (blocks > 2048) blocks = 2048;  // grid-stride: 8 blocks per CU
+        hipLaunchKernelGGL(decide_kernel, dim3((uint32_t)blocks), dim3(DECIDE_THREADS), 0, s, d_pkts, n_pkts,
                            plan->d_draws, plan->d_out_lat, plan->d_out_loss, plan->n, *round,
                            d_flags, d_deliver, (unsigned long long *)d_counters,
                            (unsigned long long *)d_stats);
