@@ -61,6 +61,10 @@ def parse_args():
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-sources", type=int, default=0, help="0 = auto (~10-30 s of CPU work)")
+    ap.add_argument("--emulate-ranks", dest="emulate_ranks", type=int, default=0,
+                    help="measurement only (dense FW, 1 GPU): time one rank of an N-rank run -- 1/N of the "
+                         "block-rows plus the pivot owner's chain every round, no collectives; the table "
+                         "is not valid and no bench line is printed, only the timing")
     return ap.parse_args()
 
 
@@ -179,12 +183,20 @@ def bench_graph(args, cfg, D):
                  f"{2 * len(src) / n_nodes:.1f} incl. self-loops), {len(nodes)} in use")
         data = "synthetic (seeded BA graph, latency U{1..300} ms, loss U[0,0.01])"
         og_args = (src, dst, lat, loss)
+    if args.emulate_ranks > 1:
+        os.environ["SRT_FW_EMULATE_RANKS"] = str(args.emulate_ranks)
     plan = RoutingPlan(g, nodes, device=D.dev)
     if D.world > 1:
         from shadow_amd import dist as sdist
         sdist.bind(plan, D.rank, D.world, D.local_rank, transport=os.environ.get("SRT_COMM", "rccl"))
     desc = plan.describe()
     elapsed, step_ms, k_ms, k_launches, k_work = timed_builds(plan, D, args.steps, args.warmup)
+    if args.emulate_ranks > 1:
+        print(json.dumps({"emulated_ranks": args.emulate_ranks, "config": args.config, "ms_per_step":
+                          elapsed * 1e3 / args.steps, "rest_ms_per_step": k_ms / args.steps,
+                          "rest_launches_per_step": k_launches // args.steps}), flush=True)
+        plan.close()
+        return None
     plan.fetch(table=False)  # connectivity check + min latency (not timed)
     n = len(nodes)
     out = None

@@ -353,6 +353,7 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     if (algo == SRT_ALGO_FW) {
         // tuning knob (measurement only): SRT_FW_STAGE=reg selects register staging
         if (const char *e = std::getenv("SRT_FW_STAGE")) p->fw_glds = std::strcmp(e, "reg") != 0;
+        if (const char *e = std::getenv("SRT_FW_EMULATE_RANKS")) p->emulate_ranks = (uint32_t)std::atoi(e);
         std::snprintf(d, sizeof d, "fw:%s B=%d g=%llu qb=%u s=%d V=%u n=%u stage=%s",
                       p->key_f64 ? "f64key" : "u64key", srt::FW_B, (unsigned long long)p->kp.g, p->kp.qb, p->kp.s,
                       p->V, n, p->fw_glds ? "glds" : "reg");

@@ -18,6 +18,7 @@
 // ops per relaxation) or as u64 (< 2^62: v_lshl_add_u64 + v_cmp_lt_u64 +
 // 2 v_cndmask = 4 ops).  Both give bit-identical tables; the host picks f64
 // whenever its bound proof fits in 53 bits.
+#include <cstdlib>
 #include <type_traits>
 
 #include "srt_internal.h"
@@ -163,6 +164,7 @@ template <typename K>
 __global__ __launch_bounds__(NT3, 2) void fw_phase1_kernel(K *__restrict__ D, uint32_t Vp, uint32_t kb) {
     __shared__ K rowbuf[2][B];
     __shared__ K colbuf[2][B];
+    __builtin_amdgcn_s_setprio(3);  // critical path of the look-ahead chain
     const int tid = threadIdx.x, tx = tid % 16, ty = tid / 16;
     const uint64_t k0 = (uint64_t)kb * B;
     K p[TR][TC];
@@ -433,6 +435,10 @@ __global__ __launch_bounds__(NT3, 2) void minplus_glds_kernel(K *__restrict__ D,
                                                            Rect r1, Rect r2) {
     static_assert(sizeof(K) == 8, "8-byte keys");
     __shared__ K lds[2 * GBUF];
+    // the look-ahead chain (phase 2 row/col, cross) shares SIMDs with the
+    // rest(kb) waves it overlaps: give it issue priority so the next round's
+    // pivot work, not the bulk update, sets the pace at high rank counts
+    if constexpr (TAG != 0) __builtin_amdgcn_s_setprio(2);
     const uint32_t n1 = r1.r.n * r1.c.n;
     uint32_t t = blockIdx.x, bi, bj;
     if (t < n1) {
@@ -517,6 +523,87 @@ __global__ __launch_bounds__(NT3, 2) void minplus_glds_kernel(K *__restrict__ D,
 #pragma unroll
         for (int j = 0; j < TC; ++j) dst[16 * j] = acc[i][j];
     }
+}
+
+// Latency-oriented variant for the look-ahead chain of the sharded schedule
+// (phase 2 row/col and cross): each 128x128 tile is split into four 64x64
+// quadrants, one 256-thread workgroup each (4x4 keys per thread), so a chain
+// launch finishes in about a quarter of a full tile's time when it is on the
+// critical path (8 ranks: the per-rank rest(kb) is only ~4 tile-waves).  In
+// phase 2 a quadrant reads the whole aliased pivot block-row/column while
+// sibling quadrants update it: P* (x) R_mixed == P* (x) R_old because P* is
+// closed (P* (x) P* == P*) and min-plus is monotone, and 8-byte stores are
+// atomic, so the result is the same bits as the unsplit update.
+constexpr int SQ = 64;
+template <typename K, int TAG>
+__global__ __launch_bounds__(256) void minplus_small_kernel(K *__restrict__ D, uint32_t Vp, uint32_t kb, Rect r1,
+                                                          Rect r2) {
+    __shared__ K As[2][SQ][KC + 1];
+    __shared__ K Bs[2][KC][SQ];
+    __builtin_amdgcn_s_setprio(2);
+    const uint32_t n1 = r1.r.n * r1.c.n;
+    uint32_t t = blockIdx.x >> 2, bi, bj;
+    const uint32_t q = blockIdx.x & 3;
+    if (t < n1) {
+        bi = span_at(r1.r, t / r1.c.n);
+        bj = span_at(r1.c, t % r1.c.n);
+    } else {
+        t -= n1;
+        bi = span_at(r2.r, t / r2.c.n);
+        bj = span_at(r2.c, t % r2.c.n);
+    }
+    const uint64_t i0 = (uint64_t)bi * B + (q >> 1) * SQ, j0 = (uint64_t)bj * B + (q & 1) * SQ;
+    const uint64_t k0 = (uint64_t)kb * B;
+    const int tid = threadIdx.x, tx = tid % 16, ty = tid / 16;
+    K acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = D[(i0 + ty * 4 + i) * Vp + j0 + tx + 16 * j];
+    K ra[4], rb[4];
+    auto fetch = [&](int kc) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int e = tid + 256 * m;
+            ra[m] = D[(i0 + e / KC) * Vp + k0 + kc + e % KC];
+            rb[m] = D[(k0 + kc + e / SQ) * Vp + j0 + e % SQ];
+        }
+    };
+    auto stash = [&](int buf) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int e = tid + 256 * m;
+            As[buf][e / KC][e % KC] = ra[m];
+            Bs[buf][e / SQ][e % SQ] = rb[m];
+        }
+    };
+    fetch(0);
+    stash(0);
+    __syncthreads();
+    constexpr int NCH = B / KC;
+#pragma unroll 1
+    for (int ch = 0; ch < NCH; ++ch) {
+        const int cur = ch & 1;
+        if (ch + 1 < NCH) fetch((ch + 1) * KC);
+#pragma unroll 4
+        for (int k = 0; k < KC; ++k) {
+            K a[4], b[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = As[cur][ty * 4 + i][k];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b[j] = Bs[cur][k][tx + 16 * j];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = KeyOps<K>::kmin(acc[i][j], a[i] + b[j]);
+        }
+        if (ch + 1 < NCH) stash(cur ^ 1);  // the other buffer's readers passed the last barrier
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) D[(i0 + ty * 4 + i) * Vp + j0 + tx + 16 * j] = acc[i][j];
 }
 
 // ------------------------------------------------------------- extract
@@ -612,7 +699,10 @@ template <typename K, int TAG>
 void launch_tiles(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1, const Rect &r2) {
     const uint32_t n = r1.r.n * r1.c.n + r2.r.n * r2.c.n;
     if (!n) return;
-    if (p->fw_glds)
+    if (TAG != 0 && p->fw_small_chain)  // sharded look-ahead chain: quarter tiles, lower latency
+        hipLaunchKernelGGL((minplus_small_kernel<K, TAG>), dim3(4 * n), dim3(256), 0, s,
+                           reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2);
+    else if (p->fw_glds)
         hipLaunchKernelGGL((minplus_glds_kernel<K, TAG>), dim3(n), dim3(NT3), 0, s,
                            reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2);
     else
@@ -633,12 +723,18 @@ template <typename K>
 srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
     K *D = reinterpret_cast<K *>(p->d_D);
     const uint32_t nblk = p->Vp / B;
-    const uint32_t rb0 = p->rb0, rb1 = p->rb1;
+    // measurement-only emulation of one rank of an N-rank run on one GPU
+    // (SRT_FW_EMULATE_RANKS): local rows = 1/N of the block-rows, and this
+    // rank plays the owner of every pivot (p1 + p2row each round: the longest
+    // per-round chain any rank has), no collectives -- the table is not valid
+    const uint32_t emu = (!p->comm && p->emulate_ranks > 1) ? p->emulate_ranks : 0;
+    const uint32_t rb0 = p->rb0, rb1 = emu ? std::max<uint32_t>(1, nblk / emu) : p->rb1;
     const bool sharded = p->comm != nullptr;  // a 1-rank comm runs the same schedule (tested)
+    p->fw_small_chain = (sharded || emu) && !std::getenv("SRT_FW_NO_SMALL_CHAIN");  // knob: A/B timing
     const uint32_t per_rank = sharded ? nblk / p->comm->nranks : nblk;
     const size_t pivot_bytes = (size_t)B * p->Vp * sizeof(K);
     hipStream_t M = p->stream, S = p->side_stream;
-    auto own = [&](uint32_t b) { return b >= rb0 && b < rb1; };
+    auto own = [&](uint32_t b) { return emu ? true : (b >= rb0 && b < rb1); };
     const Rect none{make_span(0, 0), make_span(0, 0)};
     p->p3_launches = 0;
     p->p3_work = 0.0;

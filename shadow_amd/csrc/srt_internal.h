@@ -72,6 +72,8 @@ struct srt_plan {
     srt::KeyParams kp{};
     bool key_f64 = false;  // f64-encoded keys (exact integers < 2^53)
     bool fw_glds = true;   // FW tiles staged by LDS-DMA (false: register staging)
+    bool fw_small_chain = false;  // quarter-tile kernels for the look-ahead chain (sharded)
+    uint32_t emulate_ranks = 0;   // measurement only, see fw_rounds_t
     std::string desc;
     bool identity_nodes = false;
 
