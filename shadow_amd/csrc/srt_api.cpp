@@ -322,6 +322,22 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     // ~3e12 B/s.  AUTO takes the cheaper representable one.
     std::string why_fw, why_sssp;
     const bool fw_ok = choose_key_params(g, &p->kp, &p->key_f64, &why_fw);
+    if (fw_ok) {
+        // no parallel edges (every adjacency row lists each neighbour once):
+        // the FW init can store edge keys instead of atomic-min'ing them
+        std::vector<uint32_t> stamp(g->n_nodes, 0);
+        bool unique = true;
+        for (uint32_t u = 0; u < g->n_nodes && unique; ++u)
+            for (uint64_t k = g->row_ptr[u]; k < g->row_ptr[u + 1]; ++k) {
+                const uint32_t v = g->col[k];
+                if (stamp[v] == u + 1) {
+                    unique = false;
+                    break;
+                }
+                stamp[v] = u + 1;
+            }
+        p->fw_unique_edges = unique;
+    }
     uint64_t n_in = 0;
     const bool sssp_ok = sssp_params(g, &p->sssp_g, &n_in, &why_sssp);
     const uint32_t want = opts ? opts->algo : (uint32_t)SRT_ALGO_AUTO;

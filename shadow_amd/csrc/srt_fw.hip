@@ -122,7 +122,9 @@ __device__ __forceinline__ uint64_t edge_key(uint64_t lat, float loss, const Key
 // D[u][v] = min over parallel edges u->v (one wave per graph row).  The
 // diagonal keeps 0: a self-loop never shortens a path, and the table's
 // diagonal is the raw self-loop written by the extract kernel (mod.rs:210-217).
-template <typename K>
+// UNIQUE (host-checked: no parallel edges) stores the key instead of the
+// memory-side atomic min (16k complete graph: 2.5 ms -> one plain store pass).
+template <typename K, bool UNIQUE>
 __global__ void scatter_edges_kernel(K *__restrict__ D, uint32_t Vp,
                                      const uint64_t *__restrict__ row_ptr,
                                      const uint32_t *__restrict__ col,
@@ -147,7 +149,10 @@ __global__ void scatter_edges_kernel(K *__restrict__ D, uint32_t Vp,
             } else {
                 bits = key;
             }
-            atomicMin((unsigned long long *)&D[(uint64_t)u * Vp + v], (unsigned long long)bits);
+            if constexpr (UNIQUE)
+                reinterpret_cast<uint64_t *>(D)[(uint64_t)u * Vp + v] = bits;
+            else
+                atomicMin((unsigned long long *)&D[(uint64_t)u * Vp + v], (unsigned long long)bits);
         }
     }
 }
@@ -691,8 +696,12 @@ template <typename K>
 void fw_init_t(srt_plan *p) {
     K *D = reinterpret_cast<K *>(p->d_D);
     hipLaunchKernelGGL(fill_kernel<K>, dim3(4096), dim3(256), 0, p->stream, D, p->Vp);
-    hipLaunchKernelGGL(scatter_edges_kernel<K>, dim3(2048), dim3(256), 0, p->stream, D, p->Vp,
-                       p->d_row_ptr, p->d_col, p->d_lat, p->d_loss, p->V, p->kp);
+    if (p->fw_unique_edges)
+        hipLaunchKernelGGL((scatter_edges_kernel<K, true>), dim3(2048), dim3(256), 0, p->stream, D, p->Vp,
+                           p->d_row_ptr, p->d_col, p->d_lat, p->d_loss, p->V, p->kp);
+    else
+        hipLaunchKernelGGL((scatter_edges_kernel<K, false>), dim3(2048), dim3(256), 0, p->stream, D, p->Vp,
+                           p->d_row_ptr, p->d_col, p->d_lat, p->d_loss, p->V, p->kp);
 }
 
 template <typename K, int TAG>
