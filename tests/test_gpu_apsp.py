@@ -167,3 +167,38 @@ def test_c2_scale_row_sample():
         exp_loss[r] = t.packet_loss[r, r]
         assert np.array_equal(L[r], exp_lat)
         assert np.abs(t.packet_loss[r].astype(np.float64) - exp_loss).max() <= LOSS_TOL
+
+
+def test_u64_key_path_large_latencies():
+    """Latencies up to ~2^44 ns on a sparse graph: the f64 key bound (53 bits)
+    fails and the closure runs on u64 keys (the LDS-DMA tile kernel's integer
+    branch); latency stays bit-exact."""
+    n = 150
+    src, dst, lat, loss = synth.random_graph(n, 31, p_edge=0.05, lat_range_ns=(1, 2**44))
+    g = NetworkGraph.from_edges(n, src, dst, lat, loss)
+    from shadow_amd.plan import RoutingPlan
+    plan = RoutingPlan(g, np.arange(n, dtype=np.uint32), algo=_lib.SRT_ALGO_FW)
+    assert "u64key" in plan.describe()
+    plan.close()
+    _check((src, dst, lat, loss), np.arange(n, dtype=np.uint32), False, n, algo=_lib.SRT_ALGO_FW)
+
+
+@pytest.mark.parametrize("algo", [_lib.SRT_ALGO_FW, _lib.SRT_ALGO_SSSP])
+def test_empty_in_use_set(algo):
+    # compute_shortest_paths(&[]) -> empty map, no panic (mod.rs:219: 0 == 0)
+    src, dst, lat, loss = synth.random_graph(20, 3)
+    g = NetworkGraph.from_edges(20, src, dst, lat, loss)
+    t = g.compute_shortest_paths(np.zeros(0, np.uint32), algo=algo)
+    assert t.latency_ns.shape == (0, 0) and len(t) == 0
+
+
+def test_isolated_unused_nodes_are_fine():
+    # nodes outside the in-use set may be unreachable: only in-use pairs must connect
+    n = 80
+    src, dst, lat, loss = synth.random_graph(n, 8, p_edge=0.1)
+    keep = (src < 70) & (dst < 70)  # nodes 70..79 keep only their self-loops
+    sl = (src == dst) & (src >= 70)
+    m = keep | sl
+    nodes = np.arange(70, dtype=np.uint32)
+    for algo in (_lib.SRT_ALGO_FW, _lib.SRT_ALGO_SSSP):
+        _check((src[m], dst[m], lat[m], loss[m]), nodes, False, n, algo=algo)
