@@ -170,11 +170,12 @@ def test_c2_scale_row_sample():
 
 
 def test_u64_key_path_large_latencies():
-    """Latencies up to ~2^44 ns on a sparse graph: the f64 key bound (53 bits)
-    fails and the closure runs on u64 keys (the LDS-DMA tile kernel's integer
-    branch); latency stays bit-exact."""
-    n = 150
-    src, dst, lat, loss = synth.random_graph(n, 31, p_edge=0.05, lat_range_ns=(1, 2**44))
+    """Latencies up to 2^31 ns (~2 s, no common unit) on a 20-node sparse graph:
+    the latency field needs 37 bits, so the f64 key (53 bits) has no room for
+    a 2^-24 loss resolution and the closure runs on u64 keys (the LDS-DMA tile
+    kernel's integer branch); latency stays bit-exact."""
+    n = 20
+    src, dst, lat, loss = synth.random_graph(n, 31, p_edge=0.3, lat_range_ns=(1, 2**31), loss_max=0.01)
     g = NetworkGraph.from_edges(n, src, dst, lat, loss)
     from shadow_amd.plan import RoutingPlan
     plan = RoutingPlan(g, np.arange(n, dtype=np.uint32), algo=_lib.SRT_ALGO_FW)
