@@ -9,10 +9,15 @@
 // Validation: ShadowNode/ShadowEdge::try_from (src/main/network/graph/mod.rs:28-111),
 // edge endpoints looked up by GML id (mod.rs:164-175, last node with an id wins),
 // Time units (src/main/utility/units.rs:405-439) converted to ns.
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <string>
+#include <thread>
 #include <string_view>
 #include <unordered_map>
 #include <vector>
@@ -49,6 +54,9 @@ struct KV {
 class Lexer {
    public:
     explicit Lexer(std::string_view t) : p_(t.data()), e_(t.data() + t.size()), b_(t.data()) {}
+    // sub-range [b, e) of t; error offsets stay relative to t
+    Lexer(std::string_view t, size_t b, size_t e) : p_(t.data() + b), e_(t.data() + e), b_(t.data()) {}
+    size_t pos() const { return (size_t)(p_ - b_); }
 
     [[noreturn]] void fail(const char *what) {
         throw Fail{std::string(what) + " at byte " + std::to_string(p_ - b_)};
@@ -137,8 +145,62 @@ class Lexer {
                     }
                     while (q < e_ && digit(*q)) ++q;
                 }
-                std::string tok(p_, (size_t)(q - p_));
-                const float f = std::strtof(tok.c_str(), nullptr);
+                // Fast exact path: no exponent and at most 2^24 as an integer
+                // d with k fraction digits -> d / 10^k in f32.  Both operands are
+                // exact f32 values (d < 2^24, 10^k for k <= 10) and IEEE division
+                // rounds correctly, so this is strtof's correctly rounded result.
+                {
+                    const char *r = p_;
+                    const bool neg = *r == '-';
+                    if (*r == '+' || *r == '-') ++r;
+                    uint64_t d = 0;
+                    int k = 0, nd = 0;
+                    bool frac = false, fast = true;
+                    for (; r < q; ++r) {
+                        if (*r == '.') {
+                            frac = true;
+                            continue;
+                        }
+                        if (!digit(*r)) {
+                            fast = false;  // exponent
+                            break;
+                        }
+                        d = d * 10 + (uint64_t)(*r - '0');
+                        if (d) ++nd;
+                        if (frac) ++k;
+                        if (nd > 9) {
+                            fast = false;
+                            break;
+                        }
+                    }
+                    if (fast && d < (1u << 24) && k <= 10) {
+                        static const float p10[11] = {1e0f, 1e1f, 1e2f, 1e3f, 1e4f, 1e5f,
+                                                      1e6f, 1e7f, 1e8f, 1e9f, 1e10f};
+                        float f = (float)d / p10[k];
+                        if (neg) f = -f;
+                        p_ = q;
+                        if (newline()) {
+                            v->t = VT::Float;
+                            v->f = f;
+                            return true;
+                        }
+                        p_ = save;
+                        goto string_alt;
+                    }
+                }
+                // strtof needs a terminated copy; short tokens stay on the stack
+                const size_t tl = (size_t)(q - p_);
+                char sbuf[64];
+                std::string big;
+                const char *tok = sbuf;
+                if (tl < sizeof sbuf) {
+                    std::memcpy(sbuf, p_, tl);
+                    sbuf[tl] = 0;
+                } else {
+                    big.assign(p_, tl);
+                    tok = big.c_str();
+                }
+                const float f = std::strtof(tok, nullptr);
                 p_ = q;
                 if (newline()) {
                     v->t = VT::Float;
@@ -148,6 +210,7 @@ class Lexer {
                 p_ = save;
             }
         }
+    string_alt:
         if (p_ < e_ && *p_ == '"') {  // string: non-empty run of non-'"' bytes
             const char *b = p_ + 1, *q = b;
             while (q < e_ && *q != '"') ++q;
@@ -178,6 +241,21 @@ class Lexer {
         if (!newline()) fail("expected a newline");
     }
     bool at_end() const { return p_ >= e_; }
+    // a block whose '[' is at p_ and whose ']' is the last byte of the range:
+    // the same grammar as block() without the leading sp0 and trailing newline
+    bool block_body(std::vector<KV> *kvs) {
+        if (!tag('[') || !newline()) return false;
+        while (!tag(']')) {
+            KV kv;
+            if (!key(&kv.k) || !value(&kv.v)) return false;
+            kvs->push_back(kv);
+        }
+        if (p_ != e_) return false;
+        for (size_t i = 0; i < kvs->size(); ++i)
+            for (size_t j = i + 1; j < kvs->size(); ++j)
+                if ((*kvs)[i].k == (*kvs)[j].k) return false;
+        return true;
+    }
 
    private:
     const char *p_, *e_, *b_;
@@ -289,7 +367,181 @@ bool bits_per_sec_ok(std::string_view s) {  // BitsPerSec<SiPrefixUpper>
     return parse_u64(v, &x);
 }
 
-void do_parse(std::string_view text, srt_gml *g) {
+// ---------------------------------------------------------------------------
+// Parallel ingest.  A Shadow graph at config C3 scale is ~1.3e8 edge blocks
+// (~12 GB of text), so parsing is split into segments that tile the text:
+//   gap segments   -- top-level items between blocks, ending with the key
+//                     ("node"/"edge") that opens the next block;
+//   block segments -- "[" ... "]" of one node or edge.
+// Block boundaries are the '[' / ']' bytes outside strings; string state at
+// every byte comes from the parity of '"' before it (chunk-parallel count +
+// prefix, then a chunk-parallel scan for structural bytes).  In valid GML a
+// '"' only delimits string values and '[' ']' outside strings only delimit
+// blocks, so every segment then parses with the exact sequential grammar of
+// the Lexer; any input the segment parsers reject (including inputs whose
+// stray quotes fool the parity) is re-parsed sequentially, which yields the
+// reference-order error.  Syntax errors anywhere take precedence over
+// node/edge validation (gml_parser::parse runs before NetworkGraph::parse),
+// then nodes are validated in order, then edges (first failing edge wins).
+
+struct EdgeRec {
+    int32_t s = 0, t = 0;
+    uint64_t ns = 0;
+    float loss = 0.f;
+    uint8_t err = 0;   // first failing ShadowEdge::try_from check (0 = ok)
+    uint8_t sub = 0;   // which Time error text
+};
+
+const char *time_err_text(uint8_t sub) {
+    switch (sub) {
+        case 1: return "Unable to identify value and unit";
+        case 2: return "Unit was not one of (ns|nanosecond|...|h|hr|hrs|hour|hours)";
+        case 3: return "invalid digit found in string";
+        default: return "The resulting value is outside of the bounds";
+    }
+}
+uint8_t time_err_code(const char *e) {
+    if (!std::strcmp(e, time_err_text(1))) return 1;
+    if (!std::strcmp(e, time_err_text(2))) return 2;
+    if (!std::strcmp(e, time_err_text(3))) return 3;
+    return 4;
+}
+
+// ShadowEdge::try_from (mod.rs:72-111) on one parsed block, minus the id
+// lookups (done once every node is known)
+EdgeRec check_edge(const std::vector<KV> &b) {
+    EdgeRec r;
+    const Val *s = get(b, "source"), *t = get(b, "target");
+    if (s && s->t != VT::Int) return r.err = 1, r;
+    if (!s) return r.err = 2, r;
+    if (t && t->t != VT::Int) return r.err = 3, r;
+    if (!t) return r.err = 4, r;
+    r.s = s->i;
+    r.t = t->i;
+    const Val *lat = get(b, "latency");
+    if (!lat) return r.err = 5, r;
+    if (lat->t != VT::Str) return r.err = 6, r;
+    uint64_t v = 0;
+    if (const char *e = parse_time(lat->s, &r.ns, &v)) return r.err = 7, r.sub = time_err_code(e), r;
+    if (const Val *j = get(b, "jitter")) {
+        if (j->t != VT::Str) return r.err = 8, r;
+        uint64_t jn, jv;
+        if (const char *e = parse_time(j->s, &jn, &jv)) return r.err = 9, r.sub = time_err_code(e), r;
+    }
+    if (const Val *pl = get(b, "packet_loss")) {
+        if (pl->t != VT::Float) return r.err = 10, r;
+        r.loss = pl->f;
+    }
+    if (r.loss < 0.f || r.loss > 1.f) return r.err = 11, r;
+    if (v == 0) return r.err = 12, r;
+    return r;
+}
+
+std::string edge_err_text(const EdgeRec &r) {
+    switch (r.err) {
+        case 1: return "Incorrect 'source' type";
+        case 2: return "'source' doesn't exist";
+        case 3: return "Incorrect 'target' type";
+        case 4: return "'target' doesn't exist";
+        case 5: return "Edge 'latency' was not provided";
+        case 6: return "Edge 'latency' is not a string";
+        case 7: return std::string("Edge 'latency' is not a valid unit: ") + time_err_text(r.sub);
+        case 8: return "Edge 'jitter' is not a string";
+        case 9: return std::string("Edge 'jitter' is not a valid unit: ") + time_err_text(r.sub);
+        case 10: return "Edge 'packet_loss' is not a float";
+        case 11: return "Edge 'packet_loss' is not in the range [0,1]";
+        case 12: return "Edge 'latency' must not be 0";
+        case 13: return "Edge source " + std::to_string((uint32_t)r.s) + " doesn't exist";
+        default: return "Edge target " + std::to_string((uint32_t)r.t) + " doesn't exist";
+    }
+}
+
+// ShadowNode::try_from (mod.rs:28-60)
+void check_node(const std::vector<KV> &n, uint32_t *id_out) {
+    const Val *id = get(n, "id");
+    if (id && id->t != VT::Int) throw Fail{"Incorrect 'id' type"};
+    if (!id) throw Fail{"Node 'id' was not provided"};
+    for (const char *bw : {"host_bandwidth_down", "host_bandwidth_up"}) {
+        const Val *x = get(n, bw);
+        if (!x) continue;
+        if (x->t != VT::Str) throw Fail{std::string("Node '") + bw + "' is not a string"};
+        if (!bits_per_sec_ok(x->s)) throw Fail{std::string("Node '") + bw + "' is not a valid unit"};
+    }
+    *id_out = (uint32_t)id->i;
+}
+
+template <typename F>
+void parallel_for(size_t n, unsigned T, F &&f);
+
+// petgraph adjacency: outgoing (reverse insertion), then for undirected the
+// incoming list (reverse insertion, self-loops skipped).  Edges are cut into T
+// contiguous chunks; per-chunk row counts give every chunk its own write
+// offsets (chunk T-1 first, since the order is reverse insertion), so the
+// fill runs in parallel and lands exactly where the sequential fill would.
+void build_csr(srt_gml *g, size_t V, const std::vector<uint32_t> &es, const std::vector<uint32_t> &ed,
+               const std::vector<uint64_t> &el, const std::vector<float> &eo, unsigned T = 1) {
+    const size_t m = es.size();
+    if (m < 4 * (size_t)T || T < 2) T = 1;
+    const bool und = !g->directed;
+    std::vector<uint64_t> co((size_t)T * V, 0), ci(und ? (size_t)T * V : 0, 0);
+    parallel_for(T, T, [&](size_t b, size_t e, unsigned) {
+        for (size_t t = b; t < e; ++t)
+            for (size_t i = m * t / T; i < m * (t + 1) / T; ++i) {
+                co[t * V + es[i]]++;
+                if (und && es[i] != ed[i]) ci[t * V + ed[i]]++;
+            }
+    });
+    g->row_ptr.assign(V + 1, 0);
+    std::vector<uint64_t> out_tot(V, 0);
+    for (size_t v = 0; v < V; ++v) {
+        uint64_t o = 0, in = 0;
+        for (unsigned t = 0; t < T; ++t) o += co[t * V + v], in += und ? ci[t * V + v] : 0;
+        out_tot[v] = o;
+        g->row_ptr[v + 1] = g->row_ptr[v] + o + in;
+    }
+    // start offsets: outgoing of chunk t in row v after the chunks t' > t
+    parallel_for(V, T, [&](size_t b, size_t e, unsigned) {
+        for (size_t v = b; v < e; ++v) {
+            uint64_t o = g->row_ptr[v], in = g->row_ptr[v] + out_tot[v];
+            for (unsigned t = T; t-- > 0;) {
+                const uint64_t c = co[t * V + v];
+                co[t * V + v] = o;
+                o += c;
+                if (und) {
+                    const uint64_t d = ci[t * V + v];
+                    ci[t * V + v] = in;
+                    in += d;
+                }
+            }
+        }
+    });
+    const size_t A = g->row_ptr[V];
+    g->col.resize(A);
+    g->lat.resize(A);
+    g->loss.resize(A);
+    parallel_for(T, T, [&](size_t b, size_t e, unsigned) {
+        for (size_t t = b; t < e; ++t) {
+            for (size_t i = m * (t + 1) / T; i-- > m * t / T;) {
+                const uint64_t k = co[t * V + es[i]]++;
+                g->col[k] = ed[i];
+                g->lat[k] = el[i];
+                g->loss[k] = eo[i];
+            }
+            if (und)
+                for (size_t i = m * (t + 1) / T; i-- > m * t / T;) {
+                    if (es[i] == ed[i]) continue;
+                    const uint64_t k = ci[t * V + ed[i]]++;
+                    g->col[k] = es[i];
+                    g->lat[k] = el[i];
+                    g->loss[k] = eo[i];
+                }
+        }
+    });
+}
+
+// Sequential reference path (small inputs, and the exact error for anything
+// the parallel path rejects).
+void parse_sequential(std::string_view text, srt_gml *g) {
     Lexer L(text);
     L.msp0();
     if (!L.tag(std::string_view("graph"))) L.fail("expected 'graph'");
@@ -329,82 +581,265 @@ void do_parse(std::string_view text, srt_gml *g) {
     id_map.reserve(nodes.size() * 2);
     g->ids.resize(nodes.size());
     for (size_t i = 0; i < nodes.size(); ++i) {
-        const Val *id = get(nodes[i], "id");
-        if (id && id->t != VT::Int) throw Fail{"Incorrect 'id' type"};
-        if (!id) throw Fail{"Node 'id' was not provided"};
-        for (const char *bw : {"host_bandwidth_down", "host_bandwidth_up"}) {
-            const Val *x = get(nodes[i], bw);
-            if (!x) continue;
-            if (x->t != VT::Str) throw Fail{std::string("Node '") + bw + "' is not a string"};
-            if (!bits_per_sec_ok(x->s)) throw Fail{std::string("Node '") + bw + "' is not a valid unit"};
-        }
-        g->ids[i] = (uint32_t)id->i;
-        id_map[(uint32_t)id->i] = (uint32_t)i;
+        check_node(nodes[i], &g->ids[i]);
+        id_map[g->ids[i]] = (uint32_t)i;
     }
     const size_t m = edges.size();
     std::vector<uint32_t> es(m), ed(m);
     std::vector<uint64_t> el(m);
     std::vector<float> eo(m);
     for (size_t i = 0; i < m; ++i) {
-        const auto &b = edges[i];
-        const Val *s = get(b, "source"), *t = get(b, "target");
-        if (s && s->t != VT::Int) throw Fail{"Incorrect 'source' type"};
-        if (!s) throw Fail{"'source' doesn't exist"};
-        if (t && t->t != VT::Int) throw Fail{"Incorrect 'target' type"};
-        if (!t) throw Fail{"'target' doesn't exist"};
-        const Val *lat = get(b, "latency");
-        if (!lat) throw Fail{"Edge 'latency' was not provided"};
-        if (lat->t != VT::Str) throw Fail{"Edge 'latency' is not a string"};
-        uint64_t ns = 0, v = 0;
-        if (const char *e = parse_time(lat->s, &ns, &v)) throw Fail{std::string("Edge 'latency' is not a valid unit: ") + e};
-        if (const Val *j = get(b, "jitter")) {
-            if (j->t != VT::Str) throw Fail{"Edge 'jitter' is not a string"};
-            uint64_t jn, jv;
-            if (const char *e = parse_time(j->s, &jn, &jv)) throw Fail{std::string("Edge 'jitter' is not a valid unit: ") + e};
+        EdgeRec r = check_edge(edges[i]);
+        if (!r.err) {
+            auto si = id_map.find((uint32_t)r.s), ti = id_map.find((uint32_t)r.t);
+            if (si == id_map.end()) r.err = 13;
+            else if (ti == id_map.end()) r.err = 14;
+            else es[i] = si->second, ed[i] = ti->second;
         }
-        float loss = 0.f;
-        if (const Val *pl = get(b, "packet_loss")) {
-            if (pl->t != VT::Float) throw Fail{"Edge 'packet_loss' is not a float"};
-            loss = pl->f;
+        if (r.err) throw Fail{edge_err_text(r)};
+        el[i] = r.ns;
+        eo[i] = r.loss;
+    }
+    build_csr(g, nodes.size(), es, ed, el, eo);
+}
+
+struct Bad {};  // the parallel path gives up: re-parse sequentially
+
+template <typename F>
+void parallel_for(size_t n, unsigned T, F &&f) {  // f(begin, end, thread)
+    if (T <= 1 || n < 2 * T) {
+        f((size_t)0, n, 0u);
+        return;
+    }
+    std::vector<std::thread> th;
+    std::vector<std::exception_ptr> ex(T);
+    for (unsigned t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            try {
+                f(n * t / T, n * (t + 1) / T, t);
+            } catch (...) {
+                ex[t] = std::current_exception();
+            }
+        });
+    for (auto &x : th) x.join();
+    for (auto &e : ex)
+        if (e) std::rethrow_exception(e);
+}
+
+void parse_parallel(std::string_view text, srt_gml *g, unsigned T) {
+    const bool timing = std::getenv("SRT_GML_TIMING") != nullptr;  // phase times to stderr
+    auto t_last = std::chrono::steady_clock::now();
+    auto tick = [&](const char *what) {
+        if (!timing) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[srt_gml] %-10s %8.3f s\n", what, std::chrono::duration<double>(now - t_last).count());
+        t_last = now;
+    };
+    Lexer H(text);
+    H.msp0();
+    if (!H.tag(std::string_view("graph"))) throw Bad{};
+    H.sp0();
+    if (!H.tag('[') || !H.newline()) throw Bad{};
+    const size_t h = H.pos(), N = text.size();
+    const char *base = text.data();
+    // 1. quote parity at chunk starts
+    const size_t nch = std::max<size_t>(1, std::min<size_t>(T * 8, (N - h) / (1 << 20) + 1));
+    std::vector<size_t> cb(nch + 1);
+    for (size_t c = 0; c <= nch; ++c) cb[c] = h + (N - h) * c / nch;
+    std::vector<uint64_t> quotes(nch);
+    parallel_for(nch, T, [&](size_t b, size_t e, unsigned) {
+        for (size_t c = b; c < e; ++c) quotes[c] = (uint64_t)std::count(base + cb[c], base + cb[c + 1], '"');
+    });
+    tick("quotes");
+    // 2. structural bytes ('[' / ']' outside strings) per chunk
+    std::vector<std::vector<uint64_t>> st(nch);
+    parallel_for(nch, T, [&](size_t b, size_t e, unsigned) {
+        for (size_t c = b; c < e; ++c) {
+            uint64_t q = 0;
+            for (size_t k = 0; k < c; ++k) q += quotes[k];
+            bool in_str = q & 1;
+            const char *p = base + cb[c], *end = base + cb[c + 1];
+            std::vector<uint64_t> &out = st[c];
+            while (p < end) {
+                const char x = *p;
+                if (x == '"') in_str = !in_str;
+                else if (!in_str && (x == '[' || x == ']')) out.push_back((uint64_t)(p - base));
+                ++p;
+            }
         }
-        if (loss < 0.f || loss > 1.f) throw Fail{"Edge 'packet_loss' is not in the range [0,1]"};
-        if (v == 0) throw Fail{"Edge 'latency' must not be 0"};
-        auto si = id_map.find((uint32_t)s->i), ti = id_map.find((uint32_t)t->i);
-        if (si == id_map.end()) throw Fail{"Edge source " + std::to_string((uint32_t)s->i) + " doesn't exist"};
-        if (ti == id_map.end()) throw Fail{"Edge target " + std::to_string((uint32_t)t->i) + " doesn't exist"};
-        es[i] = si->second;
-        ed[i] = ti->second;
-        el[i] = ns;
-        eo[i] = loss;
-    }
-    // petgraph adjacency: outgoing (reverse insertion), then for undirected the
-    // incoming list (reverse insertion, self-loops skipped)
-    const size_t V = nodes.size();
-    g->row_ptr.assign(V + 1, 0);
-    for (size_t i = 0; i < m; ++i) {
-        g->row_ptr[es[i] + 1]++;
-        if (!g->directed && es[i] != ed[i]) g->row_ptr[ed[i] + 1]++;
-    }
-    for (size_t v = 0; v < V; ++v) g->row_ptr[v + 1] += g->row_ptr[v];
-    const size_t A = g->row_ptr[V];
-    g->col.resize(A);
-    g->lat.resize(A);
-    g->loss.resize(A);
-    std::vector<uint64_t> fill(g->row_ptr.begin(), g->row_ptr.end() - 1);
-    for (size_t i = m; i-- > 0;) {
-        const uint64_t k = fill[es[i]]++;
-        g->col[k] = ed[i];
-        g->lat[k] = el[i];
-        g->loss[k] = eo[i];
-    }
-    if (!g->directed)
-        for (size_t i = m; i-- > 0;) {
-            if (es[i] == ed[i]) continue;
-            const uint64_t k = fill[ed[i]]++;
-            g->col[k] = es[i];
-            g->lat[k] = el[i];
-            g->loss[k] = eo[i];
+    });
+    tick("structure");
+    // 3. blocks.  In valid GML the structural bytes read "[ ] [ ] ... [ ] ]":
+    // block j = entries (2j, 2j+1) of the concatenated list and the graph's
+    // ']' is the first even entry that is a ']' (anything after it is trailing
+    // text).  Concatenate the chunk lists by prefix offsets, find that entry,
+    // check the alternation before it and pair the entries, chunk-parallel.
+    std::vector<size_t> off(nch + 1, 0);
+    for (size_t c = 0; c < nch; ++c) off[c + 1] = off[c] + st[c].size();
+    std::vector<uint64_t> E(off[nch]);
+    parallel_for(nch, T, [&](size_t b, size_t e, unsigned) {
+        for (size_t c = b; c < e; ++c) std::copy(st[c].begin(), st[c].end(), E.begin() + (ptrdiff_t)off[c]);
+    });
+    st.clear();
+    st.shrink_to_fit();
+    std::vector<size_t> first_close(T, SIZE_MAX);
+    std::vector<uint8_t> alt_bad(T, 0);
+    parallel_for(E.size(), T, [&](size_t b, size_t e, unsigned t) {
+        for (size_t i = b; i < e; ++i) {
+            const bool is_open = base[E[i]] == '[';
+            if ((i & 1) == 0 && !is_open) {
+                first_close[t] = i;
+                return;
+            }
+            if ((i & 1) == 1 && is_open) alt_bad[t] = 1;  // only matters before the graph's ']'
         }
+    });
+    size_t gi = SIZE_MAX;
+    unsigned tg = 0;
+    for (unsigned t = 0; t < T; ++t)
+        if (first_close[t] < gi) gi = first_close[t], tg = t;
+    if (gi == SIZE_MAX) throw Bad{};
+    // a nested '[' before the graph's ']' (threads past tg only saw trailing text)
+    for (unsigned t = 0; t < tg; ++t)
+        if (alt_bad[t]) throw Bad{};
+    for (size_t i = E.size() * tg / T; i < gi; ++i)
+        if ((i & 1) == 1 && base[E[i]] == '[') throw Bad{};
+    const uint64_t gend = E[gi];
+    const size_t nb = gi / 2;
+    std::vector<std::pair<uint64_t, uint64_t>> blocks(nb);
+    parallel_for(nb, T, [&](size_t b, size_t e, unsigned) {
+        for (size_t j = b; j < e; ++j) blocks[j] = {E[2 * j], E[2 * j + 1]};
+    });
+    E.clear();
+    E.shrink_to_fit();
+    tick("blocks");
+    // 4. parse gaps (before block i: [prev_end+1, blocks[i].first); the last
+    // gap ends at the graph's ']') and blocks, in parallel
+    std::vector<uint8_t> kind(nb);  // 1 node, 2 edge
+    std::vector<std::vector<KV>> gap_others(T), nodes_kv;
+    std::vector<int> gap_directed(T, 0);
+    std::vector<int> directed_val(T, -1);
+    std::vector<EdgeRec> recs;
+    std::vector<uint32_t> node_of(nb, UINT32_MAX);
+    // gaps first (they say which blocks are nodes), in order per thread
+    auto parse_gap = [&](size_t i, unsigned t) {  // gap before block i (i == nb: the tail)
+        const size_t b = i == 0 ? h : blocks[i - 1].second + 1;
+        const size_t e = i == nb ? gend : blocks[i].first;
+        Lexer L(text, b, e);
+        if (i > 0 && !L.newline()) throw Bad{};
+        for (;;) {
+            if (L.at_end()) {
+                if (i != nb) throw Bad{};
+                return;
+            }
+            std::string_view k;
+            if (!L.key(&k)) throw Bad{};
+            if (k == "node" || k == "edge") {
+                L.sp0();
+                if (i == nb || !L.at_end()) throw Bad{};
+                kind[i] = k == "node" ? 1 : 2;
+                return;
+            }
+            if (k == "directed") {
+                Val v;
+                if (!L.value(&v) || v.t != VT::Int || (v.i != 0 && v.i != 1)) throw Bad{};
+                gap_directed[t]++;
+                directed_val[t] = v.i;
+            } else {
+                KV kv{k, {}};
+                if (!L.value(&kv.v)) throw Bad{};
+                gap_others[t].push_back(kv);
+            }
+        }
+    };
+    parallel_for(nb + 1, T, [&](size_t b, size_t e, unsigned t) {
+        for (size_t i = b; i < e; ++i) parse_gap(i, t);
+    });
+    int ndirected = 0;
+    std::vector<KV> others;
+    for (unsigned t = 0; t < T; ++t) {
+        ndirected += gap_directed[t];
+        if (directed_val[t] >= 0) g->directed = directed_val[t] == 1;
+        others.insert(others.end(), gap_others[t].begin(), gap_others[t].end());
+    }
+    if (ndirected > 1) throw Bad{};
+    for (size_t i = 0; i < others.size(); ++i)
+        for (size_t j = i + 1; j < others.size(); ++j)
+            if (others[i].k == others[j].k) throw Bad{};
+    tick("gaps");
+    // node / edge numbering in file order
+    std::vector<uint32_t> idx(nb);
+    uint32_t nn = 0, ne = 0;
+    for (size_t i = 0; i < nb; ++i) idx[i] = kind[i] == 1 ? nn++ : ne++;
+    nodes_kv.resize(nn);
+    recs.resize(ne);
+    parallel_for(nb, T, [&](size_t b, size_t e, unsigned) {
+        std::vector<KV> kvs;
+        for (size_t i = b; i < e; ++i) {
+            Lexer L(text, blocks[i].first, blocks[i].second + 1);
+            kvs.clear();
+            if (!L.block_body(&kvs)) throw Bad{};
+            if (kind[i] == 1) nodes_kv[idx[i]] = kvs;
+            else recs[idx[i]] = check_edge(kvs);
+        }
+    });
+    tick("parse");
+    // 5. validation: nodes in order, then the first failing edge
+    std::unordered_map<uint32_t, uint32_t> id_map;
+    id_map.reserve((size_t)nn * 2);
+    g->ids.resize(nn);
+    for (uint32_t i = 0; i < nn; ++i) {
+        check_node(nodes_kv[i], &g->ids[i]);
+        id_map[g->ids[i]] = i;
+    }
+    nodes_kv.clear();
+    std::vector<uint32_t> es(ne), ed(ne);
+    std::vector<uint64_t> el(ne);
+    std::vector<float> eo(ne);
+    std::vector<size_t> first_bad(T, SIZE_MAX);
+    parallel_for(ne, T, [&](size_t b, size_t e, unsigned t) {
+        for (size_t i = b; i < e; ++i) {
+            EdgeRec &r = recs[i];
+            if (!r.err) {
+                auto si = id_map.find((uint32_t)r.s), ti = id_map.find((uint32_t)r.t);
+                if (si == id_map.end()) r.err = 13;
+                else if (ti == id_map.end()) r.err = 14;
+                else es[i] = si->second, ed[i] = ti->second;
+            }
+            if (r.err) {
+                first_bad[t] = std::min(first_bad[t], i);
+                return;
+            }
+            el[i] = r.ns;
+            eo[i] = r.loss;
+        }
+    });
+    const size_t fb = *std::min_element(first_bad.begin(), first_bad.end());
+    if (fb != SIZE_MAX) throw Fail{edge_err_text(recs[fb])};
+    recs.clear();
+    recs.shrink_to_fit();
+    tick("validate");
+    build_csr(g, nn, es, ed, el, eo, T);
+    tick("csr");
+}
+
+void do_parse(std::string_view text, srt_gml *g) {
+    unsigned T = std::thread::hardware_concurrency();
+    if (const char *e = std::getenv("SRT_GML_THREADS")) T = (unsigned)std::atoi(e);
+    T = std::max(1u, std::min(T, 16u));
+    size_t min_bytes = 16u << 20;  // below this the sequential parser is as fast
+    if (const char *e = std::getenv("SRT_GML_PAR_BYTES")) min_bytes = (size_t)std::atoll(e);
+    if (text.size() < min_bytes || T == 1) return parse_sequential(text, g);
+    try {
+        parse_parallel(text, g, T);
+    } catch (const Bad &) {
+        if (std::getenv("SRT_GML_STRICT_PARALLEL")) throw Fail{"parallel ingest rejected the input"};  // tests
+        *g = srt_gml();
+        parse_sequential(text, g);  // the exact reference-order error
+    } catch (const Fail &) {
+        *g = srt_gml();
+        parse_sequential(text, g);  // same error text, found in reference order
+    }
 }
 
 }  // namespace
