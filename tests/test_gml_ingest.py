@@ -114,3 +114,26 @@ def test_parallel_errors_match_sequential(k):
     with pytest.raises(_lib.SrtError) as e2:
         _parse(bad, parallel=True)
     assert str(e1.value) == str(e2.value)
+
+
+def test_float_fast_path_matches_strtof():
+    """packet_loss tokens of 1..9 significant digits, leading zeros, '+', '.5',
+    '1.' and exponent forms: the ingest's exact fast path (d / 10^k in f32)
+    and its strtof fallback must equal the oracle's strtof bit for bit."""
+    rng = np.random.default_rng(5)
+    toks = ["0", "1", "1.", ".5", "+0.25", "0.0", "1.0", "0.000001", "0.9999999", "0.99999999", "1e-3",
+            "2.5E-1", "0.1", "0.3", "0.7", "0.16777217", "0.16777216"]
+    for _ in range(400):
+        nd = int(rng.integers(1, 10))
+        digits = "".join(str(int(x)) for x in rng.integers(0, 10, nd))
+        lead = "0" * int(rng.integers(0, 4))
+        toks.append("0." + lead + digits)
+    lines = ["graph [", "  directed 1", "  node [", "    id 0", "  ]"]
+    for t in toks:
+        val = t if any(c in t for c in ".eE") else t + ".0"
+        lines.append(f'  edge [\n    source 0\n    target 0\n    latency "1 ns"\n    packet_loss {val}\n  ]')
+    text = "\n".join(lines) + "\n]\n"
+    og = O.gml_parse(text)
+    for par in (False, True):
+        g = _parse(text, parallel=par)
+        assert np.array_equal(np.sort(g.loss.view(np.uint32)), np.sort(og.loss.view(np.uint32)))
