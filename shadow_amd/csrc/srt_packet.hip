@@ -43,14 +43,15 @@ __global__ void draw_kernel(const srt_pkt *__restrict__ pkts, const uint32_t *__
     uint64_t s0 = rng[4 * (uint64_t)h], s1 = rng[4 * (uint64_t)h + 1];
     uint64_t s2 = rng[4 * (uint64_t)h + 2], s3 = rng[4 * (uint64_t)h + 3];
     const uint32_t b = host_ptr[h], e = host_ptr[h + 1];
-    // send times are fetched 8 at a time (independent loads in flight) so the
+    // send times are fetched 32 at a time (independent loads in flight) so the
     // sequential state walk is not one memory latency per packet
-    for (uint32_t p0 = b; p0 < e; p0 += 8) {
-        uint64_t tt[8];
+    constexpr int PF = 32;
+    for (uint32_t p0 = b; p0 < e; p0 += PF) {
+        uint64_t tt[PF];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) tt[q] = p0 + q < e ? pkts[p0 + q].t_ns : 0;
+        for (int q = 0; q < PF; ++q) tt[q] = p0 + q < e ? pkts[p0 + q].t_ns : 0;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
+        for (int q = 0; q < PF; ++q) {
             if (p0 + q >= e || tt[q] >= sim_end) continue;  // completed: no draw
             draws[p0 + q] = xoshiro_next(s0, s1, s2, s3);
         }

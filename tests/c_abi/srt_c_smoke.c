@@ -1,0 +1,108 @@
+/* Calls the drop-in boundary (include/srt.h) from plain C, as Shadow's Rust
+ * FFI would: builds the reference's own 3-node test graph
+ * (src/main/network/graph/mod.rs:559-647) as petgraph adjacency CSR, runs
+ * srt_compute_shortest_paths with both kernel families and srt_get_direct_paths
+ * on a complete graph, and checks the reference's golden latencies and error
+ * texts.  Exit 0 = pass.  Built by tests/c_abi/Makefile (gcc, links
+ * shadow_amd/libsrt.so); run by tests/test_gpu_c_abi.py on the GPU box. */
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/srt.h"
+
+static int fails = 0;
+#define CHECK(c, ...)                      \
+    do {                                   \
+        if (!(c)) {                        \
+            fprintf(stderr, __VA_ARGS__);  \
+            fputc('\n', stderr);           \
+            ++fails;                       \
+        }                                  \
+    } while (0)
+
+/* graph.edges(u) of the reference's 3-node test graph, GML edge order
+ * (mod.rs:576-610): self-loops 3333/5555/7777 ns, 0->1 3, 1->0 5, 0->2 7,
+ * 2->1 11; undirected = the same edges traversable both ways. */
+static void three_node(int directed, srt_csr *g, uint64_t *row_ptr, uint32_t *col, uint64_t *lat, float *loss) {
+    static const uint32_t S[] = {0, 1, 2, 0, 1, 0, 2};
+    static const uint32_t Dd[] = {0, 1, 2, 1, 0, 2, 1};
+    static const uint64_t L[] = {3333, 5555, 7777, 3, 5, 7, 11};
+    const int m = 7;
+    uint64_t cnt[4] = {0, 0, 0, 0};
+    for (int i = 0; i < m; ++i) {
+        cnt[S[i] + 1]++;
+        if (!directed && S[i] != Dd[i]) cnt[Dd[i] + 1]++;
+    }
+    for (int v = 0; v < 3; ++v) cnt[v + 1] += cnt[v];
+    memcpy(row_ptr, cnt, sizeof cnt);
+    uint64_t fill[3] = {cnt[0], cnt[1], cnt[2]};
+    for (int i = 0; i < m; ++i) {
+        uint64_t k = fill[S[i]]++;
+        col[k] = Dd[i], lat[k] = L[i], loss[k] = 0.0f;
+        if (!directed && S[i] != Dd[i]) {
+            k = fill[Dd[i]]++;
+            col[k] = S[i], lat[k] = L[i], loss[k] = 0.0f;
+        }
+    }
+    g->n_nodes = 3;
+    g->directed = (uint32_t)directed;
+    g->n_adj = cnt[3];
+    g->row_ptr = row_ptr;
+    g->col = col;
+    g->lat_ns = lat;
+    g->loss = loss;
+    g->node_ids = NULL;
+}
+
+int main(void) {
+    if (srt_abi_version() != SRT_ABI_VERSION) return 2;
+    if (srt_device_count() <= 0) {
+        fprintf(stderr, "no HIP device\n");
+        return 3;
+    }
+    /* mod.rs:626-644 golden latencies */
+    static const uint64_t gold_dir[9] = {3333, 3, 7, 5, 5555, 12, 16, 11, 7777};
+    static const uint64_t gold_und[9] = {3333, 3, 7, 3, 5555, 10, 7, 10, 7777};
+    for (int directed = 0; directed < 2; ++directed)
+        for (uint32_t algo = SRT_ALGO_FW; algo <= SRT_ALGO_SSSP; ++algo) {
+            srt_csr g;
+            uint64_t row_ptr[4], lat[16];
+            uint32_t col[16];
+            float loss[16];
+            three_node(directed, &g, row_ptr, col, lat, loss);
+            const uint32_t nodes[3] = {0, 1, 2};
+            srt_path out[9];
+            uint64_t mn = 0;
+            srt_opts o = {algo, -1, 0, 0};
+            srt_err err;
+            srt_status st = srt_compute_shortest_paths(&g, nodes, 3, out, &mn, &o, &err);
+            CHECK(st == SRT_OK, "directed=%d algo=%u: status %d %s", directed, algo, (int)st, err.msg);
+            for (int i = 0; i < 9 && st == SRT_OK; ++i)
+                CHECK(out[i].latency_ns == (directed ? gold_dir : gold_und)[i], "directed=%d algo=%u entry %d: %llu",
+                      directed, algo, i, (unsigned long long)out[i].latency_ns);
+            CHECK(mn == 3, "min latency %llu", (unsigned long long)mn);
+        }
+    /* a missing self-loop: the reference's error text (mod.rs:267-268) */
+    {
+        srt_csr g;
+        uint64_t row_ptr[4] = {0, 1, 1, 1};
+        uint32_t col[1] = {0};
+        uint64_t lat[1] = {5};
+        float loss[1] = {0.f};
+        uint32_t ids[3] = {10, 20, 30};
+        g.n_nodes = 3, g.directed = 1, g.n_adj = 1, g.row_ptr = row_ptr, g.col = col, g.lat_ns = lat;
+        g.loss = loss, g.node_ids = ids;
+        const uint32_t nodes[2] = {0, 1};
+        srt_path out[4];
+        srt_err err;
+        srt_status st = srt_compute_shortest_paths(&g, nodes, 2, out, NULL, NULL, &err);
+        CHECK(st == SRT_ERR_NO_EDGE && strcmp(err.msg, "No edge connecting node 20 to 20") == 0, "error text: %d %s",
+              (int)st, err.msg);
+    }
+    if (fails) {
+        fprintf(stderr, "%d check(s) failed\n", fails);
+        return 1;
+    }
+    printf("c abi ok\n");
+    return 0;
+}
