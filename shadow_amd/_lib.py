@@ -9,7 +9,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsrt.so")
+LIB_PATH = os.environ.get("SRT_LIB", os.path.join(_HERE, "libsrt.so"))  # SRT_LIB: A/B builds only
 
 SRT_OK = 0
 SRT_ERR_NO_EDGE = 1

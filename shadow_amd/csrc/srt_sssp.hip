@@ -93,6 +93,9 @@ __global__ __launch_bounds__(SWP_WAVES * 64) void sssp_sweep_kernel(
     if (blockIdx.x == 0 && threadIdx.x == 0) flag[((t + 1) % 3) * G + g] = 0;  // for sweep t+1
     if (t > 0 && flag[((t + 2) % 3) * G + g] == 0) return;                     // converged
     const int lane = threadIdx.x & 63;
+    // Plain block order on purpose: an XCD-contiguous remap (each XCD sweeping
+    // its own run of vertices) measured 2x slower on C4 (1.52 -> 2.9 s) -- all
+    // XCDs on neighbouring vertices keep the gathered rows in the Infinity Cache.
     const uint32_t v = __builtin_amdgcn_readfirstlane(blockIdx.x * SWP_WAVES + (threadIdx.x >> 6));
     if (v >= V) return;
     const uint64_t base = (uint64_t)g * V;  // first vertex row of the group
