@@ -415,7 +415,25 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         delete p;
         return hip_fail(err, e, "hipSetDevice");
     }
-    e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
+    // measurement knob SRT_FW_CHAIN_CUS=c: the main stream (phase-3 rest) is
+    // kept off c CUs so the look-ahead chain on the side stream never waits
+    // for a CU slot (SRT_FW_CHAIN_CU_STRIDE=1: reserved CUs spread evenly
+    // over the mask, else the last c bits)
+    if (const char *ce = std::getenv("SRT_FW_CHAIN_CUS"); ce && std::atoi(ce) > 0) {
+        hipDeviceProp_t prop;
+        int ncu = 256;
+        if (hipGetDeviceProperties(&prop, dev) == hipSuccess) ncu = prop.multiProcessorCount;
+        const int c = std::min(std::atoi(ce), ncu - 1);
+        const bool stride = std::getenv("SRT_FW_CHAIN_CU_STRIDE") != nullptr;
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+        for (int i = 0; i < ncu; ++i) {
+            const bool reserved = stride ? (i % (ncu / c) == 0 && i / (ncu / c) < c) : i >= ncu - c;
+            if (!reserved) mask[i / 32] |= 1u << (i % 32);
+        }
+        e = hipExtStreamCreateWithCUMask(&p->stream, (uint32_t)mask.size(), mask.data());
+    } else {
+        e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
+    }
     if (e != hipSuccess) {
         delete p;
         return hip_fail(err, e, "hipStreamCreate");
@@ -433,8 +451,11 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     }
     hipEventCreate(&p->ev_begin);
     hipEventCreate(&p->ev_end);
-    hipEventCreateWithFlags(&p->ev_cross, hipEventDisableTiming);
-    hipEventCreateWithFlags(&p->ev_pivot, hipEventDisableTiming);
+    // knob SRT_FW_SYNC_FENCE=dev (measurement): the stream-to-stream events
+    // of the look-ahead schedule skip the system-scope fence (same device)
+    const unsigned sync_fl = hipEventDisableTiming | (std::getenv("SRT_FW_SYNC_FENCE") ? hipEventDisableSystemFence : 0u);
+    hipEventCreateWithFlags(&p->ev_cross, sync_fl);
+    hipEventCreateWithFlags(&p->ev_pivot, sync_fl);
 
 #define PLAN_TRY(x)                \
     do {                           \

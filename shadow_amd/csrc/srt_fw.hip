@@ -165,29 +165,34 @@ __global__ void scatter_edges_kernel(K *__restrict__ D, uint32_t Vp,
 // publish them (after their own step k-1 update) into double-buffered LDS
 // vectors: one barrier per step.  The k loop is unrolled by 8 so the owned
 // element index (k & 7) is static (a runtime index would send p to scratch).
-template <typename K>
-__global__ __launch_bounds__(NT3, 2) void fw_phase1_kernel(K *__restrict__ D, uint32_t Vp, uint32_t kb) {
+// P1R = rows per thread (8: 256 threads, one wave per SIMD; 4: 512 threads,
+// two waves per SIMD so one wave's LDS/barrier wait hides behind the other's
+// VALU work -- the kernel is latency bound, 128 dependent steps).
+template <typename K, int P1R>
+__global__ __launch_bounds__(16 * (B / P1R)) void fw_phase1_kernel(K *__restrict__ D, uint32_t Vp, uint32_t kb) {
     __shared__ K rowbuf[2][B];
     __shared__ K colbuf[2][B];
     __builtin_amdgcn_s_setprio(3);  // critical path of the look-ahead chain
     const int tid = threadIdx.x, tx = tid % 16, ty = tid / 16;
     const uint64_t k0 = (uint64_t)kb * B;
-    K p[TR][TC];
+    K p[P1R][TC];
 #pragma unroll
-    for (int i = 0; i < TR; ++i) {
-        const K *src = D + (k0 + ty * TR + i) * Vp + k0 + tx * TC;
+    for (int i = 0; i < P1R; ++i) {
+        const K *src = D + (k0 + ty * P1R + i) * Vp + k0 + tx * TC;
 #pragma unroll
         for (int j = 0; j < TC; ++j) p[i][j] = src[j];
     }
-    // owners of block index g = k >> 3 publish row/column k, e = k & 7 static
+    // step k = 8g + e: row k lives in thread-row k / P1R at element k % P1R,
+    // column k in thread-column g at element e -- both static once e is
     auto publish = [&](int g, int e, int buf) {
-        if (ty == g) {
+        const int k = 8 * g + e;
+        if (ty == k / P1R) {
 #pragma unroll
-            for (int j = 0; j < TC; ++j) rowbuf[buf][tx * TC + j] = p[e][j];
+            for (int j = 0; j < TC; ++j) rowbuf[buf][tx * TC + j] = p[e % P1R][j];
         }
         if (tx == g) {
 #pragma unroll
-            for (int i = 0; i < TR; ++i) colbuf[buf][ty * TR + i] = p[i][e];
+            for (int i = 0; i < P1R; ++i) colbuf[buf][ty * P1R + i] = p[i][e];
         }
     };
     publish(0, 0, 0);
@@ -197,13 +202,13 @@ __global__ __launch_bounds__(NT3, 2) void fw_phase1_kernel(K *__restrict__ D, ui
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             const int cur = e & 1;  // k = 8g + e, parity of k == parity of e
-            K a[TR], b[TC];
+            K a[P1R], b[TC];
 #pragma unroll
-            for (int i = 0; i < TR; ++i) a[i] = colbuf[cur][ty * TR + i];
+            for (int i = 0; i < P1R; ++i) a[i] = colbuf[cur][ty * P1R + i];
 #pragma unroll
             for (int j = 0; j < TC; ++j) b[j] = rowbuf[cur][tx * TC + j];
 #pragma unroll
-            for (int i = 0; i < TR; ++i) relax_row8<K>(p[i], a[i], b);
+            for (int i = 0; i < P1R; ++i) relax_row8<K>(p[i], a[i], b);
             // publish step k+1 = 8g + e + 1
             if (e < 7) publish(g, e + 1, cur ^ 1);
             else if (g + 1 < B / 8) publish(g + 1, 0, cur ^ 1);
@@ -211,8 +216,8 @@ __global__ __launch_bounds__(NT3, 2) void fw_phase1_kernel(K *__restrict__ D, ui
         }
     }
 #pragma unroll
-    for (int i = 0; i < TR; ++i) {
-        K *dst = D + (k0 + ty * TR + i) * Vp + k0 + tx * TC;
+    for (int i = 0; i < P1R; ++i) {
+        K *dst = D + (k0 + ty * P1R + i) * Vp + k0 + tx * TC;
 #pragma unroll
         for (int j = 0; j < TC; ++j) dst[j] = p[i][j];
     }
@@ -704,6 +709,23 @@ void fw_init_t(srt_plan *p) {
                            p->d_row_ptr, p->d_col, p->d_lat, p->d_loss, p->V, p->kp);
 }
 
+// Measurement only (N-rank emulation): stands in for the pivot-row broadcast
+// on the chain stream -- one wave waits `ticks` of the constant wall clock.
+__global__ void delay_kernel(long long ticks) {
+    const long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+template <typename K>
+void launch_p1(int rows, hipStream_t s, K *D, uint32_t Vp, uint32_t kb) {
+    if (rows == 2)
+        hipLaunchKernelGGL((fw_phase1_kernel<K, 2>), dim3(1), dim3(16 * (B / 2)), 0, s, D, Vp, kb);
+    else if (rows == 4)
+        hipLaunchKernelGGL((fw_phase1_kernel<K, 4>), dim3(1), dim3(16 * (B / 4)), 0, s, D, Vp, kb);
+    else
+        hipLaunchKernelGGL((fw_phase1_kernel<K, 8>), dim3(1), dim3(16 * (B / 8)), 0, s, D, Vp, kb);
+}
+
 template <typename K, int TAG>
 void launch_tiles(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1, const Rect &r2) {
     const uint32_t n = r1.r.n * r1.c.n + r2.r.n * r2.c.n;
@@ -720,14 +742,18 @@ void launch_tiles(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1, const
 }
 
 // Round schedule with one block of look-ahead, per rank (block-rows [rb0,rb1)):
-//   main stream M:  cross(kb) | rest(kb) | (wait S) cross(kb+1) | ...
-//   side stream S:  (after cross(kb))  p1(kb+1), p2row(kb+1) on the owner of
-//                   kb+1, the pivot-row broadcast of kb+1 (multi-GPU), then
-//                   p2col(kb+1) for the local rows
+//   main stream M:  (wait pivot kb) rest(kb) | (wait pivot kb+1) rest(kb+1) | ...
+//   side stream S:  (after rest(kb-1))  cross(kb), p1(kb+1), p2row(kb+1) on
+//                   the owner of kb+1, the pivot-row broadcast of kb+1
+//                   (multi-GPU), then p2col(kb+1) for the local rows
 // cross(kb) = the round-kb phase-3 tiles that round kb+1's pivot work needs
 // (column kb+1 of the local rows; row kb+1 on its owner), rest(kb) = all other
-// phase-3 tiles.  rest(kb) never touches block-row/column kb+1, so it runs
-// concurrently with S.  Single GPU = one rank, no broadcast.
+// phase-3 tiles.  The two sets are disjoint and both read only pivot kb's row
+// and column, so the whole S chain of pivot kb+1 overlaps rest(kb): M runs
+// phase-3 kernels back to back and the round period is max(rest, chain).
+// (Measured before, with cross(kb) on M: 10 us gaps either side of it and a
+// half-empty GPU during it, 3.4% of the 16k build on one GPU.)  Single GPU =
+// one rank, no broadcast.
 template <typename K>
 srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
     K *D = reinterpret_cast<K *>(p->d_D);
@@ -747,55 +773,79 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
     const Rect none{make_span(0, 0), make_span(0, 0)};
     p->p3_launches = 0;
     p->p3_work = 0.0;
+    // phase-3 launches bracketed by timing events (kernel_stats): every
+    // ev_every-th round (knob SRT_FW_EVENT_EVERY, measurement only)
+    uint32_t ev_every = 1;
+    if (const char *e = std::getenv("SRT_FW_EVENT_EVERY")) ev_every = std::max(1, std::atoi(e));
     const size_t need = 2 * (size_t)nblk + 2;
     while (p->ev.size() < need) {
         hipEvent_t e;
-        hipEventCreateWithFlags(&e, 0);
+        // timing-only events: no system-scope fence (knob SRT_FW_TIMING_FENCE=sys restores it)
+        hipEventCreateWithFlags(&e, std::getenv("SRT_FW_TIMING_FENCE") ? 0u : (unsigned)hipEventDisableSystemFence);
         p->ev.push_back(e);
+    }
+    // phase-1 rows per thread (knob SRT_FW_P1_ROWS in {2,4,8}, measurement only)
+    int p1r = 8;
+    if (const char *e = std::getenv("SRT_FW_P1_ROWS")) p1r = std::atoi(e);
+    // emulation only: SRT_FW_EMU_BCAST_US stands in for the pivot-row broadcast latency
+    long long emu_bcast_ticks = 0;
+    if (const char *e = std::getenv("SRT_FW_EMU_BCAST_US"); e && emu) {
+        int khz = 100000;
+        hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, p->device);
+        emu_bcast_ticks = (long long)(std::atof(e) * khz / 1000.0);
     }
     srt_status st = SRT_OK;
     // prologue: pivot 0
     if (own(0)) {
-        hipLaunchKernelGGL(fw_phase1_kernel<K>, dim3(1), dim3(NT3), 0, M, D, p->Vp, 0u);
+        launch_p1<K>(p1r, M, D, p->Vp, 0u);
         launch_tiles<K, 1>(p, M, 0, Rect{make_span(0, 1), make_span(0, nblk, 0)}, none);
     }
     if (sharded && (st = comm_bcast(p->comm, D, pivot_bytes, 0, M, err)) != SRT_OK) return st;
     launch_tiles<K, 2>(p, M, 0, Rect{make_span(rb0, rb1, 0), make_span(0, 1)}, none);
 
+    // S may start round 0's cross tiles once the prologue is done
+    hipEventRecord(p->ev_cross, M);
     for (uint32_t kb = 0; kb < nblk; ++kb) {
         const bool nxt = kb + 1 < nblk;
         const uint32_t k1 = kb + 1;
+        // host order matters: both events are re-recorded every round, and a
+        // wait binds to the record enqueued before it
+        if (nxt) hipStreamWaitEvent(S, p->ev_cross, 0);  // rest(kb-1) (or the prologue) done
+        if (kb) hipStreamWaitEvent(M, p->ev_pivot, 0);    // pivot kb ready (round 0: stream order)
+        // rest(kb): local rows and all columns, minus kb and (look-ahead) k1
+        Rect rest{make_span(rb0, rb1, kb, nxt ? k1 : NONE), make_span(0, nblk, kb, nxt ? k1 : NONE)};
+        const uint32_t nt = rest.r.n * rest.c.n;
+        if (nt && kb % ev_every == 0) {
+            hipEventRecord(p->ev[2 * p->p3_launches], M);
+            launch_tiles<K, 0>(p, M, kb, rest, none);
+            hipEventRecord(p->ev[2 * p->p3_launches + 1], M);
+            p->p3_launches++;
+            p->p3_work += (double)nt * B * B * B;
+        } else if (nt) {
+            launch_tiles<K, 0>(p, M, kb, rest, none);
+        }
         if (nxt) {
-            // cross(kb): column k1 of the local rows (+ row k1 on its owner)
+            hipEventRecord(p->ev_cross, M);  // for round k1's cross tiles on S
+            // cross(kb) on S, concurrent with rest(kb) (disjoint tiles; both
+            // read only the pivot-kb row and column): column k1 of the local
+            // rows (+ row k1 on its owner)
             Rect col{make_span(rb0, rb1, kb, k1), make_span(k1, k1 + 1)};
             Rect row = own(k1) ? Rect{make_span(k1, k1 + 1), make_span(0, nblk, kb)} : none;
-            launch_tiles<K, 4>(p, M, kb, col, row);
-            hipEventRecord(p->ev_cross, M);
-            hipStreamWaitEvent(S, p->ev_cross, 0);
+            launch_tiles<K, 4>(p, S, kb, col, row);
             if (own(k1)) {
-                hipLaunchKernelGGL(fw_phase1_kernel<K>, dim3(1), dim3(NT3), 0, S, D, p->Vp, k1);
+                launch_p1<K>(p1r, S, D, p->Vp, k1);
                 launch_tiles<K, 1>(p, S, k1, Rect{make_span(k1, k1 + 1), make_span(0, nblk, k1)}, none);
             }
             if (sharded &&
                 (st = comm_bcast(p->comm, D + (uint64_t)k1 * B * p->Vp, pivot_bytes, (int)(k1 / per_rank), S,
                                  err)) != SRT_OK)
                 return st;
+            if (emu_bcast_ticks) hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, S, emu_bcast_ticks);
             // p2col(k1): column k1 of the local rows through P*(k1); rest(kb)
             // never touches column k1, so this also overlaps rest(kb)
             launch_tiles<K, 2>(p, S, k1, Rect{make_span(rb0, rb1, k1), make_span(k1, k1 + 1)}, none);
             hipEventRecord(p->ev_pivot, S);
         }
-        // rest(kb): local rows and all columns, minus kb and (look-ahead) k1
-        Rect rest{make_span(rb0, rb1, kb, nxt ? k1 : NONE), make_span(0, nblk, kb, nxt ? k1 : NONE)};
-        const uint32_t nt = rest.r.n * rest.c.n;
-        if (nt) {
-            hipEventRecord(p->ev[2 * p->p3_launches], M);
-            launch_tiles<K, 0>(p, M, kb, rest, none);
-            hipEventRecord(p->ev[2 * p->p3_launches + 1], M);
-            p->p3_launches++;
-            p->p3_work += (double)nt * B * B * B;
-        }
-        if (nxt) hipStreamWaitEvent(M, p->ev_pivot, 0);
     }
     if (sharded)
         return comm_allgather_inplace(p->comm, D, (size_t)per_rank * B * p->Vp * sizeof(K), M, err);
