@@ -443,7 +443,9 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         int lo = 0, hi = 0;
         hipDeviceGetStreamPriorityRange(&lo, &hi);
         e = hipStreamCreateWithPriority(&p->side_stream, hipStreamNonBlocking, hi);
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(&p->comm_stream, hipStreamNonBlocking, hi);
         if (e != hipSuccess) {
+            if (p->side_stream) hipStreamDestroy(p->side_stream);
             hipStreamDestroy(p->stream);
             delete p;
             return hip_fail(err, e, "hipStreamCreateWithPriority");
@@ -456,6 +458,8 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     const unsigned sync_fl = hipEventDisableTiming | (std::getenv("SRT_FW_SYNC_FENCE") ? hipEventDisableSystemFence : 0u);
     hipEventCreateWithFlags(&p->ev_cross, sync_fl);
     hipEventCreateWithFlags(&p->ev_pivot, sync_fl);
+    hipEventCreateWithFlags(&p->ev_row, sync_fl);
+    hipEventCreateWithFlags(&p->ev_bcast, sync_fl);
 
 #define PLAN_TRY(x)                \
     do {                           \
@@ -644,16 +648,14 @@ void srt_plan_destroy(srt_plan *p) {
     if (!p) return;
     hipSetDevice(p->device);
     if (p->stream) hipStreamSynchronize(p->stream);
+    if (p->side_stream) hipStreamSynchronize(p->side_stream);
+    if (p->comm_stream) hipStreamSynchronize(p->comm_stream);
     free_plan_buffers(p);
     for (hipEvent_t e : p->ev) hipEventDestroy(e);
-    if (p->ev_begin) hipEventDestroy(p->ev_begin);
-    if (p->ev_end) hipEventDestroy(p->ev_end);
-    if (p->ev_cross) hipEventDestroy(p->ev_cross);
-    if (p->ev_pivot) hipEventDestroy(p->ev_pivot);
-    if (p->side_stream) {
-        hipStreamSynchronize(p->side_stream);
-        hipStreamDestroy(p->side_stream);
-    }
+    for (hipEvent_t e : {p->ev_begin, p->ev_end, p->ev_cross, p->ev_pivot, p->ev_row, p->ev_bcast})
+        if (e) hipEventDestroy(e);
+    if (p->side_stream) hipStreamDestroy(p->side_stream);
+    if (p->comm_stream) hipStreamDestroy(p->comm_stream);
     if (p->own_stream && p->stream) hipStreamDestroy(p->stream);
     delete p;
 }

@@ -768,7 +768,7 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
     p->fw_small_chain = (sharded || emu) && !std::getenv("SRT_FW_NO_SMALL_CHAIN");  // knob: A/B timing
     const uint32_t per_rank = sharded ? nblk / p->comm->nranks : nblk;
     const size_t pivot_bytes = (size_t)B * p->Vp * sizeof(K);
-    hipStream_t M = p->stream, S = p->side_stream;
+    hipStream_t M = p->stream, S = p->side_stream, C = p->comm_stream;
     auto own = [&](uint32_t b) { return emu ? true : (b >= rb0 && b < rb1); };
     const Rect none{make_span(0, 0), make_span(0, 0)};
     p->p3_launches = 0;
@@ -803,8 +803,10 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
     if (sharded && (st = comm_bcast(p->comm, D, pivot_bytes, 0, M, err)) != SRT_OK) return st;
     launch_tiles<K, 2>(p, M, 0, Rect{make_span(rb0, rb1, 0), make_span(0, 1)}, none);
 
-    // S may start round 0's cross tiles once the prologue is done
+    // S may start round 0's cross tiles once the prologue is done; C's
+    // broadcasts follow the prologue's
     hipEventRecord(p->ev_cross, M);
+    hipStreamWaitEvent(C, p->ev_cross, 0);
     for (uint32_t kb = 0; kb < nblk; ++kb) {
         const bool nxt = kb + 1 < nblk;
         const uint32_t k1 = kb + 1;
@@ -836,17 +838,38 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
                 launch_p1<K>(p1r, S, D, p->Vp, k1);
                 launch_tiles<K, 1>(p, S, k1, Rect{make_span(k1, k1 + 1), make_span(0, nblk, k1)}, none);
             }
-            if (sharded &&
-                (st = comm_bcast(p->comm, D + (uint64_t)k1 * B * p->Vp, pivot_bytes, (int)(k1 / per_rank), S,
-                                 err)) != SRT_OK)
-                return st;
-            if (emu_bcast_ticks) hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, S, emu_bcast_ticks);
+            // pivot-row broadcast on the comm stream C: the owner's chain goes
+            // on without it (it holds row k1; its next cross/p1/p2row are
+            // local), so the transfer overlaps the owner's next pivot and only
+            // the other ranks' p2col(k1) -> rest(k1) wait for it.  Reading
+            // row k1 while the owner's later rounds lower it is harmless: every
+            // key is a real path's key, so receivers only see valid upper
+            // bounds at least as tight as round k1's (the FW invariant holds).
+            if (sharded || emu_bcast_ticks) {
+                if (own(k1)) {
+                    hipEventRecord(p->ev_row, S);
+                    hipStreamWaitEvent(C, p->ev_row, 0);
+                }
+                if (sharded &&
+                    (st = comm_bcast(p->comm, D + (uint64_t)k1 * B * p->Vp, pivot_bytes, (int)(k1 / per_rank), C,
+                                     err)) != SRT_OK)
+                    return st;
+                if (emu_bcast_ticks) hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, C, emu_bcast_ticks);
+                if (!own(k1)) {
+                    hipEventRecord(p->ev_bcast, C);
+                    hipStreamWaitEvent(S, p->ev_bcast, 0);
+                }
+            }
             // p2col(k1): column k1 of the local rows through P*(k1); rest(kb)
             // never touches column k1, so this also overlaps rest(kb)
             launch_tiles<K, 2>(p, S, k1, Rect{make_span(rb0, rb1, k1), make_span(k1, k1 + 1)}, none);
             hipEventRecord(p->ev_pivot, S);
         }
     }
+    // collectives on one communicator stay ordered: the all-gather follows
+    // the last broadcast
+    hipEventRecord(p->ev_bcast, C);
+    hipStreamWaitEvent(M, p->ev_bcast, 0);
     if (sharded)
         return comm_allgather_inplace(p->comm, D, (size_t)per_rank * B * p->Vp * sizeof(K), M, err);
     return SRT_OK;

@@ -103,6 +103,8 @@ struct srt_plan {
     hipEvent_t ev_begin = nullptr, ev_end = nullptr;
     hipEvent_t ev_cross = nullptr, ev_pivot = nullptr;  // look-ahead hand-offs M <-> S
     hipStream_t side_stream = nullptr;                  // high-priority pivot stream
+    hipStream_t comm_stream = nullptr;                  // pivot-row broadcasts (multi-GPU)
+    hipEvent_t ev_row = nullptr, ev_bcast = nullptr;    // S -> C (row ready), C -> S/M (row received)
     uint64_t p3_launches = 0;
     double p3_work = 0.0;  // relaxations done by the timed launches
     double p3_ms = 0.0, total_ms = 0.0;
