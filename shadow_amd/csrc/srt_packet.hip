@@ -43,9 +43,10 @@ __global__ void draw_kernel(const srt_pkt *__restrict__ pkts, const uint32_t *__
     uint64_t s0 = rng[4 * (uint64_t)h], s1 = rng[4 * (uint64_t)h + 1];
     uint64_t s2 = rng[4 * (uint64_t)h + 2], s3 = rng[4 * (uint64_t)h + 3];
     const uint32_t b = host_ptr[h], e = host_ptr[h + 1];
-    // send times are fetched 32 at a time (independent loads in flight) so the
-    // sequential state walk is not one memory latency per packet
-    constexpr int PF = 32;
+    // send times are fetched 16 at a time (independent loads in flight) so the
+    // sequential state walk is not one memory latency per packet (32 measured
+    // no faster and spills to scratch)
+    constexpr int PF = 16;
     for (uint32_t p0 = b; p0 < e; p0 += PF) {
         uint64_t tt[PF];
 #pragma unroll
