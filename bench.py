@@ -291,8 +291,11 @@ def bench_packets(args, cfg, D):
     t_s = torch.full((2,), -1, dtype=torch.int64, device=dev)
     stream = torch.cuda.ExternalStream(plan.stream_ptr(), device=dev)
 
+    # diagnostics only (never a reported line): SRT_BENCH_NO_COUNTERS drops the per-pair counters
+    t_cc = None if os.environ.get("SRT_BENCH_NO_COUNTERS") else t_c
+
     def one():
-        plan.packet_batch(t_pk, t_hp, t_rng, r1, 0, 2**62, t_f, t_d, t_c, t_s, sync=False)
+        plan.packet_batch(t_pk, t_hp, t_rng, r1, 0, 2**62, t_f, t_d, t_cc, t_s, sync=False)
 
     for _ in range(args.warmup):
         one()

@@ -13,6 +13,7 @@
 // Two kernels: (A) one lane per host walks its packets and advances its
 // xoshiro256++ state -- the only sequential part, ~20 integer ops per draw;
 // (B) one lane per packet does the table gather and the decision, HBM-bound.
+#include <cstdlib>
 #include <cstring>
 
 #include "srt_internal.h"
@@ -35,18 +36,20 @@ __device__ __forceinline__ uint64_t xoshiro_next(uint64_t &s0, uint64_t &s1, uin
     return r;
 }
 
-__global__ void draw_kernel(const srt_pkt *__restrict__ pkts, const uint32_t *__restrict__ host_ptr,
-                            uint32_t n_hosts, uint64_t *__restrict__ rng, uint64_t sim_end,
-                            uint64_t *__restrict__ draws) {
+// One lane per host; the walk is a dependent chain per lane, so the grid is
+// spread thin (DT threads per block: 10k hosts -> 157 CUs at DT = 64, not 40)
+// and the send times are fetched PF at a time (independent loads in flight)
+// so the walk is not one memory latency per packet.
+template <int DT, int PF>
+__global__ __launch_bounds__(DT) void draw_kernel(const srt_pkt *__restrict__ pkts,
+                                                  const uint32_t *__restrict__ host_ptr, uint32_t n_hosts,
+                                                  uint64_t *__restrict__ rng, uint64_t sim_end,
+                                                  uint64_t *__restrict__ draws) {
     const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
     if (h >= n_hosts) return;
     uint64_t s0 = rng[4 * (uint64_t)h], s1 = rng[4 * (uint64_t)h + 1];
     uint64_t s2 = rng[4 * (uint64_t)h + 2], s3 = rng[4 * (uint64_t)h + 3];
     const uint32_t b = host_ptr[h], e = host_ptr[h + 1];
-    // send times are fetched 16 at a time (independent loads in flight) so the
-    // sequential state walk is not one memory latency per packet (32 measured
-    // no faster and spills to scratch)
-    constexpr int PF = 16;
     for (uint32_t p0 = b; p0 < e; p0 += PF) {
         uint64_t tt[PF];
 #pragma unroll
@@ -70,7 +73,7 @@ __global__ __launch_bounds__(DECIDE_THREADS) void decide_kernel(const srt_pkt *_
                               const uint64_t *__restrict__ lat, const float *__restrict__ loss,
                               uint32_t n, srt_round r, uint32_t *__restrict__ flags,
                               uint64_t *__restrict__ deliver, unsigned long long *counters,
-                              unsigned long long *stats) {
+                              unsigned long long *__restrict__ partial) {
     unsigned long long min_lat = ~0ull, min_deliver = ~0ull;
     for (uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; p < n_pkts;
          p += (uint64_t)gridDim.x * blockDim.x) {
@@ -112,13 +115,46 @@ __global__ __launch_bounds__(DECIDE_THREADS) void decide_kernel(const srt_pkt *_
         red[1][w] = min_deliver;
     }
     __syncthreads();
-    if (threadIdx.x == 0 && stats) {
+    if (threadIdx.x == 0 && partial) {
         for (int k = 1; k < DECIDE_THREADS / 64; ++k) {
             min_lat = red[0][k] < min_lat ? red[0][k] : min_lat;
             min_deliver = red[1][k] < min_deliver ? red[1][k] : min_deliver;
         }
-        if (min_lat != ~0ull) atomicMin(&stats[0], min_lat);
-        if (min_deliver != ~0ull) atomicMin(&stats[1], min_deliver);
+        partial[2 * blockIdx.x] = min_lat;
+        partial[2 * blockIdx.x + 1] = min_deliver;
+    }
+}
+
+// Block partials -> the caller's stats (min-combined).  Same-address atomics
+// from every block of decide_kernel serialise at the memory-side atomic unit
+// (2048 blocks x 2 = ~60 us measured, more than the whole decision pass), so
+// they are combined here by one workgroup: two atomics per round.
+__global__ __launch_bounds__(1024) void stats_kernel(const unsigned long long *__restrict__ partial, uint32_t nblocks,
+                                                     unsigned long long *stats) {
+    unsigned long long a = ~0ull, b = ~0ull;
+    for (uint32_t i = threadIdx.x; i < nblocks; i += blockDim.x) {
+        a = partial[2 * i] < a ? partial[2 * i] : a;
+        b = partial[2 * i + 1] < b ? partial[2 * i + 1] : b;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long x = __shfl_xor(a, off), y = __shfl_xor(b, off);
+        a = x < a ? x : a;
+        b = y < b ? y : b;
+    }
+    __shared__ unsigned long long red[2][16];
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        red[0][w] = a;
+        red[1][w] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < (int)(blockDim.x >> 6); ++k) {
+            a = red[0][k] < a ? red[0][k] : a;
+            b = red[1][k] < b ? red[1][k] : b;
+        }
+        if (a != ~0ull) atomicMin(&stats[0], a);
+        if (b != ~0ull) atomicMin(&stats[1], b);
     }
 }
 
@@ -146,30 +182,52 @@ extern "C" srt_status srt_packet_batch(srt_plan *plan, const srt_pkt *d_pkts,
         return SRT_ERR_INVALID;
     }
     if (hipSetDevice(plan->device) != hipSuccess) return SRT_ERR_HIP;
-    if (n_pkts > plan->draws_cap) {
+    // scratch: one draw per packet, then {min latency, min deliver} per decide block
+    constexpr uint64_t MAX_DECIDE_BLOCKS = 2048;  // grid-stride: 8 blocks per CU
+    const uint64_t need = n_pkts + 2 * MAX_DECIDE_BLOCKS;
+    if (need > plan->draws_cap) {
         if (plan->d_draws) (void)hipFree(plan->d_draws);
         plan->d_draws = nullptr;
         plan->draws_cap = 0;
-        if (hipMalloc(&plan->d_draws, n_pkts * sizeof(uint64_t)) != hipSuccess) {
+        if (hipMalloc(&plan->d_draws, need * sizeof(uint64_t)) != hipSuccess) {
             if (err) {
                 err->code = SRT_ERR_OOM;
                 std::snprintf(err->msg, sizeof err->msg, "hipMalloc(draws) failed");
             }
             return SRT_ERR_OOM;
         }
-        plan->draws_cap = n_pkts;
+        plan->draws_cap = need;
     }
+    unsigned long long *partial = (unsigned long long *)(plan->d_draws + n_pkts);
     hipStream_t s = plan->stream;
-    if (n_hosts)
-        hipLaunchKernelGGL(draw_kernel, dim3((n_hosts + 255) / 256), dim3(256), 0, s, d_pkts,
-                           d_host_pkt_ptr, n_hosts, d_rng, round->sim_end_ns, plan->d_draws);
+    if (n_hosts) {
+        // knob SRT_PKT_DRAW (measurement only): "256x16", "64x16", "64x32", "256x32"
+        static const char *knob = std::getenv("SRT_PKT_DRAW");
+        const bool wide = knob && knob[0] == '2';
+        // default 64 x 16 (C5: 103 us/round vs 137 at 256 threads; PF 16 == 32)
+        const bool pf32 = knob && std::strstr(knob, "x32");
+        if (wide && pf32)
+            hipLaunchKernelGGL((draw_kernel<256, 32>), dim3((n_hosts + 255) / 256), dim3(256), 0, s, d_pkts,
+                               d_host_pkt_ptr, n_hosts, d_rng, round->sim_end_ns, plan->d_draws);
+        else if (wide)
+            hipLaunchKernelGGL((draw_kernel<256, 16>), dim3((n_hosts + 255) / 256), dim3(256), 0, s, d_pkts,
+                               d_host_pkt_ptr, n_hosts, d_rng, round->sim_end_ns, plan->d_draws);
+        else if (pf32)
+            hipLaunchKernelGGL((draw_kernel<64, 32>), dim3((n_hosts + 63) / 64), dim3(64), 0, s, d_pkts,
+                               d_host_pkt_ptr, n_hosts, d_rng, round->sim_end_ns, plan->d_draws);
+        else
+            hipLaunchKernelGGL((draw_kernel<64, 16>), dim3((n_hosts + 63) / 64), dim3(64), 0, s, d_pkts,
+                               d_host_pkt_ptr, n_hosts, d_rng, round->sim_end_ns, plan->d_draws);
+    }
     if (n_pkts) {
         uint64_t blocks = (n_pkts + DECIDE_THREADS - 1) / DECIDE_THREADS;
-        if (blocks > 2048) blocks = 2048;  // grid-stride: 8 blocks per CU
+        if (blocks > MAX_DECIDE_BLOCKS) blocks = MAX_DECIDE_BLOCKS;
         hipLaunchKernelGGL(decide_kernel, dim3((uint32_t)blocks), dim3(DECIDE_THREADS), 0, s, d_pkts, n_pkts,
                            plan->d_draws, plan->d_out_lat, plan->d_out_loss, plan->n, *round,
-                           d_flags, d_deliver, (unsigned long long *)d_counters,
-                           (unsigned long long *)d_stats);
+                           d_flags, d_deliver, (unsigned long long *)d_counters, d_stats ? partial : nullptr);
+        if (d_stats)
+            hipLaunchKernelGGL(stats_kernel, dim3(1), dim3(1024), 0, s, partial, (uint32_t)blocks,
+                               (unsigned long long *)d_stats);
     }
     if (hipGetLastError() != hipSuccess) {
         if (err) {

@@ -112,7 +112,10 @@ class RoutingPlan:
 
         n_hosts = host_ptr.numel() - 1
         n_pkts = flags.numel()
-        torch.cuda.synchronize(flags.device)
+        # the plan's stream waits for the producer of the inputs (torch's
+        # current stream) on the device: no host round trip per batch
+        torch.cuda.ExternalStream(self.stream_ptr(), device=flags.device).wait_stream(
+            torch.cuda.current_stream(flags.device))
         r = _lib.SrtRound(round_end_ns, bootstrap_end_ns, sim_end_ns)
         err = _lib.SrtErr()
         _lib.check(_lib.lib().srt_packet_batch(

@@ -21,3 +21,8 @@ timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-f
 echo "fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- python3 $R/bench.py "$@" --steps 1 --warmup 0 --no-cpu-baseline > $O/pmc_write.log 2>&1; rc=$?
 echo "write rc=$rc"
+[ $rc -eq 0 ] || exit $rc
+if [ -n "$SQPMC" ]; then
+  timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE -d $O/pmc_sq -o run --output-format csv -- python3 $R/bench.py "$@" --steps 1 --warmup 0 --no-cpu-baseline > $O/pmc_sq.log 2>&1; rc=$?
+  echo "sq rc=$rc"
+fi
