@@ -81,6 +81,31 @@ def main():
            "kernels": kernels}
     json.dump(doc, open(os.path.join(out, f"{tag}_pmc_traffic.json"), "w"), indent=1)
     print(json.dumps({k: round(v["hbm_bytes_per_launch"] / 1e6, 2) for k, v in kernels.items()}, indent=1))
+    sq_dir = os.path.join(src, "pmc_sq")
+    if os.path.isdir(sq_dir):
+        per = collections.defaultdict(lambda: collections.defaultdict(float))
+        disp = collections.defaultdict(set)
+        for f in glob.glob(os.path.join(sq_dir, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                k = short(r["Kernel_Name"])
+                per[k][r["Counter_Name"]] += float(r["Counter_Value"])
+                disp[k].add(r["Dispatch_Id"])
+        sq = {}
+        for k, c in per.items():
+            n = max(len(disp[k]), 1)
+            avg = {name: v / n for name, v in c.items()}
+            wave = avg.get("SQ_WAVE_CYCLES", 0.0)
+            row = {"per_dispatch": avg}
+            if wave:
+                row["frac_of_wave_cycles"] = {name: avg[name] / wave for name in
+                                              ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY",
+                                               "SQ_ACTIVE_INST_VALU") if name in avg}
+            sq[k] = row
+        json.dump({"round": tag, "config": config,
+                   "method": "one rocprofv3 --pmc pass (8 SQ counters + GRBM_GUI_ACTIVE), --steps 1; SQ cycle "
+                             "counters are quad-cycles summed over waves, GRBM_GUI_ACTIVE summed over the 8 XCDs "
+                             "(MI355X_MICROARCH.md)", "kernels": sq},
+                  open(os.path.join(out, f"{tag}_pmc_sq.json"), "w"), indent=1)
 
 
 if __name__ == "__main__":
