@@ -271,6 +271,72 @@ class RoutingInfo:
         return int(self.table.min_latency_ns) if len(self.table.nodes) else None
 
 
+# configuration.rs ONE_GBIT_SWITCH_GRAPH: one node, its self-loop at 1 ms
+ONE_GBIT_SWITCH_GRAPH = """graph [
+  directed 0
+  node [
+    id 0
+    host_bandwidth_up "1 Gbit"
+    host_bandwidth_down "1 Gbit"
+  ]
+  edge [
+    source 0
+    target 0
+    latency "1 ms"
+    packet_loss 0.0
+  ]
+]"""
+
+
+class GraphLoadError(RuntimeError):
+    """load_network_graph failures (the reference's NetGraphError contexts)."""
+
+
+def load_network_graph(options) -> str:
+    """mod.rs:494-509 (load_network_graph) + :479-492 (read_xz): the GML text of
+    a `network.graph` option, given as the configuration's mapping
+    (configuration.rs:976-1004):
+      {"type": "gml", "file": {"path": p, "compression": None | "xz"}}
+      {"type": "gml", "inline": text}
+      {"type": "1_gbit_switch"}
+    Paths get tilde expansion; xz files are decompressed on the host (the
+    reference uses lzma-rs here too) and must be UTF-8."""
+    import lzma
+    import os
+
+    kind = options.get("type")
+    if kind == "1_gbit_switch":
+        return ONE_GBIT_SWITCH_GRAPH
+    if kind != "gml":
+        raise GraphLoadError(f"unknown graph type: {kind!r}")
+    if "inline" in options:
+        return options["inline"]
+    src = options.get("file") or {}
+    path = os.path.expanduser(src["path"])
+    comp = src.get("compression")
+    if comp is None:
+        try:
+            with open(path, "r", encoding="utf-8") as f:
+                return f.read()
+        except (OSError, UnicodeDecodeError) as e:
+            raise GraphLoadError(f"Failed to read file: {src['path']}") from e
+    if comp != "xz":
+        raise GraphLoadError(f"unknown compression: {comp!r}")
+    try:
+        f = open(path, "rb")
+    except OSError as e:
+        raise GraphLoadError(f"Failed to open file: {path!r}") from e
+    with f:
+        try:
+            data = lzma.decompress(f.read(), format=lzma.FORMAT_XZ)
+        except lzma.LZMAError as e:
+            raise GraphLoadError("Failed to decompress file") from e
+    try:
+        return data.decode("utf-8")
+    except UnicodeDecodeError as e:
+        raise GraphLoadError(f"invalid utf-8 in {path!r}") from e
+
+
 def generate_routing_info(graph: NetworkGraph, node_ids: set, use_shortest_paths: bool = True) -> RoutingInfo:
     """sim_config.rs:424-461: GML ids of in-use nodes -> NodeIndex list -> table."""
     nodes = np.array([graph.node_id_to_index(x) for x in node_ids], np.uint32)
