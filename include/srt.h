@@ -202,6 +202,25 @@ srt_status srt_packet_batch(srt_plan *plan, const srt_pkt *d_pkts, const uint32_
                             const srt_round *round, uint32_t *d_flags, uint64_t *d_deliver,
                             uint64_t *d_counters, uint64_t *d_stats, srt_err *err);
 
+/* Batched Worker::push_packet_to_host (worker.rs:629-639) for the packets
+ * srt_packet_batch marked SENT: each becomes Event::new_packet
+ * (core/work/event.rs:20-31) whose src_host_event_id is its source host's
+ * next event id (Host::get_new_event_id, host.rs:691-695) in send order, and
+ * each destination host's events come out in its event queue's pop order:
+ * deliver time, then source host id, then event id (event.rs:85-150).  Host
+ * index order (the packet grouping of srt_packet_batch) is HostId order.
+ * All pointers are DEVICE pointers.  dst_host: destination host of every
+ * packet (< n_dst_hosts).  event_base: per source host, its next event id
+ * (advanced in place by its number of sent packets).  Outputs: event_id per
+ * packet (UINT64_MAX for packets not sent); order[0 .. n_sent): the sent
+ * packets' indices grouped by destination host, each group in pop order;
+ * dst_ptr[0 .. n_dst_hosts]: group offsets (dst_ptr[n_dst_hosts] = n_sent).
+ * Synchronises the plan's stream (destination range check). */
+srt_status srt_packet_events(srt_plan *plan, const uint32_t *d_host_pkt_ptr, uint32_t n_hosts, uint64_t n_pkts,
+                             const uint32_t *d_flags, const uint64_t *d_deliver, const uint32_t *d_dst_host,
+                             uint32_t n_dst_hosts, uint64_t *d_event_base, uint64_t *d_event_id,
+                             uint32_t *d_order, uint32_t *d_dst_ptr, srt_err *err);
+
 /* --------------------------------------------------------------- GML ingest */
 /* Parses Shadow GML text (gml-parser grammar + NetworkGraph validation) into a
  * library-owned graph; srt_gml_csr exposes its petgraph adjacency. */

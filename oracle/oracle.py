@@ -259,3 +259,35 @@ def packet_batch(lat, loss, pkts: np.ndarray, rng: np.ndarray, round_end, bootst
                           _p(rng, C.c_uint64), round_end, bootstrap_end, sim_end, _p(flags, C.c_uint32),
                           _p(deliver, C.c_uint64), cp, C.byref(mn), C.byref(ne))
     return flags, deliver, mn.value, ne.value
+
+
+def packet_events(host_ptr, flags, deliver, dst_host, n_dst_hosts, event_base):
+    """Restatement of Worker::push_packet_to_host (worker.rs:629-639) for a
+    batch, in the reference's own terms: walk the packets in send order (hosts
+    in HostId order), give every SENT packet Event::new_packet (event.rs:20-31)
+    with the source host's next event id (host.rs:691-695), push it on its
+    destination host's queue -- a binary heap ordered like Event (time, then
+    PacketEventData: src_host_id, then src_host_event_id; event.rs:85-150) --
+    and pop each queue empty.  event_base (per host, u64) is advanced in place.
+    Returns (event_id u64 per packet, UINT64_MAX if not sent; order u32 of the
+    sent packets by destination then pop order; dst_ptr u32[n_dst_hosts+1])."""
+    import heapq
+
+    host_ptr = np.asarray(host_ptr, np.int64)
+    m = len(flags)
+    event_id = np.full(m, np.iinfo(np.uint64).max, np.uint64)
+    queues = [[] for _ in range(n_dst_hosts)]
+    for h in range(len(host_ptr) - 1):
+        for p in range(int(host_ptr[h]), int(host_ptr[h + 1])):
+            if int(flags[p]) != PDS_INET_SENT:
+                continue
+            eid = int(event_base[h])
+            event_base[h] = np.uint64(eid + 1)
+            event_id[p] = eid
+            heapq.heappush(queues[int(dst_host[p])], (int(deliver[p]), h, eid, p))
+    order, dst_ptr = [], [0]
+    for q in queues:
+        while q:
+            order.append(heapq.heappop(q)[3])
+        dst_ptr.append(len(order))
+    return event_id, np.array(order, np.uint32), np.array(dst_ptr, np.uint32)

@@ -96,6 +96,8 @@ SIGNATURES = {
     "srt_plan_bind_comm": (C.c_int, [_vp, _vp, _errp]),
     "srt_packet_batch": (C.c_int, [_vp, _vp, _vp, C.c_uint32, C.c_uint64, _vp, C.POINTER(SrtRound), _vp, _vp, _vp,
                                    _vp, _errp]),
+    "srt_packet_events": (C.c_int, [_vp, _vp, C.c_uint32, C.c_uint64, _vp, _vp, _vp, C.c_uint32, _vp, _vp, _vp,
+                                    _vp, _errp]),
     "srt_gml_parse": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(_vp), _errp]),
     "srt_gml_csr": (C.c_int, [_vp, C.POINTER(SrtCsr)]),
     "srt_gml_free": (None, [_vp]),

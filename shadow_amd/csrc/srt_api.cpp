@@ -207,6 +207,7 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_smask);
     hipFree(p->d_sflag);
     hipFree(p->d_rstats);
+    hipFree(p->d_ev_scratch);
     if (p->h_sflag) hipHostFree(p->h_sflag);
 }
 

@@ -1,0 +1,175 @@
+// srt_events.hip -- batched packet-event push for one round.
+//
+// Reference: Worker::push_packet_to_host (src/main/core/worker.rs:629-639)
+// wraps every packet send_packet marked SENT in Event::new_packet
+// (core/work/event.rs:20-31) -- src_host_event_id = the source host's next
+// event id, Host::get_new_event_id (host/host.rs:691-695), taken in send
+// order -- and pushes it on the destination host's event queue, which pops
+// events by (time, then data): packet data orders by (src_host_id,
+// src_host_event_id) (event.rs:85-150).
+//
+// Here, for the whole batch at once: (A) one lane per source host walks its
+// packets in send order and hands out event ids to the sent ones; (B) the sent
+// packets are sorted by (destination host, deliver time) with two stable LSD
+// radix sorts (rocPRIM), starting from batch order -- which is (source host,
+// send order), i.e. (src_host_id, src_host_event_id) order, since host
+// segments are laid out by host index == HostId order; (C) per destination
+// host the offsets of its events in that order (its queue's pop order).
+#include <cstring>
+
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include "srt_internal.h"
+
+namespace {
+
+// (A) event ids; keys for (B)
+__global__ __launch_bounds__(64) void event_id_kernel(const uint32_t *__restrict__ host_ptr, uint32_t n_hosts,
+                                                      const uint32_t *__restrict__ flags,
+                                                      uint64_t *__restrict__ base, uint64_t *__restrict__ event_id) {
+    const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= n_hosts) return;
+    uint64_t next = base[h];
+    const uint32_t b = host_ptr[h], e = host_ptr[h + 1];
+    for (uint32_t p = b; p < e; ++p) event_id[p] = flags[p] == SRT_PDS_INET_SENT ? next++ : ~0ull;
+    base[h] = next;
+}
+
+__global__ void event_keys_kernel(const uint32_t *__restrict__ flags, const uint64_t *__restrict__ deliver,
+                                  uint64_t n, uint64_t *__restrict__ ktime, uint32_t *__restrict__ idx) {
+    for (uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; p < n; p += (uint64_t)gridDim.x * blockDim.x) {
+        ktime[p] = flags[p] == SRT_PDS_INET_SENT ? deliver[p] : ~0ull;
+        idx[p] = (uint32_t)p;
+    }
+}
+
+// destination key in time order; unsent packets sort last (key n_dst)
+__global__ void event_dst_keys_kernel(const uint32_t *__restrict__ idx, const uint32_t *__restrict__ flags,
+                                      const uint32_t *__restrict__ dst, uint32_t n_dst, uint64_t n,
+                                      uint32_t *__restrict__ kdst, uint32_t *__restrict__ bad) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t p = idx[i];
+        uint32_t k = n_dst;
+        if (flags[p] == SRT_PDS_INET_SENT) {
+            k = dst[p];
+            if (k >= n_dst) {
+                atomicOr(bad, 1u);
+                k = n_dst;
+            }
+        }
+        kdst[i] = k;
+    }
+}
+
+// (C) dst_ptr[d] = first position of destination d in the sorted keys
+__global__ void event_dst_ptr_kernel(const uint32_t *__restrict__ kdst, uint64_t n, uint32_t n_dst,
+                                     uint32_t *__restrict__ dst_ptr) {
+    const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d > n_dst) return;
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) / 2;
+        if (kdst[mid] < d) lo = mid + 1;
+        else hi = mid;
+    }
+    dst_ptr[d] = (uint32_t)lo;
+}
+
+void set_err(srt_err *err, srt_status code, const char *msg) {
+    if (!err) return;
+    err->code = code;
+    std::snprintf(err->msg, sizeof err->msg, "%s", msg);
+}
+
+int bit_width(uint32_t x) {
+    int b = 0;
+    while (x) {
+        ++b;
+        x >>= 1;
+    }
+    return b;
+}
+
+}  // namespace
+
+extern "C" srt_status srt_packet_events(srt_plan *plan, const uint32_t *d_host_pkt_ptr, uint32_t n_hosts,
+                                        uint64_t n_pkts, const uint32_t *d_flags, const uint64_t *d_deliver,
+                                        const uint32_t *d_dst_host, uint32_t n_dst_hosts, uint64_t *d_event_base,
+                                        uint64_t *d_event_id, uint32_t *d_order, uint32_t *d_dst_ptr,
+                                        srt_err *err) {
+    if (err) std::memset(err, 0, sizeof *err);
+    if (!plan || !d_host_pkt_ptr || !d_dst_ptr || (n_hosts && !d_event_base) ||
+        (n_pkts && (!d_flags || !d_deliver || !d_dst_host || !d_event_id || !d_order))) {
+        set_err(err, SRT_ERR_INVALID, "null argument");
+        return SRT_ERR_INVALID;
+    }
+    if (n_pkts >= 0xffffffffull || n_dst_hosts >= 0xffffffffu) {
+        set_err(err, SRT_ERR_INVALID, "more than 2^32-2 packets or destination hosts in one batch");
+        return SRT_ERR_INVALID;
+    }
+    if (hipSetDevice(plan->device) != hipSuccess) return SRT_ERR_HIP;
+    hipStream_t s = plan->stream;
+    const uint32_t n = (uint32_t)n_pkts;
+    if (n_hosts)
+        hipLaunchKernelGGL(event_id_kernel, dim3((n_hosts + 63) / 64), dim3(64), 0, s, d_host_pkt_ptr, n_hosts, d_flags,
+                           d_event_base, d_event_id);
+    if (!n) {
+        hipLaunchKernelGGL(event_dst_ptr_kernel, dim3(n_dst_hosts / 256 + 1), dim3(256), 0, s,
+                           (const uint32_t *)nullptr, 0ull, n_dst_hosts, d_dst_ptr);
+        return hipGetLastError() == hipSuccess ? SRT_OK : SRT_ERR_HIP;
+    }
+    // scratch: ktime[2n] u64, idx[2n] u32, kdst[2n] u32, bad flag, rocPRIM temp
+    const int dbits = bit_width(n_dst_hosts);  // keys 0..n_dst_hosts
+    size_t t1 = 0, t2 = 0;
+    rocprim::radix_sort_pairs((void *)nullptr, t1, (uint64_t *)nullptr, (uint64_t *)nullptr, (uint32_t *)nullptr,
+                              (uint32_t *)nullptr, n, 0, 64, s);
+    rocprim::radix_sort_pairs((void *)nullptr, t2, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                              (uint32_t *)nullptr, n, 0, (unsigned)std::max(dbits, 1), s);
+    const size_t temp = std::max(t1, t2);
+    const size_t need = 16ull * n + 16ull * n + 256 + temp;
+    if (need > plan->ev_scratch_cap) {
+        if (plan->d_ev_scratch) (void)hipFree(plan->d_ev_scratch);
+        plan->d_ev_scratch = nullptr;
+        plan->ev_scratch_cap = 0;
+        if (hipMalloc(&plan->d_ev_scratch, need) != hipSuccess) {
+            set_err(err, SRT_ERR_OOM, "hipMalloc(event scratch) failed");
+            return SRT_ERR_OOM;
+        }
+        plan->ev_scratch_cap = need;
+    }
+    char *sp = (char *)plan->d_ev_scratch;
+    uint64_t *ktime = (uint64_t *)sp, *ktime_s = ktime + n;
+    uint32_t *idx = (uint32_t *)(ktime_s + n), *idx1 = idx + n;
+    uint32_t *kdst = idx1 + n, *kdst_s = kdst + n;
+    uint32_t *bad = kdst_s + n;
+    void *tmp = (char *)(bad) + 256;
+    (void)hipMemsetAsync(bad, 0, sizeof(uint32_t), s);
+    const uint32_t blocks = std::min<uint32_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(event_keys_kernel, dim3(blocks), dim3(256), 0, s, d_flags, d_deliver, (uint64_t)n, ktime, idx);
+    size_t ts = temp;
+    if (rocprim::radix_sort_pairs(tmp, ts, ktime, ktime_s, idx, idx1, n, 0, 64, s) != hipSuccess) {
+        set_err(err, SRT_ERR_HIP, "radix sort (deliver time) failed");
+        return SRT_ERR_HIP;
+    }
+    hipLaunchKernelGGL(event_dst_keys_kernel, dim3(blocks), dim3(256), 0, s, idx1, d_flags, d_dst_host, n_dst_hosts,
+                       (uint64_t)n, kdst, bad);
+    ts = temp;
+    if (rocprim::radix_sort_pairs(tmp, ts, kdst, kdst_s, idx1, d_order, n, 0, (unsigned)std::max(dbits, 1), s) !=
+        hipSuccess) {
+        set_err(err, SRT_ERR_HIP, "radix sort (destination host) failed");
+        return SRT_ERR_HIP;
+    }
+    hipLaunchKernelGGL(event_dst_ptr_kernel, dim3(n_dst_hosts / 256 + 1), dim3(256), 0, s, kdst_s, (uint64_t)n,
+                       n_dst_hosts, d_dst_ptr);
+    uint32_t h_bad = 0;
+    if (hipMemcpyAsync(&h_bad, bad, sizeof h_bad, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+        set_err(err, SRT_ERR_HIP, "packet events: stream failed");
+        return SRT_ERR_HIP;
+    }
+    if (h_bad) {
+        set_err(err, SRT_ERR_INVALID, "destination host index out of range");
+        return SRT_ERR_INVALID;
+    }
+    return SRT_OK;
+}

@@ -93,6 +93,8 @@ struct srt_plan {
     srt_path *d_pack = nullptr;             // AoS staging for fetch
     uint64_t *d_draws = nullptr;            // packet stage: one RNG draw per packet
     uint64_t draws_cap = 0;
+    void *d_ev_scratch = nullptr;           // packet events: sort keys + rocPRIM temp
+    size_t ev_scratch_cap = 0;
 
     // host copies needed after create
     std::vector<uint32_t> nodes;

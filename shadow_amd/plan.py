@@ -101,6 +101,23 @@ class RoutingPlan:
             pass
 
     # ---------------------------------------------------------------- packets
+    def packet_events(self, host_ptr, flags, deliver, dst_host, n_dst_hosts: int, event_base, event_id, order,
+                      dst_ptr):
+        """srt_packet_events (worker.rs:629-639 + event.rs:85-150) on torch CUDA
+        tensors of this plan's device: host_ptr int32 [n_hosts+1], flags int32,
+        deliver int64, dst_host int32 [n_pkts], event_base int64 [n_hosts]
+        (advanced in place); outputs event_id int64 [n_pkts], order int32
+        [n_pkts] (first dst_ptr[-1] meaningful), dst_ptr int32 [n_dst_hosts+1]."""
+        import torch
+
+        torch.cuda.ExternalStream(self.stream_ptr(), device=flags.device).wait_stream(
+            torch.cuda.current_stream(flags.device))
+        err = _lib.SrtErr()
+        _lib.check(_lib.lib().srt_packet_events(
+            self._h, host_ptr.data_ptr(), host_ptr.numel() - 1, flags.numel(), flags.data_ptr(), deliver.data_ptr(),
+            dst_host.data_ptr(), n_dst_hosts, event_base.data_ptr(), event_id.data_ptr(), order.data_ptr(),
+            dst_ptr.data_ptr(), C.byref(err)), err)
+
     def packet_batch(self, pkts, host_ptr, rng, round_end_ns: int, bootstrap_end_ns: int, sim_end_ns: int,
                      flags, deliver, counters=None, stats=None, sync: bool = True):
         """All array arguments are torch CUDA tensors on this plan's device:
