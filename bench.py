@@ -311,6 +311,22 @@ def bench_packets(args, cfg, D):
     D.barrier()
     elapsed = D.max_over_ranks(time.perf_counter() - t0)
     dev_ms = ev0.elapsed_time(ev1) / args.steps
+    # the round's event push (srt_packet_events, worker.rs:629-639), timed
+    # after the headline loop on the last round's flags: reported beside the
+    # decision rate, not folded into it
+    dst_host = ((pk["dst_row"].astype(np.int64) + n_nodes * (np.arange(n_pkts) % max(1, hosts // n_nodes)))
+                % hosts).astype(np.int32)
+    t_dh = torch.from_numpy(dst_host).to(dev)
+    t_base = torch.zeros(hosts, dtype=torch.int64, device=dev)
+    t_eid = torch.zeros(n_pkts, dtype=torch.int64, device=dev)
+    t_ord = torch.zeros(n_pkts, dtype=torch.int32, device=dev)
+    t_ptr = torch.zeros(hosts + 1, dtype=torch.int32, device=dev)
+    ev_reps = max(3, args.steps)
+    plan.packet_events(t_hp, t_f, t_d, t_dh, hosts, t_base, t_eid, t_ord, t_ptr)
+    te0 = time.perf_counter()
+    for _ in range(ev_reps):
+        plan.packet_events(t_hp, t_f, t_d, t_dh, hosts, t_base, t_eid, t_ord, t_ptr)
+    events_ms = (time.perf_counter() - te0) * 1e3 / ev_reps
     out = None
     if D.rank == 0:
         per_round = elapsed / args.steps
@@ -341,6 +357,9 @@ def bench_packets(args, cfg, D):
                          "kernel": "draw_kernel + decide_kernel (one round)", "device_ms_per_round": dev_ms,
                          "basis": "52 B/packet + 64 B/host (SURVEY.md 8(d))"},
             "cpu_baseline": cpu,
+            "events": {"ms_per_round": events_ms, "sent": int(t_ptr[-1].item()),
+                       "what": "srt_packet_events on the round's sent packets: per-host event ids, sort to each "
+                               "destination host's queue pop order (host-synchronised call, wall clock)"},
         }
     plan.close()
     return out

@@ -110,13 +110,15 @@ class RoutingPlan:
         [n_pkts] (first dst_ptr[-1] meaningful), dst_ptr int32 [n_dst_hosts+1]."""
         import torch
 
-        torch.cuda.ExternalStream(self.stream_ptr(), device=flags.device).wait_stream(
-            torch.cuda.current_stream(flags.device))
+        ps = torch.cuda.ExternalStream(self.stream_ptr(), device=flags.device)
+        cur = torch.cuda.current_stream(flags.device)
+        ps.wait_stream(cur)
         err = _lib.SrtErr()
         _lib.check(_lib.lib().srt_packet_events(
             self._h, host_ptr.data_ptr(), host_ptr.numel() - 1, flags.numel(), flags.data_ptr(), deliver.data_ptr(),
             dst_host.data_ptr(), n_dst_hosts, event_base.data_ptr(), event_id.data_ptr(), order.data_ptr(),
             dst_ptr.data_ptr(), C.byref(err)), err)
+        cur.wait_stream(ps)  # torch-side consumers see the outputs (device-side ordering)
 
     def packet_batch(self, pkts, host_ptr, rng, round_end_ns: int, bootstrap_end_ns: int, sim_end_ns: int,
                      flags, deliver, counters=None, stats=None, sync: bool = True):

@@ -137,3 +137,18 @@ def test_gpu_events_edge_cases():
     dst[0] = 3
     with pytest.raises(_lib.SrtError, match="out of range"):
         _gpu_events(plan, host_ptr, flags, deliver, dst, 3, base)
+
+
+@gpu
+def test_gpu_events_wide_time_span():
+    """deliver times spanning ~2^60 ns with 40 destinations: the time and
+    destination bits exceed 64, so the two-sort path runs."""
+    host_ptr, flags, deliver, dst, n_dst, base = _random_batch(4, n_hosts=50, n_pkts=20_000, n_dst=40)
+    rng = np.random.default_rng(4)
+    deliver = (rng.integers(0, 8, size=len(deliver)).astype(np.uint64) << np.uint64(57)) + deliver
+    plan = _plan()
+    ob = base.copy()
+    eid_o, ord_o, ptr_o = O.packet_events(host_ptr, flags, deliver, dst, n_dst, ob)
+    eid, order, ptr, nb = _gpu_events(plan, host_ptr, flags, deliver, dst, n_dst, base)
+    assert np.array_equal(eid, eid_o) and np.array_equal(order, ord_o) and np.array_equal(ptr, ptr_o)
+    assert np.array_equal(nb, ob)
