@@ -76,7 +76,7 @@ int main(int argc, char **argv) {
         act[src] |= 1ull << s;
         pend[src] |= 1ull << s;
     }
-    uint64_t relax = 0, lines = 0, scans = 0;
+    uint64_t relax = 0, lines = 0, lines32 = 0, lines_loss = 0, scans = 0;
     uint32_t t = 0;
     for (;;) {
         int any_pend = 0;
@@ -91,12 +91,19 @@ int main(int argc, char **argv) {
                 if (!a) continue;
                 for (int q = 0; q < 4; ++q)
                     if ((a >> (16 * q)) & 0xffffull) ++lines;
+                for (int q = 0; q < 2; ++q)
+                    if ((a >> (32 * q)) & 0xffffffffull) ++lines32;
+                uint64_t need = 0;  /* split layout: lanes whose candidate latency can win */
                 for (int s = 0; s < 64; ++s)
                     if ((a >> s) & 1) {
                         ++relax;
                         const uint64_t d = D[(uint64_t)u * 64 + s];
+                        const uint64_t cur = best[s] < D[(uint64_t)v * 64 + s] ? best[s] : D[(uint64_t)v * 64 + s];
+                        if (d != UINT64_MAX && d + iw[k] <= cur) need |= 1ull << s;
                         if (d != UINT64_MAX && d + iw[k] < best[s]) best[s] = d + iw[k];
                     }
+                for (int q = 0; q < 2; ++q)
+                    if ((need >> (32 * q)) & 0xffffffffull) ++lines_loss;
             }
             uint64_t imp = 0;
             for (int s = 0; s < 64; ++s)
@@ -122,7 +129,7 @@ int main(int argc, char **argv) {
         if (!any_pend || t > 100000) break;
     }
     printf("{\"delta\": %u, \"cap\": %u, \"sweeps\": %u, \"relax_per_vs\": %.3f, \"lines_per_source\": %.1f, "
-           "\"edge_scans_per_sweep\": %.0f}\n",
-           DELTA, SWEEP_CAP, t, (double)relax / ((double)V * 64), (double)lines / 64.0, (double)scans / t);
+           "\"edge_scans_per_sweep\": %.0f, \"lines32_per_source\": %.1f, \"loss_lines32_per_source\": %.1f}\n",
+           DELTA, SWEEP_CAP, t, (double)relax / ((double)V * 64), (double)lines / 64.0, (double)scans / t, (double)lines32 / 64.0, (double)lines_loss / 64.0);
     return 0;
 }
