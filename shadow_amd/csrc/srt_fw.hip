@@ -99,13 +99,14 @@ __device__ __forceinline__ void relax_row8<double>(double (&acc)[8], double a, c
 }
 
 // ------------------------------------------------------------------ init
+// rows [r0, r1) of D: 0 on the diagonal, +inf elsewhere
 template <typename K>
-__global__ void fill_kernel(K *__restrict__ D, uint32_t Vp) {
-    const uint64_t total = (uint64_t)Vp * Vp;
+__global__ void fill_kernel(K *__restrict__ D, uint32_t Vp, uint32_t r0, uint32_t r1) {
+    const uint64_t first = (uint64_t)r0 * Vp, total = (uint64_t)(r1 - r0) * Vp;
     for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < total;
          e += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t r = (uint32_t)(e / Vp), c = (uint32_t)(e % Vp);
-        D[e] = (r == c) ? KeyOps<K>::zero() : KeyOps<K>::inf();
+        const uint32_t r = (uint32_t)((first + e) / Vp), c = (uint32_t)((first + e) % Vp);
+        D[first + e] = (r == c) ? KeyOps<K>::zero() : KeyOps<K>::inf();
     }
 }
 
@@ -129,11 +130,11 @@ __global__ void scatter_edges_kernel(K *__restrict__ D, uint32_t Vp,
                                      const uint64_t *__restrict__ row_ptr,
                                      const uint32_t *__restrict__ col,
                                      const uint64_t *__restrict__ lat,
-                                     const float *__restrict__ loss, uint32_t V, KeyParams kp) {
+                                     const float *__restrict__ loss, uint32_t u0, uint32_t u1, KeyParams kp) {
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    for (uint32_t u = wave; u < V; u += nwaves) {
+    for (uint32_t u = u0 + wave; u < u1; u += nwaves) {
         const uint64_t b = row_ptr[u], e = row_ptr[u + 1];
         for (uint64_t k = b + lane; k < e; k += 64) {
             const uint32_t v = col[k];
@@ -700,13 +701,17 @@ __global__ void pack_kernel(const uint64_t *__restrict__ lat, const float *__res
 template <typename K>
 void fw_init_t(srt_plan *p) {
     K *D = reinterpret_cast<K *>(p->d_D);
-    hipLaunchKernelGGL(fill_kernel<K>, dim3(4096), dim3(256), 0, p->stream, D, p->Vp);
+    // sharded: only the local block-rows -- every other row this rank ever
+    // reads arrives whole first (pivot-row broadcasts, the final all-gather)
+    const uint32_t r0 = p->comm ? p->rb0 * B : 0, r1 = p->comm ? p->rb1 * B : p->Vp;
+    const uint32_t u0 = std::min(r0, p->V), u1 = std::min(r1, p->V);
+    hipLaunchKernelGGL(fill_kernel<K>, dim3(4096), dim3(256), 0, p->stream, D, p->Vp, r0, r1);
     if (p->fw_unique_edges)
         hipLaunchKernelGGL((scatter_edges_kernel<K, true>), dim3(2048), dim3(256), 0, p->stream, D, p->Vp,
-                           p->d_row_ptr, p->d_col, p->d_lat, p->d_loss, p->V, p->kp);
+                           p->d_row_ptr, p->d_col, p->d_lat, p->d_loss, u0, u1, p->kp);
     else
         hipLaunchKernelGGL((scatter_edges_kernel<K, false>), dim3(2048), dim3(256), 0, p->stream, D, p->Vp,
-                           p->d_row_ptr, p->d_col, p->d_lat, p->d_loss, p->V, p->kp);
+                           p->d_row_ptr, p->d_col, p->d_lat, p->d_loss, u0, u1, p->kp);
 }
 
 // Measurement only (N-rank emulation): stands in for the pivot-row broadcast
