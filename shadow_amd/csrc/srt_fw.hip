@@ -770,7 +770,13 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
     const uint32_t emu = (!p->comm && p->emulate_ranks > 1) ? p->emulate_ranks : 0;
     const uint32_t rb0 = p->rb0, rb1 = emu ? std::max<uint32_t>(1, nblk / emu) : p->rb1;
     const bool sharded = p->comm != nullptr;  // a 1-rank comm runs the same schedule (tested)
-    p->fw_small_chain = (sharded || emu) && !std::getenv("SRT_FW_NO_SMALL_CHAIN");  // knob: A/B timing
+    // quarter-tile chain kernels whenever a round's rest() is short (sharded
+    // ranks; one GPU below ~8 tile-waves of rest, e.g. 4k nodes: 8.4 -> 7.0 ms),
+    // where the chain, not rest, would set the round period; knobs force it
+    // on / off for A/B timing
+    const uint64_t rest_tiles = (uint64_t)(rb1 - rb0) * nblk;
+    p->fw_small_chain = std::getenv("SRT_FW_SMALL_CHAIN") != nullptr ||
+                        ((sharded || emu || rest_tiles < 8ull * 512) && !std::getenv("SRT_FW_NO_SMALL_CHAIN"));
     const uint32_t per_rank = sharded ? nblk / p->comm->nranks : nblk;
     const size_t pivot_bytes = (size_t)B * p->Vp * sizeof(K);
     hipStream_t M = p->stream, S = p->side_stream, C = p->comm_stream;
