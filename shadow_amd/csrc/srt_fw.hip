@@ -818,27 +818,36 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
     // broadcasts follow the prologue's
     hipEventRecord(p->ev_cross, M);
     hipStreamWaitEvent(C, p->ev_cross, 0);
+    hipEvent_t rest_done = p->ev_cross;  // the latest point S's next cross tiles wait for
     for (uint32_t kb = 0; kb < nblk; ++kb) {
         const bool nxt = kb + 1 < nblk;
         const uint32_t k1 = kb + 1;
-        // host order matters: both events are re-recorded every round, and a
-        // wait binds to the record enqueued before it
-        if (nxt) hipStreamWaitEvent(S, p->ev_cross, 0);  // rest(kb-1) (or the prologue) done
-        if (kb) hipStreamWaitEvent(M, p->ev_pivot, 0);    // pivot kb ready (round 0: stream order)
+        // host order matters: ev_cross / ev_pivot are re-recorded every round,
+        // and a wait binds to the record enqueued before it
+        if (nxt) hipStreamWaitEvent(S, rest_done, 0);  // rest(kb-1) (or the prologue) done
+        if (kb) hipStreamWaitEvent(M, p->ev_pivot, 0);  // pivot kb ready (round 0: stream order)
         // rest(kb): local rows and all columns, minus kb and (look-ahead) k1
         Rect rest{make_span(rb0, rb1, kb, nxt ? k1 : NONE), make_span(0, nblk, kb, nxt ? k1 : NONE)};
         const uint32_t nt = rest.r.n * rest.c.n;
         if (nt && kb % ev_every == 0) {
             hipEventRecord(p->ev[2 * p->p3_launches], M);
             launch_tiles<K, 0>(p, M, kb, rest, none);
-            hipEventRecord(p->ev[2 * p->p3_launches + 1], M);
+            // the timing event after rest(kb) doubles as S's hand-off (one
+            // event packet fewer per round on the main stream)
+            rest_done = p->ev[2 * p->p3_launches + 1];
+            hipEventRecord(rest_done, M);
             p->p3_launches++;
             p->p3_work += (double)nt * B * B * B;
-        } else if (nt) {
-            launch_tiles<K, 0>(p, M, kb, rest, none);
+        } else {
+            if (nt) launch_tiles<K, 0>(p, M, kb, rest, none);
+            if (nxt) {
+                hipEventRecord(p->ev_cross, M);
+                rest_done = p->ev_cross;
+            }
         }
         if (nxt) {
-            hipEventRecord(p->ev_cross, M);  // for round k1's cross tiles on S
+            // for round k1's cross tiles on S: rest_done (waited at the top of
+            // the next iteration)
             // cross(kb) on S, concurrent with rest(kb) (disjoint tiles; both
             // read only the pivot-kb row and column): column k1 of the local
             // rows (+ row k1 on its owner)
