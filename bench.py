@@ -94,7 +94,7 @@ def cpu_baseline(og, nodes, threads, sources, label, target_s=15.0, mode=0):
                       f"extrapolated linearly to pairs/s"}
 
 
-def measured_traffic(tag, kernel_tag):
+def measured_traffic(args, kernel_tag):
     """HBM bytes per launch of the dominant kernel from the latest committed
     PMC summary (profiles/rNN_pmc_traffic.json: FETCH_SIZE and WRITE_SIZE
     passes of rocprofv3 on this same workload, gfx950 corrections applied), or
@@ -103,7 +103,10 @@ def measured_traffic(tag, kernel_tag):
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
     for f in reversed(files):
         d = json.load(open(f))
-        if tag not in d.get("config", ""):
+        # summaries are labelled "C3 16k complete graph, 1 GPU": match the
+        # config name, and the node count too when --nodes overrides it
+        cfg = d.get("config", "")
+        if not cfg.startswith(args.config.upper() + " ") or (args.nodes and str(args.nodes) not in cfg):
             continue
         for k, v in d.get("kernels", {}).items():
             if kernel_tag in k:
@@ -191,7 +194,15 @@ def bench_graph(args, cfg, D):
     plan = RoutingPlan(g, nodes, device=D.dev)
     if D.world > 1:
         from shadow_amd import dist as sdist
-        sdist.bind(plan, D.rank, D.world, D.local_rank, transport=os.environ.get("SRT_COMM", "rccl"))
+        transport = os.environ.get("SRT_COMM", "rccl")
+        try:
+            sdist.bind(plan, D.rank, D.world, D.local_rank, transport=transport)
+        except Exception as e:  # noqa: BLE001 -- a native RCCL init failure falls back to torch's RCCL group
+            if transport != "rccl":
+                raise
+            print(f"[rank {D.rank}] native RCCL communicator failed ({e}); using torch.distributed collectives",
+                  file=sys.stderr, flush=True)
+            sdist.bind(plan, D.rank, D.world, D.local_rank, transport="torch")
     desc = plan.describe()
     elapsed, step_ms, k_ms, k_launches, k_work = timed_builds(plan, D, args.steps, args.warmup)
     if args.emulate_ranks > 1:
@@ -211,7 +222,7 @@ def bench_graph(args, cfg, D):
         if desc.startswith("fw"):
             B_TILE = 128
             achieved = work_per_launch / avg_launch_s
-            traffic, traffic_src = measured_traffic(str(n), "phase 3 rest")
+            traffic, traffic_src = measured_traffic(args, "phase 3 rest")
             if D.world > 1:  # the committed PMC pass is of the 1-GPU launch (all 126^2 tiles)
                 traffic, traffic_src = None, "PMC traffic is profiled at N=1 only"
             roofline = {
@@ -219,7 +230,7 @@ def bench_graph(args, cfg, D):
                 "frac": achieved / RELAX_PEAK, "traffic": traffic, "traffic_unit": "HBM bytes per launch",
                 "traffic_source": traffic_src,
                 "algorithmic_hbm_bytes_per_launch": work_per_launch / B_TILE * 2 * 8,
-                "kernel": "minplus_tile_kernel<double, 0> (FW phase 3, rest)", "avg_launch_ms": avg_launch_s * 1e3,
+                "kernel": "minplus_glds_kernel<double, 0> (FW phase 3, rest)", "avg_launch_ms": avg_launch_s * 1e3,
                 "relax_per_launch": work_per_launch,
                 "peak_basis": f"{F64_LANE_OPS_PEAK / 1e12:.1f}e12 f64 VALU lane-ops/s / {OPS_PER_RELAX} ops "
                               f"(v_add_f64 + v_min_f64) per relaxation; the SURVEY's INT-VALU basis (5 int32 ops "
@@ -227,7 +238,7 @@ def bench_graph(args, cfg, D):
             algo = "blocked Floyd-Warshall"
         else:
             achieved = work_per_launch / avg_launch_s
-            traffic, traffic_src = measured_traffic(str(n), "sssp_sweep")
+            traffic, traffic_src = measured_traffic(args, "sssp_sweep")
             roofline = {
                 "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK, "traffic": traffic, "traffic_source": traffic_src,
