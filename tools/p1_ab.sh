@@ -1,26 +1,11 @@
 #!/bin/bash
-# Phase-1 shape A/B (SRT_FW_P1_ROWS): parity for each shape, then 1-GPU C3
-# and emulated N-rank timings, then a kernel trace of the emulated run.
+# Phase-1 shape A/B (SRT_FW_P1_ROWS = rows per thread: 8 -> 256 threads, 4 -> 512, 2 -> 1024):
+# C2 build time and the phase-1 kernel's average duration under rocprofv3.
 export TMPDIR=/tmp
-R=${GRAFT_REPO_ROOT:-$PWD}
-O=$R/gpurun_out/${1:-p1}
-N=${2:-8}
-mkdir -p $O
-cd $R
-for r in 4 2; do
-  SRT_FW_P1_ROWS=$r timeout -k 10 300 python -u -m pytest tests/test_gpu_apsp.py tests/test_golden.py -x -q --timeout 120 --timeout-method thread > $O/pytest_r$r.txt 2>&1
-  rc=$?; echo "rows=$r $(tail -1 $O/pytest_r$r.txt)"; [ $rc -eq 0 ] || exit $rc
+R=$GRAFT_REPO_ROOT; mkdir -p $R/gpurun_out
+for r in 8 4 2; do
+  cd $R && SRT_FW_P1_ROWS=$r timeout -k 10 120 python -u bench.py --config c2 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/p1_$r.txt 2>&1 || exit 1
+  python3 -c "import json;d=json.loads(open('gpurun_out/p1_$r.txt').read().strip().splitlines()[-1]);print('rows=$r c2 ms', round(d['ms_per_step'],3))"
+  cd /tmp && SRT_FW_P1_ROWS=$r timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/p1prof$r -o run --output-format csv -- python3 $R/bench.py --config c2 --steps 3 --warmup 1 --no-cpu-baseline > $R/gpurun_out/p1prof$r.log 2>&1 || exit 1
+  grep phase1 $R/gpurun_out/p1prof$r/run_kernel_stats.csv | cut -d, -f2-7
 done
-run() {  # tag, emu, env...
-  local tag=$1 emu=$2; shift 2
-  env "$@" timeout -k 10 200 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --emulate-ranks $emu > $O/$tag.json 2>&1 || return 1
-  python -c "import json; d=json.loads(open('$O/$tag.json').read().strip().splitlines()[-1]); print('$tag', round(d['ms_per_step'],2), d.get('roofline',{}).get('frac'))"
-}
-for emu in $N 1; do
-  for r in 8 4 2; do run e${emu}_r$r $emu SRT_FW_P1_ROWS=$r || exit 1; done
-done
-cd /tmp
-for r in 4 2; do
-SRT_FW_P1_ROWS=$r timeout -k 10 300 rocprofv3 --kernel-trace -d $O/tr$r -o run --output-format csv -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --emulate-ranks $N > $O/trace_log$r.txt 2>&1 || exit 1
-done
-echo traced
