@@ -21,7 +21,10 @@ def _port():
 
 
 @pytest.mark.parametrize("world,n,seed,algo", [(2, 300, 1, "fw"), (3, 520, 2, "fw"), (2, 301, 3, "sssp"),
-                                                (3, 200, 4, "sssp")])
+                                                (3, 200, 4, "sssp"),
+                                                # the driver's 8-rank layout: 16 block-rows, the pivot
+                                                # owner changes every 2 rounds
+                                                (8, 1100, 5, "fw"), (8, 700, 6, "sssp")])
 def test_sharded_build_matches_oracle(world, n, seed, algo):
     port = _port()
     env = dict(os.environ)
