@@ -206,6 +206,7 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_sD);
     hipFree(p->d_smask);
     hipFree(p->d_sflag);
+    hipFree(p->d_sact);
     hipFree(p->d_rstats);
     hipFree(p->d_ev_scratch);
     if (p->h_sflag) hipHostFree(p->h_sflag);
@@ -491,6 +492,12 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         PLAN_TRY(dmalloc(&p->d_sD, (size_t)p->sssp_nb * p->V * 64, err));
         PLAN_TRY(dmalloc(&p->d_smask, (size_t)2 * p->sssp_nb * p->V, err));
         PLAN_TRY(dmalloc(&p->d_sflag, (size_t)3 * p->sssp_nb, err));
+        if (const char *e = std::getenv("SRT_SSSP_ACT")) {
+            const int k = std::atoi(e);
+            p->sssp_act_on = k != 0;
+            p->sssp_act_from = k > 1 ? (uint32_t)k : 0u;
+        }
+        if (p->sssp_act_on) PLAN_TRY(dmalloc(&p->d_sact, (size_t)3 * (p->sssp_nb / p->sssp_r) * p->V, err));
         if ((e = hipHostMalloc((void **)&p->h_sflag, (size_t)p->sssp_nb * sizeof(uint32_t), 0)) != hipSuccess) {
             srt_plan_destroy(p);
             return hip_fail(err, e, "hipHostMalloc");

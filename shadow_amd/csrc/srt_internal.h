@@ -123,6 +123,9 @@ struct srt_plan {
     uint64_t *d_sD = nullptr;            // sssp_nb * V * 64 keys
     uint64_t *d_smask = nullptr;         // 2 * sssp_nb * V change masks
     uint32_t *d_sflag = nullptr;         // 3 * sssp_nb convergence flags
+    uint8_t *d_sact = nullptr;           // 3 * groups * V target-activation bytes (tail sweeps)
+    bool sssp_act_on = true;             // knob SRT_SSSP_ACT=0 turns target activation off
+    uint32_t sssp_act_from = 0;          // knob SRT_SSSP_ACT=k>1: from sweep k (0: from the last launch)
     uint32_t *h_sflag = nullptr;         // pinned host copy
     uint32_t sssp_nb = 0;                // 64-source words in flight (groups x sssp_r)
     uint32_t sssp_r = 1;                 // 64-source words per lane (group = 64 * sssp_r sources)

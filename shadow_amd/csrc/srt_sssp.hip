@@ -84,11 +84,21 @@ __global__ void sssp_seed_kernel(uint64_t *__restrict__ D, uint64_t *__restrict_
 // R*64 sources of its group.  Per chunk of 64 in-edges every lane loads one
 // edge and the R change masks of its source vertex; edges whose source changed
 // are walked 4 at a time with up to 4*R predicated gathers in flight.
+//
+// Target activation (tail sweeps, act_mode != 0): act[3][g][v] is a byte ring.
+// With ACT_SET a wave that improved v marks v's out-neighbours (CSR row v,
+// self-loop skipped) in act[(t+1)%3] with plain byte stores (all writers write
+// 1); with ACT_USE sweep t skips every target not marked in act[t%3] -- none of
+// its in-neighbours changed in sweep t-1, so processing it would find no active
+// edge -- and only stores its all-zero next masks.  Sweep t clears
+// act[(t+2)%3], the slot sweep t+1 marks (read in t-1, so free in t).
+constexpr uint32_t ACT_USE = 1, ACT_SET = 2;
 template <int R>
 __global__ __launch_bounds__(SWP_WAVES * 64) void sssp_sweep_kernel(
     const uint64_t *__restrict__ in_ptr, const InEdge *__restrict__ in_edge, uint32_t V,
     uint64_t *D, const uint64_t *__restrict__ mask_cur, uint64_t *__restrict__ mask_next,
-    uint32_t *flag, uint32_t t) {
+    uint32_t *flag, uint32_t t, const uint64_t *__restrict__ row_ptr, const uint32_t *__restrict__ col,
+    uint8_t *act, uint32_t act_mode) {
     const uint32_t g = blockIdx.y, G = gridDim.y;
     if (blockIdx.x == 0 && threadIdx.x == 0) flag[((t + 1) % 3) * G + g] = 0;  // for sweep t+1
     if (t > 0 && flag[((t + 2) % 3) * G + g] == 0) return;                     // converged
@@ -99,6 +109,14 @@ __global__ __launch_bounds__(SWP_WAVES * 64) void sssp_sweep_kernel(
     const uint32_t v = __builtin_amdgcn_readfirstlane(blockIdx.x * SWP_WAVES + (threadIdx.x >> 6));
     if (v >= V) return;
     const uint64_t base = (uint64_t)g * V;  // first vertex row of the group
+    const uint64_t aslot = (uint64_t)G * V;  // bytes per ring slot
+    if (act_mode) {
+        if (lane == 0) act[((t + 2) % 3) * aslot + base + v] = 0;
+        if ((act_mode & ACT_USE) && act[(t % 3) * aslot + base + v] == 0) {
+            if (lane < R) mask_next[(base + v) * R + lane] = 0;
+            return;
+        }
+    }
     const uint64_t *Dg = D + base * R * 64;
     const uint64_t *mc = mask_cur + base * R;
     uint64_t best[R];
@@ -180,6 +198,13 @@ __global__ __launch_bounds__(SWP_WAVES * 64) void sssp_sweep_kernel(
 #pragma unroll
         for (int r = 0; r < R; ++r) mask_next[(base + v) * R + r] = m_out[r];
         if (imp_any) flag[(t % 3) * G + g] = 1;  // idempotent store, no atomic
+    }
+    if ((act_mode & ACT_SET) && imp_any) {
+        uint8_t *nxt = act + ((t + 1) % 3) * aslot + base;
+        for (uint64_t k = row_ptr[v] + lane; k < row_ptr[v + 1]; k += 64) {
+            const uint32_t w = col[k];
+            if (w != v) nxt[w] = 1;
+        }
     }
 }
 
@@ -272,9 +297,9 @@ __global__ void reduce_rank_stats_kernel(const unsigned long long *rstats, int n
 }  // namespace
 
 template <int R>
-void launch_sweep(dim3 grid, hipStream_t s, srt_plan *p, uint64_t *mc, uint64_t *mn, uint32_t t) {
+void launch_sweep(dim3 grid, hipStream_t s, srt_plan *p, uint64_t *mc, uint64_t *mn, uint32_t t, uint32_t act_mode) {
     hipLaunchKernelGGL(sssp_sweep_kernel<R>, grid, dim3(SWP_WAVES * 64), 0, s, p->d_in_ptr, p->d_in_edge, p->V,
-                       p->d_sD, mc, mn, p->d_sflag, t);
+                       p->d_sD, mc, mn, p->d_sflag, t, p->d_row_ptr, p->d_col, p->d_sact, act_mode);
 }
 
 // Whole build for this rank's table rows [row0, row1), G groups of R*64
@@ -295,7 +320,7 @@ srt_status sssp_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
         (void)hipEventCreateWithFlags(&e, 0);
         p->ev.push_back(e);
     }
-    uint32_t chunk = 8;
+    uint32_t chunk = 8, t_prev = 0;
     for (uint32_t li = 0; li < launches; ++li) {
         const uint32_t g0 = p->row0 + li * per_launch;
         const uint32_t rows = std::min<uint32_t>(per_launch, p->row1 - g0);
@@ -305,16 +330,23 @@ srt_status sssp_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
                            G * R, G);
         hipLaunchKernelGGL(sssp_seed_kernel, dim3((nbat * 64 + 255) / 256), dim3(256), 0, M, p->d_sD, p->d_smask,
                            p->d_nodes, V, g0, g0 + rows, nbat, R);
+        if (p->sssp_act_on) (void)hipMemsetAsync(p->d_sact, 0, 3ull * G * V, M);
         (void)hipEventRecord(p->ev[2 * li], M);
         const dim3 grid((V + SWP_WAVES - 1) / SWP_WAVES, G);
+        // activation starts where the previous launch's sweeps thinned out
+        // (SRT_SSSP_ACT: knob; the first launch has no history)
+        uint32_t t_on = 0;
+        if (p->sssp_act_on) t_on = p->sssp_act_from ? p->sssp_act_from : (t_prev ? std::max<uint32_t>(1, t_prev * 5 / 8) : 0);
         uint32_t t = 0;
         for (;;) {
             for (uint32_t c = 0; c < chunk; ++c, ++t) {
                 uint64_t *mc = p->d_smask + (uint64_t)(t & 1) * G * R * V;
                 uint64_t *mn = p->d_smask + (uint64_t)((t + 1) & 1) * G * R * V;
-                if (R == 4) launch_sweep<4>(grid, M, p, mc, mn, t);
-                else if (R == 2) launch_sweep<2>(grid, M, p, mc, mn, t);
-                else launch_sweep<1>(grid, M, p, mc, mn, t);
+                // target activation from sweep t_on (the tail; sweep t_on-1 marks)
+                const uint32_t am = (t_on && t + 1 >= t_on) ? (ACT_SET | (t >= t_on ? ACT_USE : 0u)) : 0u;
+                if (R == 4) launch_sweep<4>(grid, M, p, mc, mn, t, am);
+                else if (R == 2) launch_sweep<2>(grid, M, p, mc, mn, t, am);
+                else launch_sweep<1>(grid, M, p, mc, mn, t, am);
             }
             // flags of the last sweep (t-1): all zero == converged
             hipError_t e = hipMemcpyAsync(p->h_sflag, p->d_sflag + ((t - 1) % 3) * G, G * sizeof(uint32_t),
@@ -344,6 +376,7 @@ srt_status sssp_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
         p->sssp_sweeps += t;
         // the next launch starts with as many sweeps as this one needed
         chunk = std::max<uint32_t>(t, 4);
+        t_prev = t;
         hipLaunchKernelGGL(sssp_emit_kernel, dim3((p->n + 63) / 64, G * R), dim3(256), 0, M, p->d_sD, V, R,
                            p->d_nodes, p->n, g0, g0 + rows, p->sssp_g, p->d_sl_lat, p->d_sl_loss, p->d_out_lat,
                            p->d_out_loss, d_stats);

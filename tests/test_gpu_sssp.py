@@ -152,3 +152,20 @@ def test_fw_and_sssp_agree_on_latency():
     b = g.compute_shortest_paths(nodes, algo=SSSP)
     assert np.array_equal(a.latency_ns, b.latency_ns)
     assert np.abs(a.packet_loss.astype(np.float64) - b.packet_loss).max() <= 1e-6
+
+
+@pytest.mark.parametrize("act", ["2", "3", "0"])
+@pytest.mark.parametrize("directed", [False, True])
+def test_target_activation_bit_exact(monkeypatch, act, directed):
+    """Tail-sweep target activation (srt_sssp.hip ACT_SET/ACT_USE): forced on
+    from an early sweep (SRT_SSSP_ACT=k) or off, the sweep must return the same
+    bits as the oracle -- a target is skipped only when no in-neighbour changed.
+    Directed graphs take the out-neighbour marks from the outgoing CSR rows."""
+    monkeypatch.setenv("SRT_SSSP_ACT", act)
+    n = 700
+    if directed:
+        edges = synth.random_graph(n, 11, p_edge=0.012, directed=True, lat_range_ns=(1, 40), loss_max=0.05)
+    else:
+        edges = synth.barabasi_albert(n, 3, 12)
+    nodes = np.arange(0, n, 2, dtype=np.uint32)
+    _check(edges, nodes, directed, n)
