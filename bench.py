@@ -150,19 +150,20 @@ def timed_builds(plan, D, steps, warmup):
         plan.run()
     D.barrier()
     step_ms = []
-    k_ms, k_launches, k_work = 0.0, 0, 0.0
+    k_ms, k_launches, k_work, k_tiles = 0.0, 0, 0.0, 0
     t_all0 = time.perf_counter()
     for _ in range(steps):
         t0 = time.perf_counter()
         plan.run()
         step_ms.append((time.perf_counter() - t0) * 1e3)
         a, b, w, _ = plan.kernel_stats()
+        k_tiles += plan.kernel_tiles()
         k_ms += a
         k_launches += b
         k_work += w
     D.barrier()
     elapsed = D.max_over_ranks(time.perf_counter() - t_all0)
-    return elapsed, step_ms, k_ms, k_launches, k_work
+    return elapsed, step_ms, k_ms, k_launches, k_work, k_tiles
 
 
 def bench_graph(args, cfg, D):
@@ -204,7 +205,7 @@ def bench_graph(args, cfg, D):
                   file=sys.stderr, flush=True)
             sdist.bind(plan, D.rank, D.world, D.local_rank, transport="torch")
     desc = plan.describe()
-    elapsed, step_ms, k_ms, k_launches, k_work = timed_builds(plan, D, args.steps, args.warmup)
+    elapsed, step_ms, k_ms, k_launches, k_work, k_tiles = timed_builds(plan, D, args.steps, args.warmup)
     if args.emulate_ranks > 1:
         print(json.dumps({"emulated_ranks": args.emulate_ranks, "config": args.config, "ms_per_step":
                           elapsed * 1e3 / args.steps, "rest_ms_per_step": k_ms / args.steps,
@@ -229,7 +230,9 @@ def bench_graph(args, cfg, D):
                 "bound": "valu", "achieved": achieved / 1e12, "peak": RELAX_PEAK / 1e12, "unit": "Trelax/s",
                 "frac": achieved / RELAX_PEAK, "traffic": traffic, "traffic_unit": "HBM bytes per launch",
                 "traffic_source": traffic_src,
-                "algorithmic_hbm_bytes_per_launch": work_per_launch / B_TILE * 2 * 8,
+                # every C tile read + written once per launch (A/B panels hit L2/MALL)
+                "algorithmic_hbm_bytes_per_launch": k_tiles / max(k_launches, 1) * B_TILE * B_TILE * 2 * 8,
+                "rounds_per_tile": k_work / max(k_tiles * B_TILE ** 3, 1),  # 2: paired rounds (1 GPU)
                 "kernel": "minplus_glds_kernel<double, 0> (FW phase 3, rest)", "avg_launch_ms": avg_launch_s * 1e3,
                 "relax_per_launch": work_per_launch,
                 "peak_basis": f"{F64_LANE_OPS_PEAK / 1e12:.1f}e12 f64 VALU lane-ops/s / {OPS_PER_RELAX} ops "

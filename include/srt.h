@@ -140,6 +140,10 @@ void *srt_plan_stream(srt_plan *plan);
 srt_status srt_plan_kernel_stats(const srt_plan *plan, double *dominant_ms,
                                  uint64_t *dominant_launches, double *dominant_work,
                                  double *total_ms);
+/* C tiles (128 x 128 keys) the last FW run's dominant launches loaded and
+ * stored, summed over those launches (0 for the SSSP sweep): the algorithmic
+ * C traffic is tiles x 128^2 x 2 x sizeof(key). */
+srt_status srt_plan_kernel_tiles(const srt_plan *plan, uint64_t *dominant_tiles);
 void srt_plan_destroy(srt_plan *plan);
 
 /* -------------------------------------------------------- multi-GPU (RCCL) */

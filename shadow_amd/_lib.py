@@ -86,6 +86,7 @@ SIGNATURES = {
     "srt_plan_table": (C.c_int, [_vp, C.POINTER(_vp), C.POINTER(_vp), _u32p]),
     "srt_plan_describe": (C.c_char_p, [_vp]),
     "srt_plan_stream": (_vp, [_vp]),
+    "srt_plan_kernel_tiles": (C.c_int, [_vp, _u64p]),
     "srt_plan_kernel_stats": (C.c_int, [_vp, C.POINTER(C.c_double), _u64p, C.POINTER(C.c_double),
                                         C.POINTER(C.c_double)]),
     "srt_plan_destroy": (None, [_vp]),

@@ -652,6 +652,12 @@ srt_status srt_plan_kernel_stats(const srt_plan *p, double *dominant_ms, uint64_
     return SRT_OK;
 }
 
+srt_status srt_plan_kernel_tiles(const srt_plan *p, uint64_t *tiles) {
+    if (!p) return SRT_ERR_INVALID;
+    if (tiles) *tiles = p->p3_tiles;
+    return SRT_OK;
+}
+
 void srt_plan_destroy(srt_plan *p) {
     if (!p) return;
     hipSetDevice(p->device);

@@ -443,7 +443,7 @@ __device__ __forceinline__ void chunk_steps(double (&acc)[TR][TC], StepOps (&o)[
 
 template <typename K, int TAG>
 __global__ __launch_bounds__(NT3, 2) void minplus_glds_kernel(K *__restrict__ D, uint32_t Vp, uint32_t kb,
-                                                           Rect r1, Rect r2) {
+                                                           Rect r1, Rect r2, uint32_t kb2) {
     static_assert(sizeof(K) == 8, "8-byte keys");
     __shared__ K lds[2 * GBUF];
     // the look-ahead chain (phase 2 row/col, cross) shares SIMDs with the
@@ -464,7 +464,18 @@ __global__ __launch_bounds__(NT3, 2) void minplus_glds_kernel(K *__restrict__ D,
         bi = span_at(r2.r, t / r2.c.n);
         bj = span_at(r2.c, t % r2.c.n);
     }
-    const uint64_t i0 = (uint64_t)bi * B, j0 = (uint64_t)bj * B, k0 = (uint64_t)kb * B;
+    // paired rounds (kb2 = kb + 1, see fw_rounds_pair_t): chunks [0, NCH) are
+    // round kb's update, [NCH, 2 NCH) round kb2's.  A tile in row/column kb
+    // had round kb as phase 2 (on the chain) and runs only round kb2's half; a
+    // tile in row/column kb2 is all chain work and exits.
+    constexpr int NCH = B / KC;
+    int ch0 = 0, ch1 = NCH;
+    if (kb2 != NONE) {
+        if (bi == kb2 || bj == kb2) return;  // workgroup-uniform, before any barrier
+        ch0 = (bi == kb || bj == kb) ? NCH : 0;
+        ch1 = 2 * NCH;
+    }
+    const uint64_t i0 = (uint64_t)bi * B, j0 = (uint64_t)bj * B;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int tx = tid % 16, ty = tid / 16;
@@ -478,12 +489,13 @@ __global__ __launch_bounds__(NT3, 2) void minplus_glds_kernel(K *__restrict__ D,
     }
     // 32 wave-instructions of 1 KiB per chunk, 8 per wave: 4 A pieces (8 rows
     // each) and 4 B rows
-    auto stage = [&](int kc, int buf) {
+    auto stage = [&](int ch, int buf) {
+        const uint64_t kk = (uint64_t)(ch < NCH ? kb : kb2) * B + (ch % NCH) * KC;  // first k row of the chunk
         K *img = lds + buf * GBUF;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int piece = wave * 4 + q;  // rows piece*8 .. +7
-            const K *g = D + (i0 + piece * 8 + lane / 8) * Vp + k0 + kc + (lane % 8) * 2;
+            const K *g = D + (i0 + piece * 8 + lane / 8) * Vp + kk + (lane % 8) * 2;
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
                                              (__attribute__((address_space(3))) void *)(img + piece * APIECE), 16,
                                              0, 0);
@@ -491,20 +503,19 @@ __global__ __launch_bounds__(NT3, 2) void minplus_glds_kernel(K *__restrict__ D,
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int kr = wave * 4 + q;  // B row
-            const K *g = D + (k0 + kc + kr) * Vp + j0 + lane * 2;
+            const K *g = D + (kk + kr) * Vp + j0 + lane * 2;
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
                                              (__attribute__((address_space(3))) void *)(img + AIMG + kr * B), 16,
                                              0, 0);
         }
     };
-    stage(0, 0);
+    stage(ch0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    constexpr int NCH = B / KC;
 #pragma unroll 1
-    for (int ch = 0; ch < NCH; ++ch) {
-        const int cur = ch & 1;
-        if (ch + 1 < NCH) stage((ch + 1) * KC, cur ^ 1);  // the other buffer's readers passed the last barrier
+    for (int ch = ch0; ch < ch1; ++ch) {
+        const int cur = (ch - ch0) & 1;
+        if (ch + 1 < ch1) stage(ch + 1, cur ^ 1);  // the other buffer's readers passed the last barrier
         const K *As = lds + cur * GBUF + ty * APIECE;     // the thread's A piece
         const K *Bs = lds + cur * GBUF + AIMG + tx;       // the thread's first B column
         if constexpr (std::is_same<K, double>::value) {
@@ -740,7 +751,7 @@ void launch_tiles(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1, const
                            reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2);
     else if (p->fw_glds)
         hipLaunchKernelGGL((minplus_glds_kernel<K, TAG>), dim3(n), dim3(NT3), 0, s,
-                           reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2);
+                           reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2, NONE);
     else
         hipLaunchKernelGGL((minplus_tile_kernel<K, TAG>), dim3(n), dim3(NT3), 0, s,
                            reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2);
@@ -759,6 +770,9 @@ void launch_tiles(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1, const
 // (Measured before, with cross(kb) on M: 10 us gaps either side of it and a
 // half-empty GPU during it, 3.4% of the 16k build on one GPU.)  Single GPU =
 // one rank, no broadcast.
+template <typename K>
+srt_status fw_rounds_pair_t(srt_plan *p, int p1r);
+
 template <typename K>
 srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
     K *D = reinterpret_cast<K *>(p->d_D);
@@ -805,6 +819,13 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
         hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, p->device);
         emu_bcast_ticks = (long long)(std::atof(e) * khz / 1000.0);
     }
+    // one GPU, rest-bound (no quarter-tile chain), even block count: paired
+    // rounds (knob SRT_FW_NO_PAIR for A/B timing)
+    // (SRT_FW_PAIR forces it at chain-bound sizes too: parity tests)
+    if (!sharded && !emu && p->fw_glds && (!p->fw_small_chain || std::getenv("SRT_FW_PAIR")) && nblk % 2 == 0 &&
+        nblk >= 4 && !std::getenv("SRT_FW_NO_PAIR"))
+        return fw_rounds_pair_t<K>(p, p1r);
+    p->p3_tiles = 0;
     srt_status st = SRT_OK;
     // prologue: pivot 0
     if (own(0)) {
@@ -838,6 +859,7 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
             hipEventRecord(rest_done, M);
             p->p3_launches++;
             p->p3_work += (double)nt * B * B * B;
+            p->p3_tiles += nt;
         } else {
             if (nt) launch_tiles<K, 0>(p, M, kb, rest, none);
             if (nxt) {
@@ -892,6 +914,87 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
     hipStreamWaitEvent(M, p->ev_bcast, 0);
     if (sharded)
         return comm_allgather_inplace(p->comm, D, (size_t)per_rank * B * p->Vp * sizeof(K), M, err);
+    return SRT_OK;
+}
+
+// One GPU, rest-bound sizes: rounds are fused in pairs (a, a+1), a even, so
+// each rest tile is loaded and stored once per two rounds (the per-tile
+// prologue/epilogue both workgroups of a CU wait out together is ~9% of a
+// single-round launch) and there are half as many rest launches.
+//   chain (pivots a, a+1) = p1(a), p2row(a), p2col(a); round a on row/col
+//       a+1 (cross); p1(a+1), p2row(a+1), p2col(a+1)
+//   F(a) on M = rounds a and a+1 on every tile outside rows/cols a+2, a+3
+//       (tiles in row/col a: round a+1 only; row/col a+1: nothing)
+//   X(a+2) on S = the same two rounds on rows/cols a+2, a+3 (overlaps F(a)),
+//       then the chain of pivots a+2, a+3.
+// Round a+1's operands D(i, a+1), D(a+1, j) are final chain output; round a's
+// D(i, a) may be lowered by round a+1 in the same launch while other tiles read
+// it -- a tighter key of a real path, so the FW invariant holds and the closure
+// is the same bits (the argument of the look-ahead chain and the broadcast).
+template <typename K>
+void launch_pair(srt_plan *p, hipStream_t s, uint32_t a, const Rect &r1, const Rect &r2, bool chain) {
+    const uint32_t n = r1.r.n * r1.c.n + r2.r.n * r2.c.n;
+    if (!n) return;
+    K *D = reinterpret_cast<K *>(p->d_D);
+    if (chain)
+        hipLaunchKernelGGL((minplus_glds_kernel<K, 5>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, a + 1);
+    else
+        hipLaunchKernelGGL((minplus_glds_kernel<K, 0>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, a + 1);
+}
+
+template <typename K>
+srt_status fw_rounds_pair_t(srt_plan *p, int p1r) {
+    K *D = reinterpret_cast<K *>(p->d_D);
+    const uint32_t nblk = p->Vp / B;
+    hipStream_t M = p->stream, S = p->side_stream;
+    const Rect none{make_span(0, 0), make_span(0, 0)};
+    // pivots a and a+1 on stream s (rows/cols a, a+1 already hold rounds < a)
+    auto pivots = [&](hipStream_t s, uint32_t a) {
+        const uint32_t b = a + 1;
+        launch_p1<K>(p1r, s, D, p->Vp, a);
+        launch_tiles<K, 1>(p, s, a, Rect{make_span(a, a + 1), make_span(0, nblk, a)}, none);
+        launch_tiles<K, 2>(p, s, a, Rect{make_span(0, nblk, a), make_span(a, a + 1)}, none);
+        launch_tiles<K, 4>(p, s, a, Rect{make_span(0, nblk, a, b), make_span(b, b + 1)},
+                           Rect{make_span(b, b + 1), make_span(0, nblk, a)});
+        launch_p1<K>(p1r, s, D, p->Vp, b);
+        launch_tiles<K, 1>(p, s, b, Rect{make_span(b, b + 1), make_span(0, nblk, b)}, none);
+        launch_tiles<K, 2>(p, s, b, Rect{make_span(0, nblk, b), make_span(b, b + 1)}, none);
+    };
+    p->p3_launches = 0;
+    p->p3_work = 0.0;
+    p->p3_tiles = 0;
+    const size_t need = nblk + 2;
+    while (p->ev.size() < need) {
+        hipEvent_t e;
+        hipEventCreateWithFlags(&e, std::getenv("SRT_FW_TIMING_FENCE") ? 0u : (unsigned)hipEventDisableSystemFence);
+        p->ev.push_back(e);
+    }
+    pivots(M, 0);
+    hipEventRecord(p->ev_cross, M);
+    hipEvent_t rest_done = p->ev_cross;
+    for (uint32_t a = 0; a < nblk; a += 2) {
+        const bool nxt = a + 2 < nblk;
+        const uint32_t c0 = nxt ? a + 2 : NONE, c1 = nxt ? a + 3 : NONE;
+        if (nxt) hipStreamWaitEvent(S, rest_done, 0);  // F(a-2) (or the prologue) done
+        if (a) hipStreamWaitEvent(M, p->ev_pivot, 0);  // pivots a, a+1 ready
+        const Rect all{make_span(0, nblk, c0, c1), make_span(0, nblk, c0, c1)};
+        hipEventRecord(p->ev[2 * p->p3_launches], M);
+        launch_pair<K>(p, M, a, all, none, false);
+        rest_done = p->ev[2 * p->p3_launches + 1];
+        hipEventRecord(rest_done, M);
+        p->p3_launches++;
+        const double m = all.r.n;  // tiles outside rows/cols a..a+1: both rounds; row/col a: round a+1 only
+        p->p3_work += (2.0 * (m - 2) * (m - 2) + 2.0 * (m - 2) + 1.0) * B * B * B;
+        p->p3_tiles += (uint64_t)((m - 1) * (m - 1));
+        if (nxt) {
+            // X(a+2): rows/cols a+2, a+3 through rounds a, a+1 (the row part's
+            // col a+1 tiles exit at once)
+            launch_pair<K>(p, S, a, Rect{make_span(0, nblk, a + 1), make_span(a + 2, a + 4)},
+                           Rect{make_span(a + 2, a + 4), make_span(0, nblk, a + 2, a + 3)}, true);
+            pivots(S, a + 2);
+            hipEventRecord(p->ev_pivot, S);
+        }
+    }
     return SRT_OK;
 }
 

@@ -109,6 +109,7 @@ struct srt_plan {
     hipEvent_t ev_row = nullptr, ev_bcast = nullptr;    // S -> C (row ready), C -> S/M (row received)
     uint64_t p3_launches = 0;
     double p3_work = 0.0;  // relaxations done by the timed launches
+    uint64_t p3_tiles = 0;  // C tiles those launches loaded and stored
     double p3_ms = 0.0, total_ms = 0.0;
     bool ran = false;
 

@@ -68,6 +68,12 @@ class RoutingPlan:
         _lib.lib().srt_plan_kernel_stats(self._h, C.byref(a), C.byref(b), C.byref(w), C.byref(c))
         return a.value, b.value, w.value, c.value
 
+    def kernel_tiles(self) -> int:
+        """C tiles the last run's dominant (FW rest) launches loaded and stored."""
+        t = C.c_uint64()
+        _lib.lib().srt_plan_kernel_tiles(self._h, C.byref(t))
+        return t.value
+
     def stream_ptr(self) -> int:
         """hipStream_t the plan launches on (for HIP events on that stream)."""
         return _lib.lib().srt_plan_stream(self._h)
