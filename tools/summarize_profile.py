@@ -22,6 +22,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LABELS = {
     "minplus_glds_kernel<double, 0>": "phase 3 rest",
     "minplus_glds_kernel<double, 4>": "phase 3 cross",
+    "minplus_glds_kernel<double, 5>": "phase 3 cross (paired rounds)",
     "minplus_glds_kernel<double, 1>": "phase 2 row",
     "minplus_glds_kernel<double, 2>": "phase 2 col",
     "minplus_tile_kernel<double, 0>": "phase 3 rest",
