@@ -18,6 +18,7 @@
 // ops per relaxation) or as u64 (< 2^62: v_lshl_add_u64 + v_cmp_lt_u64 +
 // 2 v_cndmask = 4 ops).  Both give bit-identical tables; the host picks f64
 // whenever its bound proof fits in 53 bits.
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -230,12 +231,12 @@ __global__ __launch_bounds__(16 * (B / P1R)) void fw_phase1_kernel(K *__restrict
 //   phase 2 col:  bj = kb  (Bm = P*, A aliases C);
 //   phase 3:      bi, bj != kb.
 // A launch covers up to two rectangles of tiles, each rows x cols where a
-// Span is [lo, hi) minus up to two skipped block indices.  Aliased operands
+// Span is [lo, hi) minus one skipped range of block indices [x0, x1).  Aliased operands
 // are fully staged in LDS before C is written and each tile has exactly one
 // owner workgroup, so phase-2 tiles are safe to update in place.  TAG only
 // gives each use its own kernel symbol (rocprof attribution).
 struct Span {
-    uint32_t lo, hi, s0, s1, n;  // s0 < s1, NONE = 0xffffffff
+    uint32_t lo, hi, x0, x1, n;  // skipped [x0, x1) inside [lo, hi); none: x0 = NONE
 };
 struct Rect {
     Span r, c;
@@ -244,21 +245,23 @@ constexpr uint32_t NONE = 0xffffffffu;
 
 __host__ __device__ inline uint32_t span_at(const Span &s, uint32_t i) {
     uint32_t v = s.lo + i;
-    if (v >= s.s0) ++v;
-    if (v >= s.s1) ++v;
+    if (v >= s.x0) v += s.x1 - s.x0;
     return v;
 }
 
+// [lo, hi) minus [x0, x1) (clipped; empty or NONE: nothing skipped)
+inline Span make_range(uint32_t lo, uint32_t hi, uint32_t x0, uint32_t x1) {
+    if (x0 == NONE || x1 <= lo || x0 >= hi || x1 <= x0) return Span{lo, hi, NONE, NONE, hi - lo};
+    x0 = std::max(x0, lo);
+    x1 = std::min(x1, hi);
+    return Span{lo, hi, x0, x1, (hi - lo) - (x1 - x0)};
+}
+
+// [lo, hi) minus block a and (optionally) its neighbour b = a + 1
 inline Span make_span(uint32_t lo, uint32_t hi, uint32_t a = NONE, uint32_t b = NONE) {
-    uint32_t s0 = (a >= lo && a < hi) ? a : NONE, s1 = (b >= lo && b < hi) ? b : NONE;
-    if (s0 == s1) s1 = NONE;
-    if (s0 > s1) {
-        const uint32_t t = s0;
-        s0 = s1;
-        s1 = t;
-    }
-    const uint32_t n = (hi - lo) - (s0 != NONE) - (s1 != NONE);
-    return Span{lo, hi, s0, s1, n};
+    if (a == NONE) return make_range(lo, hi, NONE, NONE);
+    if (b != NONE && b != a + 1) std::abort();  // every schedule skips adjacent blocks
+    return make_range(lo, hi, a, b == NONE ? a + 1 : b + 1);
 }
 
 template <typename K, int TAG>
@@ -443,7 +446,7 @@ __device__ __forceinline__ void chunk_steps(double (&acc)[TR][TC], StepOps (&o)[
 
 template <typename K, int TAG>
 __global__ __launch_bounds__(NT3, 2) void minplus_glds_kernel(K *__restrict__ D, uint32_t Vp, uint32_t kb,
-                                                           Rect r1, Rect r2, uint32_t kb2) {
+                                                           Rect r1, Rect r2, uint32_t ng) {
     static_assert(sizeof(K) == 8, "8-byte keys");
     __shared__ K lds[2 * GBUF];
     // the look-ahead chain (phase 2 row/col, cross) shares SIMDs with the
@@ -464,16 +467,20 @@ __global__ __launch_bounds__(NT3, 2) void minplus_glds_kernel(K *__restrict__ D,
         bi = span_at(r2.r, t / r2.c.n);
         bj = span_at(r2.c, t % r2.c.n);
     }
-    // paired rounds (kb2 = kb + 1, see fw_rounds_pair_t): chunks [0, NCH) are
-    // round kb's update, [NCH, 2 NCH) round kb2's.  A tile in row/column kb
-    // had round kb as phase 2 (on the chain) and runs only round kb2's half; a
-    // tile in row/column kb2 is all chain work and exits.
+    // grouped rounds kb .. kb+ng-1 (ng > 1, see fw_rounds_group_t): chunks
+    // [r NCH, (r+1) NCH) are round kb+r's update.  A tile whose highest
+    // row/column index inside the group is q had rounds <= q done by the chain
+    // (phase 2 of q, the in-group cross before it) and runs rounds q+1 ..; a
+    // tile in row/column kb+ng-1 is all chain work and exits.
     constexpr int NCH = B / KC;
-    int ch0 = 0, ch1 = NCH;
-    if (kb2 != NONE) {
-        if (bi == kb2 || bj == kb2) return;  // workgroup-uniform, before any barrier
-        ch0 = (bi == kb || bj == kb) ? NCH : 0;
-        ch1 = 2 * NCH;
+    int ch0 = 0;
+    const int ch1 = (int)ng * NCH;
+    if (ng > 1) {
+        const uint32_t qi = bi - kb < ng ? bi - kb : 0u, qj = bj - kb < ng ? bj - kb : 0u;
+        const bool in = bi - kb < ng || bj - kb < ng;
+        const uint32_t q = std::max(qi, qj);
+        if (in && q == ng - 1) return;  // workgroup-uniform, before any barrier
+        ch0 = in ? (int)(q + 1) * NCH : 0;
     }
     const uint64_t i0 = (uint64_t)bi * B, j0 = (uint64_t)bj * B;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -490,7 +497,7 @@ __global__ __launch_bounds__(NT3, 2) void minplus_glds_kernel(K *__restrict__ D,
     // 32 wave-instructions of 1 KiB per chunk, 8 per wave: 4 A pieces (8 rows
     // each) and 4 B rows
     auto stage = [&](int ch, int buf) {
-        const uint64_t kk = (uint64_t)(ch < NCH ? kb : kb2) * B + (ch % NCH) * KC;  // first k row of the chunk
+        const uint64_t kk = (uint64_t)(kb + ch / NCH) * B + (ch % NCH) * KC;  // first k row of the chunk
         K *img = lds + buf * GBUF;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -751,7 +758,7 @@ void launch_tiles(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1, const
                            reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2);
     else if (p->fw_glds)
         hipLaunchKernelGGL((minplus_glds_kernel<K, TAG>), dim3(n), dim3(NT3), 0, s,
-                           reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2, NONE);
+                           reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2, 1u);
     else
         hipLaunchKernelGGL((minplus_tile_kernel<K, TAG>), dim3(n), dim3(NT3), 0, s,
                            reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2);
@@ -771,7 +778,7 @@ void launch_tiles(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1, const
 // half-empty GPU during it, 3.4% of the 16k build on one GPU.)  Single GPU =
 // one rank, no broadcast.
 template <typename K>
-srt_status fw_rounds_pair_t(srt_plan *p, int p1r);
+srt_status fw_rounds_group_t(srt_plan *p, int p1r, uint32_t g);
 
 template <typename K>
 srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
@@ -819,12 +826,16 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
         hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, p->device);
         emu_bcast_ticks = (long long)(std::atof(e) * khz / 1000.0);
     }
-    // one GPU, rest-bound (no quarter-tile chain), even block count: paired
-    // rounds (knob SRT_FW_NO_PAIR for A/B timing)
-    // (SRT_FW_PAIR forces it at chain-bound sizes too: parity tests)
-    if (!sharded && !emu && p->fw_glds && (!p->fw_small_chain || std::getenv("SRT_FW_PAIR")) && nblk % 2 == 0 &&
-        nblk >= 4 && !std::getenv("SRT_FW_NO_PAIR"))
-        return fw_rounds_pair_t<K>(p, p1r);
+    // one GPU, rest-bound (no quarter-tile chain): rounds in groups of g = 4
+    // (2 when the block count is not a multiple of 4; knob SRT_FW_GROUP=1/2/4
+    // for A/B timing, SRT_FW_PAIR forces grouping at chain-bound sizes too:
+    // parity tests)
+    uint32_t grp = (nblk % 4 == 0 && nblk >= 8) ? 4 : 2;
+    if (const char *e = std::getenv("SRT_FW_GROUP")) grp = (uint32_t)std::atoi(e);
+    if (std::getenv("SRT_FW_NO_PAIR")) grp = 1;
+    if (!sharded && !emu && p->fw_glds && (!p->fw_small_chain || std::getenv("SRT_FW_PAIR")) && grp > 1 &&
+        grp <= 8 && nblk % grp == 0 && nblk >= 2 * grp)
+        return fw_rounds_group_t<K>(p, p1r, grp);
     p->p3_tiles = 0;
     srt_status st = SRT_OK;
     // prologue: pivot 0
@@ -917,53 +928,55 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
     return SRT_OK;
 }
 
-// One GPU, rest-bound sizes: rounds are fused in pairs (a, a+1), a even, so
-// each rest tile is loaded and stored once per two rounds (the per-tile
-// prologue/epilogue both workgroups of a CU wait out together is ~9% of a
-// single-round launch) and there are half as many rest launches.
-//   chain (pivots a, a+1) = p1(a), p2row(a), p2col(a); round a on row/col
-//       a+1 (cross); p1(a+1), p2row(a+1), p2col(a+1)
-//   F(a) on M = rounds a and a+1 on every tile outside rows/cols a+2, a+3
-//       (tiles in row/col a: round a+1 only; row/col a+1: nothing)
-//   X(a+2) on S = the same two rounds on rows/cols a+2, a+3 (overlaps F(a)),
-//       then the chain of pivots a+2, a+3.
-// Round a+1's operands D(i, a+1), D(a+1, j) are final chain output; round a's
-// D(i, a) may be lowered by round a+1 in the same launch while other tiles read
-// it -- a tighter key of a real path, so the FW invariant holds and the closure
-// is the same bits (the argument of the look-ahead chain and the broadcast).
+// One GPU, rest-bound sizes: rounds are fused in groups of g (2 or 4) rounds
+// a .. a+g-1 (a a multiple of g), so each rest tile is loaded and stored once
+// per g rounds (the per-tile prologue/epilogue both workgroups of a CU wait out
+// together is ~9% of a single-round launch) and there are 1/g as many rest
+// launches, launch gaps and launch tails.
+//   chain (pivots of the group) = for r = a .. a+g-1: p1(r), p2row(r),
+//       p2col(r), then round r on rows/cols r+1 .. a+g-1 (in-group cross)
+//   F(a) on M = rounds a .. a+g-1 on every tile outside rows/cols of the next
+//       group (a tile whose highest in-group row/column is q runs rounds > q)
+//   X(a+g) on S = the same rounds on rows/cols a+g .. a+2g-1 (overlaps F(a)),
+//       then the chain of the next group.
+// Operands of round r > a are final chain output; round r's column D(i, r)
+// may be lowered by a later round of the same launch while other tiles read
+// it -- a tighter key of a real path, so the FW invariant holds and the
+// closure is the same bits (the argument of the look-ahead chain and the
+// broadcast).  Tiles that two rectangles of one launch both cover (the g x g
+// corners) are updated twice with the same inputs: min is idempotent.
 template <typename K>
-void launch_pair(srt_plan *p, hipStream_t s, uint32_t a, const Rect &r1, const Rect &r2, bool chain) {
+void launch_group(srt_plan *p, hipStream_t s, uint32_t a, uint32_t g, const Rect &r1, const Rect &r2, bool chain) {
     const uint32_t n = r1.r.n * r1.c.n + r2.r.n * r2.c.n;
     if (!n) return;
     K *D = reinterpret_cast<K *>(p->d_D);
     if (chain)
-        hipLaunchKernelGGL((minplus_glds_kernel<K, 5>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, a + 1);
+        hipLaunchKernelGGL((minplus_glds_kernel<K, 5>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, g);
     else
-        hipLaunchKernelGGL((minplus_glds_kernel<K, 0>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, a + 1);
+        hipLaunchKernelGGL((minplus_glds_kernel<K, 0>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, g);
 }
 
 template <typename K>
-srt_status fw_rounds_pair_t(srt_plan *p, int p1r) {
+srt_status fw_rounds_group_t(srt_plan *p, int p1r, uint32_t g) {
     K *D = reinterpret_cast<K *>(p->d_D);
     const uint32_t nblk = p->Vp / B;
     hipStream_t M = p->stream, S = p->side_stream;
     const Rect none{make_span(0, 0), make_span(0, 0)};
-    // pivots a and a+1 on stream s (rows/cols a, a+1 already hold rounds < a)
+    // the pivots of group a on stream s (rows/cols a .. a+g-1 already hold rounds < a)
     auto pivots = [&](hipStream_t s, uint32_t a) {
-        const uint32_t b = a + 1;
-        launch_p1<K>(p1r, s, D, p->Vp, a);
-        launch_tiles<K, 1>(p, s, a, Rect{make_span(a, a + 1), make_span(0, nblk, a)}, none);
-        launch_tiles<K, 2>(p, s, a, Rect{make_span(0, nblk, a), make_span(a, a + 1)}, none);
-        launch_tiles<K, 4>(p, s, a, Rect{make_span(0, nblk, a, b), make_span(b, b + 1)},
-                           Rect{make_span(b, b + 1), make_span(0, nblk, a)});
-        launch_p1<K>(p1r, s, D, p->Vp, b);
-        launch_tiles<K, 1>(p, s, b, Rect{make_span(b, b + 1), make_span(0, nblk, b)}, none);
-        launch_tiles<K, 2>(p, s, b, Rect{make_span(0, nblk, b), make_span(b, b + 1)}, none);
+        for (uint32_t r = a; r < a + g; ++r) {
+            launch_p1<K>(p1r, s, D, p->Vp, r);
+            launch_tiles<K, 1>(p, s, r, Rect{make_span(r, r + 1), make_span(0, nblk, r)}, none);
+            launch_tiles<K, 2>(p, s, r, Rect{make_span(0, nblk, r), make_span(r, r + 1)}, none);
+            if (r + 1 < a + g)  // round r on rows/cols r+1 .. a+g-1 (the corner twice: idempotent)
+                launch_tiles<K, 4>(p, s, r, Rect{make_span(0, nblk, r), make_range(r + 1, a + g, NONE, NONE)},
+                                   Rect{make_range(r + 1, a + g, NONE, NONE), make_span(0, nblk, r)});
+        }
     };
     p->p3_launches = 0;
     p->p3_work = 0.0;
     p->p3_tiles = 0;
-    const size_t need = nblk + 2;
+    const size_t need = 2 * (nblk / g) + 2;
     while (p->ev.size() < need) {
         hipEvent_t e;
         hipEventCreateWithFlags(&e, std::getenv("SRT_FW_TIMING_FENCE") ? 0u : (unsigned)hipEventDisableSystemFence);
@@ -972,26 +985,34 @@ srt_status fw_rounds_pair_t(srt_plan *p, int p1r) {
     pivots(M, 0);
     hipEventRecord(p->ev_cross, M);
     hipEvent_t rest_done = p->ev_cross;
-    for (uint32_t a = 0; a < nblk; a += 2) {
-        const bool nxt = a + 2 < nblk;
-        const uint32_t c0 = nxt ? a + 2 : NONE, c1 = nxt ? a + 3 : NONE;
-        if (nxt) hipStreamWaitEvent(S, rest_done, 0);  // F(a-2) (or the prologue) done
-        if (a) hipStreamWaitEvent(M, p->ev_pivot, 0);  // pivots a, a+1 ready
-        const Rect all{make_span(0, nblk, c0, c1), make_span(0, nblk, c0, c1)};
+    for (uint32_t a = 0; a < nblk; a += g) {
+        const bool nxt = a + g < nblk;
+        const uint32_t c0 = nxt ? a + g : NONE, c1 = a + 2 * g;
+        if (nxt) hipStreamWaitEvent(S, rest_done, 0);  // F(a-g) (or the prologue) done
+        if (a) hipStreamWaitEvent(M, p->ev_pivot, 0);  // the group's pivots ready
+        const Rect all{make_range(0, nblk, c0, c1), make_range(0, nblk, c0, c1)};
         hipEventRecord(p->ev[2 * p->p3_launches], M);
-        launch_pair<K>(p, M, a, all, none, false);
+        launch_group<K>(p, M, a, g, all, none, false);
         rest_done = p->ev[2 * p->p3_launches + 1];
         hipEventRecord(rest_done, M);
         p->p3_launches++;
-        const double m = all.r.n;  // tiles outside rows/cols a..a+1: both rounds; row/col a: round a+1 only
-        p->p3_work += (2.0 * (m - 2) * (m - 2) + 2.0 * (m - 2) + 1.0) * B * B * B;
-        p->p3_tiles += (uint64_t)((m - 1) * (m - 1));
+        // tiles (i, j) of the launch: with t = number of in-group indices
+        // above max(i,j)'s group position, rounds = g for out-of-group tiles
+        const double m = all.r.n, o = m - g;  // o: rows outside the group
+        double work = o * o * g, tiles = o * o;
+        for (uint32_t q = 0; q + 1 < g; ++q) {
+            // tiles whose highest in-group index is q: (q+1)^2 - q^2 inside, 2 * o * 1 mixed
+            const double cnt = (2.0 * q + 1) + 2.0 * o;
+            work += cnt * (g - 1 - q);
+            tiles += cnt;
+        }
+        p->p3_work += work * B * B * B;
+        p->p3_tiles += (uint64_t)tiles;
         if (nxt) {
-            // X(a+2): rows/cols a+2, a+3 through rounds a, a+1 (the row part's
-            // col a+1 tiles exit at once)
-            launch_pair<K>(p, S, a, Rect{make_span(0, nblk, a + 1), make_span(a + 2, a + 4)},
-                           Rect{make_span(a + 2, a + 4), make_span(0, nblk, a + 2, a + 3)}, true);
-            pivots(S, a + 2);
+            // X(a+g): rows/cols a+g .. a+2g-1 through the group's rounds
+            const Span nx = make_range(a + g, a + 2 * g, NONE, NONE);
+            launch_group<K>(p, S, a, g, Rect{make_span(0, nblk), nx}, Rect{nx, make_span(0, nblk)}, true);
+            pivots(S, a + g);
             hipEventRecord(p->ev_pivot, S);
         }
     }

@@ -1,10 +1,11 @@
-"""Paired-round Floyd-Warshall schedule (srt_fw.hip fw_rounds_pair_t) on gfx950.
+"""Grouped-round Floyd-Warshall schedule (srt_fw.hip fw_rounds_group_t) on gfx950.
 
-One GPU at rest-bound sizes (>= 64 blocks of 128) fuses FW rounds in pairs;
-SRT_FW_PAIR forces the paired schedule at small sizes and SRT_FW_NO_PAIR
-turns it off, so the same graph is closed both ways.  Bar: latency bit-exact
-vs the oracle (reference Dijkstra restatement), loss within 1e-6, and the
-paired table bit-identical to the single-round one (both compute the unique
+One GPU at rest-bound sizes (>= 64 blocks of 128) fuses FW rounds in groups
+of g = 4 (2 when the block count does not allow 4); SRT_FW_PAIR forces the
+grouped schedule at small sizes, SRT_FW_GROUP picks g and SRT_FW_NO_PAIR turns
+it off, so the same graph is closed every way.  Bar: latency bit-exact vs the
+oracle (reference Dijkstra restatement), loss within 1e-6, and the grouped
+table bit-identical to the single-round one (both compute the unique
 lexicographic minimum over paths of the exact integer keys).
 """
 import numpy as np
@@ -17,21 +18,27 @@ from tests.test_gpu_apsp import _check
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("group", ["2", "4"])
 @pytest.mark.parametrize("n,seed,directed", [(400, 0, False), (500, 1, True), (777, 2, False),
-                                             (1000, 3, True), (300, 4, False)])
-def test_forced_pair_vs_oracle(monkeypatch, n, seed, directed):
-    # 400/500 -> 4 blocks, 777/1000 -> 8 blocks (paired); 300 -> 3 blocks (odd:
-    # single-round fallback)
+                                             (1000, 3, True), (1500, 5, False), (300, 4, False)])
+def test_forced_groups_vs_oracle(monkeypatch, group, n, seed, directed):
+    # 400/500 -> 4 blocks, 777/1000 -> 8, 1500 -> 12 (g=4: 3 groups); 300 -> 3
+    # blocks (odd: single-round fallback); g=4 needs >= 8 blocks
     monkeypatch.setenv("SRT_FW_PAIR", "1")
+    monkeypatch.setenv("SRT_FW_GROUP", group)
     e = synth.random_graph(n, 40 + seed, p_edge=8.0 / n, directed=directed, lat_range_ns=(1, 6), loss_max=0.05)
     nodes = np.random.default_rng(seed).permutation(n).astype(np.uint32)
     _check(e, nodes, directed, n, algo=_lib.SRT_ALGO_FW)
 
 
-def _table(monkeypatch, g, nodes, pair):
-    monkeypatch.delenv("SRT_FW_PAIR", raising=False)
-    monkeypatch.delenv("SRT_FW_NO_PAIR", raising=False)
-    monkeypatch.setenv("SRT_FW_PAIR" if pair else "SRT_FW_NO_PAIR", "1")
+def _table(monkeypatch, g, nodes, group):
+    for k in ("SRT_FW_PAIR", "SRT_FW_NO_PAIR", "SRT_FW_GROUP"):
+        monkeypatch.delenv(k, raising=False)
+    if group > 1:
+        monkeypatch.setenv("SRT_FW_PAIR", "1")
+        monkeypatch.setenv("SRT_FW_GROUP", str(group))
+    else:
+        monkeypatch.setenv("SRT_FW_NO_PAIR", "1")
     plan = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_FW)
     try:
         plan.run()
@@ -44,21 +51,23 @@ def _table(monkeypatch, g, nodes, pair):
 
 
 @pytest.mark.parametrize("n", [2048, 8192])
-def test_pair_equals_single_round(monkeypatch, n):
-    src, dst, lat, loss = synth.complete_graph(n, 7) if n <= 2048 else (None,) * 4
+def test_groups_equal_single_round(monkeypatch, n):
     if n <= 2048:
+        src, dst, lat, loss = synth.complete_graph(n, 7)
         g = NetworkGraph.from_edges(n, src, dst, lat, loss)
     else:
         row_ptr, col, lat, loss = synth.complete_csr(n, 7)
         g = NetworkGraph(n, np.arange(n, dtype=np.uint32), row_ptr, col, lat, loss, directed=False)
     nodes = np.arange(n, dtype=np.uint32)
-    tp, lp, rp = _table(monkeypatch, g, nodes, True)
-    ts, ls, rs = _table(monkeypatch, g, nodes, False)
     nblk = n // 128
-    assert lp == nblk // 2 and ls == nblk  # one rest launch per pair vs per round
-    assert 1.8 < rp <= 2.0 and rs == 1.0
-    assert np.array_equal(tp.latency_ns, ts.latency_ns)
-    assert np.array_equal(tp.packet_loss.view(np.uint32), ts.packet_loss.view(np.uint32))
-    assert tp.min_latency_ns == ts.min_latency_ns
-    L = tp.latency_ns
+    ts, ls, rs = _table(monkeypatch, g, nodes, 1)
+    assert ls == nblk and rs == 1.0
+    for grp in (2, 4):
+        tp, lp, rp = _table(monkeypatch, g, nodes, grp)
+        assert lp == nblk // grp  # one rest launch per group of rounds
+        assert 0.7 * grp < rp <= grp
+        assert np.array_equal(tp.latency_ns, ts.latency_ns)
+        assert np.array_equal(tp.packet_loss.view(np.uint32), ts.packet_loss.view(np.uint32))
+        assert tp.min_latency_ns == ts.min_latency_ns
+    L = ts.latency_ns
     assert np.array_equal(L, L.T)
