@@ -827,10 +827,13 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
         emu_bcast_ticks = (long long)(std::atof(e) * khz / 1000.0);
     }
     // one GPU, rest-bound (no quarter-tile chain): rounds in groups of g = 4
-    // (2 when the block count is not a multiple of 4; knob SRT_FW_GROUP=1/2/4
-    // for A/B timing, SRT_FW_PAIR forces grouping at chain-bound sizes too:
-    // parity tests)
-    uint32_t grp = (nblk % 4 == 0 && nblk >= 8) ? 4 : 2;
+    // from 96 blocks (12k nodes) on, 2 below or when the block count is not a
+    // multiple of 4 (measured, same box: 8k 39.0 / 37.2 / 37.6 ms for g = 1 /
+    // 2 / 4; 12k 122.8 / 118.2 / 117.2; 16k 285.4 / 274.9 / 270.7; knob
+    // SRT_FW_GROUP=1/2/4 for A/B timing, SRT_FW_PAIR forces grouping at
+    // chain-bound sizes too: parity tests)
+    uint32_t grp = (nblk % 4 == 0 && nblk >= 96) ? 4 : 2;
+    if (nblk < 96 && std::getenv("SRT_FW_PAIR") && nblk % 4 == 0 && nblk >= 8) grp = 4;
     if (const char *e = std::getenv("SRT_FW_GROUP")) grp = (uint32_t)std::atoi(e);
     if (std::getenv("SRT_FW_NO_PAIR")) grp = 1;
     if (!sharded && !emu && p->fw_glds && (!p->fw_small_chain || std::getenv("SRT_FW_PAIR")) && grp > 1 &&
