@@ -455,13 +455,24 @@ __global__ __launch_bounds__(NT3, 2) void minplus_glds_kernel(K *__restrict__ D,
     if constexpr (TAG != 0) __builtin_amdgcn_s_setprio(2);
     const uint32_t n1 = r1.r.n * r1.c.n;
     uint32_t t = blockIdx.x, bi, bj;
+    const uint32_t ngr = ng & 0xffffu;
     if (t < n1) {
         if (gridDim.x == n1 && n1 >= 64) {  // XCD-aware bijective remap (see minplus_tile_kernel)
             const uint32_t q = n1 / 8, rr = n1 % 8, xcd = t % 8;
             t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + t / 8;
         }
-        bi = span_at(r1.r, t / r1.c.n);
-        bj = span_at(r1.c, t % r1.c.n);
+        const uint32_t nc = r1.c.n, full = (r1.r.n / 8) * 8 * nc;
+        if ((ng & 0x10000u) && t < full) {
+            // banded order (grouped launches): an XCD's ~64 resident tiles
+            // cover 8 rows x 8 columns, so one round's 16 A/B panels (2 MB)
+            // stay in its L2 instead of 65
+            const uint32_t w = t % (8 * nc);
+            bi = span_at(r1.r, (t / (8 * nc)) * 8 + w % 8);
+            bj = span_at(r1.c, w / 8);
+        } else {
+            bi = span_at(r1.r, t / nc);
+            bj = span_at(r1.c, t % nc);
+        }
     } else {
         t -= n1;
         bi = span_at(r2.r, t / r2.c.n);
@@ -474,12 +485,13 @@ __global__ __launch_bounds__(NT3, 2) void minplus_glds_kernel(K *__restrict__ D,
     // tile in row/column kb+ng-1 is all chain work and exits.
     constexpr int NCH = B / KC;
     int ch0 = 0;
-    const int ch1 = (int)ng * NCH;
-    if (ng > 1) {
-        const uint32_t qi = bi - kb < ng ? bi - kb : 0u, qj = bj - kb < ng ? bj - kb : 0u;
-        const bool in = bi - kb < ng || bj - kb < ng;
+    const uint32_t ng_ = ngr;
+    const int ch1 = (int)ng_ * NCH;
+    if (ng_ > 1) {
+        const uint32_t qi = bi - kb < ng_ ? bi - kb : 0u, qj = bj - kb < ng_ ? bj - kb : 0u;
+        const bool in = bi - kb < ng_ || bj - kb < ng_;
         const uint32_t q = std::max(qi, qj);
-        if (in && q == ng - 1) return;  // workgroup-uniform, before any barrier
+        if (in && q == ng_ - 1) return;  // workgroup-uniform, before any barrier
         ch0 = in ? (int)(q + 1) * NCH : 0;
     }
     const uint64_t i0 = (uint64_t)bi * B, j0 = (uint64_t)bj * B;
@@ -953,10 +965,13 @@ void launch_group(srt_plan *p, hipStream_t s, uint32_t a, uint32_t g, const Rect
     const uint32_t n = r1.r.n * r1.c.n + r2.r.n * r2.c.n;
     if (!n) return;
     K *D = reinterpret_cast<K *>(p->d_D);
+    // bit 16: banded tile order (knob SRT_FW_BAND=0 turns it off for A/B timing)
+    static const bool band = !(std::getenv("SRT_FW_BAND") && std::getenv("SRT_FW_BAND")[0] == '0');
+    const uint32_t arg = g | (band ? 0x10000u : 0u);
     if (chain)
-        hipLaunchKernelGGL((minplus_glds_kernel<K, 5>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, g);
+        hipLaunchKernelGGL((minplus_glds_kernel<K, 5>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
     else
-        hipLaunchKernelGGL((minplus_glds_kernel<K, 0>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, g);
+        hipLaunchKernelGGL((minplus_glds_kernel<K, 0>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
 }
 
 template <typename K>
