@@ -212,6 +212,7 @@ def bench_graph(args, cfg, D):
                           "rest_launches_per_step": k_launches // args.steps}), flush=True)
         plan.close()
         return None
+    timing = plan.timing()  # phase breakdown of the last timed build
     plan.fetch(table=False)  # connectivity check + min latency (not timed)
     n = len(nodes)
     out = None
@@ -269,7 +270,11 @@ def bench_graph(args, cfg, D):
             "data": data,
             "config": {"workload": f"{label}, use_shortest_path=true, {algo}", "nodes": n_nodes, "in_use": n,
                        "pairs": pairs, "parallelism": f"rows{D.n_gpus}" if D.n_gpus > 1 else "single",
-                       "plan": desc, "step_ms": [round(x, 3) for x in step_ms], "build_wallclock_ms": ms_per_step},
+                       "plan": desc, "step_ms": [round(x, 3) for x in step_ms], "build_wallclock_ms": ms_per_step,
+                       "phases_last_build": {"device_total_ms": timing["total_ms"],
+                                             "dominant_ms": timing["dominant_ms"],
+                                             "exact_loss_pass_ms": timing["loss_ms"],
+                                             "tight_edges": timing["tight_edges"]}},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "cpu_baseline_opt": cpu_opt,

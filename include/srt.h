@@ -140,6 +140,16 @@ void *srt_plan_stream(srt_plan *plan);
 srt_status srt_plan_kernel_stats(const srt_plan *plan, double *dominant_ms,
                                  uint64_t *dominant_launches, double *dominant_work,
                                  double *total_ms);
+/* Phase breakdown of the last run (HIP events on the plan's streams). */
+typedef struct {
+    double total_ms;            /* the whole build on the device */
+    double dominant_ms;         /* FW phase-3 rest launches / SSSP sweeps, summed */
+    uint64_t dominant_launches;
+    double dominant_work;       /* relaxations (FW) / algorithmic bytes (SSSP) of those launches */
+    double loss_ms;             /* dense: exact-loss pass (tight-edge CSR + fold), 0 for SSSP */
+    uint64_t tight_edges;       /* dense: edges of the tight-edge CSR */
+} srt_timing;
+srt_status srt_plan_timing(const srt_plan *plan, srt_timing *out);
 /* C tiles (128 x 128 keys) the last FW run's dominant launches loaded and
  * stored, summed over those launches (0 for the SSSP sweep): the algorithmic
  * C traffic is tiles x 128^2 x 2 x sizeof(key). */

@@ -50,6 +50,11 @@ class SrtOpts(C.Structure):
     _fields_ = [("algo", C.c_uint32), ("device", C.c_int32), ("flags", C.c_uint32), ("reserved", C.c_uint32)]
 
 
+class SrtTiming(C.Structure):
+    _fields_ = [("total_ms", C.c_double), ("dominant_ms", C.c_double), ("dominant_launches", C.c_uint64),
+                ("dominant_work", C.c_double), ("loss_ms", C.c_double), ("tight_edges", C.c_uint64)]
+
+
 class SrtRound(C.Structure):
     _fields_ = [("round_end_ns", C.c_uint64), ("bootstrap_end_ns", C.c_uint64), ("sim_end_ns", C.c_uint64)]
 
@@ -89,6 +94,7 @@ SIGNATURES = {
     "srt_plan_kernel_tiles": (C.c_int, [_vp, _u64p]),
     "srt_plan_kernel_stats": (C.c_int, [_vp, C.POINTER(C.c_double), _u64p, C.POINTER(C.c_double),
                                         C.POINTER(C.c_double)]),
+    "srt_plan_timing": (C.c_int, [_vp, C.POINTER(SrtTiming)]),
     "srt_plan_destroy": (None, [_vp]),
     "srt_comm_unique_id": (C.c_int, [C.c_void_p, _errp]),
     "srt_comm_init": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(_vp), _errp]),

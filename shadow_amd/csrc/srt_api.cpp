@@ -81,68 +81,28 @@ srt_status edge_error(srt_err *err, int c, uint32_t a_id, uint32_t b_id) {
     return SRT_ERR_MULTI_EDGE;
 }
 
-int bits_for(unsigned __int128 x) {  // number of bits to represent x
-    int b = 0;
-    while (x) {
-        ++b;
-        x >>= 1;
-    }
-    return b;
-}
-
-// Choose the packed-key representation (see KeyParams) and prove it exact.
+// Choose the closure's key representation and prove it exact.
 //
-// Every value the closure stores is the key of a simple path whose latency is
-// at most Lmax (units of g), and every candidate is the sum of two stored
-// values.  Lmax = max edge latency when every ordered pair of graph nodes has
-// an edge (the initial matrix is finite and values only decrease), else
-// (V-1) * max edge latency.  A stored path has at most H = min(V-1,
-// Lmax / min_edge_latency) hops.  So with W usable bits (53 for f64 keys, 62
-// for u64 keys):
-//   latency field: 2*Lmax (+1) must fit in W - qb bits;
-//   loss field:    2*H*max_q must stay < 2^qb (no carry into the latency);
-// then key sums are exact integers and lexicographic (latency, loss) order is
-// plain numeric order.  s (the loss resolution) must be >= 24, i.e. loss
-// quantisation <= 2^-25 per hop; otherwise the next wider key is tried.
-bool fit_width(int W, unsigned __int128 lat_field, unsigned __int128 hops2, double max_nl, KeyParams *kp) {
-    const int lbits = bits_for(lat_field);
-    if (lbits > W) return false;
-    if (max_nl == 0.0) {  // loss-free graph: key = latency units, loss field empty
-        kp->qb = 0;
-        kp->s = 0;
-        kp->scale = 1.0;
-        kp->inv_scale = 1.0;
-        kp->q_cap = 0;
-        return true;
-    }
-    const int qb = W - lbits;
-    const double room = std::ldexp(1.0, qb) / ((double)hops2 * max_nl);
-    int s = (int)std::floor(std::log2(room)) - 1;  // one bit of margin for rounding
-    s = std::min(s, 52);
-    if (s < 24) return false;
-    kp->qb = (uint32_t)qb;
-    kp->s = s;
-    kp->scale = std::ldexp(1.0, s);
-    kp->inv_scale = std::ldexp(1.0, -s);
-    kp->q_cap = (uint64_t)std::llrint(kp->nlr_cap * kp->scale);
-    return true;
-}
-
-bool choose_key_params(const srt_csr *g, KeyParams *kp, bool *f64, std::string *why) {
-    uint64_t gcd = 0, maxlat = 0, minlat = ~0ull;
-    double max_nl = 0.0;
-    const double NLR_CAP = 40.0;  // reliability < e^-40 ~ 4e-18: loss == 1.0f in f32
+// Keys are path latencies in units of g = gcd of all edge latencies.  Every
+// value the closure stores is at most Lmax: for a complete graph the initial
+// matrix is finite and values only decrease, so Lmax = max edge latency; else
+// a stored value is never above the sequential Floyd-Warshall's value at the
+// same point (concurrent schedules only read tighter keys of real walks), a
+// simple path, so Lmax = (V-1) * max edge latency.  A candidate is a sum of
+// two stored values, so 2 Lmax must stay exact: below 2^53 the keys are f64
+// (v_add_f64 / v_min_f64), below 2^62 u64 -- and below KEY32_INF (2^31 - 1)
+// u32, the fastest.  Lmax < 2^32 - 1 additionally lets the loss pass keep
+// latencies as u32.  Knob SRT_FW_KEY=f64|u64 (measurement / A-B parity only)
+// skips the narrower representations.
+bool choose_key_params(const srt_csr *g, KeyParams *kp, int *key_type, std::string *why) {
+    uint64_t gcd = 0, maxlat = 0;
     for (uint64_t k = 0; k < g->n_adj; ++k) {
         const uint64_t l = g->lat_ns[k];
-        gcd = std::gcd(gcd, l);
+        if (gcd != 1 && (gcd == 0 || l % gcd)) gcd = std::gcd(gcd, l);
         maxlat = std::max(maxlat, l);
-        minlat = std::min(minlat, l);
-        const double nl = -std::log1p(-(double)g->loss[k]);
-        max_nl = std::max(max_nl, std::min(nl, NLR_CAP));
     }
     if (gcd == 0) gcd = 1;
     kp->g = gcd;
-    kp->nlr_cap = NLR_CAP;
     const uint64_t V = g->n_nodes;
     // complete: every node has an edge to every other node
     bool complete = V > 0;
@@ -160,21 +120,26 @@ bool choose_key_params(const srt_csr *g, KeyParams *kp, bool *f64, std::string *
             complete = distinct == V - 1;
         }
     }
-    const uint64_t maxu = maxlat / gcd, minu = std::max<uint64_t>(minlat / gcd, 1);
+    const uint64_t maxu = maxlat / gcd;
     const unsigned __int128 Lmax = complete ? (unsigned __int128)maxu : (unsigned __int128)(V ? V - 1 : 0) * maxu;
-    unsigned __int128 H = V ? V - 1 : 0;
-    if (minlat != ~0ull && Lmax / minu < H) H = Lmax / minu;
-    const unsigned __int128 lat_field = 2 * Lmax + 1;
-    const unsigned __int128 hops2 = 2 * H + 1;
-    if (fit_width(53, lat_field, hops2, max_nl, kp)) {
-        *f64 = true;
+    kp->lmax = Lmax > (unsigned __int128)~0ull ? ~0ull : (uint64_t)Lmax;
+    kp->lat32 = Lmax < 0xffffffffull;
+    const char *force = std::getenv("SRT_FW_KEY");
+    const int min_type = !force ? srt::KEY_U32 : std::strcmp(force, "u64") == 0 ? srt::KEY_U64
+                         : std::strcmp(force, "f64") == 0 ? srt::KEY_F64 : srt::KEY_U32;
+    if (min_type <= srt::KEY_U32 && 2 * Lmax + 1 < (unsigned __int128)srt::KEY32_INF) {
+        *key_type = srt::KEY_U32;
         return true;
     }
-    if (fit_width(62, lat_field, hops2, max_nl, kp)) {
-        *f64 = false;
+    if (min_type <= srt::KEY_F64 && 2 * Lmax + 1 < ((unsigned __int128)1 << 53)) {
+        *key_type = srt::KEY_F64;
         return true;
     }
-    *why = "latency range and loss resolution do not fit a 62-bit exact key";
+    if (2 * Lmax + 1 < ((unsigned __int128)1 << 62)) {
+        *key_type = srt::KEY_U64;
+        return true;
+    }
+    *why = "the latency range does not fit a 62-bit exact key";
     return false;
 }
 
@@ -209,7 +174,15 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_sact);
     hipFree(p->d_rstats);
     hipFree(p->d_ev_scratch);
+    hipFree(p->d_tflag);
+    hipFree(p->d_tcnt);
+    hipFree(p->d_tptr);
+    hipFree(p->d_tu);
+    hipFree(p->d_tw);
+    hipFree(p->d_teb);
+    hipFree(p->d_lscratch);
     if (p->h_sflag) hipHostFree(p->h_sflag);
+    if (p->h_tcount) hipHostFree(p->h_tcount);
 }
 
 // Sparse SSSP key (srt_sssp.hip): latency in units of g in the high 32 bits.
@@ -293,6 +266,13 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         set_err(err, SRT_ERR_INVALID, "row_ptr[n_nodes] != n_adj");
         return SRT_ERR_INVALID;
     }
+    // ShadowEdge::try_from rejects a zero latency (mod.rs:104-106); the loss
+    // pass relies on every edge latency being > 0
+    for (uint64_t k = 0; k < g->n_adj; ++k)
+        if (g->lat_ns[k] == 0) {
+            set_err(err, SRT_ERR_INVALID, "Edge 'latency' must not be 0");
+            return SRT_ERR_INVALID;
+        }
     // self-loop of every in-use node, in node order (mod.rs:210-217)
     std::vector<uint64_t> sl_lat(n);
     std::vector<float> sl_loss(n);
@@ -323,7 +303,7 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     // few re-activations per row, priced at ~64 B per (source, in-edge) at
     // ~3e12 B/s.  AUTO takes the cheaper representable one.
     std::string why_fw, why_sssp;
-    const bool fw_ok = choose_key_params(g, &p->kp, &p->key_f64, &why_fw);
+    const bool fw_ok = choose_key_params(g, &p->kp, &p->key_type, &why_fw);
     if (fw_ok) {
         // no parallel edges (every adjacency row lists each neighbour once):
         // the FW init can store edge keys instead of atomic-min'ing them
@@ -372,9 +352,11 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         // tuning knob (measurement only): SRT_FW_STAGE=reg selects register staging
         if (const char *e = std::getenv("SRT_FW_STAGE")) p->fw_glds = std::strcmp(e, "reg") != 0;
         if (const char *e = std::getenv("SRT_FW_EMULATE_RANKS")) p->emulate_ranks = (uint32_t)std::atoi(e);
-        std::snprintf(d, sizeof d, "fw:%s B=%d g=%llu qb=%u s=%d V=%u n=%u stage=%s",
-                      p->key_f64 ? "f64key" : "u64key", srt::FW_B, (unsigned long long)p->kp.g, p->kp.qb, p->kp.s,
-                      p->V, n, p->fw_glds ? "glds" : "reg");
+        std::snprintf(d, sizeof d, "fw:%s B=%d g=%llu lmax=%llu V=%u n=%u stage=%s loss=tight-dag%s",
+                      p->key_type == srt::KEY_U32 ? "u32key" : p->key_type == srt::KEY_F64 ? "f64key" : "u64key",
+                      srt::FW_B, (unsigned long long)p->kp.g,
+                      (unsigned long long)p->kp.lmax, p->V, n, p->fw_glds ? "glds" : "reg",
+                      p->kp.lat32 ? "/u32" : "/u64");
     } else {
         // R words of 64 sources per lane (one wave walks a vertex's in-edges
         // once for 64*R sources), and as many groups in flight as ~256 MB of
@@ -476,7 +458,9 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     PLAN_TRY(dmalloc(&p->d_lat, g->n_adj, err));
     PLAN_TRY(dmalloc(&p->d_loss, g->n_adj, err));
     PLAN_TRY(dmalloc(&p->d_nodes, n, err));
-    if (algo == SRT_ALGO_FW) PLAN_TRY(dmalloc(&p->d_D, (size_t)p->Vp * p->Vp, err));
+    if (algo == SRT_ALGO_FW)
+        PLAN_TRY(dmalloc(reinterpret_cast<uint8_t **>(&p->d_D), (size_t)p->Vp * p->Vp * srt::key_bytes(p->key_type),
+                         err));
     PLAN_TRY(dmalloc(&p->d_out_lat, (size_t)n * n, err));
     PLAN_TRY(dmalloc(&p->d_out_loss, (size_t)n * n, err));
     PLAN_TRY(dmalloc(&p->d_sl_lat, n, err));
@@ -538,25 +522,29 @@ srt_status srt_plan_run_async(srt_plan *p, srt_err *err) {
     HIP_TRY(hipSetDevice(p->device), "hipSetDevice");
     hipEventRecord(p->ev_begin, p->stream);
     srt_status st;
+    // table rows [row0, row1) of this rank; every rank then holds the whole
+    // table after the row all-gather, and the stats of all ranks
+    const int rank = p->comm ? p->comm->rank : 0, nranks = p->comm ? p->comm->nranks : 1;
+    unsigned long long *rstats = p->comm ? p->d_rstats + 2 * rank : p->d_stats;
+    p->loss_ms = 0.0;
     if (p->algo == SRT_ALGO_SSSP) {
-        // rows [row0, row1) of this rank; every rank then holds the whole
-        // table after the row all-gather, and the stats of all ranks
-        const int rank = p->comm ? p->comm->rank : 0, nranks = p->comm ? p->comm->nranks : 1;
-        st = srt::sssp_run(p, p->d_rstats + 2 * rank, err);
+        st = srt::sssp_run(p, rstats, err);
         if (st != SRT_OK) return st;
-        if (p->comm) {
-            const size_t per = (size_t)p->rows_alloc / nranks * p->n;
-            if ((st = srt::comm_allgather_inplace(p->comm, p->d_out_lat, per * 8, p->stream, err)) != SRT_OK ||
-                (st = srt::comm_allgather_inplace(p->comm, p->d_out_loss, per * 4, p->stream, err)) != SRT_OK ||
-                (st = srt::comm_allgather_inplace(p->comm, p->d_rstats, 16, p->stream, err)) != SRT_OK)
-                return st;
-        }
-        srt::reduce_rank_stats(p, nranks);
     } else {
         srt::fw_init(p);
         st = srt::fw_rounds(p, err);
         if (st != SRT_OK) return st;
-        srt::fw_extract(p);
+        // exact loss over the tight DAG (every rank holds the whole closure)
+        st = srt::fw_loss(p, rstats, err);
+        if (st != SRT_OK) return st;
+    }
+    if (p->comm) {
+        const size_t per = (size_t)p->rows_alloc / nranks * p->n;
+        if ((st = srt::comm_allgather_inplace(p->comm, p->d_out_lat, per * 8, p->stream, err)) != SRT_OK ||
+            (st = srt::comm_allgather_inplace(p->comm, p->d_out_loss, per * 4, p->stream, err)) != SRT_OK ||
+            (st = srt::comm_allgather_inplace(p->comm, p->d_rstats, 16, p->stream, err)) != SRT_OK)
+            return st;
+        srt::reduce_rank_stats(p, nranks);
     }
     hipEventRecord(p->ev_end, p->stream);
     HIP_TRY(hipGetLastError(), "kernel launch");
@@ -579,6 +567,8 @@ srt_status srt_plan_sync(srt_plan *p, srt_err *err) {
     for (uint64_t i = 0; i < p->p3_launches; ++i) {
         if (hipEventElapsedTime(&ms, p->ev[2 * i], p->ev[2 * i + 1]) == hipSuccess) p->p3_ms += ms;
     }
+    if (p->algo == SRT_ALGO_FW && p->ev_loss0 && hipEventElapsedTime(&ms, p->ev_loss0, p->ev_loss1) == hipSuccess)
+        p->loss_ms = ms;
     return SRT_OK;
 }
 
@@ -652,6 +642,17 @@ srt_status srt_plan_kernel_stats(const srt_plan *p, double *dominant_ms, uint64_
     return SRT_OK;
 }
 
+srt_status srt_plan_timing(const srt_plan *p, srt_timing *o) {
+    if (!p || !o) return SRT_ERR_INVALID;
+    o->total_ms = p->total_ms;
+    o->dominant_ms = p->p3_ms;
+    o->dominant_launches = p->p3_launches;
+    o->dominant_work = p->p3_work;
+    o->loss_ms = p->loss_ms;
+    o->tight_edges = p->algo == SRT_ALGO_FW ? p->t_edges : 0;
+    return SRT_OK;
+}
+
 srt_status srt_plan_kernel_tiles(const srt_plan *p, uint64_t *tiles) {
     if (!p) return SRT_ERR_INVALID;
     if (tiles) *tiles = p->p3_tiles;
@@ -666,7 +667,8 @@ void srt_plan_destroy(srt_plan *p) {
     if (p->comm_stream) hipStreamSynchronize(p->comm_stream);
     free_plan_buffers(p);
     for (hipEvent_t e : p->ev) hipEventDestroy(e);
-    for (hipEvent_t e : {p->ev_begin, p->ev_end, p->ev_cross, p->ev_pivot, p->ev_row, p->ev_bcast})
+    for (hipEvent_t e : {p->ev_begin, p->ev_end, p->ev_cross, p->ev_pivot, p->ev_row, p->ev_bcast, p->ev_loss0,
+                         p->ev_loss1})
         if (e) hipEventDestroy(e);
     if (p->side_stream) hipStreamDestroy(p->side_stream);
     if (p->comm_stream) hipStreamDestroy(p->comm_stream);
@@ -681,10 +683,11 @@ srt_status srt_plan_bind_comm(srt_plan *p, srt_comm *comm, srt_err *err) {
         return SRT_ERR_INVALID;
     }
     HIP_TRY(hipSetDevice(p->device), "hipSetDevice");
-    if (p->algo == SRT_ALGO_SSSP) {
-        // sources shard with no exchange until the end: rank r owns table rows
-        // [r*per, (r+1)*per) (the last rank's tail past n is padding), and the
-        // table is allocated with per*nranks rows for an equal-chunk all-gather
+    {
+        // table rows shard with no exchange until the end (SSSP sources; the
+        // dense build's loss pass): rank r owns rows [r*per, (r+1)*per) (the
+        // last rank's tail past n is padding), and the table is allocated
+        // with per*nranks rows for an equal-chunk all-gather
         const uint32_t W = (uint32_t)comm->nranks, per = (p->n + W - 1) / W;
         const uint32_t rows_alloc = per * W;
         if (rows_alloc > p->rows_alloc) {
@@ -712,7 +715,7 @@ srt_status srt_plan_bind_comm(srt_plan *p, srt_comm *comm, srt_err *err) {
         char d[64];
         std::snprintf(d, sizeof d, " ranks=%d rows=[%u,%u)", comm->nranks, p->row0, p->row1);
         p->desc += d;
-        return SRT_OK;
+        if (p->algo == SRT_ALGO_SSSP) return SRT_OK;
     }
     // pad the node range so every rank owns the same number of block-rows
     // (equal all-gather chunks); padded nodes are isolated and never in use
@@ -720,18 +723,17 @@ srt_status srt_plan_bind_comm(srt_plan *p, srt_comm *comm, srt_err *err) {
     const uint32_t Vp = std::max<uint32_t>(((p->V + unit - 1) / unit) * unit, unit);
     if (Vp != p->Vp) {
         void *ptr = nullptr;
-        hipError_t e = hipMalloc(&ptr, (size_t)Vp * Vp * sizeof(uint64_t));
+        hipError_t e = hipMalloc(&ptr, (size_t)Vp * Vp * srt::key_bytes(p->key_type));
         if (e != hipSuccess) return hip_fail(err, e, "hipMalloc(D)");
         HIP_TRY(hipFree(p->d_D), "hipFree");
         p->d_D = (uint64_t *)ptr;
         p->Vp = Vp;
     }
     const uint32_t nblk = p->Vp / srt::FW_B, per = nblk / (uint32_t)comm->nranks;
-    p->comm = comm;
     p->rb0 = per * (uint32_t)comm->rank;
     p->rb1 = p->rb0 + per;
     char d[64];
-    std::snprintf(d, sizeof d, " ranks=%d rows=[%u,%u)", comm->nranks, p->rb0 * srt::FW_B, p->rb1 * srt::FW_B);
+    std::snprintf(d, sizeof d, " closure-rows=[%u,%u)", p->rb0 * srt::FW_B, p->rb1 * srt::FW_B);
     p->desc += d;
     return SRT_OK;
 }

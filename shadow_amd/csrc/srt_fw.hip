@@ -12,12 +12,13 @@
 //                       hot loop, a min-plus "GEMM" with K = B.
 // Phases 2 and 3 run the same tile kernel (minplus_tile_kernel).
 //
-// Path keys (see KeyParams, srt_internal.h) are exact integers packed as
-//   key = (latency/g) << qb | round(-ln(1-loss) * 2^s)
-// carried either as f64 (< 2^53, the fast path: v_add_f64 + v_min_f64 = 2 VALU
-// ops per relaxation) or as u64 (< 2^62: v_lshl_add_u64 + v_cmp_lt_u64 +
-// 2 v_cndmask = 4 ops).  Both give bit-identical tables; the host picks f64
-// whenever its bound proof fits in 53 bits.
+// Path keys (see KeyParams, srt_internal.h) are path LATENCIES in units of g,
+// exact integers carried either as f64 (< 2^53, the fast path: v_add_f64 +
+// v_min_f64 = 2 VALU ops per relaxation) or as u64 (< 2^62: v_lshl_add_u64 +
+// v_cmp_lt_u64 + 2 v_cndmask = 4 ops).  Both give bit-identical latencies; the
+// host picks f64 whenever its bound proof fits in 53 bits.  packet_loss is not
+// carried through the closure: the exact-loss pass (srt_loss.hip) folds it
+// over the tight shortest-path DAG afterwards, bit for bit as the reference.
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
@@ -45,6 +46,18 @@ struct KeyOps<uint64_t> {
     static __device__ __forceinline__ uint64_t from_int(uint64_t v) { return v; }
     static __device__ __forceinline__ bool is_inf(uint64_t k) { return k >= KEY_INF; }
     static __device__ __forceinline__ uint64_t to_int(uint64_t k) { return k; }
+};
+
+// u32 latency keys (2 lmax < KEY32_INF, host-proved): INF + INF < 2^32, so a
+// candidate never wraps and min keeps every value <= KEY32_INF
+template <>
+struct KeyOps<uint32_t> {
+    static __device__ __forceinline__ uint32_t inf() { return KEY32_INF; }
+    static __device__ __forceinline__ uint32_t zero() { return 0u; }
+    static __device__ __forceinline__ uint32_t kmin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+    static __device__ __forceinline__ uint32_t from_int(uint64_t v) { return (uint32_t)v; }
+    static __device__ __forceinline__ bool is_inf(uint32_t k) { return k >= KEY32_INF; }
+    static __device__ __forceinline__ uint64_t to_int(uint32_t k) { return k; }
 };
 
 template <>
@@ -111,27 +124,24 @@ __global__ void fill_kernel(K *__restrict__ D, uint32_t Vp, uint32_t r0, uint32_
     }
 }
 
-__device__ __forceinline__ uint64_t edge_key(uint64_t lat, float loss, const KeyParams &kp) {
-    const uint64_t lq = lat / kp.g;
-    uint64_t q = 0;
-    if (kp.qb) {
-        const double nl = -log1p(-(double)loss);  // -ln(1 - loss) >= 0; loss 1 -> +inf
-        q = (nl >= kp.nlr_cap) ? kp.q_cap : (uint64_t)llrint(nl * kp.scale);
-    }
-    return (lq << kp.qb) | q;
+// key of an edge: its latency in units of g (g divides every edge latency;
+// below 2^53 the f64 quotient of two exact integers is exact, and cheaper
+// than the u64 division)
+__device__ __forceinline__ uint64_t edge_key(uint64_t lat, const KeyParams &kp) {
+    if (lat < (1ull << 53)) return (uint64_t)((double)lat / (double)kp.g);
+    return lat / kp.g;
 }
 
 // D[u][v] = min over parallel edges u->v (one wave per graph row).  The
 // diagonal keeps 0: a self-loop never shortens a path, and the table's
-// diagonal is the raw self-loop written by the extract kernel (mod.rs:210-217).
+// diagonal is the raw self-loop written by the loss pass (mod.rs:210-217).
 // UNIQUE (host-checked: no parallel edges) stores the key instead of the
 // memory-side atomic min (16k complete graph: 2.5 ms -> one plain store pass).
 template <typename K, bool UNIQUE>
 __global__ void scatter_edges_kernel(K *__restrict__ D, uint32_t Vp,
                                      const uint64_t *__restrict__ row_ptr,
                                      const uint32_t *__restrict__ col,
-                                     const uint64_t *__restrict__ lat,
-                                     const float *__restrict__ loss, uint32_t u0, uint32_t u1, KeyParams kp) {
+                                     const uint64_t *__restrict__ lat, uint32_t u0, uint32_t u1, KeyParams kp) {
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -143,18 +153,25 @@ __global__ void scatter_edges_kernel(K *__restrict__ D, uint32_t Vp,
             // integer key order == f64 order for exact integers: atomicMin on the
             // u64 value works for both representations (f64 bits of non-negative
             // doubles order like the doubles)
-            const uint64_t key = edge_key(lat[k], loss[k], kp);
-            uint64_t bits;
-            if constexpr (std::is_same<K, double>::value) {
-                const double d = (double)key;
-                bits = __builtin_bit_cast(uint64_t, d);
+            const uint64_t key = edge_key(lat[k], kp);
+            if constexpr (sizeof(K) == 4) {
+                if constexpr (UNIQUE)
+                    D[(uint64_t)u * Vp + v] = (K)key;
+                else
+                    atomicMin((unsigned int *)&D[(uint64_t)u * Vp + v], (unsigned int)key);
             } else {
-                bits = key;
+                uint64_t bits;
+                if constexpr (std::is_same<K, double>::value) {
+                    const double d = (double)key;
+                    bits = __builtin_bit_cast(uint64_t, d);
+                } else {
+                    bits = key;
+                }
+                if constexpr (UNIQUE)
+                    reinterpret_cast<uint64_t *>(D)[(uint64_t)u * Vp + v] = bits;
+                else
+                    atomicMin((unsigned long long *)&D[(uint64_t)u * Vp + v], (unsigned long long)bits);
             }
-            if constexpr (UNIQUE)
-                reinterpret_cast<uint64_t *>(D)[(uint64_t)u * Vp + v] = bits;
-            else
-                atomicMin((unsigned long long *)&D[(uint64_t)u * Vp + v], (unsigned long long)bits);
         }
     }
 }
@@ -566,6 +583,209 @@ __global__ __launch_bounds__(NT3, 2) void minplus_glds_kernel(K *__restrict__ D,
     }
 }
 
+// ------------------------------------------------------------ u32 keys
+// The same 128 x 128 tile per 256-thread workgroup, for 4-byte latency keys
+// (the host proves 2 lmax < KEY32_INF).  Two k-steps are relaxed together,
+//     acc = min3(acc, a_k + b_k, a_{k+1} + b_{k+1})
+// = 2 v_add_u32 (issued at twice the rate of other VALU ops) + 1 v_min3_u32
+// per 2 relaxations, against v_add_f64 + v_min_f64 per relaxation for f64
+// keys (profiles/r01_valu_bench.txt: 61 / 35 / 36.5 / 36.4 Tlane-ops/s).
+// Thread (tx, ty) holds rows ty + 16 i (i < 8) and columns tx*4 + c and
+// 64 + tx*4 + c (c < 4): C loads/stores are 16-B per lane, 256 B contiguous
+// per 16 lanes.  K-chunks of KC32 = 16 are staged by LDS-DMA (16 wave-
+// instructions of 1 KiB, 4 per wave, lane-linear):
+//   A image: 8 pieces of [16 rows][16 k] + 16 B pad -- a thread's row i sits
+//     in piece i at row ty, so the two rows a half-wave reads with one
+//     ds_read_b64 (ty and ty+1) are 16 dwords apart: distinct banks;
+//   B image: [16 k][128 cols] (2 k-rows per piece); a thread reads its 4+4
+//     columns of a k-row with 2 ds_read_b128, 256 contiguous bytes per 16
+//     lanes: conflict-free.
+constexpr int KC32 = 16;
+constexpr int NCH32 = B / KC32;
+constexpr int APIECE32 = 16 * KC32 + 4;       // u32 per padded A piece (1040 B)
+constexpr int AIMG32 = (B / 16) * APIECE32;   // 2080
+constexpr int BIMG32 = KC32 * B;              // 2048
+constexpr int GBUF32 = AIMG32 + BIMG32;       // u32 per buffer
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+struct StepOps32 {
+    u32x2 a[8];  // a[i] = (A[row i][k], A[row i][k+1])
+    u32x4 b[4];  // b[0] / b[1]: k-row k, columns lo / hi; b[2] / b[3]: k-row k+1
+};
+
+// LDS reads of step-pair s (k = 2s, 2s+1) into o; abase = byte address of the
+// thread's row in piece 0, bbase = of its first column in k-row 0.
+template <int s>
+__device__ __forceinline__ void lds_step32(StepOps32 &o, uint32_t abase, uint32_t bbase) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(o.a[i]) : "v"(abase), "i"(i * APIECE32 * 4 + 8 * s));
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(o.b[0]) : "v"(bbase), "i"((2 * s) * B * 4));
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(o.b[1]) : "v"(bbase), "i"((2 * s) * B * 4 + 256));
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(o.b[2]) : "v"(bbase), "i"((2 * s + 1) * B * 4));
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(o.b[3]) : "v"(bbase), "i"((2 * s + 1) * B * 4 + 256));
+}
+
+// acc[c] = min3(acc[c], a0 + b0[c], a1 + b1[c]), c < 4: 8 adds, then 4 min3
+// (one volatile block so it stays in order with the explicit waits)
+__device__ __forceinline__ void relax_quad32(uint32_t &c0, uint32_t &c1, uint32_t &c2, uint32_t &c3, uint32_t a0,
+                                             uint32_t a1, u32x4 b0, u32x4 b1) {
+    uint32_t t0, t1, t2, t3, t4, t5, t6, t7;
+    asm volatile(
+        "v_add_u32 %0, %12, %14\n\t"
+        "v_add_u32 %1, %13, %18\n\t"
+        "v_add_u32 %2, %12, %15\n\t"
+        "v_add_u32 %3, %13, %19\n\t"
+        "v_add_u32 %4, %12, %16\n\t"
+        "v_add_u32 %5, %13, %20\n\t"
+        "v_add_u32 %6, %12, %17\n\t"
+        "v_add_u32 %7, %13, %21\n\t"
+        "v_min3_u32 %8, %8, %0, %1\n\t"
+        "v_min3_u32 %9, %9, %2, %3\n\t"
+        "v_min3_u32 %10, %10, %4, %5\n\t"
+        "v_min3_u32 %11, %11, %6, %7"
+        : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "=&v"(t4), "=&v"(t5), "=&v"(t6), "=&v"(t7), "+v"(c0),
+          "+v"(c1), "+v"(c2), "+v"(c3)
+        : "v"(a0), "v"(a1), "v"(b0.x), "v"(b0.y), "v"(b0.z), "v"(b0.w), "v"(b1.x), "v"(b1.y), "v"(b1.z),
+          "v"(b1.w));
+}
+
+template <int s>
+__device__ __forceinline__ void chunk_steps32(uint32_t (&acc)[8][8], StepOps32 (&o)[2], uint32_t abase,
+                                              uint32_t bbase) {
+    if constexpr (s < KC32 / 2) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (s + 1 < KC32 / 2) lds_step32<s + 1>(o[(s + 1) & 1], abase, bbase);
+        const StepOps32 &c = o[s & 1];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            relax_quad32(acc[i][0], acc[i][1], acc[i][2], acc[i][3], c.a[i].x, c.a[i].y, c.b[0], c.b[2]);
+            relax_quad32(acc[i][4], acc[i][5], acc[i][6], acc[i][7], c.a[i].x, c.a[i].y, c.b[1], c.b[3]);
+        }
+        chunk_steps32<s + 1>(acc, o, abase, bbase);
+    }
+}
+
+// tile (bi, bj) of workgroup t in the launch's rectangles (XCD-aware remap,
+// banded order for grouped launches: see minplus_glds_kernel)
+__device__ __forceinline__ void tile_of(uint32_t t, const Rect &r1, const Rect &r2, uint32_t ng, uint32_t &bi,
+                                        uint32_t &bj) {
+    const uint32_t n1 = r1.r.n * r1.c.n;
+    if (t < n1) {
+        if (gridDim.x == n1 && n1 >= 64) {
+            const uint32_t q = n1 / 8, rr = n1 % 8, xcd = t % 8;
+            t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + t / 8;
+        }
+        const uint32_t nc = r1.c.n, full = (r1.r.n / 8) * 8 * nc;
+        if ((ng & 0x10000u) && t < full) {
+            const uint32_t w = t % (8 * nc);
+            bi = span_at(r1.r, (t / (8 * nc)) * 8 + w % 8);
+            bj = span_at(r1.c, w / 8);
+        } else {
+            bi = span_at(r1.r, t / nc);
+            bj = span_at(r1.c, t % nc);
+        }
+    } else {
+        t -= n1;
+        bi = span_at(r2.r, t / r2.c.n);
+        bj = span_at(r2.c, t % r2.c.n);
+    }
+}
+
+template <int TAG>
+__global__ __launch_bounds__(NT3, 2) void minplus_u32_kernel(uint32_t *__restrict__ D, uint32_t Vp, uint32_t kb,
+                                                             Rect r1, Rect r2, uint32_t ng) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[2 * GBUF32];
+    if constexpr (TAG != 0) __builtin_amdgcn_s_setprio(2);  // look-ahead chain: issue priority
+    uint32_t bi, bj;
+    tile_of(blockIdx.x, r1, r2, ng, bi, bj);
+    // grouped rounds (see minplus_glds_kernel)
+    const uint32_t ng_ = ng & 0xffffu;
+    int ch0 = 0;
+    const int ch1 = (int)ng_ * NCH32;
+    if (ng_ > 1) {
+        const uint32_t qi = bi - kb < ng_ ? bi - kb : 0u, qj = bj - kb < ng_ ? bj - kb : 0u;
+        const bool in = bi - kb < ng_ || bj - kb < ng_;
+        const uint32_t q = std::max(qi, qj);
+        if (in && q == ng_ - 1) return;  // workgroup-uniform, before any barrier
+        ch0 = in ? (int)(q + 1) * NCH32 : 0;
+    }
+    const uint64_t i0 = (uint64_t)bi * B, j0 = (uint64_t)bj * B;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int tx = tid % 16, ty = tid / 16;
+
+    uint32_t acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t *src = D + (i0 + ty + 16 * i) * Vp + j0 + tx * 4;
+        const u32x4 lo = *reinterpret_cast<const u32x4 *>(src);
+        const u32x4 hi = *reinterpret_cast<const u32x4 *>(src + 64);
+        acc[i][0] = lo.x;
+        acc[i][1] = lo.y;
+        acc[i][2] = lo.z;
+        acc[i][3] = lo.w;
+        acc[i][4] = hi.x;
+        acc[i][5] = hi.y;
+        acc[i][6] = hi.z;
+        acc[i][7] = hi.w;
+    }
+    auto stage = [&](int ch, int buf) {
+        const uint64_t kk = (uint64_t)(kb + ch / NCH32) * B + (ch % NCH32) * KC32;  // first k of the chunk
+        uint32_t *img = lds + buf * GBUF32;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int piece = wave * 2 + q;  // A rows piece*16 .. +15
+            const uint32_t *g = D + (i0 + piece * 16 + lane / 4) * Vp + kk + (lane % 4) * 4;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
+                                             (__attribute__((address_space(3))) void *)(img + piece * APIECE32), 16,
+                                             0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int piece = wave * 2 + q;  // B k-rows 2 piece, 2 piece + 1
+            const uint32_t *g = D + (kk + piece * 2 + lane / 32) * Vp + j0 + (lane % 32) * 4;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
+                                             (__attribute__((address_space(3))) void *)(img + AIMG32 + piece * 256),
+                                             16, 0, 0);
+        }
+    };
+    stage(ch0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll 1
+    for (int ch = ch0; ch < ch1; ++ch) {
+        const int cur = (ch - ch0) & 1;
+        if (ch + 1 < ch1) stage(ch + 1, cur ^ 1);  // the other buffer's readers passed the last barrier
+        const uint32_t *As = lds + cur * GBUF32 + ty * KC32;      // row ty of piece 0
+        const uint32_t *Bs = lds + cur * GBUF32 + AIMG32 + tx * 4;  // columns tx*4 of k-row 0
+        const uint32_t abase = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t *)As;
+        const uint32_t bbase = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t *)Bs;
+        StepOps32 o[2];
+        lds_step32<0>(o[0], abase, bbase);
+        chunk_steps32<0>(acc, o, abase, bbase);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint32_t *dst = D + (i0 + ty + 16 * i) * Vp + j0 + tx * 4;
+        u32x4 lo, hi;
+        lo.x = acc[i][0];
+        lo.y = acc[i][1];
+        lo.z = acc[i][2];
+        lo.w = acc[i][3];
+        hi.x = acc[i][4];
+        hi.y = acc[i][5];
+        hi.z = acc[i][6];
+        hi.w = acc[i][7];
+        *reinterpret_cast<u32x4 *>(dst) = lo;
+        *reinterpret_cast<u32x4 *>(dst + 64) = hi;
+    }
+}
+
 // Latency-oriented variant for the look-ahead chain of the sharded schedule
 // (phase 2 row/col and cross): each 128x128 tile is split into four 64x64
 // quadrants, one 256-thread workgroup each (4x4 keys per thread), so a chain
@@ -647,75 +867,6 @@ __global__ __launch_bounds__(256) void minplus_small_kernel(K *__restrict__ D, u
         for (int j = 0; j < 4; ++j) D[(i0 + ty * 4 + i) * Vp + j0 + tx + 16 * j] = acc[i][j];
 }
 
-// ------------------------------------------------------------- extract
-// table[i][j] = decode(D[nodes[i]][nodes[j]]); diagonal = the raw self-loop
-// edge (mod.rs:210-217); min latency over the whole table (mod.rs:474-476);
-// count of unreachable pairs (the reference's assert at mod.rs:219).
-template <typename K>
-__global__ __launch_bounds__(256) void extract_kernel(const K *__restrict__ D, uint32_t Vp,
-                                                      const uint32_t *__restrict__ nodes, uint32_t n,
-                                                      KeyParams kp, const uint64_t *__restrict__ sl_lat,
-                                                      const float *__restrict__ sl_loss,
-                                                      uint64_t *__restrict__ out_lat,
-                                                      float *__restrict__ out_loss,
-                                                      unsigned long long *stats) {
-    // grid-stride over rows; one block-level reduction and 2 atomics per block
-    __shared__ unsigned long long red_min[4], red_cnt[4];
-    uint64_t mn = ~0ull;
-    unsigned long long unreach = 0;
-    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-        const K *row = D + (uint64_t)nodes[i] * Vp;
-        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
-            uint64_t lat;
-            float loss;
-            if (i == j) {
-                lat = sl_lat[i];
-                loss = sl_loss[i];
-            } else {
-                const K kk = row[nodes[j]];
-                if (KeyOps<K>::is_inf(kk)) {
-                    ++unreach;
-                    lat = ~0ull;
-                    loss = 1.0f;
-                } else {
-                    const uint64_t k = KeyOps<K>::to_int(kk);
-                    lat = (k >> kp.qb) * kp.g;
-                    const uint64_t q = kp.qb ? (k & ((1ull << kp.qb) - 1)) : 0ull;
-                    loss = q ? (float)(-expm1(-(double)q * kp.inv_scale)) : 0.0f;
-                }
-            }
-            out_lat[(uint64_t)i * n + j] = lat;
-            out_loss[(uint64_t)i * n + j] = loss;
-            mn = lat < mn ? lat : mn;
-        }
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-        const uint64_t o = __shfl_xor(mn, off);
-        mn = o < mn ? o : mn;
-        unreach += __shfl_xor(unreach, off);
-    }
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-        red_min[w] = mn;
-        red_cnt[w] = unreach;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long m = red_min[0], c = red_cnt[0];
-        for (int k = 1; k < (int)(blockDim.x >> 6); ++k) {
-            m = red_min[k] < m ? red_min[k] : m;
-            c += red_cnt[k];
-        }
-        atomicMin(&stats[0], m);
-        if (c) atomicAdd(&stats[1], c);
-    }
-}
-
-__global__ void init_stats_kernel(unsigned long long *stats) {
-    stats[0] = ~0ull;
-    stats[1] = 0ull;
-}
-
 __global__ void pack_kernel(const uint64_t *__restrict__ lat, const float *__restrict__ loss,
                             srt_path *__restrict__ out, uint64_t total) {
     for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < total;
@@ -738,10 +889,10 @@ void fw_init_t(srt_plan *p) {
     hipLaunchKernelGGL(fill_kernel<K>, dim3(4096), dim3(256), 0, p->stream, D, p->Vp, r0, r1);
     if (p->fw_unique_edges)
         hipLaunchKernelGGL((scatter_edges_kernel<K, true>), dim3(2048), dim3(256), 0, p->stream, D, p->Vp,
-                           p->d_row_ptr, p->d_col, p->d_lat, p->d_loss, u0, u1, p->kp);
+                           p->d_row_ptr, p->d_col, p->d_lat, u0, u1, p->kp);
     else
         hipLaunchKernelGGL((scatter_edges_kernel<K, false>), dim3(2048), dim3(256), 0, p->stream, D, p->Vp,
-                           p->d_row_ptr, p->d_col, p->d_lat, p->d_loss, u0, u1, p->kp);
+                           p->d_row_ptr, p->d_col, p->d_lat, u0, u1, p->kp);
 }
 
 // Measurement only (N-rank emulation): stands in for the pivot-row broadcast
@@ -768,9 +919,14 @@ void launch_tiles(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1, const
     if (TAG != 0 && p->fw_small_chain)  // sharded look-ahead chain: quarter tiles, lower latency
         hipLaunchKernelGGL((minplus_small_kernel<K, TAG>), dim3(4 * n), dim3(256), 0, s,
                            reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2);
-    else if (p->fw_glds)
-        hipLaunchKernelGGL((minplus_glds_kernel<K, TAG>), dim3(n), dim3(NT3), 0, s,
-                           reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2, 1u);
+    else if (p->fw_glds) {
+        if constexpr (sizeof(K) == 4)
+            hipLaunchKernelGGL((minplus_u32_kernel<TAG>), dim3(n), dim3(NT3), 0, s,
+                               reinterpret_cast<uint32_t *>(p->d_D), p->Vp, kb, r1, r2, 1u);
+        else
+            hipLaunchKernelGGL((minplus_glds_kernel<K, TAG>), dim3(n), dim3(NT3), 0, s,
+                               reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2, 1u);
+    }
     else
         hipLaunchKernelGGL((minplus_tile_kernel<K, TAG>), dim3(n), dim3(NT3), 0, s,
                            reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2);
@@ -968,10 +1124,17 @@ void launch_group(srt_plan *p, hipStream_t s, uint32_t a, uint32_t g, const Rect
     // bit 16: banded tile order (knob SRT_FW_BAND=0 turns it off for A/B timing)
     static const bool band = !(std::getenv("SRT_FW_BAND") && std::getenv("SRT_FW_BAND")[0] == '0');
     const uint32_t arg = g | (band ? 0x10000u : 0u);
-    if (chain)
-        hipLaunchKernelGGL((minplus_glds_kernel<K, 5>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
-    else
-        hipLaunchKernelGGL((minplus_glds_kernel<K, 0>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
+    if constexpr (sizeof(K) == 4) {
+        if (chain)
+            hipLaunchKernelGGL((minplus_u32_kernel<5>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
+        else
+            hipLaunchKernelGGL((minplus_u32_kernel<0>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
+    } else {
+        if (chain)
+            hipLaunchKernelGGL((minplus_glds_kernel<K, 5>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
+        else
+            hipLaunchKernelGGL((minplus_glds_kernel<K, 0>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
+    }
 }
 
 template <typename K>
@@ -1037,29 +1200,17 @@ srt_status fw_rounds_group_t(srt_plan *p, int p1r, uint32_t g) {
     return SRT_OK;
 }
 
-template <typename K>
-void fw_extract_t(srt_plan *p) {
-    hipLaunchKernelGGL(init_stats_kernel, dim3(1), dim3(1), 0, p->stream, p->d_stats);
-    const uint32_t blocks = p->n < 4096 ? (p->n ? p->n : 1) : 4096;
-    hipLaunchKernelGGL(extract_kernel<K>, dim3(blocks), dim3(256), 0, p->stream,
-                       reinterpret_cast<const K *>(p->d_D), p->Vp, p->d_nodes, p->n, p->kp,
-                       p->d_sl_lat, p->d_sl_loss, p->d_out_lat, p->d_out_loss, p->d_stats);
-}
-
 }  // namespace
 
 void fw_init(srt_plan *p) {
-    if (p->key_f64) fw_init_t<double>(p);
+    if (p->key_type == KEY_U32) fw_init_t<uint32_t>(p);
+    else if (p->key_type == KEY_F64) fw_init_t<double>(p);
     else fw_init_t<uint64_t>(p);
 }
 
 srt_status fw_rounds(srt_plan *p, srt_err *err) {
-    return p->key_f64 ? fw_rounds_t<double>(p, err) : fw_rounds_t<uint64_t>(p, err);
-}
-
-void fw_extract(srt_plan *p) {
-    if (p->key_f64) fw_extract_t<double>(p);
-    else fw_extract_t<uint64_t>(p);
+    if (p->key_type == KEY_U32) return fw_rounds_t<uint32_t>(p, err);
+    return p->key_type == KEY_F64 ? fw_rounds_t<double>(p, err) : fw_rounds_t<uint64_t>(p, err);
 }
 
 void pack_paths(srt_plan *p, uint64_t first, uint64_t count) {

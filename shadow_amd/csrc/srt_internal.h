@@ -12,27 +12,30 @@
 
 namespace srt {
 
-// Path key for the dense min-plus closure.
+// Path key for the dense min-plus closure: the path LATENCY in units of g
+// (the gcd of all edge latencies), nothing else.
 //
 // The reference orders paths lexicographically by (latency_ns, packet_loss)
-// (graph/mod.rs:305-313) and folds loss as 1-(1-a)(1-b) (mod.rs:322-331).  We
-// carry loss as its additive form -ln(1-loss) in fixed point, so a path key is
-//     key = (latency / g) << qb  |  round(-ln(reliability) * 2^s)
-// and lexicographic (latency, loss) order == unsigned integer order of keys,
-// while "+" of two paths == integer "+" of keys.  The host proves that no
-// candidate sum can carry out of the loss field nor reach KEY_INF (see
-// choose_key_params in srt_api.cpp), so latency is bit-exact and the loss
-// field only decides ties among equal-latency paths.
+// (graph/mod.rs:305-313) and folds loss as 1-(1-a)(1-b) in f32
+// (mod.rs:322-331), a non-associative fold that Floyd-Warshall's joins of
+// path halves cannot reproduce.  So the closure computes only the exact
+// latencies, and the loss of every pair is recomputed afterwards, bit for bit,
+// by the left fold over the tight shortest-path DAG (srt_loss.hip, SURVEY.md
+// S-R6).  Keys are exact integers: u32 when every candidate sum (two stored
+// latencies, each <= lmax) stays below KEY32_INF (v_add_u32 + v_min3_u32: the
+// fastest relaxation), else f64 below 2^53, else u64 below KEY_INF; the host
+// proves it (choose_key_params in srt_api.cpp).
 constexpr uint64_t KEY_INF = 1ull << 62;  // INF + INF < 2^64: no wrap in the closure
+constexpr uint32_t KEY32_INF = 0x7fffffffu;  // u32 keys: INF + INF < 2^32
+
+// closure key representation, fastest first (srt_plan::key_type)
+enum KeyType { KEY_U32 = 0, KEY_F64 = 1, KEY_U64 = 2 };
+inline size_t key_bytes(int t) { return t == KEY_U32 ? 4 : 8; }
 
 struct KeyParams {
-    uint64_t g;        // latency unit (gcd of all edge latencies, ns)
-    uint32_t qb;       // bits of the loss field
-    int32_t s;         // loss scale exponent (fixed point 2^-s)
-    double scale;      // 2^s
-    double inv_scale;  // 2^-s
-    double nlr_cap;    // -ln(reliability) clamp (loss ~ 1)
-    uint64_t q_cap;    // clamp in key units
+    uint64_t g;     // latency unit (gcd of all edge latencies, ns)
+    uint64_t lmax;  // bound on any finite closure value, in units of g
+    bool lat32;     // lmax < 2^32 - 1: the loss pass keeps latencies as u32
 };
 
 // FW tile geometry: B x B blocks, one block-row/column per round.
@@ -70,7 +73,7 @@ struct srt_plan {
     uint64_t n_adj = 0;
     int algo = SRT_ALGO_FW;
     srt::KeyParams kp{};
-    bool key_f64 = false;  // f64-encoded keys (exact integers < 2^53)
+    int key_type = srt::KEY_F64;  // closure keys: u32 / f64 (exact integers < 2^53) / u64
     bool fw_glds = true;   // FW tiles staged by LDS-DMA (false: register staging)
     bool fw_small_chain = false;  // quarter-tile kernels for the look-ahead chain (sharded)
     bool fw_unique_edges = false; // no parallel edges: FW init stores instead of atomic min
@@ -84,7 +87,7 @@ struct srt_plan {
     uint64_t *d_lat = nullptr;
     float *d_loss = nullptr;
     uint32_t *d_nodes = nullptr;
-    uint64_t *d_D = nullptr;  // Vp*Vp path keys
+    uint64_t *d_D = nullptr;  // Vp*Vp path keys (key_bytes(key_type) each)
     uint64_t *d_out_lat = nullptr;
     float *d_out_loss = nullptr;
     uint64_t *d_sl_lat = nullptr;
@@ -136,6 +139,22 @@ struct srt_plan {
     // with rows_alloc >= n rows so the row all-gather has equal chunks
     uint32_t row0 = 0, row1 = 0, rows_alloc = 0;
     unsigned long long *d_rstats = nullptr;  // 2 per rank: min latency, unreachable
+
+    // exact-loss pass of the dense build (srt_loss.hip): the tight-edge pull
+    // CSR (every edge u -> v whose latency equals the closure's D[u][v]) and
+    // per-workgroup scratch
+    uint8_t *d_tflag = nullptr;      // n_adj: adjacency entry is a tight edge
+    uint32_t *d_tcnt = nullptr;      // V: in-degree count / fill cursor
+    uint64_t *d_tptr = nullptr;      // V + 1
+    uint32_t *d_tu = nullptr;        // t_cap: source vertex
+    void *d_tw = nullptr;            // t_cap: latency in units of g (u32 or u64)
+    float *d_teb = nullptr;          // t_cap: 1 - loss, rounded once in f32
+    uint64_t t_cap = 0, t_edges = 0; // capacity / tight edges of the last run
+    uint64_t *h_tcount = nullptr;    // pinned: total tight edges
+    void *d_lscratch = nullptr;      // per workgroup: order array (+ rows if not in LDS)
+    size_t lscratch_cap = 0;
+    hipEvent_t ev_loss0 = nullptr, ev_loss1 = nullptr;  // around the loss pass
+    double loss_ms = 0.0;            // exact-loss pass of the last run (tight CSR + fold)
 };
 
 namespace srt {
@@ -146,7 +165,11 @@ srt_status comm_allgather_inplace(srt_comm *c, void *buf, size_t bytes_per_rank,
 // kernels (srt_fw.hip)
 void fw_init(srt_plan *p);
 srt_status fw_rounds(srt_plan *p, srt_err *err);
-void fw_extract(srt_plan *p);
+// exact-loss pass (srt_loss.hip): tight-edge CSR from the closure, then the
+// f32 left fold over the tight DAG for table rows [row0, row1); writes the
+// table rows, the raw self-loop diagonal and (min latency, unreachable) into
+// d_stats
+srt_status fw_loss(srt_plan *p, unsigned long long *d_stats, srt_err *err);
 // table entries [first, first + count) -> d_pack[0, count) as srt_path
 void pack_paths(srt_plan *p, uint64_t first, uint64_t count);
 // kernels (srt_sssp.hip)

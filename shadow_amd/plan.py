@@ -68,6 +68,12 @@ class RoutingPlan:
         _lib.lib().srt_plan_kernel_stats(self._h, C.byref(a), C.byref(b), C.byref(w), C.byref(c))
         return a.value, b.value, w.value, c.value
 
+    def timing(self) -> dict:
+        """Phase breakdown of the last run (srt_plan_timing)."""
+        t = _lib.SrtTiming()
+        _lib.check(_lib.lib().srt_plan_timing(self._h, C.byref(t)), _lib.SrtErr())
+        return {k: getattr(t, k) for k, _ in _lib.SrtTiming._fields_}
+
     def kernel_tiles(self) -> int:
         """C tiles the last run's dominant (FW rest) launches loaded and stored."""
         t = C.c_uint64()

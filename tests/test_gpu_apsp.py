@@ -1,8 +1,10 @@
 """GPU parity of the routing build (libsrt.so on gfx950) against the oracle.
 
-Bar (BASELINE.json north_star): latency bit-exact; packet_loss within 1e-6
-absolute (LOSS_TOL below); min latency exact; error codes/texts as the
-reference.  All calls go through the C ABI (shadow_amd.graph -> libsrt.so).
+Bar: latency AND packet_loss bit-exact for both kernel families (the dense
+closure's loss is folded over the tight shortest-path DAG, srt_loss.hip; the
+north_star's 1e-6 tolerance is not needed), min latency exact, error
+codes/texts as the reference.  All calls go through the C ABI
+(shadow_amd.graph -> libsrt.so).
 """
 import numpy as np
 import pytest
@@ -12,7 +14,6 @@ from shadow_amd import NetworkGraph, _lib, synth
 
 pytestmark = pytest.mark.gpu
 
-LOSS_TOL = 1e-6  # north_star: "packet_loss within 1e-6 absolute"
 
 GOLDEN_DIRECTED = [[3333, 3, 7], [5, 5555, 12], [16, 11, 7777]]
 GOLDEN_UNDIRECTED = [[3333, 3, 7], [3, 5555, 10], [7, 10, 7777]]
@@ -31,10 +32,8 @@ def _check(graph_edges, nodes, directed, n_nodes, node_ids=None, algo=_lib.SRT_A
     g = NetworkGraph.from_edges(n_nodes, src, dst, lat, loss, directed=directed, node_ids=ids)
     t = g.compute_shortest_paths(nodes, algo=algo)
     assert np.array_equal(t.latency_ns, elat), "latency must be bit-exact"
-    err = np.abs(t.packet_loss.astype(np.float64) - eloss.astype(np.float64))
-    assert err.max() <= LOSS_TOL, f"max loss error {err.max()}"
-    # diagonal is the raw self-loop edge, bit-exact (mod.rs:210-217)
-    assert np.array_equal(np.diag(t.packet_loss).view(np.uint32), np.diag(eloss).view(np.uint32))
+    bad = t.packet_loss.view(np.uint32) != eloss.view(np.uint32)
+    assert not bad.any(), f"{int(bad.sum())} loss entries differ in bits"
     assert t.min_latency_ns == int(elat.min())
     return t
 
@@ -77,7 +76,7 @@ def test_complete_c1_slice_through_gml():
     elat, eloss = O.compute_shortest_paths(og, nodes)
     t = g.compute_shortest_paths(nodes)
     assert np.array_equal(t.latency_ns, elat)
-    assert np.abs(t.packet_loss.astype(np.float64) - eloss).max() <= LOSS_TOL
+    assert np.array_equal(t.packet_loss.view(np.uint32), eloss.view(np.uint32))
 
 
 def test_loss_free_graph_exact_zero_loss():
@@ -166,22 +165,42 @@ def test_c2_scale_row_sample():
         exp_lat[r] = L[r, r]
         exp_loss[r] = t.packet_loss[r, r]
         assert np.array_equal(L[r], exp_lat)
-        assert np.abs(t.packet_loss[r].astype(np.float64) - exp_loss).max() <= LOSS_TOL
+        assert np.array_equal(t.packet_loss[r].view(np.uint32), exp_loss.view(np.uint32))
 
 
 def test_u64_key_path_large_latencies():
-    """Latencies up to 2^31 ns (~2 s, no common unit) on a 20-node sparse graph:
-    the latency field needs 37 bits, so the f64 key (53 bits) has no room for
-    a 2^-24 loss resolution and the closure runs on u64 keys (the LDS-DMA tile
-    kernel's integer branch); latency stays bit-exact."""
+    """Latencies up to 2^51 ns with no common unit on a 20-node sparse graph:
+    2 * Lmax does not fit 53 bits, so the closure runs on u64 keys (the LDS-DMA
+    tile kernel's integer branch) and the loss pass on u64 latencies (rows in
+    global memory); latency and loss stay bit-exact."""
     n = 20
     src, dst, lat, loss = synth.random_graph(n, 31, p_edge=0.3, lat_range_ns=(1, 2**31), loss_max=0.01)
+    lat = (lat.astype(np.uint64) << np.uint64(20)) + np.uint64(1)
     g = NetworkGraph.from_edges(n, src, dst, lat, loss)
     from shadow_amd.plan import RoutingPlan
     plan = RoutingPlan(g, np.arange(n, dtype=np.uint32), algo=_lib.SRT_ALGO_FW)
-    assert "u64key" in plan.describe()
+    assert "u64key" in plan.describe() and "loss=tight-dag/u64" in plan.describe()
     plan.close()
     _check((src, dst, lat, loss), np.arange(n, dtype=np.uint32), False, n, algo=_lib.SRT_ALGO_FW)
+
+
+def test_f64_key_wide_latency_range_buckets():
+    """ns latencies with no common unit (up to 2^31): the loss pass's latency
+    buckets are wider than one value (shift > 0) and repeat until stable."""
+    n = 60
+    src, dst, lat, loss = synth.random_graph(n, 32, p_edge=0.2, lat_range_ns=(1, 2**31), loss_max=0.05)
+    _check((src, dst, lat, loss), np.arange(n, dtype=np.uint32), False, n, algo=_lib.SRT_ALGO_FW)
+    src, dst, lat, loss = synth.random_graph(n, 33, p_edge=0.2, directed=True, lat_range_ns=(1000, 1900),
+                                             loss_max=0.05)
+    _check((src, dst, lat, loss), np.arange(n, dtype=np.uint32), True, n, algo=_lib.SRT_ALGO_FW)
+
+
+def test_zero_latency_rejected():
+    # ShadowEdge::try_from: "Edge 'latency' must not be 0" (mod.rs:104-106)
+    g = NetworkGraph.from_edges(2, [0, 1, 0], [0, 1, 1], [5, 5, 0], directed=False)
+    with pytest.raises(_lib.SrtError) as e:
+        g.compute_shortest_paths([0, 1])
+    assert e.value.code == _lib.SRT_ERR_INVALID and "must not be 0" in str(e.value)
 
 
 @pytest.mark.parametrize("algo", [_lib.SRT_ALGO_FW, _lib.SRT_ALGO_SSSP])

@@ -4,9 +4,9 @@ One GPU at rest-bound sizes (>= 64 blocks of 128) fuses FW rounds in groups
 of g = 4 (2 when the block count does not allow 4); SRT_FW_PAIR forces the
 grouped schedule at small sizes, SRT_FW_GROUP picks g and SRT_FW_NO_PAIR turns
 it off, so the same graph is closed every way.  Bar: latency bit-exact vs the
-oracle (reference Dijkstra restatement), loss within 1e-6, and the grouped
-table bit-identical to the single-round one (both compute the unique
-lexicographic minimum over paths of the exact integer keys).
+oracle (reference Dijkstra restatement), loss bit-exact (the exact-loss pass
+after the closure), and the grouped table bit-identical to the single-round
+one (both compute the unique minimum latencies).
 """
 import numpy as np
 import pytest

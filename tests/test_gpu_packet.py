@@ -1,7 +1,10 @@
 """GPU parity of the batched send_packet decision (srt_packet_batch) against
-the sequential oracle restatement of worker.rs:326-410.  Bar: flags, deliver
-times, RNG states after the round, per-path counters, min latency and next
-event time all bit-exact, given the same routing table."""
+the sequential oracle restatement of worker.rs:326-410, end to end: the GPU
+builds its routing table (dense closure + exact-loss pass) and decides the
+round; the oracle builds ITS OWN table (petgraph-faithful Dijkstra) and
+decides the same round on it.  Bar: tables, flags, deliver times, RNG states
+after the round, per-path counters, min latency and next event time all
+bit-exact."""
 import numpy as np
 import pytest
 
@@ -19,13 +22,17 @@ def _run(n_nodes, n_hosts, n_pkts, seed, bootstrap_end, sim_end, loss_max=0.25):
     g = NetworkGraph.from_edges(n_nodes, src, dst, lat, loss)
     plan = RoutingPlan(g, np.arange(n_nodes, dtype=np.uint32)).run()
     table = plan.fetch()
+    # the oracle's own table (not the GPU's): drop decisions read its loss bits
+    o_lat, o_loss = O.compute_shortest_paths(O.Graph(False, np.arange(n_nodes), src, dst, lat, loss),
+                                             np.arange(n_nodes, dtype=np.uint32))
+    assert np.array_equal(table.latency_ns, o_lat)
+    assert np.array_equal(table.packet_loss.view(np.uint32), o_loss.view(np.uint32))
     r0, r1 = 1_000_000_000, 1_000_000_000 + 5 * synth.MS
     pk, host_ptr, _ = synth.packet_round(n_hosts, n_nodes, n_pkts, seed, r0, r1)
     rng = synth.host_rng_states(n_hosts, general_seed=1)
-    # oracle: sequential, with the GPU's own table as input
     rng_o = rng.copy()
     cnt_o = np.zeros((n_nodes, n_nodes), np.uint64)
-    f_o, d_o, mn_o, ne_o = O.packet_batch(table.latency_ns, table.packet_loss, pk.view(O.PKT_DTYPE), rng_o,
+    f_o, d_o, mn_o, ne_o = O.packet_batch(o_lat, o_loss, pk.view(O.PKT_DTYPE), rng_o,
                                           r1, bootstrap_end, sim_end, counters=cnt_o)
     dev = torch.device("cuda:0")
     t_pk = torch.from_numpy(pk.view(np.uint8).copy()).to(dev)

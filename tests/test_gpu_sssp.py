@@ -143,7 +143,7 @@ def test_c4_graph_row_sample():
 
 
 def test_fw_and_sssp_agree_on_latency():
-    # the dense closure (tolerance on loss) and the sparse sweep (exact loss) on one graph
+    # the dense closure + exact-loss pass and the sparse sweep on one graph: same bits
     n = 300
     e = synth.random_graph(n, 77, p_edge=0.03, lat_range_ns=(1, 6), loss_max=0.02)
     g = NetworkGraph.from_edges(n, *e)
@@ -151,7 +151,7 @@ def test_fw_and_sssp_agree_on_latency():
     a = g.compute_shortest_paths(nodes, algo=_lib.SRT_ALGO_FW)
     b = g.compute_shortest_paths(nodes, algo=SSSP)
     assert np.array_equal(a.latency_ns, b.latency_ns)
-    assert np.abs(a.packet_loss.astype(np.float64) - b.packet_loss).max() <= 1e-6
+    assert np.array_equal(a.packet_loss.view(np.uint32), b.packet_loss.view(np.uint32))
 
 
 @pytest.mark.parametrize("act", ["2", "3", "0"])
