@@ -180,6 +180,10 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_tu);
     hipFree(p->d_tw);
     hipFree(p->d_teb);
+    hipFree(p->d_tpk);
+    hipFree(p->d_tpk2);
+    hipFree(p->d_tsort_tmp);
+    hipFree(p->d_tmaxw);
     hipFree(p->d_lscratch);
     if (p->h_sflag) hipHostFree(p->h_sflag);
     if (p->h_tcount) hipHostFree(p->h_tcount);

@@ -146,11 +146,17 @@ struct srt_plan {
     uint8_t *d_tflag = nullptr;      // n_adj: adjacency entry is a tight edge
     uint32_t *d_tcnt = nullptr;      // V: in-degree count / fill cursor
     uint64_t *d_tptr = nullptr;      // V + 1
-    uint32_t *d_tu = nullptr;        // t_cap: source vertex
-    void *d_tw = nullptr;            // t_cap: latency in units of g (u32 or u64)
-    float *d_teb = nullptr;          // t_cap: 1 - loss, rounded once in f32
+    uint32_t *d_tu = nullptr;        // t_cap: source vertex (unpacked form)
+    void *d_tw = nullptr;            // t_cap: latency in units of g (u32 or u64; unpacked form)
+    float *d_teb = nullptr;          // t_cap: 1 - loss, rounded once in f32 (unpacked form)
+    uint64_t *d_tpk = nullptr;       // t_cap: packed form, (1-e) bits << 32 | (w << ubits) | u, rows sorted by w
+    uint64_t *d_tpk2 = nullptr;      // t_cap: packed form before the sort
+    void *d_tsort_tmp = nullptr;     // rocPRIM segmented sort scratch
+    size_t tsort_tmp_cap = 0;
+    uint64_t *d_tmaxw = nullptr;     // max latency (units) of a tight edge
     uint64_t t_cap = 0, t_edges = 0; // capacity / tight edges of the last run
-    uint64_t *h_tcount = nullptr;    // pinned: total tight edges
+    bool t_packed = false;           // the last run used the packed, w-sorted form
+    uint64_t *h_tcount = nullptr;    // pinned: [0] total tight edges, [1] max tight latency
     void *d_lscratch = nullptr;      // per workgroup: order array (+ rows if not in LDS)
     size_t lscratch_cap = 0;
     hipEvent_t ev_loss0 = nullptr, ev_loss1 = nullptr;  // around the loss pass

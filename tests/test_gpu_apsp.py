@@ -222,3 +222,15 @@ def test_isolated_unused_nodes_are_fine():
     nodes = np.arange(70, dtype=np.uint32)
     for algo in (_lib.SRT_ALGO_FW, _lib.SRT_ALGO_SSSP):
         _check((src[m], dst[m], lat[m], loss[m]), nodes, False, n, algo=algo)
+
+
+@pytest.mark.parametrize("seed", range(3))
+@pytest.mark.parametrize("directed", [False, True])
+def test_loss_pass_unpacked_form(monkeypatch, seed, directed):
+    """The loss pass's unpacked tight-edge form (separate u / w arrays, rows not
+    sorted by w: the fallback when vertex index and tight latency do not share
+    32 bits) gives the same bits as the oracle."""
+    monkeypatch.setenv("SRT_LOSS_UNPACKED", "1")
+    n = 90 + 17 * seed
+    e = synth.random_graph(n, 200 + seed, p_edge=0.12, directed=directed, lat_range_ns=(1, 5), loss_max=0.05)
+    _check(e, np.random.default_rng(seed).permutation(n).astype(np.uint32), directed, n, algo=_lib.SRT_ALGO_FW)

@@ -71,3 +71,30 @@ def test_groups_equal_single_round(monkeypatch, n):
         assert tp.min_latency_ns == ts.min_latency_ns
     L = ts.latency_ns
     assert np.array_equal(L, L.T)
+
+
+@pytest.mark.parametrize("n,seed,directed", [(1000, 11, False), (1300, 12, True)])
+def test_key_types_agree(monkeypatch, n, seed, directed):
+    """The closure's three key representations (u32 by default when 2 lmax <
+    2^31 - 1, f64 and u64 forced by SRT_FW_KEY) produce the same table bits,
+    single-round and grouped."""
+    e = synth.random_graph(n, seed, p_edge=6.0 / n, directed=directed, lat_range_ns=(1, 9), loss_max=0.05)
+    g = NetworkGraph.from_edges(n, *e, directed=directed)
+    nodes = np.random.default_rng(seed).permutation(n).astype(np.uint32)
+    tabs = {}
+    for key in ("u32", "f64", "u64"):
+        if key == "u32":
+            monkeypatch.delenv("SRT_FW_KEY", raising=False)
+        else:
+            monkeypatch.setenv("SRT_FW_KEY", key)
+        for grp in ("1", "2"):
+            monkeypatch.setenv("SRT_FW_PAIR", "1")
+            monkeypatch.setenv("SRT_FW_GROUP", grp)
+            plan = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_FW)
+            assert f"{key}key" in plan.describe()
+            tabs[(key, grp)] = plan.run().fetch()
+            plan.close()
+    ref = tabs[("u32", "1")]
+    for k, t in tabs.items():
+        assert np.array_equal(t.latency_ns, ref.latency_ns), k
+        assert np.array_equal(t.packet_loss.view(np.uint32), ref.packet_loss.view(np.uint32)), k
