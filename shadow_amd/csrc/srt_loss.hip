@@ -214,15 +214,19 @@ __device__ __forceinline__ uint32_t agg_inc(uint32_t *hist, uint32_t b, bool act
 constexpr uint32_t HIST_BYTES = ((NBK + 1) * 4 + 15) & ~15u;
 
 // One pass over the members ord[m0, m1) of a bucket, packed form: LPT lanes
-// per target, 4 in-edges per lane per step.  The edge array is padded past
-// its end, so the 4 loads of a step are unconditional (one 8-B load each:
+// per target, UNR in-edges per lane per step (loads in flight: the scan is
+// latency bound).  The edge array is padded past its end, so the UNR loads of
+// a step are unconditional (one 8-B load each:
 // {word, 1-e}); a slot counts only if it is inside the row and its w <= lv
-// (rows are sorted by w, so a lane stops at its first w > lv).  Tight
+// (rows are sorted by w).  Tight
 // candidates go into prow[v] by LDS atomic min on the f32 bits (non-negative
-// floats order like their bits); ITER (buckets wider than one latency) also
+// floats order like their bits); a tight edge with w == lv can only start at
+// s (every other vertex has latency >= 1), and those were pushed from s's
+// adjacency row beforehand, so a lane stops at w >= lv.  ITER (buckets wider
+// than one latency) also
 // reports whether any value dropped.  The next target's record is loaded
 // while the current one is scanned.
-template <typename LatT, int LPT, bool ITER>
+template <typename LatT, int LPT, int UNR, bool ITER>
 __device__ __forceinline__ int scan_bucket_packed(const uint4 *__restrict__ ord, uint32_t m0, uint32_t m1,
                                                   uint32_t grp, uint32_t sub, uint32_t ngrp,
                                                   const uint64_t *__restrict__ tpk, const LatT *lrow, float *prow,
@@ -237,31 +241,31 @@ __device__ __forceinline__ int scan_bucket_packed(const uint4 *__restrict__ ord,
         const LatT lv = (LatT)cur.w;
         const uint64_t *wp = tpk + cur.y + sub;
         uint32_t *dst = reinterpret_cast<uint32_t *>(prow) + v;
-        for (uint32_t e = cur.y + sub; e < e1; e += 4 * LPT, wp += 4 * LPT) {
-            uint64_t wd[4];
+        for (uint32_t e = cur.y + sub; e < e1; e += UNR * LPT, wp += UNR * LPT) {
+            uint64_t wd[UNR];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) wd[q] = wp[q * LPT];
-            bool ok[4];
-            uint32_t u[4];
-            LatT need[4], lu[4];
+            for (int q = 0; q < UNR; ++q) wd[q] = wp[q * LPT];
+            bool ok[UNR];
+            uint32_t u[UNR];
+            LatT need[UNR], lu[UNR];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < UNR; ++q) {
                 const uint32_t lo = (uint32_t)wd[q], w = lo >> ubits;
-                ok[q] = e + q * LPT < e1 && (LatT)w <= lv;
+                ok[q] = e + q * LPT < e1 && (LatT)w < lv;  // w == lv: only from s (pushed)
                 u[q] = ok[q] ? lo & umask : 0u;
                 need[q] = lv - (LatT)w;
             }
 #pragma unroll
-            for (int q = 0; q < 4; ++q) lu[q] = lrow[u[q]];
+            for (int q = 0; q < UNR; ++q) lu[q] = lrow[u[q]];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < UNR; ++q) {
                 if (ok[q] && lu[q] == need[q]) {
                     const float c = 1.0f - __fmul_rn(1.0f - prow[u[q]], __uint_as_float((uint32_t)(wd[q] >> 32)));
                     if constexpr (ITER) changed |= __float_as_uint(c) < atomicMin(dst, __float_as_uint(c));
                     else atomicMin(dst, __float_as_uint(c));
                 }
             }
-            if (!ok[3]) break;
+            if (!ok[UNR - 1]) break;
         }
     }
     return changed;
@@ -274,7 +278,9 @@ __global__ __launch_bounds__(LOSS_NT) void tight_loss_kernel(
     const LatT *__restrict__ tw, const float *__restrict__ teb, const uint64_t *__restrict__ tpk, uint32_t ubits,
     uint64_t g, const uint64_t *__restrict__ sl_lat, const float *__restrict__ sl_loss,
     uint64_t *__restrict__ out_lat, float *__restrict__ out_loss, unsigned long long *stats,
-    uint4 *__restrict__ ord_all, LatT *lat_all, float *loss_all, uint32_t diag) {
+    uint4 *__restrict__ ord_all, LatT *lat_all, float *loss_all, const uint64_t *__restrict__ row_ptr,
+    const uint32_t *__restrict__ col, const uint64_t *__restrict__ elat, const float *__restrict__ eloss,
+    uint32_t diag) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ uint64_t red[16];
     __shared__ unsigned long long red_min[16], red_cnt[16];
@@ -337,6 +343,17 @@ __global__ __launch_bounds__(LOSS_NT) void tight_loss_kernel(
         }
         if (tid == 0) prow[s] = 0.0f;  // petgraph's zero score (0 ns, 0.0)
         __syncthreads();
+        // the one-hop tight paths: s's own edges s -> v with lat == lat[s][v]
+        // (fold(0, e) = 1 - (1 - 0) (1 - e)); the bucket scans then skip
+        // every in-edge with w == lat[s][v], whose tail can only be s
+        for (uint64_t k = row_ptr[s] + tid; k < row_ptr[s + 1]; k += nt) {
+            const uint32_t v = col[k];
+            const LatT l = lrow[v];
+            if (v != s && l != LINF && (uint64_t)l * g == elat[k]) {
+                const float c = 1.0f - __fmul_rn(1.0f - 0.0f, 1.0f - eloss[k]);
+                atomicMin(reinterpret_cast<uint32_t *>(prow) + v, __float_as_uint(c));
+            }
+        }
         {  // exclusive scan of hist[0, NBK): each thread a contiguous run
             const uint32_t per = (NBK + nt - 1) / nt, b0 = std::min<uint32_t>(NBK, tid * per),
                            b1 = std::min<uint32_t>(NBK, b0 + per);
@@ -379,10 +396,10 @@ __global__ __launch_bounds__(LOSS_NT) void tight_loss_kernel(
                 int changed = 0;
                 if constexpr (PACKED) {
                     if (shift)
-                        changed = scan_bucket_packed<LatT, LPT, true>(ord, m0, m1, grp, sub, ngrp, tpk, lrow, prow,
+                        changed = scan_bucket_packed<LatT, LPT, 8, true>(ord, m0, m1, grp, sub, ngrp, tpk, lrow, prow,
                                                                       ubits, umask);
                     else
-                        scan_bucket_packed<LatT, LPT, false>(ord, m0, m1, grp, sub, ngrp, tpk, lrow, prow, ubits,
+                        scan_bucket_packed<LatT, LPT, 8, false>(ord, m0, m1, grp, sub, ngrp, tpk, lrow, prow, ubits,
                                                              umask);
                 } else {
                     for (uint32_t base = m0; base < m1; base += ngrp) {
@@ -547,8 +564,8 @@ srt_status launch_fold(srt_plan *p, unsigned long long *d_stats, uint32_t ubits,
         hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, p->stream, (const void *)p->d_D, p->key_type, p->Vp, V,
                            p->d_nodes, p->n, p->row0, p->row1, p->d_tptr, p->d_tu,
                            reinterpret_cast<const LatT *>(p->d_tw), p->d_teb, p->d_tpk, ubits, p->kp.g, p->d_sl_lat,
-                           p->d_sl_loss, p->d_out_lat, p->d_out_loss, d_stats, ord, lat_all, loss_all,
-                           std::getenv("SRT_LOSS_DIAG") ? (uint32_t)std::atoi(std::getenv("SRT_LOSS_DIAG")) : 0u);
+                           p->d_sl_loss, p->d_out_lat, p->d_out_loss, d_stats, ord, lat_all, loss_all, p->d_row_ptr,
+                           p->d_col, p->d_lat, p->d_loss, std::getenv("SRT_LOSS_DIAG") ? (uint32_t)std::atoi(std::getenv("SRT_LOSS_DIAG")) : 0u);
     return SRT_OK;
 }
 
@@ -557,7 +574,16 @@ srt_status launch_fold_lpt(srt_plan *p, unsigned long long *d_stats, uint32_t ub
     // lanes per target ~ the average tight in-degree (a group walks a target's
     // in-edges 2-4 per lane per step)
     const double avg = p->V ? (double)p->t_edges / p->V : 0.0;
-    if (avg > 48.0) return launch_fold<LatT, LROWS, PACKED ? 16 : 32, PACKED>(p, d_stats, ubits, err);
+    if constexpr (PACKED) {
+        // 4 lanes x 8 edges per target (C3, same box: 4 / 8 / 16 lanes ->
+        // 31.9 / 33.0 / 36.5 ms for the pass; knob SRT_LOSS_LPT = 8 / 16)
+        const char *k = std::getenv("SRT_LOSS_LPT");
+        if (k && std::atoi(k) == 8) return launch_fold<LatT, LROWS, 8, PACKED>(p, d_stats, ubits, err);
+        if (k && std::atoi(k) == 16) return launch_fold<LatT, LROWS, 16, PACKED>(p, d_stats, ubits, err);
+        if (avg > 10.0) return launch_fold<LatT, LROWS, 4, PACKED>(p, d_stats, ubits, err);
+        return launch_fold<LatT, LROWS, 2, PACKED>(p, d_stats, ubits, err);
+    }
+    if (avg > 48.0) return launch_fold<LatT, LROWS, 32, PACKED>(p, d_stats, ubits, err);
     if (avg > 10.0) return launch_fold<LatT, LROWS, 8, PACKED>(p, d_stats, ubits, err);
     return launch_fold<LatT, LROWS, 2, PACKED>(p, d_stats, ubits, err);
 }
@@ -601,10 +627,10 @@ srt_status tight_csr_t(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     p->t_packed = p->kp.lat32 && ubits + bits_of(maxw) <= 32 && p->t_edges < (1ull << 32) &&
                   !std::getenv("SRT_LOSS_UNPACKED");
     const size_t wsz = p->kp.lat32 ? 4 : 8;
-    if (p->t_edges + 512 > p->t_cap || !p->d_tu) {
+    if (p->t_edges + 1024 > p->t_cap || !p->d_tu) {
         // grow every edge array together (25% headroom)
-        // (+512: the packed scan reads up to 3 * LPT entries past a row's end)
-        const uint64_t cap = std::max<uint64_t>(p->t_edges + p->t_edges / 4 + 512, 1024);
+        // (+1024: the packed scan reads up to (UNR - 1) * LPT entries past a row's end)
+        const uint64_t cap = std::max<uint64_t>(p->t_edges + p->t_edges / 4 + 1024, 2048);
         for (void *q : {(void *)p->d_tu, p->d_tw, (void *)p->d_teb, (void *)p->d_tpk, (void *)p->d_tpk2})
             (void)hipFree(q);
         p->d_tu = nullptr;
