@@ -4,23 +4,34 @@ routing-table build wall-clock, 16k-node graph at 1/2/4/8 MI355X).
 Default workload (--config c3): one "step" = one full routing build of the
 16,384-node complete undirected graph (config C3: latency U{1..300} ms, loss
 U[0,0.01], self-loops, seed 3), from the CSR resident in HBM to the n x n
-(latency, loss) table resident in HBM (all-gathered on every rank for N > 1).
-value = n^2 pairs / step time.
+(latency, loss) table resident in HBM (all-gathered on every rank for N > 1):
+the latency closure plus the exact-loss pass.  value = n^2 pairs / step time.
+Beside it the line carries the end-to-end build through the C ABI
+(srt_compute_shortest_paths: host CSR in, srt_path[n*n] in the caller's host
+buffer out, every validation and PCIe copy included) -- BASELINE.md's t_build.
 
-Other configs (not the headline line, same JSON shape):
+Other configs (same JSON shape):
+  --config c1   1,000-node complete graph through its GML TEXT: parse + build +
+                fetch to the host per step; the reference CPU path (faithful
+                restatement, all sources) is timed in full beside it
   --config c2   4,096-node complete graph (blocked Floyd-Warshall, 1 GPU)
   --config c4   100,000-node Barabasi-Albert graph, m=4 (batched sparse sweep)
   --config c5   1M packets/round send_packet decision on the C1 table (packets/s)
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3]
-Multi-GPU: launched by torch.distributed.run, one rank per GPU (RCCL).
-Prints one JSON line on rank 0.
+Multi-GPU: one rank per GPU (RCCL), launched by torch.distributed.run; run as
+`python bench.py --gpus N` without a launcher it starts the N ranks itself
+(before any GPU call) and exits with their status.  Prints one JSON line on
+rank 0.
 """
 from __future__ import annotations
 
 import argparse
+import ctypes as C
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -29,22 +40,23 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# MI355X constants (/opt/skills/guides/MI355X_MICROARCH.md): FP64 vector peak
-# 78.6 TFLOP/s counts an FMA as 2 -> 39.3e12 f64 lane-ops/s (v_add_f64 and
-# v_min_f64 each one op; tools/valu_bench measured 36.5e12).  One lexicographic
-# (latency, loss) relaxation on the f64-encoded path key is one v_add_f64 + one
-# v_min_f64.
-F64_LANE_OPS_PEAK = 256 * 64 * 2.4e9  # 39.3e12
-OPS_PER_RELAX = 2
-RELAX_PEAK = F64_LANE_OPS_PEAK / OPS_PER_RELAX  # 19.66e12 relaxations/s
+# MI355X constants (/opt/skills/guides/MI355X_MICROARCH.md; profiles/r01_valu_bench.txt)
+VALU_LANE_OPS_PEAK = 256 * 64 * 2.4e9  # 39.3e12 lane-ops/s (one 4-cycle VALU slot per lane per cycle)
+# u32 latency keys: 2 v_add_u32 (double rate) + 1 v_min3_u32 per 2 relaxations =
+# 2 slots per 2 relaxations -> one slot per relaxation
+RELAX_PEAK = {"u32": VALU_LANE_OPS_PEAK / 1.0, "f64": VALU_LANE_OPS_PEAK / 2.0, "u64": VALU_LANE_OPS_PEAK / 4.0}
+RELAX_BASIS = {"u32": "2 v_add_u32 (issued at twice the rate) + 1 v_min3_u32 per 2 relaxations = 1 VALU slot",
+               "f64": "v_add_f64 + v_min_f64 = 2 VALU slots", "u64": "v_lshl_add_u64 + v_cmp + 2 v_cndmask = 4 slots"}
 HBM_PEAK = 8.0e12  # B/s
 
 CONFIGS = {
+    "c1": dict(kind="gml", nodes=1000, seed=1),
     "c2": dict(kind="complete", nodes=4096, seed=2),
     "c3": dict(kind="complete", nodes=16384, seed=3),
     "c4": dict(kind="ba", nodes=100_000, seed=4, m=4),
     "c5": dict(kind="packets", nodes=1000, seed=5, hosts=10_000, packets=1_000_000),
 }
+PATH_DTYPE = np.dtype([("lat", "<u8"), ("loss", "<f4"), ("pad", "<u4")])
 
 
 def parse_args():
@@ -59,8 +71,9 @@ def parse_args():
     ap.add_argument("--seed", type=int, default=-1)
     ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the CPUs this process may use")
     ap.add_argument("--cpu-sources", type=int, default=0, help="0 = auto (~10-30 s of CPU work)")
+    ap.add_argument("--no-e2e", dest="e2e", action="store_false", default=True)
     ap.add_argument("--emulate-ranks", dest="emulate_ranks", type=int, default=0,
                     help="measurement only (dense FW, 1 GPU): time one rank of an N-rank run -- 1/N of the "
                          "block-rows plus the pivot owner's chain every round, no collectives; the table "
@@ -68,17 +81,40 @@ def parse_args():
     return ap.parse_args()
 
 
-def cpu_baseline(og, nodes, threads, sources, label, target_s=15.0, mode=0):
+def cpu_share():
+    """Threads the CPU baseline runs on: the CPUs this process may use (rayon's
+    default pool is every logical CPU it sees), capped by the job's CPU share
+    when the box declares one (OMP_NUM_THREADS), plus the CPU model."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(aff, share) if share > 0 else aff
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return threads, aff, model
+
+
+def cpu_baseline(og, nodes, threads, sources, label, target_s=15.0, mode=0, full=False):
     """The oracle's faithful restatement of compute_shortest_paths (mode 0:
     hash-map Dijkstra per source, the `nodes.contains` filter, per-source map,
     merged map; rayon-style pool) -- or its array-based variant (mode 1, the
     same algorithm without the hash maps: an "opt-cpu" for honesty) -- timed on
-    a bounded sample of sources of the same graph; pairs/s extrapolated
-    linearly (sources are independent, mod.rs:190-208)."""
+    a bounded sample of sources of the same graph (all of them when full);
+    pairs/s extrapolated linearly (sources are independent, mod.rs:190-208)."""
     from oracle import oracle as O
 
     n = len(nodes)
-    if sources <= 0:
+    if full:
+        sources = n
+    elif sources <= 0:
         # calibrate: one source per thread, then scale to ~target_s
         t0 = time.perf_counter()
         O.compute_shortest_paths(og, nodes, threads=threads, mode=mode, src_count=threads)
@@ -89,24 +125,28 @@ def cpu_baseline(og, nodes, threads, sources, label, target_s=15.0, mode=0):
     dt = time.perf_counter() - t0
     what = ("faithful hash-map Dijkstra (oracle mode 0)" if mode == 0 else
             "array-score Dijkstra, same algorithm without the hash maps (oracle mode 1)")
+    _, aff, model = cpu_share()
     return {"value": sources * n / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"{sources} of {n} sources of the same {label} graph, {what}, {dt:.1f} s wall, "
-                      f"extrapolated linearly to pairs/s"}
+            "cpu_model": model, "cpus_visible": aff,
+            "sample": (f"all {n} sources" if sources == n else f"{sources} of {n} sources") +
+                      f" of the same {label} graph, {what}, {dt:.2f} s wall" +
+                      ("" if sources == n else ", extrapolated linearly to pairs/s")}
 
 
-def measured_traffic(args, kernel_tag):
-    """HBM bytes per launch of the dominant kernel from the latest committed
-    PMC summary (profiles/rNN_pmc_traffic.json: FETCH_SIZE and WRITE_SIZE
-    passes of rocprofv3 on this same workload, gfx950 corrections applied), or
-    None."""
+def measured_traffic(args, kernel_tag, schedule):
+    """HBM bytes per launch of the dominant kernel from the newest committed PMC
+    summary (profiles/rNN*_pmc_traffic.json: FETCH_SIZE and WRITE_SIZE passes of
+    rocprofv3 on this same workload and schedule, gfx950 corrections applied),
+    or None.  A summary counts only if its config name, node count and recorded
+    schedule (key type, rounds per launch, ranks) match this run's."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
     for f in reversed(files):
         d = json.load(open(f))
-        # summaries are labelled "C3 16k complete graph, 1 GPU": match the
-        # config name, and the node count too when --nodes overrides it
         cfg = d.get("config", "")
         if not cfg.startswith(args.config.upper() + " ") or (args.nodes and str(args.nodes) not in cfg):
+            continue
+        if d.get("schedule") != schedule:
             continue
         for k, v in d.get("kernels", {}).items():
             if kernel_tag in k:
@@ -115,14 +155,13 @@ def measured_traffic(args, kernel_tag):
 
 
 class Dist:
-    def __init__(self, gpus):
+    def __init__(self):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        self.n_gpus = max(gpus, self.world)
         if self.world > 1:
             torch.cuda.set_device(self.local_rank)
             dist.init_process_group("nccl", device_id=torch.device("cuda", self.local_rank))
@@ -166,6 +205,94 @@ def timed_builds(plan, D, steps, warmup):
     return elapsed, step_ms, k_ms, k_launches, k_work, k_tiles
 
 
+def e2e_build(g, nodes, reps=2):
+    """BASELINE.md t_build: srt_compute_shortest_paths from the host CSR to the
+    srt_path table in the caller's (pre-touched, reused) host buffer -- plan
+    creation and validation, the CSR upload, the build, the download -- as the
+    Rust shim would call it.  Best of `reps` calls."""
+    from shadow_amd import _lib
+
+    L = _lib.lib()
+    n = len(nodes)
+    out = np.empty(n * n, PATH_DTYPE)  # the caller's table: pages touched once, like a reused Vec
+    out.view(np.uint8).fill(0)
+    nodes = np.ascontiguousarray(nodes, np.uint32)
+    csr = g.csr()
+    opts = _lib.SrtOpts(_lib.SRT_ALGO_AUTO, -1, 0, 0)
+    best = None
+    for _ in range(reps):
+        err, mn = _lib.SrtErr(), C.c_uint64()
+        t0 = time.perf_counter()
+        rc = L.srt_compute_shortest_paths(C.byref(csr), nodes.ctypes.data_as(C.POINTER(C.c_uint32)), n,
+                                          out.ctypes.data_as(C.POINTER(_lib.SrtPath)), C.byref(mn), C.byref(opts),
+                                          C.byref(err))
+        dt = time.perf_counter() - t0
+        _lib.check(rc, err)
+        best = dt if best is None else min(best, dt)
+    return {"ms": best * 1e3, "pairs_per_s": n * n / best, "calls": reps,
+            "span": "srt_compute_shortest_paths: host CSR (borrowed) -> srt_path[n*n] in the caller's host buffer; "
+                    "validation, CSR upload, build, table download and plan teardown included"}
+
+
+def gml_graph(n_nodes, seed):
+    from shadow_amd import synth
+    src, dst, lat, loss = synth.complete_graph(n_nodes, seed)
+    return synth.gml_text(n_nodes, src, dst, lat, loss)
+
+
+def bench_gml(args, cfg, D):
+    """C1: a step = NetworkGraph::parse of the GML text (srt_gml_parse) + the
+    routing build + the table in host memory (srt_compute_shortest_paths) --
+    the reference's generate_routing_info span on this input.  The CPU
+    reference path (oracle GML parse + faithful Dijkstra over all sources) is
+    timed in full beside it."""
+    from shadow_amd import NetworkGraph
+
+    n_nodes = args.nodes or cfg["nodes"]
+    seed = cfg["seed"] if args.seed < 0 else args.seed
+    text = gml_graph(n_nodes, seed)
+    nodes = np.arange(n_nodes, dtype=np.uint32)
+
+    def step():
+        g = NetworkGraph.parse(text)
+        return e2e_build(g, nodes, reps=1)
+
+    for _ in range(args.warmup):
+        step()
+    D.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    D.barrier()
+    elapsed = D.max_over_ranks(time.perf_counter() - t0)
+    out = None
+    if D.rank == 0:
+        per = elapsed / args.steps
+        cpu = None
+        if args.cpu_baseline:
+            from oracle import oracle as O
+            threads = args.cpu_threads or cpu_share()[0]
+            t1 = time.perf_counter()
+            og = O.gml_parse(text)
+            parse_s = time.perf_counter() - t1
+            cpu = cpu_baseline(og, nodes, threads, 0, "C1", full=True)
+            cpu["sample"] += f"; plus the oracle's GML parse ({parse_s:.2f} s, not in value)"
+        out = {
+            "metric": "APSP pairs/sec (routing-table build from GML text, 1k-node graph)",
+            "value": D.world * n_nodes * n_nodes / per, "unit": "pairs/s", "n_gpus": D.world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": per * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (seeded complete GML graph, latency U{1..300} ms, loss U[0,0.01])",
+            "config": {"workload": f"C1: {n_nodes}-node complete undirected GML graph, use_shortest_path=true: "
+                                   f"GML text -> srt_gml_parse -> srt_compute_shortest_paths -> host table",
+                       "nodes": n_nodes, "pairs": n_nodes * n_nodes, "gml_bytes": len(text),
+                       "parallelism": "replicas" if D.world > 1 else "single"},
+            "roofline": None,
+            "cpu_baseline": cpu,
+        }
+    return out
+
+
 def bench_graph(args, cfg, D):
     from shadow_amd import NetworkGraph, synth
     from shadow_amd.plan import RoutingPlan
@@ -176,7 +303,8 @@ def bench_graph(args, cfg, D):
         row_ptr, col, lat, loss = synth.complete_csr(n_nodes, seed)
         g = NetworkGraph(n_nodes, np.arange(n_nodes, dtype=np.uint32), row_ptr, col, lat, loss, directed=False)
         nodes = np.arange(n_nodes, dtype=np.uint32)
-        label = f"{args.config.upper()}: {n_nodes}-node complete undirected GML graph"
+        label = (f"{args.config.upper()}: {n_nodes}-node complete undirected graph (CSR built directly; the same "
+                 f"values as the GML text of synth.gml_text, GML ingest not in this step)")
         data = "synthetic (seeded complete graph, latency U{1..300} ms, loss U[0,0.01])"
         og_args = None
         del row_ptr, col, lat, loss
@@ -193,6 +321,7 @@ def bench_graph(args, cfg, D):
     if args.emulate_ranks > 1:
         os.environ["SRT_FW_EMULATE_RANKS"] = str(args.emulate_ranks)
     plan = RoutingPlan(g, nodes, device=D.dev)
+    ranks = 1
     if D.world > 1:
         from shadow_amd import dist as sdist
         transport = os.environ.get("SRT_COMM", "rccl")
@@ -205,6 +334,10 @@ def bench_graph(args, cfg, D):
                   file=sys.stderr, flush=True)
             sdist.bind(plan, D.rank, D.world, D.local_rank, transport="torch")
     desc = plan.describe()
+    if " ranks=" in desc:
+        ranks = int(desc.split(" ranks=")[1].split()[0])
+    if ranks != D.world:
+        raise SystemExit(f"plan bound to {ranks} ranks but WORLD_SIZE={D.world}")
     elapsed, step_ms, k_ms, k_launches, k_work, k_tiles = timed_builds(plan, D, args.steps, args.warmup)
     if args.emulate_ranks > 1:
         print(json.dumps({"emulated_ranks": args.emulate_ranks, "config": args.config, "ms_per_step":
@@ -214,38 +347,49 @@ def bench_graph(args, cfg, D):
         return None
     timing = plan.timing()  # phase breakdown of the last timed build
     plan.fetch(table=False)  # connectivity check + min latency (not timed)
+    plan.close()
     n = len(nodes)
+    e2e = None
+    if args.e2e and D.world == 1 and cfg["kind"] == "complete":
+        e2e = e2e_build(g, nodes)
     out = None
     if D.rank == 0:
         pairs = n * n
         ms_per_step = elapsed * 1e3 / args.steps
         avg_launch_s = (k_ms / 1e3) / max(k_launches, 1)
         work_per_launch = k_work / max(k_launches, 1)
+        key = desc.split(":")[1][:3] if desc.startswith("fw") else "u64"
         if desc.startswith("fw"):
             B_TILE = 128
+            kbytes = 4 if key == "u32" else 8
             achieved = work_per_launch / avg_launch_s
-            traffic, traffic_src = measured_traffic(args, "phase 3 rest")
-            if D.world > 1:  # the committed PMC pass is of the 1-GPU launch (all 126^2 tiles)
-                traffic, traffic_src = None, "PMC traffic is profiled at N=1 only"
+            rounds = k_work / max(k_tiles * B_TILE ** 3, 1)
+            schedule = {"key": key, "launch_rounds": int(round(rounds)), "ranks": D.world}
+            traffic, traffic_src = measured_traffic(args, "minplus", schedule)
+            peak = RELAX_PEAK[key]
             roofline = {
-                "bound": "valu", "achieved": achieved / 1e12, "peak": RELAX_PEAK / 1e12, "unit": "Trelax/s",
-                "frac": achieved / RELAX_PEAK, "traffic": traffic, "traffic_unit": "HBM bytes per launch",
-                "traffic_source": traffic_src,
+                "bound": "valu", "achieved": achieved / 1e12, "peak": peak / 1e12, "unit": "Trelax/s",
+                "frac": achieved / peak, "traffic": traffic,
+                "traffic_unit": "HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction)",
+                "traffic_source": (f"{traffic_src}: committed rocprofv3 PMC summary of this workload and schedule, "
+                                   f"not measured in this run" if traffic_src else
+                                   "no committed PMC summary for this workload/schedule"),
+                "schedule": schedule,
                 # every C tile read + written once per launch (A/B panels hit L2/MALL)
-                "algorithmic_hbm_bytes_per_launch": k_tiles / max(k_launches, 1) * B_TILE * B_TILE * 2 * 8,
-                "rounds_per_tile": k_work / max(k_tiles * B_TILE ** 3, 1),  # 2: paired rounds (1 GPU)
-                "kernel": "minplus_glds_kernel<double, 0> (FW phase 3, rest)", "avg_launch_ms": avg_launch_s * 1e3,
-                "relax_per_launch": work_per_launch,
-                "peak_basis": f"{F64_LANE_OPS_PEAK / 1e12:.1f}e12 f64 VALU lane-ops/s / {OPS_PER_RELAX} ops "
-                              f"(v_add_f64 + v_min_f64) per relaxation; the SURVEY's INT-VALU basis (5 int32 ops "
-                              f"per u64 relaxation) would be 7.86 Trelax/s"}
-            algo = "blocked Floyd-Warshall"
+                "algorithmic_hbm_bytes_per_launch": k_tiles / max(k_launches, 1) * B_TILE * B_TILE * 2 * kbytes,
+                "rounds_per_tile": rounds,
+                "kernel": f"minplus_{'u32' if key == 'u32' else 'glds'}_kernel<0> (FW phase 3, rest)",
+                "avg_launch_ms": avg_launch_s * 1e3, "relax_per_launch": work_per_launch,
+                "peak_basis": f"{VALU_LANE_OPS_PEAK / 1e12:.1f}e12 VALU lane-op slots/s; {key} keys: "
+                              f"{RELAX_BASIS[key]} per relaxation (f64 keys would peak at 19.7, the SURVEY's "
+                              f"5-int32-op u64 basis at 7.86 Trelax/s)"}
+            algo = "blocked Floyd-Warshall (u32 latency closure) + exact-loss fold over the tight DAG"
         else:
             achieved = work_per_launch / avg_launch_s
-            traffic, traffic_src = measured_traffic(args, "sssp_sweep")
             roofline = {
                 "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK, "traffic": traffic, "traffic_source": traffic_src,
+                "frac": achieved / HBM_PEAK, "traffic": None,
+                "traffic_source": "PMC traffic of the sweep: profiles/*c4_pmc_traffic.json (per sweep launch)",
                 "kernel": "sssp_sweep_kernel (all sweeps of one 64-source batch group)",
                 "avg_group_ms": avg_launch_s * 1e3, "groups_per_step": k_launches // max(args.steps, 1),
                 "algorithmic_bytes_per_group": work_per_launch,
@@ -254,32 +398,33 @@ def bench_graph(args, cfg, D):
         cpu = cpu_opt = None
         if args.cpu_baseline and D.world == 1:
             from oracle import oracle as O
+            threads = args.cpu_threads or cpu_share()[0]
             if og_args is None:
                 og = O.Graph(False, np.arange(n_nodes), *synth.complete_graph(n_nodes, seed))
             else:
                 og = O.Graph(False, np.arange(n_nodes), *og_args)
-            cpu = cpu_baseline(og, nodes, args.cpu_threads, args.cpu_sources, args.config.upper())
-            cpu_opt = cpu_baseline(og, nodes, args.cpu_threads, args.cpu_sources, args.config.upper(),
-                                   target_s=8.0, mode=1)
+            cpu = cpu_baseline(og, nodes, threads, args.cpu_sources, args.config.upper())
+            cpu_opt = cpu_baseline(og, nodes, threads, args.cpu_sources, args.config.upper(), target_s=8.0,
+                                   mode=1)
         out = {
             "metric": f"APSP pairs/sec (routing-table build, {n_nodes // 1000 if n_nodes >= 1000 else n_nodes}"
                       f"{'k' if n_nodes >= 1000 else ''}-node graph)",
-            "value": pairs / (elapsed / args.steps), "unit": "pairs/s", "n_gpus": D.n_gpus, "steps": args.steps,
+            "value": pairs / (elapsed / args.steps), "unit": "pairs/s", "n_gpus": ranks, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "strong",
-            "vs_baseline": None, "dtype": "f64" if "f64key" in desc else ("u64" if desc.startswith("fw") else "u64"),
+            "vs_baseline": None, "dtype": key,
             "data": data,
             "config": {"workload": f"{label}, use_shortest_path=true, {algo}", "nodes": n_nodes, "in_use": n,
-                       "pairs": pairs, "parallelism": f"rows{D.n_gpus}" if D.n_gpus > 1 else "single",
+                       "pairs": pairs, "parallelism": f"rows{ranks}" if ranks > 1 else "single",
                        "plan": desc, "step_ms": [round(x, 3) for x in step_ms], "build_wallclock_ms": ms_per_step,
                        "phases_last_build": {"device_total_ms": timing["total_ms"],
                                              "dominant_ms": timing["dominant_ms"],
                                              "exact_loss_pass_ms": timing["loss_ms"],
-                                             "tight_edges": timing["tight_edges"]}},
+                                             "tight_edges": timing["tight_edges"]},
+                       "e2e": e2e},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "cpu_baseline_opt": cpu_opt,
         }
-    plan.close()
     return out
 
 
@@ -362,12 +507,15 @@ def bench_packets(args, cfg, D):
                 O.packet_batch(table.latency_ns, table.packet_loss, pk.view(O.PKT_DTYPE), rng, r1, 0, 2**62)
                 reps += 1
             dt = time.perf_counter() - t0
+            _, aff, model = cpu_share()
             cpu = {"value": reps * n_pkts / dt, "unit": "packets/s", "cores": 1, "kind": "port",
+                   "cpu_model": model, "cpus_visible": aff,
                    "sample": f"{reps} rounds of the same 1M-packet batch through the oracle's sequential "
-                             f"send_packet restatement (one thread), {dt:.1f} s"}
+                             f"send_packet restatement (one thread: Shadow decides a host's packets on the one "
+                             f"worker thread that runs the host), {dt:.1f} s"}
         out = {
             "metric": "batched send_packet decisions/sec (1M packets/round)", "value": D.world * n_pkts / per_round,
-            "unit": "packets/s", "n_gpus": D.n_gpus, "steps": args.steps, "warmup": args.warmup,
+            "unit": "packets/s", "n_gpus": D.world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": per_round * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "u64", "data": "synthetic (seeded packet round, 10k hosts on the C1 nodes, loss U[0,0.25])",
             "config": {"workload": "C5: 1M packets/round, latency lookup + per-host xoshiro256++ loss drops",
@@ -386,11 +534,34 @@ def bench_packets(args, cfg, D):
     return out
 
 
+def spawn_ranks(args):
+    """--gpus N > 1 without a launcher: start the N ranks under
+    torch.distributed.run as child processes (this process has not touched the
+    GPU) and exit with their status."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
 def main():
     args = parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and world == 1:
+        sys.exit(spawn_ranks(args))
+    if args.gpus != world:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
     cfg = CONFIGS[args.config]
-    D = Dist(args.gpus)
-    out = bench_packets(args, cfg, D) if cfg["kind"] == "packets" else bench_graph(args, cfg, D)
+    D = Dist()
+    if cfg["kind"] == "packets":
+        out = bench_packets(args, cfg, D)
+    elif cfg["kind"] == "gml":
+        out = bench_gml(args, cfg, D)
+    else:
+        out = bench_graph(args, cfg, D)
     if out is not None:
         print(json.dumps(out), flush=True)
     D.close()

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -19,6 +20,7 @@
 #include <new>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "srt_internal.h"
@@ -54,20 +56,19 @@ srt_status hip_fail(srt_err *err, hipError_t e, const char *what) {
 
 uint32_t node_id(const srt_csr *g, uint32_t idx) { return g->node_ids ? g->node_ids[idx] : idx; }
 
-// Edge lookup with petgraph's edges_connecting semantics (mod.rs:256-293):
-// count adjacency entries of row a whose far endpoint is b.
-int count_edges(const srt_csr *g, uint32_t a, uint32_t b, uint64_t *lat, float *loss) {
-    int c = 0;
-    for (uint64_t k = g->row_ptr[a]; k < g->row_ptr[a + 1]; ++k)
-        if (g->col[k] == b) {
-            if (c == 0) {
-                *lat = g->lat_ns[k];
-                *loss = g->loss[k];
-            }
-            ++c;
-        }
-    return c;
-}
+// SRT_TRACE=1: host-side phase timings on stderr (measurement only)
+struct Trace {
+    bool on = std::getenv("SRT_TRACE") != nullptr;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), last = t0;
+    void mark(const char *what) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[srt] %-28s %9.3f ms (total %9.3f)\n", what,
+                     std::chrono::duration<double, std::milli>(now - last).count(),
+                     std::chrono::duration<double, std::milli>(now - t0).count());
+        last = now;
+    }
+};
 
 srt_status edge_error(srt_err *err, int c, uint32_t a_id, uint32_t b_id) {
     char buf[160];
@@ -79,6 +80,114 @@ srt_status edge_error(srt_err *err, int c, uint32_t a_id, uint32_t b_id) {
     std::snprintf(buf, sizeof buf, "More than one edge connecting node %u to %u", a_id, b_id);
     set_err(err, SRT_ERR_MULTI_EDGE, buf, a_id, b_id);
     return SRT_ERR_MULTI_EDGE;
+}
+
+// One pass over the borrowed CSR: the edge-attribute checks of
+// ShadowEdge::try_from that the ABI cannot assume (mod.rs:72-111: latency != 0,
+// loss in [0, 1]), endpoints in range, the self-loops of every node
+// (mod.rs:210-217, 256-293), and the statistics the key proofs need (gcd and
+// max of the latencies, completeness, parallel edges).  Rows are split over
+// host threads (the CPU share of the job: OMP_NUM_THREADS, else up to 32) by
+// equal adjacency counts; it runs while the main thread sets up the device
+// and uploads the CSR.  A row counts as free of parallel edges when its
+// far endpoints are strictly monotone (petgraph lists a node's edges in
+// reverse insertion order, so a GML graph written in node order is); any
+// other row is treated as possibly parallel, which only costs the FW init an
+// atomic min and the key proof its completeness shortcut.
+struct CsrStats {
+    uint64_t gcd = 0, maxlat = 0, selfloops = 0;
+    uint64_t zero_k = ~0ull, badloss_k = ~0ull, badcol_k = ~0ull;
+    bool unique = true, complete = true;
+    std::vector<uint32_t> sl_cnt;    // per node: self-loop entries
+    std::vector<uint64_t> sl_first;  // per node: first self-loop entry
+};
+
+int host_threads(uint64_t work) {
+    if (work < (1ull << 20)) return 1;
+    int t = (int)std::thread::hardware_concurrency();
+    if (const char *e = std::getenv("OMP_NUM_THREADS")) t = std::atoi(e);
+    if (const char *e = std::getenv("SRT_HOST_THREADS")) t = std::atoi(e);
+    return std::max(1, std::min(t, 32));
+}
+
+void csr_scan(const srt_csr *g, CsrStats *out) {
+    const uint32_t V = g->n_nodes;
+    out->sl_cnt.assign(V, 0);
+    out->sl_first.assign(V, ~0ull);
+    const int T = host_threads(g->n_adj);
+    std::vector<CsrStats> part(T);
+    auto work = [&](int t, uint32_t r0, uint32_t r1) {
+        CsrStats &st = part[t];
+        uint64_t gcd = 0, maxlat = 0, selfl = 0;
+        for (uint32_t u = r0; u < r1; ++u) {
+            const uint64_t b = g->row_ptr[u], e = g->row_ptr[u + 1];
+            uint32_t cnt = 0, prev = 0;
+            uint64_t first = ~0ull;
+            bool inc = true, dec = true;
+            for (uint64_t k = b; k < e; ++k) {
+                const uint32_t c = g->col[k];
+                const uint64_t l = g->lat_ns[k];
+                const float q = g->loss[k];
+                if (c >= V && st.badcol_k == ~0ull) st.badcol_k = k;
+                if (l == 0 && st.zero_k == ~0ull) st.zero_k = k;
+                if (!(q >= 0.0f && q <= 1.0f) && st.badloss_k == ~0ull) st.badloss_k = k;
+                maxlat = l > maxlat ? l : maxlat;
+                if (gcd != 1 && l) {
+                    // divisibility by the running gcd: exact in f64 below 2^53
+                    bool divides;
+                    if (gcd && l < (1ull << 53) && gcd < (1ull << 53)) {
+                        const uint64_t qi = (uint64_t)((double)l / (double)gcd);
+                        divides = qi * gcd == l;
+                    } else {
+                        divides = gcd && l % gcd == 0;
+                    }
+                    if (!divides) gcd = std::gcd(gcd, l);
+                }
+                if (c == u) {
+                    if (!cnt) first = k;
+                    ++cnt;
+                }
+                if (k > b) {
+                    inc &= c > prev;
+                    dec &= c < prev;
+                }
+                prev = c;
+            }
+            out->sl_cnt[u] = cnt;
+            out->sl_first[u] = first;
+            selfl += cnt;
+            const bool uniq = inc || dec;
+            st.unique &= uniq;
+            st.complete &= uniq && (e - b - cnt) == (uint64_t)V - 1;
+        }
+        st.gcd = gcd;
+        st.maxlat = maxlat;
+        st.selfloops = selfl;
+    };
+    // row ranges with about n_adj / T entries each
+    std::vector<uint32_t> cut(T + 1, V);
+    cut[0] = 0;
+    for (int t = 1; t < T; ++t) {
+        const uint64_t target = g->n_adj * (uint64_t)t / T;
+        cut[t] = (uint32_t)(std::lower_bound(g->row_ptr, g->row_ptr + V + 1, target) - g->row_ptr);
+        cut[t] = std::max(std::min(cut[t], V), cut[t - 1]);
+    }
+    std::vector<std::thread> pool;
+    for (int t = 1; t < T; ++t) pool.emplace_back(work, t, cut[t], cut[t + 1]);
+    work(0, cut[0], cut[1]);
+    for (auto &th : pool) th.join();
+    out->complete = V > 0;
+    for (const CsrStats &st : part) {
+        out->gcd = std::gcd(out->gcd, st.gcd);
+        out->maxlat = std::max(out->maxlat, st.maxlat);
+        out->selfloops += st.selfloops;
+        out->zero_k = std::min(out->zero_k, st.zero_k);
+        out->badloss_k = std::min(out->badloss_k, st.badloss_k);
+        out->badcol_k = std::min(out->badcol_k, st.badcol_k);
+        out->unique &= st.unique;
+        out->complete &= st.complete;
+    }
+    if (out->gcd == 0) out->gcd = 1;
 }
 
 // Choose the closure's key representation and prove it exact.
@@ -94,34 +203,11 @@ srt_status edge_error(srt_err *err, int c, uint32_t a_id, uint32_t b_id) {
 // u32, the fastest.  Lmax < 2^32 - 1 additionally lets the loss pass keep
 // latencies as u32.  Knob SRT_FW_KEY=f64|u64 (measurement / A-B parity only)
 // skips the narrower representations.
-bool choose_key_params(const srt_csr *g, KeyParams *kp, int *key_type, std::string *why) {
-    uint64_t gcd = 0, maxlat = 0;
-    for (uint64_t k = 0; k < g->n_adj; ++k) {
-        const uint64_t l = g->lat_ns[k];
-        if (gcd != 1 && (gcd == 0 || l % gcd)) gcd = std::gcd(gcd, l);
-        maxlat = std::max(maxlat, l);
-    }
-    if (gcd == 0) gcd = 1;
-    kp->g = gcd;
-    const uint64_t V = g->n_nodes;
-    // complete: every node has an edge to every other node
-    bool complete = V > 0;
-    {
-        std::vector<uint32_t> stamp(V, 0);
-        for (uint64_t u = 0; u < V && complete; ++u) {
-            uint64_t distinct = 0;
-            for (uint64_t k = g->row_ptr[u]; k < g->row_ptr[u + 1]; ++k) {
-                const uint32_t v = g->col[k];
-                if (v != u && stamp[v] != u + 1) {
-                    stamp[v] = (uint32_t)(u + 1);
-                    ++distinct;
-                }
-            }
-            complete = distinct == V - 1;
-        }
-    }
-    const uint64_t maxu = maxlat / gcd;
-    const unsigned __int128 Lmax = complete ? (unsigned __int128)maxu : (unsigned __int128)(V ? V - 1 : 0) * maxu;
+bool choose_key_params(const CsrStats &cs, uint32_t V, KeyParams *kp, int *key_type, std::string *why) {
+    kp->g = cs.gcd;
+    const uint64_t maxu = cs.maxlat / cs.gcd;
+    const unsigned __int128 Lmax =
+        cs.complete ? (unsigned __int128)maxu : (unsigned __int128)(V ? V - 1 : 0) * maxu;
     kp->lmax = Lmax > (unsigned __int128)~0ull ? ~0ull : (uint64_t)Lmax;
     kp->lat32 = Lmax < 0xffffffffull;
     const char *force = std::getenv("SRT_FW_KEY");
@@ -193,18 +279,8 @@ void free_plan_buffers(srt_plan *p) {
 // A stored value is a simple path (<= V-1 edges) and a candidate adds one
 // edge, so V * max_edge_latency / g < 2^32 - 1 keeps every sum exact and
 // below the all-ones "unreached" key.
-bool sssp_params(const srt_csr *g, uint64_t *g_out, uint64_t *n_in, std::string *why) {
-    uint64_t gcd = 0, maxlat = 0, selfloops = 0;
-    for (uint32_t u = 0; u < g->n_nodes; ++u)
-        for (uint64_t k = g->row_ptr[u]; k < g->row_ptr[u + 1]; ++k) {
-            gcd = std::gcd(gcd, g->lat_ns[k]);
-            maxlat = std::max(maxlat, g->lat_ns[k]);
-            selfloops += g->col[k] == u;
-        }
-    if (gcd == 0) gcd = 1;
-    *g_out = gcd;
-    *n_in = g->n_adj - selfloops;
-    if ((unsigned __int128)g->n_nodes * (maxlat / gcd) >= 0xffffffffull) {
+bool sssp_params(const CsrStats &cs, uint32_t V, std::string *why) {
+    if ((unsigned __int128)V * (cs.maxlat / cs.gcd) >= 0xffffffffull) {
         *why = "V * max edge latency exceeds the 32-bit latency field of the SSSP key";
         return false;
     }
@@ -252,6 +328,7 @@ int srt_device_count(void) {
 srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
                            const srt_opts *opts, srt_plan **plan_out, srt_err *err) {
     clear_err(err);
+    Trace tr;
     if (!g || !plan_out || (n && !nodes) || !g->row_ptr || (g->n_adj && (!g->col || !g->lat_ns || !g->loss))) {
         set_err(err, SRT_ERR_INVALID, "null argument");
         return SRT_ERR_INVALID;
@@ -270,21 +347,6 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         set_err(err, SRT_ERR_INVALID, "row_ptr[n_nodes] != n_adj");
         return SRT_ERR_INVALID;
     }
-    // ShadowEdge::try_from rejects a zero latency (mod.rs:104-106); the loss
-    // pass relies on every edge latency being > 0
-    for (uint64_t k = 0; k < g->n_adj; ++k)
-        if (g->lat_ns[k] == 0) {
-            set_err(err, SRT_ERR_INVALID, "Edge 'latency' must not be 0");
-            return SRT_ERR_INVALID;
-        }
-    // self-loop of every in-use node, in node order (mod.rs:210-217)
-    std::vector<uint64_t> sl_lat(n);
-    std::vector<float> sl_loss(n);
-    for (uint32_t i = 0; i < n; ++i) {
-        const int c = count_edges(g, nodes[i], nodes[i], &sl_lat[i], &sl_loss[i]);
-        if (c != 1) return edge_error(err, c, node_id(g, nodes[i]), node_id(g, nodes[i]));
-    }
-
     srt_plan *p = new (std::nothrow) srt_plan();
     if (!p) {
         set_err(err, SRT_ERR_OOM, "out of host memory");
@@ -302,30 +364,115 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     for (uint32_t i = 0; i < n && p->identity_nodes; ++i) p->identity_nodes = nodes[i] == i;
     if (g->node_ids) p->node_ids.assign(g->node_ids, g->node_ids + g->n_nodes);
 
-    // Kernel family.  Dense closure (FW) costs Vp^3 relaxations at ~1.2e13/s;
-    // the batched sparse sweep costs ~n * (E_in + V) row gathers of 8 B with a
-    // few re-activations per row, priced at ~64 B per (source, in-edge) at
-    // ~3e12 B/s.  AUTO takes the cheaper representable one.
-    std::string why_fw, why_sssp;
-    const bool fw_ok = choose_key_params(g, &p->kp, &p->key_type, &why_fw);
-    if (fw_ok) {
-        // no parallel edges (every adjacency row lists each neighbour once):
-        // the FW init can store edge keys instead of atomic-min'ing them
-        std::vector<uint32_t> stamp(g->n_nodes, 0);
-        bool unique = true;
-        for (uint32_t u = 0; u < g->n_nodes && unique; ++u)
-            for (uint64_t k = g->row_ptr[u]; k < g->row_ptr[u + 1]; ++k) {
-                const uint32_t v = g->col[k];
-                if (stamp[v] == u + 1) {
-                    unique = false;
-                    break;
-                }
-                stamp[v] = u + 1;
+    // 1. the CSR scan (validation + statistics) on host threads while this
+    //    thread sets up the device and uploads the CSR
+    CsrStats cs;
+    std::thread scanner([&] { csr_scan(g, &cs); });
+    srt_err derr{};
+    const srt_status dst = [&]() -> srt_status {
+        srt_err *err = &derr;
+        int dev = opts && opts->device >= 0 ? opts->device : -1;
+        if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
+        p->device = dev;
+        hipError_t e = hipSetDevice(dev);
+        if (e != hipSuccess) return hip_fail(err, e, "hipSetDevice");
+        // measurement knob SRT_FW_CHAIN_CUS=c: the main stream (phase-3 rest) is
+        // kept off c CUs so the look-ahead chain on the side stream never waits
+        // for a CU slot (SRT_FW_CHAIN_CU_STRIDE=1: reserved CUs spread evenly
+        // over the mask, else the last c bits)
+        if (const char *ce = std::getenv("SRT_FW_CHAIN_CUS"); ce && std::atoi(ce) > 0) {
+            hipDeviceProp_t prop;
+            int ncu = 256;
+            if (hipGetDeviceProperties(&prop, dev) == hipSuccess) ncu = prop.multiProcessorCount;
+            const int c = std::min(std::atoi(ce), ncu - 1);
+            const bool stride = std::getenv("SRT_FW_CHAIN_CU_STRIDE") != nullptr;
+            std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+            for (int i = 0; i < ncu; ++i) {
+                const bool reserved = stride ? (i % (ncu / c) == 0 && i / (ncu / c) < c) : i >= ncu - c;
+                if (!reserved) mask[i / 32] |= 1u << (i % 32);
             }
-        p->fw_unique_edges = unique;
+            e = hipExtStreamCreateWithCUMask(&p->stream, (uint32_t)mask.size(), mask.data());
+        } else {
+            e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
+        }
+        if (e != hipSuccess) return hip_fail(err, e, "hipStreamCreate");
+        p->own_stream = true;
+        int lo = 0, hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+        e = hipStreamCreateWithPriority(&p->side_stream, hipStreamNonBlocking, hi);
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(&p->comm_stream, hipStreamNonBlocking, hi);
+        if (e != hipSuccess) return hip_fail(err, e, "hipStreamCreateWithPriority");
+        (void)hipEventCreate(&p->ev_begin);
+        (void)hipEventCreate(&p->ev_end);
+        // knob SRT_FW_SYNC_FENCE=dev (measurement): the stream-to-stream events
+        // of the look-ahead schedule skip the system-scope fence (same device)
+        const unsigned sync_fl =
+            hipEventDisableTiming | (std::getenv("SRT_FW_SYNC_FENCE") ? hipEventDisableSystemFence : 0u);
+        (void)hipEventCreateWithFlags(&p->ev_cross, sync_fl);
+        (void)hipEventCreateWithFlags(&p->ev_pivot, sync_fl);
+        (void)hipEventCreateWithFlags(&p->ev_row, sync_fl);
+        (void)hipEventCreateWithFlags(&p->ev_bcast, sync_fl);
+        srt_status st;
+        if ((st = dmalloc(&p->d_row_ptr, (size_t)g->n_nodes + 1, err)) != SRT_OK ||
+            (st = dmalloc(&p->d_col, g->n_adj, err)) != SRT_OK || (st = dmalloc(&p->d_lat, g->n_adj, err)) != SRT_OK ||
+            (st = dmalloc(&p->d_loss, g->n_adj, err)) != SRT_OK || (st = dmalloc(&p->d_nodes, n, err)) != SRT_OK ||
+            (st = dmalloc(&p->d_sl_lat, n, err)) != SRT_OK || (st = dmalloc(&p->d_sl_loss, n, err)) != SRT_OK ||
+            (st = dmalloc(&p->d_stats, 2, err)) != SRT_OK || (st = dmalloc(&p->d_rstats, 2, err)) != SRT_OK)
+            return st;
+        auto up = [&](void *dst, const void *src, size_t bytes) -> hipError_t {
+            if (!bytes) return hipSuccess;
+            return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, p->stream);
+        };
+        if ((e = up(p->d_row_ptr, g->row_ptr, ((size_t)g->n_nodes + 1) * 8)) != hipSuccess ||
+            (e = up(p->d_col, g->col, g->n_adj * 4)) != hipSuccess ||
+            (e = up(p->d_lat, g->lat_ns, g->n_adj * 8)) != hipSuccess ||
+            (e = up(p->d_loss, g->loss, g->n_adj * 4)) != hipSuccess ||
+            (e = up(p->d_nodes, nodes, (size_t)n * 4)) != hipSuccess)
+            return hip_fail(err, e, "upload");
+        return SRT_OK;
+    }();
+    tr.mark("create: device setup+upload");
+    scanner.join();
+    tr.mark("create: CSR scan (joined)");
+
+    // 2. the reference's errors, in its order: edge attributes (parse time),
+    //    then the self-loop of every in-use node in node order (mod.rs:210-217)
+    auto fail = [&](srt_status s, const char *msg) {
+        srt_plan_destroy(p);
+        set_err(err, s, msg);
+        return s;
+    };
+    if (cs.badcol_k != ~0ull) return fail(SRT_ERR_INVALID, "adjacency entry names a node out of range");
+    if (cs.zero_k != ~0ull) return fail(SRT_ERR_INVALID, "Edge 'latency' must not be 0");
+    if (cs.badloss_k != ~0ull) return fail(SRT_ERR_INVALID, "Edge 'packet_loss' is not in the range [0,1]");
+    std::vector<uint64_t> sl_lat(n);
+    std::vector<float> sl_loss(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t u = nodes[i], c = cs.sl_cnt[u];
+        if (c != 1) {
+            srt_plan_destroy(p);
+            return edge_error(err, (int)c, node_id(g, u), node_id(g, u));
+        }
+        sl_lat[i] = g->lat_ns[cs.sl_first[u]];
+        sl_loss[i] = g->loss[cs.sl_first[u]];
     }
-    uint64_t n_in = 0;
-    const bool sssp_ok = sssp_params(g, &p->sssp_g, &n_in, &why_sssp);
+    if (dst != SRT_OK) {
+        srt_plan_destroy(p);
+        if (err) *err = derr;
+        return dst;
+    }
+
+    // 3. kernel family.  Dense closure (FW) costs Vp^3 relaxations at
+    // ~1.2e13/s; the batched sparse sweep costs ~n * (E_in + V) row gathers of
+    // 8 B with a few re-activations per row, priced at ~64 B per (source,
+    // in-edge) at ~3e12 B/s.  AUTO takes the cheaper representable one.
+    std::string why_fw, why_sssp;
+    const bool fw_ok = choose_key_params(cs, p->V, &p->kp, &p->key_type, &why_fw);
+    // no parallel edges: the FW init can store edge keys instead of atomic-min'ing them
+    p->fw_unique_edges = cs.unique;
+    const uint64_t n_in = g->n_adj - cs.selfloops;
+    const bool sssp_ok = sssp_params(cs, p->V, &why_sssp);
+    p->sssp_g = cs.gcd;
     const uint32_t want = opts ? opts->algo : (uint32_t)SRT_ALGO_AUTO;
     int algo = -1;
     if (want == SRT_ALGO_FW) {
@@ -337,15 +484,11 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         const double t_sssp = sssp_ok ? (double)n * ((double)n_in + p->V) * 64.0 / 3e12 : 1e300;
         if (fw_ok || sssp_ok) algo = t_sssp < t_fw ? SRT_ALGO_SSSP : SRT_ALGO_FW;
     } else {
-        delete p;
-        set_err(err, SRT_ERR_INVALID, "unknown srt_opts.algo");
-        return SRT_ERR_INVALID;
+        return fail(SRT_ERR_INVALID, "unknown srt_opts.algo");
     }
     if (algo < 0) {
-        delete p;
         const std::string why = want == SRT_ALGO_SSSP ? why_sssp : want == SRT_ALGO_FW ? why_fw : why_fw + "; " + why_sssp;
-        set_err(err, SRT_ERR_UNSUPPORTED, ("no exact path key for this graph: " + why).c_str());
-        return SRT_ERR_UNSUPPORTED;
+        return fail(SRT_ERR_UNSUPPORTED, ("no exact path key for this graph: " + why).c_str());
     }
     p->algo = algo;
     p->row0 = 0;
@@ -358,9 +501,8 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         if (const char *e = std::getenv("SRT_FW_EMULATE_RANKS")) p->emulate_ranks = (uint32_t)std::atoi(e);
         std::snprintf(d, sizeof d, "fw:%s B=%d g=%llu lmax=%llu V=%u n=%u stage=%s loss=tight-dag%s",
                       p->key_type == srt::KEY_U32 ? "u32key" : p->key_type == srt::KEY_F64 ? "f64key" : "u64key",
-                      srt::FW_B, (unsigned long long)p->kp.g,
-                      (unsigned long long)p->kp.lmax, p->V, n, p->fw_glds ? "glds" : "reg",
-                      p->kp.lat32 ? "/u32" : "/u64");
+                      srt::FW_B, (unsigned long long)p->kp.g, (unsigned long long)p->kp.lmax, p->V, n,
+                      p->fw_glds ? "glds" : "reg", p->kp.lat32 ? "/u32" : "/u64");
     } else {
         // R words of 64 sources per lane (one wave walks a vertex's in-edges
         // once for 64*R sources), and as many groups in flight as ~256 MB of
@@ -391,64 +533,11 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
                       p->sssp_nb / p->sssp_r);
     }
     p->desc = d;
+    tr.mark("create: key/algo choice");
 
-    int dev = opts && opts->device >= 0 ? opts->device : -1;
-    if (dev < 0) {
-        if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-    }
-    p->device = dev;
+    // 4. the family's buffers; self-loop values
     srt_status st;
-    hipError_t e = hipSetDevice(dev);
-    if (e != hipSuccess) {
-        delete p;
-        return hip_fail(err, e, "hipSetDevice");
-    }
-    // measurement knob SRT_FW_CHAIN_CUS=c: the main stream (phase-3 rest) is
-    // kept off c CUs so the look-ahead chain on the side stream never waits
-    // for a CU slot (SRT_FW_CHAIN_CU_STRIDE=1: reserved CUs spread evenly
-    // over the mask, else the last c bits)
-    if (const char *ce = std::getenv("SRT_FW_CHAIN_CUS"); ce && std::atoi(ce) > 0) {
-        hipDeviceProp_t prop;
-        int ncu = 256;
-        if (hipGetDeviceProperties(&prop, dev) == hipSuccess) ncu = prop.multiProcessorCount;
-        const int c = std::min(std::atoi(ce), ncu - 1);
-        const bool stride = std::getenv("SRT_FW_CHAIN_CU_STRIDE") != nullptr;
-        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-        for (int i = 0; i < ncu; ++i) {
-            const bool reserved = stride ? (i % (ncu / c) == 0 && i / (ncu / c) < c) : i >= ncu - c;
-            if (!reserved) mask[i / 32] |= 1u << (i % 32);
-        }
-        e = hipExtStreamCreateWithCUMask(&p->stream, (uint32_t)mask.size(), mask.data());
-    } else {
-        e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
-    }
-    if (e != hipSuccess) {
-        delete p;
-        return hip_fail(err, e, "hipStreamCreate");
-    }
-    p->own_stream = true;
-    {
-        int lo = 0, hi = 0;
-        hipDeviceGetStreamPriorityRange(&lo, &hi);
-        e = hipStreamCreateWithPriority(&p->side_stream, hipStreamNonBlocking, hi);
-        if (e == hipSuccess) e = hipStreamCreateWithPriority(&p->comm_stream, hipStreamNonBlocking, hi);
-        if (e != hipSuccess) {
-            if (p->side_stream) hipStreamDestroy(p->side_stream);
-            hipStreamDestroy(p->stream);
-            delete p;
-            return hip_fail(err, e, "hipStreamCreateWithPriority");
-        }
-    }
-    hipEventCreate(&p->ev_begin);
-    hipEventCreate(&p->ev_end);
-    // knob SRT_FW_SYNC_FENCE=dev (measurement): the stream-to-stream events
-    // of the look-ahead schedule skip the system-scope fence (same device)
-    const unsigned sync_fl = hipEventDisableTiming | (std::getenv("SRT_FW_SYNC_FENCE") ? hipEventDisableSystemFence : 0u);
-    hipEventCreateWithFlags(&p->ev_cross, sync_fl);
-    hipEventCreateWithFlags(&p->ev_pivot, sync_fl);
-    hipEventCreateWithFlags(&p->ev_row, sync_fl);
-    hipEventCreateWithFlags(&p->ev_bcast, sync_fl);
-
+    hipError_t e;
 #define PLAN_TRY(x)                \
     do {                           \
         st = (x);                  \
@@ -457,20 +546,11 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
             return st;             \
         }                          \
     } while (0)
-    PLAN_TRY(dmalloc(&p->d_row_ptr, (size_t)g->n_nodes + 1, err));
-    PLAN_TRY(dmalloc(&p->d_col, g->n_adj, err));
-    PLAN_TRY(dmalloc(&p->d_lat, g->n_adj, err));
-    PLAN_TRY(dmalloc(&p->d_loss, g->n_adj, err));
-    PLAN_TRY(dmalloc(&p->d_nodes, n, err));
     if (algo == SRT_ALGO_FW)
         PLAN_TRY(dmalloc(reinterpret_cast<uint8_t **>(&p->d_D), (size_t)p->Vp * p->Vp * srt::key_bytes(p->key_type),
                          err));
     PLAN_TRY(dmalloc(&p->d_out_lat, (size_t)n * n, err));
     PLAN_TRY(dmalloc(&p->d_out_loss, (size_t)n * n, err));
-    PLAN_TRY(dmalloc(&p->d_sl_lat, n, err));
-    PLAN_TRY(dmalloc(&p->d_sl_loss, n, err));
-    PLAN_TRY(dmalloc(&p->d_stats, 2, err));
-    PLAN_TRY(dmalloc(&p->d_rstats, 2, err));
     if (algo == SRT_ALGO_SSSP) {
         std::vector<uint64_t> in_ptr;
         std::vector<srt::InEdge> in_edge;
@@ -480,8 +560,8 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         PLAN_TRY(dmalloc(&p->d_sD, (size_t)p->sssp_nb * p->V * 64, err));
         PLAN_TRY(dmalloc(&p->d_smask, (size_t)2 * p->sssp_nb * p->V, err));
         PLAN_TRY(dmalloc(&p->d_sflag, (size_t)3 * p->sssp_nb, err));
-        if (const char *e = std::getenv("SRT_SSSP_ACT")) {
-            const int k = std::atoi(e);
+        if (const char *ev = std::getenv("SRT_SSSP_ACT")) {
+            const int k = std::atoi(ev);
             p->sssp_act_on = k != 0;
             p->sssp_act_from = k > 1 ? (uint32_t)k : 0u;
         }
@@ -498,21 +578,15 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         }
     }
 #undef PLAN_TRY
-    auto up = [&](void *dst, const void *src, size_t bytes) -> hipError_t {
-        if (!bytes) return hipSuccess;
-        return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, p->stream);
-    };
-    if ((e = up(p->d_row_ptr, g->row_ptr, ((size_t)g->n_nodes + 1) * 8)) != hipSuccess ||
-        (e = up(p->d_col, g->col, g->n_adj * 4)) != hipSuccess ||
-        (e = up(p->d_lat, g->lat_ns, g->n_adj * 8)) != hipSuccess ||
-        (e = up(p->d_loss, g->loss, g->n_adj * 4)) != hipSuccess ||
-        (e = up(p->d_nodes, nodes, (size_t)n * 4)) != hipSuccess ||
-        (e = up(p->d_sl_lat, sl_lat.data(), (size_t)n * 8)) != hipSuccess ||
-        (e = up(p->d_sl_loss, sl_loss.data(), (size_t)n * 4)) != hipSuccess ||
+    if ((n && (e = hipMemcpyAsync(p->d_sl_lat, sl_lat.data(), (size_t)n * 8, hipMemcpyHostToDevice, p->stream)) !=
+                  hipSuccess) ||
+        (n && (e = hipMemcpyAsync(p->d_sl_loss, sl_loss.data(), (size_t)n * 4, hipMemcpyHostToDevice, p->stream)) !=
+                  hipSuccess) ||
         (e = hipStreamSynchronize(p->stream)) != hipSuccess) {
         srt_plan_destroy(p);
         return hip_fail(err, e, "upload");
     }
+    tr.mark("create: upload");
     *plan_out = p;
     return SRT_OK;
 }
@@ -584,6 +658,7 @@ srt_status srt_plan_run(srt_plan *p, srt_err *err) {
 
 srt_status srt_plan_fetch(srt_plan *p, srt_path *out, uint64_t *min_latency_ns, srt_err *err) {
     clear_err(err);
+    Trace tr;
     if (!p || !p->ran) {
         set_err(err, SRT_ERR_INVALID, "plan has not been run");
         return SRT_ERR_INVALID;
@@ -621,6 +696,7 @@ srt_status srt_plan_fetch(srt_plan *p, srt_path *out, uint64_t *min_latency_ns, 
             HIP_TRY(hipStreamSynchronize(p->stream), "sync");
         }
     }
+    tr.mark("fetch: pack+download");
     return SRT_OK;
 }
 
@@ -746,11 +822,16 @@ srt_status srt_compute_shortest_paths(const srt_csr *g, const uint32_t *nodes, u
                                       srt_path *out, uint64_t *min_latency_ns,
                                       const srt_opts *opts, srt_err *err) {
     srt_plan *p = nullptr;
+    Trace tr;
     srt_status s = srt_plan_create(g, nodes, n, opts, &p, err);
+    tr.mark("e2e: create");
     if (s != SRT_OK) return s;
     s = srt_plan_run(p, err);
+    tr.mark("e2e: run");
     if (s == SRT_OK) s = srt_plan_fetch(p, out, min_latency_ns, err);
+    tr.mark("e2e: fetch");
     srt_plan_destroy(p);
+    tr.mark("e2e: destroy");
     return s;
 }
 
