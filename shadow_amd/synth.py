@@ -25,11 +25,12 @@ def complete_graph(n: int, seed: int, lat_ms=(1, 300), loss_max=0.01, self_loops
     return iu.astype(np.uint32), ju.astype(np.uint32), lat, loss
 
 
-def complete_csr(n: int, seed: int, lat_ms=(1, 300), loss_max=0.01):
+def complete_csr(n: int, seed: int, lat_ms=(1, 300), loss_max=0.01, edges=None):
     """CSR (petgraph adjacency of the undirected complete graph) built directly,
     without the O(n^2) edge-list sort: row u lists all v (self-loop once).
-    Values are identical to complete_graph(n, seed) traversed both ways."""
-    src, dst, lat, loss = complete_graph(n, seed, lat_ms, loss_max)
+    Values are identical to complete_graph(n, seed) traversed both ways
+    (pass that edge list as `edges` to skip regenerating it)."""
+    src, dst, lat, loss = complete_graph(n, seed, lat_ms, loss_max) if edges is None else edges
     L = np.zeros((n, n), np.uint64)
     P = np.zeros((n, n), np.float32)
     L[src, dst] = lat
