@@ -15,6 +15,9 @@
  *                                  src/main/core/worker.rs:326-410 (+ :539-553)
  *   srt_gml_parse               <- NetworkGraph::parse / gml_parser::parse
  *                                  src/main/network/graph/mod.rs:134-181
+ *   srt_routing_info_*          <- generate_routing_info + RoutingInfo
+ *                                  src/main/core/sim_config.rs:424-461,
+ *                                  src/main/network/graph/mod.rs:428-477
  *
  * Conventions (mirroring the reference's FFI: plain C types, no exceptions
  * across the boundary, caller-owned outputs):
@@ -234,6 +237,45 @@ srt_status srt_packet_events(srt_plan *plan, const uint32_t *d_host_pkt_ptr, uin
                              const uint32_t *d_flags, const uint64_t *d_deliver, const uint32_t *d_dst_host,
                              uint32_t n_dst_hosts, uint64_t *d_event_base, uint64_t *d_event_id,
                              uint32_t *d_order, uint32_t *d_dst_ptr, srt_err *err);
+
+/* ------------------------------------------------------------- RoutingInfo */
+/* Dense RoutingInfo keyed by GML node ids: replaces the
+ * HashMap<(u32,u32), PathProperties> and the RwLock<HashMap> packet counters of
+ * RoutingInfo (mod.rs:428-477), and the NodeIndex -> GML id re-keying of every
+ * pair in generate_routing_info (sim_config.rs:436-458): the table stays
+ * row-major over the in-use nodes and a GML id -> row map resolves ids.
+ * Thread-safe for concurrent path() / increment_packet_count() calls (worker
+ * threads); build and destroy from one thread. */
+typedef struct srt_routing_info srt_routing_info;
+
+/* generate_routing_info (sim_config.rs:424-461) in one call: the in-use nodes
+ * are NodeIndex values (node_id_to_index of the GML ids); use_shortest_paths
+ * selects srt_compute_shortest_paths (mod.rs:183-228) or srt_get_direct_paths
+ * (mod.rs:230-252); g->node_ids gives the GML ids (NULL: NodeIndex).  Errors
+ * as those functions'. */
+srt_status srt_routing_info_build(const srt_csr *g, const uint32_t *nodes, uint32_t n, int use_shortest_paths,
+                                  const srt_opts *opts, srt_routing_info **out, srt_err *err);
+/* The same over a plan that has run (srt_plan_run): fetches its table. */
+srt_status srt_routing_info_from_plan(srt_plan *plan, srt_routing_info **out, srt_err *err);
+/* RoutingInfo::path (mod.rs:444-446): SRT_OK and *out, or SRT_ERR_INVALID when
+ * either GML id is not an in-use node (the reference's None). */
+srt_status srt_routing_info_path(const srt_routing_info *ri, uint32_t src_id, uint32_t dst_id, srt_path *out);
+/* RoutingInfo::increment_packet_count (mod.rs:449-456): saturating +1 (an id
+ * that is not in use is ignored: the reference would panic on the missing
+ * path when logging) */
+void srt_routing_info_increment_packet_count(srt_routing_info *ri, uint32_t src_id, uint32_t dst_id);
+/* adds a device round's per-pair counters (srt_packet_batch's n*n array,
+ * copied to the host) into the counters, saturating */
+void srt_routing_info_add_packet_counts(srt_routing_info *ri, const uint64_t *counts);
+uint64_t srt_routing_info_packet_count(const srt_routing_info *ri, uint32_t src_id, uint32_t dst_id);
+/* RoutingInfo::get_smallest_latency_ns (mod.rs:474-476): 0 = None (empty), 1 = *out set */
+int srt_routing_info_smallest_latency_ns(const srt_routing_info *ri, uint64_t *out);
+/* table row of a GML id (the srt_pkt src_row / dst_row of its host), -1 if not in use */
+int64_t srt_routing_info_row(const srt_routing_info *ri, uint32_t gml_id);
+uint32_t srt_routing_info_size(const srt_routing_info *ri);
+/* the dense table, row-major size x size, rows in in-use order (read-only) */
+const srt_path *srt_routing_info_table(const srt_routing_info *ri);
+void srt_routing_info_destroy(srt_routing_info *ri);
 
 /* --------------------------------------------------------------- GML ingest */
 /* Parses Shadow GML text (gml-parser grammar + NetworkGraph validation) into a

@@ -105,6 +105,18 @@ SIGNATURES = {
                                    _vp, _errp]),
     "srt_packet_events": (C.c_int, [_vp, _vp, C.c_uint32, C.c_uint64, _vp, _vp, _vp, C.c_uint32, _vp, _vp, _vp,
                                     _vp, _errp]),
+    "srt_routing_info_build": (C.c_int, [C.POINTER(SrtCsr), _u32p, C.c_uint32, C.c_int, C.POINTER(SrtOpts),
+                                         C.POINTER(_vp), _errp]),
+    "srt_routing_info_from_plan": (C.c_int, [_vp, C.POINTER(_vp), _errp]),
+    "srt_routing_info_path": (C.c_int, [_vp, C.c_uint32, C.c_uint32, C.POINTER(SrtPath)]),
+    "srt_routing_info_increment_packet_count": (None, [_vp, C.c_uint32, C.c_uint32]),
+    "srt_routing_info_add_packet_counts": (None, [_vp, _u64p]),
+    "srt_routing_info_packet_count": (C.c_uint64, [_vp, C.c_uint32, C.c_uint32]),
+    "srt_routing_info_smallest_latency_ns": (C.c_int, [_vp, _u64p]),
+    "srt_routing_info_row": (C.c_int64, [_vp, C.c_uint32]),
+    "srt_routing_info_size": (C.c_uint32, [_vp]),
+    "srt_routing_info_table": (C.POINTER(SrtPath), [_vp]),
+    "srt_routing_info_destroy": (None, [_vp]),
     "srt_gml_parse": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(_vp), _errp]),
     "srt_gml_csr": (C.c_int, [_vp, C.POINTER(SrtCsr)]),
     "srt_gml_free": (None, [_vp]),

@@ -244,31 +244,83 @@ class IpAssignment:
 
 
 class RoutingInfo:
-    """mod.rs:428-477 over a dense table keyed by GML ids: path() is an index
-    lookup; packet counters are a dense array (no global RwLock)."""
+    """RoutingInfo (mod.rs:428-477) over libsrt's dense srt_routing_info: the
+    GPU-built table stays row-major over the in-use nodes, a GML id -> row map
+    answers path(), and the packet counters are a dense array of atomics with
+    the reference's saturating add (no RwLock<HashMap>)."""
 
-    def __init__(self, table: PathTable, gml_ids: np.ndarray):
-        self.table = table
-        self._row = {int(gml_ids[int(v)]): i for i, v in enumerate(table.nodes)}
-        n = len(table.nodes)
-        self.packet_counters = np.zeros((n, n), np.uint64)
+    def __init__(self, handle):
+        self._h = handle
+
+    @classmethod
+    def build(cls, graph: "NetworkGraph", nodes, use_shortest_paths: bool = True, algo: int = _lib.SRT_ALGO_AUTO,
+              device: int = -1) -> "RoutingInfo":
+        L = _lib.lib()
+        _lib.require_device()
+        nodes = np.ascontiguousarray(np.asarray(list(nodes) if not isinstance(nodes, np.ndarray) else nodes),
+                                     np.uint32)
+        h = C.c_void_p()
+        err = _lib.SrtErr()
+        opts = _lib.SrtOpts(algo, device, 0, 0)
+        csr = graph.csr()
+        _lib.check(L.srt_routing_info_build(C.byref(csr), nodes.ctypes.data_as(C.POINTER(C.c_uint32)), len(nodes),
+                                            int(bool(use_shortest_paths)), C.byref(opts), C.byref(h), C.byref(err)),
+                   err)
+        return cls(h)
+
+    @classmethod
+    def from_plan(cls, plan) -> "RoutingInfo":
+        h = C.c_void_p()
+        err = _lib.SrtErr()
+        _lib.check(_lib.lib().srt_routing_info_from_plan(plan.handle, C.byref(h), C.byref(err)), err)
+        return cls(h)
+
+    def __len__(self) -> int:
+        return int(_lib.lib().srt_routing_info_size(self._h))
 
     def path(self, start: int, end: int) -> Optional[PathProperties]:
-        i, j = self._row.get(int(start)), self._row.get(int(end))
-        if i is None or j is None:
+        p = _lib.SrtPath()
+        if _lib.lib().srt_routing_info_path(self._h, int(start), int(end), C.byref(p)) != _lib.SRT_OK:
             return None
-        return PathProperties(int(self.table.latency_ns[i, j]), float(self.table.packet_loss[i, j]))
+        return PathProperties(int(p.latency_ns), float(np.float32(p.packet_loss)))
 
     def row_of(self, gml_id: int) -> Optional[int]:
-        return self._row.get(int(gml_id))
+        r = _lib.lib().srt_routing_info_row(self._h, int(gml_id))
+        return None if r < 0 else int(r)
 
     def increment_packet_count(self, start: int, end: int) -> None:
-        i, j = self._row[int(start)], self._row[int(end)]
-        if self.packet_counters[i, j] != np.uint64(2**64 - 1):
-            self.packet_counters[i, j] += np.uint64(1)
+        _lib.lib().srt_routing_info_increment_packet_count(self._h, int(start), int(end))
+
+    def add_packet_counts(self, counts: np.ndarray) -> None:
+        counts = np.ascontiguousarray(counts, np.uint64)
+        assert counts.size == len(self) ** 2
+        _lib.lib().srt_routing_info_add_packet_counts(self._h, counts.ctypes.data_as(C.POINTER(C.c_uint64)))
+
+    def packet_count(self, start: int, end: int) -> int:
+        return int(_lib.lib().srt_routing_info_packet_count(self._h, int(start), int(end)))
 
     def get_smallest_latency_ns(self) -> Optional[int]:
-        return int(self.table.min_latency_ns) if len(self.table.nodes) else None
+        v = C.c_uint64()
+        return int(v.value) if _lib.lib().srt_routing_info_smallest_latency_ns(self._h, C.byref(v)) else None
+
+    def table(self):
+        """(latency_ns u64[n,n], packet_loss f32[n,n]) copies of the dense table."""
+        n = len(self)
+        ptr = _lib.lib().srt_routing_info_table(self._h)
+        raw = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint8)), shape=(max(n * n, 1) * 16,))
+        rec = raw.view(np.dtype([("lat", "<u8"), ("loss", "<f4"), ("pad", "<u4")]))[:n * n]
+        return rec["lat"].reshape(n, n).copy(), rec["loss"].reshape(n, n).copy()
+
+    def close(self):
+        if self._h:
+            _lib.lib().srt_routing_info_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 # configuration.rs ONE_GBIT_SWITCH_GRAPH: one node, its self-loop at 1 ms
@@ -338,7 +390,8 @@ def load_network_graph(options) -> str:
 
 
 def generate_routing_info(graph: NetworkGraph, node_ids: set, use_shortest_paths: bool = True) -> RoutingInfo:
-    """sim_config.rs:424-461: GML ids of in-use nodes -> NodeIndex list -> table."""
+    """sim_config.rs:424-461: GML ids of the in-use nodes -> NodeIndex list ->
+    srt_routing_info_build (the table keyed by GML ids without re-keying every
+    pair)."""
     nodes = np.array([graph.node_id_to_index(x) for x in node_ids], np.uint32)
-    table = graph.compute_shortest_paths(nodes) if use_shortest_paths else graph.get_direct_paths(nodes)
-    return RoutingInfo(table, graph.node_ids)
+    return RoutingInfo.build(graph, nodes, use_shortest_paths)

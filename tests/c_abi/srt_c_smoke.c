@@ -3,7 +3,7 @@
  * (src/main/network/graph/mod.rs:559-647) as petgraph adjacency CSR, runs
  * srt_compute_shortest_paths with both kernel families and srt_get_direct_paths
  * on a complete graph, and checks the reference's golden latencies and error
- * texts.  Exit 0 = pass.  Built by tests/c_abi/Makefile (gcc, links
+ * texts, then builds the dense RoutingInfo (srt_routing_info_*) by GML id.  Exit 0 = pass.  Built by tests/c_abi/Makefile (gcc, links
  * shadow_amd/libsrt.so); run by tests/test_gpu_c_abi.py on the GPU box. */
 #include <stdio.h>
 #include <string.h>
@@ -98,6 +98,43 @@ int main(void) {
         srt_status st = srt_compute_shortest_paths(&g, nodes, 2, out, NULL, NULL, &err);
         CHECK(st == SRT_ERR_NO_EDGE && strcmp(err.msg, "No edge connecting node 20 to 20") == 0, "error text: %d %s",
               (int)st, err.msg);
+    }
+    /* generate_routing_info + RoutingInfo (sim_config.rs:424-461, mod.rs:428-477)
+     * on the directed 3-node graph with GML ids 10/20/30, in-use nodes in
+     * HashSet-like order: path() by GML id, None for an unknown id, the
+     * smallest latency, saturating counters */
+    {
+        srt_csr g;
+        uint64_t row_ptr[4], lat[16];
+        uint32_t col[16];
+        float loss[16];
+        three_node(1, &g, row_ptr, col, lat, loss);
+        const uint32_t ids[3] = {10, 20, 30};
+        g.node_ids = ids;
+        const uint32_t nodes[3] = {2, 0, 1};
+        srt_routing_info *ri = NULL;
+        srt_err err;
+        srt_status st = srt_routing_info_build(&g, nodes, 3, 1, NULL, &ri, &err);
+        CHECK(st == SRT_OK && ri, "routing info: %d %s", (int)st, err.msg);
+        if (ri) {
+            for (uint32_t a = 0; a < 3; ++a)
+                for (uint32_t b = 0; b < 3; ++b) {
+                    srt_path p;
+                    st = srt_routing_info_path(ri, ids[a], ids[b], &p);
+                    CHECK(st == SRT_OK && p.latency_ns == gold_dir[a * 3 + b], "path(%u,%u) = %llu", ids[a],
+                          ids[b], (unsigned long long)p.latency_ns);
+                }
+            srt_path p;
+            CHECK(srt_routing_info_path(ri, 10, 99, &p) == SRT_ERR_INVALID, "unknown id must be None");
+            uint64_t mn = 0;
+            CHECK(srt_routing_info_smallest_latency_ns(ri, &mn) == 1 && mn == 3, "smallest latency %llu",
+                  (unsigned long long)mn);
+            CHECK(srt_routing_info_row(ri, 30) == 0 && srt_routing_info_row(ri, 10) == 1, "rows");
+            srt_routing_info_increment_packet_count(ri, 20, 30);
+            srt_routing_info_increment_packet_count(ri, 20, 30);
+            CHECK(srt_routing_info_packet_count(ri, 20, 30) == 2, "packet count");
+            srt_routing_info_destroy(ri);
+        }
     }
     if (fails) {
         fprintf(stderr, "%d check(s) failed\n", fails);
