@@ -499,10 +499,11 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         // tuning knob (measurement only): SRT_FW_STAGE=reg selects register staging
         if (const char *e = std::getenv("SRT_FW_STAGE")) p->fw_glds = std::strcmp(e, "reg") != 0;
         if (const char *e = std::getenv("SRT_FW_EMULATE_RANKS")) p->emulate_ranks = (uint32_t)std::atoi(e);
-        std::snprintf(d, sizeof d, "fw:%s B=%d g=%llu lmax=%llu V=%u n=%u stage=%s loss=tight-dag%s",
+        if (const char *e = std::getenv("SRT_FW_BAND")) p->fw_band = e[0] != '0';
+        std::snprintf(d, sizeof d, "fw:%s B=%d g=%llu lmax=%llu V=%u n=%u stage=%s band=%d loss=tight-dag%s",
                       p->key_type == srt::KEY_U32 ? "u32key" : p->key_type == srt::KEY_F64 ? "f64key" : "u64key",
                       srt::FW_B, (unsigned long long)p->kp.g, (unsigned long long)p->kp.lmax, p->V, n,
-                      p->fw_glds ? "glds" : "reg", p->kp.lat32 ? "/u32" : "/u64");
+                      p->fw_glds ? "glds" : "reg", (int)p->fw_band, p->kp.lat32 ? "/u32" : "/u64");
     } else {
         // R words of 64 sources per lane (one wave walks a vertex's in-edges
         // once for 64*R sources), and as many groups in flight as ~256 MB of
@@ -668,10 +669,11 @@ srt_status srt_plan_fetch(srt_plan *p, srt_path *out, uint64_t *min_latency_ns, 
     HIP_TRY(hipMemcpyAsync(stats, p->d_stats, sizeof stats, hipMemcpyDeviceToHost, p->stream), "stats");
     HIP_TRY(hipStreamSynchronize(p->stream), "sync");
     if (stats[1] != 0) {
+        // the reference panics in assert_eq!(paths.len(), nodes.len().pow(2))
+        // (mod.rs:219); this is Rust 1.76's assert_eq! panic message
         char buf[200];
         const unsigned long long nn = (unsigned long long)p->n * p->n;
-        std::snprintf(buf, sizeof buf,
-                      "assertion `left == right` failed: %llu != %llu (graph not connected)",
+        std::snprintf(buf, sizeof buf, "assertion `left == right` failed\n  left: %llu\n right: %llu",
                       nn - stats[1], nn);
         set_err(err, SRT_ERR_DISCONNECTED, buf);
         return SRT_ERR_DISCONNECTED;

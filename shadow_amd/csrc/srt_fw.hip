@@ -1121,9 +1121,8 @@ void launch_group(srt_plan *p, hipStream_t s, uint32_t a, uint32_t g, const Rect
     const uint32_t n = r1.r.n * r1.c.n + r2.r.n * r2.c.n;
     if (!n) return;
     K *D = reinterpret_cast<K *>(p->d_D);
-    // bit 16: banded tile order (knob SRT_FW_BAND=0 turns it off for A/B timing)
-    static const bool band = !(std::getenv("SRT_FW_BAND") && std::getenv("SRT_FW_BAND")[0] == '0');
-    const uint32_t arg = g | (band ? 0x10000u : 0u);
+    // bit 16: banded tile order (plan knob SRT_FW_BAND=0 turns it off for A/B timing)
+    const uint32_t arg = g | (p->fw_band ? 0x10000u : 0u);
     if constexpr (sizeof(K) == 4) {
         if (chain)
             hipLaunchKernelGGL((minplus_u32_kernel<5>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);

@@ -104,6 +104,9 @@ def test_disconnected_raises():
     with pytest.raises(_lib.SrtError) as e:
         g.compute_shortest_paths([0, 1, 2])
     assert e.value.code == _lib.SRT_ERR_DISCONNECTED
+    # Rust's assert_eq! panic text for paths.len() == nodes.len().pow(2) (mod.rs:219):
+    # sources 0 / 1 / 2 reach {0, 1} / {1} / {2}
+    assert str(e.value) == "assertion `left == right` failed\n  left: 4\n right: 9"
 
 
 def test_missing_selfloop_error_text():

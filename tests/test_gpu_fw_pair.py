@@ -1,9 +1,12 @@
 """Grouped-round Floyd-Warshall schedule (srt_fw.hip fw_rounds_group_t) on gfx950.
 
-One GPU at rest-bound sizes (>= 64 blocks of 128) fuses FW rounds in groups
-of g = 4 (2 when the block count does not allow 4); SRT_FW_PAIR forces the
-grouped schedule at small sizes, SRT_FW_GROUP picks g and SRT_FW_NO_PAIR turns
-it off, so the same graph is closed every way.  Bar: latency bit-exact vs the
+One GPU at rest-bound sizes fuses FW rounds in groups: g = 4 when the block
+count is a multiple of 4 and >= 96 (12k nodes), else 2 (srt_fw.hip
+fw_rounds_t); an odd block count, or fewer than 2 g blocks, keeps the
+single-round schedule.  SRT_FW_PAIR forces the grouped schedule at small
+sizes, SRT_FW_GROUP picks g, SRT_FW_NO_PAIR turns it off and SRT_FW_BAND=0
+turns off the banded tile order of grouped launches, so the same graph is
+closed every way.  Bar: latency bit-exact vs the
 oracle (reference Dijkstra restatement), loss bit-exact (the exact-loss pass
 after the closure), and the grouped table bit-identical to the single-round
 one (both compute the unique minimum latencies).
@@ -18,14 +21,16 @@ from tests.test_gpu_apsp import _check
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("band", ["1", "0"])
 @pytest.mark.parametrize("group", ["2", "4"])
 @pytest.mark.parametrize("n,seed,directed", [(400, 0, False), (500, 1, True), (777, 2, False),
                                              (1000, 3, True), (1500, 5, False), (300, 4, False)])
-def test_forced_groups_vs_oracle(monkeypatch, group, n, seed, directed):
+def test_forced_groups_vs_oracle(monkeypatch, band, group, n, seed, directed):
     # 400/500 -> 4 blocks, 777/1000 -> 8, 1500 -> 12 (g=4: 3 groups); 300 -> 3
     # blocks (odd: single-round fallback); g=4 needs >= 8 blocks
     monkeypatch.setenv("SRT_FW_PAIR", "1")
     monkeypatch.setenv("SRT_FW_GROUP", group)
+    monkeypatch.setenv("SRT_FW_BAND", band)
     e = synth.random_graph(n, 40 + seed, p_edge=8.0 / n, directed=directed, lat_range_ns=(1, 6), loss_max=0.05)
     nodes = np.random.default_rng(seed).permutation(n).astype(np.uint32)
     _check(e, nodes, directed, n, algo=_lib.SRT_ALGO_FW)
