@@ -500,6 +500,7 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         if (const char *e = std::getenv("SRT_FW_STAGE")) p->fw_glds = std::strcmp(e, "reg") != 0;
         if (const char *e = std::getenv("SRT_FW_EMULATE_RANKS")) p->emulate_ranks = (uint32_t)std::atoi(e);
         if (const char *e = std::getenv("SRT_FW_BAND")) p->fw_band = e[0] != '0';
+        if (const char *e = std::getenv("SRT_FW_OCC")) p->fw_occ3 = std::atoi(e) == 3;
         std::snprintf(d, sizeof d, "fw:%s B=%d g=%llu lmax=%llu V=%u n=%u stage=%s band=%d loss=tight-dag%s",
                       p->key_type == srt::KEY_U32 ? "u32key" : p->key_type == srt::KEY_F64 ? "f64key" : "u64key",
                       srt::FW_B, (unsigned long long)p->kp.g, (unsigned long long)p->kp.lmax, p->V, n,

@@ -628,26 +628,27 @@ __device__ __forceinline__ void lds_step32(StepOps32 &o, uint32_t abase, uint32_
     asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(o.b[3]) : "v"(bbase), "i"((2 * s + 1) * B * 4 + 256));
 }
 
-// acc[c] = min3(acc[c], a0 + b0[c], a1 + b1[c]), c < 4: 8 adds, then 4 min3
-// (one volatile block so it stays in order with the explicit waits)
+// acc[c] = min3(acc[c], a0 + b0[c], a1 + b1[c]), c < 4: two rounds of 4 adds
+// + 2 min3 through 4 temporaries (one volatile block so it stays in order
+// with the explicit waits; 4 temporaries instead of 8 keep the kernel under
+// 168 VGPRs, the 3-workgroups-per-CU budget)
 __device__ __forceinline__ void relax_quad32(uint32_t &c0, uint32_t &c1, uint32_t &c2, uint32_t &c3, uint32_t a0,
                                              uint32_t a1, u32x4 b0, u32x4 b1) {
-    uint32_t t0, t1, t2, t3, t4, t5, t6, t7;
+    uint32_t t0, t1, t2, t3;
     asm volatile(
-        "v_add_u32 %0, %12, %14\n\t"
-        "v_add_u32 %1, %13, %18\n\t"
-        "v_add_u32 %2, %12, %15\n\t"
-        "v_add_u32 %3, %13, %19\n\t"
-        "v_add_u32 %4, %12, %16\n\t"
-        "v_add_u32 %5, %13, %20\n\t"
-        "v_add_u32 %6, %12, %17\n\t"
-        "v_add_u32 %7, %13, %21\n\t"
-        "v_min3_u32 %8, %8, %0, %1\n\t"
-        "v_min3_u32 %9, %9, %2, %3\n\t"
-        "v_min3_u32 %10, %10, %4, %5\n\t"
-        "v_min3_u32 %11, %11, %6, %7"
-        : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "=&v"(t4), "=&v"(t5), "=&v"(t6), "=&v"(t7), "+v"(c0),
-          "+v"(c1), "+v"(c2), "+v"(c3)
+        "v_add_u32 %0, %8, %10\n\t"
+        "v_add_u32 %1, %9, %14\n\t"
+        "v_add_u32 %2, %8, %11\n\t"
+        "v_add_u32 %3, %9, %15\n\t"
+        "v_min3_u32 %4, %4, %0, %1\n\t"
+        "v_min3_u32 %5, %5, %2, %3\n\t"
+        "v_add_u32 %0, %8, %12\n\t"
+        "v_add_u32 %1, %9, %16\n\t"
+        "v_add_u32 %2, %8, %13\n\t"
+        "v_add_u32 %3, %9, %17\n\t"
+        "v_min3_u32 %6, %6, %0, %1\n\t"
+        "v_min3_u32 %7, %7, %2, %3"
+        : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3)
         : "v"(a0), "v"(a1), "v"(b0.x), "v"(b0.y), "v"(b0.z), "v"(b0.w), "v"(b1.x), "v"(b1.y), "v"(b1.z),
           "v"(b1.w));
 }
@@ -694,9 +695,9 @@ __device__ __forceinline__ void tile_of(uint32_t t, const Rect &r1, const Rect &
     }
 }
 
-template <int TAG>
-__global__ __launch_bounds__(NT3, 2) void minplus_u32_kernel(uint32_t *__restrict__ D, uint32_t Vp, uint32_t kb,
-                                                             Rect r1, Rect r2, uint32_t ng) {
+template <int TAG, int OCC>
+__global__ __launch_bounds__(NT3, OCC) void minplus_u32_kernel(uint32_t *__restrict__ D, uint32_t Vp, uint32_t kb,
+                                                               Rect r1, Rect r2, uint32_t ng) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[2 * GBUF32];
     if constexpr (TAG != 0) __builtin_amdgcn_s_setprio(2);  // look-ahead chain: issue priority
     uint32_t bi, bj;
@@ -920,9 +921,14 @@ void launch_tiles(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1, const
         hipLaunchKernelGGL((minplus_small_kernel<K, TAG>), dim3(4 * n), dim3(256), 0, s,
                            reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2);
     else if (p->fw_glds) {
-        if constexpr (sizeof(K) == 4)
-            hipLaunchKernelGGL((minplus_u32_kernel<TAG>), dim3(n), dim3(NT3), 0, s,
-                               reinterpret_cast<uint32_t *>(p->d_D), p->Vp, kb, r1, r2, 1u);
+        if constexpr (sizeof(K) == 4) {
+            if (p->fw_occ3)
+                hipLaunchKernelGGL((minplus_u32_kernel<TAG, 3>), dim3(n), dim3(NT3), 0, s,
+                                   reinterpret_cast<uint32_t *>(p->d_D), p->Vp, kb, r1, r2, 1u);
+            else
+                hipLaunchKernelGGL((minplus_u32_kernel<TAG, 2>), dim3(n), dim3(NT3), 0, s,
+                                   reinterpret_cast<uint32_t *>(p->d_D), p->Vp, kb, r1, r2, 1u);
+        }
         else
             hipLaunchKernelGGL((minplus_glds_kernel<K, TAG>), dim3(n), dim3(NT3), 0, s,
                                reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2, 1u);
@@ -1124,10 +1130,14 @@ void launch_group(srt_plan *p, hipStream_t s, uint32_t a, uint32_t g, const Rect
     // bit 16: banded tile order (plan knob SRT_FW_BAND=0 turns it off for A/B timing)
     const uint32_t arg = g | (p->fw_band ? 0x10000u : 0u);
     if constexpr (sizeof(K) == 4) {
-        if (chain)
-            hipLaunchKernelGGL((minplus_u32_kernel<5>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
+        if (chain && p->fw_occ3)
+            hipLaunchKernelGGL((minplus_u32_kernel<5, 3>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
+        else if (chain)
+            hipLaunchKernelGGL((minplus_u32_kernel<5, 2>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
+        else if (p->fw_occ3)
+            hipLaunchKernelGGL((minplus_u32_kernel<0, 3>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
         else
-            hipLaunchKernelGGL((minplus_u32_kernel<0>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
+            hipLaunchKernelGGL((minplus_u32_kernel<0, 2>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
     } else {
         if (chain)
             hipLaunchKernelGGL((minplus_glds_kernel<K, 5>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);

@@ -77,6 +77,7 @@ struct srt_plan {
     bool fw_glds = true;   // FW tiles staged by LDS-DMA (false: register staging)
     bool fw_small_chain = false;  // quarter-tile kernels for the look-ahead chain (sharded)
     bool fw_unique_edges = false; // no parallel edges: FW init stores instead of atomic min
+    bool fw_occ3 = false;         // u32 tile kernel at 3 workgroups per CU (knob SRT_FW_OCC=3)
     bool fw_band = true;          // grouped launches: banded tile order (knob SRT_FW_BAND=0, read at create)
     uint32_t emulate_ranks = 0;   // measurement only, see fw_rounds_t
     std::string desc;
