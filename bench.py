@@ -340,9 +340,14 @@ def bench_graph(args, cfg, D):
         raise SystemExit(f"plan bound to {ranks} ranks but WORLD_SIZE={D.world}")
     elapsed, step_ms, k_ms, k_launches, k_work, k_tiles = timed_builds(plan, D, args.steps, args.warmup)
     if args.emulate_ranks > 1:
+        t = plan.timing()
         print(json.dumps({"emulated_ranks": args.emulate_ranks, "config": args.config, "ms_per_step":
                           elapsed * 1e3 / args.steps, "rest_ms_per_step": k_ms / args.steps,
-                          "rest_launches_per_step": k_launches // args.steps}), flush=True)
+                          "rest_launches_per_step": k_launches // args.steps,
+                          "tail_ms_last": t["loss_ms"], "build_ms_last": t["total_ms"],
+                          "note": "rank 0 of an N-rank run on one GPU: closure schedule on the closed D, loss pass "
+                                  "on its own rows; collectives modelled as waits (25 us + bytes / 300 GB/s)"}),
+              flush=True)
         plan.close()
         return None
     timing = plan.timing()  # phase breakdown of the last timed build

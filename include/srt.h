@@ -151,6 +151,10 @@ typedef struct {
     double dominant_work;       /* relaxations (FW) / algorithmic bytes (SSSP) of those launches */
     double loss_ms;             /* dense: exact-loss pass (tight-edge CSR + fold), 0 for SSSP */
     uint64_t tight_edges;       /* dense: edges of the tight-edge CSR */
+    uint32_t sharded_tail;      /* dense, comm bound: 1 = the loss pass ran on this rank's own
+                                   closure rows (no key all-gather; tight-edge lists and
+                                   u32 + f32 table rows exchanged), 0 = replicated */
+    uint32_t reserved;
 } srt_timing;
 srt_status srt_plan_timing(const srt_plan *plan, srt_timing *out);
 /* C tiles (128 x 128 keys) the last FW run's dominant launches loaded and

@@ -41,6 +41,8 @@ void clear_err(srt_err *err) {
     if (err) std::memset(err, 0, sizeof *err);
 }
 
+srt_status build_loss_rows(srt_plan *p, int W, uint32_t rows_per, srt_err *err);
+
 srt_status hip_fail(srt_err *err, hipError_t e, const char *what) {
     char buf[256];
     std::snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
@@ -271,6 +273,13 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_tsort_tmp);
     hipFree(p->d_tmaxw);
     hipFree(p->d_lscratch);
+    hipFree(p->d_lrows);
+    hipFree(p->d_slat);
+    hipFree(p->d_sloss);
+    hipFree(p->d_tlist);
+    hipFree(p->d_tinfo);
+    hipFree(p->d_tcursor);
+    if (p->h_tinfo) hipHostFree(p->h_tinfo);
     if (p->h_sflag) hipHostFree(p->h_sflag);
     if (p->h_tcount) hipHostFree(p->h_tcount);
 }
@@ -499,8 +508,16 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         // tuning knob (measurement only): SRT_FW_STAGE=reg selects register staging
         if (const char *e = std::getenv("SRT_FW_STAGE")) p->fw_glds = std::strcmp(e, "reg") != 0;
         if (const char *e = std::getenv("SRT_FW_EMULATE_RANKS")) p->emulate_ranks = (uint32_t)std::atoi(e);
+        if (p->emulate_ranks > 1) {
+            // emulated rank 0 owns the first max(1, blocks / N) block-rows (fw_rounds_t)
+            const uint32_t nblk = p->Vp / srt::FW_B;
+            const uint32_t rows_per = std::max<uint32_t>(1, nblk / p->emulate_ranks) * srt::FW_B;
+            if (srt_status st = build_loss_rows(p, (int)p->emulate_ranks, rows_per, err); st != SRT_OK) {
+                srt_plan_destroy(p);
+                return st;
+            }
+        }
         if (const char *e = std::getenv("SRT_FW_BAND")) p->fw_band = e[0] != '0';
-        if (const char *e = std::getenv("SRT_FW_OCC")) p->fw_occ3 = std::atoi(e) == 3;
         std::snprintf(d, sizeof d, "fw:%s B=%d g=%llu lmax=%llu V=%u n=%u stage=%s band=%d loss=tight-dag%s",
                       p->key_type == srt::KEY_U32 ? "u32key" : p->key_type == srt::KEY_F64 ? "f64key" : "u64key",
                       srt::FW_B, (unsigned long long)p->kp.g, (unsigned long long)p->kp.lmax, p->V, n,
@@ -611,14 +628,29 @@ srt_status srt_plan_run_async(srt_plan *p, srt_err *err) {
         st = srt::sssp_run(p, rstats, err);
         if (st != SRT_OK) return st;
     } else {
-        srt::fw_init(p);
+        // N-rank emulation (measurement only): the first run closes D for
+        // real; later runs replay rank 0's schedule on the closed D (every
+        // round leaves a closed D unchanged, and the kernels' cost does not
+        // depend on the keys), so rank 0's loss-pass share sees valid keys
+        if (!p->emu_closed) srt::fw_init(p);
         st = srt::fw_rounds(p, err);
         if (st != SRT_OK) return st;
-        // exact loss over the tight DAG (every rank holds the whole closure)
+        // exact loss over the tight DAG (sharded: over this rank's own
+        // closure rows, see fw_loss)
         st = srt::fw_loss(p, rstats, err);
         if (st != SRT_OK) return st;
+        if (!p->comm && p->emulate_ranks > 1) p->emu_closed = true;
     }
-    if (p->comm) {
+    if (!p->comm && p->shard_tail) {
+        srt::expand_shard_rows(p, (int)p->emulate_ranks);  // emulation: the others' slots are stale
+    } else if (p->comm && p->shard_tail) {
+        // the staged rows (u32 latency units + f32 loss per pair) were
+        // all-gathered chunk by chunk behind the fold (fw_loss); every rank
+        // expands all ranks' rows into its table
+        if ((st = srt::comm_allgather_inplace(p->comm, p->d_rstats, 16, p->stream, err)) != SRT_OK) return st;
+        srt::expand_shard_rows(p, nranks);
+        srt::reduce_rank_stats(p, nranks);
+    } else if (p->comm) {
         const size_t per = (size_t)p->rows_alloc / nranks * p->n;
         if ((st = srt::comm_allgather_inplace(p->comm, p->d_out_lat, per * 8, p->stream, err)) != SRT_OK ||
             (st = srt::comm_allgather_inplace(p->comm, p->d_out_loss, per * 4, p->stream, err)) != SRT_OK ||
@@ -733,6 +765,8 @@ srt_status srt_plan_timing(const srt_plan *p, srt_timing *o) {
     o->dominant_work = p->p3_work;
     o->loss_ms = p->loss_ms;
     o->tight_edges = p->algo == SRT_ALGO_FW ? p->t_edges : 0;
+    o->sharded_tail = p->algo == SRT_ALGO_FW && p->shard_tail ? 1u : 0u;
+    o->reserved = 0;
     return SRT_OK;
 }
 
@@ -750,6 +784,7 @@ void srt_plan_destroy(srt_plan *p) {
     if (p->comm_stream) hipStreamSynchronize(p->comm_stream);
     free_plan_buffers(p);
     for (hipEvent_t e : p->ev) hipEventDestroy(e);
+    for (hipEvent_t e : p->ev_tail) hipEventDestroy(e);
     for (hipEvent_t e : {p->ev_begin, p->ev_end, p->ev_cross, p->ev_pivot, p->ev_row, p->ev_bcast, p->ev_loss0,
                          p->ev_loss1})
         if (e) hipEventDestroy(e);
@@ -758,6 +793,59 @@ void srt_plan_destroy(srt_plan *p) {
     if (p->own_stream && p->stream) hipStreamDestroy(p->stream);
     delete p;
 }
+
+// loss-pass rows of every rank of a sharded dense build: the table rows whose
+// source lies in the rank's closure block-rows (rows_per graph rows each; all
+// ranks compute the same lists).  Row staging and the exchange buffers are
+// sized by them and reallocated at the next run.
+namespace {
+srt_status build_loss_rows(srt_plan *p, int W, uint32_t rows_per, srt_err *err) {
+    std::vector<std::vector<uint32_t>> lists(W);
+    for (uint32_t i = 0; i < p->n; ++i) lists[std::min<uint32_t>(p->nodes[i] / rows_per, W - 1)].push_back(i);
+    p->lrow_cnt.assign(W, 0);
+    uint32_t most = 1;
+    for (int r = 0; r < W; ++r) {
+        p->lrow_cnt[r] = (uint32_t)lists[r].size();
+        most = std::max(most, p->lrow_cnt[r]);
+    }
+    // chunks of >= 64 rows, 4 by default (knob SRT_TAIL_CHUNKS, 1..16)
+    uint32_t q = 4;
+    if (const char *e = std::getenv("SRT_TAIL_CHUNKS")) q = (uint32_t)std::max(1, std::min(16, std::atoi(e)));
+    q = std::max<uint32_t>(1, std::min<uint32_t>(q, most / 64));
+    p->tail_q = q;
+    p->tail_cr = (most + q - 1) / q;
+    p->lrow_max = q * p->tail_cr;
+    std::vector<uint32_t> flat((size_t)W * p->lrow_max, ~0u);
+    for (int r = 0; r < W; ++r)
+        for (uint32_t k = 0; k < p->lrow_cnt[r]; ++k) {
+            const uint32_t c = k / p->tail_cr;
+            flat[((size_t)c * W + r) * p->tail_cr + k % p->tail_cr] = lists[r][k];
+        }
+    while (p->ev_tail.size() < 2 * (size_t)q) {
+        hipEvent_t ev;
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) break;
+        p->ev_tail.push_back(ev);
+    }
+    void *a = nullptr;
+    hipError_t e = hipMalloc(&a, flat.size() * 4);
+    if (e == hipSuccess) e = hipMemcpy(a, flat.data(), flat.size() * 4, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        hipFree(a);
+        return hip_fail(err, e, "loss-pass row lists");
+    }
+    hipFree(p->d_lrows);
+    p->d_lrows = (uint32_t *)a;
+    hipFree(p->d_slat);
+    hipFree(p->d_sloss);
+    p->d_slat = nullptr;
+    p->d_sloss = nullptr;
+    if (p->h_tinfo) hipHostFree(p->h_tinfo);
+    p->h_tinfo = nullptr;
+    hipFree(p->d_tinfo);
+    p->d_tinfo = nullptr;
+    return SRT_OK;
+}
+}  // namespace
 
 srt_status srt_plan_bind_comm(srt_plan *p, srt_comm *comm, srt_err *err) {
     clear_err(err);
@@ -815,6 +903,7 @@ srt_status srt_plan_bind_comm(srt_plan *p, srt_comm *comm, srt_err *err) {
     const uint32_t nblk = p->Vp / srt::FW_B, per = nblk / (uint32_t)comm->nranks;
     p->rb0 = per * (uint32_t)comm->rank;
     p->rb1 = p->rb0 + per;
+    if (srt_status st = build_loss_rows(p, comm->nranks, per * srt::FW_B, err); st != SRT_OK) return st;
     char d[64];
     std::snprintf(d, sizeof d, " closure-rows=[%u,%u)", p->rb0 * srt::FW_B, p->rb1 * srt::FW_B);
     p->desc += d;

@@ -695,8 +695,8 @@ __device__ __forceinline__ void tile_of(uint32_t t, const Rect &r1, const Rect &
     }
 }
 
-template <int TAG, int OCC>
-__global__ __launch_bounds__(NT3, OCC) void minplus_u32_kernel(uint32_t *__restrict__ D, uint32_t Vp, uint32_t kb,
+template <int TAG>
+__global__ __launch_bounds__(NT3, 2) void minplus_u32_kernel(uint32_t *__restrict__ D, uint32_t Vp, uint32_t kb,
                                                                Rect r1, Rect r2, uint32_t ng) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[2 * GBUF32];
     if constexpr (TAG != 0) __builtin_amdgcn_s_setprio(2);  // look-ahead chain: issue priority
@@ -921,14 +921,9 @@ void launch_tiles(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1, const
         hipLaunchKernelGGL((minplus_small_kernel<K, TAG>), dim3(4 * n), dim3(256), 0, s,
                            reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2);
     else if (p->fw_glds) {
-        if constexpr (sizeof(K) == 4) {
-            if (p->fw_occ3)
-                hipLaunchKernelGGL((minplus_u32_kernel<TAG, 3>), dim3(n), dim3(NT3), 0, s,
-                                   reinterpret_cast<uint32_t *>(p->d_D), p->Vp, kb, r1, r2, 1u);
-            else
-                hipLaunchKernelGGL((minplus_u32_kernel<TAG, 2>), dim3(n), dim3(NT3), 0, s,
-                                   reinterpret_cast<uint32_t *>(p->d_D), p->Vp, kb, r1, r2, 1u);
-        }
+        if constexpr (sizeof(K) == 4)
+            hipLaunchKernelGGL((minplus_u32_kernel<TAG>), dim3(n), dim3(NT3), 0, s,
+                               reinterpret_cast<uint32_t *>(p->d_D), p->Vp, kb, r1, r2, 1u);
         else
             hipLaunchKernelGGL((minplus_glds_kernel<K, TAG>), dim3(n), dim3(NT3), 0, s,
                                reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2, 1u);
@@ -962,7 +957,8 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
     // (SRT_FW_EMULATE_RANKS): local rows = 1/N of the block-rows, and this
     // rank plays the owner of every pivot (p1 + p2row each round: the longest
     // per-round chain any rank has), no collectives -- the table is not valid
-    const uint32_t emu = (!p->comm && p->emulate_ranks > 1) ? p->emulate_ranks : 0;
+    // (after the first run, which closes D for real: see srt_plan_run_async)
+    const uint32_t emu = (!p->comm && p->emulate_ranks > 1 && p->emu_closed) ? p->emulate_ranks : 0;
     const uint32_t rb0 = p->rb0, rb1 = emu ? std::max<uint32_t>(1, nblk / emu) : p->rb1;
     const bool sharded = p->comm != nullptr;  // a 1-rank comm runs the same schedule (tested)
     // quarter-tile chain kernels whenever a round's rest() is short (sharded
@@ -1096,12 +1092,12 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
             hipEventRecord(p->ev_pivot, S);
         }
     }
-    // collectives on one communicator stay ordered: the all-gather follows
-    // the last broadcast
+    // collectives on one communicator stay ordered: the loss pass's
+    // exchanges (srt_loss.hip) follow the last broadcast.  The closure rows
+    // stay sharded: the loss pass of a rank only reads its own rows, and
+    // fw_gather_keys is its fallback.
     hipEventRecord(p->ev_bcast, C);
     hipStreamWaitEvent(M, p->ev_bcast, 0);
-    if (sharded)
-        return comm_allgather_inplace(p->comm, D, (size_t)per_rank * B * p->Vp * sizeof(K), M, err);
     return SRT_OK;
 }
 
@@ -1130,14 +1126,10 @@ void launch_group(srt_plan *p, hipStream_t s, uint32_t a, uint32_t g, const Rect
     // bit 16: banded tile order (plan knob SRT_FW_BAND=0 turns it off for A/B timing)
     const uint32_t arg = g | (p->fw_band ? 0x10000u : 0u);
     if constexpr (sizeof(K) == 4) {
-        if (chain && p->fw_occ3)
-            hipLaunchKernelGGL((minplus_u32_kernel<5, 3>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
-        else if (chain)
-            hipLaunchKernelGGL((minplus_u32_kernel<5, 2>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
-        else if (p->fw_occ3)
-            hipLaunchKernelGGL((minplus_u32_kernel<0, 3>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
+        if (chain)
+            hipLaunchKernelGGL((minplus_u32_kernel<5>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
         else
-            hipLaunchKernelGGL((minplus_u32_kernel<0, 2>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
+            hipLaunchKernelGGL((minplus_u32_kernel<0>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
     } else {
         if (chain)
             hipLaunchKernelGGL((minplus_glds_kernel<K, 5>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
@@ -1215,6 +1207,12 @@ void fw_init(srt_plan *p) {
     if (p->key_type == KEY_U32) fw_init_t<uint32_t>(p);
     else if (p->key_type == KEY_F64) fw_init_t<double>(p);
     else fw_init_t<uint64_t>(p);
+}
+
+srt_status fw_gather_keys(srt_plan *p, srt_err *err) {
+    const uint32_t per_rank = (p->Vp / FW_B) / p->comm->nranks;
+    return comm_allgather_inplace(p->comm, p->d_D, (size_t)per_rank * FW_B * p->Vp * key_bytes(p->key_type),
+                                  p->stream, err);
 }
 
 srt_status fw_rounds(srt_plan *p, srt_err *err) {

@@ -77,9 +77,10 @@ struct srt_plan {
     bool fw_glds = true;   // FW tiles staged by LDS-DMA (false: register staging)
     bool fw_small_chain = false;  // quarter-tile kernels for the look-ahead chain (sharded)
     bool fw_unique_edges = false; // no parallel edges: FW init stores instead of atomic min
-    bool fw_occ3 = false;         // u32 tile kernel at 3 workgroups per CU (knob SRT_FW_OCC=3)
     bool fw_band = true;          // grouped launches: banded tile order (knob SRT_FW_BAND=0, read at create)
     uint32_t emulate_ranks = 0;   // measurement only, see fw_rounds_t
+    bool emu_closed = false;      // emulation: D holds the closure (first run done)
+    uint64_t emu_tight = 0, emu_maxw = 0;  // emulation: tight edges / max latency of the closure
     std::string desc;
     bool identity_nodes = false;
 
@@ -163,6 +164,28 @@ struct srt_plan {
     size_t lscratch_cap = 0;
     hipEvent_t ev_loss0 = nullptr, ev_loss1 = nullptr;  // around the loss pass
     double loss_ms = 0.0;            // exact-loss pass of the last run (tight CSR + fold)
+
+    // sharded dense tail (comm bound, srt_loss.hip fw_loss_sharded): the loss
+    // pass of rank r covers the in-use sources inside its own closure
+    // block-rows (their D rows are final locally, so no key all-gather); the
+    // tight edges of its own adjacency rows are all-gathered as a list; its
+    // table rows travel as u32 latency units + f32 loss and are expanded into
+    // the table on every rank
+    bool shard_tail = false;               // this run used the sharded tail
+    std::vector<uint32_t> lrow_cnt;        // per rank: loss-pass rows
+    uint32_t lrow_max = 0;                 // staging rows per rank (tail_q chunks of tail_cr rows)
+    uint32_t tail_q = 1, tail_cr = 0;      // the fold runs in tail_q chunks; chunk c's all-gather
+                                           // overlaps the fold of chunk c + 1
+    std::vector<hipEvent_t> ev_tail;       // per chunk: fold done (M -> C), then all-gather done
+    uint32_t *d_lrows = nullptr;           // slot (c * nranks + r) * tail_cr + k: rank r's row
+                                           // c * tail_cr + k (~0: padding)
+    uint32_t *d_slat = nullptr;            // nranks * lrow_max * n: latency units (~0: unreachable)
+    float *d_sloss = nullptr;              // nranks * lrow_max * n
+    uint4 *d_tlist = nullptr;              // nranks * tlist_cap tight edges {v, u, w, 1-e bits} (v = ~0: pad)
+    uint64_t tlist_cap = 0;
+    unsigned long long *d_tinfo = nullptr; // 2 per rank: local tight-edge count, max tight latency
+    unsigned long long *d_tcursor = nullptr;  // list fill cursor
+    unsigned long long *h_tinfo = nullptr; // pinned copy of d_tinfo
 };
 
 namespace srt {
@@ -173,11 +196,16 @@ srt_status comm_allgather_inplace(srt_comm *c, void *buf, size_t bytes_per_rank,
 // kernels (srt_fw.hip)
 void fw_init(srt_plan *p);
 srt_status fw_rounds(srt_plan *p, srt_err *err);
+// sharded closure: every rank's block-rows of D to every rank (the loss
+// pass's fallback when the sharded tail does not apply)
+srt_status fw_gather_keys(srt_plan *p, srt_err *err);
 // exact-loss pass (srt_loss.hip): tight-edge CSR from the closure, then the
 // f32 left fold over the tight DAG for table rows [row0, row1); writes the
 // table rows, the raw self-loop diagonal and (min latency, unreachable) into
 // d_stats
 srt_status fw_loss(srt_plan *p, unsigned long long *d_stats, srt_err *err);
+// sharded tail: every rank's staged rows (d_slat / d_sloss, all-gathered) into the table
+void expand_shard_rows(srt_plan *p, int nranks);
 // table entries [first, first + count) -> d_pack[0, count) as srt_path
 void pack_paths(srt_plan *p, uint64_t first, uint64_t count);
 // kernels (srt_sssp.hip)

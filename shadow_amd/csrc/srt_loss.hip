@@ -94,15 +94,16 @@ __device__ __forceinline__ uint64_t closure_lat(const void *D, uint64_t idx, int
 // self-loop) when lat[k] == D[u][v] * g, count it for v, track the largest
 // tight latency.
 template <typename K>
-__global__ void tight_flag_kernel(const K *__restrict__ D, uint32_t Vp, uint32_t V,
+__global__ void tight_flag_kernel(const K *__restrict__ D, uint32_t Vp, uint32_t u0, uint32_t u1,
                                   const uint64_t *__restrict__ row_ptr, const uint32_t *__restrict__ col,
                                   const uint64_t *__restrict__ lat, uint64_t g, uint8_t *__restrict__ flag,
-                                  uint32_t *__restrict__ cnt, unsigned long long *maxw) {
+                                  uint32_t *__restrict__ cnt, unsigned long long *maxw,
+                                  unsigned long long *total) {
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    uint64_t mw = 0;
-    for (uint32_t u = wave; u < V; u += nwaves) {
+    uint64_t mw = 0, tot = 0;
+    for (uint32_t u = u0 + wave; u < u1; u += nwaves) {
         const K *Du = D + (uint64_t)u * Vp;
         const uint64_t b = row_ptr[u], e = row_ptr[u + 1];
         for (uint64_t k = b + lane; k < e; k += 64) {
@@ -113,8 +114,9 @@ __global__ void tight_flag_kernel(const K *__restrict__ D, uint32_t Vp, uint32_t
                 const uint64_t w = KeyLat<K>::lat(d);
                 if (!KeyLat<K>::inf(d) && w * g == lat[k]) {
                     f = 1;
-                    atomicAdd(&cnt[v], 1u);
+                    if (cnt) atomicAdd(&cnt[v], 1u);
                     mw = w > mw ? w : mw;
+                    ++tot;
                 }
             }
             flag[k] = f;
@@ -123,8 +125,85 @@ __global__ void tight_flag_kernel(const K *__restrict__ D, uint32_t Vp, uint32_t
     for (int off = 32; off > 0; off >>= 1) {
         const uint64_t o = __shfl_xor(mw, off);
         mw = o > mw ? o : mw;
+        tot += __shfl_xor(tot, off);
     }
     if (lane == 0 && mw) atomicMax(maxw, (unsigned long long)mw);
+    if (lane == 0 && total && tot) atomicAdd(total, (unsigned long long)tot);
+}
+
+// Sharded tail: the flagged entries of the rank's own adjacency rows [u0, u1)
+// as records {v, u, w, 1f32 - e bits} at list[cursor..): a wave counts its
+// row's flags, takes the row's range with one atomic (one per chunk would
+// serialise ~10^6 atomics on the cursor), then writes them in order.
+__global__ void tight_list_kernel(uint32_t u0, uint32_t u1, const uint64_t *__restrict__ row_ptr,
+                                  const uint32_t *__restrict__ col, const uint64_t *__restrict__ lat,
+                                  const float *__restrict__ loss, uint64_t g, const uint8_t *__restrict__ flag,
+                                  uint4 *__restrict__ list, unsigned long long *cursor) {
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t u = u0 + wave; u < u1; u += nwaves) {
+        const uint64_t b = row_ptr[u], e = row_ptr[u + 1];
+        uint32_t cnt = 0;
+        for (uint64_t k = b + lane; k < e; k += 64) cnt += flag[k];
+        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+        if (!cnt) continue;
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(cursor, (unsigned long long)cnt);
+        base = __shfl(base, 0);
+        for (uint64_t k0 = b; k0 < e; k0 += 64) {
+            const uint64_t k = k0 + lane;
+            const bool f = k < e && flag[k];
+            const uint64_t m = __ballot(f);
+            if (f) {
+                const uint64_t pos = base + __popcll(m & ((1ull << lane) - 1ull));
+                const float eb = 1.0f - loss[k];  // the reference's (1f32 - other.packet_loss), mod.rs:328
+                list[pos] = make_uint4(col[k], u, (uint32_t)(lat[k] / g), __float_as_uint(eb));
+            }
+            base += __popcll(m);
+        }
+    }
+}
+
+// Sharded tail: per-target counts of the all-gathered list (v = ~0: padding)
+__global__ void tight_list_count_kernel(const uint4 *__restrict__ list, uint64_t slots, uint32_t *__restrict__ cnt) {
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < slots; e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t v = list[e].x;
+        if (v != ~0u) atomicAdd(&cnt[v], 1u);
+    }
+}
+
+// ... and the packed pull CSR entries of the list
+__global__ void tight_list_fill_kernel(const uint4 *__restrict__ list, uint64_t slots,
+                                       const uint64_t *__restrict__ ptr, uint32_t *__restrict__ cur,
+                                       uint64_t *__restrict__ tpk, uint32_t ubits) {
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < slots; e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 r = list[e];
+        if (r.x == ~0u) continue;
+        const uint64_t pos = ptr[r.x] + atomicAdd(&cur[r.x], 1u);
+        tpk[pos] = ((uint64_t)r.w << 32) | ((r.z << ubits) | r.y);
+    }
+}
+
+// Sharded tail: every rank's staged rows into the table.  slot s = r * lrow_max
+// + k holds table row lrows[s] (~0: padding) as latency units (~0:
+// unreachable) and loss.
+__global__ void expand_rows_kernel(const uint32_t *__restrict__ lrows, uint32_t slots, uint32_t n,
+                                   const uint32_t *__restrict__ slat, const float *__restrict__ sloss, uint64_t g,
+                                   uint64_t *__restrict__ out_lat, float *__restrict__ out_loss) {
+    for (uint32_t sl = blockIdx.x; sl < slots; sl += gridDim.x) {
+        const uint32_t i = lrows[sl];
+        if (i == ~0u) continue;
+        const uint32_t *sl_ = slat + (uint64_t)sl * n;
+        const float *sp = sloss + (uint64_t)sl * n;
+        uint64_t *ol = out_lat + (uint64_t)i * n;
+        float *op = out_loss + (uint64_t)i * n;
+        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
+            const uint32_t l = sl_[j];
+            ol[j] = l == ~0u ? ~0ull : (uint64_t)l * g;
+            op[j] = sp[j];
+        }
+    }
 }
 
 // Single workgroup: ptr = exclusive scan of cnt (ptr[V] = total), cnt reset
@@ -280,6 +359,7 @@ __global__ __launch_bounds__(LOSS_NT) void tight_loss_kernel(
     uint64_t *__restrict__ out_lat, float *__restrict__ out_loss, unsigned long long *stats,
     uint4 *__restrict__ ord_all, LatT *lat_all, float *loss_all, const uint64_t *__restrict__ row_ptr,
     const uint32_t *__restrict__ col, const uint64_t *__restrict__ elat, const float *__restrict__ eloss,
+    const uint32_t *__restrict__ row_list, uint32_t *__restrict__ out32, float *__restrict__ out32_loss,
     uint32_t diag) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ uint64_t red[16];
@@ -305,7 +385,12 @@ __global__ __launch_bounds__(LOSS_NT) void tight_loss_kernel(
     uint64_t mn = ~0ull;
     unsigned long long unreach = 0;
 
-    for (uint32_t i = row0 + blockIdx.x; i < row1; i += gridDim.x) {
+    // rows: [row0, row1) of the table, or (sharded tail) row_list[0, row1) --
+    // then the row goes to slot k of the u32 staging (latency units, ~0 =
+    // unreachable) instead of the table
+    const uint32_t nrows = row_list ? row1 : row1 - row0;
+    for (uint32_t k = blockIdx.x; k < nrows; k += gridDim.x) {
+        const uint32_t i = row_list ? row_list[k] : row0 + k;
         const uint32_t s = nodes[i];
         // 1. the row's latencies (units of g) and its largest finite one
         uint64_t mx = 0;
@@ -436,9 +521,11 @@ __global__ __launch_bounds__(LOSS_NT) void tight_loss_kernel(
                 if (shift == 0 || !any) break;  // width-1 buckets: one pass is exact
             }
         }
-        // 4. table row i
+        // 4. table row i (or staging slot k)
         uint64_t *ol = out_lat + (uint64_t)i * n;
         float *op = out_loss + (uint64_t)i * n;
+        uint32_t *o32 = out32 ? out32 + (uint64_t)k * n : nullptr;
+        float *o32p = out32 ? out32_loss + (uint64_t)k * n : nullptr;
         for (uint32_t j = tid; j < ((diag & 2u) ? 0u : n); j += nt) {
             uint64_t latv;
             float lossv;
@@ -457,8 +544,13 @@ __global__ __launch_bounds__(LOSS_NT) void tight_loss_kernel(
                     lossv = prow[v];
                 }
             }
-            ol[j] = latv;
-            op[j] = lossv;
+            if (o32) {
+                o32[j] = latv == ~0ull ? ~0u : (uint32_t)(latv / g);
+                o32p[j] = lossv;
+            } else {
+                ol[j] = latv;
+                op[j] = lossv;
+            }
             mn = latv < mn ? latv : mn;
         }
         __syncthreads();  // the next row rewrites the LDS rows
@@ -531,9 +623,17 @@ int bits_of(uint64_t x) {
     return b;
 }
 
+// rows: [row0, row1) of the table, or the sharded tail's row list (RowJob)
+struct RowJob {
+    const uint32_t *list = nullptr;  // device, count entries
+    uint32_t count = 0;
+    uint32_t *out32 = nullptr;
+    float *out32_loss = nullptr;
+};
+
 template <typename LatT, bool LROWS, int LPT, bool PACKED>
-srt_status launch_fold(srt_plan *p, unsigned long long *d_stats, uint32_t ubits, srt_err *err) {
-    const uint32_t V = p->V, rows = p->row1 - p->row0;
+srt_status launch_fold(srt_plan *p, unsigned long long *d_stats, uint32_t ubits, const RowJob &job, srt_err *err) {
+    const uint32_t V = p->V, rows = job.list ? job.count : p->row1 - p->row0;
     const uint32_t nt = V >= 2048 ? LOSS_NT : 256;
     const size_t lds = LROWS ? HIST_BYTES + (((size_t)V * sizeof(LatT) + 15) & ~(size_t)15) + (size_t)V * 4
                              : HIST_BYTES;
@@ -562,15 +662,16 @@ srt_status launch_fold(srt_plan *p, unsigned long long *d_stats, uint32_t ubits,
     }
     if (rows)
         hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, p->stream, (const void *)p->d_D, p->key_type, p->Vp, V,
-                           p->d_nodes, p->n, p->row0, p->row1, p->d_tptr, p->d_tu,
+                           p->d_nodes, p->n, job.list ? 0u : p->row0, job.list ? job.count : p->row1, p->d_tptr, p->d_tu,
                            reinterpret_cast<const LatT *>(p->d_tw), p->d_teb, p->d_tpk, ubits, p->kp.g, p->d_sl_lat,
                            p->d_sl_loss, p->d_out_lat, p->d_out_loss, d_stats, ord, lat_all, loss_all, p->d_row_ptr,
-                           p->d_col, p->d_lat, p->d_loss, std::getenv("SRT_LOSS_DIAG") ? (uint32_t)std::atoi(std::getenv("SRT_LOSS_DIAG")) : 0u);
+                           p->d_col, p->d_lat, p->d_loss, job.list, job.out32, job.out32_loss, std::getenv("SRT_LOSS_DIAG") ? (uint32_t)std::atoi(std::getenv("SRT_LOSS_DIAG")) : 0u);
     return SRT_OK;
 }
 
 template <typename LatT, bool LROWS, bool PACKED>
-srt_status launch_fold_lpt(srt_plan *p, unsigned long long *d_stats, uint32_t ubits, srt_err *err) {
+srt_status launch_fold_lpt(srt_plan *p, unsigned long long *d_stats, uint32_t ubits, const RowJob &job,
+                           srt_err *err) {
     // lanes per target ~ the average tight in-degree (a group walks a target's
     // in-edges 2-4 per lane per step)
     const double avg = p->V ? (double)p->t_edges / p->V : 0.0;
@@ -578,14 +679,64 @@ srt_status launch_fold_lpt(srt_plan *p, unsigned long long *d_stats, uint32_t ub
         // 4 lanes x 8 edges per target (C3, same box: 4 / 8 / 16 lanes ->
         // 31.9 / 33.0 / 36.5 ms for the pass; knob SRT_LOSS_LPT = 8 / 16)
         const char *k = std::getenv("SRT_LOSS_LPT");
-        if (k && std::atoi(k) == 8) return launch_fold<LatT, LROWS, 8, PACKED>(p, d_stats, ubits, err);
-        if (k && std::atoi(k) == 16) return launch_fold<LatT, LROWS, 16, PACKED>(p, d_stats, ubits, err);
-        if (avg > 10.0) return launch_fold<LatT, LROWS, 4, PACKED>(p, d_stats, ubits, err);
-        return launch_fold<LatT, LROWS, 2, PACKED>(p, d_stats, ubits, err);
+        if (k && std::atoi(k) == 8) return launch_fold<LatT, LROWS, 8, PACKED>(p, d_stats, ubits, job, err);
+        if (k && std::atoi(k) == 16) return launch_fold<LatT, LROWS, 16, PACKED>(p, d_stats, ubits, job, err);
+        if (avg > 10.0) return launch_fold<LatT, LROWS, 4, PACKED>(p, d_stats, ubits, job, err);
+        return launch_fold<LatT, LROWS, 2, PACKED>(p, d_stats, ubits, job, err);
     }
-    if (avg > 48.0) return launch_fold<LatT, LROWS, 32, PACKED>(p, d_stats, ubits, err);
-    if (avg > 10.0) return launch_fold<LatT, LROWS, 8, PACKED>(p, d_stats, ubits, err);
-    return launch_fold<LatT, LROWS, 2, PACKED>(p, d_stats, ubits, err);
+    if (avg > 48.0) return launch_fold<LatT, LROWS, 32, PACKED>(p, d_stats, ubits, job, err);
+    if (avg > 10.0) return launch_fold<LatT, LROWS, 8, PACKED>(p, d_stats, ubits, job, err);
+    return launch_fold<LatT, LROWS, 2, PACKED>(p, d_stats, ubits, job, err);
+}
+
+// tight edge arrays for p->t_edges entries (grown together, 25% headroom;
+// +1024: the packed scan reads up to (UNR - 1) * LPT entries past a row's end)
+srt_status ensure_edge_arrays(srt_plan *p, srt_err *err) {
+    if (p->t_edges + 1024 <= p->t_cap && p->d_tu) return SRT_OK;
+    const size_t wsz = p->kp.lat32 ? 4 : 8;
+    const uint64_t cap = std::max<uint64_t>(p->t_edges + p->t_edges / 4 + 1024, 2048);
+    for (void *q : {(void *)p->d_tu, p->d_tw, (void *)p->d_teb, (void *)p->d_tpk, (void *)p->d_tpk2}) (void)hipFree(q);
+    p->d_tu = nullptr;
+    p->d_tw = nullptr;
+    p->d_teb = nullptr;
+    p->d_tpk = p->d_tpk2 = nullptr;
+    p->t_cap = 0;
+    void *a = nullptr, *b = nullptr, *c = nullptr, *d = nullptr, *f = nullptr;
+    hipError_t e = hipMalloc(&a, cap * 4);
+    if (e == hipSuccess) e = hipMalloc(&b, cap * wsz);
+    if (e == hipSuccess) e = hipMalloc(&c, cap * 4);
+    if (e == hipSuccess) e = hipMalloc(&d, cap * 8);
+    if (e == hipSuccess) e = hipMalloc(&f, cap * 8);
+    if (e != hipSuccess) {
+        for (void *q : {a, b, c, d, f}) (void)hipFree(q);
+        return fail(err, e, "hipMalloc(tight edges)");
+    }
+    p->d_tu = (uint32_t *)a;
+    p->d_tw = b;
+    p->d_teb = (float *)c;
+    p->d_tpk = (uint64_t *)d;
+    p->d_tpk2 = (uint64_t *)f;
+    p->t_cap = cap;
+    return SRT_OK;
+}
+
+// packed entries d_tpk2 (rows by d_tptr) -> d_tpk, every target's row sorted
+// by w (bits ubits .. of the low word)
+srt_status sort_packed(srt_plan *p, uint32_t ubits, uint64_t maxw, srt_err *err) {
+    const unsigned end_bit = ubits + (unsigned)std::max(1, bits_of(maxw));
+    size_t need = 0;
+    hipError_t e = rocprim::segmented_radix_sort_keys(nullptr, need, p->d_tpk2, p->d_tpk, (unsigned)p->t_edges, p->V,
+                                                      p->d_tptr, p->d_tptr + 1, ubits, end_bit, p->stream);
+    if (e != hipSuccess) return fail(err, e, "segmented sort (size)");
+    uint64_t tcap = p->tsort_tmp_cap;
+    srt_status st = grow(reinterpret_cast<uint8_t **>(&p->d_tsort_tmp), &tcap, need + 256, err, "hipMalloc(sort scratch)");
+    p->tsort_tmp_cap = tcap;
+    if (st != SRT_OK) return st;
+    size_t have = p->tsort_tmp_cap;
+    e = rocprim::segmented_radix_sort_keys(p->d_tsort_tmp, have, p->d_tpk2, p->d_tpk, (unsigned)p->t_edges, p->V,
+                                           p->d_tptr, p->d_tptr + 1, ubits, end_bit, p->stream);
+    if (e != hipSuccess) return fail(err, e, "segmented sort");
+    return SRT_OK;
 }
 
 template <typename K>
@@ -611,8 +762,8 @@ srt_status tight_csr_t(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     p->h_tcount[0] = p->h_tcount[1] = 0;
     if (V) {
         hipLaunchKernelGGL(tight_flag_kernel<K>, dim3(blocks), dim3(256), 0, M, reinterpret_cast<const K *>(p->d_D),
-                           p->Vp, V, p->d_row_ptr, p->d_col, p->d_lat, p->kp.g, p->d_tflag, p->d_tcnt,
-                           (unsigned long long *)p->d_tmaxw);
+                           p->Vp, 0u, V, p->d_row_ptr, p->d_col, p->d_lat, p->kp.g, p->d_tflag, p->d_tcnt,
+                           (unsigned long long *)p->d_tmaxw, (unsigned long long *)nullptr);
         hipLaunchKernelGGL(tight_scan_kernel, dim3(1), dim3(1024), 0, M, p->d_tcnt, p->d_tptr, V);
         (void)hipMemcpyAsync(p->h_tcount, p->d_tptr + V, sizeof(uint64_t), hipMemcpyDeviceToHost, M);
         (void)hipMemcpyAsync(p->h_tcount + 1, p->d_tmaxw, sizeof(uint64_t), hipMemcpyDeviceToHost, M);
@@ -626,54 +777,13 @@ srt_status tight_csr_t(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     // SRT_LOSS_UNPACKED=1 forces the 3-array form for A/B and parity tests)
     p->t_packed = p->kp.lat32 && ubits + bits_of(maxw) <= 32 && p->t_edges < (1ull << 32) &&
                   !std::getenv("SRT_LOSS_UNPACKED");
-    const size_t wsz = p->kp.lat32 ? 4 : 8;
-    if (p->t_edges + 1024 > p->t_cap || !p->d_tu) {
-        // grow every edge array together (25% headroom)
-        // (+1024: the packed scan reads up to (UNR - 1) * LPT entries past a row's end)
-        const uint64_t cap = std::max<uint64_t>(p->t_edges + p->t_edges / 4 + 1024, 2048);
-        for (void *q : {(void *)p->d_tu, p->d_tw, (void *)p->d_teb, (void *)p->d_tpk, (void *)p->d_tpk2})
-            (void)hipFree(q);
-        p->d_tu = nullptr;
-        p->d_tw = nullptr;
-        p->d_teb = nullptr;
-        p->d_tpk = p->d_tpk2 = nullptr;
-        p->t_cap = 0;
-        void *a = nullptr, *b = nullptr, *c = nullptr, *d = nullptr, *f = nullptr;
-        e = hipMalloc(&a, cap * 4);
-        if (e == hipSuccess) e = hipMalloc(&b, cap * wsz);
-        if (e == hipSuccess) e = hipMalloc(&c, cap * 4);
-        if (e == hipSuccess) e = hipMalloc(&d, cap * 8);
-        if (e == hipSuccess) e = hipMalloc(&f, cap * 8);
-        if (e != hipSuccess) {
-            for (void *q : {a, b, c, d}) (void)hipFree(q);
-            return fail(err, e, "hipMalloc(tight edges)");
-        }
-        p->d_tu = (uint32_t *)a;
-        p->d_tw = b;
-        p->d_teb = (float *)c;
-        p->d_tpk = (uint64_t *)d;
-        p->d_tpk2 = (uint64_t *)f;
-        p->t_cap = cap;
-    }
+    if ((st = ensure_edge_arrays(p, err)) != SRT_OK) return st;
     if (!V) return SRT_OK;
     if (p->t_packed) {
         hipLaunchKernelGGL((tight_fill_kernel<uint32_t, true>), dim3(blocks), dim3(256), 0, M, V, p->d_row_ptr,
                            p->d_col, p->d_lat, p->d_loss, p->kp.g, p->d_tflag, p->d_tptr, p->d_tcnt,
                            (uint32_t *)nullptr, (uint32_t *)nullptr, (float *)nullptr, p->d_tpk2, ubits);
-        // every target's row sorted by w (bits ubits .. of the low word) into d_tpk
-        const unsigned end_bit = ubits + (unsigned)std::max(1, bits_of(maxw));
-        size_t need = 0;
-        e = rocprim::segmented_radix_sort_keys(nullptr, need, p->d_tpk2, p->d_tpk, (unsigned)p->t_edges, V,
-                                               p->d_tptr, p->d_tptr + 1, ubits, end_bit, M);
-        if (e != hipSuccess) return fail(err, e, "segmented sort (size)");
-        uint64_t tcap = p->tsort_tmp_cap;
-        st = grow(reinterpret_cast<uint8_t **>(&p->d_tsort_tmp), &tcap, need + 256, err, "hipMalloc(sort scratch)");
-        p->tsort_tmp_cap = tcap;
-        if (st != SRT_OK) return st;
-        size_t have = p->tsort_tmp_cap;
-        e = rocprim::segmented_radix_sort_keys(p->d_tsort_tmp, have, p->d_tpk2, p->d_tpk, (unsigned)p->t_edges, V,
-                                               p->d_tptr, p->d_tptr + 1, ubits, end_bit, M);
-        if (e != hipSuccess) return fail(err, e, "segmented sort");
+        if ((st = sort_packed(p, ubits, maxw, err)) != SRT_OK) return st;
     } else if (p->kp.lat32) {
         hipLaunchKernelGGL((tight_fill_kernel<uint32_t, false>), dim3(blocks), dim3(256), 0, M, V, p->d_row_ptr,
                            p->d_col, p->d_lat, p->d_loss, p->kp.g, p->d_tflag, p->d_tptr, p->d_tcnt, p->d_tu,
@@ -686,21 +796,267 @@ srt_status tight_csr_t(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     return SRT_OK;
 }
 
-srt_status fold(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
+srt_status fold(srt_plan *p, unsigned long long *d_stats, const RowJob &job, srt_err *err) {
     const uint32_t V = p->V;
     const uint32_t ubits = (uint32_t)std::max(1, bits_of(V ? V - 1 : 0));
     const bool lds_rows = HIST_BYTES + (size_t)V * 8 + 16 <= LDS_BUDGET - 4096;
     if (p->kp.lat32) {
         if (p->t_packed)
-            return lds_rows ? launch_fold_lpt<uint32_t, true, true>(p, d_stats, ubits, err)
-                            : launch_fold_lpt<uint32_t, false, true>(p, d_stats, ubits, err);
-        return lds_rows ? launch_fold_lpt<uint32_t, true, false>(p, d_stats, 0, err)
-                        : launch_fold_lpt<uint32_t, false, false>(p, d_stats, 0, err);
+            return lds_rows ? launch_fold_lpt<uint32_t, true, true>(p, d_stats, ubits, job, err)
+                            : launch_fold_lpt<uint32_t, false, true>(p, d_stats, ubits, job, err);
+        return lds_rows ? launch_fold_lpt<uint32_t, true, false>(p, d_stats, 0, job, err)
+                        : launch_fold_lpt<uint32_t, false, false>(p, d_stats, 0, job, err);
     }
-    return launch_fold_lpt<uint64_t, false, false>(p, d_stats, 0, err);
+    return launch_fold_lpt<uint64_t, false, false>(p, d_stats, 0, job, err);
+}
+
+// Sharded tail (comm bound): the tight edges of this rank's own adjacency
+// rows (its closure block-rows, final locally), the (count, max latency) of
+// every rank exchanged, then -- when the packed form applies -- the edge
+// lists all-gathered and the full pull CSR built from them on every rank.
+// *sharded = false: not packable, the caller falls back to the key
+// all-gather and the replicated CSR.
+template <typename K>
+srt_status tight_csr_shard_t(srt_plan *p, unsigned long long *d_stats, bool *sharded, srt_err *err) {
+    hipStream_t M = p->stream;
+    const uint32_t V = p->V, W = (uint32_t)p->comm->nranks, r = (uint32_t)p->comm->rank;
+    const uint32_t u0 = (uint32_t)std::min<uint64_t>((uint64_t)p->rb0 * FW_B, V);
+    const uint32_t u1 = (uint32_t)std::min<uint64_t>((uint64_t)p->rb1 * FW_B, V);
+    *sharded = false;
+    srt_status st;
+    uint64_t cap_flag = p->d_tflag ? p->n_adj : 0, cap_cnt = p->d_tcnt ? V : 0, cap_ptr = p->d_tptr ? V + 1ull : 0,
+             cap_mw = p->d_tmaxw ? 1 : 0, cap_info = p->d_tinfo ? 2ull * W : 0, cap_cur = p->d_tcursor ? 1 : 0;
+    if ((st = grow(&p->d_tflag, &cap_flag, std::max<uint64_t>(p->n_adj, 1), err, "hipMalloc(tight flags)")) != SRT_OK ||
+        (st = grow(&p->d_tcnt, &cap_cnt, std::max<uint64_t>(V, 1), err, "hipMalloc(tight counts)")) != SRT_OK ||
+        (st = grow(&p->d_tptr, &cap_ptr, V + 1ull, err, "hipMalloc(tight ptr)")) != SRT_OK ||
+        (st = grow(&p->d_tmaxw, &cap_mw, 1, err, "hipMalloc(tight max)")) != SRT_OK ||
+        (st = grow(&p->d_tinfo, &cap_info, 2ull * W, err, "hipMalloc(tight info)")) != SRT_OK ||
+        (st = grow(&p->d_tcursor, &cap_cur, 1, err, "hipMalloc(tight cursor)")) != SRT_OK)
+        return st;
+    if (!p->h_tinfo) {
+        const hipError_t e = hipHostMalloc((void **)&p->h_tinfo, 2 * sizeof(unsigned long long) * W, 0);
+        if (e != hipSuccess) return fail(err, e, "hipHostMalloc");
+    }
+    hipLaunchKernelGGL(loss_stats_init_kernel, dim3(1), dim3(1), 0, M, d_stats, (unsigned long long *)p->d_tmaxw);
+    (void)hipMemsetAsync(p->d_tinfo, 0, 2 * sizeof(unsigned long long) * W, M);
+    (void)hipMemsetAsync(p->d_tcursor, 0, sizeof(unsigned long long), M);
+    const uint32_t own_rows = u1 > u0 ? u1 - u0 : 0;
+    const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(8192, (own_rows + 3) / 4));
+    if (own_rows)
+        hipLaunchKernelGGL(tight_flag_kernel<K>, dim3(blocks), dim3(256), 0, M, reinterpret_cast<const K *>(p->d_D),
+                           p->Vp, u0, u1, p->d_row_ptr, p->d_col, p->d_lat, p->kp.g, p->d_tflag, (uint32_t *)nullptr,
+                           p->d_tinfo + 2 * r + 1, p->d_tinfo + 2 * r);
+    if ((st = comm_allgather_inplace(p->comm, p->d_tinfo, 2 * sizeof(unsigned long long), M, err)) != SRT_OK)
+        return st;
+    (void)hipMemcpyAsync(p->h_tinfo, p->d_tinfo, 2 * sizeof(unsigned long long) * W, hipMemcpyDeviceToHost, M);
+    hipError_t e = hipStreamSynchronize(M);
+    if (e != hipSuccess) return fail(err, e, "tight-edge count exchange");
+    uint64_t total = 0, maxw = 0, C = 1;
+    for (uint32_t q = 0; q < W; ++q) {
+        total += p->h_tinfo[2 * q];
+        maxw = std::max<uint64_t>(maxw, p->h_tinfo[2 * q + 1]);
+        C = std::max<uint64_t>(C, p->h_tinfo[2 * q]);
+    }
+    const uint32_t ubits = (uint32_t)std::max(1, bits_of(V ? V - 1 : 0));
+    if (!(p->kp.lat32 && ubits + bits_of(maxw) <= 32 && total < (1ull << 32) && !std::getenv("SRT_LOSS_UNPACKED")))
+        return SRT_OK;
+    if (C > p->tlist_cap || !p->d_tlist) {
+        const uint64_t cap = C + C / 4 + 64;
+        (void)hipFree(p->d_tlist);
+        p->d_tlist = nullptr;
+        p->tlist_cap = 0;
+        if ((e = hipMalloc(&p->d_tlist, cap * W * sizeof(uint4))) != hipSuccess) return fail(err, e, "hipMalloc(tight list)");
+        p->tlist_cap = cap;
+    }
+    // own chunk: the records, then v = ~0 padding up to C
+    (void)hipMemsetAsync(p->d_tlist + (uint64_t)r * C, 0xff, C * sizeof(uint4), M);
+    if (own_rows)
+        hipLaunchKernelGGL(tight_list_kernel, dim3(blocks), dim3(256), 0, M, u0, u1, p->d_row_ptr, p->d_col, p->d_lat,
+                           p->d_loss, p->kp.g, p->d_tflag, p->d_tlist + (uint64_t)r * C, p->d_tcursor);
+    if ((st = comm_allgather_inplace(p->comm, p->d_tlist, C * sizeof(uint4), M, err)) != SRT_OK) return st;
+    p->t_edges = total;
+    p->t_packed = true;
+    if ((st = ensure_edge_arrays(p, err)) != SRT_OK) return st;
+    const uint64_t slots = C * W;
+    const uint32_t lblocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, (slots + 255) / 256));
+    (void)hipMemsetAsync(p->d_tcnt, 0, (size_t)V * 4, M);
+    hipLaunchKernelGGL(tight_list_count_kernel, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tcnt);
+    hipLaunchKernelGGL(tight_scan_kernel, dim3(1), dim3(1024), 0, M, p->d_tcnt, p->d_tptr, V);
+    hipLaunchKernelGGL(tight_list_fill_kernel, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tptr, p->d_tcnt,
+                       p->d_tpk2, ubits);
+    if ((st = sort_packed(p, ubits, maxw, err)) != SRT_OK) return st;
+    *sharded = true;
+    return SRT_OK;
+}
+
+template <typename K>
+srt_status loss_sharded_t(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
+    bool sharded = false;
+    srt_status st = tight_csr_shard_t<K>(p, d_stats, &sharded, err);
+    if (st != SRT_OK) return st;
+    if (!sharded) {
+        // replicated fallback: every rank's closure rows, then the CSR of all rows
+        if ((st = fw_gather_keys(p, err)) != SRT_OK) return st;
+        if ((st = tight_csr_t<K>(p, d_stats, err)) != SRT_OK) return st;
+        return fold(p, d_stats, RowJob{}, err);
+    }
+    const uint32_t W = (uint32_t)p->comm->nranks, r = (uint32_t)p->comm->rank;
+    const size_t chunk = (size_t)p->lrow_max * p->n;
+    if (!p->d_slat) {
+        void *a = nullptr, *b = nullptr;
+        hipError_t e = hipMalloc(&a, std::max<size_t>(chunk * W, 1) * 4);
+        if (e == hipSuccess) e = hipMalloc(&b, std::max<size_t>(chunk * W, 1) * 4);
+        if (e != hipSuccess) {
+            (void)hipFree(a);
+            return fail(err, e, "hipMalloc(row staging)");
+        }
+        p->d_slat = (uint32_t *)a;
+        p->d_sloss = (float *)b;
+    }
+    // the fold in tail_q chunks of tail_cr rows; chunk c's rows go to every
+    // rank on the comm stream while chunk c + 1 folds (collectives stay in
+    // one order on every rank: the chunks, then -- on M, after the last
+    // chunk -- the rank stats)
+    const uint32_t q = p->tail_q, cr = p->tail_cr;
+    const size_t cbytes = (size_t)cr * p->n * 4;
+    hipStream_t M = p->stream, C = p->comm_stream;
+    for (uint32_t c = 0; c < q; ++c) {
+        const size_t slot = ((size_t)c * W + r) * cr;
+        RowJob job;
+        job.list = p->d_lrows + slot;
+        job.count = p->lrow_cnt[r] > c * cr ? std::min(cr, p->lrow_cnt[r] - c * cr) : 0u;
+        job.out32 = p->d_slat + slot * p->n;
+        job.out32_loss = p->d_sloss + slot * p->n;
+        if ((st = fold(p, d_stats, job, err)) != SRT_OK) return st;
+        (void)hipEventRecord(p->ev_tail[c], M);
+        (void)hipStreamWaitEvent(C, p->ev_tail[c], 0);
+        const size_t base = (size_t)c * W * cr * p->n;
+        if ((st = comm_allgather_inplace(p->comm, p->d_slat + base, cbytes, C, err)) != SRT_OK ||
+            (st = comm_allgather_inplace(p->comm, p->d_sloss + base, cbytes, C, err)) != SRT_OK)
+            return st;
+    }
+    (void)hipEventRecord(p->ev_tail[q], C);
+    (void)hipStreamWaitEvent(M, p->ev_tail[q], 0);
+    p->shard_tail = true;
+    return SRT_OK;
+}
+
+// Measurement only (SRT_FW_EMULATE_RANKS = N, no comm): wait `ticks` of the
+// constant wall clock on the stream -- stands in for a collective
+__global__ void emu_wait_kernel(long long ticks) {
+    const long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+// Emulated rank 0 of an N-rank sharded tail, on the closure the first run
+// left in D: the flags of its own adjacency rows, the list over every row
+// (the other rows' flags are the closing run's, of the same D), the count /
+// scan / fill / sort of the full list, the fold of its own rows into the
+// staging.  The three all-gathers are waits of SRT_FW_EMU_AG_US (default 25)
+// + received bytes / SRT_FW_EMU_AG_GBPS (default 300).
+template <typename K>
+srt_status loss_emulated_t(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
+    hipStream_t M = p->stream;
+    const uint32_t V = p->V, W = p->emulate_ranks;
+    const uint32_t u1 = (uint32_t)std::min<uint64_t>((uint64_t)std::max<uint32_t>(1, p->Vp / FW_B / W) * FW_B, V);
+    srt_status st;
+    uint64_t cap_info = p->d_tinfo ? 2 : 0, cap_cur = p->d_tcursor ? 1 : 0;
+    if ((st = grow(&p->d_tinfo, &cap_info, 2, err, "hipMalloc(tight info)")) != SRT_OK ||
+        (st = grow(&p->d_tcursor, &cap_cur, 1, err, "hipMalloc(tight cursor)")) != SRT_OK)
+        return st;
+    if (!p->h_tinfo) {
+        const hipError_t e = hipHostMalloc((void **)&p->h_tinfo, 2 * sizeof(unsigned long long), 0);
+        if (e != hipSuccess) return fail(err, e, "hipHostMalloc");
+    }
+    int khz = 100000;
+    (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, p->device);
+    const double lat_us = std::getenv("SRT_FW_EMU_AG_US") ? std::atof(std::getenv("SRT_FW_EMU_AG_US")) : 25.0;
+    const double gbps = std::getenv("SRT_FW_EMU_AG_GBPS") ? std::atof(std::getenv("SRT_FW_EMU_AG_GBPS")) : 300.0;
+    auto allgather_on = [&](double bytes_per_rank, hipStream_t s) {
+        const double us = lat_us + bytes_per_rank * (W - 1) / (gbps * 1e3);
+        hipLaunchKernelGGL(emu_wait_kernel, dim3(1), dim3(64), 0, s, (long long)(us * khz / 1000.0));
+    };
+    auto allgather = [&](double bytes_per_rank) { allgather_on(bytes_per_rank, M); };
+    hipLaunchKernelGGL(loss_stats_init_kernel, dim3(1), dim3(1), 0, M, d_stats, (unsigned long long *)p->d_tmaxw);
+    (void)hipMemsetAsync(p->d_tinfo, 0, 2 * sizeof(unsigned long long), M);
+    (void)hipMemsetAsync(p->d_tcursor, 0, sizeof(unsigned long long), M);
+    const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(8192, (u1 + 3) / 4));
+    hipLaunchKernelGGL(tight_flag_kernel<K>, dim3(blocks), dim3(256), 0, M, reinterpret_cast<const K *>(p->d_D), p->Vp,
+                       0u, u1, p->d_row_ptr, p->d_col, p->d_lat, p->kp.g, p->d_tflag, (uint32_t *)nullptr,
+                       p->d_tinfo + 1, p->d_tinfo);
+    allgather(16.0);
+    (void)hipMemcpyAsync(p->h_tinfo, p->d_tinfo, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, M);
+    hipError_t e = hipStreamSynchronize(M);
+    if (e != hipSuccess) return fail(err, e, "tight-edge count");
+    const uint64_t total = p->emu_tight, maxw = p->emu_maxw;
+    const uint64_t C = std::max<uint64_t>({1, p->h_tinfo[0], (total + W - 1) / W});
+    const uint32_t ubits = (uint32_t)std::max(1, bits_of(V ? V - 1 : 0));
+    if (!(p->kp.lat32 && ubits + bits_of(maxw) <= 32 && total < (1ull << 32)))
+        return fail(err, hipErrorNotSupported, "rank emulation needs the packed tight-edge form");
+    if (C > p->tlist_cap || !p->d_tlist) {
+        (void)hipFree(p->d_tlist);
+        p->d_tlist = nullptr;
+        p->tlist_cap = 0;
+        if ((e = hipMalloc(&p->d_tlist, C * W * sizeof(uint4))) != hipSuccess) return fail(err, e, "hipMalloc(tight list)");
+        p->tlist_cap = C;
+    }
+    const uint64_t slots = C * W;
+    (void)hipMemsetAsync(p->d_tlist, 0xff, slots * sizeof(uint4), M);
+    const uint32_t vblocks = std::max<uint32_t>(1, std::min<uint32_t>(8192, (V + 3) / 4));
+    hipLaunchKernelGGL(tight_list_kernel, dim3(vblocks), dim3(256), 0, M, 0u, V, p->d_row_ptr, p->d_col, p->d_lat,
+                       p->d_loss, p->kp.g, p->d_tflag, p->d_tlist, p->d_tcursor);
+    allgather((double)C * sizeof(uint4));
+    p->t_edges = total;
+    p->t_packed = true;
+    if ((st = ensure_edge_arrays(p, err)) != SRT_OK) return st;
+    const uint32_t lblocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, (slots + 255) / 256));
+    (void)hipMemsetAsync(p->d_tcnt, 0, (size_t)V * 4, M);
+    hipLaunchKernelGGL(tight_list_count_kernel, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tcnt);
+    hipLaunchKernelGGL(tight_scan_kernel, dim3(1), dim3(1024), 0, M, p->d_tcnt, p->d_tptr, V);
+    hipLaunchKernelGGL(tight_list_fill_kernel, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tptr, p->d_tcnt,
+                       p->d_tpk2, ubits);
+    if ((st = sort_packed(p, ubits, maxw, err)) != SRT_OK) return st;
+    const size_t chunk = (size_t)p->lrow_max * p->n;
+    if (!p->d_slat) {
+        void *a = nullptr, *b = nullptr;
+        e = hipMalloc(&a, std::max<size_t>(chunk * W, 1) * 4);
+        if (e == hipSuccess) e = hipMalloc(&b, std::max<size_t>(chunk * W, 1) * 4);
+        if (e != hipSuccess) {
+            (void)hipFree(a);
+            return fail(err, e, "hipMalloc(row staging)");
+        }
+        p->d_slat = (uint32_t *)a;
+        p->d_sloss = (float *)b;
+    }
+    const uint32_t q = p->tail_q, cr = p->tail_cr;
+    hipStream_t Cs = p->comm_stream;
+    for (uint32_t c = 0; c < q; ++c) {
+        const size_t slot = (size_t)c * W * cr;  // rank 0's slots of chunk c
+        RowJob job;
+        job.list = p->d_lrows + slot;
+        job.count = p->lrow_cnt[0] > c * cr ? std::min(cr, p->lrow_cnt[0] - c * cr) : 0u;
+        job.out32 = p->d_slat + slot * p->n;
+        job.out32_loss = p->d_sloss + slot * p->n;
+        if ((st = fold(p, d_stats, job, err)) != SRT_OK) return st;
+        (void)hipEventRecord(p->ev_tail[c], M);
+        (void)hipStreamWaitEvent(Cs, p->ev_tail[c], 0);
+        allgather_on((double)cr * p->n * 8.0, Cs);  // latency units + loss
+    }
+    (void)hipEventRecord(p->ev_tail[q], Cs);
+    (void)hipStreamWaitEvent(M, p->ev_tail[q], 0);
+    allgather(16.0);  // rank stats
+    p->shard_tail = true;
+    return SRT_OK;
 }
 
 }  // namespace
+
+void expand_shard_rows(srt_plan *p, int nranks) {
+    const uint32_t slots = (uint32_t)nranks * p->lrow_max;
+    if (!slots || !p->n) return;
+    hipLaunchKernelGGL(expand_rows_kernel, dim3(std::min<uint32_t>(slots, 4096)), dim3(256), 0, p->stream, p->d_lrows,
+                       slots, p->n, p->d_slat, p->d_sloss, p->kp.g, p->d_out_lat, p->d_out_loss);
+}
 
 srt_status fw_loss(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     if (!p->ev_loss0) {
@@ -709,11 +1065,30 @@ srt_status fw_loss(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     }
     (void)hipEventRecord(p->ev_loss0, p->stream);
     srt_status st;
+    p->shard_tail = false;
+    if (p->comm) {
+        if (p->key_type == KEY_U32) st = loss_sharded_t<uint32_t>(p, d_stats, err);
+        else if (p->key_type == KEY_F64) st = loss_sharded_t<double>(p, d_stats, err);
+        else st = loss_sharded_t<uint64_t>(p, d_stats, err);
+        if (st != SRT_OK) return st;
+        (void)hipEventRecord(p->ev_loss1, p->stream);
+        return SRT_OK;
+    }
+    if (p->emulate_ranks > 1 && p->emu_closed) {
+        if (p->key_type == KEY_U32) st = loss_emulated_t<uint32_t>(p, d_stats, err);
+        else if (p->key_type == KEY_F64) st = loss_emulated_t<double>(p, d_stats, err);
+        else st = loss_emulated_t<uint64_t>(p, d_stats, err);
+        if (st != SRT_OK) return st;
+        (void)hipEventRecord(p->ev_loss1, p->stream);
+        return SRT_OK;
+    }
     if (p->key_type == KEY_U32) st = tight_csr_t<uint32_t>(p, d_stats, err);
     else if (p->key_type == KEY_F64) st = tight_csr_t<double>(p, d_stats, err);
     else st = tight_csr_t<uint64_t>(p, d_stats, err);
     if (st != SRT_OK) return st;
-    if ((st = fold(p, d_stats, err)) != SRT_OK) return st;
+    p->emu_tight = p->t_edges;
+    p->emu_maxw = p->h_tcount[1];
+    if ((st = fold(p, d_stats, RowJob{}, err)) != SRT_OK) return st;
     (void)hipEventRecord(p->ev_loss1, p->stream);
     return SRT_OK;
 }

@@ -20,16 +20,21 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("world,n,seed,algo", [(2, 300, 1, "fw"), (3, 520, 2, "fw"), (2, 301, 3, "sssp"),
-                                                (3, 200, 4, "sssp"),
-                                                # the driver's 8-rank layout: 16 block-rows, the pivot
-                                                # owner changes every 2 rounds
-                                                (8, 1100, 5, "fw"), (8, 700, 6, "sssp")])
-def test_sharded_build_matches_oracle(world, n, seed, algo):
+@pytest.mark.parametrize("world,n,seed,algo,wide", [(2, 300, 1, "fw", False), (3, 520, 2, "fw", False),
+                                                     (2, 301, 3, "sssp", False), (3, 200, 4, "sssp", False),
+                                                     # the driver's 8-rank layout: 16 block-rows, the pivot
+                                                     # owner changes every 2 rounds
+                                                     (8, 1100, 5, "fw", False), (8, 700, 6, "sssp", False),
+                                                     # u64 keys: replicated loss pass after the key all-gather
+                                                     (3, 400, 7, "fw", True)])
+def test_sharded_build_matches_oracle(world, n, seed, algo, wide):
+    """Dense builds assert the sharded tail ran (or, "wide", the replicated
+    fallback); every rank's table equals the oracle's bit for bit."""
     port = _port()
     env = dict(os.environ)
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker.py"), str(r), str(world), str(port),
-                               str(n), str(seed), "torch", algo], env=env, stdout=subprocess.PIPE,
+                               str(n), str(seed), "torch", algo] + (["wide"] if wide else []), env=env,
+                              stdout=subprocess.PIPE,
                               stderr=subprocess.STDOUT, text=True) for r in range(world)]
     outs = []
     for p in procs:
@@ -72,6 +77,7 @@ def test_rccl_transport_single_rank(algo_name):
     plan.bind_comm(h)
     t = plan.run().fetch()
     assert "ranks=1" in plan.describe()
+    assert plan.timing()["sharded_tail"] == (1 if algo_name == "fw" else 0)
     plan.close()
     L.srt_comm_destroy(h)
     assert np.array_equal(t.latency_ns, ref.latency_ns)
