@@ -950,6 +950,10 @@ template <typename K>
 srt_status fw_rounds_group_t(srt_plan *p, int p1r, uint32_t g);
 
 template <typename K>
+srt_status fw_rounds_group_sharded_t(srt_plan *p, int p1r, uint32_t g, uint32_t rb0, uint32_t rb1, bool emu,
+                                     long long emu_bcast_ticks, srt_err *err);
+
+template <typename K>
 srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
     K *D = reinterpret_cast<K *>(p->d_D);
     const uint32_t nblk = p->Vp / B;
@@ -1009,6 +1013,19 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
     if (!sharded && !emu && p->fw_glds && (!p->fw_small_chain || std::getenv("SRT_FW_PAIR")) && grp > 1 &&
         grp <= 8 && nblk % grp == 0 && nblk >= 2 * grp)
         return fw_rounds_group_t<K>(p, p1r, grp);
+    // sharded: groups of 2 when every rank's block-rows split into whole
+    // groups (one owner per group) and there are >= 2 groups.  Emulated 8
+    // ranks, C3 (16k): 37.3 / 36.7 / 39.6 ms for g = 1 / 2 / 4 -- at g = 4 the
+    // chain (X(b) 257 us + 4 x (p1, p2row, p2col, cross)) outlasts F(a) 810 us
+    // (knob SRT_FW_SHARD_GROUP=0 / 2 / 4 for A/B timing)
+    {
+        uint32_t sg = 2;
+        if (const char *e = std::getenv("SRT_FW_SHARD_GROUP")) sg = (uint32_t)std::atoi(e);
+        const uint32_t per_local = emu ? std::max<uint32_t>(1, nblk / emu) : per_rank;
+        if ((sharded || emu) && p->fw_glds && sg > 1 && sg <= 8 && per_local % sg == 0 && nblk % sg == 0 &&
+            nblk >= 2 * sg)
+            return fw_rounds_group_sharded_t<K>(p, p1r, sg, rb0, rb1, emu != 0, emu_bcast_ticks, err);
+    }
     p->p3_tiles = 0;
     srt_status st = SRT_OK;
     // prologue: pivot 0
@@ -1198,6 +1215,135 @@ srt_status fw_rounds_group_t(srt_plan *p, int p1r, uint32_t g) {
             hipEventRecord(p->ev_pivot, S);
         }
     }
+    return SRT_OK;
+}
+
+// Tiles and relaxations of a grouped launch over rows x cols for the group
+// a .. a+g-1: a tile whose highest in-group row/column position is q runs
+// rounds q+1 .. (g - 1 - q of them), others all g.
+void group_work(const Span &r, const Span &c, uint32_t a, uint32_t g, double &work, double &tiles) {
+    for (uint32_t i = 0; i < r.n; ++i) {
+        const uint32_t bi = span_at(r, i);
+        for (uint32_t j = 0; j < c.n; ++j) {
+            const uint32_t bj = span_at(c, j);
+            const bool ii = bi - a < g, jj = bj - a < g;
+            uint32_t rounds = g;
+            if (ii || jj) rounds = g - 1 - std::max(ii ? bi - a : 0u, jj ? bj - a : 0u);
+            if (rounds) {
+                work += rounds;
+                tiles += 1;
+            }
+        }
+    }
+}
+
+// Sharded build (or its one-GPU emulation), rounds in groups of g; g divides
+// every rank's block-row count, so the pivot rows of a group have one owner.
+// Per group a (b = a + g the next, G(x) = block-rows/cols x .. x+g-1):
+//   M: F(a) = rounds G(a) on the local rows x all columns, minus columns G(b)
+//      and (on b's owner) rows G(b) -- the grouped rule of fw_rounds_group_t
+//      for tiles in G(a)
+//   S: X(b) = rounds G(a) on the local rows x columns G(b), and on b's owner
+//      rows G(b) x all columns; then chain(b): per r in G(b), on the owner
+//      p1(r), p2row(r), then the broadcast of block-row r on C (pipelined:
+//      row r is final for the chain once p2row(r) ran), p2col(r) on the local
+//      rows, round r on rows r+1.. of G(b) x all columns and on the local rows
+//      x columns r+1.. of G(b); on the other ranks, per r: row r received,
+//      p2col(r), round r on the local rows x columns r+1.. of G(b).
+// One broadcast per pivot block-row as before, 1/g as many rest launches,
+// each tile loaded and stored once per g rounds.  Operands read while a
+// concurrent launch lowers them are real paths' keys at least as tight as
+// the round's (the FW invariant of the look-ahead chain), so the closure is
+// the same bits.  Emulation (measurement only): this rank owns every group
+// and also waits out each row's modelled broadcast (SRT_FW_EMU_BCAST_US) as a
+// receiver would -- the longest chain any rank has.
+template <typename K>
+srt_status fw_rounds_group_sharded_t(srt_plan *p, int p1r, uint32_t g, uint32_t rb0, uint32_t rb1, bool emu,
+                                     long long emu_bcast_ticks, srt_err *err) {
+    K *D = reinterpret_cast<K *>(p->d_D);
+    const uint32_t nblk = p->Vp / B;
+    const bool sharded = p->comm != nullptr;
+    const uint32_t per_rank = sharded ? nblk / p->comm->nranks : nblk;
+    const size_t pivot_bytes = (size_t)B * p->Vp * sizeof(K);
+    hipStream_t M = p->stream, S = p->side_stream, C = p->comm_stream;
+    const Rect none{make_span(0, 0), make_span(0, 0)};
+    auto own = [&](uint32_t blk) { return emu || (blk >= rb0 && blk < rb1); };
+    p->p3_launches = 0;
+    p->p3_work = 0.0;
+    p->p3_tiles = 0;
+    const size_t need = 2 * (nblk / g) + 2;
+    while (p->ev.size() < need) {
+        hipEvent_t e;
+        hipEventCreateWithFlags(&e, std::getenv("SRT_FW_TIMING_FENCE") ? 0u : (unsigned)hipEventDisableSystemFence);
+        p->ev.push_back(e);
+    }
+    auto chain = [&](hipStream_t s, uint32_t a) -> srt_status {
+        const bool o = own(a);
+        for (uint32_t r = a; r < a + g; ++r) {
+            if (o) {
+                launch_p1<K>(p1r, s, D, p->Vp, r);
+                launch_tiles<K, 1>(p, s, r, Rect{make_span(r, r + 1), make_span(0, nblk, r)}, none);
+            }
+            if (sharded || emu_bcast_ticks) {
+                if (o) {
+                    hipEventRecord(p->ev_row, s);
+                    hipStreamWaitEvent(C, p->ev_row, 0);
+                }
+                if (sharded) {
+                    const srt_status st =
+                        comm_bcast(p->comm, D + (uint64_t)r * B * p->Vp, pivot_bytes, (int)(r / per_rank), C, err);
+                    if (st != SRT_OK) return st;
+                }
+                if (emu_bcast_ticks) hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, C, emu_bcast_ticks);
+                if (!o || emu_bcast_ticks) {
+                    hipEventRecord(p->ev_bcast, C);
+                    hipStreamWaitEvent(s, p->ev_bcast, 0);
+                }
+            }
+            launch_tiles<K, 2>(p, s, r, Rect{make_span(rb0, rb1, r), make_span(r, r + 1)}, none);
+            if (r + 1 < a + g)
+                launch_tiles<K, 4>(p, s, r, Rect{make_span(rb0, rb1, r), make_range(r + 1, a + g, NONE, NONE)},
+                                   o ? Rect{make_range(r + 1, a + g, NONE, NONE), make_span(0, nblk, r)} : none);
+        }
+        return SRT_OK;
+    };
+    // S starts after fw_init on M; chain(0)
+    hipEventRecord(p->ev_cross, M);
+    hipStreamWaitEvent(S, p->ev_cross, 0);
+    srt_status st = chain(S, 0);
+    if (st != SRT_OK) return st;
+    hipEventRecord(p->ev_pivot, S);
+    hipEvent_t rest_done = p->ev_cross;
+    for (uint32_t a = 0; a < nblk; a += g) {
+        const bool nxt = a + g < nblk;
+        const uint32_t b = a + g, c0 = nxt ? b : NONE, c1 = b + g;
+        if (nxt) hipStreamWaitEvent(S, rest_done, 0);  // F(a-g) done
+        hipStreamWaitEvent(M, p->ev_pivot, 0);         // chain(a) done
+        // rows of the next group this rank's S stream runs (X(b) rows): G(b)
+        // on its owner; in the emulation a local group stands in for it, so
+        // the emulated rank carries exactly an owner's load
+        const uint32_t lg = emu ? rb0 + ((b / g) % ((rb1 - rb0) / g)) * g : b;
+        const bool xr = nxt && own(b);
+        const Rect f{make_range(rb0, rb1, xr ? lg : NONE, lg + g), make_range(0, nblk, c0, c1)};
+        hipEventRecord(p->ev[2 * p->p3_launches], M);
+        launch_group<K>(p, M, a, g, f, none, false);
+        rest_done = p->ev[2 * p->p3_launches + 1];
+        hipEventRecord(rest_done, M);
+        p->p3_launches++;
+        double work = 0.0, tiles = 0.0;
+        group_work(f.r, f.c, a, g, work, tiles);
+        p->p3_work += work * B * B * B;
+        p->p3_tiles += (uint64_t)tiles;
+        if (nxt) {
+            const Span nx = make_range(b, b + g, NONE, NONE);
+            launch_group<K>(p, S, a, g, Rect{make_span(rb0, rb1), nx},
+                            xr ? Rect{make_range(lg, lg + g, NONE, NONE), make_range(0, nblk, b, b + g)} : none, true);
+            if ((st = chain(S, b)) != SRT_OK) return st;
+            hipEventRecord(p->ev_pivot, S);
+        }
+    }
+    hipEventRecord(p->ev_bcast, C);
+    hipStreamWaitEvent(M, p->ev_bcast, 0);
     return SRT_OK;
 }
 

@@ -41,7 +41,10 @@ def main():
     sdist.bind(plan, rank, world, 0, transport=transport)
     plan.run()
     t = plan.fetch()
-    tail = plan.timing()["sharded_tail"]
+    tm = plan.timing()
+    tail = tm["sharded_tail"]
+    # grouped sharded rounds: one rest launch per group (SRT_TEST_EXPECT_RESTS)
+    want_rests = os.environ.get("SRT_TEST_EXPECT_RESTS")
     ck = torch.tensor([int(np.bitwise_xor.reduce(t.latency_ns.reshape(-1) * np.uint64(2654435761))),
                        int(np.bitwise_xor.reduce(t.packet_loss.view(np.uint32).reshape(-1)))], dtype=torch.int64)
     all_ck = [torch.zeros_like(ck) for _ in range(world)]
@@ -55,7 +58,8 @@ def main():
         ok = ok and np.array_equal(t.packet_loss.view(np.uint32), eloss.view(np.uint32))
         # dense builds: the loss pass ran on the rank's own closure rows
         ok = ok and (algo_name != "fw" or tail == (0 if wide else 1))
-        print(f"rank0: {plan.describe()} sharded_tail={tail} ok={ok}", flush=True)
+        ok = ok and (want_rests is None or tm["dominant_launches"] == int(want_rests))
+        print(f"rank0: {plan.describe()} sharded_tail={tail} rests={tm['dominant_launches']} ok={ok}", flush=True)
     plan.close()
     dist.destroy_process_group()
     sys.exit(0 if ok else 1)

@@ -20,18 +20,23 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("world,n,seed,algo,wide", [(2, 300, 1, "fw", False), (3, 520, 2, "fw", False),
-                                                     (2, 301, 3, "sssp", False), (3, 200, 4, "sssp", False),
-                                                     # the driver's 8-rank layout: 16 block-rows, the pivot
-                                                     # owner changes every 2 rounds
-                                                     (8, 1100, 5, "fw", False), (8, 700, 6, "sssp", False),
-                                                     # u64 keys: replicated loss pass after the key all-gather
-                                                     (3, 400, 7, "fw", True)])
-def test_sharded_build_matches_oracle(world, n, seed, algo, wide):
+@pytest.mark.parametrize("world,n,seed,algo,wide,group", [
+    (2, 300, 1, "fw", False, None), (3, 520, 2, "fw", False, None),
+    (2, 301, 3, "sssp", False, None), (3, 200, 4, "sssp", False, None),
+    # the driver's 8-rank layout: 16 block-rows, the pivot owner changes every 2 rounds
+    (8, 1100, 5, "fw", False, None), (8, 700, 6, "sssp", False, None),
+    # grouped sharded rounds: 4 block-rows per rank in groups of 4, and groups of 2 (the default)
+    (2, 1000, 8, "fw", False, "4:2"), (3, 1300, 9, "fw", False, "4:3"), (8, 1100, 10, "fw", False, "2:8"),
+    (2, 1000, 11, "fw", False, "2:4"),
+    # u64 keys: replicated loss pass after the key all-gather
+    (3, 400, 7, "fw", True, None)])
+def test_sharded_build_matches_oracle(world, n, seed, algo, wide, group):
     """Dense builds assert the sharded tail ran (or, "wide", the replicated
     fallback); every rank's table equals the oracle's bit for bit."""
     port = _port()
     env = dict(os.environ)
+    if group:  # "g:rest launches"
+        env["SRT_FW_SHARD_GROUP"], env["SRT_TEST_EXPECT_RESTS"] = group.split(":")
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker.py"), str(r), str(world), str(port),
                                str(n), str(seed), "torch", algo] + (["wide"] if wide else []), env=env,
                               stdout=subprocess.PIPE,
