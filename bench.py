@@ -42,10 +42,13 @@ sys.path.insert(0, ROOT)
 
 # MI355X constants (/opt/skills/guides/MI355X_MICROARCH.md; profiles/r01_valu_bench.txt)
 VALU_LANE_OPS_PEAK = 256 * 64 * 2.4e9  # 39.3e12 lane-ops/s (one 4-cycle VALU slot per lane per cycle)
-# u32 latency keys: 2 v_add_u32 (double rate) + 1 v_min3_u32 per 2 relaxations =
-# 2 slots per 2 relaxations -> one slot per relaxation
-RELAX_PEAK = {"u32": VALU_LANE_OPS_PEAK / 1.0, "f64": VALU_LANE_OPS_PEAK / 2.0, "u64": VALU_LANE_OPS_PEAK / 4.0}
-RELAX_BASIS = {"u32": "2 v_add_u32 (issued at twice the rate) + 1 v_min3_u32 per 2 relaxations = 1 VALU slot",
+# u16 latency keys: v_pk_add_u16 + v_pk_min_u16 relax 2 keys = 1 slot per relaxation;
+# u32: 2 v_add_u32 (double rate) + 1 v_min3_u32 per 2 relaxations = 1 slot (an
+# optimistic basis: the mix measures 28.1 Trelax/s, tools/valu_bench.hip)
+RELAX_PEAK = {"u16": VALU_LANE_OPS_PEAK / 1.0, "u32": VALU_LANE_OPS_PEAK / 1.0, "f64": VALU_LANE_OPS_PEAK / 2.0,
+              "u64": VALU_LANE_OPS_PEAK / 4.0}
+RELAX_BASIS = {"u16": "v_pk_add_u16 + v_pk_min_u16 per 2 relaxations (2 keys per VGPR) = 1 VALU slot",
+               "u32": "2 v_add_u32 (issued at twice the rate) + 1 v_min3_u32 per 2 relaxations = 1 VALU slot",
                "f64": "v_add_f64 + v_min_f64 = 2 VALU slots", "u64": "v_lshl_add_u64 + v_cmp + 2 v_cndmask = 4 slots"}
 HBM_PEAK = 8.0e12  # B/s
 
@@ -281,7 +284,7 @@ def bench_gml(args, cfg, D):
             "metric": "APSP pairs/sec (routing-table build from GML text, 1k-node graph)",
             "value": D.world * n_nodes * n_nodes / per, "unit": "pairs/s", "n_gpus": D.world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": per * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "scaling": "weak", "vs_baseline": None, "dtype": "u16",
             "data": "synthetic (seeded complete GML graph, latency U{1..300} ms, loss U[0,0.01])",
             "config": {"workload": f"C1: {n_nodes}-node complete undirected GML graph, use_shortest_path=true: "
                                    f"GML text -> srt_gml_parse -> srt_compute_shortest_paths -> host table",
@@ -366,16 +369,16 @@ def bench_graph(args, cfg, D):
         key = desc.split(":")[1][:3] if desc.startswith("fw") else "u64"
         if desc.startswith("fw"):
             B_TILE = 128
-            kbytes = 4 if key == "u32" else 8
+            kbytes = {"u16": 2, "u32": 4}.get(key, 8)
             achieved = work_per_launch / avg_launch_s
             rounds = k_work / max(k_tiles * B_TILE ** 3, 1)
             schedule = {"key": key, "launch_rounds": int(round(rounds)), "ranks": D.world}
-            traffic, traffic_src = measured_traffic(args, "minplus", schedule)
+            traffic, traffic_src = measured_traffic(args, "(phase 3 rest)", schedule)
             peak = RELAX_PEAK[key]
             roofline = {
                 "bound": "valu", "achieved": achieved / 1e12, "peak": peak / 1e12, "unit": "Trelax/s",
                 "frac": achieved / peak, "traffic": traffic,
-                "traffic_unit": "HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction)",
+                "traffic_unit": "HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE: gfx950 16-B/lane correction)",
                 "traffic_source": (f"{traffic_src}: committed rocprofv3 PMC summary of this workload and schedule, "
                                    f"not measured in this run" if traffic_src else
                                    "no committed PMC summary for this workload/schedule"),
@@ -383,12 +386,12 @@ def bench_graph(args, cfg, D):
                 # every C tile read + written once per launch (A/B panels hit L2/MALL)
                 "algorithmic_hbm_bytes_per_launch": k_tiles / max(k_launches, 1) * B_TILE * B_TILE * 2 * kbytes,
                 "rounds_per_tile": rounds,
-                "kernel": f"minplus_{'u32' if key == 'u32' else 'glds'}_kernel<0> (FW phase 3, rest)",
+                "kernel": f"minplus_{key if key in ('u16', 'u32') else 'glds'}_kernel<0> (FW phase 3, rest)",
                 "avg_launch_ms": avg_launch_s * 1e3, "relax_per_launch": work_per_launch,
                 "peak_basis": f"{VALU_LANE_OPS_PEAK / 1e12:.1f}e12 VALU lane-op slots/s; {key} keys: "
                               f"{RELAX_BASIS[key]} per relaxation (f64 keys would peak at 19.7, the SURVEY's "
                               f"5-int32-op u64 basis at 7.86 Trelax/s)"}
-            algo = "blocked Floyd-Warshall (u32 latency closure) + exact-loss fold over the tight DAG"
+            algo = f"blocked Floyd-Warshall ({key} latency closure) + exact-loss fold over the tight DAG"
         else:
             achieved = work_per_launch / avg_launch_s
             roofline = {

@@ -212,9 +212,15 @@ bool choose_key_params(const CsrStats &cs, uint32_t V, KeyParams *kp, int *key_t
         cs.complete ? (unsigned __int128)maxu : (unsigned __int128)(V ? V - 1 : 0) * maxu;
     kp->lmax = Lmax > (unsigned __int128)~0ull ? ~0ull : (uint64_t)Lmax;
     kp->lat32 = Lmax < 0xffffffffull;
+    // knob SRT_FW_KEY = u16 / u32 / f64 / u64: the narrowest key allowed (A/B, tests)
     const char *force = std::getenv("SRT_FW_KEY");
+    const bool allow16 = !force || std::strcmp(force, "u16") == 0;
     const int min_type = !force ? srt::KEY_U32 : std::strcmp(force, "u64") == 0 ? srt::KEY_U64
                          : std::strcmp(force, "f64") == 0 ? srt::KEY_F64 : srt::KEY_U32;
+    if (allow16 && 2 * Lmax + 1 < (unsigned __int128)srt::KEY16_INF) {
+        *key_type = srt::KEY_U16;
+        return true;
+    }
     if (min_type <= srt::KEY_U32 && 2 * Lmax + 1 < (unsigned __int128)srt::KEY32_INF) {
         *key_type = srt::KEY_U32;
         return true;
@@ -518,8 +524,13 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
             }
         }
         if (const char *e = std::getenv("SRT_FW_BAND")) p->fw_band = e[0] != '0';
+        if (const char *e = std::getenv("SRT_FW_RELAX")) p->fw_relax = std::atoi(e);
+        if (const char *e = std::getenv("SRT_FW_ABLATE")) p->fw_ablate = (uint32_t)std::atoi(e) & 15u;
         std::snprintf(d, sizeof d, "fw:%s B=%d g=%llu lmax=%llu V=%u n=%u stage=%s band=%d loss=tight-dag%s",
-                      p->key_type == srt::KEY_U32 ? "u32key" : p->key_type == srt::KEY_F64 ? "f64key" : "u64key",
+                      p->key_type == srt::KEY_U16   ? "u16key"
+                      : p->key_type == srt::KEY_U32 ? "u32key"
+                      : p->key_type == srt::KEY_F64 ? "f64key"
+                                                    : "u64key",
                       srt::FW_B, (unsigned long long)p->kp.g, (unsigned long long)p->kp.lmax, p->V, n,
                       p->fw_glds ? "glds" : "reg", (int)p->fw_band, p->kp.lat32 ? "/u32" : "/u64");
     } else {

@@ -60,6 +60,18 @@ struct KeyOps<uint32_t> {
     static __device__ __forceinline__ uint64_t to_int(uint32_t k) { return k; }
 };
 
+// u16 latency keys (2 lmax < KEY16_INF, host-proved -- a complete graph's
+// shortest paths never exceed its longest edge): INF + INF < 2^16, like u32
+template <>
+struct KeyOps<uint16_t> {
+    static __device__ __forceinline__ uint16_t inf() { return KEY16_INF; }
+    static __device__ __forceinline__ uint16_t zero() { return 0; }
+    static __device__ __forceinline__ uint16_t kmin(uint32_t a, uint32_t b) { return (uint16_t)(a < b ? a : b); }
+    static __device__ __forceinline__ uint16_t from_int(uint64_t v) { return (uint16_t)v; }
+    static __device__ __forceinline__ bool is_inf(uint16_t k) { return k >= KEY16_INF; }
+    static __device__ __forceinline__ uint64_t to_int(uint16_t k) { return k; }
+};
+
 template <>
 struct KeyOps<double> {
     static __device__ __forceinline__ double inf() { return __builtin_huge_val(); }
@@ -84,6 +96,15 @@ template <typename K>
 __device__ __forceinline__ void relax_row8(K (&acc)[8], K a, const K (&b)[8]) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = KeyOps<K>::kmin(acc[j], a + b[j]);
+}
+
+template <>
+__device__ __forceinline__ void relax_row8<uint16_t>(uint16_t (&acc)[8], uint16_t a, const uint16_t (&b)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint32_t t = (uint32_t)a + b[j];  // < 2^16: both operands <= KEY16_INF
+        acc[j] = (uint16_t)(acc[j] < t ? acc[j] : t);
+    }
 }
 
 template <>
@@ -154,7 +175,22 @@ __global__ void scatter_edges_kernel(K *__restrict__ D, uint32_t Vp,
             // u64 value works for both representations (f64 bits of non-negative
             // doubles order like the doubles)
             const uint64_t key = edge_key(lat[k], kp);
-            if constexpr (sizeof(K) == 4) {
+            if constexpr (sizeof(K) == 2) {
+                K *dst = &D[(uint64_t)u * Vp + v];
+                if constexpr (UNIQUE) {
+                    *dst = (K)key;
+                } else {
+                    // 16-bit atomic min: CAS on the aligned 32-bit word
+                    unsigned int *w = (unsigned int *)((uintptr_t)dst & ~(uintptr_t)3);
+                    const unsigned sh = ((uintptr_t)dst & 2) ? 16u : 0u;
+                    unsigned int old = *w, assumed;
+                    do {
+                        assumed = old;
+                        if (((assumed >> sh) & 0xffffu) <= key) break;
+                        old = atomicCAS(w, assumed, (assumed & ~(0xffffu << sh)) | ((unsigned)key << sh));
+                    } while (old != assumed);
+                }
+            } else if constexpr (sizeof(K) == 4) {
                 if constexpr (UNIQUE)
                     D[(uint64_t)u * Vp + v] = (K)key;
                 else
@@ -653,19 +689,63 @@ __device__ __forceinline__ void relax_quad32(uint32_t &c0, uint32_t &c1, uint32_
           "v"(b1.w));
 }
 
-template <int s>
+// 8 adds t[c] = a + b0[c] / b1[c] (c < 4) into 8 temporaries
+__device__ __forceinline__ void add8_32(uint32_t (&t)[8], uint32_t a, u32x4 b0, u32x4 b1) {
+    asm volatile(
+        "v_add_u32 %0, %8, %9\n\t"
+        "v_add_u32 %1, %8, %10\n\t"
+        "v_add_u32 %2, %8, %11\n\t"
+        "v_add_u32 %3, %8, %12\n\t"
+        "v_add_u32 %4, %8, %13\n\t"
+        "v_add_u32 %5, %8, %14\n\t"
+        "v_add_u32 %6, %8, %15\n\t"
+        "v_add_u32 %7, %8, %16"
+        : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "=&v"(t[5]), "=&v"(t[6]), "=&v"(t[7])
+        : "v"(a), "v"(b0.x), "v"(b0.y), "v"(b0.z), "v"(b0.w), "v"(b1.x), "v"(b1.y), "v"(b1.z), "v"(b1.w));
+}
+
+// acc[c] = min3(acc[c], t[c], u[c]), c < 8
+__device__ __forceinline__ void min8_32(uint32_t (&acc)[8], const uint32_t (&t)[8], const uint32_t (&u)[8]) {
+    asm volatile(
+        "v_min3_u32 %0, %0, %8, %16\n\t"
+        "v_min3_u32 %1, %1, %9, %17\n\t"
+        "v_min3_u32 %2, %2, %10, %18\n\t"
+        "v_min3_u32 %3, %3, %11, %19\n\t"
+        "v_min3_u32 %4, %4, %12, %20\n\t"
+        "v_min3_u32 %5, %5, %13, %21\n\t"
+        "v_min3_u32 %6, %6, %14, %22\n\t"
+        "v_min3_u32 %7, %7, %15, %23"
+        : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[6]),
+          "+v"(acc[7])
+        : "v"(t[0]), "v"(t[1]), "v"(t[2]), "v"(t[3]), "v"(t[4]), "v"(t[5]), "v"(t[6]), "v"(t[7]), "v"(u[0]),
+          "v"(u[1]), "v"(u[2]), "v"(u[3]), "v"(u[4]), "v"(u[5]), "v"(u[6]), "v"(u[7]));
+}
+
+template <int s, int RV>
 __device__ __forceinline__ void chunk_steps32(uint32_t (&acc)[8][8], StepOps32 (&o)[2], uint32_t abase,
                                               uint32_t bbase) {
     if constexpr (s < KC32 / 2) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if constexpr (s + 1 < KC32 / 2) lds_step32<s + 1>(o[(s + 1) & 1], abase, bbase);
         const StepOps32 &c = o[s & 1];
+        if constexpr (RV == 0) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            relax_quad32(acc[i][0], acc[i][1], acc[i][2], acc[i][3], c.a[i].x, c.a[i].y, c.b[0], c.b[2]);
-            relax_quad32(acc[i][4], acc[i][5], acc[i][6], acc[i][7], c.a[i].x, c.a[i].y, c.b[1], c.b[3]);
+            for (int i = 0; i < 8; ++i) {
+                relax_quad32(acc[i][0], acc[i][1], acc[i][2], acc[i][3], c.a[i].x, c.a[i].y, c.b[0], c.b[2]);
+                relax_quad32(acc[i][4], acc[i][5], acc[i][6], acc[i][7], c.a[i].x, c.a[i].y, c.b[1], c.b[3]);
+            }
+        } else {
+            // a row's 16 adds (k, k+1) before its 8 min3: each min3 reads
+            // sums produced >= 8 instructions earlier
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                uint32_t t[8], u[8];
+                add8_32(t, c.a[i].x, c.b[0], c.b[1]);
+                add8_32(u, c.a[i].y, c.b[2], c.b[3]);
+                min8_32(acc[i], t, u);
+            }
         }
-        chunk_steps32<s + 1>(acc, o, abase, bbase);
+        chunk_steps32<s + 1, RV>(acc, o, abase, bbase);
     }
 }
 
@@ -695,7 +775,7 @@ __device__ __forceinline__ void tile_of(uint32_t t, const Rect &r1, const Rect &
     }
 }
 
-template <int TAG>
+template <int TAG, int RV = 0>
 __global__ __launch_bounds__(NT3, 2) void minplus_u32_kernel(uint32_t *__restrict__ D, uint32_t Vp, uint32_t kb,
                                                                Rect r1, Rect r2, uint32_t ng) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[2 * GBUF32];
@@ -718,12 +798,19 @@ __global__ __launch_bounds__(NT3, 2) void minplus_u32_kernel(uint32_t *__restric
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int tx = tid % 16, ty = tid / 16;
 
+    // measurement-only ablations (bits 20.., knob SRT_FW_ABLATE; the closure
+    // is wrong with any of them): 1 no C load, 2 no C store, 4 no chunk
+    // staging after the first, 8 no per-chunk wait + barrier
+    const uint32_t abl = ng >> 20;
     uint32_t acc[8][8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const uint32_t *src = D + (i0 + ty + 16 * i) * Vp + j0 + tx * 4;
-        const u32x4 lo = *reinterpret_cast<const u32x4 *>(src);
-        const u32x4 hi = *reinterpret_cast<const u32x4 *>(src + 64);
+        u32x4 lo = {0x3fffffffu, 0x3fffffffu, 0x3fffffffu, 0x3fffffffu}, hi = lo;
+        if (!(abl & 1)) {
+            lo = *reinterpret_cast<const u32x4 *>(src);
+            hi = *reinterpret_cast<const u32x4 *>(src + 64);
+        }
         acc[i][0] = lo.x;
         acc[i][1] = lo.y;
         acc[i][2] = lo.z;
@@ -759,17 +846,20 @@ __global__ __launch_bounds__(NT3, 2) void minplus_u32_kernel(uint32_t *__restric
 #pragma unroll 1
     for (int ch = ch0; ch < ch1; ++ch) {
         const int cur = (ch - ch0) & 1;
-        if (ch + 1 < ch1) stage(ch + 1, cur ^ 1);  // the other buffer's readers passed the last barrier
+        if (ch + 1 < ch1 && !(abl & 4)) stage(ch + 1, cur ^ 1);  // the other buffer's readers passed the last barrier
         const uint32_t *As = lds + cur * GBUF32 + ty * KC32;      // row ty of piece 0
         const uint32_t *Bs = lds + cur * GBUF32 + AIMG32 + tx * 4;  // columns tx*4 of k-row 0
         const uint32_t abase = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t *)As;
         const uint32_t bbase = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t *)Bs;
         StepOps32 o[2];
         lds_step32<0>(o[0], abase, bbase);
-        chunk_steps32<0>(acc, o, abase, bbase);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        chunk_steps32<0, RV>(acc, o, abase, bbase);
+        if (!(abl & 8)) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
     }
+    if (abl & 2) return;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         uint32_t *dst = D + (i0 + ty + 16 * i) * Vp + j0 + tx * 4;
@@ -784,6 +874,181 @@ __global__ __launch_bounds__(NT3, 2) void minplus_u32_kernel(uint32_t *__restric
         hi.w = acc[i][7];
         *reinterpret_cast<u32x4 *>(dst) = lo;
         *reinterpret_cast<u32x4 *>(dst + 64) = hi;
+    }
+}
+
+// ------------------------------------------------------------ u16 keys
+// Packed 16-bit latency keys (the host proves 2 lmax < KEY16_INF): a VGPR
+// holds the keys of two adjacent columns and
+//     acc = v_pk_min_u16(acc, v_pk_add_u16(a_k, b_pair))
+// relaxes both with 2 instructions (A's key is broadcast to both halves by
+// op_sel) -- 1 VALU slot per relaxation, where u32 keys measure 1.4
+// (tools/valu_bench.hip: the u16 mix 37.6 / 34.5, the u32 mix 28.1 / 23.9
+// Trelax/s at 8 / 2 waves per SIMD), and half the LDS and HBM bytes.
+// Same 128 x 128 tile per 256-thread workgroup; thread (tx, ty) holds rows
+// ty + 16 i (i < 8) and the 8 columns tx*8 .. tx*8+7 as 4 pairs: C loads and
+// stores are 16 B per lane, 256 contiguous bytes per 16 lanes.  K-chunks of
+// KC16 = 32 keys staged by LDS-DMA (16 wave-instructions of 1 KiB per chunk):
+//   A image: 8 pieces of [16 rows][32 k] + 16 B pad -- byte for byte the u32
+//     kernel's layout (64-B rows), so a thread reads k .. k+3 of its row i
+//     with one ds_read_b64;
+//   B image: [32 k][128 cols], 4 k-rows per 1-KiB piece; a thread reads its 8
+//     columns of a k-row with one ds_read_b128 (16 lanes: 256 contiguous B).
+constexpr int KC16 = 32;
+constexpr int NCH16 = B / KC16;
+constexpr int APIECE16 = 16 * KC16 + 8;      // u16 per padded A piece (1040 B)
+constexpr int AIMG16 = (B / 16) * APIECE16;  // 4160
+constexpr int BIMG16 = KC16 * B;             // 4096
+constexpr int GBUF16 = AIMG16 + BIMG16;      // u16 per buffer (16.5 KB)
+
+struct StepOps16 {
+    u32x2 a[8];  // a[i] = A[row i][k .. k+3] (2 keys per dword)
+    u32x4 b[4];  // b[m] = B[k+m][the thread's 8 columns] (4 pairs)
+};
+
+// LDS reads of step-quad s (k = 4s .. 4s+3) into o; abase = byte address of
+// the thread's row in piece 0, bbase = of its first column in k-row 0.
+template <int s>
+__device__ __forceinline__ void lds_step16(StepOps16 &o, uint32_t abase, uint32_t bbase) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(o.a[i]) : "v"(abase), "i"(i * APIECE16 * 2 + 8 * s));
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(o.b[m]) : "v"(bbase), "i"((4 * s + m) * B * 2));
+}
+
+// acc[p] = pk_min(acc[p], a.H + b[p]) for the 4 column pairs p, where a.H =
+// the low (H = 0) or high (H = 1) key of a, broadcast to both halves
+template <int H>
+__device__ __forceinline__ void relax_pairs16(uint32_t (&acc)[4], uint32_t a, u32x4 b) {
+    uint32_t t0, t1, t2, t3;
+    if constexpr (H == 0)
+        asm volatile(
+            "v_pk_add_u16 %0, %8, %9 op_sel_hi:[0,1]\n\t"
+            "v_pk_add_u16 %1, %8, %10 op_sel_hi:[0,1]\n\t"
+            "v_pk_add_u16 %2, %8, %11 op_sel_hi:[0,1]\n\t"
+            "v_pk_add_u16 %3, %8, %12 op_sel_hi:[0,1]\n\t"
+            "v_pk_min_u16 %4, %4, %0\n\t"
+            "v_pk_min_u16 %5, %5, %1\n\t"
+            "v_pk_min_u16 %6, %6, %2\n\t"
+            "v_pk_min_u16 %7, %7, %3"
+            : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3])
+            : "v"(a), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w));
+    else
+        asm volatile(
+            "v_pk_add_u16 %0, %8, %9 op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+            "v_pk_add_u16 %1, %8, %10 op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+            "v_pk_add_u16 %2, %8, %11 op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+            "v_pk_add_u16 %3, %8, %12 op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+            "v_pk_min_u16 %4, %4, %0\n\t"
+            "v_pk_min_u16 %5, %5, %1\n\t"
+            "v_pk_min_u16 %6, %6, %2\n\t"
+            "v_pk_min_u16 %7, %7, %3"
+            : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3])
+            : "v"(a), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w));
+}
+
+template <int s>
+__device__ __forceinline__ void chunk_steps16(uint32_t (&acc)[8][4], StepOps16 (&o)[2], uint32_t abase,
+                                              uint32_t bbase) {
+    if constexpr (s < KC16 / 4) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (s + 1 < KC16 / 4) lds_step16<s + 1>(o[(s + 1) & 1], abase, bbase);
+        const StepOps16 &c = o[s & 1];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            relax_pairs16<0>(acc[i], c.a[i].x, c.b[0]);
+            relax_pairs16<1>(acc[i], c.a[i].x, c.b[1]);
+            relax_pairs16<0>(acc[i], c.a[i].y, c.b[2]);
+            relax_pairs16<1>(acc[i], c.a[i].y, c.b[3]);
+        }
+        chunk_steps16<s + 1>(acc, o, abase, bbase);
+    }
+}
+
+template <int TAG>
+__global__ __launch_bounds__(NT3, 2) void minplus_u16_kernel(uint16_t *__restrict__ D, uint32_t Vp, uint32_t kb,
+                                                             Rect r1, Rect r2, uint32_t ng) {
+    __shared__ __attribute__((aligned(16))) uint16_t lds[2 * GBUF16];
+    if constexpr (TAG != 0) __builtin_amdgcn_s_setprio(2);  // look-ahead chain: issue priority
+    uint32_t bi, bj;
+    tile_of(blockIdx.x, r1, r2, ng, bi, bj);
+    // grouped rounds (see minplus_glds_kernel)
+    const uint32_t ng_ = ng & 0xffffu;
+    int ch0 = 0;
+    const int ch1 = (int)ng_ * NCH16;
+    if (ng_ > 1) {
+        const uint32_t qi = bi - kb < ng_ ? bi - kb : 0u, qj = bj - kb < ng_ ? bj - kb : 0u;
+        const bool in = bi - kb < ng_ || bj - kb < ng_;
+        const uint32_t q = std::max(qi, qj);
+        if (in && q == ng_ - 1) return;  // workgroup-uniform, before any barrier
+        ch0 = in ? (int)(q + 1) * NCH16 : 0;
+    }
+    const uint64_t i0 = (uint64_t)bi * B, j0 = (uint64_t)bj * B;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int tx = tid % 16, ty = tid / 16;
+    const uint32_t abl = ng >> 20;  // measurement-only ablations, as the u32 kernel
+
+    uint32_t acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        u32x4 v = {0x3fff3fffu, 0x3fff3fffu, 0x3fff3fffu, 0x3fff3fffu};
+        if (!(abl & 1)) v = *reinterpret_cast<const u32x4 *>(D + (i0 + ty + 16 * i) * Vp + j0 + tx * 8);
+        acc[i][0] = v.x;
+        acc[i][1] = v.y;
+        acc[i][2] = v.z;
+        acc[i][3] = v.w;
+    }
+    auto stage = [&](int ch, int buf) {
+        const uint64_t kk = (uint64_t)(kb + ch / NCH16) * B + (ch % NCH16) * KC16;  // first k of the chunk
+        uint16_t *img = lds + buf * GBUF16;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int piece = wave * 2 + q;  // A rows piece*16 .. +15, 64 B each
+            const uint16_t *g = D + (i0 + piece * 16 + lane / 4) * Vp + kk + (lane % 4) * 8;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
+                                             (__attribute__((address_space(3))) void *)(img + piece * APIECE16), 16,
+                                             0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int piece = wave * 2 + q;  // B k-rows 4 piece .. 4 piece + 3, 256 B each
+            const uint16_t *g = D + (kk + piece * 4 + lane / 16) * Vp + j0 + (lane % 16) * 8;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
+                                             (__attribute__((address_space(3))) void *)(img + AIMG16 + piece * 512),
+                                             16, 0, 0);
+        }
+    };
+    stage(ch0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll 1
+    for (int ch = ch0; ch < ch1; ++ch) {
+        const int cur = (ch - ch0) & 1;
+        if (ch + 1 < ch1 && !(abl & 4)) stage(ch + 1, cur ^ 1);  // the other buffer's readers passed the last barrier
+        const uint16_t *As = lds + cur * GBUF16 + ty * KC16;      // row ty of piece 0
+        const uint16_t *Bs = lds + cur * GBUF16 + AIMG16 + tx * 8;  // columns tx*8 of k-row 0
+        const uint32_t abase = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint16_t *)As;
+        const uint32_t bbase = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint16_t *)Bs;
+        StepOps16 o[2];
+        lds_step16<0>(o[0], abase, bbase);
+        chunk_steps16<0>(acc, o, abase, bbase);
+        if (!(abl & 8)) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+    }
+    if (abl & 2) return;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        u32x4 v;
+        v.x = acc[i][0];
+        v.y = acc[i][1];
+        v.z = acc[i][2];
+        v.w = acc[i][3];
+        *reinterpret_cast<u32x4 *>(D + (i0 + ty + 16 * i) * Vp + j0 + tx * 8) = v;
     }
 }
 
@@ -921,7 +1186,10 @@ void launch_tiles(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1, const
         hipLaunchKernelGGL((minplus_small_kernel<K, TAG>), dim3(4 * n), dim3(256), 0, s,
                            reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2);
     else if (p->fw_glds) {
-        if constexpr (sizeof(K) == 4)
+        if constexpr (sizeof(K) == 2)
+            hipLaunchKernelGGL((minplus_u16_kernel<TAG>), dim3(n), dim3(NT3), 0, s,
+                               reinterpret_cast<uint16_t *>(p->d_D), p->Vp, kb, r1, r2, 1u);
+        else if constexpr (sizeof(K) == 4)
             hipLaunchKernelGGL((minplus_u32_kernel<TAG>), dim3(n), dim3(NT3), 0, s,
                                reinterpret_cast<uint32_t *>(p->d_D), p->Vp, kb, r1, r2, 1u);
         else
@@ -1141,10 +1409,17 @@ void launch_group(srt_plan *p, hipStream_t s, uint32_t a, uint32_t g, const Rect
     if (!n) return;
     K *D = reinterpret_cast<K *>(p->d_D);
     // bit 16: banded tile order (plan knob SRT_FW_BAND=0 turns it off for A/B timing)
-    const uint32_t arg = g | (p->fw_band ? 0x10000u : 0u);
-    if constexpr (sizeof(K) == 4) {
+    const uint32_t arg = g | (p->fw_band ? 0x10000u : 0u) | (chain ? 0u : p->fw_ablate << 20);
+    if constexpr (sizeof(K) == 2) {
+        if (chain)
+            hipLaunchKernelGGL((minplus_u16_kernel<5>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
+        else
+            hipLaunchKernelGGL((minplus_u16_kernel<0>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
+    } else if constexpr (sizeof(K) == 4) {
         if (chain)
             hipLaunchKernelGGL((minplus_u32_kernel<5>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
+        else if (p->fw_relax)
+            hipLaunchKernelGGL((minplus_u32_kernel<0, 1>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
         else
             hipLaunchKernelGGL((minplus_u32_kernel<0>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
     } else {
@@ -1350,7 +1625,8 @@ srt_status fw_rounds_group_sharded_t(srt_plan *p, int p1r, uint32_t g, uint32_t 
 }  // namespace
 
 void fw_init(srt_plan *p) {
-    if (p->key_type == KEY_U32) fw_init_t<uint32_t>(p);
+    if (p->key_type == KEY_U16) fw_init_t<uint16_t>(p);
+    else if (p->key_type == KEY_U32) fw_init_t<uint32_t>(p);
     else if (p->key_type == KEY_F64) fw_init_t<double>(p);
     else fw_init_t<uint64_t>(p);
 }
@@ -1362,6 +1638,7 @@ srt_status fw_gather_keys(srt_plan *p, srt_err *err) {
 }
 
 srt_status fw_rounds(srt_plan *p, srt_err *err) {
+    if (p->key_type == KEY_U16) return fw_rounds_t<uint16_t>(p, err);
     if (p->key_type == KEY_U32) return fw_rounds_t<uint32_t>(p, err);
     return p->key_type == KEY_F64 ? fw_rounds_t<double>(p, err) : fw_rounds_t<uint64_t>(p, err);
 }

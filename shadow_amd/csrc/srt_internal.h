@@ -21,16 +21,18 @@ namespace srt {
 // path halves cannot reproduce.  So the closure computes only the exact
 // latencies, and the loss of every pair is recomputed afterwards, bit for bit,
 // by the left fold over the tight shortest-path DAG (srt_loss.hip, SURVEY.md
-// S-R6).  Keys are exact integers: u32 when every candidate sum (two stored
-// latencies, each <= lmax) stays below KEY32_INF (v_add_u32 + v_min3_u32: the
-// fastest relaxation), else f64 below 2^53, else u64 below KEY_INF; the host
-// proves it (choose_key_params in srt_api.cpp).
+// S-R6).  Keys are exact integers: u16 when every candidate sum (two stored
+// latencies, each <= lmax) stays below KEY16_INF (packed: v_pk_add_u16 +
+// v_pk_min_u16 relax two keys per instruction pair -- the fastest), else u32
+// below KEY32_INF (v_add_u32 + v_min3_u32), else f64 below 2^53, else u64
+// below KEY_INF; the host proves it (choose_key_params in srt_api.cpp).
 constexpr uint64_t KEY_INF = 1ull << 62;  // INF + INF < 2^64: no wrap in the closure
 constexpr uint32_t KEY32_INF = 0x7fffffffu;  // u32 keys: INF + INF < 2^32
+constexpr uint16_t KEY16_INF = 0x7fff;       // u16 keys: INF + INF < 2^16
 
-// closure key representation, fastest first (srt_plan::key_type)
-enum KeyType { KEY_U32 = 0, KEY_F64 = 1, KEY_U64 = 2 };
-inline size_t key_bytes(int t) { return t == KEY_U32 ? 4 : 8; }
+// closure key representation (srt_plan::key_type); u32 < f64 < u64 in speed
+enum KeyType { KEY_U32 = 0, KEY_F64 = 1, KEY_U64 = 2, KEY_U16 = 3 };
+inline size_t key_bytes(int t) { return t == KEY_U16 ? 2 : t == KEY_U32 ? 4 : 8; }
 
 struct KeyParams {
     uint64_t g;     // latency unit (gcd of all edge latencies, ns)
@@ -77,6 +79,8 @@ struct srt_plan {
     bool fw_glds = true;   // FW tiles staged by LDS-DMA (false: register staging)
     bool fw_small_chain = false;  // quarter-tile kernels for the look-ahead chain (sharded)
     bool fw_unique_edges = false; // no parallel edges: FW init stores instead of atomic min
+    int fw_relax = 0;             // u32 rest kernel relax order (SRT_FW_RELAX, A/B)
+    uint32_t fw_ablate = 0;       // measurement only: u32 rest-kernel ablations (SRT_FW_ABLATE, see the kernel)
     bool fw_band = true;          // grouped launches: banded tile order (knob SRT_FW_BAND=0, read at create)
     uint32_t emulate_ranks = 0;   // measurement only, see fw_rounds_t
     bool emu_closed = false;      // emulation: D holds the closure (first run done)

@@ -57,6 +57,11 @@ constexpr size_t LDS_BUDGET = 160 * 1024 - 1024;
 template <typename K>
 struct KeyLat;
 template <>
+struct KeyLat<uint16_t> {
+    static __device__ __forceinline__ bool inf(uint16_t k) { return k >= KEY16_INF; }
+    static __device__ __forceinline__ uint64_t lat(uint16_t k) { return k; }
+};
+template <>
 struct KeyLat<uint32_t> {
     static __device__ __forceinline__ bool inf(uint32_t k) { return k >= KEY32_INF; }
     static __device__ __forceinline__ uint64_t lat(uint32_t k) { return k; }
@@ -74,6 +79,11 @@ struct KeyLat<uint64_t> {
 
 // latency (units of g) of closure entry idx; kt = srt_plan::key_type (uniform)
 __device__ __forceinline__ uint64_t closure_lat(const void *D, uint64_t idx, int kt, bool &inf) {
+    if (kt == KEY_U16) {
+        const uint16_t k = reinterpret_cast<const uint16_t *>(D)[idx];
+        inf = KeyLat<uint16_t>::inf(k);
+        return k;
+    }
     if (kt == KEY_U32) {
         const uint32_t k = reinterpret_cast<const uint32_t *>(D)[idx];
         inf = KeyLat<uint32_t>::inf(k);
@@ -1067,7 +1077,8 @@ srt_status fw_loss(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     srt_status st;
     p->shard_tail = false;
     if (p->comm) {
-        if (p->key_type == KEY_U32) st = loss_sharded_t<uint32_t>(p, d_stats, err);
+        if (p->key_type == KEY_U16) st = loss_sharded_t<uint16_t>(p, d_stats, err);
+        else if (p->key_type == KEY_U32) st = loss_sharded_t<uint32_t>(p, d_stats, err);
         else if (p->key_type == KEY_F64) st = loss_sharded_t<double>(p, d_stats, err);
         else st = loss_sharded_t<uint64_t>(p, d_stats, err);
         if (st != SRT_OK) return st;
@@ -1075,14 +1086,16 @@ srt_status fw_loss(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
         return SRT_OK;
     }
     if (p->emulate_ranks > 1 && p->emu_closed) {
-        if (p->key_type == KEY_U32) st = loss_emulated_t<uint32_t>(p, d_stats, err);
+        if (p->key_type == KEY_U16) st = loss_emulated_t<uint16_t>(p, d_stats, err);
+        else if (p->key_type == KEY_U32) st = loss_emulated_t<uint32_t>(p, d_stats, err);
         else if (p->key_type == KEY_F64) st = loss_emulated_t<double>(p, d_stats, err);
         else st = loss_emulated_t<uint64_t>(p, d_stats, err);
         if (st != SRT_OK) return st;
         (void)hipEventRecord(p->ev_loss1, p->stream);
         return SRT_OK;
     }
-    if (p->key_type == KEY_U32) st = tight_csr_t<uint32_t>(p, d_stats, err);
+    if (p->key_type == KEY_U16) st = tight_csr_t<uint16_t>(p, d_stats, err);
+    else if (p->key_type == KEY_U32) st = tight_csr_t<uint32_t>(p, d_stats, err);
     else if (p->key_type == KEY_F64) st = tight_csr_t<double>(p, d_stats, err);
     else st = tight_csr_t<uint64_t>(p, d_stats, err);
     if (st != SRT_OK) return st;

@@ -80,19 +80,19 @@ def test_groups_equal_single_round(monkeypatch, n):
 
 @pytest.mark.parametrize("n,seed,directed", [(1000, 11, False), (1300, 12, True)])
 def test_key_types_agree(monkeypatch, n, seed, directed):
-    """The closure's three key representations (u32 by default when 2 lmax <
-    2^31 - 1, f64 and u64 forced by SRT_FW_KEY) produce the same table bits,
-    single-round and grouped."""
+    """The closure's four key representations (u16 by default here: 2 (n-1)
+    x 9 units < 2^15 - 1; u32, f64 and u64 forced by SRT_FW_KEY) produce the
+    same table bits, single-round and grouped by 2 and 4."""
     e = synth.random_graph(n, seed, p_edge=6.0 / n, directed=directed, lat_range_ns=(1, 9), loss_max=0.05)
     g = NetworkGraph.from_edges(n, *e, directed=directed)
     nodes = np.random.default_rng(seed).permutation(n).astype(np.uint32)
     tabs = {}
-    for key in ("u32", "f64", "u64"):
-        if key == "u32":
+    for key in ("u16", "u32", "f64", "u64"):
+        if key == "u16":
             monkeypatch.delenv("SRT_FW_KEY", raising=False)
         else:
             monkeypatch.setenv("SRT_FW_KEY", key)
-        for grp in ("1", "2"):
+        for grp in ("1", "2", "4"):
             monkeypatch.setenv("SRT_FW_PAIR", "1")
             monkeypatch.setenv("SRT_FW_GROUP", grp)
             plan = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_FW)

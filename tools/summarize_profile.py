@@ -7,7 +7,9 @@ under profiles/ (committed; gpurun_out/ is scratch):
                                      every kernel (bench.py reads the dominant
                                      kernel's entry as roofline.traffic)
 
-usage: python tools/summarize_profile.py gpurun_out/<tag> <tag> "<config text>"
+usage: python tools/summarize_profile.py gpurun_out/<tag> <tag> "<config text>" ['<schedule json>']
+(the schedule -- key type, rounds per rest launch, ranks -- is what bench.py
+matches before it quotes a summary's traffic for a run)
 """
 import csv
 import collections
@@ -20,6 +22,12 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 LABELS = {
+    "minplus_u16_kernel<0>": "phase 3 rest",
+    "minplus_u16_kernel<5>": "phase 3 look-ahead (grouped)",
+    "minplus_u32_kernel<0>": "phase 3 rest",
+    "minplus_u32_kernel<5>": "phase 3 look-ahead (grouped)",
+    "tight_loss_kernel": "exact-loss fold",
+    "tight_flag_kernel": "tight-edge flags",
     "minplus_glds_kernel<double, 0>": "phase 3 rest",
     "minplus_glds_kernel<double, 4>": "phase 3 cross",
     "minplus_glds_kernel<double, 5>": "phase 3 cross (paired rounds)",
@@ -30,6 +38,13 @@ LABELS = {
     "decide_kernel": "packet decide",
     "draw_kernel": "packet draw",
 }
+
+
+# FETCH_SIZE correction per kernel (MI355X_MICROARCH.md HBM section: x2 for
+# 16-B/lane streaming reads, global_load and buffer_load ... lds alike).  The
+# u16 / u32 tile kernels read C tiles and panels 16 B per lane; others as recorded
+# (the f64 tile kernels' 8-B/lane C loads were calibrated 1:1 in r01).
+FETCH_CORR = {"minplus_u32_kernel": 2.0, "minplus_u16_kernel": 2.0}
 
 
 def short(name):
@@ -69,16 +84,18 @@ def main():
         wkb, wn = write.get(k, (0.0, 1))
         label = next((v for p, v in LABELS.items() if k.startswith(p)), None)
         key = f"{k} ({label})" if label else k
+        corr = next((v for p, v in FETCH_CORR.items() if k.startswith(p)), 1.0)
         kernels[key] = {"dispatches": max(fn, wn), "FETCH_SIZE_KB_per_launch": fkb / max(fn, 1),
-                        "WRITE_SIZE_KB_per_launch": wkb / max(wn, 1),
-                        "hbm_bytes_per_launch": 1024.0 * (fkb / max(fn, 1) + wkb / max(wn, 1))}
+                        "WRITE_SIZE_KB_per_launch": wkb / max(wn, 1), "fetch_correction": corr,
+                        "hbm_bytes_per_launch": 1024.0 * (corr * fkb / max(fn, 1) + wkb / max(wn, 1))}
     doc = {"round": tag, "config": config,
+           "schedule": json.loads(sys.argv[4]) if len(sys.argv) > 4 else None,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (MI355X_MICROARCH.md "
-                     "HBM section), KB per dispatch averaged over the dispatches of each kernel.  Raw counter "
-                     "values: the guide's x2 FETCH_SIZE correction applies to 16-B/lane streams; the FW tile "
-                     "kernels' HBM reads are the 8-B/lane C-tile loads (calibrated 1:1 in r01: FETCH_SIZE of the "
-                     "rest kernel == 126^2 x 128 KB of C tiles) while their 16-B/lane LDS-DMA panel loads are "
-                     "served by L2 / Infinity Cache, so no correction is applied.",
+                     "HBM section), KB per dispatch averaged over the dispatches of each kernel. "
+                     "hbm_bytes_per_launch = fetch_correction x FETCH_SIZE + WRITE_SIZE: x2 for the u32 tile "
+                     "kernel (16-B/lane C-tile and LDS-DMA panel reads, the guide's gfx950 correction); 1 "
+                     "elsewhere (raw counter: the f64 tile kernels' 8-B/lane C loads calibrated 1:1 in r01, "
+                     "other widths uncalibrated).",
            "kernels": kernels}
     json.dump(doc, open(os.path.join(out, f"{tag}_pmc_traffic.json"), "w"), indent=1)
     print(json.dumps({k: round(v["hbm_bytes_per_launch"] / 1e6, 2) for k, v in kernels.items()}, indent=1))

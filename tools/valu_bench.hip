@@ -109,10 +109,73 @@ __global__ __launch_bounds__(256) void k_relax_u32sat(unsigned *out, unsigned se
     if (seed == 12345u) out[threadIdx.x] = sink;
 }
 
+// the u32 rest kernel's instruction mix (relax_quad32: 4 v_add_u32 + 2
+// v_min3_u32 per 4 relaxations), 64 accumulators per lane like the kernel
+__global__ __launch_bounds__(256) void k_mix_u32(unsigned *out, unsigned seed) {
+    unsigned acc[16];
+    for (int i = 0; i < 16; ++i) acc[i] = ~0u >> 1;
+    unsigned a0 = seed + threadIdx.x, a1 = a0 * 3u, b0 = seed * 5u, b1 = b0 + 1, b2 = b0 + 2, b3 = b0 + 3,
+             b4 = b0 + 4, b5 = b0 + 5, b6 = b0 + 6, b7 = b0 + 7;
+    for (int it = 0; it < ITER; ++it) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            unsigned t0, t1, t2, t3;
+            asm volatile(
+                "v_add_u32 %0, %8, %10\n\t"
+                "v_add_u32 %1, %9, %14\n\t"
+                "v_add_u32 %2, %8, %11\n\t"
+                "v_add_u32 %3, %9, %15\n\t"
+                "v_min3_u32 %4, %4, %0, %1\n\t"
+                "v_min3_u32 %5, %5, %2, %3\n\t"
+                "v_add_u32 %0, %8, %12\n\t"
+                "v_add_u32 %1, %9, %16\n\t"
+                "v_add_u32 %2, %8, %13\n\t"
+                "v_add_u32 %3, %9, %17\n\t"
+                "v_min3_u32 %6, %6, %0, %1\n\t"
+                "v_min3_u32 %7, %7, %2, %3"
+                : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "+v"(acc[4 * q]), "+v"(acc[4 * q + 1]),
+                  "+v"(acc[4 * q + 2]), "+v"(acc[4 * q + 3])
+                : "v"(a0), "v"(a1), "v"(b0), "v"(b1), "v"(b2), "v"(b3), "v"(b4), "v"(b5), "v"(b6), "v"(b7));
+        }
+    }
+    unsigned sink = 0;
+    for (int i = 0; i < 16; ++i) sink ^= acc[i];
+    if (seed == 12345u) out[threadIdx.x] = sink;
+}
+
+// packed u16 keys: acc pair (c, c+1) = pk_min(acc, sat(a_k + b_pair)), the A
+// value broadcast to both halves with op_sel; 2 relaxations per instruction pair
+__global__ __launch_bounds__(256) void k_mix_u16(unsigned *out, unsigned seed) {
+    unsigned acc[16];
+    for (int i = 0; i < 16; ++i) acc[i] = 0x7fff7fffu;
+    unsigned a0 = seed + threadIdx.x, b0 = seed * 5u, b1 = b0 + 1, b2 = b0 + 2, b3 = b0 + 3;
+    for (int it = 0; it < ITER; ++it) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            unsigned t0, t1, t2, t3;
+            asm volatile(
+                "v_pk_add_u16 %0, %8, %9 op_sel_hi:[0,1] clamp\n\t"
+                "v_pk_add_u16 %1, %8, %10 op_sel_hi:[0,1] clamp\n\t"
+                "v_pk_add_u16 %2, %8, %11 op_sel:[1,0] op_sel_hi:[1,1] clamp\n\t"
+                "v_pk_add_u16 %3, %8, %12 op_sel:[1,0] op_sel_hi:[1,1] clamp\n\t"
+                "v_pk_min_u16 %4, %4, %0\n\t"
+                "v_pk_min_u16 %5, %5, %1\n\t"
+                "v_pk_min_u16 %6, %6, %2\n\t"
+                "v_pk_min_u16 %7, %7, %3"
+                : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "+v"(acc[4 * q]), "+v"(acc[4 * q + 1]),
+                  "+v"(acc[4 * q + 2]), "+v"(acc[4 * q + 3])
+                : "v"(a0), "v"(b0), "v"(b1), "v"(b2), "v"(b3));
+        }
+    }
+    unsigned sink = 0;
+    for (int i = 0; i < 16; ++i) sink ^= acc[i];
+    if (seed == 12345u) out[threadIdx.x] = sink;
+}
+
 typedef void (*kfn)(unsigned *, unsigned);
 
-static void run(const char *name, kfn k, int instr_per_iter, unsigned *d) {
-    const int grid = 2048, block = 256;
+static void run(const char *name, kfn k, int instr_per_iter, unsigned *d, int grid = 2048) {
+    const int block = 256;
     hipLaunchKernelGGL(k, dim3(grid), dim3(block), 0, 0, d, 1u);  // warm
     hipDeviceSynchronize();
     hipEvent_t a, b;
@@ -144,6 +207,15 @@ int main() {
     run("v_min_f64", k_min_f64, 8, d);
     run("relax_u64(x1)", k_relax_u64, 8, d);  // reported per relaxation
     run("relax_u32sat(x1)", k_relax_u32sat, 8, d);
+    // per relaxation (16 per asm block x 4 blocks per iteration = 32 relax... see k_mix_u32)
+    run("mix_u32 8w/SIMD", k_mix_u32, 32, d);
+    run("mix_u32 2w/SIMD", k_mix_u32, 32, d, 512);
+    run("mix_u32 1w/SIMD", k_mix_u32, 32, d, 256);
+    run("v_add_u32 2w/SIMD", k_add_u32, 8, d, 512);
+    // 4 blocks x 8 instructions = 32 instructions = 32 relaxations (2 per packed pair of ops)
+    run("mix_u16 8w/SIMD", k_mix_u16, 32, d);
+    run("mix_u16 2w/SIMD", k_mix_u16, 32, d, 512);
+    run("v_min3 2w/SIMD", k_min3_u32, 8, d, 512);
     hipFree(d);
     return 0;
 }
