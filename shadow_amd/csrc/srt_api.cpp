@@ -340,8 +340,21 @@ int srt_device_count(void) {
     return n;
 }
 
+namespace {
+srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n, const srt_opts *opts,
+                            srt_plan **plan_out, srt_err *err, bool defer_loss);
+}
+
 srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
                            const srt_opts *opts, srt_plan **plan_out, srt_err *err) {
+    return plan_create_impl(g, nodes, n, opts, plan_out, err, false);
+}
+
+namespace {
+// defer_loss (end-to-end build only): the edge-loss array is uploaded by
+// run_tail, while the closure runs -- g->loss must stay valid until then
+srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n, const srt_opts *opts,
+                            srt_plan **plan_out, srt_err *err, bool defer_loss) {
     clear_err(err);
     Trace tr;
     if (!g || !plan_out || (n && !nodes) || !g->row_ptr || (g->n_adj && (!g->col || !g->lat_ns || !g->loss))) {
@@ -438,10 +451,11 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
             if (!bytes) return hipSuccess;
             return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, p->stream);
         };
+        if (defer_loss) p->h_loss_defer = g->loss;
         if ((e = up(p->d_row_ptr, g->row_ptr, ((size_t)g->n_nodes + 1) * 8)) != hipSuccess ||
             (e = up(p->d_col, g->col, g->n_adj * 4)) != hipSuccess ||
             (e = up(p->d_lat, g->lat_ns, g->n_adj * 8)) != hipSuccess ||
-            (e = up(p->d_loss, g->loss, g->n_adj * 4)) != hipSuccess ||
+            (e = defer_loss ? hipSuccess : up(p->d_loss, g->loss, g->n_adj * 4)) != hipSuccess ||
             (e = up(p->d_nodes, nodes, (size_t)n * 4)) != hipSuccess)
             return hip_fail(err, e, "upload");
         return SRT_OK;
@@ -621,31 +635,38 @@ srt_status srt_plan_create(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     return SRT_OK;
 }
 
-srt_status srt_plan_run_async(srt_plan *p, srt_err *err) {
-    clear_err(err);
-    if (!p) {
-        set_err(err, SRT_ERR_INVALID, "null plan");
-        return SRT_ERR_INVALID;
-    }
+// The device build in two host phases: the closure (FW rounds / SSSP sweeps)
+// is enqueued first, so that run_tail's blocking host work (the deferred
+// loss upload) overlaps it on the GPU.
+srt_status run_closure(srt_plan *p, srt_err *err) {
     HIP_TRY(hipSetDevice(p->device), "hipSetDevice");
     hipEventRecord(p->ev_begin, p->stream);
+    p->loss_ms = 0.0;
+    const int rank = p->comm ? p->comm->rank : 0;
+    unsigned long long *rstats = p->comm ? p->d_rstats + 2 * rank : p->d_stats;
+    if (p->algo == SRT_ALGO_SSSP) return srt::sssp_run(p, rstats, err);
+    // N-rank emulation (measurement only): the first run closes D for
+    // real; later runs replay rank 0's schedule on the closed D (every
+    // round leaves a closed D unchanged, and the kernels' cost does not
+    // depend on the keys), so rank 0's loss-pass share sees valid keys
+    if (!p->emu_closed) srt::fw_init(p);
+    return srt::fw_rounds(p, err);
+}
+
+srt_status run_tail(srt_plan *p, srt_err *err) {
     srt_status st;
     // table rows [row0, row1) of this rank; every rank then holds the whole
-    // table after the row all-gather, and the stats of all ranks
+    // table after the row exchange, and the stats of all ranks
     const int rank = p->comm ? p->comm->rank : 0, nranks = p->comm ? p->comm->nranks : 1;
     unsigned long long *rstats = p->comm ? p->d_rstats + 2 * rank : p->d_stats;
-    p->loss_ms = 0.0;
-    if (p->algo == SRT_ALGO_SSSP) {
-        st = srt::sssp_run(p, rstats, err);
-        if (st != SRT_OK) return st;
-    } else {
-        // N-rank emulation (measurement only): the first run closes D for
-        // real; later runs replay rank 0's schedule on the closed D (every
-        // round leaves a closed D unchanged, and the kernels' cost does not
-        // depend on the keys), so rank 0's loss-pass share sees valid keys
-        if (!p->emu_closed) srt::fw_init(p);
-        st = srt::fw_rounds(p, err);
-        if (st != SRT_OK) return st;
+    if (p->h_loss_defer) {
+        // end-to-end build: the edge losses, uploaded while the closure runs
+        // (pageable source: the copy returns once the data is on the device)
+        HIP_TRY(hipMemcpyAsync(p->d_loss, p->h_loss_defer, p->n_adj * 4, hipMemcpyHostToDevice, p->stream),
+                "upload (loss)");
+        p->h_loss_defer = nullptr;
+    }
+    if (p->algo != SRT_ALGO_SSSP) {
         // exact loss over the tight DAG (sharded: over this rank's own
         // closure rows, see fw_loss)
         st = srt::fw_loss(p, rstats, err);
@@ -673,6 +694,18 @@ srt_status srt_plan_run_async(srt_plan *p, srt_err *err) {
     HIP_TRY(hipGetLastError(), "kernel launch");
     p->ran = true;
     return SRT_OK;
+}
+}  // namespace
+
+srt_status srt_plan_run_async(srt_plan *p, srt_err *err) {
+    clear_err(err);
+    if (!p) {
+        set_err(err, SRT_ERR_INVALID, "null plan");
+        return SRT_ERR_INVALID;
+    }
+    srt_status st = run_closure(p, err);
+    if (st == SRT_OK) st = run_tail(p, err);
+    return st;
 }
 
 srt_status srt_plan_sync(srt_plan *p, srt_err *err) {
@@ -736,7 +769,7 @@ srt_status srt_plan_fetch(srt_plan *p, srt_path *out, uint64_t *min_latency_ns, 
         }
         for (uint64_t off = 0; off < total; off += chunk) {
             const uint64_t c = std::min<uint64_t>(chunk, total - off);
-            srt::pack_paths(p, off, c);
+            srt::pack_paths(p, off, c, p->d_pack, p->stream);
             HIP_TRY(hipMemcpyAsync(out + off, p->d_pack, c * sizeof(srt_path), hipMemcpyDeviceToHost, p->stream),
                     "download");
             HIP_TRY(hipStreamSynchronize(p->stream), "sync");
@@ -921,18 +954,60 @@ srt_status srt_plan_bind_comm(srt_plan *p, srt_comm *comm, srt_err *err) {
     return SRT_OK;
 }
 
+namespace {
+// End-to-end download behind the chunked fold (fw_loss with fold_chunk_rows):
+// chunk c's rows are packed and copied to the host on the comm stream (idle
+// on one GPU) once ev_fold[c] fires, while the fold of chunk c + 1 runs.
+srt_status fetch_pipelined(srt_plan *p, srt_path *out, uint64_t *min_latency_ns, srt_err *err) {
+    const uint64_t nn = (uint64_t)p->n * p->n, per = (uint64_t)p->fold_chunk_rows * p->n;
+    const uint32_t nc = (uint32_t)((nn + per - 1) / per);
+    if (!p->d_pack) {
+        void *ptr = nullptr;
+        hipError_t e = hipMalloc(&ptr, per * sizeof(srt_path));
+        if (e != hipSuccess) return hip_fail(err, e, "hipMalloc(pack)");
+        p->d_pack = (srt_path *)ptr;
+    }
+    hipStream_t C = p->comm_stream;
+    for (uint32_t c = 0; c < nc; ++c) {
+        const uint64_t first = (uint64_t)c * per, cnt = std::min(per, nn - first);
+        HIP_TRY(hipStreamWaitEvent(C, p->ev_fold[c], 0), "wait fold chunk");
+        srt::pack_paths(p, first, cnt, p->d_pack, C);
+        HIP_TRY(hipMemcpyAsync(out + first, p->d_pack, cnt * sizeof(srt_path), hipMemcpyDeviceToHost, C),
+                "download");
+    }
+    HIP_TRY(hipStreamSynchronize(C), "sync");
+    srt_status s = srt_plan_sync(p, err);
+    // connectivity (the reference's assert) and the min latency; the table is home
+    if (s == SRT_OK) s = srt_plan_fetch(p, nullptr, min_latency_ns, err);
+    return s;
+}
+}  // namespace
+
 srt_status srt_compute_shortest_paths(const srt_csr *g, const uint32_t *nodes, uint32_t n,
                                       srt_path *out, uint64_t *min_latency_ns,
                                       const srt_opts *opts, srt_err *err) {
     srt_plan *p = nullptr;
     Trace tr;
-    srt_status s = srt_plan_create(g, nodes, n, opts, &p, err);
+    srt_status s = plan_create_impl(g, nodes, n, opts, &p, err, true);
     tr.mark("e2e: create");
     if (s != SRT_OK) return s;
-    s = srt_plan_run(p, err);
-    tr.mark("e2e: run");
-    if (s == SRT_OK) s = srt_plan_fetch(p, out, min_latency_ns, err);
-    tr.mark("e2e: fetch");
+    // one-GPU dense build with a table wanted: the fold runs in chunks of <= 64
+    // Mi entries whose downloads overlap the next chunk's fold
+    const bool pipe = out && p->n && p->algo == SRT_ALGO_FW && !p->comm && p->emulate_ranks <= 1;
+    if (pipe)
+        p->fold_chunk_rows = (uint32_t)std::max<uint64_t>(
+            1, std::min<uint64_t>((uint64_t)p->n * p->n, 1ull << 26) / p->n);
+    s = run_closure(p, err);
+    tr.mark("e2e: closure enqueued");
+    if (s == SRT_OK) s = run_tail(p, err);  // the deferred loss upload overlaps the closure
+    tr.mark("e2e: loss upload + tail enqueued");
+    if (s == SRT_OK && pipe) {
+        s = fetch_pipelined(p, out, min_latency_ns, err);
+    } else if (s == SRT_OK) {
+        s = srt_plan_sync(p, err);
+        if (s == SRT_OK) s = srt_plan_fetch(p, out, min_latency_ns, err);
+    }
+    tr.mark("e2e: build + fetch");
     srt_plan_destroy(p);
     tr.mark("e2e: destroy");
     return s;

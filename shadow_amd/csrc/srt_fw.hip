@@ -1643,9 +1643,9 @@ srt_status fw_rounds(srt_plan *p, srt_err *err) {
     return p->key_type == KEY_F64 ? fw_rounds_t<double>(p, err) : fw_rounds_t<uint64_t>(p, err);
 }
 
-void pack_paths(srt_plan *p, uint64_t first, uint64_t count) {
-    hipLaunchKernelGGL(pack_kernel, dim3(4096), dim3(256), 0, p->stream, p->d_out_lat + first,
-                       p->d_out_loss + first, p->d_pack, count);
+void pack_paths(srt_plan *p, uint64_t first, uint64_t count, srt_path *dst, hipStream_t s) {
+    hipLaunchKernelGGL(pack_kernel, dim3(4096), dim3(256), 0, s, p->d_out_lat + first, p->d_out_loss + first, dst,
+                       count);
 }
 
 }  // namespace srt

@@ -83,7 +83,13 @@ struct srt_plan {
     uint32_t fw_ablate = 0;       // measurement only: u32 rest-kernel ablations (SRT_FW_ABLATE, see the kernel)
     bool fw_band = true;          // grouped launches: banded tile order (knob SRT_FW_BAND=0, read at create)
     uint32_t emulate_ranks = 0;   // measurement only, see fw_rounds_t
-    bool emu_closed = false;      // emulation: D holds the closure (first run done)
+    bool emu_closed = false;
+    // end-to-end build (srt_compute_shortest_paths): the loss array is uploaded
+    // while the closure runs, and the fold runs in chunks of fold_chunk_rows
+    // table rows (ev_fold after each) so their download overlaps the next
+    const float *h_loss_defer = nullptr;
+    uint32_t fold_chunk_rows = 0;
+    std::vector<hipEvent_t> ev_fold;      // emulation: D holds the closure (first run done)
     uint64_t emu_tight = 0, emu_maxw = 0;  // emulation: tight edges / max latency of the closure
     std::string desc;
     bool identity_nodes = false;
@@ -211,7 +217,7 @@ srt_status fw_loss(srt_plan *p, unsigned long long *d_stats, srt_err *err);
 // sharded tail: every rank's staged rows (d_slat / d_sloss, all-gathered) into the table
 void expand_shard_rows(srt_plan *p, int nranks);
 // table entries [first, first + count) -> d_pack[0, count) as srt_path
-void pack_paths(srt_plan *p, uint64_t first, uint64_t count);
+void pack_paths(srt_plan *p, uint64_t first, uint64_t count, srt_path *dst, hipStream_t s);
 // kernels (srt_sssp.hip)
 srt_status sssp_run(srt_plan *p, unsigned long long *d_stats, srt_err *err);
 void reduce_rank_stats(srt_plan *p, int nranks);

@@ -637,13 +637,15 @@ int bits_of(uint64_t x) {
 struct RowJob {
     const uint32_t *list = nullptr;  // device, count entries
     uint32_t count = 0;
+    bool range = false;              // no list: table rows [r0, r1) instead of [row0, row1)
+    uint32_t r0 = 0, r1 = 0;
     uint32_t *out32 = nullptr;
     float *out32_loss = nullptr;
 };
 
 template <typename LatT, bool LROWS, int LPT, bool PACKED>
 srt_status launch_fold(srt_plan *p, unsigned long long *d_stats, uint32_t ubits, const RowJob &job, srt_err *err) {
-    const uint32_t V = p->V, rows = job.list ? job.count : p->row1 - p->row0;
+    const uint32_t V = p->V, rows = job.list ? job.count : job.range ? job.r1 - job.r0 : p->row1 - p->row0;
     const uint32_t nt = V >= 2048 ? LOSS_NT : 256;
     const size_t lds = LROWS ? HIST_BYTES + (((size_t)V * sizeof(LatT) + 15) & ~(size_t)15) + (size_t)V * 4
                              : HIST_BYTES;
@@ -672,7 +674,8 @@ srt_status launch_fold(srt_plan *p, unsigned long long *d_stats, uint32_t ubits,
     }
     if (rows)
         hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, p->stream, (const void *)p->d_D, p->key_type, p->Vp, V,
-                           p->d_nodes, p->n, job.list ? 0u : p->row0, job.list ? job.count : p->row1, p->d_tptr, p->d_tu,
+                           p->d_nodes, p->n, job.list ? 0u : job.range ? job.r0 : p->row0,
+                           job.list ? job.count : job.range ? job.r1 : p->row1, p->d_tptr, p->d_tu,
                            reinterpret_cast<const LatT *>(p->d_tw), p->d_teb, p->d_tpk, ubits, p->kp.g, p->d_sl_lat,
                            p->d_sl_loss, p->d_out_lat, p->d_out_loss, d_stats, ord, lat_all, loss_all, p->d_row_ptr,
                            p->d_col, p->d_lat, p->d_loss, job.list, job.out32, job.out32_loss, std::getenv("SRT_LOSS_DIAG") ? (uint32_t)std::atoi(std::getenv("SRT_LOSS_DIAG")) : 0u);
@@ -1101,7 +1104,26 @@ srt_status fw_loss(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     if (st != SRT_OK) return st;
     p->emu_tight = p->t_edges;
     p->emu_maxw = p->h_tcount[1];
-    if ((st = fold(p, d_stats, RowJob{}, err)) != SRT_OK) return st;
+    if (p->fold_chunk_rows) {
+        // chunks of table rows, each followed by its event (the end-to-end
+        // download of chunk c overlaps the fold of chunk c + 1)
+        const uint32_t cr = p->fold_chunk_rows, nc = (p->row1 - p->row0 + cr - 1) / cr;
+        while (p->ev_fold.size() < nc) {
+            hipEvent_t e;
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(err, hipErrorUnknown, "event");
+            p->ev_fold.push_back(e);
+        }
+        for (uint32_t c = 0; c < nc; ++c) {
+            RowJob job;
+            job.range = true;
+            job.r0 = p->row0 + c * cr;
+            job.r1 = std::min(p->row1, job.r0 + cr);
+            if ((st = fold(p, d_stats, job, err)) != SRT_OK) return st;
+            (void)hipEventRecord(p->ev_fold[c], p->stream);
+        }
+    } else if ((st = fold(p, d_stats, RowJob{}, err)) != SRT_OK) {
+        return st;
+    }
     (void)hipEventRecord(p->ev_loss1, p->stream);
     return SRT_OK;
 }
