@@ -1281,15 +1281,16 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
     if (!sharded && !emu && p->fw_glds && (!p->fw_small_chain || std::getenv("SRT_FW_PAIR")) && grp > 1 &&
         grp <= 8 && nblk % grp == 0 && nblk >= 2 * grp)
         return fw_rounds_group_t<K>(p, p1r, grp);
-    // sharded: groups of 2 when every rank's block-rows split into whole
-    // groups (one owner per group) and there are >= 2 groups.  Emulated 8
-    // ranks, C3 (16k): 37.3 / 36.7 / 39.6 ms for g = 1 / 2 / 4 -- at g = 4 the
-    // chain (X(b) 257 us + 4 x (p1, p2row, p2col, cross)) outlasts F(a) 810 us
-    // (knob SRT_FW_SHARD_GROUP=0 / 2 / 4 for A/B timing)
+    // sharded: groups of 2 when a rank holds >= 32 block-rows (rest-bound)
+    // that split into whole groups (one owner per group) and there are >= 2
+    // groups.  Emulated C3 (16k, u16 keys), g = 1 / 2 / 4: 2 ranks 82.7 / 80.6
+    // / 82.6 ms, 4 ranks 47.8 / 45.7 / 50.2, 8 ranks 33.4 / 35.8 / 39.8 -- at 16
+    // block-rows a rank the chain (X(b) + g x (p1, p2row, p2col, cross))
+    // outlasts F(a) (knob SRT_FW_SHARD_GROUP=0 / 2 / 4 for A/B timing)
     {
-        uint32_t sg = 2;
-        if (const char *e = std::getenv("SRT_FW_SHARD_GROUP")) sg = (uint32_t)std::atoi(e);
         const uint32_t per_local = emu ? std::max<uint32_t>(1, nblk / emu) : per_rank;
+        uint32_t sg = per_local >= 32 ? 2 : 0;
+        if (const char *e = std::getenv("SRT_FW_SHARD_GROUP")) sg = (uint32_t)std::atoi(e);
         if ((sharded || emu) && p->fw_glds && sg > 1 && sg <= 8 && per_local % sg == 0 && nblk % sg == 0 &&
             nblk >= 2 * sg)
             return fw_rounds_group_sharded_t<K>(p, p1r, sg, rb0, rb1, emu != 0, emu_bcast_ticks, err);
