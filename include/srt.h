@@ -154,7 +154,9 @@ typedef struct {
     uint32_t sharded_tail;      /* dense, comm bound: 1 = the loss pass ran on this rank's own
                                    closure rows (no key all-gather; tight-edge lists and
                                    u32 + f32 table rows exchanged), 0 = replicated */
-    uint32_t reserved;
+    uint32_t sparse_split;      /* sparse: 1 = the split sweep's table (u16 latency sweep, then the
+                                   loss sweep over tight edges), 0 = the fused u64 sweep (the split
+                                   one saturated or is turned off) */
 } srt_timing;
 srt_status srt_plan_timing(const srt_plan *plan, srt_timing *out);
 /* C tiles (128 x 128 keys) the last FW run's dominant launches loaded and

@@ -604,6 +604,10 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         PLAN_TRY(dmalloc(&p->d_sD, (size_t)p->sssp_nb * p->V * 64, err));
         PLAN_TRY(dmalloc(&p->d_smask, (size_t)2 * p->sssp_nb * p->V, err));
         PLAN_TRY(dmalloc(&p->d_sflag, (size_t)3 * p->sssp_nb, err));
+        if (const char *ev = std::getenv("SRT_SSSP_SPLIT")) p->sssp_split = std::atoi(ev) != 0;
+        if (const char *ev = std::getenv("SRT_SSSP_LOSS_ACT")) p->sssp_loss_act = std::atoi(ev) != 0;
+        if (const char *ev = std::getenv("SRT_SSSP_TB")) p->sssp_tb = std::atoi(ev) != 0;
+        if (const char *ev = std::getenv("SRT_SSSP_ALT")) p->sssp_alt = std::atoi(ev) != 0;
         if (const char *ev = std::getenv("SRT_SSSP_ACT")) {
             const int k = std::atoi(ev);
             p->sssp_act_on = k != 0;
@@ -810,7 +814,7 @@ srt_status srt_plan_timing(const srt_plan *p, srt_timing *o) {
     o->loss_ms = p->loss_ms;
     o->tight_edges = p->algo == SRT_ALGO_FW ? p->t_edges : 0;
     o->sharded_tail = p->algo == SRT_ALGO_FW && p->shard_tail ? 1u : 0u;
-    o->reserved = 0;
+    o->sparse_split = p->algo == SRT_ALGO_SSSP && p->sssp_used_split ? 1u : 0u;
     return SRT_OK;
 }
 

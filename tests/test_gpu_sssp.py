@@ -17,6 +17,18 @@ pytestmark = pytest.mark.gpu
 SSSP = _lib.SRT_ALGO_SSSP
 
 
+@pytest.fixture(autouse=True, params=["split", "fused"])
+def sweep_mode(request, monkeypatch):
+    """Every test runs both sparse sweeps: the fused u64 sweep (the default,
+    and the split sweep's fallback) and the split one (SRT_SSSP_SPLIT=1: u16
+    latency sweep, then the loss sweep over tight edges)."""
+    if request.param == "fused":
+        monkeypatch.delenv("SRT_SSSP_SPLIT", raising=False)
+    else:
+        monkeypatch.setenv("SRT_SSSP_SPLIT", "1")
+    return request.param
+
+
 def _bits(a):
     return np.ascontiguousarray(a, np.float32).view(np.uint32)
 
@@ -169,3 +181,29 @@ def test_target_activation_bit_exact(monkeypatch, act, directed):
         edges = synth.barabasi_albert(n, 3, 12)
     nodes = np.arange(0, n, 2, dtype=np.uint32)
     _check(edges, nodes, directed, n)
+
+
+def test_split_saturation_falls_back(sweep_mode):
+    """Path latencies past the split sweep's u16 range (a 90-node ring of
+    1,000-2,000 ns edges, gcd 1: the far side is ~67k units away) saturate it;
+    the rows are rebuilt by the fused u64 sweep, bit-exact."""
+    n = 90
+    rng = np.random.default_rng(5)
+    src = np.concatenate([np.arange(n), np.arange(n)]).astype(np.uint32)
+    dst = np.concatenate([np.arange(n), (np.arange(n) + 1) % n]).astype(np.uint32)
+    lat = rng.integers(1000, 2000, 2 * n).astype(np.uint64) | np.uint64(1)
+    loss = rng.uniform(0, 0.05, 2 * n).astype(np.float32)
+    nodes = np.arange(n, dtype=np.uint32)
+    _check((src, dst, lat, loss), nodes, False, n)
+    g = NetworkGraph.from_edges(n, src, dst, lat, loss, directed=False)
+    plan = RoutingPlan(g, nodes, algo=SSSP).run()
+    assert plan.timing()["sparse_split"] == 0
+    plan.close()
+
+
+def test_split_sweep_is_used(sweep_mode):
+    src, dst, lat, loss = synth.barabasi_albert(3000, 4, 4)
+    g = NetworkGraph.from_edges(3000, src, dst, lat, loss)
+    plan = RoutingPlan(g, np.arange(300, dtype=np.uint32), algo=SSSP).run()
+    assert plan.timing()["sparse_split"] == (1 if sweep_mode == "split" else 0)
+    plan.close()
