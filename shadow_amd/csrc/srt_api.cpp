@@ -539,6 +539,7 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         }
         if (const char *e = std::getenv("SRT_FW_BAND")) p->fw_band = e[0] != '0';
         if (const char *e = std::getenv("SRT_FW_RELAX")) p->fw_relax = std::atoi(e);
+        if (const char *e = std::getenv("SRT_LOSS_PUSH")) p->loss_push = std::atoi(e) != 0;
         if (const char *e = std::getenv("SRT_FW_ABLATE")) p->fw_ablate = (uint32_t)std::atoi(e) & 15u;
         std::snprintf(d, sizeof d, "fw:%s B=%d g=%llu lmax=%llu V=%u n=%u stage=%s band=%d loss=tight-dag%s",
                       p->key_type == srt::KEY_U16   ? "u16key"

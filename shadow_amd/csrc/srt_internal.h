@@ -176,6 +176,8 @@ struct srt_plan {
     uint64_t *d_tmaxw = nullptr;     // max latency (units) of a tight edge
     uint64_t t_cap = 0, t_edges = 0; // capacity / tight edges of the last run
     bool t_packed = false;           // the last run used the packed, w-sorted form
+    bool loss_push = true;           // fold in push form over tight OUT-edges (knob SRT_LOSS_PUSH=0: pull)
+    bool t_push = false;             // the last run's CSR is the push form (rows by source)
     uint64_t *h_tcount = nullptr;    // pinned: [0] total tight edges, [1] max tight latency
     void *d_lscratch = nullptr;      // per workgroup: order array (+ rows if not in LDS)
     size_t lscratch_cap = 0;

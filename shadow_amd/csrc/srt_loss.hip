@@ -175,23 +175,28 @@ __global__ void tight_list_kernel(uint32_t u0, uint32_t u1, const uint64_t *__re
     }
 }
 
-// Sharded tail: per-target counts of the all-gathered list (v = ~0: padding)
+// Per-row counts of a tight-edge list (v = ~0: padding): rows by target v
+// (pull CSR) or, BY_SRC, by source u (push CSR)
+template <bool BY_SRC>
 __global__ void tight_list_count_kernel(const uint4 *__restrict__ list, uint64_t slots, uint32_t *__restrict__ cnt) {
     for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < slots; e += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t v = list[e].x;
-        if (v != ~0u) atomicAdd(&cnt[v], 1u);
+        const uint4 r = list[e];
+        if (r.x != ~0u) atomicAdd(&cnt[BY_SRC ? r.y : r.x], 1u);
     }
 }
 
-// ... and the packed pull CSR entries of the list
+// ... and the packed CSR entries of the list: (1-e) bits << 32 | w << ubits |
+// the other endpoint (u for pull rows, v for push rows)
+template <bool BY_SRC>
 __global__ void tight_list_fill_kernel(const uint4 *__restrict__ list, uint64_t slots,
                                        const uint64_t *__restrict__ ptr, uint32_t *__restrict__ cur,
                                        uint64_t *__restrict__ tpk, uint32_t ubits) {
     for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < slots; e += (uint64_t)gridDim.x * blockDim.x) {
         const uint4 r = list[e];
         if (r.x == ~0u) continue;
-        const uint64_t pos = ptr[r.x] + atomicAdd(&cur[r.x], 1u);
-        tpk[pos] = ((uint64_t)r.w << 32) | ((r.z << ubits) | r.y);
+        const uint32_t row = BY_SRC ? r.y : r.x, other = BY_SRC ? r.x : r.y;
+        const uint64_t pos = ptr[row] + atomicAdd(&cur[row], 1u);
+        tpk[pos] = ((uint64_t)r.w << 32) | ((r.z << ubits) | other);
     }
 }
 
@@ -360,7 +365,61 @@ __device__ __forceinline__ int scan_bucket_packed(const uint4 *__restrict__ ord,
     return changed;
 }
 
-template <typename LatT, bool LROWS, int LPT, bool PACKED>
+// Push form (the default when the tight out-edge CSR is built): ord's members
+// are the sources u of the bucket, record {u, first tight out-edge, end, lim}
+// with lim = max latency of the row + 1 - lat(u); u's final loss goes along
+// each out-edge u -> v with w < lim (no target of the row is further away)
+// where lat(v) == lat(u) + w, by LDS atomic min on prow[v].  Against the pull
+// form's per-target bound (w < lat(v)) the row-wide bound scans far fewer
+// edges on the dense configs (C3: a vertex two units away pushes only its
+// one-unit edges).
+template <typename LatT, int LPT, int UNR, bool ITER>
+__device__ __forceinline__ int scan_bucket_push(const uint4 *__restrict__ ord, uint32_t m0, uint32_t m1,
+                                                uint32_t grp, uint32_t sub, uint32_t ngrp,
+                                                const uint64_t *__restrict__ tpk, const LatT *lrow, float *prow,
+                                                uint32_t ubits, uint32_t umask, LatT maxp1) {
+    int changed = 0;
+    uint32_t m = m0 + grp;
+    uint4 rec = m < m1 ? ord[m] : make_uint4(0, 0, 0, 0);
+    for (; m < m1; m += ngrp) {
+        const uint4 cur = rec;
+        if (m + ngrp < m1) rec = ord[m + ngrp];
+        const uint32_t e1 = cur.z;
+        const LatT lim = (LatT)cur.w, lu = maxp1 - lim;
+        const float onem = 1.0f - prow[cur.x];
+        const uint64_t *wp = tpk + cur.y + sub;
+        for (uint32_t e = cur.y + sub; e < e1; e += UNR * LPT, wp += UNR * LPT) {
+            uint64_t wd[UNR];
+#pragma unroll
+            for (int q = 0; q < UNR; ++q) wd[q] = wp[q * LPT];
+            bool ok[UNR];
+            uint32_t v[UNR];
+            LatT want[UNR], lv[UNR];
+#pragma unroll
+            for (int q = 0; q < UNR; ++q) {
+                const uint32_t lo = (uint32_t)wd[q], w = lo >> ubits;
+                ok[q] = e + q * LPT < e1 && (LatT)w < lim;
+                v[q] = ok[q] ? lo & umask : 0u;
+                want[q] = lu + (LatT)w;
+            }
+#pragma unroll
+            for (int q = 0; q < UNR; ++q) lv[q] = lrow[v[q]];
+#pragma unroll
+            for (int q = 0; q < UNR; ++q) {
+                if (ok[q] && lv[q] == want[q]) {
+                    const float c = 1.0f - __fmul_rn(onem, __uint_as_float((uint32_t)(wd[q] >> 32)));
+                    uint32_t *dst = reinterpret_cast<uint32_t *>(prow) + v[q];
+                    if constexpr (ITER) changed |= __float_as_uint(c) < atomicMin(dst, __float_as_uint(c));
+                    else atomicMin(dst, __float_as_uint(c));
+                }
+            }
+            if (!ok[UNR - 1]) break;
+        }
+    }
+    return changed;
+}
+
+template <typename LatT, bool LROWS, int LPT, bool PACKED, bool PUSH>
 __global__ __launch_bounds__(LOSS_NT) void tight_loss_kernel(
     const void *__restrict__ D, int key_type, uint32_t Vp, uint32_t V, const uint32_t *__restrict__ nodes,
     uint32_t n, uint32_t row0, uint32_t row1, const uint64_t *__restrict__ tptr, const uint32_t *__restrict__ tu,
@@ -439,14 +498,27 @@ __global__ __launch_bounds__(LOSS_NT) void tight_loss_kernel(
         if (tid == 0) prow[s] = 0.0f;  // petgraph's zero score (0 ns, 0.0)
         __syncthreads();
         // the one-hop tight paths: s's own edges s -> v with lat == lat[s][v]
-        // (fold(0, e) = 1 - (1 - 0) (1 - e)); the bucket scans then skip
-        // every in-edge with w == lat[s][v], whose tail can only be s
-        for (uint64_t k = row_ptr[s] + tid; k < row_ptr[s + 1]; k += nt) {
-            const uint32_t v = col[k];
-            const LatT l = lrow[v];
-            if (v != s && l != LINF && (uint64_t)l * g == elat[k]) {
-                const float c = 1.0f - __fmul_rn(1.0f - 0.0f, 1.0f - eloss[k]);
-                atomicMin(reinterpret_cast<uint32_t *>(prow) + v, __float_as_uint(c));
+        // (fold(0, e) = 1 - (1 - 0) (1 - e)); the pull scans then skip every
+        // in-edge with w == lat[s][v], whose tail can only be s.  Push: s's
+        // tight out-edges (w <= the row's max latency), else its adjacency row.
+        if constexpr (PUSH) {
+            const uint64_t p0 = tptr[s], p1 = tptr[s + 1];
+            for (uint64_t k = p0 + tid; k < p1; k += nt) {
+                const uint64_t wd = tpk[k];
+                const uint32_t lo = (uint32_t)wd, w = lo >> ubits, v = lo & umask;
+                if ((uint64_t)w <= mx && lrow[v] == (LatT)w) {
+                    const float c = 1.0f - __fmul_rn(1.0f - 0.0f, __uint_as_float((uint32_t)(wd >> 32)));
+                    atomicMin(reinterpret_cast<uint32_t *>(prow) + v, __float_as_uint(c));
+                }
+            }
+        } else {
+            for (uint64_t k = row_ptr[s] + tid; k < row_ptr[s + 1]; k += nt) {
+                const uint32_t v = col[k];
+                const LatT l = lrow[v];
+                if (v != s && l != LINF && (uint64_t)l * g == elat[k]) {
+                    const float c = 1.0f - __fmul_rn(1.0f - 0.0f, 1.0f - eloss[k]);
+                    atomicMin(reinterpret_cast<uint32_t *>(prow) + v, __float_as_uint(c));
+                }
             }
         }
         {  // exclusive scan of hist[0, NBK): each thread a contiguous run
@@ -479,7 +551,9 @@ __global__ __launch_bounds__(LOSS_NT) void tight_loss_kernel(
             uint32_t pos = 0;
             if (few) pos = agg_inc(hist, b, ok);
             else if (ok) pos = atomicAdd(&hist[b], 1u);
-            if (ok) ord[pos] = make_uint4(v, (uint32_t)tptr[v], (uint32_t)tptr[v + 1], (uint32_t)l);
+            if (ok)
+                ord[pos] = make_uint4(v, (uint32_t)tptr[v], (uint32_t)tptr[v + 1],
+                                      PUSH ? (uint32_t)(mx + 1 - (uint64_t)l) : (uint32_t)l);
         }
         __syncthreads();
         // hist[b] is now the end of bucket b (its start: hist[b-1], or 0)
@@ -489,7 +563,14 @@ __global__ __launch_bounds__(LOSS_NT) void tight_loss_kernel(
             if (m0 == m1) continue;  // uniform
             for (;;) {
                 int changed = 0;
-                if constexpr (PACKED) {
+                if constexpr (PUSH) {
+                    if (shift)
+                        changed = scan_bucket_push<LatT, LPT, 8, true>(ord, m0, m1, grp, sub, ngrp, tpk, lrow, prow,
+                                                                    ubits, umask, (LatT)(mx + 1));
+                    else
+                        scan_bucket_push<LatT, LPT, 8, false>(ord, m0, m1, grp, sub, ngrp, tpk, lrow, prow, ubits,
+                                                           umask, (LatT)(mx + 1));
+                } else if constexpr (PACKED) {
                     if (shift)
                         changed = scan_bucket_packed<LatT, LPT, 8, true>(ord, m0, m1, grp, sub, ngrp, tpk, lrow, prow,
                                                                       ubits, umask);
@@ -643,7 +724,7 @@ struct RowJob {
     float *out32_loss = nullptr;
 };
 
-template <typename LatT, bool LROWS, int LPT, bool PACKED>
+template <typename LatT, bool LROWS, int LPT, bool PACKED, bool PUSH>
 srt_status launch_fold(srt_plan *p, unsigned long long *d_stats, uint32_t ubits, const RowJob &job, srt_err *err) {
     const uint32_t V = p->V, rows = job.list ? job.count : job.range ? job.r1 - job.r0 : p->row1 - p->row0;
     const uint32_t nt = V >= 2048 ? LOSS_NT : 256;
@@ -665,7 +746,7 @@ srt_status launch_fold(srt_plan *p, unsigned long long *d_stats, uint32_t ubits,
     uint4 *ord = reinterpret_cast<uint4 *>(base);
     LatT *lat_all = reinterpret_cast<LatT *>(base + ord_b);
     float *loss_all = reinterpret_cast<float *>(base + ord_b + lat_b);
-    auto kern = tight_loss_kernel<LatT, LROWS, LPT, PACKED>;
+    auto kern = tight_loss_kernel<LatT, LROWS, LPT, PACKED, PUSH>;
     static bool lds_attr_set = false;  // per instantiation
     if (LROWS && !lds_attr_set) {
         (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -689,17 +770,21 @@ srt_status launch_fold_lpt(srt_plan *p, unsigned long long *d_stats, uint32_t ub
     // in-edges 2-4 per lane per step)
     const double avg = p->V ? (double)p->t_edges / p->V : 0.0;
     if constexpr (PACKED) {
+        if (p->t_push) {
+            if (avg > 10.0) return launch_fold<LatT, LROWS, 4, true, true>(p, d_stats, ubits, job, err);
+            return launch_fold<LatT, LROWS, 2, true, true>(p, d_stats, ubits, job, err);
+        }
         // 4 lanes x 8 edges per target (C3, same box: 4 / 8 / 16 lanes ->
         // 31.9 / 33.0 / 36.5 ms for the pass; knob SRT_LOSS_LPT = 8 / 16)
         const char *k = std::getenv("SRT_LOSS_LPT");
-        if (k && std::atoi(k) == 8) return launch_fold<LatT, LROWS, 8, PACKED>(p, d_stats, ubits, job, err);
-        if (k && std::atoi(k) == 16) return launch_fold<LatT, LROWS, 16, PACKED>(p, d_stats, ubits, job, err);
-        if (avg > 10.0) return launch_fold<LatT, LROWS, 4, PACKED>(p, d_stats, ubits, job, err);
-        return launch_fold<LatT, LROWS, 2, PACKED>(p, d_stats, ubits, job, err);
+        if (k && std::atoi(k) == 8) return launch_fold<LatT, LROWS, 8, PACKED, false>(p, d_stats, ubits, job, err);
+        if (k && std::atoi(k) == 16) return launch_fold<LatT, LROWS, 16, PACKED, false>(p, d_stats, ubits, job, err);
+        if (avg > 10.0) return launch_fold<LatT, LROWS, 4, PACKED, false>(p, d_stats, ubits, job, err);
+        return launch_fold<LatT, LROWS, 2, PACKED, false>(p, d_stats, ubits, job, err);
     }
-    if (avg > 48.0) return launch_fold<LatT, LROWS, 32, PACKED>(p, d_stats, ubits, job, err);
-    if (avg > 10.0) return launch_fold<LatT, LROWS, 8, PACKED>(p, d_stats, ubits, job, err);
-    return launch_fold<LatT, LROWS, 2, PACKED>(p, d_stats, ubits, job, err);
+    if (avg > 48.0) return launch_fold<LatT, LROWS, 32, PACKED, false>(p, d_stats, ubits, job, err);
+    if (avg > 10.0) return launch_fold<LatT, LROWS, 8, PACKED, false>(p, d_stats, ubits, job, err);
+    return launch_fold<LatT, LROWS, 2, PACKED, false>(p, d_stats, ubits, job, err);
 }
 
 // tight edge arrays for p->t_edges entries (grown together, 25% headroom;
@@ -752,6 +837,59 @@ srt_status sort_packed(srt_plan *p, uint32_t ubits, uint64_t maxw, srt_err *err)
     return SRT_OK;
 }
 
+// Push-form tight CSR on one GPU: the flagged adjacency entries compacted
+// per source row (tight_list_kernel), then rows by source u, packed with v and
+// sorted by w.  *done = false: not packable, the caller builds the pull form.
+template <typename K>
+srt_status tight_csr_push_t(srt_plan *p, unsigned long long *d_stats, bool *done, srt_err *err) {
+    hipStream_t M = p->stream;
+    const uint32_t V = p->V;
+    *done = false;
+    srt_status st;
+    uint64_t cap_info = p->d_tinfo ? 2 : 0, cap_cur = p->d_tcursor ? 1 : 0;
+    if ((st = grow(&p->d_tinfo, &cap_info, 2, err, "hipMalloc(tight info)")) != SRT_OK ||
+        (st = grow(&p->d_tcursor, &cap_cur, 1, err, "hipMalloc(tight cursor)")) != SRT_OK)
+        return st;
+    hipLaunchKernelGGL(loss_stats_init_kernel, dim3(1), dim3(1), 0, M, d_stats, (unsigned long long *)p->d_tmaxw);
+    (void)hipMemsetAsync(p->d_tinfo, 0, 2 * sizeof(unsigned long long), M);
+    (void)hipMemsetAsync(p->d_tcursor, 0, sizeof(unsigned long long), M);
+    const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(8192, (V + 3) / 4));
+    hipLaunchKernelGGL(tight_flag_kernel<K>, dim3(blocks), dim3(256), 0, M, reinterpret_cast<const K *>(p->d_D),
+                       p->Vp, 0u, V, p->d_row_ptr, p->d_col, p->d_lat, p->kp.g, p->d_tflag, (uint32_t *)nullptr,
+                       (unsigned long long *)p->d_tmaxw, p->d_tinfo);
+    (void)hipMemcpyAsync(p->h_tcount, p->d_tinfo, sizeof(uint64_t), hipMemcpyDeviceToHost, M);
+    (void)hipMemcpyAsync(p->h_tcount + 1, p->d_tmaxw, sizeof(uint64_t), hipMemcpyDeviceToHost, M);
+    hipError_t e = hipStreamSynchronize(M);
+    if (e != hipSuccess) return fail(err, e, "tight-edge count");
+    const uint64_t total = p->h_tcount[0], maxw = p->h_tcount[1];
+    const uint32_t ubits = (uint32_t)std::max(1, bits_of(V ? V - 1 : 0));
+    if (!(p->kp.lat32 && ubits + bits_of(maxw) <= 32 && total < (1ull << 32))) return SRT_OK;
+    p->t_edges = total;
+    if ((st = ensure_edge_arrays(p, err)) != SRT_OK) return st;
+    const uint64_t C = std::max<uint64_t>(total, 1);
+    if (C > p->tlist_cap || !p->d_tlist) {
+        const uint64_t cap = C + C / 4 + 64;
+        (void)hipFree(p->d_tlist);
+        p->d_tlist = nullptr;
+        p->tlist_cap = 0;
+        if ((e = hipMalloc(&p->d_tlist, cap * sizeof(uint4))) != hipSuccess) return fail(err, e, "hipMalloc(tight list)");
+        p->tlist_cap = cap;
+    }
+    hipLaunchKernelGGL(tight_list_kernel, dim3(blocks), dim3(256), 0, M, 0u, V, p->d_row_ptr, p->d_col, p->d_lat,
+                       p->d_loss, p->kp.g, p->d_tflag, p->d_tlist, p->d_tcursor);
+    const uint32_t lblocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, (total + 255) / 256));
+    (void)hipMemsetAsync(p->d_tcnt, 0, (size_t)V * 4, M);
+    hipLaunchKernelGGL(tight_list_count_kernel<true>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, total, p->d_tcnt);
+    hipLaunchKernelGGL(tight_scan_kernel, dim3(1), dim3(1024), 0, M, p->d_tcnt, p->d_tptr, V);
+    hipLaunchKernelGGL(tight_list_fill_kernel<true>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, total, p->d_tptr,
+                       p->d_tcnt, p->d_tpk2, ubits);
+    if ((st = sort_packed(p, ubits, maxw, err)) != SRT_OK) return st;
+    p->t_packed = true;
+    p->t_push = true;
+    *done = true;
+    return SRT_OK;
+}
+
 template <typename K>
 srt_status tight_csr_t(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     hipStream_t M = p->stream;
@@ -767,6 +905,11 @@ srt_status tight_csr_t(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     if (!p->h_tcount) {
         const hipError_t e = hipHostMalloc((void **)&p->h_tcount, 2 * sizeof(uint64_t), 0);
         if (e != hipSuccess) return fail(err, e, "hipHostMalloc");
+    }
+    p->t_push = false;
+    if (p->loss_push && V && !std::getenv("SRT_LOSS_UNPACKED")) {
+        bool done = false;
+        if ((st = tight_csr_push_t<K>(p, d_stats, &done, err)) != SRT_OK || done) return st;
     }
     hipLaunchKernelGGL(loss_stats_init_kernel, dim3(1), dim3(1), 0, M, d_stats,
                        (unsigned long long *)p->d_tmaxw);
@@ -893,10 +1036,18 @@ srt_status tight_csr_shard_t(srt_plan *p, unsigned long long *d_stats, bool *sha
     const uint64_t slots = C * W;
     const uint32_t lblocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, (slots + 255) / 256));
     (void)hipMemsetAsync(p->d_tcnt, 0, (size_t)V * 4, M);
-    hipLaunchKernelGGL(tight_list_count_kernel, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tcnt);
+    if (p->loss_push)
+        hipLaunchKernelGGL(tight_list_count_kernel<true>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tcnt);
+    else
+        hipLaunchKernelGGL(tight_list_count_kernel<false>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tcnt);
     hipLaunchKernelGGL(tight_scan_kernel, dim3(1), dim3(1024), 0, M, p->d_tcnt, p->d_tptr, V);
-    hipLaunchKernelGGL(tight_list_fill_kernel, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tptr, p->d_tcnt,
-                       p->d_tpk2, ubits);
+    if (p->loss_push)
+        hipLaunchKernelGGL(tight_list_fill_kernel<true>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tptr,
+                           p->d_tcnt, p->d_tpk2, ubits);
+    else
+        hipLaunchKernelGGL(tight_list_fill_kernel<false>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tptr,
+                           p->d_tcnt, p->d_tpk2, ubits);
+    p->t_push = p->loss_push;
     if ((st = sort_packed(p, ubits, maxw, err)) != SRT_OK) return st;
     *sharded = true;
     return SRT_OK;
@@ -1024,10 +1175,18 @@ srt_status loss_emulated_t(srt_plan *p, unsigned long long *d_stats, srt_err *er
     if ((st = ensure_edge_arrays(p, err)) != SRT_OK) return st;
     const uint32_t lblocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, (slots + 255) / 256));
     (void)hipMemsetAsync(p->d_tcnt, 0, (size_t)V * 4, M);
-    hipLaunchKernelGGL(tight_list_count_kernel, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tcnt);
+    if (p->loss_push)
+        hipLaunchKernelGGL(tight_list_count_kernel<true>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tcnt);
+    else
+        hipLaunchKernelGGL(tight_list_count_kernel<false>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tcnt);
     hipLaunchKernelGGL(tight_scan_kernel, dim3(1), dim3(1024), 0, M, p->d_tcnt, p->d_tptr, V);
-    hipLaunchKernelGGL(tight_list_fill_kernel, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tptr, p->d_tcnt,
-                       p->d_tpk2, ubits);
+    if (p->loss_push)
+        hipLaunchKernelGGL(tight_list_fill_kernel<true>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tptr,
+                           p->d_tcnt, p->d_tpk2, ubits);
+    else
+        hipLaunchKernelGGL(tight_list_fill_kernel<false>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tptr,
+                           p->d_tcnt, p->d_tpk2, ubits);
+    p->t_push = p->loss_push;
     if ((st = sort_packed(p, ubits, maxw, err)) != SRT_OK) return st;
     const size_t chunk = (size_t)p->lrow_max * p->n;
     if (!p->d_slat) {
