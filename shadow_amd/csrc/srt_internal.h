@@ -198,7 +198,9 @@ struct srt_plan {
     std::vector<hipEvent_t> ev_tail;       // per chunk: fold done (M -> C), then all-gather done
     uint32_t *d_lrows = nullptr;           // slot (c * nranks + r) * tail_cr + k: rank r's row
                                            // c * tail_cr + k (~0: padding)
-    uint32_t *d_slat = nullptr;            // nranks * lrow_max * n: latency units (~0: unreachable)
+    uint32_t *d_slat = nullptr;            // nranks * lrow_max * n: latency units (~0: unreachable),
+                                           // u16 when stage16 (u16 keys), else u32
+    bool stage16 = false;
     float *d_sloss = nullptr;              // nranks * lrow_max * n
     uint4 *d_tlist = nullptr;              // nranks * tlist_cap tight edges {v, u, w, 1-e bits} (v = ~0: pad)
     uint64_t tlist_cap = 0;

@@ -204,18 +204,26 @@ __global__ void tight_list_fill_kernel(const uint4 *__restrict__ list, uint64_t 
 // + k holds table row lrows[s] (~0: padding) as latency units (~0:
 // unreachable) and loss.
 __global__ void expand_rows_kernel(const uint32_t *__restrict__ lrows, uint32_t slots, uint32_t n,
-                                   const uint32_t *__restrict__ slat, const float *__restrict__ sloss, uint64_t g,
-                                   uint64_t *__restrict__ out_lat, float *__restrict__ out_loss) {
+                                   const void *__restrict__ slat, bool lat16, const float *__restrict__ sloss,
+                                   uint64_t g, uint64_t *__restrict__ out_lat, float *__restrict__ out_loss) {
     for (uint32_t sl = blockIdx.x; sl < slots; sl += gridDim.x) {
         const uint32_t i = lrows[sl];
         if (i == ~0u) continue;
-        const uint32_t *sl_ = slat + (uint64_t)sl * n;
+        const uint16_t *s16 = reinterpret_cast<const uint16_t *>(slat) + (uint64_t)sl * n;
+        const uint32_t *s32 = reinterpret_cast<const uint32_t *>(slat) + (uint64_t)sl * n;
         const float *sp = sloss + (uint64_t)sl * n;
         uint64_t *ol = out_lat + (uint64_t)i * n;
         float *op = out_loss + (uint64_t)i * n;
         for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
-            const uint32_t l = sl_[j];
-            ol[j] = l == ~0u ? ~0ull : (uint64_t)l * g;
+            uint64_t l;
+            if (lat16) {
+                const uint32_t x = s16[j];
+                l = x == 0xffffu ? ~0ull : (uint64_t)x * g;
+            } else {
+                const uint32_t x = s32[j];
+                l = x == ~0u ? ~0ull : (uint64_t)x * g;
+            }
+            ol[j] = l;
             op[j] = sp[j];
         }
     }
@@ -428,7 +436,7 @@ __global__ __launch_bounds__(LOSS_NT) void tight_loss_kernel(
     uint64_t *__restrict__ out_lat, float *__restrict__ out_loss, unsigned long long *stats,
     uint4 *__restrict__ ord_all, LatT *lat_all, float *loss_all, const uint64_t *__restrict__ row_ptr,
     const uint32_t *__restrict__ col, const uint64_t *__restrict__ elat, const float *__restrict__ eloss,
-    const uint32_t *__restrict__ row_list, uint32_t *__restrict__ out32, float *__restrict__ out32_loss,
+    const uint32_t *__restrict__ row_list, void *__restrict__ out32, float *__restrict__ out32_loss, bool stage16,
     uint32_t diag) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ uint64_t red[16];
@@ -615,7 +623,10 @@ __global__ __launch_bounds__(LOSS_NT) void tight_loss_kernel(
         // 4. table row i (or staging slot k)
         uint64_t *ol = out_lat + (uint64_t)i * n;
         float *op = out_loss + (uint64_t)i * n;
-        uint32_t *o32 = out32 ? out32 + (uint64_t)k * n : nullptr;
+        // staging slot k: latency units as u16 (stage16: u16 keys, < 0x7fff)
+        // or u32, ~0 = unreachable
+        uint32_t *o32 = out32 && !stage16 ? reinterpret_cast<uint32_t *>(out32) + (uint64_t)k * n : nullptr;
+        uint16_t *o16 = out32 && stage16 ? reinterpret_cast<uint16_t *>(out32) + (uint64_t)k * n : nullptr;
         float *o32p = out32 ? out32_loss + (uint64_t)k * n : nullptr;
         for (uint32_t j = tid; j < ((diag & 2u) ? 0u : n); j += nt) {
             uint64_t latv;
@@ -635,7 +646,10 @@ __global__ __launch_bounds__(LOSS_NT) void tight_loss_kernel(
                     lossv = prow[v];
                 }
             }
-            if (o32) {
+            if (o16) {
+                o16[j] = latv == ~0ull ? (uint16_t)0xffffu : (uint16_t)(latv / g);
+                o32p[j] = lossv;
+            } else if (o32) {
                 o32[j] = latv == ~0ull ? ~0u : (uint32_t)(latv / g);
                 o32p[j] = lossv;
             } else {
@@ -720,7 +734,7 @@ struct RowJob {
     uint32_t count = 0;
     bool range = false;              // no list: table rows [r0, r1) instead of [row0, row1)
     uint32_t r0 = 0, r1 = 0;
-    uint32_t *out32 = nullptr;
+    void *out32 = nullptr;           // staging row 0 (u16 or u32 latency units, see srt_plan::stage16)
     float *out32_loss = nullptr;
 };
 
@@ -759,7 +773,7 @@ srt_status launch_fold(srt_plan *p, unsigned long long *d_stats, uint32_t ubits,
                            job.list ? job.count : job.range ? job.r1 : p->row1, p->d_tptr, p->d_tu,
                            reinterpret_cast<const LatT *>(p->d_tw), p->d_teb, p->d_tpk, ubits, p->kp.g, p->d_sl_lat,
                            p->d_sl_loss, p->d_out_lat, p->d_out_loss, d_stats, ord, lat_all, loss_all, p->d_row_ptr,
-                           p->d_col, p->d_lat, p->d_loss, job.list, job.out32, job.out32_loss, std::getenv("SRT_LOSS_DIAG") ? (uint32_t)std::atoi(std::getenv("SRT_LOSS_DIAG")) : 0u);
+                           p->d_col, p->d_lat, p->d_loss, job.list, job.out32, job.out32_loss, p->stage16, std::getenv("SRT_LOSS_DIAG") ? (uint32_t)std::atoi(std::getenv("SRT_LOSS_DIAG")) : 0u);
     return SRT_OK;
 }
 
@@ -1066,6 +1080,8 @@ srt_status loss_sharded_t(srt_plan *p, unsigned long long *d_stats, srt_err *err
     }
     const uint32_t W = (uint32_t)p->comm->nranks, r = (uint32_t)p->comm->rank;
     const size_t chunk = (size_t)p->lrow_max * p->n;
+    p->stage16 = p->key_type == KEY_U16;
+    const size_t lb = p->stage16 ? 2 : 4;  // bytes per staged latency
     if (!p->d_slat) {
         void *a = nullptr, *b = nullptr;
         hipError_t e = hipMalloc(&a, std::max<size_t>(chunk * W, 1) * 4);
@@ -1082,20 +1098,21 @@ srt_status loss_sharded_t(srt_plan *p, unsigned long long *d_stats, srt_err *err
     // one order on every rank: the chunks, then -- on M, after the last
     // chunk -- the rank stats)
     const uint32_t q = p->tail_q, cr = p->tail_cr;
-    const size_t cbytes = (size_t)cr * p->n * 4;
+    const size_t cbytes = (size_t)cr * p->n * 4, lbytes = (size_t)cr * p->n * lb;
     hipStream_t M = p->stream, C = p->comm_stream;
     for (uint32_t c = 0; c < q; ++c) {
         const size_t slot = ((size_t)c * W + r) * cr;
         RowJob job;
         job.list = p->d_lrows + slot;
         job.count = p->lrow_cnt[r] > c * cr ? std::min(cr, p->lrow_cnt[r] - c * cr) : 0u;
-        job.out32 = p->d_slat + slot * p->n;
+        job.out32 = reinterpret_cast<uint8_t *>(p->d_slat) + slot * p->n * lb;
         job.out32_loss = p->d_sloss + slot * p->n;
         if ((st = fold(p, d_stats, job, err)) != SRT_OK) return st;
         (void)hipEventRecord(p->ev_tail[c], M);
         (void)hipStreamWaitEvent(C, p->ev_tail[c], 0);
         const size_t base = (size_t)c * W * cr * p->n;
-        if ((st = comm_allgather_inplace(p->comm, p->d_slat + base, cbytes, C, err)) != SRT_OK ||
+        if ((st = comm_allgather_inplace(p->comm, reinterpret_cast<uint8_t *>(p->d_slat) + base * lb, lbytes, C,
+                                         err)) != SRT_OK ||
             (st = comm_allgather_inplace(p->comm, p->d_sloss + base, cbytes, C, err)) != SRT_OK)
             return st;
     }
@@ -1189,6 +1206,8 @@ srt_status loss_emulated_t(srt_plan *p, unsigned long long *d_stats, srt_err *er
     p->t_push = p->loss_push;
     if ((st = sort_packed(p, ubits, maxw, err)) != SRT_OK) return st;
     const size_t chunk = (size_t)p->lrow_max * p->n;
+    p->stage16 = p->key_type == KEY_U16;
+    const size_t lb = p->stage16 ? 2 : 4;  // bytes per staged latency
     if (!p->d_slat) {
         void *a = nullptr, *b = nullptr;
         e = hipMalloc(&a, std::max<size_t>(chunk * W, 1) * 4);
@@ -1207,12 +1226,12 @@ srt_status loss_emulated_t(srt_plan *p, unsigned long long *d_stats, srt_err *er
         RowJob job;
         job.list = p->d_lrows + slot;
         job.count = p->lrow_cnt[0] > c * cr ? std::min(cr, p->lrow_cnt[0] - c * cr) : 0u;
-        job.out32 = p->d_slat + slot * p->n;
+        job.out32 = reinterpret_cast<uint8_t *>(p->d_slat) + slot * p->n * lb;
         job.out32_loss = p->d_sloss + slot * p->n;
         if ((st = fold(p, d_stats, job, err)) != SRT_OK) return st;
         (void)hipEventRecord(p->ev_tail[c], M);
         (void)hipStreamWaitEvent(Cs, p->ev_tail[c], 0);
-        allgather_on((double)cr * p->n * 8.0, Cs);  // latency units + loss
+        allgather_on((double)cr * p->n * (4.0 + lb), Cs);  // latency units + loss
     }
     (void)hipEventRecord(p->ev_tail[q], Cs);
     (void)hipStreamWaitEvent(M, p->ev_tail[q], 0);
@@ -1227,7 +1246,8 @@ void expand_shard_rows(srt_plan *p, int nranks) {
     const uint32_t slots = (uint32_t)nranks * p->lrow_max;
     if (!slots || !p->n) return;
     hipLaunchKernelGGL(expand_rows_kernel, dim3(std::min<uint32_t>(slots, 4096)), dim3(256), 0, p->stream, p->d_lrows,
-                       slots, p->n, p->d_slat, p->d_sloss, p->kp.g, p->d_out_lat, p->d_out_loss);
+                       slots, p->n, (const void *)p->d_slat, p->stage16, p->d_sloss, p->kp.g, p->d_out_lat,
+                       p->d_out_loss);
 }
 
 srt_status fw_loss(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
