@@ -194,17 +194,26 @@ void csr_scan(const srt_csr *g, CsrStats *out) {
 
 // Choose the closure's key representation and prove it exact.
 //
-// Keys are path latencies in units of g = gcd of all edge latencies.  Every
-// value the closure stores is at most Lmax: for a complete graph the initial
-// matrix is finite and values only decrease, so Lmax = max edge latency; else
-// a stored value is never above the sequential Floyd-Warshall's value at the
-// same point (concurrent schedules only read tighter keys of real walks), a
-// simple path, so Lmax = (V-1) * max edge latency.  A candidate is a sum of
-// two stored values, so 2 Lmax must stay exact: below 2^53 the keys are f64
-// (v_add_f64 / v_min_f64), below 2^62 u64 -- and below KEY32_INF (2^31 - 1)
-// u32, the fastest.  Lmax < 2^32 - 1 additionally lets the loss pass keep
-// latencies as u32.  Knob SRT_FW_KEY=f64|u64 (measurement / A-B parity only)
-// skips the narrower representations.
+// Keys are path latencies in units of g = gcd of all edge latencies (latency
+// only: the loss is recomputed exactly by the loss pass, so no loss bits share
+// the key).  Lmax bounds every shortest-path latency: the longest edge for a
+// complete graph (a direct edge bounds every pair), else (V-1) * max edge.
+// Exactness does not depend on the schedule's read order: (1) every stored
+// value only decreases from its initial value <= INF, so each operand is <=
+// INF and a candidate (sum of two) is <= 2 INF, which the key type holds
+// without wrapping (u16 lanes: 0xFFFE; u32: 2^32 - 2) -- no candidate is ever
+// corrupted, whatever the grouped / look-ahead / sharded schedules read; (2) a
+// candidate below INF is the exact length of a real walk, so no stored value
+// drops below the true distance d; (3) the schedule's values are never above
+// the sequential Floyd-Warshall's (its candidates are formed from operands at
+// least as tight), which ends at d.  So the closure ends at d exactly when
+// every finite d < INF -- Lmax < INF.  The test below asks for 2 Lmax + 1 <
+// INF, a margin kept from the r01 packed (latency, loss) keys.  Below 2^53 the
+// keys may be f64 (v_add_f64 / v_min_f64), below 2^62 u64, and below
+// KEY32_INF (2^31 - 1) u32; u16 below KEY16_INF.  Lmax < 2^32 - 1
+// additionally lets the loss pass keep latencies as u32.  Knob
+// SRT_FW_KEY=u32|f64|u64 (measurement / A-B parity only) skips the narrower
+// representations.
 bool choose_key_params(const CsrStats &cs, uint32_t V, KeyParams *kp, int *key_type, std::string *why) {
     kp->g = cs.gcd;
     const uint64_t maxu = cs.maxlat / cs.gcd;
@@ -263,6 +272,7 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_in_ptr);
     hipFree(p->d_in_edge);
     hipFree(p->d_sD);
+    hipFree(p->d_scl);
     hipFree(p->d_smask);
     hipFree(p->d_sflag);
     hipFree(p->d_sact);
@@ -565,6 +575,10 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b)
             budget_mb = std::max<uint64_t>(64, std::min<uint64_t>(budget_mb, (free_b >> 20) / 8));
         if (const char *e = std::getenv("SRT_SSSP_MB")) budget_mb = (uint64_t)std::atoll(e);
+        // the sweep variants and their knobs (measurement / A-B parity only):
+        // SRT_SSSP_CL=1 the compact-list sweep, SRT_SSSP_SPLIT=1 the split sweep
+        if (const char *ev = std::getenv("SRT_SSSP_SPLIT")) p->sssp_split = std::atoi(ev) != 0;
+        if (const char *ev = std::getenv("SRT_SSSP_CL")) p->sssp_cl = std::atoi(ev) != 0;
         const uint32_t R = (rmax >= 4 && words >= 4) ? 4 : (rmax >= 2 && words >= 2) ? 2 : 1;
         const uint64_t per_group = (uint64_t)p->V * 64 * 8 * R;
         uint64_t G = std::max<uint64_t>(1, (budget_mb << 20) / std::max<uint64_t>(per_group, 1));
@@ -573,9 +587,9 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         p->sssp_r = R;
         p->sssp_nb = (uint32_t)(G * R);
         p->n_in_edges = n_in;
-        std::snprintf(d, sizeof d, "sssp:lat32|f32 g=%llu V=%u n=%u E_in=%llu R=%u groups=%u",
+        std::snprintf(d, sizeof d, "sssp:lat32|f32 g=%llu V=%u n=%u E_in=%llu R=%u groups=%u state=%s",
                       (unsigned long long)p->sssp_g, p->V, n, (unsigned long long)n_in, p->sssp_r,
-                      p->sssp_nb / p->sssp_r);
+                      p->sssp_nb / p->sssp_r, p->sssp_cl ? "planes+lists" : "keys");
     }
     p->desc = d;
     tr.mark("create: key/algo choice");
@@ -605,7 +619,6 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         PLAN_TRY(dmalloc(&p->d_sD, (size_t)p->sssp_nb * p->V * 64, err));
         PLAN_TRY(dmalloc(&p->d_smask, (size_t)2 * p->sssp_nb * p->V, err));
         PLAN_TRY(dmalloc(&p->d_sflag, (size_t)3 * p->sssp_nb, err));
-        if (const char *ev = std::getenv("SRT_SSSP_SPLIT")) p->sssp_split = std::atoi(ev) != 0;
         if (const char *ev = std::getenv("SRT_SSSP_LOSS_ACT")) p->sssp_loss_act = std::atoi(ev) != 0;
         if (const char *ev = std::getenv("SRT_SSSP_TB")) p->sssp_tb = std::atoi(ev) != 0;
         if (const char *ev = std::getenv("SRT_SSSP_ALT")) p->sssp_alt = std::atoi(ev) != 0;
@@ -614,6 +627,7 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
             p->sssp_act_on = k != 0;
             p->sssp_act_from = k > 1 ? (uint32_t)k : 0u;
         }
+        if (p->sssp_cl) PLAN_TRY(dmalloc(&p->d_scl, (size_t)2 * p->sssp_nb * p->V * 64, err));
         if (p->sssp_act_on) PLAN_TRY(dmalloc(&p->d_sact, (size_t)3 * (p->sssp_nb / p->sssp_r) * p->V, err));
         if ((e = hipHostMalloc((void **)&p->h_sflag, (size_t)p->sssp_nb * sizeof(uint32_t), 0)) != hipSuccess) {
             srt_plan_destroy(p);

@@ -213,26 +213,222 @@ __global__ __launch_bounds__(SWP_WAVES * 64) void sssp_sweep_kernel(
     }
 }
 
+// ------------------------------------------------------------ compact lists
+// The fused sweep above gathers D[u][s] for every changed lane s of u: with
+// 16 keys per 128-B line, a row whose changed lanes are scattered costs up to
+// 4 lines for a handful of keys (C4: 475k lines per source per build; a line
+// holds ~1.9 useful keys).  Here every wave that improves v also writes the
+// improved keys of each 64-source word COMPACTLY, in lane order, into a
+// parity slot CL[t+1 & 1][v][r][0..63]: key i of the slot belongs to the i-th
+// set bit of v's next change mask.  A reader of in-edge u -> v takes lane s's
+// key from slot index popcount(mask_u & lanes below s) -- the changed keys of
+// a word sit in ceil(c / 16) lines (C4, simulated: 265k lines per source).
+// The slot holds sweep t-1's values (Jacobi for the propagation; simulated:
+// the same 28 sweeps as in-place Gauss-Seidel reads).  Nobody but v's own
+// wave reads v's state any more, so it is kept as two planes -- latency u32
+// and loss f32 bits -- and the closing compare reads the loss plane only on
+// a latency tie: lexicographic (latency, loss) order, the same decisions as
+// the u64 key compare.  Layout in d_sD: Lat[b][v][lane] then Loss[b][v][lane].
+// Measured (C4, one 8,192-source launch; profiles/r02c4_*): FETCH 323 -> 220
+// GB, time unchanged (1.52 s per build): in the heavy sweeps most lanes of a
+// word have changed, so a list is as long as the row (peak-sweep FETCH only
+// -8%, and those sweeps run at the ~5.8 TB/s random-line ceiling: TCC misses
+// x 128 B), while the light sweeps are bound by each wave's chain of dependent
+// loads (SQ: 63% of wave cycles waiting on memory, VALU 27% busy).  Variants
+// that skipped idle words per edge or loaded the own latencies early, and 512
+// sources per wave, measured 5-20% slower.  Opt-in (SRT_SSSP_CL=1): it needs
+// 3x the state memory for no gain.
+template <int R>
+__global__ __launch_bounds__(SWP_WAVES * 64) void sssp_cl_sweep_kernel(
+    const uint64_t *__restrict__ in_ptr, const InEdge *__restrict__ in_edge, uint32_t V,
+    uint32_t *__restrict__ Lat, uint32_t *__restrict__ Loss, const uint64_t *__restrict__ cl_cur,
+    uint64_t *__restrict__ cl_next, const uint64_t *__restrict__ mask_cur, uint64_t *__restrict__ mask_next,
+    uint32_t *flag, uint32_t t, const uint64_t *__restrict__ row_ptr, const uint32_t *__restrict__ col,
+    uint8_t *act, uint32_t act_mode) {
+    const uint32_t g = blockIdx.y, G = gridDim.y;
+    if (blockIdx.x == 0 && threadIdx.x == 0) flag[((t + 1) % 3) * G + g] = 0;  // for sweep t+1
+    if (t > 0 && flag[((t + 2) % 3) * G + g] == 0) return;                     // converged
+    const int lane = threadIdx.x & 63;
+    const uint32_t vi = __builtin_amdgcn_readfirstlane(blockIdx.x * SWP_WAVES + (threadIdx.x >> 6));
+    if (vi >= V) return;
+    const uint32_t v = (act_mode & ACT_REV) ? V - 1 - vi : vi;
+    const uint64_t base = (uint64_t)g * V;
+    const uint64_t aslot = (uint64_t)G * V;
+    if (act_mode & (ACT_USE | ACT_SET)) {
+        if (lane == 0) act[((t + 2) % 3) * aslot + base + v] = 0;
+        if ((act_mode & ACT_USE) && act[(t % 3) * aslot + base + v] == 0) {
+            if (lane < R) mask_next[(base + v) * R + lane] = 0;
+            return;
+        }
+    }
+    const uint64_t *clg = cl_cur + base * R * 64;
+    const uint64_t *mc = mask_cur + base * R;
+    uint64_t best[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) best[r] = SKEY_INF;
+    const uint64_t e0 = in_ptr[v], e1 = in_ptr[v + 1];
+    for (uint64_t c0 = e0; c0 < e1; c0 += 64) {
+        const uint64_t k = c0 + lane;
+        uint32_t eu = 0, ew = 0;
+        float eeb = 0.f;
+        uint64_t em[R];
+        bool any = false;
+#pragma unroll
+        for (int r = 0; r < R; ++r) em[r] = 0;
+        if (k < e1) {
+            const InEdge e = in_edge[k];
+            eu = e.u;
+            ew = e.w;
+            eeb = e.eb;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                em[r] = mc[(uint64_t)eu * R + r];
+                any |= em[r] != 0;
+            }
+        }
+        uint64_t actv = __ballot(any);
+        while (actv) {
+            uint64_t du[4][R];
+            uint32_t w[4];
+            float eb[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                w[q] = 0;
+                eb[q] = 0.f;
+#pragma unroll
+                for (int r = 0; r < R; ++r) du[q][r] = SKEY_INF;
+                if (actv) {
+                    const int j = __builtin_ctzll(actv);
+                    actv &= actv - 1;
+                    const uint32_t u = __builtin_amdgcn_readlane(eu, j);
+                    w[q] = __builtin_amdgcn_readlane(ew, j);
+                    eb[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(eeb), j));
+                    const uint64_t *Cu = clg + (uint64_t)u * R * 64;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const uint32_t mlo = __builtin_amdgcn_readlane((uint32_t)em[r], j);
+                        const uint32_t mhi = __builtin_amdgcn_readlane((uint32_t)(em[r] >> 32), j);
+                        const uint32_t bit = lane < 32 ? (mlo >> lane) : (mhi >> (lane - 32));
+                        const uint32_t idx = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, 0u));
+                        if (bit & 1u) du[q][r] = Cu[r * 64 + idx];
+                    }
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if (du[q][r] != SKEY_INF) {
+                        const uint64_t c = relax(du[q][r], w[q], eb[q]);
+                        best[r] = c < best[r] ? c : best[r];
+                    }
+                }
+            }
+        }
+    }
+    const uint64_t vrow = (base + v) * R;
+    bool imp_any = false;
+    uint64_t m_out[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint64_t e = (vrow + r) * 64 + lane;
+        bool imp = false;
+        if (best[r] != SKEY_INF) {
+            // lexicographic (latency, loss) compare; the loss plane only on a tie
+            const uint32_t bl = (uint32_t)(best[r] >> 32), cl = Lat[e];
+            imp = bl < cl || (bl == cl && (uint32_t)best[r] < Loss[e]);
+            if (imp) {
+                Lat[e] = bl;
+                Loss[e] = (uint32_t)best[r];
+            }
+        }
+        m_out[r] = __ballot(imp);
+        imp_any |= m_out[r] != 0;
+        if (imp) {
+            const uint32_t idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(m_out[r] >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m_out[r], 0u));
+            cl_next[(vrow + r) * 64 + idx] = best[r];
+        }
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) mask_next[vrow + r] = m_out[r];
+        if (imp_any) flag[(t % 3) * G + g] = 1;
+    }
+    if ((act_mode & ACT_SET) && imp_any) {
+        uint8_t *nxt = act + ((t + 1) % 3) * aslot + base;
+        for (uint64_t k = row_ptr[v] + lane; k < row_ptr[v + 1]; k += 64) {
+            const uint32_t w = col[k];
+            if (w != v) nxt[w] = 1;
+        }
+    }
+}
+
+// planes + compact lists of G groups: latency INF, change masks and flags 0
+// (the loss plane is read only on a latency tie, so INF latency needs no loss)
+__global__ void sssp_cl_init_kernel(uint32_t *__restrict__ Lat, uint64_t *__restrict__ mask, uint32_t *flag,
+                                    uint32_t V, uint32_t nbat, uint32_t G) {
+    const uint64_t nD = (uint64_t)nbat * V * 64, nM = 2ull * nbat * V;
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < nD;
+         e += (uint64_t)gridDim.x * blockDim.x) {
+        Lat[e] = 0xffffffffu;
+        if (e < nM) mask[e] = 0;
+        if (e < 3ull * G) flag[e] = 0;
+    }
+}
+
+// sources: (0, 0.0) in the planes, their change bit, and the key in slot 0 of
+// the parity-0 compact list (sources within a word are distinct vertices, so
+// a seeded (vertex, word) has exactly one changed lane)
+__global__ void sssp_cl_seed_kernel(uint32_t *__restrict__ Lat, uint32_t *__restrict__ Loss,
+                                    uint64_t *__restrict__ cl0, uint64_t *__restrict__ mask,
+                                    const uint32_t *__restrict__ nodes, uint32_t V, uint32_t row0, uint32_t row1,
+                                    uint32_t nbat, uint32_t R) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nbat * 64) return;
+    const uint32_t g = q / (64 * R), r = (q / 64) % R, s = q % 64;
+    if (row0 + q >= row1) return;
+    const uint64_t row = (uint64_t)g * V + nodes[row0 + q];
+    Lat[(row * R + r) * 64 + s] = 0;
+    Loss[(row * R + r) * 64 + s] = 0;
+    cl0[(row * R + r) * 64] = 0ull;
+    mask[row * R + r] = 1ull << s;
+}
+
 // Table rows of the group: row = row0 + (g*R + r)*64 + s for lane s of word r.
 // A 64 x 64 (sources x columns) tile goes through LDS so both the gather from
 // D (64 sources of one vertex) and the row-major table stores are coalesced.
 // Diagonal = the raw self-loop (mod.rs:210-217); min latency (mod.rs:474-476)
 // and unreachable count (the assert at mod.rs:219) are block-reduced into
 // stats[0] (min) / stats[1] (count).  blockIdx.y = g*R + r.
+// PL: the state is the compact-list sweep's two planes (D = Lat, then Loss
+// nbat * V * 64 words further on), else u64 keys.
+template <bool PL>
 __global__ __launch_bounds__(256) void sssp_emit_kernel(
     const uint64_t *__restrict__ D, uint32_t V, uint32_t R, const uint32_t *__restrict__ nodes, uint32_t n,
     uint32_t row0, uint32_t row1, uint64_t gunit, const uint64_t *__restrict__ sl_lat,
     const float *__restrict__ sl_loss, uint64_t *__restrict__ out_lat, float *__restrict__ out_loss,
-    unsigned long long *stats) {
+    unsigned long long *stats, uint64_t plane_words) {
     __shared__ uint64_t tile[64][65];
     __shared__ unsigned long long red_min[4], red_cnt[4];
     const uint32_t b = blockIdx.y, g = b / R, r = b % R, j0 = blockIdx.x * 64;
     const int tid = threadIdx.x;
-    const uint64_t *Dg = D + (uint64_t)g * V * R * 64 + (uint64_t)r * 64;
+    const uint64_t off = (uint64_t)g * V * R * 64 + (uint64_t)r * 64;
+    const uint32_t *Lat = reinterpret_cast<const uint32_t *>(D), *Loss = Lat + plane_words;
     for (int idx = tid; idx < 64 * 64; idx += 256) {
         const int jj = idx / 64, s = idx % 64;
         const uint32_t j = j0 + jj;
-        tile[jj][s] = j < n ? Dg[(uint64_t)nodes[j] * R * 64 + s] : SKEY_INF;
+        uint64_t k = SKEY_INF;
+        if (j < n) {
+            const uint64_t e = off + (uint64_t)nodes[j] * R * 64 + s;
+            if (PL) {
+                const uint32_t l = Lat[e];
+                if (l != 0xffffffffu) k = ((uint64_t)l << 32) | Loss[e];
+            } else {
+                k = D[e];
+            }
+        }
+        tile[jj][s] = k;
     }
     __syncthreads();
     uint64_t mn = ~0ull;
@@ -828,6 +1024,16 @@ void launch_sweep(dim3 grid, hipStream_t s, srt_plan *p, uint64_t *mc, uint64_t 
 }
 
 template <int R>
+void launch_cl_sweep(dim3 grid, hipStream_t s, srt_plan *p, uint64_t plane_words, uint64_t *mc, uint64_t *mn,
+                     uint32_t t, uint32_t act_mode) {
+    uint32_t *Lat = reinterpret_cast<uint32_t *>(p->d_sD);
+    const uint64_t par = plane_words;  // one parity slot of the compact lists = one plane of keys
+    hipLaunchKernelGGL(sssp_cl_sweep_kernel<R>, grid, dim3(SWP_WAVES * 64), 0, s, p->d_in_ptr, p->d_in_edge, p->V,
+                       Lat, Lat + plane_words, p->d_scl + (t & 1) * par, p->d_scl + ((t + 1) & 1) * par, mc, mn,
+                       p->d_sflag, t, p->d_row_ptr, p->d_col, p->d_sact, act_mode);
+}
+
+template <int R>
 void launch_lat16(dim3 grid, hipStream_t s, srt_plan *p, uint64_t *mc, uint64_t *mn, uint32_t t, uint32_t act_mode) {
     hipLaunchKernelGGL(lat16_sweep_kernel<R>, grid, dim3(SWP_WAVES * 64), 0, s, p->d_in_ptr, p->d_in_edge, p->V,
                        reinterpret_cast<uint16_t *>(p->d_sD), mc, mn, p->d_sflag, t, p->d_row_ptr, p->d_col,
@@ -898,17 +1104,25 @@ srt_status sssp_pass(srt_plan *p, unsigned long long *d_stats, bool split, srt_e
     }
     uint16_t *L16 = reinterpret_cast<uint16_t *>(p->d_sD);
     uint32_t *LS = reinterpret_cast<uint32_t *>(L16 + (uint64_t)p->sssp_nb * V * 64);
+    const bool cl = !split && p->sssp_cl && p->d_scl;
     uint32_t chunk = 8, t_prev = 0, chunk_b = 8;
     for (uint32_t li = 0; li < launches; ++li) {
         const uint32_t g0 = p->row0 + li * per_launch;
         const uint32_t rows = std::min<uint32_t>(per_launch, p->row1 - g0);
         const uint32_t nbat = (rows + 63) / 64;           // 64-source words with work
         const uint32_t G = (nbat + R - 1) / R;            // groups in this launch
+        const uint64_t plane_words = (uint64_t)G * R * V * 64;  // compact-list layout: plane / parity slot
         if (split) {
             hipLaunchKernelGGL(split_init_kernel, dim3(4096), dim3(256), 0, M, L16, LS, p->d_smask, p->d_sflag, V,
                                G * R, G);
             hipLaunchKernelGGL(split_seed_kernel, dim3((nbat * 64 + 255) / 256), dim3(256), 0, M, L16, LS,
                                p->d_smask, p->d_nodes, V, g0, g0 + rows, nbat, R);
+        } else if (cl) {
+            uint32_t *Lat = reinterpret_cast<uint32_t *>(p->d_sD);
+            hipLaunchKernelGGL(sssp_cl_init_kernel, dim3(4096), dim3(256), 0, M, Lat, p->d_smask, p->d_sflag, V,
+                               G * R, G);
+            hipLaunchKernelGGL(sssp_cl_seed_kernel, dim3((nbat * 64 + 255) / 256), dim3(256), 0, M, Lat,
+                               Lat + plane_words, p->d_scl, p->d_smask, p->d_nodes, V, g0, g0 + rows, nbat, R);
         } else {
             hipLaunchKernelGGL(sssp_init_kernel, dim3(4096), dim3(256), 0, M, p->d_sD, p->d_smask, p->d_sflag, V,
                                G * R, G);
@@ -937,6 +1151,10 @@ srt_status sssp_pass(srt_plan *p, unsigned long long *d_stats, bool split, srt_e
                 if (R == 4) launch_lat16<4>(grid, M, p, mc, mn, tt, am);
                 else if (R == 2) launch_lat16<2>(grid, M, p, mc, mn, tt, am);
                 else launch_lat16<1>(grid, M, p, mc, mn, tt, am);
+            } else if (cl) {
+                if (R == 4) launch_cl_sweep<4>(grid, M, p, plane_words, mc, mn, tt, am);
+                else if (R == 2) launch_cl_sweep<2>(grid, M, p, plane_words, mc, mn, tt, am);
+                else launch_cl_sweep<1>(grid, M, p, plane_words, mc, mn, tt, am);
             } else {
                 if (R == 4) launch_sweep<4>(grid, M, p, mc, mn, tt, am);
                 else if (R == 2) launch_sweep<2>(grid, M, p, mc, mn, tt, am);
@@ -1005,10 +1223,14 @@ srt_status sssp_pass(srt_plan *p, unsigned long long *d_stats, bool split, srt_e
             hipLaunchKernelGGL(split_emit_kernel, dim3((p->n + 63) / 64, G * R), dim3(256), 0, M, L16, LS, V, R,
                                p->d_nodes, p->n, g0, g0 + rows, p->sssp_g, p->d_sl_lat, p->d_sl_loss, p->d_out_lat,
                                p->d_out_loss, d_stats);
+        else if (cl)
+            hipLaunchKernelGGL(sssp_emit_kernel<true>, dim3((p->n + 63) / 64, G * R), dim3(256), 0, M, p->d_sD, V,
+                               R, p->d_nodes, p->n, g0, g0 + rows, p->sssp_g, p->d_sl_lat, p->d_sl_loss,
+                               p->d_out_lat, p->d_out_loss, d_stats, plane_words);
         else
-            hipLaunchKernelGGL(sssp_emit_kernel, dim3((p->n + 63) / 64, G * R), dim3(256), 0, M, p->d_sD, V, R,
-                               p->d_nodes, p->n, g0, g0 + rows, p->sssp_g, p->d_sl_lat, p->d_sl_loss, p->d_out_lat,
-                               p->d_out_loss, d_stats);
+            hipLaunchKernelGGL(sssp_emit_kernel<false>, dim3((p->n + 63) / 64, G * R), dim3(256), 0, M, p->d_sD,
+                               V, R, p->d_nodes, p->n, g0, g0 + rows, p->sssp_g, p->d_sl_lat, p->d_sl_loss,
+                               p->d_out_lat, p->d_out_loss, d_stats, 0ull);
     }
     // algorithmic bytes: 12 B per in-edge + 12 B per vertex, per source
     p->p3_work = (double)(p->row1 - p->row0) * 12.0 * ((double)p->n_in_edges + (double)V);

@@ -17,15 +17,19 @@ pytestmark = pytest.mark.gpu
 SSSP = _lib.SRT_ALGO_SSSP
 
 
-@pytest.fixture(autouse=True, params=["split", "fused"])
+@pytest.fixture(autouse=True, params=["split", "fused", "lists"])
 def sweep_mode(request, monkeypatch):
-    """Every test runs both sparse sweeps: the fused u64 sweep (the default,
-    and the split sweep's fallback) and the split one (SRT_SSSP_SPLIT=1: u16
-    latency sweep, then the loss sweep over tight edges)."""
-    if request.param == "fused":
-        monkeypatch.delenv("SRT_SSSP_SPLIT", raising=False)
-    else:
+    """Every test runs the three sparse sweeps: the fused sweep over u64 keys
+    (the default, and the split sweep's fallback), the fused sweep with
+    latency / loss planes and compact change lists (SRT_SSSP_CL=1) and the
+    split one (SRT_SSSP_SPLIT=1: u16 latency sweep, then the loss sweep over
+    tight edges)."""
+    monkeypatch.delenv("SRT_SSSP_SPLIT", raising=False)
+    monkeypatch.delenv("SRT_SSSP_CL", raising=False)
+    if request.param == "split":
         monkeypatch.setenv("SRT_SSSP_SPLIT", "1")
+    elif request.param == "lists":
+        monkeypatch.setenv("SRT_SSSP_CL", "1")
     return request.param
 
 
@@ -206,4 +210,15 @@ def test_split_sweep_is_used(sweep_mode):
     g = NetworkGraph.from_edges(3000, src, dst, lat, loss)
     plan = RoutingPlan(g, np.arange(300, dtype=np.uint32), algo=SSSP).run()
     assert plan.timing()["sparse_split"] == (1 if sweep_mode == "split" else 0)
+    plan.close()
+
+
+def test_state_layout_is_reported(sweep_mode):
+    """The plan names the fused sweep's state layout: u64 keys by default, two
+    planes + compact change lists under SRT_SSSP_CL=1."""
+    src, dst, lat, loss = synth.barabasi_albert(500, 3, 9)
+    g = NetworkGraph.from_edges(500, src, dst, lat, loss)
+    plan = RoutingPlan(g, np.arange(100, dtype=np.uint32), algo=SSSP)
+    want = "state=planes+lists" if sweep_mode == "lists" else "state=keys"
+    assert want in plan.describe()
     plan.close()
