@@ -10,13 +10,16 @@
 //   3. every ordered pair must be reachable (the assert at mod.rs:219) ->
 //      SRT_ERR_DISCONNECTED.
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <atomic>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <numeric>
 #include <string>
@@ -268,6 +271,7 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_sl_loss);
     hipFree(p->d_stats);
     hipFree(p->d_pack);
+    hipFree(p->d_pack8);
     hipFree(p->d_draws);
     hipFree(p->d_in_ptr);
     hipFree(p->d_in_edge);
@@ -974,6 +978,130 @@ srt_status srt_plan_bind_comm(srt_plan *p, srt_comm *comm, srt_err *err) {
 }
 
 namespace {
+// Pinned host staging of the compact download, kept for the process (pinning
+// 64 MB costs milliseconds, more than a whole piece's transfer), one user at a
+// time (a second concurrent build takes the 16-byte path).
+struct PinnedPool {
+    std::mutex m;
+    void *buf = nullptr;
+    size_t bytes = 0;
+};
+PinnedPool g_pinned;
+constexpr int DEPTH_MAX = 4;
+// Pieces of 8 Mi entries (64 MB), 3 in flight: C3 (16k), 4 calls each, the
+// table on the host 42-44 ms after the fold starts; 2 in flight measured
+// bimodal (45 or 80 ms: the DMA idles whenever the host is still expanding
+// the piece whose buffer it needs next); 4 Mi or 16 Mi pieces no better.
+// Knobs (measurement): SRT_FETCH_PIECE = log2 entries, SRT_FETCH_DEPTH.
+void fetch_geometry(uint64_t *piece, int *depth) {
+    *piece = 1ull << 23;
+    *depth = 3;
+    if (const char *k = std::getenv("SRT_FETCH_PIECE")) *piece = 1ull << std::max(16, std::min(24, std::atoi(k)));
+    if (const char *k = std::getenv("SRT_FETCH_DEPTH")) *depth = std::max(2, std::min(DEPTH_MAX, std::atoi(k)));
+}
+
+// End-to-end download of a kp.lat32 table in 8-byte records (latency / g as
+// u32 + loss bits: half the PCIe bytes of srt_path), pipelined three ways:
+// the device packs and copies piece c + 1 into one pinned buffer while host
+// threads expand piece c from the other into the caller's srt_path table, and
+// the fold of later rows still runs on the main stream.  Piece c waits for the
+// fold chunk holding its last entry (ev_fold).
+srt_status fetch_pipelined8(srt_plan *p, srt_path *out, uint8_t *pinned, srt_err *err) {
+    Trace tr;
+    const uint64_t nn = (uint64_t)p->n * p->n, per_fold = (uint64_t)p->fold_chunk_rows * p->n;
+    uint64_t PIECE;
+    int DEPTH;
+    fetch_geometry(&PIECE, &DEPTH);
+    const uint32_t np = (uint32_t)((nn + PIECE - 1) / PIECE);
+    if (!p->d_pack8) HIP_TRY(hipMalloc(&p->d_pack8, PIECE * 8 * DEPTH), "hipMalloc(pack8)");
+    uint2 *h[DEPTH_MAX];
+    hipEvent_t ev[DEPTH_MAX];
+    for (int i = 0; i < DEPTH; ++i) {
+        h[i] = reinterpret_cast<uint2 *>(pinned) + (uint64_t)i * PIECE;
+        HIP_TRY(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming), "event");
+    }
+    hipStream_t C = p->comm_stream;
+    auto enqueue = [&](uint32_t c) -> hipError_t {
+        const uint64_t first = (uint64_t)c * PIECE, cnt = std::min(PIECE, nn - first);
+        hipError_t e = hipStreamWaitEvent(C, p->ev_fold[(first + cnt - 1) / per_fold], 0);
+        if (e != hipSuccess) return e;
+        uint2 *dst = reinterpret_cast<uint2 *>(p->d_pack8) + (uint64_t)(c % DEPTH) * PIECE;
+        srt::pack_paths8(p, first, cnt, dst, C);
+        e = hipMemcpyAsync(h[c % DEPTH], dst, cnt * 8, hipMemcpyDeviceToHost, C);
+        return e == hipSuccess ? hipEventRecord(ev[c % DEPTH], C) : e;
+    };
+    const uint64_t g = p->kp.g;
+    const int T = host_threads(nn);
+    // expansion of entries [a, b) of piece c into the caller's table: one
+    // 16-byte non-temporal store per entry when the table is 16-byte aligned
+    // (no read-for-ownership of the destination lines)
+    const bool nt = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+    auto expand_range = [&](uint32_t c, uint64_t a, uint64_t b) {
+        const uint64_t first = (uint64_t)c * PIECE;
+        const uint2 *src = h[c % DEPTH];
+        srt_path *dst = out + first;
+        if (nt) {
+            for (uint64_t i = a; i < b; ++i) {
+                const uint2 r = src[i];
+                const uint64_t l = r.x == 0xffffffffu ? ~0ull : (uint64_t)r.x * g;
+                _mm_stream_si128(reinterpret_cast<__m128i *>(dst + i), _mm_set_epi64x((long long)r.y, (long long)l));
+            }
+        } else {
+            for (uint64_t i = a; i < b; ++i) {
+                const uint2 r = src[i];
+                srt_path q;
+                q.latency_ns = r.x == 0xffffffffu ? ~0ull : (uint64_t)r.x * g;
+                std::memcpy(&q.packet_loss, &r.y, 4);
+                q._pad = 0;
+                dst[i] = q;
+            }
+        }
+    };
+    std::atomic<int> ready{-1}, stop{0};
+    std::atomic<uint64_t> done{0};
+    auto expand = [&](int w) {
+        for (uint32_t c = 0; c < np; ++c) {
+            while (ready.load(std::memory_order_acquire) < (int)c) {
+                if (stop.load(std::memory_order_relaxed)) return;
+                std::this_thread::yield();
+            }
+            const uint64_t first = (uint64_t)c * PIECE, cnt = std::min(PIECE, nn - first);
+            expand_range(c, cnt * w / T, cnt * (w + 1) / T);
+            _mm_sfence();
+            done.fetch_add(1, std::memory_order_acq_rel);
+        }
+    };
+    hipError_t e = hipSuccess;
+    for (uint32_t c = 0; c < (uint32_t)DEPTH && c < np && e == hipSuccess; ++c) e = enqueue(c);
+    std::vector<std::thread> pool;
+    for (int w = 1; w < T && e == hipSuccess; ++w) pool.emplace_back(expand, w);
+    double wait_dma = 0.0, wait_expand = 0.0;  // SRT_TRACE: where the main thread waited
+    for (uint32_t c = 0; c < np && e == hipSuccess; ++c) {
+        auto t0 = std::chrono::steady_clock::now();
+        e = hipEventSynchronize(ev[c % DEPTH]);
+        if (e != hipSuccess) break;
+        auto t1 = std::chrono::steady_clock::now();
+        if (c > 0) wait_dma += std::chrono::duration<double, std::milli>(t1 - t0).count();
+        if (c == 0) tr.mark("fetch8: first piece on the host");
+        ready.store((int)c, std::memory_order_release);
+        // this thread expands its own slice, then waits for the others
+        expand_range(c, 0, std::min(PIECE, nn - (uint64_t)c * PIECE) / T);
+        _mm_sfence();
+        while (done.load(std::memory_order_acquire) < (uint64_t)(c + 1) * (T - 1)) std::this_thread::yield();
+        wait_expand += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+        if (c + DEPTH < np) e = enqueue(c + DEPTH);
+    }
+    stop.store(1);
+    for (auto &th : pool) th.join();
+    if (tr.on)
+        std::fprintf(stderr, "[srt] fetch8: %u pieces, %d threads, nt=%d: waited %.1f ms on DMA, %.1f ms expanding\n",
+                     np, T, (int)nt, wait_dma, wait_expand);
+    tr.mark("fetch8: pieces downloaded + expanded");
+    for (int i = 0; i < DEPTH; ++i) (void)hipEventDestroy(ev[i]);
+    if (e != hipSuccess) return hip_fail(err, e, "compact download");
+    return SRT_OK;
+}
+
 // End-to-end download behind the chunked fold (fw_loss with fold_chunk_rows):
 // chunk c's rows are packed and copied to the host on the comm stream (idle
 // on one GPU) once ev_fold[c] fires, while the fold of chunk c + 1 runs.
@@ -987,6 +1115,30 @@ srt_status fetch_pipelined(srt_plan *p, srt_path *out, uint64_t *min_latency_ns,
         p->d_pack = (srt_path *)ptr;
     }
     hipStream_t C = p->comm_stream;
+    // compact (8-byte) records when every latency fits u32 units (knob
+    // SRT_FETCH16=1: the 16-byte srt_path download, for A/B)
+    if (p->kp.lat32 && !std::getenv("SRT_FETCH16")) {
+        PinnedPool &pp = g_pinned;
+        std::unique_lock<std::mutex> lk(pp.m, std::try_to_lock);
+        if (lk.owns_lock()) {
+            uint64_t piece;
+            int depth;
+            fetch_geometry(&piece, &depth);
+            const size_t need = (size_t)depth * piece * 8;
+            if (pp.bytes < need) {
+                if (pp.buf) (void)hipHostFree(pp.buf);
+                pp.buf = nullptr;
+                pp.bytes = 0;
+                if (hipHostMalloc(&pp.buf, need, 0) == hipSuccess) pp.bytes = need;
+            }
+            if (pp.buf) {
+                srt_status s = fetch_pipelined8(p, out, reinterpret_cast<uint8_t *>(pp.buf), err);
+                if (s == SRT_OK) s = srt_plan_sync(p, err);
+                if (s == SRT_OK) s = srt_plan_fetch(p, nullptr, min_latency_ns, err);
+                return s;
+            }
+        }
+    }
     for (uint32_t c = 0; c < nc; ++c) {
         const uint64_t first = (uint64_t)c * per, cnt = std::min(per, nn - first);
         HIP_TRY(hipStreamWaitEvent(C, p->ev_fold[c], 0), "wait fold chunk");

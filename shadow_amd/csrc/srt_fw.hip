@@ -1145,6 +1145,19 @@ __global__ void pack_kernel(const uint64_t *__restrict__ lat, const float *__res
     }
 }
 
+// 8-byte download form of a table entry: latency in units of g (u32, the
+// unreachable ~0 as 0xFFFFFFFF) + the f32 loss bits; the host expands it into
+// srt_path.  Needs every finite latency / g < 2^32 - 1 (KeyParams::lat32;
+// the diagonal's self-loop latency is an edge latency, so a multiple of g).
+__global__ void pack8_kernel(const uint64_t *__restrict__ lat, const float *__restrict__ loss, uint2 *__restrict__ out,
+                             uint64_t total, uint64_t g) {
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < total;
+         e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t l = lat[e];
+        out[e] = make_uint2(l == ~0ull ? 0xffffffffu : (uint32_t)(l / g), __float_as_uint(loss[e]));
+    }
+}
+
 template <typename K>
 void fw_init_t(srt_plan *p) {
     K *D = reinterpret_cast<K *>(p->d_D);
@@ -1642,6 +1655,11 @@ srt_status fw_rounds(srt_plan *p, srt_err *err) {
     if (p->key_type == KEY_U16) return fw_rounds_t<uint16_t>(p, err);
     if (p->key_type == KEY_U32) return fw_rounds_t<uint32_t>(p, err);
     return p->key_type == KEY_F64 ? fw_rounds_t<double>(p, err) : fw_rounds_t<uint64_t>(p, err);
+}
+
+void pack_paths8(srt_plan *p, uint64_t first, uint64_t count, void *dst, hipStream_t s) {
+    hipLaunchKernelGGL(pack8_kernel, dim3(4096), dim3(256), 0, s, p->d_out_lat + first, p->d_out_loss + first,
+                       reinterpret_cast<uint2 *>(dst), count, p->kp.g);
 }
 
 void pack_paths(srt_plan *p, uint64_t first, uint64_t count, srt_path *dst, hipStream_t s) {

@@ -107,6 +107,7 @@ struct srt_plan {
     float *d_sl_loss = nullptr;
     unsigned long long *d_stats = nullptr;  // [0] min latency, [1] unreachable pairs
     srt_path *d_pack = nullptr;             // AoS staging for fetch
+    void *d_pack8 = nullptr;                // 8-byte staging of the compact end-to-end download
     uint64_t *d_draws = nullptr;            // packet stage: one RNG draw per packet
     uint64_t draws_cap = 0;
     void *d_ev_scratch = nullptr;           // packet events: sort keys + rocPRIM temp
@@ -232,6 +233,8 @@ srt_status fw_loss(srt_plan *p, unsigned long long *d_stats, srt_err *err);
 void expand_shard_rows(srt_plan *p, int nranks);
 // table entries [first, first + count) -> d_pack[0, count) as srt_path
 void pack_paths(srt_plan *p, uint64_t first, uint64_t count, srt_path *dst, hipStream_t s);
+// the same entries as 8-byte (latency / g as u32, loss bits) records (kp.lat32 plans)
+void pack_paths8(srt_plan *p, uint64_t first, uint64_t count, void *dst, hipStream_t s);
 // kernels (srt_sssp.hip)
 srt_status sssp_run(srt_plan *p, unsigned long long *d_stats, srt_err *err);
 void reduce_rank_stats(srt_plan *p, int nranks);

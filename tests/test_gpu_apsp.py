@@ -237,3 +237,32 @@ def test_loss_pass_unpacked_form(monkeypatch, seed, directed):
     n = 90 + 17 * seed
     e = synth.random_graph(n, 200 + seed, p_edge=0.12, directed=directed, lat_range_ns=(1, 5), loss_max=0.05)
     _check(e, np.random.default_rng(seed).permutation(n).astype(np.uint32), directed, n, algo=_lib.SRT_ALGO_FW)
+
+
+def test_end_to_end_compact_download_matches_device_table(monkeypatch):
+    """srt_compute_shortest_paths on a dense graph downloads the table as
+    8-byte records (latency / g, loss bits) in pieces behind the chunked fold,
+    expanded on host threads; 9,000 nodes = 2 fold chunks, 20 pieces.  The
+    host table must equal, bit for bit, the device table of the same build
+    and the 16-byte download (SRT_FETCH16=1)."""
+    import torch
+
+    from shadow_amd.dist import _CudaBuf
+    from shadow_amd.plan import RoutingPlan
+    n = 9000
+    row_ptr, col, lat, loss = synth.complete_csr(n, 21)
+    g = NetworkGraph(n, np.arange(n, dtype=np.uint32), row_ptr, col, lat, loss, directed=False)
+    nodes = np.arange(n, dtype=np.uint32)
+    t = g.compute_shortest_paths(nodes)
+    plan = RoutingPlan(g, nodes).run()
+    lat_p, loss_p, m = plan.table_ptrs()
+    dev = torch.device("cuda", 0)
+    L = torch.as_tensor(_CudaBuf(lat_p, m * m * 8), device=dev).view(torch.int64).cpu().numpy().view(np.uint64)
+    P = torch.as_tensor(_CudaBuf(loss_p, m * m * 4), device=dev).view(torch.int32).cpu().numpy().view(np.uint32)
+    plan.close()
+    assert np.array_equal(t.latency_ns.reshape(-1), L)
+    assert np.array_equal(t.packet_loss.reshape(-1).view(np.uint32), P)
+    monkeypatch.setenv("SRT_FETCH16", "1")
+    t16 = g.compute_shortest_paths(nodes)
+    assert np.array_equal(t16.latency_ns, t.latency_ns)
+    assert np.array_equal(t16.packet_loss.view(np.uint32), t.packet_loss.view(np.uint32))
