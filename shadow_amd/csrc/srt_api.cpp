@@ -683,10 +683,20 @@ srt_status run_tail(srt_plan *p, srt_err *err) {
     const int rank = p->comm ? p->comm->rank : 0, nranks = p->comm ? p->comm->nranks : 1;
     unsigned long long *rstats = p->comm ? p->d_rstats + 2 * rank : p->d_stats;
     if (p->h_loss_defer) {
-        // end-to-end build: the edge losses, uploaded while the closure runs
-        // (pageable source: the copy returns once the data is on the device)
-        HIP_TRY(hipMemcpyAsync(p->d_loss, p->h_loss_defer, p->n_adj * 4, hipMemcpyHostToDevice, p->stream),
+        // end-to-end build: the edge losses, uploaded while the closure runs.
+        // The pageable copy runs on the host thread once its stream reaches
+        // it, so it goes on the comm stream (idle on one GPU; the closure is
+        // all on the main and side streams) and the main stream waits for it
+        // before the loss pass -- on the main stream it would queue behind the
+        // closure (measured: C3 +19 ms, the 1 GB at ~55 GB/s, serial).
+        hipStream_t up = p->comm ? p->stream : p->comm_stream;
+        HIP_TRY(hipMemcpyAsync(p->d_loss, p->h_loss_defer, p->n_adj * 4, hipMemcpyHostToDevice, up),
                 "upload (loss)");
+        if (up != p->stream) {
+            if (!p->ev_upload) HIP_TRY(hipEventCreateWithFlags(&p->ev_upload, hipEventDisableTiming), "event");
+            HIP_TRY(hipEventRecord(p->ev_upload, up), "event record");
+            HIP_TRY(hipStreamWaitEvent(p->stream, p->ev_upload, 0), "event wait");
+        }
         p->h_loss_defer = nullptr;
     }
     if (p->algo != SRT_ALGO_SSSP) {
@@ -853,7 +863,7 @@ void srt_plan_destroy(srt_plan *p) {
     for (hipEvent_t e : p->ev) hipEventDestroy(e);
     for (hipEvent_t e : p->ev_tail) hipEventDestroy(e);
     for (hipEvent_t e : {p->ev_begin, p->ev_end, p->ev_cross, p->ev_pivot, p->ev_row, p->ev_bcast, p->ev_loss0,
-                         p->ev_loss1})
+                         p->ev_loss1, p->ev_upload})
         if (e) hipEventDestroy(e);
     if (p->side_stream) hipStreamDestroy(p->side_stream);
     if (p->comm_stream) hipStreamDestroy(p->comm_stream);
@@ -1012,6 +1022,10 @@ srt_status fetch_pipelined8(srt_plan *p, srt_path *out, uint8_t *pinned, srt_err
     uint64_t PIECE;
     int DEPTH;
     fetch_geometry(&PIECE, &DEPTH);
+    // u16-key plans (every finite latency < 0x4000 units): 6-byte records, a
+    // piece = its u16 latencies, then (16-byte aligned) its f32 losses
+    const bool rec6 = p->key_type == srt::KEY_U16 && !std::getenv("SRT_FETCH8");
+    auto loss_off = [](uint64_t cnt) { return (cnt * 2 + 15) & ~15ull; };
     const uint32_t np = (uint32_t)((nn + PIECE - 1) / PIECE);
     if (!p->d_pack8) HIP_TRY(hipMalloc(&p->d_pack8, PIECE * 8 * DEPTH), "hipMalloc(pack8)");
     uint2 *h[DEPTH_MAX];
@@ -1026,8 +1040,13 @@ srt_status fetch_pipelined8(srt_plan *p, srt_path *out, uint8_t *pinned, srt_err
         hipError_t e = hipStreamWaitEvent(C, p->ev_fold[(first + cnt - 1) / per_fold], 0);
         if (e != hipSuccess) return e;
         uint2 *dst = reinterpret_cast<uint2 *>(p->d_pack8) + (uint64_t)(c % DEPTH) * PIECE;
-        srt::pack_paths8(p, first, cnt, dst, C);
-        e = hipMemcpyAsync(h[c % DEPTH], dst, cnt * 8, hipMemcpyDeviceToHost, C);
+        if (rec6) {
+            srt::pack_paths6(p, first, cnt, dst, loss_off(cnt), C);
+            e = hipMemcpyAsync(h[c % DEPTH], dst, loss_off(cnt) + cnt * 4, hipMemcpyDeviceToHost, C);
+        } else {
+            srt::pack_paths8(p, first, cnt, dst, C);
+            e = hipMemcpyAsync(h[c % DEPTH], dst, cnt * 8, hipMemcpyDeviceToHost, C);
+        }
         return e == hipSuccess ? hipEventRecord(ev[c % DEPTH], C) : e;
     };
     const uint64_t g = p->kp.g;
@@ -1040,7 +1059,23 @@ srt_status fetch_pipelined8(srt_plan *p, srt_path *out, uint8_t *pinned, srt_err
         const uint64_t first = (uint64_t)c * PIECE;
         const uint2 *src = h[c % DEPTH];
         srt_path *dst = out + first;
-        if (nt) {
+        if (rec6) {
+            const uint64_t cnt = std::min(PIECE, nn - first);
+            const uint16_t *l16 = reinterpret_cast<const uint16_t *>(src);
+            const uint32_t *lb = reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(src) + loss_off(cnt));
+            for (uint64_t i = a; i < b; ++i) {
+                const uint64_t l = l16[i] == 0xffffu ? ~0ull : (uint64_t)l16[i] * g;
+                if (nt) {
+                    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + i), _mm_set_epi64x((long long)lb[i], (long long)l));
+                } else {
+                    srt_path q;
+                    q.latency_ns = l;
+                    std::memcpy(&q.packet_loss, lb + i, 4);
+                    q._pad = 0;
+                    dst[i] = q;
+                }
+            }
+        } else if (nt) {
             for (uint64_t i = a; i < b; ++i) {
                 const uint2 r = src[i];
                 const uint64_t l = r.x == 0xffffffffu ? ~0ull : (uint64_t)r.x * g;
@@ -1094,8 +1129,8 @@ srt_status fetch_pipelined8(srt_plan *p, srt_path *out, uint8_t *pinned, srt_err
     stop.store(1);
     for (auto &th : pool) th.join();
     if (tr.on)
-        std::fprintf(stderr, "[srt] fetch8: %u pieces, %d threads, nt=%d: waited %.1f ms on DMA, %.1f ms expanding\n",
-                     np, T, (int)nt, wait_dma, wait_expand);
+        std::fprintf(stderr, "[srt] fetch8: %u pieces of %d-byte records, %d threads, nt=%d: waited %.1f ms on DMA, "
+                     "%.1f ms expanding\n", np, rec6 ? 6 : 8, T, (int)nt, wait_dma, wait_expand);
     tr.mark("fetch8: pieces downloaded + expanded");
     for (int i = 0; i < DEPTH; ++i) (void)hipEventDestroy(ev[i]);
     if (e != hipSuccess) return hip_fail(err, e, "compact download");

@@ -1158,6 +1158,21 @@ __global__ void pack8_kernel(const uint64_t *__restrict__ lat, const float *__re
     }
 }
 
+// 6-byte download form for u16-key plans (every finite latency / g < 0x4000):
+// the piece's latencies as u16 (unreachable 0xFFFF), then its f32 losses at
+// byte offset loss_off
+__global__ void pack6_kernel(const uint64_t *__restrict__ lat, const float *__restrict__ loss, uint8_t *__restrict__ out,
+                             uint64_t total, uint64_t g, uint64_t loss_off) {
+    uint16_t *l16 = reinterpret_cast<uint16_t *>(out);
+    float *lf = reinterpret_cast<float *>(out + loss_off);
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < total;
+         e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t l = lat[e];
+        l16[e] = l == ~0ull ? (uint16_t)0xffffu : (uint16_t)(l / g);
+        lf[e] = loss[e];
+    }
+}
+
 template <typename K>
 void fw_init_t(srt_plan *p) {
     K *D = reinterpret_cast<K *>(p->d_D);
@@ -1660,6 +1675,11 @@ srt_status fw_rounds(srt_plan *p, srt_err *err) {
 void pack_paths8(srt_plan *p, uint64_t first, uint64_t count, void *dst, hipStream_t s) {
     hipLaunchKernelGGL(pack8_kernel, dim3(4096), dim3(256), 0, s, p->d_out_lat + first, p->d_out_loss + first,
                        reinterpret_cast<uint2 *>(dst), count, p->kp.g);
+}
+
+void pack_paths6(srt_plan *p, uint64_t first, uint64_t count, void *dst, uint64_t loss_off, hipStream_t s) {
+    hipLaunchKernelGGL(pack6_kernel, dim3(4096), dim3(256), 0, s, p->d_out_lat + first, p->d_out_loss + first,
+                       reinterpret_cast<uint8_t *>(dst), count, p->kp.g, loss_off);
 }
 
 void pack_paths(srt_plan *p, uint64_t first, uint64_t count, srt_path *dst, hipStream_t s) {

@@ -124,6 +124,7 @@ struct srt_plan {
     hipStream_t side_stream = nullptr;                  // high-priority pivot stream
     hipStream_t comm_stream = nullptr;                  // pivot-row broadcasts (multi-GPU)
     hipEvent_t ev_row = nullptr, ev_bcast = nullptr;    // S -> C (row ready), C -> S/M (row received)
+    hipEvent_t ev_upload = nullptr;                     // end-to-end: deferred loss upload done (C -> M)
     uint64_t p3_launches = 0;
     double p3_work = 0.0;  // relaxations done by the timed launches
     uint64_t p3_tiles = 0;  // C tiles those launches loaded and stored
@@ -235,6 +236,8 @@ void expand_shard_rows(srt_plan *p, int nranks);
 void pack_paths(srt_plan *p, uint64_t first, uint64_t count, srt_path *dst, hipStream_t s);
 // the same entries as 8-byte (latency / g as u32, loss bits) records (kp.lat32 plans)
 void pack_paths8(srt_plan *p, uint64_t first, uint64_t count, void *dst, hipStream_t s);
+// u16-key plans: u16 latency units, then the f32 losses at byte offset loss_off
+void pack_paths6(srt_plan *p, uint64_t first, uint64_t count, void *dst, uint64_t loss_off, hipStream_t s);
 // kernels (srt_sssp.hip)
 srt_status sssp_run(srt_plan *p, unsigned long long *d_stats, srt_err *err);
 void reduce_rank_stats(srt_plan *p, int nranks);

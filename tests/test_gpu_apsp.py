@@ -241,10 +241,11 @@ def test_loss_pass_unpacked_form(monkeypatch, seed, directed):
 
 def test_end_to_end_compact_download_matches_device_table(monkeypatch):
     """srt_compute_shortest_paths on a dense graph downloads the table as
-    8-byte records (latency / g, loss bits) in pieces behind the chunked fold,
-    expanded on host threads; 9,000 nodes = 2 fold chunks, 20 pieces.  The
-    host table must equal, bit for bit, the device table of the same build
-    and the 16-byte download (SRT_FETCH16=1)."""
+    6-byte records (u16 keys: latency / g as u16, loss bits) in pieces behind
+    the chunked fold, expanded on host threads; 9,000 nodes = 2 fold chunks,
+    10 pieces.  The host table must equal, bit for bit, the device table of
+    the same build, the 8-byte records (SRT_FETCH8=1) and the 16-byte
+    download (SRT_FETCH16=1)."""
     import torch
 
     from shadow_amd.dist import _CudaBuf
@@ -262,7 +263,9 @@ def test_end_to_end_compact_download_matches_device_table(monkeypatch):
     plan.close()
     assert np.array_equal(t.latency_ns.reshape(-1), L)
     assert np.array_equal(t.packet_loss.reshape(-1).view(np.uint32), P)
-    monkeypatch.setenv("SRT_FETCH16", "1")
-    t16 = g.compute_shortest_paths(nodes)
-    assert np.array_equal(t16.latency_ns, t.latency_ns)
-    assert np.array_equal(t16.packet_loss.view(np.uint32), t.packet_loss.view(np.uint32))
+    for knob in ("SRT_FETCH8", "SRT_FETCH16"):  # 8-byte records; the 16-byte srt_path download
+        monkeypatch.setenv(knob, "1")
+        t2 = g.compute_shortest_paths(nodes)
+        monkeypatch.delenv(knob)
+        assert np.array_equal(t2.latency_ns, t.latency_ns), knob
+        assert np.array_equal(t2.packet_loss.view(np.uint32), t.packet_loss.view(np.uint32)), knob
