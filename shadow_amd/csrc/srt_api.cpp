@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <atomic>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <numeric>
@@ -115,72 +116,72 @@ int host_threads(uint64_t work) {
     return std::max(1, std::min(t, 32));
 }
 
-void csr_scan(const srt_csr *g, CsrStats *out) {
+// Rows [r0, r1) into the thread's accumulator st (sl_cnt / sl_first of the
+// rows go to out).  Optional, for the piece-pipelined upload: lat32 (the
+// rows' latencies as u32, indexed from entry k_base; *lat_over set when one
+// does not fit) and *identity (cleared unless every row is exactly the
+// entries 0 .. V-1 in order, so col need not be uploaded).
+void scan_rows(const srt_csr *g, uint32_t r0, uint32_t r1, CsrStats &st, CsrStats *out, uint32_t *lat32 = nullptr,
+               uint64_t k_base = 0, bool *lat_over = nullptr, bool *identity = nullptr) {
     const uint32_t V = g->n_nodes;
-    out->sl_cnt.assign(V, 0);
-    out->sl_first.assign(V, ~0ull);
-    const int T = host_threads(g->n_adj);
-    std::vector<CsrStats> part(T);
-    auto work = [&](int t, uint32_t r0, uint32_t r1) {
-        CsrStats &st = part[t];
-        uint64_t gcd = 0, maxlat = 0, selfl = 0;
-        for (uint32_t u = r0; u < r1; ++u) {
-            const uint64_t b = g->row_ptr[u], e = g->row_ptr[u + 1];
-            uint32_t cnt = 0, prev = 0;
-            uint64_t first = ~0ull;
-            bool inc = true, dec = true;
-            for (uint64_t k = b; k < e; ++k) {
-                const uint32_t c = g->col[k];
-                const uint64_t l = g->lat_ns[k];
-                const float q = g->loss[k];
-                if (c >= V && st.badcol_k == ~0ull) st.badcol_k = k;
-                if (l == 0 && st.zero_k == ~0ull) st.zero_k = k;
-                if (!(q >= 0.0f && q <= 1.0f) && st.badloss_k == ~0ull) st.badloss_k = k;
-                maxlat = l > maxlat ? l : maxlat;
-                if (gcd != 1 && l) {
-                    // divisibility by the running gcd: exact in f64 below 2^53
-                    bool divides;
-                    if (gcd && l < (1ull << 53) && gcd < (1ull << 53)) {
-                        const uint64_t qi = (uint64_t)((double)l / (double)gcd);
-                        divides = qi * gcd == l;
-                    } else {
-                        divides = gcd && l % gcd == 0;
-                    }
-                    if (!divides) gcd = std::gcd(gcd, l);
-                }
-                if (c == u) {
-                    if (!cnt) first = k;
-                    ++cnt;
-                }
-                if (k > b) {
-                    inc &= c > prev;
-                    dec &= c < prev;
-                }
-                prev = c;
+    uint64_t gcd = st.gcd, maxlat = st.maxlat, selfl = st.selfloops;
+    bool ident = true, over = false;
+    for (uint32_t u = r0; u < r1; ++u) {
+        const uint64_t b = g->row_ptr[u], e = g->row_ptr[u + 1];
+        uint32_t cnt = 0, prev = 0;
+        uint64_t first = ~0ull;
+        bool inc = true, dec = true;
+        if (identity) ident &= e - b == V;
+        for (uint64_t k = b; k < e; ++k) {
+            const uint32_t c = g->col[k];
+            const uint64_t l = g->lat_ns[k];
+            const float q = g->loss[k];
+            if (c >= V && st.badcol_k == ~0ull) st.badcol_k = k;
+            if (l == 0 && st.zero_k == ~0ull) st.zero_k = k;
+            if (!(q >= 0.0f && q <= 1.0f) && st.badloss_k == ~0ull) st.badloss_k = k;
+            maxlat = l > maxlat ? l : maxlat;
+            if (lat32) {
+                over |= l > 0xffffffffull;
+                lat32[k - k_base] = (uint32_t)l;
             }
-            out->sl_cnt[u] = cnt;
-            out->sl_first[u] = first;
-            selfl += cnt;
-            const bool uniq = inc || dec;
-            st.unique &= uniq;
-            st.complete &= uniq && (e - b - cnt) == (uint64_t)V - 1;
+            if (identity) ident &= c == (uint32_t)(k - b);
+            if (gcd != 1 && l) {
+                // divisibility by the running gcd: exact in f64 below 2^53
+                bool divides;
+                if (gcd && l < (1ull << 53) && gcd < (1ull << 53)) {
+                    const uint64_t qi = (uint64_t)((double)l / (double)gcd);
+                    divides = qi * gcd == l;
+                } else {
+                    divides = gcd && l % gcd == 0;
+                }
+                if (!divides) gcd = std::gcd(gcd, l);
+            }
+            if (c == u) {
+                if (!cnt) first = k;
+                ++cnt;
+            }
+            if (k > b) {
+                inc &= c > prev;
+                dec &= c < prev;
+            }
+            prev = c;
         }
-        st.gcd = gcd;
-        st.maxlat = maxlat;
-        st.selfloops = selfl;
-    };
-    // row ranges with about n_adj / T entries each
-    std::vector<uint32_t> cut(T + 1, V);
-    cut[0] = 0;
-    for (int t = 1; t < T; ++t) {
-        const uint64_t target = g->n_adj * (uint64_t)t / T;
-        cut[t] = (uint32_t)(std::lower_bound(g->row_ptr, g->row_ptr + V + 1, target) - g->row_ptr);
-        cut[t] = std::max(std::min(cut[t], V), cut[t - 1]);
+        out->sl_cnt[u] = cnt;
+        out->sl_first[u] = first;
+        selfl += cnt;
+        const bool uniq = inc || dec;
+        st.unique &= uniq;
+        st.complete &= uniq && (e - b - cnt) == (uint64_t)V - 1;
     }
-    std::vector<std::thread> pool;
-    for (int t = 1; t < T; ++t) pool.emplace_back(work, t, cut[t], cut[t + 1]);
-    work(0, cut[0], cut[1]);
-    for (auto &th : pool) th.join();
+    st.gcd = gcd;
+    st.maxlat = maxlat;
+    st.selfloops = selfl;
+    if (lat_over && over) *lat_over = true;
+    if (identity && !ident) *identity = false;
+}
+
+// per-thread accumulators into out
+void merge_stats(const std::vector<CsrStats> &part, uint32_t V, CsrStats *out) {
     out->complete = V > 0;
     for (const CsrStats &st : part) {
         out->gcd = std::gcd(out->gcd, st.gcd);
@@ -194,6 +195,181 @@ void csr_scan(const srt_csr *g, CsrStats *out) {
     }
     if (out->gcd == 0) out->gcd = 1;
 }
+
+void csr_scan(const srt_csr *g, CsrStats *out) {
+    const uint32_t V = g->n_nodes;
+    out->sl_cnt.assign(V, 0);
+    out->sl_first.assign(V, ~0ull);
+    const int T = host_threads(g->n_adj);
+    std::vector<CsrStats> part(T);
+    auto work = [&](int t, uint32_t r0, uint32_t r1) { scan_rows(g, r0, r1, part[t], out); };
+    // row ranges with about n_adj / T entries each
+    std::vector<uint32_t> cut(T + 1, V);
+    cut[0] = 0;
+    for (int t = 1; t < T; ++t) {
+        const uint64_t target = g->n_adj * (uint64_t)t / T;
+        cut[t] = (uint32_t)(std::lower_bound(g->row_ptr, g->row_ptr + V + 1, target) - g->row_ptr);
+        cut[t] = std::max(std::min(cut[t], V), cut[t - 1]);
+    }
+    std::vector<std::thread> pool;
+    for (int t = 1; t < T; ++t) pool.emplace_back(work, t, cut[t], cut[t + 1]);
+    work(0, cut[0], cut[1]);
+    for (auto &th : pool) th.join();
+    merge_stats(part, V, out);
+}
+
+// Pinned host staging of the piece-pipelined upload and download, kept for
+// the process (pinning 192 MB costs tens of milliseconds, more than the
+// transfers it speeds up), one user at a time (a concurrent build takes the
+// pageable / 16-byte paths).
+struct PinnedPool {
+    std::mutex m;
+    void *buf = nullptr;
+    size_t bytes = 0;
+    bool ensure(size_t need) {  // call with m held
+        if (bytes >= need) return true;
+        if (buf) (void)hipHostFree(buf);
+        buf = nullptr;
+        bytes = 0;
+        if (hipHostMalloc(&buf, need, 0) != hipSuccess) return false;
+        bytes = need;
+        return true;
+    }
+};
+PinnedPool g_pinned;
+constexpr size_t PINNED_BYTES = 3ull * (1ull << 23) * 8;  // 3 pieces of 8 Mi 8-byte records = 3 x 16 Mi u32
+
+// Piece-pipelined CSR scan + upload (graphs of >= 16 Mi adjacency entries).
+// The CSR scan's host threads walk the rows in pieces of <= 16 Mi entries,
+// in order, and write each piece's latencies as u32 into a pinned slot (3 in
+// flight); the main thread uploads a finished piece (64 MB instead of the
+// 128 MB of u64) and a device kernel widens it into d_lat.  A piece whose
+// rows are all exactly the entries 0 .. V-1 in order (a complete graph with
+// self-loops, as Shadow's atlas graphs) uploads no col at all: a kernel writes
+// it.  A piece with a latency >= 2^32 ns, or irregular rows, sends that array
+// from the caller's memory as before.  C3 (16k complete): 3.2 GB -> 1.07 GB
+// over PCIe.  Knobs (tests / A-B): SRT_UPLOAD_PIPE=0 off, SRT_UPLOAD_PIECE=
+// log2 entries per piece (also forces the pipeline on small graphs).
+struct PieceUpload {
+    static constexpr int DEPTH = 3;
+    const srt_csr *g = nullptr;
+    uint64_t PE = 1ull << 24;
+    std::vector<uint32_t> cut;  // piece c = rows [cut[c], cut[c+1])
+    uint32_t P = 0;
+    int T = 1;
+    std::vector<CsrStats> part;
+    std::vector<uint8_t> over, ident;  // per (piece, thread)
+    std::unique_ptr<std::atomic<int>[]> done;
+    std::atomic<int> ready{-1};
+    std::vector<std::thread> pool;
+    std::unique_lock<std::mutex> lk;
+    uint32_t *slot[DEPTH] = {};
+    hipEvent_t ev[DEPTH] = {};
+    bool on = false;
+
+    bool init(const srt_csr *g_, CsrStats *cs) {
+        g = g_;
+        const char *pe = std::getenv("SRT_UPLOAD_PIECE");
+        if (const char *k = std::getenv("SRT_UPLOAD_PIPE"); k && std::atoi(k) == 0) return false;
+        if (pe) PE = 1ull << std::max(4, std::min(24, std::atoi(pe)));
+        else if (g->n_adj < PE) return false;
+        const uint32_t V = g->n_nodes;
+        cut.push_back(0);
+        while (cut.back() < V) {
+            const uint64_t k0 = g->row_ptr[cut.back()];
+            uint32_t r = (uint32_t)(std::upper_bound(g->row_ptr + cut.back(), g->row_ptr + V + 1, k0 + PE) - g->row_ptr) - 1;
+            if (r <= cut.back()) return false;  // one row larger than a piece
+            cut.push_back(std::min(r, V));
+        }
+        P = (uint32_t)cut.size() - 1;
+        // only when the pinned staging already exists: pinning it costs more
+        // than the pipeline saves (srt_compute_shortest_paths allocates it
+        // behind its first closure, for the download)
+        lk = std::unique_lock<std::mutex>(g_pinned.m, std::try_to_lock);
+        if (!lk.owns_lock() || g_pinned.bytes < std::max<size_t>(PINNED_BYTES, DEPTH * PE * 4)) return false;
+        for (int i = 0; i < DEPTH; ++i) slot[i] = reinterpret_cast<uint32_t *>(g_pinned.buf) + (uint64_t)i * PE;
+        cs->sl_cnt.assign(V, 0);
+        cs->sl_first.assign(V, ~0ull);
+        T = host_threads(g->n_adj);
+        part.assign(T, CsrStats());
+        over.assign((size_t)P * T, 0);
+        ident.assign((size_t)P * T, 1);
+        done.reset(new std::atomic<int>[P]);
+        for (uint32_t c = 0; c < P; ++c) done[c].store(0);
+        ready.store(std::min<int>(DEPTH, (int)P) - 1);
+        for (int w = 0; w < T; ++w) pool.emplace_back([this, cs, w] { work(cs, w); });
+        on = true;
+        return true;
+    }
+    void work(CsrStats *cs, int w) {
+        for (uint32_t c = 0; c < P; ++c) {
+            while (ready.load(std::memory_order_acquire) < (int)c) std::this_thread::yield();
+            const uint64_t k0 = g->row_ptr[cut[c]], k1 = g->row_ptr[cut[c + 1]];
+            auto row_at = [&](uint64_t k) {
+                return (uint32_t)(std::lower_bound(g->row_ptr + cut[c], g->row_ptr + cut[c + 1], k) - g->row_ptr);
+            };
+            const uint32_t a = w == 0 ? cut[c] : row_at(k0 + (k1 - k0) * w / T);
+            const uint32_t b = w == T - 1 ? cut[c + 1] : row_at(k0 + (k1 - k0) * (w + 1) / T);
+            bool ov = false, id = true;
+            if (a < b) scan_rows(g, a, b, part[w], cs, slot[c % DEPTH], k0, &ov, &id);
+            over[(size_t)c * T + w] = ov;
+            ident[(size_t)c * T + w] = id;
+            done[c].fetch_add(1, std::memory_order_acq_rel);
+        }
+    }
+    // main thread, device ready: upload the pieces as the scan finishes them
+    srt_status run(srt_plan *p, srt_err *err) {
+        hipStream_t M = p->stream;
+        HIP_TRY(hipMalloc(&p->d_up32, (size_t)DEPTH * PE * 4), "hipMalloc(upload slots)");
+        for (int i = 0; i < DEPTH; ++i) HIP_TRY(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming), "event");
+        for (uint32_t c = 0; c < P; ++c) {
+            while (done[c].load(std::memory_order_acquire) < T) std::this_thread::yield();
+            bool lat_ok = true, id = true;
+            for (int w = 0; w < T; ++w) {
+                lat_ok &= !over[(size_t)c * T + w];
+                id &= ident[(size_t)c * T + w] != 0;
+            }
+            const uint64_t k0 = g->row_ptr[cut[c]], cnt = g->row_ptr[cut[c + 1]] - k0;
+            uint32_t *dslot = p->d_up32 + (uint64_t)(c % DEPTH) * PE;
+            if (cnt && lat_ok) {
+                HIP_TRY(hipMemcpyAsync(dslot, slot[c % DEPTH], cnt * 4, hipMemcpyHostToDevice, M), "upload (lat)");
+                srt::widen_u32(p->d_lat + k0, dslot, cnt, M);
+            } else if (cnt) {
+                HIP_TRY(hipMemcpyAsync(p->d_lat + k0, g->lat_ns + k0, cnt * 8, hipMemcpyHostToDevice, M), "upload (lat)");
+            }
+            HIP_TRY(hipEventRecord(ev[c % DEPTH], M), "event");
+            if (cnt && id) srt::iota_rows(p->d_col + k0, cnt, g->n_nodes, M);
+            else if (cnt)
+                HIP_TRY(hipMemcpyAsync(p->d_col + k0, g->col + k0, cnt * 4, hipMemcpyHostToDevice, M), "upload (col)");
+            if (c + DEPTH < P) {
+                // the slot of piece c + DEPTH is piece c's: free once its copy is done
+                HIP_TRY(hipEventSynchronize(ev[c % DEPTH]), "sync (upload)");
+                ready.store((int)(c + DEPTH), std::memory_order_release);
+            }
+        }
+        return SRT_OK;
+    }
+    // every thread joined, the stats merged, the slots drained, the pool free
+    void finish(CsrStats *cs) {
+        ready.store((int)P);
+        for (auto &th : pool) th.join();
+        pool.clear();
+        merge_stats(part, g->n_nodes, cs);
+        for (int i = 0; i < DEPTH; ++i)
+            if (ev[i]) {
+                (void)hipEventSynchronize(ev[i]);
+                (void)hipEventDestroy(ev[i]);
+                ev[i] = nullptr;
+            }
+        if (lk.owns_lock()) lk.unlock();
+    }
+    ~PieceUpload() {
+        if (on && !pool.empty()) {
+            ready.store((int)P);
+            for (auto &th : pool) th.join();
+        }
+    }
+};
 
 // Choose the closure's key representation and prove it exact.
 //
@@ -272,6 +448,7 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_stats);
     hipFree(p->d_pack);
     hipFree(p->d_pack8);
+    hipFree(p->d_up32);
     hipFree(p->d_draws);
     hipFree(p->d_in_ptr);
     hipFree(p->d_in_edge);
@@ -409,7 +586,10 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     // 1. the CSR scan (validation + statistics) on host threads while this
     //    thread sets up the device and uploads the CSR
     CsrStats cs;
-    std::thread scanner([&] { csr_scan(g, &cs); });
+    PieceUpload pu;
+    const bool piped = pu.init(g, &cs);
+    std::thread scanner;
+    if (!piped) scanner = std::thread([&] { csr_scan(g, &cs); });
     srt_err derr{};
     const srt_status dst = [&]() -> srt_status {
         srt_err *err = &derr;
@@ -467,15 +647,18 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         };
         if (defer_loss) p->h_loss_defer = g->loss;
         if ((e = up(p->d_row_ptr, g->row_ptr, ((size_t)g->n_nodes + 1) * 8)) != hipSuccess ||
-            (e = up(p->d_col, g->col, g->n_adj * 4)) != hipSuccess ||
-            (e = up(p->d_lat, g->lat_ns, g->n_adj * 8)) != hipSuccess ||
-            (e = defer_loss ? hipSuccess : up(p->d_loss, g->loss, g->n_adj * 4)) != hipSuccess ||
-            (e = up(p->d_nodes, nodes, (size_t)n * 4)) != hipSuccess)
+            (e = up(p->d_nodes, nodes, (size_t)n * 4)) != hipSuccess ||
+            (e = piped ? hipSuccess : up(p->d_col, g->col, g->n_adj * 4)) != hipSuccess ||
+            (e = piped ? hipSuccess : up(p->d_lat, g->lat_ns, g->n_adj * 8)) != hipSuccess)
+            return hip_fail(err, e, "upload");
+        if (piped && (st = pu.run(p, err)) != SRT_OK) return st;
+        if ((e = defer_loss ? hipSuccess : up(p->d_loss, g->loss, g->n_adj * 4)) != hipSuccess)
             return hip_fail(err, e, "upload");
         return SRT_OK;
     }();
-    tr.mark("create: device setup+upload");
-    scanner.join();
+    tr.mark(piped ? "create: device setup+piece upload" : "create: device setup+upload");
+    if (piped) pu.finish(&cs);
+    else scanner.join();
     tr.mark("create: CSR scan (joined)");
 
     // 2. the reference's errors, in its order: edge attributes (parse time),
@@ -988,15 +1171,7 @@ srt_status srt_plan_bind_comm(srt_plan *p, srt_comm *comm, srt_err *err) {
 }
 
 namespace {
-// Pinned host staging of the compact download, kept for the process (pinning
-// 64 MB costs milliseconds, more than a whole piece's transfer), one user at a
-// time (a second concurrent build takes the 16-byte path).
-struct PinnedPool {
-    std::mutex m;
-    void *buf = nullptr;
-    size_t bytes = 0;
-};
-PinnedPool g_pinned;
+
 constexpr int DEPTH_MAX = 4;
 // Pieces of 8 Mi entries (64 MB), 3 in flight: C3 (16k), 4 calls each, the
 // table on the host 42-44 ms after the fold starts; 2 in flight measured
@@ -1159,14 +1334,7 @@ srt_status fetch_pipelined(srt_plan *p, srt_path *out, uint64_t *min_latency_ns,
             uint64_t piece;
             int depth;
             fetch_geometry(&piece, &depth);
-            const size_t need = (size_t)depth * piece * 8;
-            if (pp.bytes < need) {
-                if (pp.buf) (void)hipHostFree(pp.buf);
-                pp.buf = nullptr;
-                pp.bytes = 0;
-                if (hipHostMalloc(&pp.buf, need, 0) == hipSuccess) pp.bytes = need;
-            }
-            if (pp.buf) {
+            if (pp.ensure(std::max<size_t>(PINNED_BYTES, (size_t)depth * piece * 8))) {
                 srt_status s = fetch_pipelined8(p, out, reinterpret_cast<uint8_t *>(pp.buf), err);
                 if (s == SRT_OK) s = srt_plan_sync(p, err);
                 if (s == SRT_OK) s = srt_plan_fetch(p, nullptr, min_latency_ns, err);
@@ -1205,8 +1373,18 @@ srt_status srt_compute_shortest_paths(const srt_csr *g, const uint32_t *nodes, u
             1, std::min<uint64_t>((uint64_t)p->n * p->n, 1ull << 26) / p->n);
     s = run_closure(p, err);
     tr.mark("e2e: closure enqueued");
+    // the pinned staging of the compact download, pinned while the closure
+    // runs (first call of the process: ~1 ms per MB, too slow to pay inline)
+    std::thread pinner;
+    if (s == SRT_OK && pipe && p->kp.lat32 && g_pinned.bytes < PINNED_BYTES)
+        pinner = std::thread([] {
+            std::lock_guard<std::mutex> lk(g_pinned.m);
+            (void)g_pinned.ensure(PINNED_BYTES);
+        });
     if (s == SRT_OK) s = run_tail(p, err);  // the deferred loss upload overlaps the closure
     tr.mark("e2e: loss upload + tail enqueued");
+    if (pinner.joinable()) pinner.join();
+    tr.mark("e2e: pinned staging ready");
     if (s == SRT_OK && pipe) {
         s = fetch_pipelined(p, out, min_latency_ns, err);
     } else if (s == SRT_OK) {

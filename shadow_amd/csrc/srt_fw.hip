@@ -1173,6 +1173,16 @@ __global__ void pack6_kernel(const uint64_t *__restrict__ lat, const float *__re
     }
 }
 
+__global__ void widen_u32_kernel(uint64_t *__restrict__ dst, const uint32_t *__restrict__ src, uint64_t count) {
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < count; e += (uint64_t)gridDim.x * blockDim.x)
+        dst[e] = src[e];
+}
+
+__global__ void iota_rows_kernel(uint32_t *__restrict__ dst, uint64_t count, uint32_t V) {
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < count; e += (uint64_t)gridDim.x * blockDim.x)
+        dst[e] = (uint32_t)(e % V);
+}
+
 template <typename K>
 void fw_init_t(srt_plan *p) {
     K *D = reinterpret_cast<K *>(p->d_D);
@@ -1675,6 +1685,14 @@ srt_status fw_rounds(srt_plan *p, srt_err *err) {
 void pack_paths8(srt_plan *p, uint64_t first, uint64_t count, void *dst, hipStream_t s) {
     hipLaunchKernelGGL(pack8_kernel, dim3(4096), dim3(256), 0, s, p->d_out_lat + first, p->d_out_loss + first,
                        reinterpret_cast<uint2 *>(dst), count, p->kp.g);
+}
+
+void widen_u32(uint64_t *dst, const uint32_t *src, uint64_t count, hipStream_t s) {
+    hipLaunchKernelGGL(widen_u32_kernel, dim3(2048), dim3(256), 0, s, dst, src, count);
+}
+
+void iota_rows(uint32_t *dst, uint64_t count, uint32_t V, hipStream_t s) {
+    hipLaunchKernelGGL(iota_rows_kernel, dim3(2048), dim3(256), 0, s, dst, count, V);
 }
 
 void pack_paths6(srt_plan *p, uint64_t first, uint64_t count, void *dst, uint64_t loss_off, hipStream_t s) {

@@ -108,6 +108,7 @@ struct srt_plan {
     unsigned long long *d_stats = nullptr;  // [0] min latency, [1] unreachable pairs
     srt_path *d_pack = nullptr;             // AoS staging for fetch
     void *d_pack8 = nullptr;                // 8-byte staging of the compact end-to-end download
+    uint32_t *d_up32 = nullptr;             // u32 latency slots of the piece-pipelined upload
     uint64_t *d_draws = nullptr;            // packet stage: one RNG draw per packet
     uint64_t draws_cap = 0;
     void *d_ev_scratch = nullptr;           // packet events: sort keys + rocPRIM temp
@@ -236,6 +237,9 @@ void expand_shard_rows(srt_plan *p, int nranks);
 void pack_paths(srt_plan *p, uint64_t first, uint64_t count, srt_path *dst, hipStream_t s);
 // the same entries as 8-byte (latency / g as u32, loss bits) records (kp.lat32 plans)
 void pack_paths8(srt_plan *p, uint64_t first, uint64_t count, void *dst, hipStream_t s);
+// piece-pipelined upload: dst[i] = src[i] (u32 -> u64); dst[k] = k % V (identity rows)
+void widen_u32(uint64_t *dst, const uint32_t *src, uint64_t count, hipStream_t s);
+void iota_rows(uint32_t *dst, uint64_t count, uint32_t V, hipStream_t s);
 // u16-key plans: u16 latency units, then the f32 losses at byte offset loss_off
 void pack_paths6(srt_plan *p, uint64_t first, uint64_t count, void *dst, uint64_t loss_off, hipStream_t s);
 // kernels (srt_sssp.hip)

@@ -269,3 +269,59 @@ def test_end_to_end_compact_download_matches_device_table(monkeypatch):
         monkeypatch.delenv(knob)
         assert np.array_equal(t2.latency_ns, t.latency_ns), knob
         assert np.array_equal(t2.packet_loss.view(np.uint32), t.packet_loss.view(np.uint32)), knob
+
+
+@pytest.fixture
+def small_upload_pieces(monkeypatch):
+    """Force the piece-pipelined CSR scan + upload on small graphs: pieces of
+    2^6 adjacency entries (many pieces, 3 in flight)."""
+    monkeypatch.setenv("SRT_UPLOAD_PIECE", "6")
+    yield
+    monkeypatch.delenv("SRT_UPLOAD_PIECE")
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_piece_upload_irregular_rows(small_upload_pieces, seed):
+    """Sparse rows (col uploaded per piece) and u32 latencies, both families."""
+    n = 120
+    edges = synth.random_graph(n, 40 + seed, p_edge=0.08, lat_range_ns=(1, 50), loss_max=0.05)
+    _check(edges, np.arange(n, dtype=np.uint32), False, n, algo=_lib.SRT_ALGO_FW)
+    _check(edges, np.arange(0, n, 3, dtype=np.uint32), False, n, algo=_lib.SRT_ALGO_SSSP)
+
+
+def test_piece_upload_identity_rows(small_upload_pieces):
+    """A complete graph with self-loops, rows in node order: every piece's
+    col is written on the device, nothing uploaded."""
+    n = 70
+    row_ptr, col, lat, loss = synth.complete_csr(n, 44)
+    src = np.repeat(np.arange(n), n)
+    # the same graph as a directed edge list (both orientations): checked vs the oracle
+    t1 = _check((src, col, lat, loss), np.arange(n, dtype=np.uint32), True, n, algo=_lib.SRT_ALGO_FW)
+    g = NetworkGraph(n, np.arange(n, dtype=np.uint32), row_ptr, col, lat, loss, directed=False)
+    t = g.compute_shortest_paths(np.arange(n, dtype=np.uint32))
+    assert np.array_equal(t.latency_ns, t1.latency_ns)
+    assert np.array_equal(t.packet_loss.view(np.uint32), t1.packet_loss.view(np.uint32))
+
+
+def test_piece_upload_wide_latencies(small_upload_pieces):
+    """Latencies past 2^32 ns: those pieces send the caller's u64 array."""
+    n = 20
+    src, dst, lat, loss = synth.random_graph(n, 31, p_edge=0.3, lat_range_ns=(1, 2**31), loss_max=0.01)
+    lat = (lat.astype(np.uint64) << np.uint64(20)) + np.uint64(1)
+    _check((src, dst, lat, loss), np.arange(n, dtype=np.uint32), False, n, algo=_lib.SRT_ALGO_FW)
+
+
+def test_piece_upload_errors_in_reference_order(small_upload_pieces):
+    """The scan's checks are the same under the pipeline: a zero latency, a
+    missing self-loop."""
+    g = NetworkGraph.from_edges(2, [0, 1, 0], [0, 1, 1], [5, 5, 0], directed=False)
+    with pytest.raises(_lib.SrtError) as e:
+        g.compute_shortest_paths([0, 1])
+    assert e.value.code == _lib.SRT_ERR_INVALID and "must not be 0" in str(e.value)
+    n = 40
+    src, dst, lat, loss = synth.random_graph(n, 3, p_edge=0.3)
+    keep = ~((src == 8) & (dst == 8))
+    g = NetworkGraph.from_edges(n, src[keep], dst[keep], lat[keep], loss[keep])
+    with pytest.raises(_lib.SrtError) as e:
+        g.compute_shortest_paths(np.arange(n, dtype=np.uint32))
+    assert e.value.code == _lib.SRT_ERR_NO_EDGE and str(e.value) == "No edge connecting node 8 to 8"
