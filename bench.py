@@ -397,13 +397,25 @@ def bench_graph(args, cfg, D):
             algo = f"blocked Floyd-Warshall ({key} latency closure) + exact-loss fold over the tight DAG"
         else:
             achieved = work_per_launch / avg_launch_s
+            launches_per_step = k_launches // max(args.steps, 1)
+            sweeps_per_launch = timing["sparse_sweeps"] / max(launches_per_step, 1)
+            state = desc.split("state=")[1].split()[0] if "state=" in desc else "keys"
+            schedule = {"state": state, "words_per_lane": int(desc.split(" R=")[1].split()[0]) if " R=" in desc else 0}
+            per_sweep, traffic_src = measured_traffic(args, "(sssp_sweep)", schedule)
             roofline = {
                 "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK, "traffic": None,
-                "traffic_source": "PMC traffic of the sweep: profiles/*c4_pmc_traffic.json (per sweep launch)",
-                "kernel": "sssp_sweep_kernel (all sweeps of one 64-source batch group)",
-                "avg_group_ms": avg_launch_s * 1e3, "groups_per_step": k_launches // max(args.steps, 1),
-                "algorithmic_bytes_per_group": work_per_launch,
+                "frac": achieved / HBM_PEAK,
+                # one "launch" = every sweep of the groups in flight (groups x 64 R sources)
+                "traffic": per_sweep * sweeps_per_launch if per_sweep else None,
+                "traffic_unit": "HBM bytes per launch (PMC bytes per sweep dispatch x this run's sweeps per launch)",
+                "traffic_source": (f"{traffic_src}: committed rocprofv3 PMC summary of this workload and layout, "
+                                   f"not measured in this run" if traffic_src else
+                                   "no committed PMC summary for this workload/layout"),
+                "schedule": schedule,
+                "kernel": "sssp_sweep_kernel (all sweeps of one launch)",
+                "avg_launch_ms": avg_launch_s * 1e3, "launches_per_step": launches_per_step,
+                "sweeps_per_launch": sweeps_per_launch,
+                "algorithmic_bytes_per_launch": work_per_launch,
                 "basis": "12 B x (E_in + V) per source (SURVEY.md 8(d)), E_in = in-edges without self-loops"}
             algo = "batched sparse sweep"
         cpu = cpu_opt = None

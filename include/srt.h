@@ -157,6 +157,8 @@ typedef struct {
     uint32_t sparse_split;      /* sparse: 1 = the split sweep's table (u16 latency sweep, then the
                                    loss sweep over tight edges), 0 = the fused u64 sweep (the split
                                    one saturated or is turned off) */
+    uint64_t sparse_sweeps;     /* sparse: sweep launches of the last run, summed over its source
+                                   launches (each covers every group in flight) */
 } srt_timing;
 srt_status srt_plan_timing(const srt_plan *plan, srt_timing *out);
 /* C tiles (128 x 128 keys) the last FW run's dominant launches loaded and

@@ -1027,6 +1027,7 @@ srt_status srt_plan_timing(const srt_plan *p, srt_timing *o) {
     o->tight_edges = p->algo == SRT_ALGO_FW ? p->t_edges : 0;
     o->sharded_tail = p->algo == SRT_ALGO_FW && p->shard_tail ? 1u : 0u;
     o->sparse_split = p->algo == SRT_ALGO_SSSP && p->sssp_used_split ? 1u : 0u;
+    o->sparse_sweeps = p->algo == SRT_ALGO_SSSP ? p->sssp_sweeps : 0;
     return SRT_OK;
 }
 
