@@ -357,6 +357,7 @@ def bench_graph(args, cfg, D):
         plan.close()
         return None
     timing = plan.timing()  # phase breakdown of the last timed build
+    desc = plan.describe()  # after the runs: the first one adds what it measured (e.g. sym=triangle)
     plan.fetch(table=False)  # connectivity check + min latency (not timed)
     plan.close()
     n = len(nodes)

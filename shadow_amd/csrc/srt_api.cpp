@@ -449,6 +449,7 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_pack);
     hipFree(p->d_pack8);
     hipFree(p->d_up32);
+    hipFree(p->d_flag32);
     hipFree(p->d_draws);
     hipFree(p->d_in_ptr);
     hipFree(p->d_in_edge);
@@ -856,6 +857,10 @@ srt_status run_closure(srt_plan *p, srt_err *err) {
     // round leaves a closed D unchanged, and the kernels' cost does not
     // depend on the keys), so rank 0's loss-pass share sees valid keys
     if (!p->emu_closed) srt::fw_init(p);
+    if (!p->fw_sym_known) {
+        if (!p->d_flag32) HIP_TRY(hipMalloc(&p->d_flag32, 4), "hipMalloc(flag)");
+        if (srt_status st = srt::fw_sym_check(p, err); st != SRT_OK) return st;
+    }
     return srt::fw_rounds(p, err);
 }
 

@@ -967,13 +967,56 @@ __device__ __forceinline__ void chunk_steps16(uint32_t (&acc)[8][4], StepOps16 (
     }
 }
 
-template <int TAG>
+// Symmetric closures (undirected graphs: D == D^T at every round, see
+// fw_sym_check): a rest launch over a square span runs only the tiles with
+// span position pi <= pj and writes each off-diagonal result twice, as
+// (bi, bj) and transposed as (bj, bi) -- half the relaxations.  Grid order:
+// bands of up to 8 rows, band b = rows 8b .. 8b+7 x columns 8b .. m-1, a
+// column of 8 tiles after another (the banded order of tile_of); the
+// band's 28 below-diagonal slots exit at once.  The mirrored tile (bj, bi)
+// is never an operand the launch's grouping rule does not already allow to
+// be read mid-update (its row or column is in the group exactly when
+// (bi, bj)'s is), and the excluded next-group rows/cols are symmetric.
+__host__ __device__ inline uint32_t sym_grid(uint32_t m) {
+    uint32_t n = 0;
+    for (uint32_t b0 = 0; b0 < m; b0 += 8) n += std::min(8u, m - b0) * (m - b0);
+    return n;
+}
+__device__ __forceinline__ bool tile_of_sym(uint32_t t, const Span &s, uint32_t &bi, uint32_t &bj) {
+    const uint32_t n1 = gridDim.x;
+    if (n1 >= 64) {  // XCD-aware bijective remap, as tile_of
+        const uint32_t q = n1 / 8, rr = n1 % 8, xcd = t % 8;
+        t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + t / 8;
+    }
+    const uint32_t m = s.n;
+    uint32_t b0 = 0, base = 0, pi = 0, pj = 0;
+    for (; b0 < m; b0 += 8) {
+        const uint32_t rows = min(8u, m - b0), cnt = rows * (m - b0);
+        if (t < base + cnt) {
+            const uint32_t w = t - base;
+            pi = b0 + w % rows;
+            pj = b0 + w / rows;
+            break;
+        }
+        base += cnt;
+    }
+    if (pi > pj) return false;
+    bi = span_at(s, pi);
+    bj = span_at(s, pj);
+    return true;
+}
+
+template <int TAG, bool SYM = false>
 __global__ __launch_bounds__(NT3, 2) void minplus_u16_kernel(uint16_t *__restrict__ D, uint32_t Vp, uint32_t kb,
                                                              Rect r1, Rect r2, uint32_t ng) {
     __shared__ __attribute__((aligned(16))) uint16_t lds[2 * GBUF16];
     if constexpr (TAG != 0) __builtin_amdgcn_s_setprio(2);  // look-ahead chain: issue priority
     uint32_t bi, bj;
-    tile_of(blockIdx.x, r1, r2, ng, bi, bj);
+    if constexpr (SYM) {
+        if (!tile_of_sym(blockIdx.x, r1.r, bi, bj)) return;  // workgroup-uniform, before any barrier
+    } else {
+        tile_of(blockIdx.x, r1, r2, ng, bi, bj);
+    }
     // grouped rounds (see minplus_glds_kernel)
     const uint32_t ng_ = ng & 0xffffu;
     int ch0 = 0;
@@ -1050,6 +1093,52 @@ __global__ __launch_bounds__(NT3, 2) void minplus_u16_kernel(uint16_t *__restric
         v.w = acc[i][3];
         *reinterpret_cast<u32x4 *>(D + (i0 + ty + 16 * i) * Vp + j0 + tx * 8) = v;
     }
+    if constexpr (SYM) {
+        if (bi != bj) {
+            // the mirror tile: transpose through LDS ([128][129] u16 = the two
+            // stage buffers, idle since the last chunk's barrier; row stride 129
+            // spreads a wave's 16 column groups over 16 banks)
+            constexpr int LT = B + 1;
+            static_assert(B * LT <= 2 * GBUF16, "transpose image fits the stage buffers");
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    const int r = ty + 16 * i, c = tx * 8 + 2 * p;
+                    lds[c * LT + r] = (uint16_t)(acc[i][p] & 0xffffu);
+                    lds[(c + 1) * LT + r] = (uint16_t)(acc[i][p] >> 16);
+                }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int c = ty + 16 * i;  // row of the mirror tile
+                const uint16_t *src = lds + c * LT + tx * 8;
+                u32x4 v;
+                v.x = (uint32_t)src[0] | ((uint32_t)src[1] << 16);
+                v.y = (uint32_t)src[2] | ((uint32_t)src[3] << 16);
+                v.z = (uint32_t)src[4] | ((uint32_t)src[5] << 16);
+                v.w = (uint32_t)src[6] | ((uint32_t)src[7] << 16);
+                *reinterpret_cast<u32x4 *>(D + (j0 + c) * Vp + i0 + tx * 8) = v;
+            }
+        }
+    }
+}
+
+// D == D^T?  One 64 x 64 tile pair per workgroup, through LDS; any mismatch
+// clears *sym (set to 1 beforehand).  Only blocks on or above the diagonal.
+template <typename K>
+__global__ __launch_bounds__(256) void sym_check_kernel(const K *__restrict__ D, uint32_t Vp, uint32_t nb,
+                                                        uint32_t *sym) {
+    __shared__ K t[64][65];
+    const uint32_t bi = blockIdx.y, bj = blockIdx.x;
+    if (bi > bj) return;
+    const int tid = threadIdx.x;
+    const uint64_t i0 = (uint64_t)bi * 64, j0 = (uint64_t)bj * 64;
+    for (int e = tid; e < 64 * 64; e += 256) t[e / 64][e % 64] = D[(j0 + e / 64) * Vp + i0 + e % 64];
+    __syncthreads();
+    bool ok = true;
+    for (int e = tid; e < 64 * 64; e += 256) ok &= D[(i0 + e / 64) * Vp + j0 + e % 64] == t[e % 64][e / 64];
+    if (!ok) *sym = 0;  // every writer stores 0
 }
 
 // Latency-oriented variant for the look-ahead chain of the sharded schedule
@@ -1452,6 +1541,9 @@ void launch_group(srt_plan *p, hipStream_t s, uint32_t a, uint32_t g, const Rect
     if constexpr (sizeof(K) == 2) {
         if (chain)
             hipLaunchKernelGGL((minplus_u16_kernel<5>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
+        else if (p->fw_sym)  // square span, r2 empty (fw_rounds_group_t)
+            hipLaunchKernelGGL((minplus_u16_kernel<0, true>), dim3(sym_grid(r1.r.n)), dim3(NT3), 0, s, D, p->Vp, a,
+                               r1, r2, arg);
         else
             hipLaunchKernelGGL((minplus_u16_kernel<0>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
     } else if constexpr (sizeof(K) == 4) {
@@ -1468,6 +1560,8 @@ void launch_group(srt_plan *p, hipStream_t s, uint32_t a, uint32_t g, const Rect
             hipLaunchKernelGGL((minplus_glds_kernel<K, 0>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
     }
 }
+
+void group_work_sym(const Span &r, uint32_t a, uint32_t g, double &work, double &tiles);
 
 template <typename K>
 srt_status fw_rounds_group_t(srt_plan *p, int p1r, uint32_t g) {
@@ -1519,6 +1613,11 @@ srt_status fw_rounds_group_t(srt_plan *p, int p1r, uint32_t g) {
             work += cnt * (g - 1 - q);
             tiles += cnt;
         }
+        if (p->fw_sym && sizeof(K) == 2) {
+            // the triangle actually run: pi <= pj (a tile computed once, stored twice)
+            work = tiles = 0.0;
+            group_work_sym(all.r, a, g, work, tiles);
+        }
         p->p3_work += work * B * B * B;
         p->p3_tiles += (uint64_t)tiles;
         if (nxt) {
@@ -1530,6 +1629,23 @@ srt_status fw_rounds_group_t(srt_plan *p, int p1r, uint32_t g) {
         }
     }
     return SRT_OK;
+}
+
+// group_work over the symmetric launch's tiles pi <= pj of the square span r
+void group_work_sym(const Span &r, uint32_t a, uint32_t g, double &work, double &tiles) {
+    for (uint32_t i = 0; i < r.n; ++i) {
+        const uint32_t bi = span_at(r, i);
+        for (uint32_t j = i; j < r.n; ++j) {
+            const uint32_t bj = span_at(r, j);
+            const bool ii = bi - a < g, jj = bj - a < g;
+            uint32_t rounds = g;
+            if (ii || jj) rounds = g - 1 - std::max(ii ? bi - a : 0u, jj ? bj - a : 0u);
+            if (rounds) {
+                work += rounds;
+                tiles += 1;
+            }
+        }
+    }
 }
 
 // Tiles and relaxations of a grouped launch over rows x cols for the group
@@ -1662,6 +1778,35 @@ srt_status fw_rounds_group_sharded_t(srt_plan *p, int p1r, uint32_t g, uint32_t 
 }
 
 }  // namespace
+
+// Once per plan, after the first init (one GPU, u16 keys, knob SRT_FW_SYM=0
+// off): is the initial D symmetric?  FW keeps a symmetric D symmetric, so
+// every later round may then run the triangle (minplus_u16_kernel<0, true>).
+srt_status fw_sym_check(srt_plan *p, srt_err *err) {
+    p->fw_sym_known = true;
+    p->fw_sym = false;
+    if (p->comm || p->emulate_ranks > 1 || p->key_type != KEY_U16) return SRT_OK;
+    if (const char *e = std::getenv("SRT_FW_SYM"); e && std::atoi(e) == 0) return SRT_OK;
+    const uint32_t nb = p->Vp / 64;
+    uint32_t one = 1, h = 0;
+    hipError_t e = hipMemcpyAsync(p->d_flag32, &one, 4, hipMemcpyHostToDevice, p->stream);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(sym_check_kernel<uint16_t>, dim3(nb, nb), dim3(256), 0, p->stream,
+                           reinterpret_cast<const uint16_t *>(p->d_D), p->Vp, nb, p->d_flag32);
+        e = hipMemcpyAsync(&h, p->d_flag32, 4, hipMemcpyDeviceToHost, p->stream);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
+    if (e != hipSuccess) {
+        if (err) {
+            err->code = SRT_ERR_HIP;
+            std::snprintf(err->msg, sizeof err->msg, "symmetry check: %s", hipGetErrorString(e));
+        }
+        return SRT_ERR_HIP;
+    }
+    p->fw_sym = h != 0;
+    if (p->fw_sym) p->desc += " sym=triangle";
+    return SRT_OK;
+}
 
 void fw_init(srt_plan *p) {
     if (p->key_type == KEY_U16) fw_init_t<uint16_t>(p);

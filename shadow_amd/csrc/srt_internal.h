@@ -79,6 +79,9 @@ struct srt_plan {
     bool fw_glds = true;   // FW tiles staged by LDS-DMA (false: register staging)
     bool fw_small_chain = false;  // quarter-tile kernels for the look-ahead chain (sharded)
     bool fw_unique_edges = false; // no parallel edges: FW init stores instead of atomic min
+    bool fw_sym = false;          // D symmetric (fw_sym_check): rest launches run the triangle
+    bool fw_sym_known = false;
+    uint32_t *d_flag32 = nullptr; // device scratch flag (symmetry check)
     int fw_relax = 0;             // u32 rest kernel relax order (SRT_FW_RELAX, A/B)
     uint32_t fw_ablate = 0;       // measurement only: u32 rest-kernel ablations (SRT_FW_ABLATE, see the kernel)
     bool fw_band = true;          // grouped launches: banded tile order (knob SRT_FW_BAND=0, read at create)
@@ -222,6 +225,7 @@ srt_status comm_allgather_inplace(srt_comm *c, void *buf, size_t bytes_per_rank,
                                   srt_err *err);
 // kernels (srt_fw.hip)
 void fw_init(srt_plan *p);
+srt_status fw_sym_check(srt_plan *p, srt_err *err);
 srt_status fw_rounds(srt_plan *p, srt_err *err);
 // sharded closure: every rank's block-rows of D to every rank (the loss
 // pass's fallback when the sharded tail does not apply)

@@ -103,3 +103,47 @@ def test_key_types_agree(monkeypatch, n, seed, directed):
     for k, t in tabs.items():
         assert np.array_equal(t.latency_ns, ref.latency_ns), k
         assert np.array_equal(t.packet_loss.view(np.uint32), ref.packet_loss.view(np.uint32)), k
+
+
+@pytest.mark.parametrize("n,complete", [(8192, True), (1500, False)])
+def test_symmetric_triangle_equals_full(monkeypatch, n, complete):
+    """Undirected graph, u16 keys, grouped schedule: the rest launches run only
+    the tiles on or above the diagonal and store each result twice
+    (minplus_u16_kernel<0, true>); the table must be bit-identical to the
+    full-square schedule (SRT_FW_SYM=0), and the plan must report the
+    triangle.  8192 = 64 blocks (g = 2, no quarter-tile chain); 1500 forced
+    to g = 4."""
+    if complete:
+        row_ptr, col, lat, loss = synth.complete_csr(n, 8)
+        g = NetworkGraph(n, np.arange(n, dtype=np.uint32), row_ptr, col, lat, loss, directed=False)
+    else:
+        monkeypatch.setenv("SRT_FW_PAIR", "1")
+        monkeypatch.setenv("SRT_FW_GROUP", "4")
+        e = synth.random_graph(n, 77, p_edge=8.0 / n, lat_range_ns=(1, 6), loss_max=0.05)
+        g = NetworkGraph.from_edges(n, *e, directed=False)
+    nodes = np.arange(n, dtype=np.uint32)
+    tabs = []
+    for sym in ("1", "0"):
+        monkeypatch.setenv("SRT_FW_SYM", sym)
+        plan = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_FW)
+        try:
+            plan.run()
+            desc = plan.describe()
+            tabs.append(plan.fetch())
+        finally:
+            plan.close()
+        assert ("sym=triangle" in desc) == (sym == "1"), desc
+    assert np.array_equal(tabs[0].latency_ns, tabs[1].latency_ns)
+    assert np.array_equal(tabs[0].packet_loss.view(np.uint32), tabs[1].packet_loss.view(np.uint32))
+
+
+def test_directed_graph_keeps_the_full_square():
+    n = 1000
+    e = synth.random_graph(n, 78, p_edge=8.0 / n, directed=True, lat_range_ns=(1, 6), loss_max=0.05)
+    g = NetworkGraph.from_edges(n, *e, directed=True)
+    plan = RoutingPlan(g, np.arange(n, dtype=np.uint32), algo=_lib.SRT_ALGO_FW)
+    try:
+        plan.run()
+        assert "sym=triangle" not in plan.describe()
+    finally:
+        plan.close()
