@@ -1006,13 +1006,17 @@ __device__ __forceinline__ bool tile_of_sym(uint32_t t, const Span &s, uint32_t 
     return true;
 }
 
-template <int TAG, bool SYM = false>
+// SYM: 0 = the rect(s) as given; 1 = the triangle of the square span r1.r
+// (rest launches); 2 = the rect(s) as given, each off-diagonal result also
+// stored transposed (the symmetric chain: p2row also writes p2col's tiles,
+// one cross rect also writes the other).
+template <int TAG, int SYM = 0>
 __global__ __launch_bounds__(NT3, 2) void minplus_u16_kernel(uint16_t *__restrict__ D, uint32_t Vp, uint32_t kb,
                                                              Rect r1, Rect r2, uint32_t ng) {
     __shared__ __attribute__((aligned(16))) uint16_t lds[2 * GBUF16];
     if constexpr (TAG != 0) __builtin_amdgcn_s_setprio(2);  // look-ahead chain: issue priority
     uint32_t bi, bj;
-    if constexpr (SYM) {
+    if constexpr (SYM == 1) {
         if (!tile_of_sym(blockIdx.x, r1.r, bi, bj)) return;  // workgroup-uniform, before any barrier
     } else {
         tile_of(blockIdx.x, r1, r2, ng, bi, bj);
@@ -1093,7 +1097,7 @@ __global__ __launch_bounds__(NT3, 2) void minplus_u16_kernel(uint16_t *__restric
         v.w = acc[i][3];
         *reinterpret_cast<u32x4 *>(D + (i0 + ty + 16 * i) * Vp + j0 + tx * 8) = v;
     }
-    if constexpr (SYM) {
+    if constexpr (SYM != 0) {
         if (bi != bj) {
             // the mirror tile: transpose through LDS ([128][129] u16 = the two
             // stage buffers, idle since the last chunk's barrier; row stride 129
@@ -1328,6 +1332,20 @@ void launch_tiles(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1, const
                            reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2);
 }
 
+// One rect of chain tiles that also stores each off-diagonal result
+// transposed (symmetric D, u16 keys): the mirror of a phase-2 row tile is the
+// phase-2 column tile, so p2col needs no launch; in a cross rect the
+// corner's tiles appear with their mirrors, both writing the same bits.
+template <typename K, int TAG>
+void launch_mirror(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1) {
+    const uint32_t n = r1.r.n * r1.c.n;
+    if (!n) return;
+    if constexpr (sizeof(K) == 2)
+        hipLaunchKernelGGL((minplus_u16_kernel<TAG, 2>), dim3(n), dim3(NT3), 0, s,
+                           reinterpret_cast<uint16_t *>(p->d_D), p->Vp, kb, r1,
+                           Rect{make_span(0, 0), make_span(0, 0)}, 1u);
+}
+
 // Round schedule with one block of look-ahead, per rank (block-rows [rb0,rb1)):
 //   main stream M:  (wait pivot kb) rest(kb) | (wait pivot kb+1) rest(kb+1) | ...
 //   side stream S:  (after rest(kb-1))  cross(kb), p1(kb+1), p2row(kb+1) on
@@ -1539,10 +1557,13 @@ void launch_group(srt_plan *p, hipStream_t s, uint32_t a, uint32_t g, const Rect
     // bit 16: banded tile order (plan knob SRT_FW_BAND=0 turns it off for A/B timing)
     const uint32_t arg = g | (p->fw_band ? 0x10000u : 0u) | (chain ? 0u : p->fw_ablate << 20);
     if constexpr (sizeof(K) == 2) {
-        if (chain)
+        if (chain && p->fw_sym)  // r1 only; its transposes are r2 (fw_rounds_group_t)
+            hipLaunchKernelGGL((minplus_u16_kernel<5, 2>), dim3(r1.r.n * r1.c.n), dim3(NT3), 0, s, D, p->Vp, a, r1,
+                               Rect{make_span(0, 0), make_span(0, 0)}, arg);
+        else if (chain)
             hipLaunchKernelGGL((minplus_u16_kernel<5>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
         else if (p->fw_sym)  // square span, r2 empty (fw_rounds_group_t)
-            hipLaunchKernelGGL((minplus_u16_kernel<0, true>), dim3(sym_grid(r1.r.n)), dim3(NT3), 0, s, D, p->Vp, a,
+            hipLaunchKernelGGL((minplus_u16_kernel<0, 1>), dim3(sym_grid(r1.r.n)), dim3(NT3), 0, s, D, p->Vp, a,
                                r1, r2, arg);
         else
             hipLaunchKernelGGL((minplus_u16_kernel<0>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
@@ -1570,9 +1591,18 @@ srt_status fw_rounds_group_t(srt_plan *p, int p1r, uint32_t g) {
     hipStream_t M = p->stream, S = p->side_stream;
     const Rect none{make_span(0, 0), make_span(0, 0)};
     // the pivots of group a on stream s (rows/cols a .. a+g-1 already hold rounds < a)
+    // symmetric D (u16 keys, see fw_sym_check): p2row also stores p2col's
+    // tiles transposed, and the cross runs one rect and stores the other
+    const bool symc = p->fw_sym && sizeof(K) == 2 && !p->fw_small_chain;
     auto pivots = [&](hipStream_t s, uint32_t a) {
         for (uint32_t r = a; r < a + g; ++r) {
             launch_p1<K>(p1r, s, D, p->Vp, r);
+            if (symc) {
+                launch_mirror<K, 1>(p, s, r, Rect{make_span(r, r + 1), make_span(0, nblk, r)});
+                if (r + 1 < a + g)
+                    launch_mirror<K, 4>(p, s, r, Rect{make_span(0, nblk, r), make_range(r + 1, a + g, NONE, NONE)});
+                continue;
+            }
             launch_tiles<K, 1>(p, s, r, Rect{make_span(r, r + 1), make_span(0, nblk, r)}, none);
             launch_tiles<K, 2>(p, s, r, Rect{make_span(0, nblk, r), make_span(r, r + 1)}, none);
             if (r + 1 < a + g)  // round r on rows/cols r+1 .. a+g-1 (the corner twice: idempotent)
