@@ -376,7 +376,8 @@ def bench_graph(args, cfg, D):
             kbytes = {"u16": 2, "u32": 4}.get(key, 8)
             achieved = work_per_launch / avg_launch_s
             rounds = k_work / max(k_tiles * B_TILE ** 3, 1)
-            schedule = {"key": key, "launch_rounds": int(round(rounds)), "ranks": D.world}
+            schedule = {"key": key, "launch_rounds": int(round(rounds)), "ranks": D.world,
+                        "tiles": "triangle" if "sym=triangle" in desc else "square"}
             traffic, traffic_src = measured_traffic(args, "(phase 3 rest)", schedule)
             peak = RELAX_PEAK[key]
             roofline = {
@@ -387,8 +388,10 @@ def bench_graph(args, cfg, D):
                                    f"not measured in this run" if traffic_src else
                                    "no committed PMC summary for this workload/schedule"),
                 "schedule": schedule,
-                # every C tile read + written once per launch (A/B panels hit L2/MALL)
-                "algorithmic_hbm_bytes_per_launch": k_tiles / max(k_launches, 1) * B_TILE * B_TILE * 2 * kbytes,
+                # every C tile read + written once per launch (A/B panels hit L2/MALL);
+                # triangle launches also write each off-diagonal tile's mirror
+                "algorithmic_hbm_bytes_per_launch": k_tiles / max(k_launches, 1) * B_TILE * B_TILE * kbytes *
+                                                    (3 if "sym=triangle" in desc else 2),
                 "rounds_per_tile": rounds,
                 "kernel": f"minplus_{key if key in ('u16', 'u32') else 'glds'}_kernel<0> (FW phase 3, rest)",
                 "avg_launch_ms": avg_launch_s * 1e3, "relax_per_launch": work_per_launch,

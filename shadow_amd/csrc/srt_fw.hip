@@ -1332,6 +1332,15 @@ void launch_tiles(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1, const
                            reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2);
 }
 
+// A single round's rest over a square span, as its triangle (u16 keys)
+template <typename K>
+void launch_rest_sym(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1) {
+    if constexpr (sizeof(K) == 2)
+        hipLaunchKernelGGL((minplus_u16_kernel<0, 1>), dim3(sym_grid(r1.r.n)), dim3(NT3), 0, s,
+                           reinterpret_cast<uint16_t *>(p->d_D), p->Vp, kb, r1,
+                           Rect{make_span(0, 0), make_span(0, 0)}, 1u);
+}
+
 // One rect of chain tiles that also stores each off-diagonal result
 // transposed (symmetric D, u16 keys): the mirror of a phase-2 row tile is the
 // phase-2 column tile, so p2col needs no launch; in a cross rect the
@@ -1465,18 +1474,23 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
         // rest(kb): local rows and all columns, minus kb and (look-ahead) k1
         Rect rest{make_span(rb0, rb1, kb, nxt ? k1 : NONE), make_span(0, nblk, kb, nxt ? k1 : NONE)};
         const uint32_t nt = rest.r.n * rest.c.n;
+        // symmetric D on one GPU: the rest runs its triangle (see minplus_u16_kernel)
+        const bool tri = p->fw_sym && sizeof(K) == 2 && !sharded && !emu && p->fw_glds;
         if (nt && kb % ev_every == 0) {
             hipEventRecord(p->ev[2 * p->p3_launches], M);
-            launch_tiles<K, 0>(p, M, kb, rest, none);
+            if (tri) launch_rest_sym<K>(p, M, kb, rest);
+            else launch_tiles<K, 0>(p, M, kb, rest, none);
             // the timing event after rest(kb) doubles as S's hand-off (one
             // event packet fewer per round on the main stream)
             rest_done = p->ev[2 * p->p3_launches + 1];
             hipEventRecord(rest_done, M);
             p->p3_launches++;
-            p->p3_work += (double)nt * B * B * B;
-            p->p3_tiles += nt;
+            const double run = tri ? (double)rest.r.n * (rest.r.n + 1) / 2 : (double)nt;  // tiles run
+            p->p3_work += run * B * B * B;
+            p->p3_tiles += (uint64_t)run;
         } else {
-            if (nt) launch_tiles<K, 0>(p, M, kb, rest, none);
+            if (nt && tri) launch_rest_sym<K>(p, M, kb, rest);
+            else if (nt) launch_tiles<K, 0>(p, M, kb, rest, none);
             if (nxt) {
                 hipEventRecord(p->ev_cross, M);
                 rest_done = p->ev_cross;
