@@ -450,6 +450,11 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_pack8);
     hipFree(p->d_up32);
     hipFree(p->d_flag32);
+    hipFree(p->d_tl_all);
+    hipFree(p->d_tl_cnt);
+    hipFree(p->d_tl_cross);
+    hipFree(p->d_rowslots);
+    hipFree(p->d_fbuf);
     hipFree(p->d_draws);
     hipFree(p->d_in_ptr);
     hipFree(p->d_in_edge);

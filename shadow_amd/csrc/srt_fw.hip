@@ -278,6 +278,72 @@ __global__ __launch_bounds__(16 * (B / P1R)) void fw_phase1_kernel(K *__restrict
     }
 }
 
+// Phase 1 for u16 keys: the layout of fw_phase1_kernel<uint16_t, 8> with each
+// thread's 8 columns as 4 packed pairs, relaxed by v_pk_add_u16 +
+// v_pk_min_u16 (a broadcast to both halves): a third of the scalar u16
+// version's VALU (add, min, and the u16 widening) per step.  Sums stay below
+// 2^16 (both operands <= KEY16_INF), so the packed add never wraps.
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(256) void fw_phase1_u16pk_kernel(uint16_t *__restrict__ D, uint32_t Vp, uint32_t kb) {
+    __shared__ us2 rowbuf[2][B / 2];
+    __shared__ uint16_t colbuf[2][B];
+    __builtin_amdgcn_s_setprio(3);  // critical path of the look-ahead chain
+    const int tid = threadIdx.x, tx = tid % 16, ty = tid / 16;
+    const uint64_t k0 = (uint64_t)kb * B;
+    us2 p[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(D + (k0 + ty * 8 + i) * Vp + k0 + tx * 8);
+        p[i][0] = __builtin_bit_cast(us2, v.x);
+        p[i][1] = __builtin_bit_cast(us2, v.y);
+        p[i][2] = __builtin_bit_cast(us2, v.z);
+        p[i][3] = __builtin_bit_cast(us2, v.w);
+    }
+    // step k = 8g + e: row k in thread-row g at element e, column k in
+    // thread-column g at element e (pair e / 2, half e % 2)
+    auto publish = [&](int g, int e, int buf) {
+        if (ty == g) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rowbuf[buf][tx * 4 + q] = p[e][q];
+        }
+        if (tx == g) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) colbuf[buf][ty * 8 + i] = p[i][e / 2][e % 2];
+        }
+    };
+    publish(0, 0, 0);
+    __syncthreads();
+#pragma unroll 1
+    for (int g = 0; g < B / 8; ++g) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int cur = e & 1;
+            us2 b[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) b[q] = rowbuf[cur][tx * 4 + q];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint16_t a = colbuf[cur][ty * 8 + i];
+                const us2 a2 = {a, a};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) p[i][q] = __builtin_elementwise_min(p[i][q], a2 + b[q]);
+            }
+            if (e < 7) publish(g, e + 1, cur ^ 1);
+            else if (g + 1 < B / 8) publish(g + 1, 0, cur ^ 1);
+            __syncthreads();
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint4 v;
+        v.x = __builtin_bit_cast(uint32_t, p[i][0]);
+        v.y = __builtin_bit_cast(uint32_t, p[i][1]);
+        v.z = __builtin_bit_cast(uint32_t, p[i][2]);
+        v.w = __builtin_bit_cast(uint32_t, p[i][3]);
+        *reinterpret_cast<uint4 *>(D + (k0 + ty * 8 + i) * Vp + k0 + tx * 8) = v;
+    }
+}
+
 // ------------------------------------------------------ phases 2 and 3
 // Every min-plus update of a round is C(bi,bj) <- min(C, A(bi,kb) (x) Bm(kb,bj)):
 //   phase 2 row:  bi = kb  (A = P*, Bm aliases C);
@@ -1018,6 +1084,15 @@ __global__ __launch_bounds__(NT3, 2) void minplus_u16_kernel(uint16_t *__restric
     uint32_t bi, bj;
     if constexpr (SYM == 1) {
         if (!tile_of_sym(blockIdx.x, r1.r, bi, bj)) return;  // workgroup-uniform, before any barrier
+    } else if constexpr (SYM == 3) {
+        // tile list (symmetric sharded schedule): the list's device address in
+        // r2.r.lo / r2.r.hi, entries (i << 16) | j; tiles in row or column
+        // r1.r.x0 or r1.r.x1 (this round's pivot and look-ahead) are skipped
+        const uint32_t *tl = reinterpret_cast<const uint32_t *>(((uint64_t)r2.r.hi << 32) | r2.r.lo);
+        const uint32_t e = tl[blockIdx.x];
+        bi = e >> 16;
+        bj = e & 0xffffu;
+        if (bi == r1.r.x0 || bj == r1.r.x0 || bi == r1.r.x1 || bj == r1.r.x1) return;
     } else {
         tile_of(blockIdx.x, r1, r2, ng, bi, bj);
     }
@@ -1097,7 +1172,7 @@ __global__ __launch_bounds__(NT3, 2) void minplus_u16_kernel(uint16_t *__restric
         v.w = acc[i][3];
         *reinterpret_cast<u32x4 *>(D + (i0 + ty + 16 * i) * Vp + j0 + tx * 8) = v;
     }
-    if constexpr (SYM != 0) {
+    if constexpr (SYM == 1 || SYM == 2) {
         if (bi != bj) {
             // the mirror tile: transpose through LDS ([128][129] u16 = the two
             // stage buffers, idle since the last chunk's barrier; row stride 129
@@ -1143,6 +1218,73 @@ __global__ __launch_bounds__(256) void sym_check_kernel(const K *__restrict__ D,
     bool ok = true;
     for (int e = tid; e < 64 * 64; e += 256) ok &= D[(i0 + e / 64) * Vp + j0 + e % 64] == t[e % 64][e / 64];
     if (!ok) *sym = 0;  // every writer stores 0
+}
+
+// ---------------------------------------------------- symmetric sharded schedule
+// u16 128 x 128 tile moves through LDS (256 threads, one tile per workgroup):
+// dst <- src, or src^T.  Row strides in keys.
+__device__ __forceinline__ void move_tile16(const uint16_t *__restrict__ src, uint64_t ss, uint16_t *__restrict__ dst,
+                                            uint64_t ds, bool transpose, uint16_t (*t)[B + 1]) {
+    const int tid = threadIdx.x;
+    if (!transpose) {
+        for (int e = tid; e < B * B / 8; e += 256) {  // 8 keys (16 B) per thread-step
+            const int r = e / (B / 8), c = (e % (B / 8)) * 8;
+            *reinterpret_cast<u32x4 *>(dst + r * ds + c) = *reinterpret_cast<const u32x4 *>(src + r * ss + c);
+        }
+        return;
+    }
+    for (int e = tid; e < B * B; e += 256) t[e / B][e % B] = src[(e / B) * ss + e % B];
+    __syncthreads();
+    for (int e = tid; e < B * B; e += 256) dst[(e / B) * ds + e % B] = t[e % B][e / B];
+}
+
+// Own tiles of row/column k (list entries (i << 16) | j with i == k or j == k)
+// into this rank's all-gather slot, as row-k tiles: tile (k, c) at slot index
+// c / N (its owner is (k + c) mod N, so the indices are distinct); a tile
+// stored as (c, k), c < k, moves transposed.
+__global__ __launch_bounds__(256) void pack_row16_kernel(const uint16_t *__restrict__ D, uint32_t Vp,
+                                                         const uint32_t *__restrict__ tl, uint32_t k, uint32_t N,
+                                                         uint16_t *__restrict__ slot) {
+    __shared__ uint16_t t[B][B + 1];
+    const uint32_t e = tl[blockIdx.x], i = e >> 16, j = e & 0xffffu;
+    const uint32_t c = i == k ? j : i;
+    move_tile16(D + (uint64_t)i * B * Vp + (uint64_t)j * B, Vp, slot + (uint64_t)(c / N) * B * B, B, i != k, t);
+}
+
+// Row k assembled from every rank's slot (S tiles each): tile (k, c) from
+// rank (k + c) mod N, index c / N.
+__global__ __launch_bounds__(256) void unpack_row16_kernel(uint16_t *__restrict__ row, uint32_t Vp, uint32_t k,
+                                                           uint32_t N, uint32_t S, const uint16_t *__restrict__ slots) {
+    __shared__ uint16_t t[B][B + 1];
+    const uint32_t c = blockIdx.x;  // row = block-row k of D (B x Vp keys)
+    const uint16_t *src = slots + ((uint64_t)((k + c) % N) * S + c / N) * B * B;
+    move_tile16(src, B, row + (uint64_t)c * B, Vp, false, t);
+}
+
+// Every tile of a list into consecutive slots (the final exchange)
+__global__ __launch_bounds__(256) void pack_list16_kernel(const uint16_t *__restrict__ D, uint32_t Vp,
+                                                          const uint32_t *__restrict__ tl, uint16_t *__restrict__ buf) {
+    __shared__ uint16_t t[B][B + 1];
+    const uint32_t e = tl[blockIdx.x], i = e >> 16, j = e & 0xffffu;
+    move_tile16(D + (uint64_t)i * B * Vp + (uint64_t)j * B, Vp, buf + (uint64_t)blockIdx.x * B * B, B, false, t);
+}
+
+// Rank blockIdx.y's tiles (its list: lists + y * tmax, cnt[y] entries) from
+// its buffer into D, each off-diagonal one also transposed into its mirror
+__global__ __launch_bounds__(256) void unpack_list16_kernel(uint16_t *__restrict__ D, uint32_t Vp,
+                                                            const uint32_t *__restrict__ lists,
+                                                            const uint32_t *__restrict__ cnt, uint32_t tmax,
+                                                            const uint16_t *__restrict__ bufs, uint32_t emu) {
+    __shared__ uint16_t t[B][B + 1];
+    const uint32_t r = emu ? 0u : blockIdx.y, x = blockIdx.x;  // emulation: rank 0's tiles, N times
+    if (x >= cnt[r]) return;
+    const uint32_t e = lists[(uint64_t)r * tmax + x], i = e >> 16, j = e & 0xffffu;
+    const uint16_t *src = bufs + ((uint64_t)r * tmax + x) * B * B;
+    move_tile16(src, B, D + (uint64_t)i * B * Vp + (uint64_t)j * B, Vp, false, t);
+    if (i != j) {
+        __syncthreads();
+        move_tile16(src, B, D + (uint64_t)j * B * Vp + (uint64_t)i * B, Vp, true, t);
+    }
 }
 
 // Latency-oriented variant for the look-ahead chain of the sharded schedule
@@ -1281,7 +1423,10 @@ void fw_init_t(srt_plan *p) {
     K *D = reinterpret_cast<K *>(p->d_D);
     // sharded: only the local block-rows -- every other row this rank ever
     // reads arrives whole first (pivot-row broadcasts, the final all-gather)
-    const uint32_t r0 = p->comm ? p->rb0 * B : 0, r1 = p->comm ? p->rb1 * B : p->Vp;
+    // (the symmetric sharded schedule needs every row: fw_sym_check runs on
+    // the first build's full init, and symmetric plans keep it)
+    const bool local = p->comm && !(sizeof(K) == 2 && (p->fw_sym || !p->fw_sym_known));
+    const uint32_t r0 = local ? p->rb0 * B : 0, r1 = local ? p->rb1 * B : p->Vp;
     const uint32_t u0 = std::min(r0, p->V), u1 = std::min(r1, p->V);
     hipLaunchKernelGGL(fill_kernel<K>, dim3(4096), dim3(256), 0, p->stream, D, p->Vp, r0, r1);
     if (p->fw_unique_edges)
@@ -1301,6 +1446,13 @@ __global__ void delay_kernel(long long ticks) {
 
 template <typename K>
 void launch_p1(int rows, hipStream_t s, K *D, uint32_t Vp, uint32_t kb) {
+    if constexpr (sizeof(K) == 2) {
+        if (rows == 8 && !std::getenv("SRT_FW_P1_SCALAR")) {
+            hipLaunchKernelGGL(fw_phase1_u16pk_kernel, dim3(1), dim3(256), 0, s, reinterpret_cast<uint16_t *>(D), Vp,
+                               kb);
+            return;
+        }
+    }
     if (rows == 2)
         hipLaunchKernelGGL((fw_phase1_kernel<K, 2>), dim3(1), dim3(16 * (B / 2)), 0, s, D, Vp, kb);
     else if (rows == 4)
@@ -1375,6 +1527,167 @@ template <typename K>
 srt_status fw_rounds_group_sharded_t(srt_plan *p, int p1r, uint32_t g, uint32_t rb0, uint32_t rb1, bool emu,
                                      long long emu_bcast_ticks, srt_err *err);
 
+// Symmetric D on N ranks (u16 keys): the triangle's tiles (i, j), i <= j,
+// are dealt to ranks by (i + j) mod N -- every block-row then has
+// ceil(nblk / N) or fewer tiles on each rank, and every rank ~1/N of the
+// triangle.  Each rank keeps a full D; its own tiles are current, the rest
+// only where a round needs them.  Per round kb (k1 = kb + 1):
+//   M: rest(kb) over the own list, minus rows/cols kb and k1 (operands: row kb
+//      and its mirror, column kb, both complete on every rank);
+//   S: cross(kb) = own tiles in row/col k1, round kb; pack them into this
+//      rank's slot as row-k1 tiles; C: all-gather the slots (ceil(nblk/N)
+//      tiles a rank); S: unpack row k1 from all slots, p1(k1) and p2row(k1)
+//      with its mirror (column k1) -- the same bits on every rank.
+// After the last round the own tiles are all-gathered and written with their
+// mirrors, so every rank holds the whole closure (the sharded loss tail then
+// reads its own rows).  Half the relaxations of the row-sharded schedule,
+// one all-gather of ceil(nblk/N) tiles a round instead of a broadcast of
+// nblk.  The prologue needs no exchange: every rank starts from the same
+// full initial D.
+srt_status sym_sharded_setup(srt_plan *p, uint32_t N, uint32_t r, srt_err *err) {
+    if (p->d_tl_all) return SRT_OK;
+    const uint32_t nblk = p->Vp / B;
+    std::vector<std::vector<uint32_t>> lists(N);
+    for (uint32_t i = 0; i < nblk; ++i)
+        for (uint32_t j = i; j < nblk; ++j) lists[(i + j) % N].push_back((i << 16) | j);
+    uint32_t tmax = 0;
+    for (auto &l : lists) tmax = std::max<uint32_t>(tmax, (uint32_t)l.size());
+    std::vector<uint32_t> all((size_t)N * tmax, 0), cnt(N);
+    for (uint32_t q = 0; q < N; ++q) {
+        cnt[q] = (uint32_t)lists[q].size();
+        std::copy(lists[q].begin(), lists[q].end(), all.begin() + (size_t)q * tmax);
+    }
+    std::vector<uint32_t> cross;
+    p->tl_cross_off.assign(nblk + 1, 0);
+    for (uint32_t k = 0; k < nblk; ++k) {
+        p->tl_cross_off[k] = (uint32_t)cross.size();
+        for (uint32_t e : lists[r])
+            if ((e >> 16) == k || (e & 0xffffu) == k) cross.push_back(e);
+    }
+    p->tl_cross_off[nblk] = (uint32_t)cross.size();
+    p->tl_max = tmax;
+    p->tl_own = cnt[r];
+    const uint32_t S = (nblk + N - 1) / N;
+    hipError_t e = hipMalloc(&p->d_tl_all, all.size() * 4);
+    if (e == hipSuccess) e = hipMalloc(&p->d_tl_cnt, N * 4);
+    if (e == hipSuccess) e = hipMalloc(&p->d_tl_cross, std::max<size_t>(cross.size(), 1) * 4);
+    if (e == hipSuccess) e = hipMalloc(&p->d_rowslots, (size_t)N * S * B * B * 2);
+    if (e == hipSuccess) e = hipMalloc(&p->d_fbuf, (size_t)N * tmax * B * B * 2);
+    if (e == hipSuccess) e = hipMemcpy(p->d_tl_all, all.data(), all.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(p->d_tl_cnt, cnt.data(), N * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess && !cross.empty())
+        e = hipMemcpy(p->d_tl_cross, cross.data(), cross.size() * 4, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        if (err) {
+            err->code = SRT_ERR_HIP;
+            std::snprintf(err->msg, sizeof err->msg, "symmetric sharded setup: %s", hipGetErrorString(e));
+        }
+        return SRT_ERR_HIP;
+    }
+    return SRT_OK;
+}
+
+// a list launch of the SYM == 3 rest kernel: n entries at tl, skipping rows /
+// columns a and b
+void launch_list16(hipStream_t s, uint16_t *D, uint32_t Vp, uint32_t kb, const uint32_t *tl, uint32_t n, uint32_t a,
+                   uint32_t b) {
+    if (!n) return;
+    Span skip{0, 0, a, b, 0};
+    const uint64_t addr = reinterpret_cast<uint64_t>(tl);
+    Span ptr{(uint32_t)addr, (uint32_t)(addr >> 32), NONE, NONE, 0};
+    hipLaunchKernelGGL((minplus_u16_kernel<0, 3>), dim3(n), dim3(NT3), 0, s, D, Vp, kb, Rect{skip, skip},
+                       Rect{ptr, ptr}, 1u);
+}
+
+// Emulation (measurement only, SRT_FW_EMULATE_RANKS=N, one GPU, D already
+// closed): rank 0's schedule, each all-gather a wait of SRT_FW_EMU_AG_US +
+// received bytes / SRT_FW_EMU_AG_GBPS (as the loss tail's); the row unpack
+// goes to scratch (the other ranks' slots hold no real rows) and the final
+// unpack writes rank 0's tiles N times (every rank's volume), so D stays the
+// closure for the loss tail that follows.
+srt_status fw_rounds_sym_sharded(srt_plan *p, int p1r, srt_err *err) {
+    const bool emu = p->comm == nullptr;
+    const uint32_t N = emu ? p->emulate_ranks : (uint32_t)p->comm->nranks, r = emu ? 0u : (uint32_t)p->comm->rank;
+    if (srt_status st = sym_sharded_setup(p, N, r, err); st != SRT_OK) return st;
+    uint16_t *D = reinterpret_cast<uint16_t *>(p->d_D);
+    const uint32_t nblk = p->Vp / B;
+    const uint32_t S_t = (nblk + N - 1) / N;
+    long long ag_lat = 0;
+    double ag_per_byte = 0.0;
+    if (emu) {
+        int khz = 100000;
+        (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, p->device);
+        const double lat_us = std::getenv("SRT_FW_EMU_AG_US") ? std::atof(std::getenv("SRT_FW_EMU_AG_US")) : 25.0;
+        const double gbps = std::getenv("SRT_FW_EMU_AG_GBPS") ? std::atof(std::getenv("SRT_FW_EMU_AG_GBPS")) : 300.0;
+        ag_lat = (long long)(lat_us * khz / 1000.0);
+        ag_per_byte = (double)(N - 1) / (gbps * 1e3) * khz / 1000.0;  // ticks per byte a rank sends
+    }
+    auto gather = [&](void *buf, size_t bytes_per_rank, hipStream_t s) -> srt_status {
+        if (!emu) return comm_allgather_inplace(p->comm, buf, bytes_per_rank, s, err);
+        hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, s, ag_lat + (long long)(bytes_per_rank * ag_per_byte));
+        return SRT_OK;
+    };
+    hipStream_t M = p->stream, S = p->side_stream, C = p->comm_stream;
+    const uint32_t *own = p->d_tl_all + (size_t)r * p->tl_max;
+    uint16_t *myslot = p->d_rowslots + (size_t)r * S_t * B * B;
+    p->p3_launches = 0;
+    p->p3_work = 0.0;
+    p->p3_tiles = 0;
+    while (p->ev.size() < 2 * (size_t)nblk + 2) {
+        hipEvent_t e;
+        hipEventCreateWithFlags(&e, (unsigned)hipEventDisableSystemFence);
+        p->ev.push_back(e);
+    }
+    srt_status st = SRT_OK;
+    // prologue: pivot 0 on every rank (the same full initial D)
+    launch_p1<uint16_t>(p1r, M, D, p->Vp, 0u);
+    launch_mirror<uint16_t, 1>(p, M, 0, Rect{make_span(0, 1), make_span(0, nblk, 0)});
+    hipEventRecord(p->ev_cross, M);
+    hipEvent_t rest_done = p->ev_cross;
+    for (uint32_t kb = 0; kb < nblk; ++kb) {
+        const bool nxt = kb + 1 < nblk;
+        const uint32_t k1 = kb + 1;
+        if (nxt) hipStreamWaitEvent(S, rest_done, 0);
+        if (kb) hipStreamWaitEvent(M, p->ev_pivot, 0);
+        hipEventRecord(p->ev[2 * p->p3_launches], M);
+        launch_list16(M, D, p->Vp, kb, own, p->tl_own, kb, nxt ? k1 : NONE);
+        rest_done = p->ev[2 * p->p3_launches + 1];
+        hipEventRecord(rest_done, M);
+        p->p3_launches++;
+        p->p3_work += (double)p->tl_own * B * B * B;  // minus the few skipped row/col tiles
+        p->p3_tiles += p->tl_own;
+        if (!nxt) break;
+        const uint32_t *cl = p->d_tl_cross + p->tl_cross_off[k1];
+        const uint32_t cn = p->tl_cross_off[k1 + 1] - p->tl_cross_off[k1];
+        launch_list16(S, D, p->Vp, kb, cl, cn, kb, NONE);
+        if (cn) hipLaunchKernelGGL(pack_row16_kernel, dim3(cn), dim3(256), 0, S, D, p->Vp, cl, k1, N, myslot);
+        // the row all-gather on S itself: nothing else waits on S meanwhile,
+        // and two cross-stream event hops (~13 us each) fewer per round
+        if ((st = gather(p->d_rowslots, (size_t)S_t * B * B * 2, S)) != SRT_OK) return st;
+        // emulation: the other slots hold no real rows, so the unpack (same
+        // volume) goes to scratch and the closed D stays as it is
+        hipLaunchKernelGGL(unpack_row16_kernel, dim3(nblk), dim3(256), 0, S,
+                           emu ? p->d_fbuf : D + (uint64_t)k1 * B * p->Vp, p->Vp, k1, N, S_t,
+                           (const uint16_t *)p->d_rowslots);
+        launch_p1<uint16_t>(p1r, S, D, p->Vp, k1);
+        launch_mirror<uint16_t, 1>(p, S, k1, Rect{make_span(k1, k1 + 1), make_span(0, nblk, k1)});
+        hipEventRecord(p->ev_pivot, S);
+    }
+    // final exchange: every rank's tiles, written with their mirrors
+    if (p->tl_own)
+        hipLaunchKernelGGL(pack_list16_kernel, dim3(p->tl_own), dim3(256), 0, M, D, p->Vp, own,
+                           p->d_fbuf + (size_t)r * p->tl_max * B * B);
+    hipEventRecord(p->ev_row, M);
+    hipStreamWaitEvent(C, p->ev_row, 0);
+    if ((st = gather(p->d_fbuf, (size_t)p->tl_max * B * B * 2, C)) != SRT_OK) return st;
+    hipEventRecord(p->ev_bcast, C);
+    hipStreamWaitEvent(M, p->ev_bcast, 0);
+    hipLaunchKernelGGL(unpack_list16_kernel, dim3(p->tl_max, N), dim3(256), 0, M, D, p->Vp,
+                       (const uint32_t *)p->d_tl_all, (const uint32_t *)p->d_tl_cnt, p->tl_max,
+                       (const uint16_t *)p->d_fbuf, emu ? 1u : 0u);
+    return SRT_OK;
+}
+
 template <typename K>
 srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
     K *D = reinterpret_cast<K *>(p->d_D);
@@ -1435,6 +1748,9 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
     if (!sharded && !emu && p->fw_glds && (!p->fw_small_chain || std::getenv("SRT_FW_PAIR")) && grp > 1 &&
         grp <= 8 && nblk % grp == 0 && nblk >= 2 * grp)
         return fw_rounds_group_t<K>(p, p1r, grp);
+    // symmetric D on several ranks: the triangle dealt by (i + j) mod N
+    if constexpr (sizeof(K) == 2)
+        if ((sharded || emu) && p->fw_sym && p->fw_glds) return fw_rounds_sym_sharded(p, p1r, err);
     // sharded: groups of 2 when a rank holds >= 32 block-rows (rest-bound)
     // that split into whole groups (one owner per group) and there are >= 2
     // groups.  Emulated C3 (16k, u16 keys), g = 1 / 2 / 4: 2 ranks 82.7 / 80.6
@@ -1829,7 +2145,7 @@ srt_status fw_rounds_group_sharded_t(srt_plan *p, int p1r, uint32_t g, uint32_t 
 srt_status fw_sym_check(srt_plan *p, srt_err *err) {
     p->fw_sym_known = true;
     p->fw_sym = false;
-    if (p->comm || p->emulate_ranks > 1 || p->key_type != KEY_U16) return SRT_OK;
+    if (p->key_type != KEY_U16) return SRT_OK;
     if (const char *e = std::getenv("SRT_FW_SYM"); e && std::atoi(e) == 0) return SRT_OK;
     const uint32_t nb = p->Vp / 64;
     uint32_t one = 1, h = 0;

@@ -82,6 +82,15 @@ struct srt_plan {
     bool fw_sym = false;          // D symmetric (fw_sym_check): rest launches run the triangle
     bool fw_sym_known = false;
     uint32_t *d_flag32 = nullptr; // device scratch flag (symmetry check)
+    // symmetric sharded schedule (fw_rounds_sym_sharded): tile (i, j), i <= j,
+    // belongs to rank (i + j) mod N
+    uint32_t *d_tl_all = nullptr;      // N x tl_max lists, entries (i << 16) | j
+    uint32_t *d_tl_cnt = nullptr;      // N counts
+    uint32_t *d_tl_cross = nullptr;    // own tiles with i == k or j == k, concatenated over k
+    std::vector<uint32_t> tl_cross_off;
+    uint32_t tl_max = 0, tl_own = 0;
+    uint16_t *d_rowslots = nullptr;    // N x ceil(nblk / N) tiles: the per-round row exchange
+    uint16_t *d_fbuf = nullptr;        // N x tl_max tiles: the final exchange
     int fw_relax = 0;             // u32 rest kernel relax order (SRT_FW_RELAX, A/B)
     uint32_t fw_ablate = 0;       // measurement only: u32 rest-kernel ablations (SRT_FW_ABLATE, see the kernel)
     bool fw_band = true;          // grouped launches: banded tile order (knob SRT_FW_BAND=0, read at create)

@@ -1,8 +1,10 @@
 """One rank of the sharded routing build (spawned by tests/test_gpu_dist.py).
 
-usage: dist_worker.py RANK WORLD PORT N SEED TRANSPORT [ALGO [wide]]
+usage: dist_worker.py RANK WORLD PORT N SEED TRANSPORT [ALGO [wide|undirected]]
 ("wide": latencies << 34 plus 1, past the u32 key range -- the dense build takes the
-replicated loss pass, key all-gather included)
+replicated loss pass, key all-gather included; "undirected": a symmetric graph,
+so the dense build runs the symmetric sharded schedule -- triangle tiles dealt
+by (i + j) mod N, one row all-gather a round)
 All ranks share cuda:0 (the box has one GPU); collectives go through
 torch.distributed/gloo via the callback transport, which exercises exactly the
 same per-round schedule as the RCCL transport.  Exit code 0 = table matches
@@ -21,6 +23,7 @@ def main():
     transport = sys.argv[6]
     algo_name = sys.argv[7] if len(sys.argv) > 7 else "auto"
     wide = len(sys.argv) > 8 and sys.argv[8] == "wide"
+    undirected = len(sys.argv) > 8 and sys.argv[8] == "undirected"
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -30,11 +33,11 @@ def main():
     from shadow_amd.plan import RoutingPlan
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-    src, dst, lat, loss = synth.random_graph(n, seed, p_edge=0.08, directed=True, lat_range_ns=(1, 9),
+    src, dst, lat, loss = synth.random_graph(n, seed, p_edge=0.08, directed=not undirected, lat_range_ns=(1, 9),
                                              loss_max=0.05)
     if wide:
         lat = (np.asarray(lat, dtype=np.uint64) << np.uint64(34)) + np.uint64(1)  # gcd 1: no unit rescale
-    g = NetworkGraph.from_edges(n, src, dst, lat, loss, directed=True)
+    g = NetworkGraph.from_edges(n, src, dst, lat, loss, directed=not undirected)
     nodes = np.random.default_rng(seed).permutation(n).astype(np.uint32)
     algo = {"auto": _lib.SRT_ALGO_AUTO, "fw": _lib.SRT_ALGO_FW, "sssp": _lib.SRT_ALGO_SSSP}[algo_name]
     plan = RoutingPlan(g, nodes, algo=algo, device=0)
@@ -52,13 +55,15 @@ def main():
     ok = all(bool((c == all_ck[0]).all()) for c in all_ck)
     if rank == 0:
         from oracle import oracle as O
-        elat, eloss = O.compute_shortest_paths(O.Graph(True, np.arange(n), src, dst, lat, loss), nodes)
+        elat, eloss = O.compute_shortest_paths(O.Graph(not undirected, np.arange(n), src, dst, lat, loss), nodes)
         ok = ok and np.array_equal(t.latency_ns, elat)
         # both kernel families fold loss exactly like the reference
         ok = ok and np.array_equal(t.packet_loss.view(np.uint32), eloss.view(np.uint32))
         # dense builds: the loss pass ran on the rank's own closure rows
         ok = ok and (algo_name != "fw" or tail == (0 if wide else 1))
         ok = ok and (want_rests is None or tm["dominant_launches"] == int(want_rests))
+        # a symmetric dense graph runs the triangle schedule, a directed one never
+        ok = ok and (algo_name != "fw" or ("sym=triangle" in plan.describe()) == undirected)
         print(f"rank0: {plan.describe()} sharded_tail={tail} rests={tm['dominant_launches']} ok={ok}", flush=True)
     plan.close()
     dist.destroy_process_group()

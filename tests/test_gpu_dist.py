@@ -29,16 +29,21 @@ def _port():
     (2, 1000, 8, "fw", False, "4:2"), (3, 1300, 9, "fw", False, "4:3"), (8, 1100, 10, "fw", False, "2:8"),
     (2, 1000, 11, "fw", False, "2:4"),
     # u64 keys: replicated loss pass after the key all-gather
-    (3, 400, 7, "fw", True, None)])
+    (3, 400, 7, "fw", True, None),
+    # symmetric graphs: triangle tiles dealt by (i + j) mod N, a row all-gather per round
+    (2, 300, 12, "fw", "undirected", None), (3, 520, 13, "fw", "undirected", None),
+    (8, 1100, 14, "fw", "undirected", None), (3, 200, 15, "sssp", "undirected", None)])
 def test_sharded_build_matches_oracle(world, n, seed, algo, wide, group):
     """Dense builds assert the sharded tail ran (or, "wide", the replicated
-    fallback); every rank's table equals the oracle's bit for bit."""
+    fallback) and, for undirected graphs, the symmetric schedule; every rank's
+    table equals the oracle's bit for bit."""
     port = _port()
     env = dict(os.environ)
     if group:  # "g:rest launches"
         env["SRT_FW_SHARD_GROUP"], env["SRT_TEST_EXPECT_RESTS"] = group.split(":")
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker.py"), str(r), str(world), str(port),
-                               str(n), str(seed), "torch", algo] + (["wide"] if wide else []), env=env,
+                               str(n), str(seed), "torch", algo] +
+                              (["undirected"] if wide == "undirected" else ["wide"] if wide else []), env=env,
                               stdout=subprocess.PIPE,
                               stderr=subprocess.STDOUT, text=True) for r in range(world)]
     outs = []
