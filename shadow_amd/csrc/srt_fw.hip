@@ -1075,7 +1075,8 @@ __device__ __forceinline__ bool tile_of_sym(uint32_t t, const Span &s, uint32_t 
 // SYM: 0 = the rect(s) as given; 1 = the triangle of the square span r1.r
 // (rest launches); 2 = the rect(s) as given, each off-diagonal result also
 // stored transposed (the symmetric chain: p2row also writes p2col's tiles,
-// one cross rect also writes the other).
+// one cross rect also writes the other); 3 = a tile list (symmetric sharded
+// schedule), mirrored like 1 and 2.
 template <int TAG, int SYM = 0>
 __global__ __launch_bounds__(NT3, 2) void minplus_u16_kernel(uint16_t *__restrict__ D, uint32_t Vp, uint32_t kb,
                                                              Rect r1, Rect r2, uint32_t ng) {
@@ -1087,7 +1088,8 @@ __global__ __launch_bounds__(NT3, 2) void minplus_u16_kernel(uint16_t *__restric
     } else if constexpr (SYM == 3) {
         // tile list (symmetric sharded schedule): the list's device address in
         // r2.r.lo / r2.r.hi, entries (i << 16) | j; tiles in row or column
-        // r1.r.x0 or r1.r.x1 (this round's pivot and look-ahead) are skipped
+        // r1.r.x0 or r1.r.x1 (this round's pivot and look-ahead) are skipped;
+        // results are also stored mirrored (below)
         const uint32_t *tl = reinterpret_cast<const uint32_t *>(((uint64_t)r2.r.hi << 32) | r2.r.lo);
         const uint32_t e = tl[blockIdx.x];
         bi = e >> 16;
@@ -1172,7 +1174,7 @@ __global__ __launch_bounds__(NT3, 2) void minplus_u16_kernel(uint16_t *__restric
         v.w = acc[i][3];
         *reinterpret_cast<u32x4 *>(D + (i0 + ty + 16 * i) * Vp + j0 + tx * 8) = v;
     }
-    if constexpr (SYM == 1 || SYM == 2) {
+    if constexpr (SYM != 0) {
         if (bi != bj) {
             // the mirror tile: transpose through LDS ([128][129] u16 = the two
             // stage buffers, idle since the last chunk's barrier; row stride 129
@@ -1240,15 +1242,16 @@ __device__ __forceinline__ void move_tile16(const uint16_t *__restrict__ src, ui
 
 // Own tiles of row/column k (list entries (i << 16) | j with i == k or j == k)
 // into this rank's all-gather slot, as row-k tiles: tile (k, c) at slot index
-// c / N (its owner is (k + c) mod N, so the indices are distinct); a tile
-// stored as (c, k), c < k, moves transposed.
+// c / N (its owner is (k + c) mod N, so the indices are distinct).  The list
+// kernels store every own tile's mirror too, so (k, c) is current in row
+// orientation whichever of (k, c) / (c, k) the rank owns: a plain copy.
 __global__ __launch_bounds__(256) void pack_row16_kernel(const uint16_t *__restrict__ D, uint32_t Vp,
                                                          const uint32_t *__restrict__ tl, uint32_t k, uint32_t N,
                                                          uint16_t *__restrict__ slot) {
     __shared__ uint16_t t[B][B + 1];
     const uint32_t e = tl[blockIdx.x], i = e >> 16, j = e & 0xffffu;
     const uint32_t c = i == k ? j : i;
-    move_tile16(D + (uint64_t)i * B * Vp + (uint64_t)j * B, Vp, slot + (uint64_t)(c / N) * B * B, B, i != k, t);
+    move_tile16(D + (uint64_t)k * B * Vp + (uint64_t)c * B, Vp, slot + (uint64_t)(c / N) * B * B, B, false, t);
 }
 
 // Row k assembled from every rank's slot (S tiles each): tile (k, c) from
