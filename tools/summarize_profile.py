@@ -23,6 +23,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 LABELS = {
     "minplus_u16_kernel<0>": "phase 3 rest",
+    "minplus_u16_kernel<0, 1>": "phase 3 rest",
+    "minplus_u16_kernel<0, 3>": "phase 3 rest",
     "minplus_u16_kernel<5>": "phase 3 look-ahead (grouped)",
     "minplus_u32_kernel<0>": "phase 3 rest",
     "minplus_u32_kernel<5>": "phase 3 look-ahead (grouped)",
