@@ -897,9 +897,9 @@ srt_status tight_csr_push_t(srt_plan *p, unsigned long long *d_stats, bool *done
     hipLaunchKernelGGL(tight_scan_kernel, dim3(1), dim3(1024), 0, M, p->d_tcnt, p->d_tptr, V);
     hipLaunchKernelGGL(tight_list_fill_kernel<true>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, total, p->d_tptr,
                        p->d_tcnt, p->d_tpk2, ubits);
+    p->t_push = true;
     if ((st = sort_packed(p, ubits, maxw, err)) != SRT_OK) return st;
     p->t_packed = true;
-    p->t_push = true;
     *done = true;
     return SRT_OK;
 }
