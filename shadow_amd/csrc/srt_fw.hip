@@ -1371,6 +1371,107 @@ __global__ __launch_bounds__(256) void minplus_small_kernel(K *__restrict__ D, u
         for (int j = 0; j < 4; ++j) D[(i0 + ty * 4 + i) * Vp + j0 + tx + 16 * j] = acc[i][j];
 }
 
+// Quarter-tile chain kernel for u16 keys with packed relaxations: a 64 x 64
+// quarter of a 128 x 128 tile per 256-thread workgroup (4 per tile), thread
+// (tx, ty) holding rows ty*4 .. +3 and columns tx*4 .. +3 as 2 packed pairs
+// (v_pk_add_u16 + v_pk_min_u16: 8 + 8 VALU per k against the scalar quarter
+// kernel's ~48).  K chunks of 32 staged through LDS, double-buffered.  Every
+// off-diagonal result is also stored transposed into its mirror (symmetric D).
+// LIST: tiles from a list (entries (i << 16) | j, address in r2.r.lo/hi, rows
+// or columns r1.r.x0 / r1.r.x1 skipped), else the rect r1.
+template <int TAG, bool LIST>
+__global__ __launch_bounds__(256) void minplus_q16_kernel(uint16_t *__restrict__ D, uint32_t Vp, uint32_t kb, Rect r1,
+                                                          Rect r2) {
+    constexpr int QK = 32;
+    __shared__ uint16_t As[2][SQ][QK + 2];  // [row][k]
+    __shared__ us2 Bs[2][QK][SQ / 2];        // [k][column pair]
+    __shared__ uint16_t T[SQ][SQ + 1];
+    __builtin_amdgcn_s_setprio(2);
+    uint32_t t = blockIdx.x >> 2, bi, bj;
+    const uint32_t q = blockIdx.x & 3;
+    if constexpr (LIST) {
+        const uint32_t *tl = reinterpret_cast<const uint32_t *>(((uint64_t)r2.r.hi << 32) | r2.r.lo);
+        const uint32_t e = tl[t];
+        bi = e >> 16;
+        bj = e & 0xffffu;
+        if (bi == r1.r.x0 || bj == r1.r.x0 || bi == r1.r.x1 || bj == r1.r.x1) return;
+    } else {
+        bi = span_at(r1.r, t / r1.c.n);
+        bj = span_at(r1.c, t % r1.c.n);
+    }
+    const uint64_t i0 = (uint64_t)bi * B + (q >> 1) * SQ, j0 = (uint64_t)bj * B + (q & 1) * SQ;
+    const uint64_t k0 = (uint64_t)kb * B;
+    const int tid = threadIdx.x, tx = tid % 16, ty = tid / 16;
+    us2 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint2 v = *reinterpret_cast<const uint2 *>(D + (i0 + ty * 4 + i) * Vp + j0 + tx * 4);
+        acc[i][0] = __builtin_bit_cast(us2, v.x);
+        acc[i][1] = __builtin_bit_cast(us2, v.y);
+    }
+    // a chunk: A = 64 rows x 32 k (8 keys a thread), B = 32 k x 64 columns (8 keys)
+    uint4 ra, rb;
+    auto fetch = [&](int kc) {
+        ra = *reinterpret_cast<const uint4 *>(D + (i0 + tid / 4) * Vp + k0 + kc + (tid % 4) * 8);
+        rb = *reinterpret_cast<const uint4 *>(D + (k0 + kc + tid / 8) * Vp + j0 + (tid % 8) * 8);
+    };
+    auto stash = [&](int buf) {
+        uint16_t *a = &As[buf][tid / 4][(tid % 4) * 8];
+        const uint16_t *ra16 = reinterpret_cast<const uint16_t *>(&ra);
+#pragma unroll
+        for (int x = 0; x < 8; ++x) a[x] = ra16[x];
+        us2 *b = &Bs[buf][tid / 8][(tid % 8) * 4];
+        b[0] = __builtin_bit_cast(us2, rb.x);
+        b[1] = __builtin_bit_cast(us2, rb.y);
+        b[2] = __builtin_bit_cast(us2, rb.z);
+        b[3] = __builtin_bit_cast(us2, rb.w);
+    };
+    fetch(0);
+    stash(0);
+    __syncthreads();
+    constexpr int NCH = B / QK;
+#pragma unroll 1
+    for (int ch = 0; ch < NCH; ++ch) {
+        const int cur = ch & 1;
+        if (ch + 1 < NCH) fetch((ch + 1) * QK);
+#pragma unroll 8
+        for (int k = 0; k < QK; ++k) {
+            const us2 b0 = Bs[cur][k][tx * 2], b1 = Bs[cur][k][tx * 2 + 1];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint16_t a = As[cur][ty * 4 + i][k];
+                const us2 a2 = {a, a};
+                acc[i][0] = __builtin_elementwise_min(acc[i][0], a2 + b0);
+                acc[i][1] = __builtin_elementwise_min(acc[i][1], a2 + b1);
+            }
+        }
+        if (ch + 1 < NCH) stash(cur ^ 1);  // the other buffer's readers passed the last barrier
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        uint2 v;
+        v.x = __builtin_bit_cast(uint32_t, acc[i][0]);
+        v.y = __builtin_bit_cast(uint32_t, acc[i][1]);
+        *reinterpret_cast<uint2 *>(D + (i0 + ty * 4 + i) * Vp + j0 + tx * 4) = v;
+    }
+    if (bi != bj) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) T[tx * 4 + c][ty * 4 + i] = acc[i][c / 2][c % 2];
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = ty * 4 + i;  // row of the mirror quarter
+            uint2 v;
+            v.x = (uint32_t)T[r][tx * 4] | ((uint32_t)T[r][tx * 4 + 1] << 16);
+            v.y = (uint32_t)T[r][tx * 4 + 2] | ((uint32_t)T[r][tx * 4 + 3] << 16);
+            *reinterpret_cast<uint2 *>(D + (j0 + r) * Vp + i0 + tx * 4) = v;
+        }
+    }
+}
+
 __global__ void pack_kernel(const uint64_t *__restrict__ lat, const float *__restrict__ loss,
                             srt_path *__restrict__ out, uint64_t total) {
     for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < total;
@@ -1642,9 +1743,22 @@ srt_status fw_rounds_sym_sharded(srt_plan *p, int p1r, srt_err *err) {
         p->ev.push_back(e);
     }
     srt_status st = SRT_OK;
+    // the chain as packed quarter tiles (minplus_q16_kernel) when a rank's
+    // rest is short (< 4096 own tiles: from 4 ranks on at 16k) -- it is then
+    // the round's critical path; knob SRT_FW_SYM_SMALL=0/1 for A/B
+    bool small = p->tl_own < 4096;
+    if (const char *e = std::getenv("SRT_FW_SYM_SMALL")) small = std::atoi(e) != 0;
+    auto p2row_mirror = [&](hipStream_t s, uint32_t k) {
+        const Rect row{make_span(k, k + 1), make_span(0, nblk, k)};
+        if (small)
+            hipLaunchKernelGGL((minplus_q16_kernel<1, false>), dim3(4 * row.c.n), dim3(256), 0, s, D, p->Vp, k, row,
+                               Rect{make_span(0, 0), make_span(0, 0)});
+        else
+            launch_mirror<uint16_t, 1>(p, s, k, row);
+    };
     // prologue: pivot 0 on every rank (the same full initial D)
     launch_p1<uint16_t>(p1r, M, D, p->Vp, 0u);
-    launch_mirror<uint16_t, 1>(p, M, 0, Rect{make_span(0, 1), make_span(0, nblk, 0)});
+    p2row_mirror(M, 0);
     hipEventRecord(p->ev_cross, M);
     hipEvent_t rest_done = p->ev_cross;
     for (uint32_t kb = 0; kb < nblk; ++kb) {
@@ -1662,7 +1776,15 @@ srt_status fw_rounds_sym_sharded(srt_plan *p, int p1r, srt_err *err) {
         if (!nxt) break;
         const uint32_t *cl = p->d_tl_cross + p->tl_cross_off[k1];
         const uint32_t cn = p->tl_cross_off[k1 + 1] - p->tl_cross_off[k1];
-        launch_list16(S, D, p->Vp, kb, cl, cn, kb, NONE);
+        if (small && cn) {
+            Span skip{0, 0, kb, NONE, 0};
+            const uint64_t addr = reinterpret_cast<uint64_t>(cl);
+            Span ptr{(uint32_t)addr, (uint32_t)(addr >> 32), NONE, NONE, 0};
+            hipLaunchKernelGGL((minplus_q16_kernel<4, true>), dim3(4 * cn), dim3(256), 0, S, D, p->Vp, kb,
+                               Rect{skip, skip}, Rect{ptr, ptr});
+        } else {
+            launch_list16(S, D, p->Vp, kb, cl, cn, kb, NONE);
+        }
         if (cn) hipLaunchKernelGGL(pack_row16_kernel, dim3(cn), dim3(256), 0, S, D, p->Vp, cl, k1, N, myslot);
         // the row all-gather on S itself: nothing else waits on S meanwhile,
         // and two cross-stream event hops (~13 us each) fewer per round
@@ -1673,7 +1795,7 @@ srt_status fw_rounds_sym_sharded(srt_plan *p, int p1r, srt_err *err) {
                            emu ? p->d_fbuf : D + (uint64_t)k1 * B * p->Vp, p->Vp, k1, N, S_t,
                            (const uint16_t *)p->d_rowslots);
         launch_p1<uint16_t>(p1r, S, D, p->Vp, k1);
-        launch_mirror<uint16_t, 1>(p, S, k1, Rect{make_span(k1, k1 + 1), make_span(0, nblk, k1)});
+        p2row_mirror(S, k1);
         hipEventRecord(p->ev_pivot, S);
     }
     // final exchange: every rank's tiles, written with their mirrors

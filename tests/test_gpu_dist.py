@@ -59,6 +59,20 @@ def test_sharded_build_matches_oracle(world, n, seed, algo, wide, group):
         assert p.returncode == 0, out[-3000:]
 
 
+def test_symmetric_sharded_full_tile_chain():
+    """The symmetric schedule's chain with full-tile cross / p2row launches
+    (SRT_FW_SYM_SMALL=0; the default at >= 4096 own tiles a rank, i.e. 2 ranks
+    at 16k) -- small graphs otherwise take the packed quarter-tile chain."""
+    port = _port()
+    env = dict(os.environ, SRT_FW_SYM_SMALL="0")
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker.py"), str(r), "2", str(port), "400",
+                               "16", "torch", "fw", "undirected"], env=env, stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for r in range(2)]
+    outs = [p.communicate(timeout=110)[0] for p in procs]
+    for p, out in zip(procs, outs):
+        assert p.returncode == 0, out[-3000:]
+
+
 @pytest.mark.parametrize("algo_name", ["fw", "sssp"])
 def test_rccl_transport_single_rank(algo_name):
     """Native RCCL communicator (1 rank on the box): runs the sharded schedule
