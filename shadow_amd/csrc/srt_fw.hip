@@ -278,37 +278,40 @@ __global__ __launch_bounds__(16 * (B / P1R)) void fw_phase1_kernel(K *__restrict
     }
 }
 
-// Phase 1 for u16 keys: the layout of fw_phase1_kernel<uint16_t, 8> with each
+// Phase 1 for u16 keys: the layout of fw_phase1_kernel<uint16_t, P1R> with each
 // thread's 8 columns as 4 packed pairs, relaxed by v_pk_add_u16 +
 // v_pk_min_u16 (a broadcast to both halves): a third of the scalar u16
 // version's VALU (add, min, and the u16 widening) per step.  Sums stay below
 // 2^16 (both operands <= KEY16_INF), so the packed add never wraps.
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-__global__ __launch_bounds__(256) void fw_phase1_u16pk_kernel(uint16_t *__restrict__ D, uint32_t Vp, uint32_t kb) {
+template <int P1R>
+__global__ __launch_bounds__(16 * (B / P1R)) void fw_phase1_u16pk_kernel(uint16_t *__restrict__ D, uint32_t Vp,
+                                                                        uint32_t kb) {
     __shared__ us2 rowbuf[2][B / 2];
     __shared__ uint16_t colbuf[2][B];
     __builtin_amdgcn_s_setprio(3);  // critical path of the look-ahead chain
     const int tid = threadIdx.x, tx = tid % 16, ty = tid / 16;
     const uint64_t k0 = (uint64_t)kb * B;
-    us2 p[8][4];
+    us2 p[P1R][4];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(D + (k0 + ty * 8 + i) * Vp + k0 + tx * 8);
+    for (int i = 0; i < P1R; ++i) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(D + (k0 + ty * P1R + i) * Vp + k0 + tx * 8);
         p[i][0] = __builtin_bit_cast(us2, v.x);
         p[i][1] = __builtin_bit_cast(us2, v.y);
         p[i][2] = __builtin_bit_cast(us2, v.z);
         p[i][3] = __builtin_bit_cast(us2, v.w);
     }
-    // step k = 8g + e: row k in thread-row g at element e, column k in
-    // thread-column g at element e (pair e / 2, half e % 2)
+    // step k = 8g + e: row k in thread-row k / P1R at element k % P1R, column
+    // k in thread-column g at element e (pair e / 2, half e % 2)
     auto publish = [&](int g, int e, int buf) {
-        if (ty == g) {
+        const int k = 8 * g + e;
+        if (ty == k / P1R) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) rowbuf[buf][tx * 4 + q] = p[e][q];
+            for (int q = 0; q < 4; ++q) rowbuf[buf][tx * 4 + q] = p[k % P1R][q];
         }
         if (tx == g) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) colbuf[buf][ty * 8 + i] = p[i][e / 2][e % 2];
+            for (int i = 0; i < P1R; ++i) colbuf[buf][ty * P1R + i] = p[i][e / 2][e % 2];
         }
     };
     publish(0, 0, 0);
@@ -322,8 +325,8 @@ __global__ __launch_bounds__(256) void fw_phase1_u16pk_kernel(uint16_t *__restri
 #pragma unroll
             for (int q = 0; q < 4; ++q) b[q] = rowbuf[cur][tx * 4 + q];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const uint16_t a = colbuf[cur][ty * 8 + i];
+            for (int i = 0; i < P1R; ++i) {
+                const uint16_t a = colbuf[cur][ty * P1R + i];
                 const us2 a2 = {a, a};
 #pragma unroll
                 for (int q = 0; q < 4; ++q) p[i][q] = __builtin_elementwise_min(p[i][q], a2 + b[q]);
@@ -334,13 +337,13 @@ __global__ __launch_bounds__(256) void fw_phase1_u16pk_kernel(uint16_t *__restri
         }
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < P1R; ++i) {
         uint4 v;
         v.x = __builtin_bit_cast(uint32_t, p[i][0]);
         v.y = __builtin_bit_cast(uint32_t, p[i][1]);
         v.z = __builtin_bit_cast(uint32_t, p[i][2]);
         v.w = __builtin_bit_cast(uint32_t, p[i][3]);
-        *reinterpret_cast<uint4 *>(D + (k0 + ty * 8 + i) * Vp + k0 + tx * 8) = v;
+        *reinterpret_cast<uint4 *>(D + (k0 + ty * P1R + i) * Vp + k0 + tx * 8) = v;
     }
 }
 
@@ -1551,9 +1554,14 @@ __global__ void delay_kernel(long long ticks) {
 template <typename K>
 void launch_p1(int rows, hipStream_t s, K *D, uint32_t Vp, uint32_t kb) {
     if constexpr (sizeof(K) == 2) {
-        if (rows == 8 && !std::getenv("SRT_FW_P1_SCALAR")) {
-            hipLaunchKernelGGL(fw_phase1_u16pk_kernel, dim3(1), dim3(256), 0, s, reinterpret_cast<uint16_t *>(D), Vp,
-                               kb);
+        if (!std::getenv("SRT_FW_P1_SCALAR")) {
+            uint16_t *D16 = reinterpret_cast<uint16_t *>(D);
+            if (rows == 2)
+                hipLaunchKernelGGL(fw_phase1_u16pk_kernel<2>, dim3(1), dim3(16 * (B / 2)), 0, s, D16, Vp, kb);
+            else if (rows == 4)
+                hipLaunchKernelGGL(fw_phase1_u16pk_kernel<4>, dim3(1), dim3(16 * (B / 4)), 0, s, D16, Vp, kb);
+            else
+                hipLaunchKernelGGL(fw_phase1_u16pk_kernel<8>, dim3(1), dim3(16 * (B / 8)), 0, s, D16, Vp, kb);
             return;
         }
     }
@@ -1851,7 +1859,10 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
         p->ev.push_back(e);
     }
     // phase-1 rows per thread (knob SRT_FW_P1_ROWS in {2,4,8}, measurement only)
-    int p1r = 8;
+    // (u16 keys: the packed kernel at 4 rows a thread, 512 threads -- emulated
+    // 8 ranks 29.4 -> 28.3 ms, where phase 1 is on the round's critical path;
+    // one GPU unchanged)
+    int p1r = sizeof(K) == 2 ? 4 : 8;
     if (const char *e = std::getenv("SRT_FW_P1_ROWS")) p1r = std::atoi(e);
     // emulation only: SRT_FW_EMU_BCAST_US stands in for the pivot-row broadcast latency
     long long emu_bcast_ticks = 0;
