@@ -52,6 +52,10 @@ namespace {
 
 constexpr int NBK = 2048;        // latency buckets per row
 constexpr int LOSS_NT = 1024;    // threads of the fold workgroup (16 waves)
+// push scan: edges a lane loads per step (C3: 2 / 4 / 8 / 16 -> 24.8 / 20.7 /
+// 21.7 / 25.7 ms for the pass: a member's edges below its bound are few, so
+// wider steps fetch past the bound and narrower ones expose the latency)
+constexpr int PUNR = 4;
 constexpr size_t LDS_BUDGET = 160 * 1024 - 1024;
 
 template <typename K>
@@ -573,10 +577,10 @@ __global__ __launch_bounds__(LOSS_NT) void tight_loss_kernel(
                 int changed = 0;
                 if constexpr (PUSH) {
                     if (shift)
-                        changed = scan_bucket_push<LatT, LPT, 8, true>(ord, m0, m1, grp, sub, ngrp, tpk, lrow, prow,
+                        changed = scan_bucket_push<LatT, LPT, PUNR, true>(ord, m0, m1, grp, sub, ngrp, tpk, lrow, prow,
                                                                     ubits, umask, (LatT)(mx + 1));
                     else
-                        scan_bucket_push<LatT, LPT, 8, false>(ord, m0, m1, grp, sub, ngrp, tpk, lrow, prow, ubits,
+                        scan_bucket_push<LatT, LPT, PUNR, false>(ord, m0, m1, grp, sub, ngrp, tpk, lrow, prow, ubits,
                                                            umask, (LatT)(mx + 1));
                 } else if constexpr (PACKED) {
                     if (shift)
@@ -785,7 +789,11 @@ srt_status launch_fold_lpt(srt_plan *p, unsigned long long *d_stats, uint32_t ub
     const double avg = p->V ? (double)p->t_edges / p->V : 0.0;
     if constexpr (PACKED) {
         if (p->t_push) {
-            if (avg > 10.0) return launch_fold<LatT, LROWS, 4, true, true>(p, d_stats, ubits, job, err);
+            const char *k = std::getenv("SRT_LOSS_LPT");  // lanes per pushing member (A/B)
+            if (k && std::atoi(k) == 8) return launch_fold<LatT, LROWS, 8, true, true>(p, d_stats, ubits, job, err);
+            if (k && std::atoi(k) == 2) return launch_fold<LatT, LROWS, 2, true, true>(p, d_stats, ubits, job, err);
+            if ((k && std::atoi(k) == 4) || avg > 10.0)
+                return launch_fold<LatT, LROWS, 4, true, true>(p, d_stats, ubits, job, err);
             return launch_fold<LatT, LROWS, 2, true, true>(p, d_stats, ubits, job, err);
         }
         // 4 lanes x 8 edges per target (C3, same box: 4 / 8 / 16 lanes ->
