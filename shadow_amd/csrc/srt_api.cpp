@@ -741,6 +741,12 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
             }
         }
         if (const char *e = std::getenv("SRT_FW_BAND")) p->fw_band = e[0] != '0';
+        if (const char *e = std::getenv("SRT_FW_XCD")) p->fw_xcd = e[0] != '0';
+        if (const char *e = std::getenv("SRT_FW_BAND_H")) {
+            const int h = std::atoi(e);
+            p->fw_band_h = 1;
+            while (p->fw_band_h * 2 <= (uint32_t)std::min(h, 64)) p->fw_band_h *= 2;
+        }
         if (const char *e = std::getenv("SRT_FW_RELAX")) p->fw_relax = std::atoi(e);
         if (const char *e = std::getenv("SRT_LOSS_PUSH")) p->loss_push = std::atoi(e) != 0;
         if (const char *e = std::getenv("SRT_FW_ABLATE")) p->fw_ablate = (uint32_t)std::atoi(e) & 15u;

@@ -1040,27 +1040,43 @@ __device__ __forceinline__ void chunk_steps16(uint32_t (&acc)[8][4], StepOps16 (
 // fw_sym_check): a rest launch over a square span runs only the tiles with
 // span position pi <= pj and writes each off-diagonal result twice, as
 // (bi, bj) and transposed as (bj, bi) -- half the relaxations.  Grid order:
-// bands of up to 8 rows, band b = rows 8b .. 8b+7 x columns 8b .. m-1, a
-// column of 8 tiles after another (the banded order of tile_of); the
-// band's 28 below-diagonal slots exit at once.  The mirrored tile (bj, bi)
+// bands of up to h rows, band b = rows hb .. hb+h-1 x columns hb .. m-1, a
+// column of h tiles after another (the banded order of tile_of); the band's
+// h(h-1)/2 below-diagonal slots exit at once.  h = 1 (plain row-major
+// triangle, no exits) without the XCD remap of tile_of is the default: C3
+// rest per build, same box, with the remap, h = 32 / 16 / 8 / 4 / 2 / 1:
+// 74.9 / 66.4 / 63.5 / 62.9 / 62.4 / 62.2 ms; without it h = 4 / 2 / 1:
+// 62.2 / 61.1 / 60.9 ms (knobs SRT_FW_BAND_H, SRT_FW_XCD=1; taller bands'
+// L2 reuse does not pay -- the launch is VALU-bound, not fetch-bound -- and
+// the remap puts a band's short in-group tiles all on one XCD, which then
+// idles in the launch's tail; a group-last order measured 62.1).  The
+// mirrored tile (bj, bi)
 // is never an operand the launch's grouping rule does not already allow to
 // be read mid-update (its row or column is in the group exactly when
 // (bi, bj)'s is), and the excluded next-group rows/cols are symmetric.
-__host__ __device__ inline uint32_t sym_grid(uint32_t m) {
+// Band height h = band_h(ng) = 1 << bits 17-19 of ng (plan field fw_band_h, a power of 2)
+__host__ __device__ inline uint32_t sym_grid(uint32_t m, uint32_t h = 8) {
     uint32_t n = 0;
-    for (uint32_t b0 = 0; b0 < m; b0 += 8) n += std::min(8u, m - b0) * (m - b0);
+    for (uint32_t b0 = 0; b0 < m; b0 += h) n += std::min(h, m - b0) * (m - b0);
     return n;
 }
-__device__ __forceinline__ bool tile_of_sym(uint32_t t, const Span &s, uint32_t &bi, uint32_t &bj) {
+__host__ __device__ inline uint32_t band_bits(uint32_t h) {
+    uint32_t c = 0;
+    while ((2u << c) <= h && c < 7) ++c;
+    return c << 17;
+}
+__device__ __forceinline__ uint32_t band_h(uint32_t ng) { return 1u << ((ng >> 17) & 7u); }
+__device__ __forceinline__ bool tile_of_sym(uint32_t t, const Span &s, uint32_t h, bool xcd_map, uint32_t &bi,
+                                            uint32_t &bj) {
     const uint32_t n1 = gridDim.x;
-    if (n1 >= 64) {  // XCD-aware bijective remap, as tile_of
+    if (n1 >= 64 && xcd_map) {  // XCD-aware bijective remap, as tile_of
         const uint32_t q = n1 / 8, rr = n1 % 8, xcd = t % 8;
         t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + t / 8;
     }
     const uint32_t m = s.n;
     uint32_t b0 = 0, base = 0, pi = 0, pj = 0;
-    for (; b0 < m; b0 += 8) {
-        const uint32_t rows = min(8u, m - b0), cnt = rows * (m - b0);
+    for (; b0 < m; b0 += h) {
+        const uint32_t rows = min(h, m - b0), cnt = rows * (m - b0);
         if (t < base + cnt) {
             const uint32_t w = t - base;
             pi = b0 + w % rows;
@@ -1087,7 +1103,8 @@ __global__ __launch_bounds__(NT3, 2) void minplus_u16_kernel(uint16_t *__restric
     if constexpr (TAG != 0) __builtin_amdgcn_s_setprio(2);  // look-ahead chain: issue priority
     uint32_t bi, bj;
     if constexpr (SYM == 1) {
-        if (!tile_of_sym(blockIdx.x, r1.r, bi, bj)) return;  // workgroup-uniform, before any barrier
+        if (!tile_of_sym(blockIdx.x, r1.r, band_h(ng), (ng & (1u << 24)) != 0, bi, bj))
+            return;  // workgroup-uniform, before any barrier
     } else if constexpr (SYM == 3) {
         // tile list (symmetric sharded schedule): the list's device address in
         // r2.r.lo / r2.r.hi, entries (i << 16) | j; tiles in row or column
@@ -1600,9 +1617,10 @@ void launch_tiles(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1, const
 template <typename K>
 void launch_rest_sym(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1) {
     if constexpr (sizeof(K) == 2)
-        hipLaunchKernelGGL((minplus_u16_kernel<0, 1>), dim3(sym_grid(r1.r.n)), dim3(NT3), 0, s,
+        hipLaunchKernelGGL((minplus_u16_kernel<0, 1>), dim3(sym_grid(r1.r.n, p->fw_band_h)), dim3(NT3), 0, s,
                            reinterpret_cast<uint16_t *>(p->d_D), p->Vp, kb, r1,
-                           Rect{make_span(0, 0), make_span(0, 0)}, 1u);
+                           Rect{make_span(0, 0), make_span(0, 0)},
+                           1u | band_bits(p->fw_band_h) | (p->fw_xcd ? 1u << 24 : 0u));
 }
 
 // One rect of chain tiles that also stores each off-diagonal result
@@ -2021,7 +2039,9 @@ void launch_group(srt_plan *p, hipStream_t s, uint32_t a, uint32_t g, const Rect
     if (!n) return;
     K *D = reinterpret_cast<K *>(p->d_D);
     // bit 16: banded tile order (plan knob SRT_FW_BAND=0 turns it off for A/B timing)
-    const uint32_t arg = g | (p->fw_band ? 0x10000u : 0u) | (chain ? 0u : p->fw_ablate << 20);
+    // bit 24: XCD remap of the triangle order (knob SRT_FW_XCD=1, A/B timing)
+    const uint32_t arg = g | (p->fw_band ? 0x10000u : 0u) | band_bits(p->fw_band_h) |
+                         (chain ? 0u : p->fw_ablate << 20) | (p->fw_xcd ? 1u << 24 : 0u);
     if constexpr (sizeof(K) == 2) {
         if (chain && p->fw_sym)  // r1 only; its transposes are r2 (fw_rounds_group_t)
             hipLaunchKernelGGL((minplus_u16_kernel<5, 2>), dim3(r1.r.n * r1.c.n), dim3(NT3), 0, s, D, p->Vp, a, r1,
@@ -2029,8 +2049,8 @@ void launch_group(srt_plan *p, hipStream_t s, uint32_t a, uint32_t g, const Rect
         else if (chain)
             hipLaunchKernelGGL((minplus_u16_kernel<5>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
         else if (p->fw_sym)  // square span, r2 empty (fw_rounds_group_t)
-            hipLaunchKernelGGL((minplus_u16_kernel<0, 1>), dim3(sym_grid(r1.r.n)), dim3(NT3), 0, s, D, p->Vp, a,
-                               r1, r2, arg);
+            hipLaunchKernelGGL((minplus_u16_kernel<0, 1>), dim3(sym_grid(r1.r.n, p->fw_band_h)), dim3(NT3), 0, s, D,
+                               p->Vp, a, r1, r2, arg);
         else
             hipLaunchKernelGGL((minplus_u16_kernel<0>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
     } else if constexpr (sizeof(K) == 4) {

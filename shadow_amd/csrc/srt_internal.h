@@ -93,6 +93,8 @@ struct srt_plan {
     uint16_t *d_fbuf = nullptr;        // N x tl_max tiles: the final exchange
     int fw_relax = 0;             // u32 rest kernel relax order (SRT_FW_RELAX, A/B)
     uint32_t fw_ablate = 0;       // measurement only: u32 rest-kernel ablations (SRT_FW_ABLATE, see the kernel)
+    bool fw_xcd = false;          // triangle rest: XCD remap of the order (knob SRT_FW_XCD=1, A/B timing)
+    uint32_t fw_band_h = 1;       // triangle rest: rows per band (power of 2, knob SRT_FW_BAND_H, read at create)
     bool fw_band = true;          // grouped launches: banded tile order (knob SRT_FW_BAND=0, read at create)
     uint32_t emulate_ranks = 0;   // measurement only, see fw_rounds_t
     bool emu_closed = false;
