@@ -740,8 +740,9 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
                 return st;
             }
         }
-        if (const char *e = std::getenv("SRT_FW_BAND")) p->fw_band = e[0] != '0';
+        if (const char *e = std::getenv("SRT_FW_BAND")) p->fw_band = e[0] == '1';
         if (const char *e = std::getenv("SRT_FW_XCD")) p->fw_xcd = e[0] != '0';
+        if (const char *e = std::getenv("SRT_FW_SQ_XCD")) p->fw_sq_xcd = e[0] == '1';
         if (const char *e = std::getenv("SRT_FW_BAND_H")) {
             const int h = std::atoi(e);
             p->fw_band_h = 1;

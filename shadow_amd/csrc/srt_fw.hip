@@ -824,7 +824,7 @@ __device__ __forceinline__ void tile_of(uint32_t t, const Rect &r1, const Rect &
                                         uint32_t &bj) {
     const uint32_t n1 = r1.r.n * r1.c.n;
     if (t < n1) {
-        if (gridDim.x == n1 && n1 >= 64) {
+        if (gridDim.x == n1 && n1 >= 64 && !(ng & (1u << 26))) {  // bit 26: no remap (plan field fw_sq_xcd)
             const uint32_t q = n1 / 8, rr = n1 % 8, xcd = t % 8;
             t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + t / 8;
         }
@@ -2041,7 +2041,8 @@ void launch_group(srt_plan *p, hipStream_t s, uint32_t a, uint32_t g, const Rect
     // bit 16: banded tile order (plan knob SRT_FW_BAND=0 turns it off for A/B timing)
     // bit 24: XCD remap of the triangle order (knob SRT_FW_XCD=1, A/B timing)
     const uint32_t arg = g | (p->fw_band ? 0x10000u : 0u) | band_bits(p->fw_band_h) |
-                         (chain ? 0u : p->fw_ablate << 20) | (p->fw_xcd ? 1u << 24 : 0u);
+                         (chain ? 0u : p->fw_ablate << 20) | (p->fw_xcd ? 1u << 24 : 0u) |
+                         (p->fw_sq_xcd || chain ? 0u : 1u << 26);
     if constexpr (sizeof(K) == 2) {
         if (chain && p->fw_sym)  // r1 only; its transposes are r2 (fw_rounds_group_t)
             hipLaunchKernelGGL((minplus_u16_kernel<5, 2>), dim3(r1.r.n * r1.c.n), dim3(NT3), 0, s, D, p->Vp, a, r1,

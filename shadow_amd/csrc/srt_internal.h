@@ -94,8 +94,13 @@ struct srt_plan {
     int fw_relax = 0;             // u32 rest kernel relax order (SRT_FW_RELAX, A/B)
     uint32_t fw_ablate = 0;       // measurement only: u32 rest-kernel ablations (SRT_FW_ABLATE, see the kernel)
     bool fw_xcd = false;          // triangle rest: XCD remap of the order (knob SRT_FW_XCD=1, A/B timing)
+    // square rest order: plain row-major, dealt round-robin over the XCDs, by
+    // default -- C3 forced square (SRT_FW_SYM=0), rest per build: remapped +
+    // banded 119.3 ms, remapped 120.5, neither 117.9 (the remap concentrates
+    // the group's short tiles on one XCD; see the triangle order in srt_fw.hip)
+    bool fw_sq_xcd = false;       // square rest: XCD remap of the order (knob SRT_FW_SQ_XCD=1, A/B timing)
     uint32_t fw_band_h = 1;       // triangle rest: rows per band (power of 2, knob SRT_FW_BAND_H, read at create)
-    bool fw_band = true;          // grouped launches: banded tile order (knob SRT_FW_BAND=0, read at create)
+    bool fw_band = false;         // grouped launches: banded tile order (knob SRT_FW_BAND=1, read at create)
     uint32_t emulate_ranks = 0;   // measurement only, see fw_rounds_t
     bool emu_closed = false;
     // end-to-end build (srt_compute_shortest_paths): the loss array is uploaded

@@ -4,8 +4,8 @@ One GPU at rest-bound sizes fuses FW rounds in groups: g = 4 when the block
 count is a multiple of 4 and >= 96 (12k nodes), else 2 (srt_fw.hip
 fw_rounds_t); an odd block count, or fewer than 2 g blocks, keeps the
 single-round schedule.  SRT_FW_PAIR forces the grouped schedule at small
-sizes, SRT_FW_GROUP picks g, SRT_FW_NO_PAIR turns it off and SRT_FW_BAND=0
-turns off the banded tile order of grouped launches, so the same graph is
+sizes, SRT_FW_GROUP picks g, SRT_FW_NO_PAIR turns it off and SRT_FW_BAND=1
+turns on the banded tile order of grouped launches, so the same graph is
 closed every way.  Bar: latency bit-exact vs the
 oracle (reference Dijkstra restatement), loss bit-exact (the exact-loss pass
 after the closure), and the grouped table bit-identical to the single-round
