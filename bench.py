@@ -45,9 +45,11 @@ VALU_LANE_OPS_PEAK = 256 * 64 * 2.4e9  # 39.3e12 lane-ops/s (one 4-cycle VALU sl
 # u16 latency keys: v_pk_add_u16 + v_pk_min_u16 relax 2 keys = 1 slot per relaxation;
 # u32: 2 v_add_u32 (double rate) + 1 v_min3_u32 per 2 relaxations = 1 slot (an
 # optimistic basis: the mix measures 28.1 Trelax/s, tools/valu_bench.hip)
-RELAX_PEAK = {"u16": VALU_LANE_OPS_PEAK / 1.0, "u32": VALU_LANE_OPS_PEAK / 1.0, "f64": VALU_LANE_OPS_PEAK / 2.0,
+RELAX_PEAK = {"f16": VALU_LANE_OPS_PEAK / 0.75, "u16": VALU_LANE_OPS_PEAK / 1.0, "u32": VALU_LANE_OPS_PEAK / 1.0, "f64": VALU_LANE_OPS_PEAK / 2.0,
               "u64": VALU_LANE_OPS_PEAK / 4.0}
-RELAX_BASIS = {"u16": "v_pk_add_u16 + v_pk_min_u16 per 2 relaxations (2 keys per VGPR) = 1 VALU slot",
+RELAX_BASIS = {"f16": "2 v_pk_add_f16 + 1 v_pk_minimum3_f16 per 4 relaxations (2 keys per VGPR, two k-steps "
+                      "folded by the 3-input min) = 0.75 VALU slot",
+               "u16": "v_pk_add_u16 + v_pk_min_u16 per 2 relaxations (2 keys per VGPR) = 1 VALU slot",
                "u32": "2 v_add_u32 (issued at twice the rate) + 1 v_min3_u32 per 2 relaxations = 1 VALU slot",
                "f64": "v_add_f64 + v_min_f64 = 2 VALU slots", "u64": "v_lshl_add_u64 + v_cmp + 2 v_cndmask = 4 slots"}
 HBM_PEAK = 8.0e12  # B/s
@@ -373,7 +375,7 @@ def bench_graph(args, cfg, D):
         key = desc.split(":")[1][:3] if desc.startswith("fw") else "u64"
         if desc.startswith("fw"):
             B_TILE = 128
-            kbytes = {"u16": 2, "u32": 4}.get(key, 8)
+            kbytes = {"f16": 2, "u16": 2, "u32": 4}.get(key, 8)
             achieved = work_per_launch / avg_launch_s
             rounds = k_work / max(k_tiles * B_TILE ** 3, 1)
             schedule = {"key": key, "launch_rounds": int(round(rounds)), "ranks": D.world,
@@ -383,6 +385,8 @@ def bench_graph(args, cfg, D):
             roofline = {
                 "bound": "valu", "achieved": achieved / 1e12, "peak": peak / 1e12, "unit": "Trelax/s",
                 "frac": achieved / peak, "traffic": traffic,
+                # f16 keys: also on the 1-slot-per-relaxation basis of the u16 kernel
+                "frac_1slot_basis": achieved / VALU_LANE_OPS_PEAK,
                 "traffic_unit": "HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE: gfx950 16-B/lane correction)",
                 "traffic_source": (f"{traffic_src}: committed rocprofv3 PMC summary of this workload and schedule, "
                                    f"not measured in this run" if traffic_src else
@@ -393,7 +397,8 @@ def bench_graph(args, cfg, D):
                 "algorithmic_hbm_bytes_per_launch": k_tiles / max(k_launches, 1) * B_TILE * B_TILE * kbytes *
                                                     (3 if "sym=triangle" in desc else 2),
                 "rounds_per_tile": rounds,
-                "kernel": f"minplus_{key if key in ('u16', 'u32') else 'glds'}_kernel<0> (FW phase 3, rest)",
+                "kernel": (f"minplus_u16_kernel<0, SYM, F16={key == 'f16'}>" if key in ("f16", "u16") else
+                           f"minplus_{key if key == 'u32' else 'glds'}_kernel<0>") + " (FW phase 3, rest)",
                 "avg_launch_ms": avg_launch_s * 1e3, "relax_per_launch": work_per_launch,
                 "peak_basis": f"{VALU_LANE_OPS_PEAK / 1e12:.1f}e12 VALU lane-op slots/s; {key} keys: "
                               f"{RELAX_BASIS[key]} per relaxation (f64 keys would peak at 19.7, the SURVEY's "

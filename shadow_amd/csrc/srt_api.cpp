@@ -376,7 +376,10 @@ struct PieceUpload {
 // Keys are path latencies in units of g = gcd of all edge latencies (latency
 // only: the loss is recomputed exactly by the loss pass, so no loss bits share
 // the key).  Lmax bounds every shortest-path latency: the longest edge for a
-// complete graph (a direct edge bounds every pair), else (V-1) * max edge.
+// complete graph (a direct edge bounds every pair), else (V-1) * max edge --
+// or, tighter, in-eccentricity + out-eccentricity of one node that reaches
+// and is reached by every node (fw_ecc_bound: d(u,v) <= d(u,s) + d(s,v)).
+// Edges longer than Lmax are then stored saturated at INF (the init kernels).
 // Exactness does not depend on the schedule's read order: (1) every stored
 // value only decreases from its initial value <= INF, so each operand is <=
 // INF and a candidate (sum of two) is <= 2 INF, which the key type holds
@@ -393,11 +396,13 @@ struct PieceUpload {
 // additionally lets the loss pass keep latencies as u32.  Knob
 // SRT_FW_KEY=u32|f64|u64 (measurement / A-B parity only) skips the narrower
 // representations.
-bool choose_key_params(const CsrStats &cs, uint32_t V, KeyParams *kp, int *key_type, std::string *why) {
+bool choose_key_params(const CsrStats &cs, uint32_t V, uint64_t ecc_units, KeyParams *kp, int *key_type, bool *f16,
+                       std::string *why) {
     kp->g = cs.gcd;
     const uint64_t maxu = cs.maxlat / cs.gcd;
-    const unsigned __int128 Lmax =
-        cs.complete ? (unsigned __int128)maxu : (unsigned __int128)(V ? V - 1 : 0) * maxu;
+    unsigned __int128 Lmax = cs.complete ? (unsigned __int128)maxu : (unsigned __int128)(V ? V - 1 : 0) * maxu;
+    // the eccentricity bound (fw_ecc_bound), when the sweeps found one
+    if (ecc_units != ~0ull && (unsigned __int128)ecc_units < Lmax) Lmax = ecc_units;
     kp->lmax = Lmax > (unsigned __int128)~0ull ? ~0ull : (uint64_t)Lmax;
     kp->lat32 = Lmax < 0xffffffffull;
     // knob SRT_FW_KEY = u16 / u32 / f64 / u64: the narrowest key allowed (A/B, tests)
@@ -405,8 +410,14 @@ bool choose_key_params(const CsrStats &cs, uint32_t V, KeyParams *kp, int *key_t
     const bool allow16 = !force || std::strcmp(force, "u16") == 0;
     const int min_type = !force ? srt::KEY_U32 : std::strcmp(force, "u64") == 0 ? srt::KEY_U64
                          : std::strcmp(force, "f64") == 0 ? srt::KEY_F64 : srt::KEY_U32;
+    *f16 = false;
     if (allow16 && 2 * Lmax + 1 < (unsigned __int128)srt::KEY16_INF) {
         *key_type = srt::KEY_U16;
+        // f16 integer arithmetic on the same 2-byte keys (0.75 VALU slot per
+        // relaxation instead of 1): every finite distance < 1024 = F16 INF,
+        // so candidates stay <= 2048, exact in f16 (srt_fw.hip).  SRT_FW_KEY=u16
+        // keeps integer arithmetic (A/B parity tests).
+        *f16 = !force && Lmax < 1024;
         return true;
     }
     if (min_type <= srt::KEY_U32 && 2 * Lmax + 1 < (unsigned __int128)srt::KEY32_INF) {
@@ -694,12 +705,40 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         return dst;
     }
 
+    // 2b. the key-width proof from the real diameter, where the family is
+    //     likely dense, the graph is not complete (complete graphs have the
+    //     longest-edge bound) and (V-1) * max edge would not allow f16 keys
+    uint64_t ecc_units = ~0ull;
+    uint32_t ecc_sweeps = 0;
+    {
+        const uint64_t maxu = cs.maxlat / cs.gcd;
+        const uint64_t nin = g->n_adj - cs.selfloops;
+        const uint32_t want0 = opts ? opts->algo : (uint32_t)SRT_ALGO_AUTO;
+        const bool dense_likely = want0 == SRT_ALGO_FW ||
+                                  (want0 == SRT_ALGO_AUTO && (double)p->Vp * p->Vp * p->Vp / 1.2e13 <
+                                                                 (double)n * ((double)nin + p->V) * 64.0 / 3e12);
+        if (!cs.complete && dense_likely && (unsigned __int128)(p->V ? p->V - 1 : 0) * maxu >= 1024 &&
+            !std::getenv("SRT_FW_NO_ECC")) {
+            uint64_t b = ~0ull;
+            srt_err e2{};
+            if (srt::fw_ecc_bound(p, 512, &b, &ecc_sweeps, &e2) != SRT_OK) {
+                srt_plan_destroy(p);
+                if (err) *err = e2;
+                return SRT_ERR_HIP;
+            }
+            if (b != ~0ull) ecc_units = b / cs.gcd;
+        }
+    }
+    (void)ecc_sweeps;
+    tr.mark("create: eccentricity sweeps");
+
     // 3. kernel family.  Dense closure (FW) costs Vp^3 relaxations at
     // ~1.2e13/s; the batched sparse sweep costs ~n * (E_in + V) row gathers of
     // 8 B with a few re-activations per row, priced at ~64 B per (source,
     // in-edge) at ~3e12 B/s.  AUTO takes the cheaper representable one.
     std::string why_fw, why_sssp;
-    const bool fw_ok = choose_key_params(cs, p->V, &p->kp, &p->key_type, &why_fw);
+    bool f16 = false;
+    const bool fw_ok = choose_key_params(cs, p->V, ecc_units, &p->kp, &p->key_type, &f16, &why_fw);
     // no parallel edges: the FW init can store edge keys instead of atomic-min'ing them
     p->fw_unique_edges = cs.unique;
     const uint64_t n_in = g->n_adj - cs.selfloops;
@@ -730,6 +769,7 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     if (algo == SRT_ALGO_FW) {
         // tuning knob (measurement only): SRT_FW_STAGE=reg selects register staging
         if (const char *e = std::getenv("SRT_FW_STAGE")) p->fw_glds = std::strcmp(e, "reg") != 0;
+        p->fw_f16 = f16 && p->fw_glds;
         if (const char *e = std::getenv("SRT_FW_EMULATE_RANKS")) p->emulate_ranks = (uint32_t)std::atoi(e);
         if (p->emulate_ranks > 1) {
             // emulated rank 0 owns the first max(1, blocks / N) block-rows (fw_rounds_t)
@@ -751,12 +791,15 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         if (const char *e = std::getenv("SRT_FW_RELAX")) p->fw_relax = std::atoi(e);
         if (const char *e = std::getenv("SRT_LOSS_PUSH")) p->loss_push = std::atoi(e) != 0;
         if (const char *e = std::getenv("SRT_FW_ABLATE")) p->fw_ablate = (uint32_t)std::atoi(e) & 15u;
-        std::snprintf(d, sizeof d, "fw:%s B=%d g=%llu lmax=%llu V=%u n=%u stage=%s band=%d loss=tight-dag%s",
-                      p->key_type == srt::KEY_U16   ? "u16key"
+        std::snprintf(d, sizeof d, "fw:%s B=%d g=%llu lmax=%llu%s V=%u n=%u stage=%s band=%d loss=tight-dag%s",
+                      p->fw_f16                     ? "f16key"
+                      : p->key_type == srt::KEY_U16 ? "u16key"
                       : p->key_type == srt::KEY_U32 ? "u32key"
                       : p->key_type == srt::KEY_F64 ? "f64key"
                                                     : "u64key",
-                      srt::FW_B, (unsigned long long)p->kp.g, (unsigned long long)p->kp.lmax, p->V, n,
+                      srt::FW_B, (unsigned long long)p->kp.g, (unsigned long long)p->kp.lmax,
+                      cs.complete ? "(complete)" : ecc_units != ~0ull && ecc_units == p->kp.lmax ? "(ecc)" : "(V-1)",
+                      p->V, n,
                       p->fw_glds ? "glds" : "reg", (int)p->fw_band, p->kp.lat32 ? "/u32" : "/u64");
     } else {
         // R words of 64 sources per lane (one wave walks a vertex's in-edges

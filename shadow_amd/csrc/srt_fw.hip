@@ -145,6 +145,52 @@ __global__ void fill_kernel(K *__restrict__ D, uint32_t Vp, uint32_t r0, uint32_
     }
 }
 
+// f16-key plans (srt_plan::fw_f16): the closure runs on f16 integer keys
+// (exact below 2048, INF = 1024 = 0x6400) and every other stage -- init, the
+// loss pass, the exchanges, fetch -- sees the u16 integer keys
+// (KEY16_INF = unreachable).  One pass each way over D (2 x 2 B per pair,
+// ~0.1 ms at 16k).  Values >= 1024 saturate to INF: exact, since the host
+// proved every finite distance < 1024 (every stored key is then min(real
+// walk, INF), as for u16 / u32 keys).
+constexpr uint16_t F16_INF_BITS = 0x6400;  // 1024.0
+__global__ void keys_to_f16_kernel(uint16_t *__restrict__ D, uint64_t n8) {
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < n8; e += (uint64_t)gridDim.x * blockDim.x) {
+        uint4 v = reinterpret_cast<uint4 *>(D)[e];
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint32_t o = 0;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t k = (w[q] >> (16 * h)) & 0xffffu;
+                const uint16_t f = k >= 1024u ? F16_INF_BITS : __builtin_bit_cast(uint16_t, (_Float16)(float)k);
+                o |= (uint32_t)f << (16 * h);
+            }
+            w[q] = o;
+        }
+        reinterpret_cast<uint4 *>(D)[e] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+__global__ void keys_from_f16_kernel(uint16_t *__restrict__ D, uint64_t n8) {
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < n8; e += (uint64_t)gridDim.x * blockDim.x) {
+        uint4 v = reinterpret_cast<uint4 *>(D)[e];
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint32_t o = 0;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint16_t f = (uint16_t)((w[q] >> (16 * h)) & 0xffffu);
+                const uint32_t k =
+                    f >= F16_INF_BITS ? (uint32_t)KEY16_INF : (uint32_t)(float)__builtin_bit_cast(_Float16, f);
+                o |= k << (16 * h);
+            }
+            w[q] = o;
+        }
+        reinterpret_cast<uint4 *>(D)[e] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
 // key of an edge: its latency in units of g (g divides every edge latency;
 // below 2^53 the f64 quotient of two exact integers is exact, and cheaper
 // than the u64 division)
@@ -174,7 +220,15 @@ __global__ void scatter_edges_kernel(K *__restrict__ D, uint32_t Vp,
             // integer key order == f64 order for exact integers: atomicMin on the
             // u64 value works for both representations (f64 bits of non-negative
             // doubles order like the doubles)
-            const uint64_t key = edge_key(lat[k], kp);
+            // an edge longer than the proved bound (possible under the
+            // eccentricity proof) is never on a shortest path: stored as INF
+            uint64_t key = edge_key(lat[k], kp);
+            if constexpr (std::is_same<K, double>::value) {
+                if (key >= (1ull << 53)) key = 0x7ff0000000000000ull;  // marker, mapped to +inf below
+            } else {
+                const uint64_t inf = KeyOps<K>::to_int(KeyOps<K>::inf());
+                key = key < inf ? key : inf;
+            }
             if constexpr (sizeof(K) == 2) {
                 K *dst = &D[(uint64_t)u * Vp + v];
                 if constexpr (UNIQUE) {
@@ -198,7 +252,7 @@ __global__ void scatter_edges_kernel(K *__restrict__ D, uint32_t Vp,
             } else {
                 uint64_t bits;
                 if constexpr (std::is_same<K, double>::value) {
-                    const double d = (double)key;
+                    const double d = key == 0x7ff0000000000000ull ? KeyOps<double>::inf() : (double)key;
                     bits = __builtin_bit_cast(uint64_t, d);
                 } else {
                     bits = key;
@@ -284,7 +338,16 @@ __global__ __launch_bounds__(16 * (B / P1R)) void fw_phase1_kernel(K *__restrict
 // version's VALU (add, min, and the u16 widening) per step.  Sums stay below
 // 2^16 (both operands <= KEY16_INF), so the packed add never wraps.
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-template <int P1R>
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+// a2 + b of packed keys: u16 integers, or f16 integers (F16; exact below 2048)
+template <bool F16>
+__device__ __forceinline__ us2 add_keys2(us2 a, us2 b) {
+    if constexpr (F16) return __builtin_bit_cast(us2, __builtin_bit_cast(h2, a) + __builtin_bit_cast(h2, b));
+    else return a + b;
+}
+// F16: f16 integer keys (the sum in f16; the min on the bits, which order
+// like the values for non-negative f16)
+template <int P1R, bool F16 = false>
 __global__ __launch_bounds__(16 * (B / P1R)) void fw_phase1_u16pk_kernel(uint16_t *__restrict__ D, uint32_t Vp,
                                                                         uint32_t kb) {
     __shared__ us2 rowbuf[2][B / 2];
@@ -329,7 +392,7 @@ __global__ __launch_bounds__(16 * (B / P1R)) void fw_phase1_u16pk_kernel(uint16_
                 const uint16_t a = colbuf[cur][ty * P1R + i];
                 const us2 a2 = {a, a};
 #pragma unroll
-                for (int q = 0; q < 4; ++q) p[i][q] = __builtin_elementwise_min(p[i][q], a2 + b[q]);
+                for (int q = 0; q < 4; ++q) p[i][q] = __builtin_elementwise_min(p[i][q], add_keys2<F16>(a2, b[q]));
             }
             if (e < 7) publish(g, e + 1, cur ^ 1);
             else if (g + 1 < B / 8) publish(g + 1, 0, cur ^ 1);
@@ -1018,7 +1081,39 @@ __device__ __forceinline__ void relax_pairs16(uint32_t (&acc)[4], uint32_t a, u3
             : "v"(a), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w));
 }
 
-template <int s>
+// f16 keys (F16 below; the host proves every finite distance < F16_INF =
+// 1024 units, so a candidate -- two stored keys, each <= 1024 -- is an
+// integer <= 2048, exact in f16, and non-negative f16 bits order like the
+// integers): two k-steps at once,
+//     acc = v_pk_minimum3_f16(acc, a_k + b_k, a_{k+1} + b_{k+1})
+// for a column pair: 2 v_pk_add_f16 (A's key of step k / k+1 broadcast by
+// op_sel from the packed pair a) + 1 v_pk_minimum3_f16 per 4 relaxations --
+// 0.75 VALU slot per relaxation against the u16 form's 1.0
+// (tools/valu_bench.hip on the box: the f16 mix 50.7 / 47.1 Trelax/s at 8 / 2
+// waves per SIMD, the u16 mix 37.7 / 34.7).  Saturation at INF is exact for
+// the same reason as in u16/u32 (choose_key_params): every stored key is
+// min(real walk, INF).
+__device__ __forceinline__ void relax_pairs_f16(uint32_t (&acc)[4], uint32_t a, u32x4 b0, u32x4 b1) {
+    uint32_t t0, t1, t2, t3, t4, t5, t6, t7;
+    asm volatile(
+        "v_pk_add_f16 %0, %12, %13 op_sel_hi:[0,1]\n\t"
+        "v_pk_add_f16 %1, %12, %17 op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+        "v_pk_add_f16 %2, %12, %14 op_sel_hi:[0,1]\n\t"
+        "v_pk_add_f16 %3, %12, %18 op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+        "v_pk_add_f16 %4, %12, %15 op_sel_hi:[0,1]\n\t"
+        "v_pk_add_f16 %5, %12, %19 op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+        "v_pk_add_f16 %6, %12, %16 op_sel_hi:[0,1]\n\t"
+        "v_pk_add_f16 %7, %12, %20 op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+        "v_pk_minimum3_f16 %8, %8, %0, %1\n\t"
+        "v_pk_minimum3_f16 %9, %9, %2, %3\n\t"
+        "v_pk_minimum3_f16 %10, %10, %4, %5\n\t"
+        "v_pk_minimum3_f16 %11, %11, %6, %7"
+        : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "=&v"(t4), "=&v"(t5), "=&v"(t6), "=&v"(t7), "+v"(acc[0]),
+          "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3])
+        : "v"(a), "v"(b0.x), "v"(b0.y), "v"(b0.z), "v"(b0.w), "v"(b1.x), "v"(b1.y), "v"(b1.z), "v"(b1.w));
+}
+
+template <int s, bool F16>
 __device__ __forceinline__ void chunk_steps16(uint32_t (&acc)[8][4], StepOps16 (&o)[2], uint32_t abase,
                                               uint32_t bbase) {
     if constexpr (s < KC16 / 4) {
@@ -1027,12 +1122,17 @@ __device__ __forceinline__ void chunk_steps16(uint32_t (&acc)[8][4], StepOps16 (
         const StepOps16 &c = o[s & 1];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            relax_pairs16<0>(acc[i], c.a[i].x, c.b[0]);
-            relax_pairs16<1>(acc[i], c.a[i].x, c.b[1]);
-            relax_pairs16<0>(acc[i], c.a[i].y, c.b[2]);
-            relax_pairs16<1>(acc[i], c.a[i].y, c.b[3]);
+            if constexpr (F16) {
+                relax_pairs_f16(acc[i], c.a[i].x, c.b[0], c.b[1]);
+                relax_pairs_f16(acc[i], c.a[i].y, c.b[2], c.b[3]);
+            } else {
+                relax_pairs16<0>(acc[i], c.a[i].x, c.b[0]);
+                relax_pairs16<1>(acc[i], c.a[i].x, c.b[1]);
+                relax_pairs16<0>(acc[i], c.a[i].y, c.b[2]);
+                relax_pairs16<1>(acc[i], c.a[i].y, c.b[3]);
+            }
         }
-        chunk_steps16<s + 1>(acc, o, abase, bbase);
+        chunk_steps16<s + 1, F16>(acc, o, abase, bbase);
     }
 }
 
@@ -1096,7 +1196,8 @@ __device__ __forceinline__ bool tile_of_sym(uint32_t t, const Span &s, uint32_t 
 // stored transposed (the symmetric chain: p2row also writes p2col's tiles,
 // one cross rect also writes the other); 3 = a tile list (symmetric sharded
 // schedule), mirrored like 1 and 2.
-template <int TAG, int SYM = 0>
+// F16: the keys are f16 integers (see relax_pairs_f16), else u16 integers.
+template <int TAG, int SYM = 0, bool F16 = false>
 __global__ __launch_bounds__(NT3, 2) void minplus_u16_kernel(uint16_t *__restrict__ D, uint32_t Vp, uint32_t kb,
                                                              Rect r1, Rect r2, uint32_t ng) {
     __shared__ __attribute__((aligned(16))) uint16_t lds[2 * GBUF16];
@@ -1178,7 +1279,7 @@ __global__ __launch_bounds__(NT3, 2) void minplus_u16_kernel(uint16_t *__restric
         const uint32_t bbase = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint16_t *)Bs;
         StepOps16 o[2];
         lds_step16<0>(o[0], abase, bbase);
-        chunk_steps16<0>(acc, o, abase, bbase);
+        chunk_steps16<0, F16>(acc, o, abase, bbase);
         if (!(abl & 8)) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
@@ -1397,9 +1498,12 @@ __global__ __launch_bounds__(256) void minplus_small_kernel(K *__restrict__ D, u
 // (v_pk_add_u16 + v_pk_min_u16: 8 + 8 VALU per k against the scalar quarter
 // kernel's ~48).  K chunks of 32 staged through LDS, double-buffered.  Every
 // off-diagonal result is also stored transposed into its mirror (symmetric D).
-// LIST: tiles from a list (entries (i << 16) | j, address in r2.r.lo/hi, rows
-// or columns r1.r.x0 / r1.r.x1 skipped), else the rect r1.
-template <int TAG, bool LIST>
+// MODE 2: tiles from a list (entries (i << 16) | j, address in r2.r.lo/hi,
+// rows or columns r1.r.x0 / r1.r.x1 skipped), mirrored; MODE 1: the rect r1,
+// mirrored; MODE 0: the rects r1 then r2, not mirrored (the look-ahead chain
+// of one GPU at chain-bound sizes and of the row-sharded schedule).  F16: f16
+// integer keys (see relax_pairs_f16).
+template <int TAG, int MODE, bool F16>
 __global__ __launch_bounds__(256) void minplus_q16_kernel(uint16_t *__restrict__ D, uint32_t Vp, uint32_t kb, Rect r1,
                                                           Rect r2) {
     constexpr int QK = 32;
@@ -1409,15 +1513,22 @@ __global__ __launch_bounds__(256) void minplus_q16_kernel(uint16_t *__restrict__
     __builtin_amdgcn_s_setprio(2);
     uint32_t t = blockIdx.x >> 2, bi, bj;
     const uint32_t q = blockIdx.x & 3;
-    if constexpr (LIST) {
+    if constexpr (MODE == 2) {
         const uint32_t *tl = reinterpret_cast<const uint32_t *>(((uint64_t)r2.r.hi << 32) | r2.r.lo);
         const uint32_t e = tl[t];
         bi = e >> 16;
         bj = e & 0xffffu;
         if (bi == r1.r.x0 || bj == r1.r.x0 || bi == r1.r.x1 || bj == r1.r.x1) return;
     } else {
-        bi = span_at(r1.r, t / r1.c.n);
-        bj = span_at(r1.c, t % r1.c.n);
+        const uint32_t n1 = r1.r.n * r1.c.n;
+        if (MODE == 1 || t < n1) {
+            bi = span_at(r1.r, t / r1.c.n);
+            bj = span_at(r1.c, t % r1.c.n);
+        } else {
+            t -= n1;
+            bi = span_at(r2.r, t / r2.c.n);
+            bj = span_at(r2.c, t % r2.c.n);
+        }
     }
     const uint64_t i0 = (uint64_t)bi * B + (q >> 1) * SQ, j0 = (uint64_t)bj * B + (q & 1) * SQ;
     const uint64_t k0 = (uint64_t)kb * B;
@@ -1461,8 +1572,8 @@ __global__ __launch_bounds__(256) void minplus_q16_kernel(uint16_t *__restrict__
             for (int i = 0; i < 4; ++i) {
                 const uint16_t a = As[cur][ty * 4 + i][k];
                 const us2 a2 = {a, a};
-                acc[i][0] = __builtin_elementwise_min(acc[i][0], a2 + b0);
-                acc[i][1] = __builtin_elementwise_min(acc[i][1], a2 + b1);
+                acc[i][0] = __builtin_elementwise_min(acc[i][0], add_keys2<F16>(a2, b0));
+                acc[i][1] = __builtin_elementwise_min(acc[i][1], add_keys2<F16>(a2, b1));
             }
         }
         if (ch + 1 < NCH) stash(cur ^ 1);  // the other buffer's readers passed the last barrier
@@ -1475,7 +1586,7 @@ __global__ __launch_bounds__(256) void minplus_q16_kernel(uint16_t *__restrict__
         v.y = __builtin_bit_cast(uint32_t, acc[i][1]);
         *reinterpret_cast<uint2 *>(D + (i0 + ty * 4 + i) * Vp + j0 + tx * 4) = v;
     }
-    if (bi != bj) {
+    if (MODE != 0 && bi != bj) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1568,19 +1679,31 @@ __global__ void delay_kernel(long long ticks) {
     while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
 }
 
+// the u16 kernels of a plan's key arithmetic (f16: fw_f16 plans)
+template <int TAG, int SYM>
+auto u16k(bool f16) {
+    return f16 ? &minplus_u16_kernel<TAG, SYM, true> : &minplus_u16_kernel<TAG, SYM, false>;
+}
+template <int TAG, int MODE>
+auto q16k(bool f16) {
+    return f16 ? &minplus_q16_kernel<TAG, MODE, true> : &minplus_q16_kernel<TAG, MODE, false>;
+}
+template <int P1R>
+auto p1k(bool f16) {
+    return f16 ? &fw_phase1_u16pk_kernel<P1R, true> : &fw_phase1_u16pk_kernel<P1R, false>;
+}
+
 template <typename K>
-void launch_p1(int rows, hipStream_t s, K *D, uint32_t Vp, uint32_t kb) {
+void launch_p1(int rows, hipStream_t s, K *D, uint32_t Vp, uint32_t kb, bool f16 = false) {
     if constexpr (sizeof(K) == 2) {
-        if (!std::getenv("SRT_FW_P1_SCALAR")) {
-            uint16_t *D16 = reinterpret_cast<uint16_t *>(D);
-            if (rows == 2)
-                hipLaunchKernelGGL(fw_phase1_u16pk_kernel<2>, dim3(1), dim3(16 * (B / 2)), 0, s, D16, Vp, kb);
-            else if (rows == 4)
-                hipLaunchKernelGGL(fw_phase1_u16pk_kernel<4>, dim3(1), dim3(16 * (B / 4)), 0, s, D16, Vp, kb);
-            else
-                hipLaunchKernelGGL(fw_phase1_u16pk_kernel<8>, dim3(1), dim3(16 * (B / 8)), 0, s, D16, Vp, kb);
-            return;
-        }
+        uint16_t *D16 = reinterpret_cast<uint16_t *>(D);
+        if (rows == 2)
+            hipLaunchKernelGGL(p1k<2>(f16), dim3(1), dim3(16 * (B / 2)), 0, s, D16, Vp, kb);
+        else if (rows == 4)
+            hipLaunchKernelGGL(p1k<4>(f16), dim3(1), dim3(16 * (B / 4)), 0, s, D16, Vp, kb);
+        else
+            hipLaunchKernelGGL(p1k<8>(f16), dim3(1), dim3(16 * (B / 8)), 0, s, D16, Vp, kb);
+        return;
     }
     if (rows == 2)
         hipLaunchKernelGGL((fw_phase1_kernel<K, 2>), dim3(1), dim3(16 * (B / 2)), 0, s, D, Vp, kb);
@@ -1594,12 +1717,16 @@ template <typename K, int TAG>
 void launch_tiles(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1, const Rect &r2) {
     const uint32_t n = r1.r.n * r1.c.n + r2.r.n * r2.c.n;
     if (!n) return;
-    if (TAG != 0 && p->fw_small_chain)  // sharded look-ahead chain: quarter tiles, lower latency
-        hipLaunchKernelGGL((minplus_small_kernel<K, TAG>), dim3(4 * n), dim3(256), 0, s,
-                           reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2);
-    else if (p->fw_glds) {
+    if (TAG != 0 && p->fw_small_chain) {  // look-ahead chain: quarter tiles, lower latency
         if constexpr (sizeof(K) == 2)
-            hipLaunchKernelGGL((minplus_u16_kernel<TAG>), dim3(n), dim3(NT3), 0, s,
+            hipLaunchKernelGGL((q16k<TAG, 0>(p->fw_f16)), dim3(4 * n), dim3(256), 0, s,
+                               reinterpret_cast<uint16_t *>(p->d_D), p->Vp, kb, r1, r2);
+        else
+            hipLaunchKernelGGL((minplus_small_kernel<K, TAG>), dim3(4 * n), dim3(256), 0, s,
+                               reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2);
+    } else if (p->fw_glds) {
+        if constexpr (sizeof(K) == 2)
+            hipLaunchKernelGGL((u16k<TAG, 0>(p->fw_f16)), dim3(n), dim3(NT3), 0, s,
                                reinterpret_cast<uint16_t *>(p->d_D), p->Vp, kb, r1, r2, 1u);
         else if constexpr (sizeof(K) == 4)
             hipLaunchKernelGGL((minplus_u32_kernel<TAG>), dim3(n), dim3(NT3), 0, s,
@@ -1617,7 +1744,7 @@ void launch_tiles(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1, const
 template <typename K>
 void launch_rest_sym(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1) {
     if constexpr (sizeof(K) == 2)
-        hipLaunchKernelGGL((minplus_u16_kernel<0, 1>), dim3(sym_grid(r1.r.n, p->fw_band_h)), dim3(NT3), 0, s,
+        hipLaunchKernelGGL((u16k<0, 1>(p->fw_f16)), dim3(sym_grid(r1.r.n, p->fw_band_h)), dim3(NT3), 0, s,
                            reinterpret_cast<uint16_t *>(p->d_D), p->Vp, kb, r1,
                            Rect{make_span(0, 0), make_span(0, 0)},
                            1u | band_bits(p->fw_band_h) | (p->fw_xcd ? 1u << 24 : 0u));
@@ -1632,7 +1759,7 @@ void launch_mirror(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1) {
     const uint32_t n = r1.r.n * r1.c.n;
     if (!n) return;
     if constexpr (sizeof(K) == 2)
-        hipLaunchKernelGGL((minplus_u16_kernel<TAG, 2>), dim3(n), dim3(NT3), 0, s,
+        hipLaunchKernelGGL((u16k<TAG, 2>(p->fw_f16)), dim3(n), dim3(NT3), 0, s,
                            reinterpret_cast<uint16_t *>(p->d_D), p->Vp, kb, r1,
                            Rect{make_span(0, 0), make_span(0, 0)}, 1u);
 }
@@ -1720,12 +1847,12 @@ srt_status sym_sharded_setup(srt_plan *p, uint32_t N, uint32_t r, srt_err *err) 
 // a list launch of the SYM == 3 rest kernel: n entries at tl, skipping rows /
 // columns a and b
 void launch_list16(hipStream_t s, uint16_t *D, uint32_t Vp, uint32_t kb, const uint32_t *tl, uint32_t n, uint32_t a,
-                   uint32_t b) {
+                   uint32_t b, bool f16) {
     if (!n) return;
     Span skip{0, 0, a, b, 0};
     const uint64_t addr = reinterpret_cast<uint64_t>(tl);
     Span ptr{(uint32_t)addr, (uint32_t)(addr >> 32), NONE, NONE, 0};
-    hipLaunchKernelGGL((minplus_u16_kernel<0, 3>), dim3(n), dim3(NT3), 0, s, D, Vp, kb, Rect{skip, skip},
+    hipLaunchKernelGGL((u16k<0, 3>(f16)), dim3(n), dim3(NT3), 0, s, D, Vp, kb, Rect{skip, skip},
                        Rect{ptr, ptr}, 1u);
 }
 
@@ -1777,13 +1904,13 @@ srt_status fw_rounds_sym_sharded(srt_plan *p, int p1r, srt_err *err) {
     auto p2row_mirror = [&](hipStream_t s, uint32_t k) {
         const Rect row{make_span(k, k + 1), make_span(0, nblk, k)};
         if (small)
-            hipLaunchKernelGGL((minplus_q16_kernel<1, false>), dim3(4 * row.c.n), dim3(256), 0, s, D, p->Vp, k, row,
+            hipLaunchKernelGGL((q16k<1, 1>(p->fw_f16)), dim3(4 * row.c.n), dim3(256), 0, s, D, p->Vp, k, row,
                                Rect{make_span(0, 0), make_span(0, 0)});
         else
             launch_mirror<uint16_t, 1>(p, s, k, row);
     };
     // prologue: pivot 0 on every rank (the same full initial D)
-    launch_p1<uint16_t>(p1r, M, D, p->Vp, 0u);
+    launch_p1<uint16_t>(p1r, M, D, p->Vp, 0u, p->fw_f16);
     p2row_mirror(M, 0);
     hipEventRecord(p->ev_cross, M);
     hipEvent_t rest_done = p->ev_cross;
@@ -1793,7 +1920,7 @@ srt_status fw_rounds_sym_sharded(srt_plan *p, int p1r, srt_err *err) {
         if (nxt) hipStreamWaitEvent(S, rest_done, 0);
         if (kb) hipStreamWaitEvent(M, p->ev_pivot, 0);
         hipEventRecord(p->ev[2 * p->p3_launches], M);
-        launch_list16(M, D, p->Vp, kb, own, p->tl_own, kb, nxt ? k1 : NONE);
+        launch_list16(M, D, p->Vp, kb, own, p->tl_own, kb, nxt ? k1 : NONE, p->fw_f16);
         rest_done = p->ev[2 * p->p3_launches + 1];
         hipEventRecord(rest_done, M);
         p->p3_launches++;
@@ -1806,10 +1933,10 @@ srt_status fw_rounds_sym_sharded(srt_plan *p, int p1r, srt_err *err) {
             Span skip{0, 0, kb, NONE, 0};
             const uint64_t addr = reinterpret_cast<uint64_t>(cl);
             Span ptr{(uint32_t)addr, (uint32_t)(addr >> 32), NONE, NONE, 0};
-            hipLaunchKernelGGL((minplus_q16_kernel<4, true>), dim3(4 * cn), dim3(256), 0, S, D, p->Vp, kb,
+            hipLaunchKernelGGL((q16k<4, 2>(p->fw_f16)), dim3(4 * cn), dim3(256), 0, S, D, p->Vp, kb,
                                Rect{skip, skip}, Rect{ptr, ptr});
         } else {
-            launch_list16(S, D, p->Vp, kb, cl, cn, kb, NONE);
+            launch_list16(S, D, p->Vp, kb, cl, cn, kb, NONE, p->fw_f16);
         }
         if (cn) hipLaunchKernelGGL(pack_row16_kernel, dim3(cn), dim3(256), 0, S, D, p->Vp, cl, k1, N, myslot);
         // the row all-gather on S itself: nothing else waits on S meanwhile,
@@ -1820,7 +1947,7 @@ srt_status fw_rounds_sym_sharded(srt_plan *p, int p1r, srt_err *err) {
         hipLaunchKernelGGL(unpack_row16_kernel, dim3(nblk), dim3(256), 0, S,
                            emu ? p->d_fbuf : D + (uint64_t)k1 * B * p->Vp, p->Vp, k1, N, S_t,
                            (const uint16_t *)p->d_rowslots);
-        launch_p1<uint16_t>(p1r, S, D, p->Vp, k1);
+        launch_p1<uint16_t>(p1r, S, D, p->Vp, k1, p->fw_f16);
         p2row_mirror(S, k1);
         hipEventRecord(p->ev_pivot, S);
     }
@@ -1923,7 +2050,7 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
     srt_status st = SRT_OK;
     // prologue: pivot 0
     if (own(0)) {
-        launch_p1<K>(p1r, M, D, p->Vp, 0u);
+        launch_p1<K>(p1r, M, D, p->Vp, 0u, p->fw_f16);
         launch_tiles<K, 1>(p, M, 0, Rect{make_span(0, 1), make_span(0, nblk, 0)}, none);
     }
     if (sharded && (st = comm_bcast(p->comm, D, pivot_bytes, 0, M, err)) != SRT_OK) return st;
@@ -1976,7 +2103,7 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
             Rect row = own(k1) ? Rect{make_span(k1, k1 + 1), make_span(0, nblk, kb)} : none;
             launch_tiles<K, 4>(p, S, kb, col, row);
             if (own(k1)) {
-                launch_p1<K>(p1r, S, D, p->Vp, k1);
+                launch_p1<K>(p1r, S, D, p->Vp, k1, p->fw_f16);
                 launch_tiles<K, 1>(p, S, k1, Rect{make_span(k1, k1 + 1), make_span(0, nblk, k1)}, none);
             }
             // pivot-row broadcast on the comm stream C: the owner's chain goes
@@ -2045,15 +2172,15 @@ void launch_group(srt_plan *p, hipStream_t s, uint32_t a, uint32_t g, const Rect
                          (p->fw_sq_xcd || chain ? 0u : 1u << 26);
     if constexpr (sizeof(K) == 2) {
         if (chain && p->fw_sym)  // r1 only; its transposes are r2 (fw_rounds_group_t)
-            hipLaunchKernelGGL((minplus_u16_kernel<5, 2>), dim3(r1.r.n * r1.c.n), dim3(NT3), 0, s, D, p->Vp, a, r1,
+            hipLaunchKernelGGL((u16k<5, 2>(p->fw_f16)), dim3(r1.r.n * r1.c.n), dim3(NT3), 0, s, D, p->Vp, a, r1,
                                Rect{make_span(0, 0), make_span(0, 0)}, arg);
         else if (chain)
-            hipLaunchKernelGGL((minplus_u16_kernel<5>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
+            hipLaunchKernelGGL((u16k<5, 0>(p->fw_f16)), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
         else if (p->fw_sym)  // square span, r2 empty (fw_rounds_group_t)
-            hipLaunchKernelGGL((minplus_u16_kernel<0, 1>), dim3(sym_grid(r1.r.n, p->fw_band_h)), dim3(NT3), 0, s, D,
+            hipLaunchKernelGGL((u16k<0, 1>(p->fw_f16)), dim3(sym_grid(r1.r.n, p->fw_band_h)), dim3(NT3), 0, s, D,
                                p->Vp, a, r1, r2, arg);
         else
-            hipLaunchKernelGGL((minplus_u16_kernel<0>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
+            hipLaunchKernelGGL((u16k<0, 0>(p->fw_f16)), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
     } else if constexpr (sizeof(K) == 4) {
         if (chain)
             hipLaunchKernelGGL((minplus_u32_kernel<5>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
@@ -2083,7 +2210,7 @@ srt_status fw_rounds_group_t(srt_plan *p, int p1r, uint32_t g) {
     const bool symc = p->fw_sym && sizeof(K) == 2 && !p->fw_small_chain;
     auto pivots = [&](hipStream_t s, uint32_t a) {
         for (uint32_t r = a; r < a + g; ++r) {
-            launch_p1<K>(p1r, s, D, p->Vp, r);
+            launch_p1<K>(p1r, s, D, p->Vp, r, p->fw_f16);
             if (symc) {
                 launch_mirror<K, 1>(p, s, r, Rect{make_span(r, r + 1), make_span(0, nblk, r)});
                 if (r + 1 < a + g)
@@ -2228,7 +2355,7 @@ srt_status fw_rounds_group_sharded_t(srt_plan *p, int p1r, uint32_t g, uint32_t 
         const bool o = own(a);
         for (uint32_t r = a; r < a + g; ++r) {
             if (o) {
-                launch_p1<K>(p1r, s, D, p->Vp, r);
+                launch_p1<K>(p1r, s, D, p->Vp, r, p->fw_f16);
                 launch_tiles<K, 1>(p, s, r, Rect{make_span(r, r + 1), make_span(0, nblk, r)}, none);
             }
             if (sharded || emu_bcast_ticks) {
@@ -2294,6 +2421,69 @@ srt_status fw_rounds_group_sharded_t(srt_plan *p, int p1r, uint32_t g, uint32_t 
     return SRT_OK;
 }
 
+// ------------------------------------------------ key-width proof (eccentricity)
+// Bellman-Ford sweeps from one source s over the CSR, both directions at
+// once: dout[v] = d(s, v) by pushes along u -> v (atomic min), din[u] =
+// d(u, s) by the row's own pull over its out-edges (min over k of lat[k] +
+// din[col[k]]; only u's wave writes din[u]).  Values only decrease and every
+// value is a real walk's latency, so racing readers stay correct; the sweeps
+// repeat until one changes nothing.  Sums saturate instead of wrapping.
+__global__ __launch_bounds__(256) void ecc_sweep_kernel(const uint64_t *__restrict__ row_ptr,
+                                                        const uint32_t *__restrict__ col,
+                                                        const uint64_t *__restrict__ lat, uint32_t V,
+                                                        unsigned long long *dout, unsigned long long *din,
+                                                        uint32_t *changed) {
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    bool ch = false;
+    for (uint32_t u = wave; u < V; u += nwaves) {
+        const uint64_t du = __atomic_load_n(&dout[u], __ATOMIC_RELAXED);
+        uint64_t best = ~0ull;
+        for (uint64_t k = row_ptr[u] + lane; k < row_ptr[u + 1]; k += 64) {
+            const uint32_t v = col[k];
+            const uint64_t w = lat[k];
+            if (du != ~0ull && du + w >= du) {
+                const uint64_t nd = du + w;
+                if (nd < __atomic_load_n(&dout[v], __ATOMIC_RELAXED)) {
+                    atomicMin(&dout[v], (unsigned long long)nd);
+                    ch = true;
+                }
+            }
+            const uint64_t dv = __atomic_load_n(&din[v], __ATOMIC_RELAXED);
+            if (dv != ~0ull && dv + w >= dv && dv + w < best) best = dv + w;
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint64_t o = __shfl_xor(best, off);
+            best = o < best ? o : best;
+        }
+        if (lane == 0 && best < __atomic_load_n(&din[u], __ATOMIC_RELAXED)) {
+            __atomic_store_n(&din[u], (unsigned long long)best, __ATOMIC_RELAXED);
+            ch = true;
+        }
+    }
+    if (__builtin_amdgcn_ballot_w64(ch) && lane == 0) *changed = 1;  // every writer stores 1
+}
+
+// out[0] = max dout, out[1] = max din (~0 if any node is unreached)
+__global__ __launch_bounds__(256) void ecc_max_kernel(const unsigned long long *__restrict__ dout,
+                                                      const unsigned long long *__restrict__ din, uint32_t V,
+                                                      unsigned long long *out) {
+    uint64_t a = 0, b = 0;
+    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < V; v += gridDim.x * blockDim.x) {
+        a = dout[v] > a ? dout[v] : a;
+        b = din[v] > b ? din[v] : b;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t x = __shfl_xor(a, off), y = __shfl_xor(b, off);
+        a = x > a ? x : a;
+        b = y > b ? y : b;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(&out[0], (unsigned long long)a);
+        atomicMax(&out[1], (unsigned long long)b);
+    }
+}
+
 }  // namespace
 
 // Once per plan, after the first init (one GPU, u16 keys, knob SRT_FW_SYM=0
@@ -2325,6 +2515,61 @@ srt_status fw_sym_check(srt_plan *p, srt_err *err) {
     return SRT_OK;
 }
 
+// Key-width proof from the graph's real diameter: for a node
+// s that reaches every node and is reached by every node, any pair has
+// d(u, v) <= d(u, s) + d(s, v) <= max_u d(u, s) + max_v d(s, v).  Runs the
+// sweeps above from s = 0 on the uploaded CSR (p->stream, synchronous);
+// *bound_ns = ~0 when s misses a node either way or the sweeps do not settle
+// within max_sweeps (the caller keeps its (V - 1) * max edge bound).
+srt_status fw_ecc_bound(srt_plan *p, uint32_t max_sweeps, uint64_t *bound_ns, uint32_t *sweeps, srt_err *err) {
+    *bound_ns = ~0ull;
+    *sweeps = 0;
+    const uint32_t V = p->V;
+    if (!V) return SRT_OK;
+    unsigned long long *buf = nullptr;  // dout[V], din[V], out[2], flag
+    hipError_t e = hipMalloc(&buf, ((size_t)2 * V + 3) * 8);
+    unsigned long long *dout = buf, *din = buf + V, *out = buf + 2 * (size_t)V;
+    uint32_t *flag = reinterpret_cast<uint32_t *>(buf + 2 * (size_t)V + 2);
+    const unsigned long long zero = 0;
+    if (e == hipSuccess) e = hipMemsetAsync(buf, 0xff, (size_t)2 * V * 8, p->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(dout, &zero, 8, hipMemcpyHostToDevice, p->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(din, &zero, 8, hipMemcpyHostToDevice, p->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(out, 0, 16, p->stream);
+    const uint32_t blocks = std::min<uint32_t>(4096, (V + 3) / 4);
+    bool settled = false;
+    for (uint32_t it = 0; e == hipSuccess && it < max_sweeps; ++it) {
+        uint32_t h = 0;
+        e = hipMemsetAsync(flag, 0, 4, p->stream);
+        if (e != hipSuccess) break;
+        hipLaunchKernelGGL(ecc_sweep_kernel, dim3(blocks), dim3(256), 0, p->stream, p->d_row_ptr, p->d_col, p->d_lat,
+                           V, dout, din, flag);
+        e = hipMemcpyAsync(&h, flag, 4, hipMemcpyDeviceToHost, p->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
+        *sweeps = it + 1;
+        if (e == hipSuccess && !h) {
+            settled = true;
+            break;
+        }
+    }
+    unsigned long long m[2] = {~0ull, ~0ull};
+    if (e == hipSuccess && settled) {
+        hipLaunchKernelGGL(ecc_max_kernel, dim3(std::min<uint32_t>(1024, (V + 255) / 256)), dim3(256), 0, p->stream,
+                           dout, din, V, out);
+        e = hipMemcpyAsync(m, out, 16, hipMemcpyDeviceToHost, p->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
+    }
+    hipFree(buf);
+    if (e != hipSuccess) {
+        if (err) {
+            err->code = SRT_ERR_HIP;
+            std::snprintf(err->msg, sizeof err->msg, "eccentricity sweeps: %s", hipGetErrorString(e));
+        }
+        return SRT_ERR_HIP;
+    }
+    if (settled && m[0] != ~0ull && m[1] != ~0ull && m[0] + m[1] >= m[0]) *bound_ns = m[0] + m[1];
+    return SRT_OK;
+}
+
 void fw_init(srt_plan *p) {
     if (p->key_type == KEY_U16) fw_init_t<uint16_t>(p);
     else if (p->key_type == KEY_U32) fw_init_t<uint32_t>(p);
@@ -2339,7 +2584,16 @@ srt_status fw_gather_keys(srt_plan *p, srt_err *err) {
 }
 
 srt_status fw_rounds(srt_plan *p, srt_err *err) {
-    if (p->key_type == KEY_U16) return fw_rounds_t<uint16_t>(p, err);
+    if (p->key_type == KEY_U16) {
+        // f16 plans: D to f16 keys and back around the closure, on the main
+        // stream (every schedule's last kernel runs there, or joins it)
+        const uint64_t n8 = (uint64_t)p->Vp * p->Vp / 8;
+        uint16_t *D = reinterpret_cast<uint16_t *>(p->d_D);
+        if (p->fw_f16) hipLaunchKernelGGL(keys_to_f16_kernel, dim3(4096), dim3(256), 0, p->stream, D, n8);
+        const srt_status st = fw_rounds_t<uint16_t>(p, err);
+        if (p->fw_f16) hipLaunchKernelGGL(keys_from_f16_kernel, dim3(4096), dim3(256), 0, p->stream, D, n8);
+        return st;
+    }
     if (p->key_type == KEY_U32) return fw_rounds_t<uint32_t>(p, err);
     return p->key_type == KEY_F64 ? fw_rounds_t<double>(p, err) : fw_rounds_t<uint64_t>(p, err);
 }

@@ -77,6 +77,7 @@ struct srt_plan {
     srt::KeyParams kp{};
     int key_type = srt::KEY_F64;  // closure keys: u32 / f64 (exact integers < 2^53) / u64
     bool fw_glds = true;   // FW tiles staged by LDS-DMA (false: register staging)
+    bool fw_f16 = false;   // u16-stored keys relaxed as f16 integers (every finite distance < 1024 units)
     bool fw_small_chain = false;  // quarter-tile kernels for the look-ahead chain (sharded)
     bool fw_unique_edges = false; // no parallel edges: FW init stores instead of atomic min
     bool fw_sym = false;          // D symmetric (fw_sym_check): rest launches run the triangle
@@ -242,6 +243,9 @@ srt_status comm_allgather_inplace(srt_comm *c, void *buf, size_t bytes_per_rank,
 // kernels (srt_fw.hip)
 void fw_init(srt_plan *p);
 srt_status fw_sym_check(srt_plan *p, srt_err *err);
+// key-width proof: a bound on every finite distance (ns) from one source's
+// in- and out-eccentricity, ~0 if none (srt_fw.hip)
+srt_status fw_ecc_bound(srt_plan *p, uint32_t max_sweeps, uint64_t *bound_ns, uint32_t *sweeps, srt_err *err);
 srt_status fw_rounds(srt_plan *p, srt_err *err);
 // sharded closure: every rank's block-rows of D to every rank (the loss
 // pass's fallback when the sharded tail does not apply)

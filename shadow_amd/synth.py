@@ -42,6 +42,32 @@ def complete_csr(n: int, seed: int, lat_ms=(1, 300), loss_max=0.01, edges=None):
     return row_ptr, col, L.reshape(-1), P.reshape(-1)
 
 
+def dense_graph(n: int, seed: int, drop=0.3, lat_ms=(1, 300), loss_max=0.01):
+    """The complete graph of complete_graph(n, seed) with a seeded fraction
+    `drop` of its off-diagonal undirected edges removed (self-loops kept):
+    a dense NON-complete graph, so the key-width proof cannot use the
+    longest-edge bound and runs the eccentricity sweeps (fw_ecc_bound).
+    Returns the kept edge list (i <= j)."""
+    src, dst, lat, loss = complete_graph(n, seed, lat_ms, loss_max)
+    keep = (src == dst) | (np.random.default_rng(seed + 1000).random(len(src)) >= drop)
+    return src[keep], dst[keep], lat[keep], loss[keep]
+
+
+def dense_csr(n: int, edges):
+    """CSR of an undirected edge list without parallel edges (i <= j each
+    once, self-loops once): row u lists its neighbours in increasing order,
+    as the GML reader's adjacency of a graph written in node order."""
+    src, dst, lat, loss = edges
+    a = np.concatenate([src, dst[src != dst]]).astype(np.int64)
+    b = np.concatenate([dst, src[src != dst]]).astype(np.int64)
+    la = np.concatenate([lat, lat[src != dst]])
+    lo = np.concatenate([loss, loss[src != dst]])
+    order = np.lexsort((b, a))
+    row_ptr = np.concatenate([[0], np.cumsum(np.bincount(a, minlength=n))]).astype(np.uint64)
+    return (row_ptr, b[order].astype(np.uint32), la[order].astype(np.uint64),
+            lo[order].astype(np.float32))
+
+
 def gml_text(n_nodes: int, src, dst, lat_ns, loss, directed=False, bandwidth="1 Gbit") -> str:
     """Shadow GML (docs/network_graph_spec.md) for an edge list; latency is
     written in ms when exact, else ns; packet_loss as a 6-decimal float token."""

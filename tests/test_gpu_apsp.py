@@ -171,11 +171,13 @@ def test_c2_scale_row_sample():
         assert np.array_equal(t.packet_loss[r].view(np.uint32), exp_loss.view(np.uint32))
 
 
-def test_u64_key_path_large_latencies():
+def test_u64_key_path_large_latencies(monkeypatch):
     """Latencies up to 2^51 ns with no common unit on a 20-node sparse graph:
-    2 * Lmax does not fit 53 bits, so the closure runs on u64 keys (the LDS-DMA
-    tile kernel's integer branch) and the loss pass on u64 latencies (rows in
-    global memory); latency and loss stay bit-exact."""
+    with the (V-1) x max edge proof (SRT_FW_NO_ECC: the eccentricity bound
+    would allow f64) 2 * Lmax does not fit 53 bits, so the closure runs on u64
+    keys (the LDS-DMA tile kernel's integer branch) and the loss pass on u64
+    latencies (rows in global memory); latency and loss stay bit-exact."""
+    monkeypatch.setenv("SRT_FW_NO_ECC", "1")
     n = 20
     src, dst, lat, loss = synth.random_graph(n, 31, p_edge=0.3, lat_range_ns=(1, 2**31), loss_max=0.01)
     lat = (lat.astype(np.uint64) << np.uint64(20)) + np.uint64(1)

@@ -80,15 +80,17 @@ def test_groups_equal_single_round(monkeypatch, n):
 
 @pytest.mark.parametrize("n,seed,directed", [(1000, 11, False), (1300, 12, True)])
 def test_key_types_agree(monkeypatch, n, seed, directed):
-    """The closure's four key representations (u16 by default here: 2 (n-1)
-    x 9 units < 2^15 - 1; u32, f64 and u64 forced by SRT_FW_KEY) produce the
-    same table bits, single-round and grouped by 2 and 4."""
+    """The closure's five key representations (f16 by default here: the
+    eccentricity proof; u16, u32, f64 and u64 forced by SRT_FW_KEY) produce
+    the same table bits, single-round and grouped by 2 and 4."""
     e = synth.random_graph(n, seed, p_edge=6.0 / n, directed=directed, lat_range_ns=(1, 9), loss_max=0.05)
     g = NetworkGraph.from_edges(n, *e, directed=directed)
     nodes = np.random.default_rng(seed).permutation(n).astype(np.uint32)
     tabs = {}
-    for key in ("u16", "u32", "f64", "u64"):
-        if key == "u16":
+    # default: f16 keys (the eccentricity proof bounds every distance far below
+    # 1024 units: a random graph of 9-unit edges); the rest forced
+    for key in ("f16", "u16", "u32", "f64", "u64"):
+        if key == "f16":
             monkeypatch.delenv("SRT_FW_KEY", raising=False)
         else:
             monkeypatch.setenv("SRT_FW_KEY", key)
@@ -103,6 +105,49 @@ def test_key_types_agree(monkeypatch, n, seed, directed):
     for k, t in tabs.items():
         assert np.array_equal(t.latency_ns, ref.latency_ns), k
         assert np.array_equal(t.packet_loss.view(np.uint32), ref.packet_loss.view(np.uint32)), k
+
+
+@pytest.mark.parametrize("n,sym,group", [(1000, "1", None), (2048, "1", "2"), (2048, "1", "4"), (2048, "0", "4"),
+                                         (4096, "1", None), (4096, "0", None), (8192, "1", None)])
+def test_f16_keys_equal_u16(monkeypatch, n, sym, group):
+    """Complete graphs (lmax = the longest edge, 300 units < 1024) close on
+    f16 integer keys by default (v_pk_add_f16 + v_pk_minimum3_f16); the table
+    must be bit-identical to the u16-integer closure (SRT_FW_KEY=u16) -- and,
+    at 1000 nodes, to the oracle.  Covers the single-round schedule with the
+    quarter-tile chain (1000, 4096: C2), forced groups, the grouped triangle
+    (8192) and the square (SRT_FW_SYM=0)."""
+    monkeypatch.setenv("SRT_FW_SYM", sym)
+    if group:
+        monkeypatch.setenv("SRT_FW_PAIR", "1")
+        monkeypatch.setenv("SRT_FW_GROUP", group)
+    if n <= 2048:
+        src, dst, lat, loss = synth.complete_graph(n, 20 + n % 7)
+        g = NetworkGraph.from_edges(n, src, dst, lat, loss)
+    else:
+        row_ptr, col, lat, loss = synth.complete_csr(n, 21)
+        g = NetworkGraph(n, np.arange(n, dtype=np.uint32), row_ptr, col, lat, loss, directed=False)
+    nodes = np.arange(n, dtype=np.uint32)
+    tabs = {}
+    for key in ("f16", "u16"):
+        if key == "u16":
+            monkeypatch.setenv("SRT_FW_KEY", "u16")
+        else:
+            monkeypatch.delenv("SRT_FW_KEY", raising=False)
+        plan = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_FW)
+        try:
+            assert plan.describe().startswith(f"fw:{key}key"), plan.describe()
+            tabs[key] = plan.run().fetch()
+            assert ("sym=triangle" in plan.describe()) == (sym == "1")
+        finally:
+            plan.close()
+    assert np.array_equal(tabs["f16"].latency_ns, tabs["u16"].latency_ns)
+    assert np.array_equal(tabs["f16"].packet_loss.view(np.uint32), tabs["u16"].packet_loss.view(np.uint32))
+    assert tabs["f16"].min_latency_ns == tabs["u16"].min_latency_ns
+    if n == 1000:
+        from oracle import oracle as O
+        elat, eloss = O.compute_shortest_paths(O.Graph(False, nodes, src, dst, lat, loss), nodes)
+        assert np.array_equal(tabs["f16"].latency_ns, elat)
+        assert np.array_equal(tabs["f16"].packet_loss.view(np.uint32), eloss.view(np.uint32))
 
 
 @pytest.mark.parametrize("n,complete", [(8192, True), (1500, False)])
@@ -145,5 +190,87 @@ def test_directed_graph_keeps_the_full_square():
     try:
         plan.run()
         assert "sym=triangle" not in plan.describe()
+    finally:
+        plan.close()
+
+
+def _dense_nc(n, seed, drop=0.3):
+    e = synth.dense_graph(n, seed, drop=drop)
+    row_ptr, col, lat, loss = synth.dense_csr(n, e)
+    return e, NetworkGraph(n, np.arange(n, dtype=np.uint32), row_ptr, col, lat, loss, directed=False)
+
+
+@pytest.mark.parametrize("n,rows", [(1024, None), (4096, 16)])
+def test_eccentricity_proof_dense_noncomplete(n, rows):
+    """A dense NON-complete graph (30% of the complete graph's edges dropped):
+    the longest-edge bound does not apply and (V-1) x 300 units would force
+    u32 keys; the eccentricity sweeps bound every distance by d(u,s) + d(s,v)
+    and the plan closes on f16 keys.  Table vs the oracle: in full at 1024,
+    16 seeded rows at 4096 (C2-sized)."""
+    from oracle import oracle as O
+    e, g = _dense_nc(n, 30 + n % 5)
+    nodes = np.arange(n, dtype=np.uint32)
+    plan = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_FW)
+    try:
+        d = plan.describe()
+        assert d.startswith("fw:f16key") and "(ecc)" in d, d
+        t = plan.run().fetch()
+    finally:
+        plan.close()
+    og = O.Graph(False, nodes, *e)
+    if rows is None:
+        elat, eloss = O.compute_shortest_paths(og, nodes)
+        assert np.array_equal(t.latency_ns, elat)
+        assert np.array_equal(t.packet_loss.view(np.uint32), eloss.view(np.uint32))
+        return
+    pick = np.random.default_rng(n).choice(n, rows, replace=False)
+    order = np.concatenate([pick, np.setdiff1d(nodes, pick)]).astype(np.uint32)
+    elat, eloss = O.compute_shortest_paths(og, order, src_count=rows, mode=1)
+    inv = np.empty(n, np.int64)
+    inv[order] = np.arange(n)
+    for i, r in enumerate(pick):
+        exp_l, exp_p = elat[i][inv], eloss[i][inv].view(np.uint32)
+        exp_l[r], exp_p[r] = t.latency_ns[r, r], t.packet_loss[r, r].view(np.uint32)  # raw self-loop
+        assert np.array_equal(t.latency_ns[r], exp_l), r
+        assert np.array_equal(t.packet_loss[r].view(np.uint32), exp_p), r
+
+
+def test_eccentricity_proof_saturates_long_edges():
+    """Edges far longer than the graph's diameter (50,000 units, > the u16
+    and f16 key ranges) cannot lie on a shortest path: the init stores them
+    as INF and the narrow key stays exact -- vs the oracle in full."""
+    from oracle import oracle as O
+    n = 600
+    src, dst, lat, loss = synth.random_graph(n, 91, p_edge=0.05, lat_range_ns=(1, 9), loss_max=0.05)
+    lat = lat.copy()
+    long_ = np.random.default_rng(91).random(len(lat)) < 0.02
+    lat[long_ & (src != dst)] = 50_000
+    g = NetworkGraph.from_edges(n, src, dst, lat, loss, directed=False)
+    nodes = np.arange(n, dtype=np.uint32)
+    plan = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_FW)
+    try:
+        assert plan.describe().startswith("fw:f16key") and "(ecc)" in plan.describe(), plan.describe()
+        t = plan.run().fetch()
+    finally:
+        plan.close()
+    elat, eloss = O.compute_shortest_paths(O.Graph(False, nodes, src, dst, lat, loss), nodes)
+    assert np.array_equal(t.latency_ns, elat)
+    assert np.array_equal(t.packet_loss.view(np.uint32), eloss.view(np.uint32))
+
+
+def test_eccentricity_proof_needs_strong_connectivity():
+    """A directed graph with a node nobody reaches: the sweeps from node 0 miss
+    it, so no diameter bound is claimed and the (V-1) x max edge proof picks
+    the key (u16 here: 2 x 299 x 9 < 2^15)."""
+    n = 300
+    src, dst, lat, loss = synth.random_graph(n, 92, p_edge=0.05, directed=True, lat_range_ns=(1, 9))
+    keep = dst != 7  # no edge into node 7 (its self-loop is dropped too ...)
+    src, dst, lat, loss = src[keep], dst[keep], lat[keep], loss[keep]
+    src, dst = np.append(src, 7).astype(np.uint32), np.append(dst, 7).astype(np.uint32)  # ... and restored
+    lat, loss = np.append(lat, 3).astype(np.uint64), np.append(loss, 0.0).astype(np.float32)
+    g = NetworkGraph.from_edges(n, src, dst, lat, loss, directed=True)
+    plan = RoutingPlan(g, np.array([0, 1, 2], np.uint32), algo=_lib.SRT_ALGO_FW)
+    try:
+        assert plan.describe().startswith("fw:u16key") and "(V-1)" in plan.describe(), plan.describe()
     finally:
         plan.close()

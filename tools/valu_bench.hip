@@ -172,6 +172,81 @@ __global__ __launch_bounds__(256) void k_mix_u16(unsigned *out, unsigned seed) {
     if (seed == 12345u) out[threadIdx.x] = sink;
 }
 
+// f16 integer keys (exact below 2048): per row and k-pair, two packed adds
+// (A[r][k] / A[r][k+1] broadcast by op_sel) and one v_pk_minimum3_f16 fold
+// four candidates into a column pair: 3 instructions per 4 relaxations
+K32(k_pk_add_f16, "v_pk_add_f16")
+K32(k_pk_min_f16, "v_pk_min_f16")
+K32_3(k_pk_minimum3_f16, "v_pk_minimum3_f16")
+K32_3(k_minimum3_f32, "v_minimum3_f32")
+K32_3(k_min3_f32, "v_min3_f32")
+K64(k_pk_add_f32, "v_pk_add_f32 %0, %0, %1")
+__global__ __launch_bounds__(256) void k_mix_f16(unsigned *out, unsigned seed) {
+    unsigned acc[16];
+    for (int i = 0; i < 16; ++i) acc[i] = 0x64006400u;  // (1024, 1024)
+    unsigned a0 = 0x3c003c00u + (threadIdx.x & 7), b0 = 0x40004000u + seed, b1 = b0 + 1, b2 = b0 + 2,
+             b3 = b0 + 3, b4 = b0 + 4, b5 = b0 + 5, b6 = b0 + 6, b7 = b0 + 7;
+    for (int it = 0; it < ITER; ++it) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            unsigned t0, t1, t2, t3;
+            asm volatile(
+                "v_pk_add_f16 %0, %8, %9 op_sel_hi:[0,1]\n\t"
+                "v_pk_add_f16 %1, %8, %10 op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+                "v_pk_add_f16 %2, %8, %11 op_sel_hi:[0,1]\n\t"
+                "v_pk_add_f16 %3, %8, %12 op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+                "v_pk_minimum3_f16 %4, %4, %0, %1\n\t"
+                "v_pk_minimum3_f16 %5, %5, %2, %3\n\t"
+                "v_pk_add_f16 %0, %8, %13 op_sel_hi:[0,1]\n\t"
+                "v_pk_add_f16 %1, %8, %14 op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+                "v_pk_add_f16 %2, %8, %15 op_sel_hi:[0,1]\n\t"
+                "v_pk_add_f16 %3, %8, %16 op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+                "v_pk_minimum3_f16 %6, %6, %0, %1\n\t"
+                "v_pk_minimum3_f16 %7, %7, %2, %3"
+                : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "+v"(acc[4 * q]), "+v"(acc[4 * q + 1]),
+                  "+v"(acc[4 * q + 2]), "+v"(acc[4 * q + 3])
+                : "v"(a0), "v"(b0), "v"(b1), "v"(b2), "v"(b3), "v"(b4), "v"(b5), "v"(b6), "v"(b7));
+        }
+    }
+    unsigned sink = 0;
+    for (int i = 0; i < 16; ++i) sink ^= acc[i];
+    if (seed == 12345u) out[threadIdx.x] = sink;
+}
+
+// f32 integer keys (exact below 2^24): v_pk_add_f32 forms two candidates (A
+// broadcast), v_min3_f32 folds two into one accumulator: 2 instructions per 2
+// relaxations if the packed add issues at full rate
+__global__ __launch_bounds__(256) void k_mix_f32(unsigned *out, unsigned seed) {
+    float acc[16];
+    for (int i = 0; i < 16; ++i) acc[i] = 1e9f;
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 a0 = {1.0f + (threadIdx.x & 7), 2.0f}, b0 = {(float)seed, 3.0f}, b1 = b0 + 1.0f, b2 = b0 + 2.0f,
+       b3 = b0 + 3.0f;
+    for (int it = 0; it < ITER; ++it) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            f2 t0, t1, t2, t3;
+            asm volatile(
+                "v_pk_add_f32 %0, %4, %5 op_sel_hi:[0,1]\n\t"
+                "v_pk_add_f32 %1, %4, %6 op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+                "v_pk_add_f32 %2, %4, %7 op_sel_hi:[0,1]\n\t"
+                "v_pk_add_f32 %3, %4, %8 op_sel:[1,0] op_sel_hi:[1,1]"
+                : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3)
+                : "v"(a0), "v"(b0), "v"(b1), "v"(b2), "v"(b3));
+            asm volatile(
+                "v_min3_f32 %0, %0, %4, %5\n\t"
+                "v_min3_f32 %1, %1, %6, %7\n\t"
+                "v_min3_f32 %2, %2, %8, %9\n\t"
+                "v_min3_f32 %3, %3, %10, %11"
+                : "+v"(acc[4 * q]), "+v"(acc[4 * q + 1]), "+v"(acc[4 * q + 2]), "+v"(acc[4 * q + 3])
+                : "v"(t0.x), "v"(t1.x), "v"(t0.y), "v"(t1.y), "v"(t2.x), "v"(t3.x), "v"(t2.y), "v"(t3.y));
+        }
+    }
+    float sink = 0;
+    for (int i = 0; i < 16; ++i) sink += acc[i];
+    if (seed == 12345u) out[threadIdx.x] = __float_as_uint(sink);
+}
+
 typedef void (*kfn)(unsigned *, unsigned);
 
 static void run(const char *name, kfn k, int instr_per_iter, unsigned *d, int grid = 2048) {
@@ -216,6 +291,18 @@ int main() {
     run("mix_u16 8w/SIMD", k_mix_u16, 32, d);
     run("mix_u16 2w/SIMD", k_mix_u16, 32, d, 512);
     run("v_min3 2w/SIMD", k_min3_u32, 8, d, 512);
+    run("v_pk_add_f16", k_pk_add_f16, 8, d);
+    run("v_pk_min_f16", k_pk_min_f16, 8, d);
+    run("v_pk_minimum3_f16", k_pk_minimum3_f16, 8, d);
+    run("v_minimum3_f32", k_minimum3_f32, 8, d);
+    run("v_min3_f32", k_min3_f32, 8, d);
+    run("v_pk_add_f32", k_pk_add_f32, 8, d);
+    // per relaxation: 4 blocks x 16 relaxations (12 instructions) per iteration
+    run("mix_f16 8w/SIMD", k_mix_f16, 64, d);
+    run("mix_f16 2w/SIMD", k_mix_f16, 64, d, 512);
+    // per relaxation: 4 blocks x 8 relaxations (8 instructions) per iteration
+    run("mix_f32 8w/SIMD", k_mix_f32, 32, d);
+    run("mix_f32 2w/SIMD", k_mix_f32, 32, d, 512);
     hipFree(d);
     return 0;
 }
