@@ -762,6 +762,9 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         return fail(SRT_ERR_UNSUPPORTED, ("no exact path key for this graph: " + why).c_str());
     }
     p->algo = algo;
+    // SSSP plans read their in-edges (with loss) from the host-built list, never
+    // d_loss: drop the deferred upload so run_tail does not copy it
+    if (algo == SRT_ALGO_SSSP) p->h_loss_defer = nullptr;
     p->row0 = 0;
     p->row1 = n;
     p->rows_alloc = n;

@@ -228,7 +228,7 @@ struct srt_plan {
                                            // u16 when stage16 (u16 keys), else u32
     bool stage16 = false;
     float *d_sloss = nullptr;              // nranks * lrow_max * n
-    uint4 *d_tlist = nullptr;              // nranks * tlist_cap tight edges {v, u, w, 1-e bits} (v = ~0: pad)
+    uint4 *d_tlist = nullptr;              // tlist_cap allocated slots of tight edges {v, u, w, 1-e bits} (v = ~0: pad)
     uint64_t tlist_cap = 0;
     unsigned long long *d_tinfo = nullptr; // 2 per rank: local tight-edge count, max tight latency
     unsigned long long *d_tcursor = nullptr;  // list fill cursor

@@ -765,12 +765,11 @@ srt_status launch_fold(srt_plan *p, unsigned long long *d_stats, uint32_t ubits,
     LatT *lat_all = reinterpret_cast<LatT *>(base + ord_b);
     float *loss_all = reinterpret_cast<float *>(base + ord_b + lat_b);
     auto kern = tight_loss_kernel<LatT, LROWS, LPT, PACKED, PUSH>;
-    static bool lds_attr_set = false;  // per instantiation
-    if (LROWS && !lds_attr_set) {
+    // set on every launch (cheap): a once-per-process flag would miss a
+    // second device and race between plans built concurrently
+    if (LROWS)
         (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)(LDS_BUDGET - 4096));
-        lds_attr_set = true;
-    }
     if (rows)
         hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, p->stream, (const void *)p->d_D, p->key_type, p->Vp, V,
                            p->d_nodes, p->n, job.list ? 0u : job.range ? job.r0 : p->row0,
@@ -859,6 +858,20 @@ srt_status sort_packed(srt_plan *p, uint32_t ubits, uint64_t maxw, srt_err *err)
     return SRT_OK;
 }
 
+// The tight-edge list buffer holds p->tlist_cap uint4 slots in every path
+// (one GPU: the whole list; sharded and emulated: W per-rank chunks of C
+// slots).  Grow to `cap` slots when fewer than `need` are allocated.
+static srt_status ensure_tlist(srt_plan *p, uint64_t cap, uint64_t need, srt_err *err) {
+    if (p->d_tlist && need <= p->tlist_cap) return SRT_OK;
+    (void)hipFree(p->d_tlist);
+    p->d_tlist = nullptr;
+    p->tlist_cap = 0;
+    hipError_t e = hipMalloc(&p->d_tlist, cap * sizeof(uint4));
+    if (e != hipSuccess) return fail(err, e, "hipMalloc(tight list)");
+    p->tlist_cap = cap;
+    return SRT_OK;
+}
+
 // Push-form tight CSR on one GPU: the flagged adjacency entries compacted
 // per source row (tight_list_kernel), then rows by source u, packed with v and
 // sorted by w.  *done = false: not packable, the caller builds the pull form.
@@ -889,14 +902,7 @@ srt_status tight_csr_push_t(srt_plan *p, unsigned long long *d_stats, bool *done
     p->t_edges = total;
     if ((st = ensure_edge_arrays(p, err)) != SRT_OK) return st;
     const uint64_t C = std::max<uint64_t>(total, 1);
-    if (C > p->tlist_cap || !p->d_tlist) {
-        const uint64_t cap = C + C / 4 + 64;
-        (void)hipFree(p->d_tlist);
-        p->d_tlist = nullptr;
-        p->tlist_cap = 0;
-        if ((e = hipMalloc(&p->d_tlist, cap * sizeof(uint4))) != hipSuccess) return fail(err, e, "hipMalloc(tight list)");
-        p->tlist_cap = cap;
-    }
+    if ((st = ensure_tlist(p, C + C / 4 + 64, C, err)) != SRT_OK) return st;
     hipLaunchKernelGGL(tight_list_kernel, dim3(blocks), dim3(256), 0, M, 0u, V, p->d_row_ptr, p->d_col, p->d_lat,
                        p->d_loss, p->kp.g, p->d_tflag, p->d_tlist, p->d_tcursor);
     const uint32_t lblocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, (total + 255) / 256));
@@ -1038,14 +1044,7 @@ srt_status tight_csr_shard_t(srt_plan *p, unsigned long long *d_stats, bool *sha
     const uint32_t ubits = (uint32_t)std::max(1, bits_of(V ? V - 1 : 0));
     if (!(p->kp.lat32 && ubits + bits_of(maxw) <= 32 && total < (1ull << 32) && !std::getenv("SRT_LOSS_UNPACKED")))
         return SRT_OK;
-    if (C > p->tlist_cap || !p->d_tlist) {
-        const uint64_t cap = C + C / 4 + 64;
-        (void)hipFree(p->d_tlist);
-        p->d_tlist = nullptr;
-        p->tlist_cap = 0;
-        if ((e = hipMalloc(&p->d_tlist, cap * W * sizeof(uint4))) != hipSuccess) return fail(err, e, "hipMalloc(tight list)");
-        p->tlist_cap = cap;
-    }
+    if ((st = ensure_tlist(p, (C + C / 4 + 64) * W, C * W, err)) != SRT_OK) return st;
     // own chunk: the records, then v = ~0 padding up to C
     (void)hipMemsetAsync(p->d_tlist + (uint64_t)r * C, 0xff, C * sizeof(uint4), M);
     if (own_rows)
@@ -1182,14 +1181,8 @@ srt_status loss_emulated_t(srt_plan *p, unsigned long long *d_stats, srt_err *er
     const uint32_t ubits = (uint32_t)std::max(1, bits_of(V ? V - 1 : 0));
     if (!(p->kp.lat32 && ubits + bits_of(maxw) <= 32 && total < (1ull << 32)))
         return fail(err, hipErrorNotSupported, "rank emulation needs the packed tight-edge form");
-    if (C > p->tlist_cap || !p->d_tlist) {
-        (void)hipFree(p->d_tlist);
-        p->d_tlist = nullptr;
-        p->tlist_cap = 0;
-        if ((e = hipMalloc(&p->d_tlist, C * W * sizeof(uint4))) != hipSuccess) return fail(err, e, "hipMalloc(tight list)");
-        p->tlist_cap = C;
-    }
     const uint64_t slots = C * W;
+    if ((st = ensure_tlist(p, slots, slots, err)) != SRT_OK) return st;
     (void)hipMemsetAsync(p->d_tlist, 0xff, slots * sizeof(uint4), M);
     const uint32_t vblocks = std::max<uint32_t>(1, std::min<uint32_t>(8192, (V + 3) / 4));
     hipLaunchKernelGGL(tight_list_kernel, dim3(vblocks), dim3(256), 0, M, 0u, V, p->d_row_ptr, p->d_col, p->d_lat,

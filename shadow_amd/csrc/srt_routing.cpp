@@ -92,11 +92,14 @@ srt_status srt_routing_info_build(const srt_csr *g, const uint32_t *nodes, uint3
         return SRT_ERR_INVALID;
     }
     *out = nullptr;
-    for (uint32_t i = 0; i < n; ++i)
-        if (nodes[i] >= g->n_nodes) {
+    std::vector<uint8_t> seen(g->n_nodes, 0);
+    for (uint32_t i = 0; i < n; ++i) {
+        if (nodes[i] >= g->n_nodes || seen[nodes[i]]) {
             rerr(err, SRT_ERR_INVALID, "in-use node list has an out-of-range or duplicate NodeIndex");
             return SRT_ERR_INVALID;
         }
+        seen[nodes[i]] = 1;
+    }
     const std::vector<uint32_t> ids = gml_ids(g, nodes, n);
     srt_routing_info *ri = nullptr;
     srt_status st = make_info(n, ids.data(), &ri, err);
