@@ -159,6 +159,9 @@ typedef struct {
                                    one saturated or is turned off) */
     uint64_t sparse_sweeps;     /* sparse: sweep launches of the last run, summed over its source
                                    launches (each covers every group in flight) */
+    uint32_t loss_fold;         /* dense: 1 = the level fold (tight edges walked by weight class
+                                   from the smaller latency level), 0 = the single-direction scan */
+    uint32_t reserved0;
 } srt_timing;
 srt_status srt_plan_timing(const srt_plan *plan, srt_timing *out);
 /* C tiles (128 x 128 keys) the last FW run's dominant launches loaded and

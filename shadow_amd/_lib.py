@@ -54,7 +54,7 @@ class SrtTiming(C.Structure):
     _fields_ = [("total_ms", C.c_double), ("dominant_ms", C.c_double), ("dominant_launches", C.c_uint64),
                 ("dominant_work", C.c_double), ("loss_ms", C.c_double), ("tight_edges", C.c_uint64),
                 ("sharded_tail", C.c_uint32), ("sparse_split", C.c_uint32),
-                ("sparse_sweeps", C.c_uint64)]
+                ("sparse_sweeps", C.c_uint64), ("loss_fold", C.c_uint32), ("reserved0", C.c_uint32)]
 
 
 class SrtRound(C.Structure):

@@ -485,6 +485,9 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_tpk);
     hipFree(p->d_tpk2);
     hipFree(p->d_tsort_tmp);
+    hipFree(p->d_tcls);
+    hipFree(p->d_tccnt);
+    hipFree(p->d_tscan_tmp);
     hipFree(p->d_tmaxw);
     hipFree(p->d_lscratch);
     hipFree(p->d_lrows);
@@ -1091,6 +1094,8 @@ srt_status srt_plan_timing(const srt_plan *p, srt_timing *o) {
     o->sharded_tail = p->algo == SRT_ALGO_FW && p->shard_tail ? 1u : 0u;
     o->sparse_split = p->algo == SRT_ALGO_SSSP && p->sssp_used_split ? 1u : 0u;
     o->sparse_sweeps = p->algo == SRT_ALGO_SSSP ? p->sssp_sweeps : 0;
+    o->loss_fold = p->algo == SRT_ALGO_FW && p->t_level ? 1u : 0u;
+    o->reserved0 = 0;
     return SRT_OK;
 }
 

@@ -205,6 +205,16 @@ struct srt_plan {
     bool loss_push = true;           // fold in push form over tight OUT-edges (knob SRT_LOSS_PUSH=0: pull)
     bool t_push = false;             // the last run's CSR is the push form (rows by source)
     uint64_t *h_tcount = nullptr;    // pinned: [0] total tight edges, [1] max tight latency
+    // level fold (srt_loss.hip level_loss_kernel): the tight edges grouped by
+    // (vertex, exact weight class w = 1..15) twice -- out-rows in d_tpk, in-rows
+    // in d_tpk2, entries (1-e) bits << 32 | other endpoint; class w of vertex x
+    // is [tcls[x*16 + w-1], tcls[x*16 + w]) (in-rows: offset V*16 + 1)
+    bool t_level = false;            // the last run built the class CSRs (and folds by levels)
+    uint32_t *d_tcls = nullptr;      // 2 * (V*16 + 1) class offsets
+    uint32_t *d_tccnt = nullptr;     // 2 * (V*16 + 1) class counts / fill cursors
+    uint64_t tcls_cap = 0;           // entries of d_tcls and d_tccnt
+    void *d_tscan_tmp = nullptr;     // rocPRIM scan scratch
+    size_t tscan_tmp_cap = 0;
     void *d_lscratch = nullptr;      // per workgroup: order array (+ rows if not in LDS)
     size_t lscratch_cap = 0;
     hipEvent_t ev_loss0 = nullptr, ev_loss1 = nullptr;  // around the loss pass

@@ -42,6 +42,7 @@
 #include <cstdlib>
 #include <cstring>
 
+#include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_segmented_radix_sort.hpp>
 
 #include "srt_internal.h"
@@ -685,6 +686,269 @@ __global__ __launch_bounds__(LOSS_NT) void tight_loss_kernel(
     }
 }
 
+// --------------------------------------------------------------- level fold
+// The pull form scans, for every target v of a row, its tight in-edges with
+// w < lat[s][v]; the push form scans, for every u, its tight out-edges up to
+// the row's largest latency.  Both walk ~10x more edges than end up tight for
+// the row (C3: ~1.9M edge tests a row for ~0.27M tight ones).  With the
+// vertices grouped by latency level (N_l = {v : lat[s][v] = l}, N_0 = {s})
+// the candidates of level l are exactly the edges u -> v, u in N_j, v in N_l,
+// of weight w = l - j, and for each weight class w that set can be walked
+// from either end: push from N_j along class-w out-edges, or pull into N_l
+// along class-w in-edges -- whichever level is smaller (a class's out- and
+// in-degrees are alike).  C3: ~0.26M edge tests a row.  Every candidate is
+// the same fold(loss[s][u], e) either way, min-ed into loss[s][v] by LDS
+// atomics, and level j < l is final before level l starts (one barrier per
+// level), so the result is the same bits as the single-direction scans.
+//
+// Class CSRs (built from the tight-edge list, no sort): out-rows and in-rows
+// grouped by exact weight w = 1..WC; tcls[x*CLS + w-1] .. tcls[x*CLS + w] is
+// class w of vertex x.  Applies when every tight edge has w <= WC, every
+// closure latency is < NBK units (proof bound lmax), V < 65536 (u16 member
+// lists) and the row fits LDS: lat u16 + loss f32 + members u16 (8 B/vertex).
+constexpr uint32_t WC = 15;   // exact weight classes
+constexpr uint32_t CLS = 16;  // offsets per vertex (classes 1..WC, then the end)
+
+__global__ void tcls_count_kernel(const uint4 *__restrict__ list, uint64_t slots, uint32_t *__restrict__ cnt,
+                                  uint64_t vc1) {
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < slots; e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 r = list[e];
+        if (r.x == ~0u) continue;
+        atomicAdd(&cnt[(uint64_t)r.y * CLS + r.z - 1], 1u);        // out-row of u
+        atomicAdd(&cnt[vc1 + (uint64_t)r.x * CLS + r.z - 1], 1u);  // in-row of v
+    }
+}
+
+__global__ void tcls_fill_kernel(const uint4 *__restrict__ list, uint64_t slots, const uint32_t *__restrict__ off,
+                                 uint32_t *__restrict__ cur, uint64_t *__restrict__ ce_out,
+                                 uint64_t *__restrict__ ce_in, uint64_t vc1) {
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < slots; e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 r = list[e];
+        if (r.x == ~0u) continue;
+        const uint64_t a = (uint64_t)r.y * CLS + r.z - 1, b = vc1 + (uint64_t)r.x * CLS + r.z - 1;
+        ce_out[off[a] + atomicAdd(&cur[a], 1u)] = ((uint64_t)r.w << 32) | r.x;
+        ce_in[off[b] + atomicAdd(&cur[b], 1u)] = ((uint64_t)r.w << 32) | r.y;
+    }
+}
+
+// One workgroup per table row, 16 waves.  LDS: hist (level ends), lat u16
+// (0xffff: unreachable), loss f32 bits, members u16 (the vertices in level
+// order, counting sort).  Output as tight_loss_kernel.
+template <int LPT, int UNR>
+__global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
+    const void *__restrict__ D, int key_type, uint32_t Vp, uint32_t V, const uint32_t *__restrict__ nodes, uint32_t n,
+    uint32_t row0, uint32_t row1, const uint32_t *__restrict__ tcls, uint64_t vc1,
+    const uint64_t *__restrict__ ce_out, const uint64_t *__restrict__ ce_in, uint64_t g,
+    const uint64_t *__restrict__ sl_lat, const float *__restrict__ sl_loss, uint64_t *__restrict__ out_lat,
+    float *__restrict__ out_loss, unsigned long long *stats, const uint32_t *__restrict__ row_list,
+    void *__restrict__ out32, float *__restrict__ out32_loss, bool stage16) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ uint64_t red[16];
+    __shared__ unsigned long long red_min[16], red_cnt[16];
+    __shared__ uint32_t plan_end[WC + 1];  // inclusive prefix of the class item counts
+    __shared__ uint32_t plan_push;         // bit w: class w pushes from N_{l-w}
+    uint32_t *hist = reinterpret_cast<uint32_t *>(smem);
+    uint16_t *lrow = reinterpret_cast<uint16_t *>(smem + HIST_BYTES);
+    const size_t lat_b = ((size_t)V * 2 + 15) & ~(size_t)15;
+    uint32_t *prow = reinterpret_cast<uint32_t *>(smem + HIST_BYTES + lat_b);
+    uint16_t *mem = reinterpret_cast<uint16_t *>(smem + HIST_BYTES + lat_b + (size_t)V * 4);
+    const uint16_t LINF = 0xffffu;
+    const uint32_t FINF = 0x7f800000u;  // +inf bits
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    const int lane = tid & 63, wv = tid >> 6, nw = nt >> 6;
+    const uint32_t grp = tid / LPT, sub = tid % LPT, ngrp = nt / LPT;
+    const uint32_t *cls_out = tcls, *cls_in = tcls + vc1;
+    uint64_t mn = ~0ull;
+    unsigned long long unreach = 0;
+    const uint32_t nrows = row_list ? row1 : row1 - row0;
+    for (uint32_t k = blockIdx.x; k < nrows; k += gridDim.x) {
+        const uint32_t i = row_list ? row_list[k] : row0 + k;
+        const uint32_t s = nodes[i];
+        // 1. the row's latencies (units of g, < NBK by the host's proof bound)
+        uint32_t mx = 0;
+        for (uint32_t v = tid; v < V; v += nt) {
+            bool inf;
+            const uint64_t l64 = closure_lat(D, (uint64_t)s * Vp + v, key_type, inf);
+            const uint16_t l = inf ? LINF : v == s ? (uint16_t)0 : (uint16_t)l64;
+            lrow[v] = l;
+            prow[v] = v == s ? 0u : FINF;  // petgraph's zero score (0 ns, 0.0) at s
+            if (l != LINF && l > mx) mx = l;
+        }
+        for (uint32_t b = tid; b <= (uint32_t)NBK; b += nt) hist[b] = 0;
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint32_t o = __shfl_xor(mx, off);
+            mx = o > mx ? o : mx;
+        }
+        if (lane == 0) red[wv] = mx;
+        __syncthreads();
+        mx = 0;
+        for (int q = 0; q < nw; ++q) mx = red[q] > mx ? (uint32_t)red[q] : mx;
+        const bool few = mx < 64;  // uniform: aggregate the LDS atomics per wave
+        // 2. counting sort of the reachable vertices (s at level 0) by level
+        for (uint32_t base = 0; base < V; base += nt) {
+            const uint32_t v = base + tid;
+            const uint16_t l = v < V ? lrow[v] : LINF;
+            const bool ok = l != LINF;
+            if (few) agg_inc(hist, ok ? l : 0u, ok);
+            else if (ok) atomicAdd(&hist[l], 1u);
+        }
+        __syncthreads();
+        {  // exclusive scan of hist[0, NBK): each thread a contiguous run
+            const uint32_t per = (NBK + nt - 1) / nt, b0 = std::min<uint32_t>(NBK, tid * per),
+                           b1 = std::min<uint32_t>(NBK, b0 + per);
+            uint32_t sum = 0;
+            for (uint32_t b = b0; b < b1; ++b) sum += hist[b];
+            uint32_t x = sum;
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(x, off);
+                if (lane >= off) x += y;
+            }
+            __syncthreads();  // everyone has read red (max) before it is rewritten
+            if (lane == 63) red[wv] = x;
+            __syncthreads();
+            uint32_t run = x - sum;
+            for (int q = 0; q < wv; ++q) run += (uint32_t)red[q];
+            for (uint32_t b = b0; b < b1; ++b) {
+                const uint32_t c = hist[b];
+                hist[b] = run;
+                run += c;
+            }
+        }
+        __syncthreads();
+        for (uint32_t base = 0; base < V; base += nt) {
+            const uint32_t v = base + tid;
+            const uint16_t l = v < V ? lrow[v] : LINF;
+            const bool ok = l != LINF;
+            uint32_t pos = 0;
+            if (few) pos = agg_inc(hist, ok ? l : 0u, ok);
+            else if (ok) pos = atomicAdd(&hist[l], 1u);
+            if (ok) mem[pos] = (uint16_t)v;
+        }
+        __syncthreads();
+        // hist[l] is now the end of level l (its start: hist[l-1], or 0)
+        // 3. levels in increasing latency, every weight class from its smaller end
+        for (uint32_t l = 1; l <= mx; ++l) {
+            const uint32_t lo = hist[l - 1], cnt_l = hist[l] - lo;
+            if (!cnt_l) continue;  // uniform
+            if (tid == 0) {
+                uint32_t run = 0, pm = 0;
+                for (uint32_t w = 1; w <= WC; ++w) {
+                    uint32_t items = 0;
+                    if (w <= l) {
+                        const uint32_t j = l - w, nj = hist[j] - (j ? hist[j - 1] : 0u);
+                        if (nj <= cnt_l) pm |= 1u << w;
+                        items = nj < cnt_l ? nj : cnt_l;
+                    }
+                    run += items;
+                    plan_end[w] = run;
+                }
+                plan_push = pm;
+            }
+            __syncthreads();
+            const uint32_t T = plan_end[WC], pm = plan_push;
+            for (uint32_t t = grp; t < T; t += ngrp) {
+                uint32_t w = 1;
+                while (t >= plan_end[w]) ++w;
+                const uint32_t m = t - (w > 1 ? plan_end[w - 1] : 0u), j = l - w;
+                const bool push = (pm >> w) & 1u;
+                const uint32_t x = mem[(push ? (j ? hist[j - 1] : 0u) : lo) + m];
+                const uint32_t *cl = push ? cls_out : cls_in;
+                const uint64_t *ce = push ? ce_out : ce_in;
+                const uint32_t e0 = cl[(uint64_t)x * CLS + w - 1], e1 = cl[(uint64_t)x * CLS + w];
+                // push: x in N_j, its class-w out-edges x -> v, v in N_l;
+                // pull: x in N_l, its class-w in-edges u -> x, u in N_j
+                const uint16_t want = (uint16_t)(push ? l : j);
+                const float onem = push ? 1.0f - __uint_as_float(prow[x]) : 0.0f;
+                for (uint32_t b = e0; b < e1; b += UNR * LPT) {
+                    uint64_t wd[UNR];
+#pragma unroll
+                    for (int q = 0; q < UNR; ++q) wd[q] = ce[b + sub + q * LPT];  // padded past the end
+                    uint32_t o[UNR];
+                    bool ok[UNR];
+#pragma unroll
+                    for (int q = 0; q < UNR; ++q) {
+                        ok[q] = b + sub + q * LPT < e1;
+                        o[q] = ok[q] ? (uint32_t)wd[q] : 0u;
+                    }
+                    uint16_t lo_[UNR];
+#pragma unroll
+                    for (int q = 0; q < UNR; ++q) lo_[q] = lrow[o[q]];
+#pragma unroll
+                    for (int q = 0; q < UNR; ++q) {
+                        if (ok[q] && lo_[q] == want) {
+                            const float r = __uint_as_float((uint32_t)(wd[q] >> 32));
+                            if (push) {
+                                const float c = 1.0f - __fmul_rn(onem, r);
+                                atomicMin(&prow[o[q]], __float_as_uint(c));
+                            } else {
+                                const float c = 1.0f - __fmul_rn(1.0f - __uint_as_float(prow[o[q]]), r);
+                                atomicMin(&prow[x], __float_as_uint(c));
+                            }
+                        }
+                    }
+                }
+            }
+            __syncthreads();  // level l final; plan_end rewritten by the next level
+        }
+        // 4. table row i (or staging slot k)
+        uint64_t *ol = out_lat + (uint64_t)i * n;
+        float *op = out_loss + (uint64_t)i * n;
+        uint32_t *o32 = out32 && !stage16 ? reinterpret_cast<uint32_t *>(out32) + (uint64_t)k * n : nullptr;
+        uint16_t *o16 = out32 && stage16 ? reinterpret_cast<uint16_t *>(out32) + (uint64_t)k * n : nullptr;
+        float *o32p = out32 ? out32_loss + (uint64_t)k * n : nullptr;
+        for (uint32_t j = tid; j < n; j += nt) {
+            uint64_t latv;
+            float lossv;
+            if (j == i) {
+                latv = sl_lat[j];
+                lossv = sl_loss[j];
+            } else {
+                const uint32_t v = nodes[j];
+                const uint16_t l = lrow[v];
+                if (l == LINF) {
+                    ++unreach;
+                    latv = ~0ull;
+                    lossv = 1.0f;
+                } else {
+                    latv = (uint64_t)l * g;
+                    lossv = __uint_as_float(prow[v]);
+                }
+            }
+            if (o16) {
+                o16[j] = latv == ~0ull ? (uint16_t)0xffffu : (uint16_t)(latv / g);
+                o32p[j] = lossv;
+            } else if (o32) {
+                o32[j] = latv == ~0ull ? ~0u : (uint32_t)(latv / g);
+                o32p[j] = lossv;
+            } else {
+                ol[j] = latv;
+                op[j] = lossv;
+            }
+            mn = latv < mn ? latv : mn;
+        }
+        __syncthreads();  // the next row rewrites the LDS rows
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(mn, off);
+        mn = o < mn ? o : mn;
+        unreach += __shfl_xor(unreach, off);
+    }
+    if (lane == 0) {
+        red_min[wv] = mn;
+        red_cnt[wv] = unreach;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long m = red_min[0], c = red_cnt[0];
+        for (int q = 1; q < nw; ++q) {
+            m = red_min[q] < m ? red_min[q] : m;
+            c += red_cnt[q];
+        }
+        atomicMin(&stats[0], m);
+        if (c) atomicAdd(&stats[1], c);
+    }
+}
+
 __global__ void loss_stats_init_kernel(unsigned long long *stats, unsigned long long *maxw) {
     stats[0] = ~0ull;
     stats[1] = 0ull;
@@ -872,6 +1136,89 @@ static srt_status ensure_tlist(srt_plan *p, uint64_t cap, uint64_t need, srt_err
     return SRT_OK;
 }
 
+// The level fold applies (see level_loss_kernel): every tight weight <= WC,
+// every closure latency < NBK units, u16 member lists, the row in LDS.
+bool level_ok(const srt_plan *p, uint64_t maxw) {
+    if (const char *e = std::getenv("SRT_LOSS_LEVEL"))  // A/B and parity tests of the scan folds
+        if (std::atoi(e) == 0) return false;
+    const size_t lds = HIST_BYTES + (((size_t)p->V * 2 + 15) & ~(size_t)15) + (size_t)p->V * 4 + (size_t)p->V * 2;
+    return p->kp.lat32 && maxw >= 1 && maxw <= WC && p->kp.lmax < (uint64_t)NBK && p->V < 65536 &&
+           lds + 16 <= LDS_BUDGET - 4096;
+}
+
+// Rows of the tight-edge list (slots records, v = ~0: padding, p->t_edges
+// real ones): the class CSRs when the level fold applies (no sort), else the
+// packed push (rows by source) or pull rows sorted by w.
+srt_status build_tight_rows(srt_plan *p, uint64_t slots, uint32_t ubits, uint64_t maxw, srt_err *err) {
+    hipStream_t M = p->stream;
+    const uint32_t V = p->V;
+    srt_status st;
+    const uint32_t lblocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, (slots + 255) / 256));
+    p->t_level = level_ok(p, maxw);
+    if (p->t_level) {
+        const uint64_t vc1 = (uint64_t)V * CLS + 1;
+        uint64_t c1 = p->tcls_cap, c2 = p->tcls_cap;
+        if ((st = grow(&p->d_tcls, &c1, 2 * vc1, err, "hipMalloc(class offsets)")) != SRT_OK ||
+            (st = grow(&p->d_tccnt, &c2, 2 * vc1, err, "hipMalloc(class counts)")) != SRT_OK)
+            return st;
+        p->tcls_cap = std::min(c1, c2);
+        (void)hipMemsetAsync(p->d_tccnt, 0, 2 * vc1 * 4, M);
+        hipLaunchKernelGGL(tcls_count_kernel, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tccnt, vc1);
+        size_t need = 0;
+        hipError_t e = rocprim::exclusive_scan(nullptr, need, p->d_tccnt, p->d_tcls, 0u, (size_t)vc1,
+                                               rocprim::plus<uint32_t>(), M);
+        if (e != hipSuccess) return fail(err, e, "class scan (size)");
+        uint64_t tcap = p->tscan_tmp_cap;
+        if ((st = grow(reinterpret_cast<uint8_t **>(&p->d_tscan_tmp), &tcap, need + 256, err,
+                       "hipMalloc(scan scratch)")) != SRT_OK)
+            return st;
+        p->tscan_tmp_cap = tcap;
+        for (int d = 0; d < 2; ++d) {
+            size_t have = p->tscan_tmp_cap;
+            e = rocprim::exclusive_scan(p->d_tscan_tmp, have, p->d_tccnt + d * vc1, p->d_tcls + d * vc1, 0u,
+                                        (size_t)vc1, rocprim::plus<uint32_t>(), M);
+            if (e != hipSuccess) return fail(err, e, "class scan");
+        }
+        (void)hipMemsetAsync(p->d_tccnt, 0, 2 * vc1 * 4, M);
+        hipLaunchKernelGGL(tcls_fill_kernel, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tcls,
+                           p->d_tccnt, p->d_tpk, p->d_tpk2, vc1);
+        p->t_push = false;
+        return SRT_OK;
+    }
+    (void)hipMemsetAsync(p->d_tcnt, 0, (size_t)V * 4, M);
+    if (p->loss_push)
+        hipLaunchKernelGGL(tight_list_count_kernel<true>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tcnt);
+    else
+        hipLaunchKernelGGL(tight_list_count_kernel<false>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tcnt);
+    hipLaunchKernelGGL(tight_scan_kernel, dim3(1), dim3(1024), 0, M, p->d_tcnt, p->d_tptr, V);
+    if (p->loss_push)
+        hipLaunchKernelGGL(tight_list_fill_kernel<true>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tptr,
+                           p->d_tcnt, p->d_tpk2, ubits);
+    else
+        hipLaunchKernelGGL(tight_list_fill_kernel<false>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tptr,
+                           p->d_tcnt, p->d_tpk2, ubits);
+    p->t_push = p->loss_push;
+    return sort_packed(p, ubits, maxw, err);
+}
+
+template <int LPT>
+srt_status launch_level(srt_plan *p, unsigned long long *d_stats, const RowJob &job) {
+    const uint32_t V = p->V, rows = job.list ? job.count : job.range ? job.r1 - job.r0 : p->row1 - p->row0;
+    if (!rows) return SRT_OK;
+    const size_t lds = HIST_BYTES + (((size_t)V * 2 + 15) & ~(size_t)15) + (size_t)V * 4 + (size_t)V * 2;
+    const uint32_t nt = V >= 2048 ? LOSS_NT : 256;
+    const int per_cu = std::max(1, std::min(2048 / (int)nt, (int)std::max<size_t>(1, (160 * 1024) / (lds + 2048))));
+    const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(rows, (uint32_t)(cu_count(p->device) * per_cu)));
+    auto kern = level_loss_kernel<LPT, 4>;
+    (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(LDS_BUDGET - 4096));
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, p->stream, (const void *)p->d_D, p->key_type, p->Vp, V,
+                       p->d_nodes, p->n, job.list ? 0u : job.range ? job.r0 : p->row0,
+                       job.list ? job.count : job.range ? job.r1 : p->row1, p->d_tcls, (uint64_t)V * CLS + 1,
+                       p->d_tpk, p->d_tpk2, p->kp.g, p->d_sl_lat, p->d_sl_loss, p->d_out_lat, p->d_out_loss, d_stats,
+                       job.list, job.out32, job.out32_loss, p->stage16);
+    return SRT_OK;
+}
+
 // Push-form tight CSR on one GPU: the flagged adjacency entries compacted
 // per source row (tight_list_kernel), then rows by source u, packed with v and
 // sorted by w.  *done = false: not packable, the caller builds the pull form.
@@ -905,14 +1252,7 @@ srt_status tight_csr_push_t(srt_plan *p, unsigned long long *d_stats, bool *done
     if ((st = ensure_tlist(p, C + C / 4 + 64, C, err)) != SRT_OK) return st;
     hipLaunchKernelGGL(tight_list_kernel, dim3(blocks), dim3(256), 0, M, 0u, V, p->d_row_ptr, p->d_col, p->d_lat,
                        p->d_loss, p->kp.g, p->d_tflag, p->d_tlist, p->d_tcursor);
-    const uint32_t lblocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, (total + 255) / 256));
-    (void)hipMemsetAsync(p->d_tcnt, 0, (size_t)V * 4, M);
-    hipLaunchKernelGGL(tight_list_count_kernel<true>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, total, p->d_tcnt);
-    hipLaunchKernelGGL(tight_scan_kernel, dim3(1), dim3(1024), 0, M, p->d_tcnt, p->d_tptr, V);
-    hipLaunchKernelGGL(tight_list_fill_kernel<true>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, total, p->d_tptr,
-                       p->d_tcnt, p->d_tpk2, ubits);
-    p->t_push = true;
-    if ((st = sort_packed(p, ubits, maxw, err)) != SRT_OK) return st;
+    if ((st = build_tight_rows(p, total, ubits, maxw, err)) != SRT_OK) return st;
     p->t_packed = true;
     *done = true;
     return SRT_OK;
@@ -935,6 +1275,7 @@ srt_status tight_csr_t(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
         if (e != hipSuccess) return fail(err, e, "hipHostMalloc");
     }
     p->t_push = false;
+    p->t_level = false;
     if (p->loss_push && V && !std::getenv("SRT_LOSS_UNPACKED")) {
         bool done = false;
         if ((st = tight_csr_push_t<K>(p, d_stats, &done, err)) != SRT_OK || done) return st;
@@ -982,6 +1323,14 @@ srt_status tight_csr_t(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
 
 srt_status fold(srt_plan *p, unsigned long long *d_stats, const RowJob &job, srt_err *err) {
     const uint32_t V = p->V;
+    if (p->t_level) {
+        // lanes per class walk (knob SRT_LOSS_LPT = 2 / 4 / 8 for A/B)
+        const char *k = std::getenv("SRT_LOSS_LPT");
+        const int lpt = k ? std::atoi(k) : 4;
+        if (lpt == 2) return launch_level<2>(p, d_stats, job);
+        if (lpt == 8) return launch_level<8>(p, d_stats, job);
+        return launch_level<4>(p, d_stats, job);
+    }
     const uint32_t ubits = (uint32_t)std::max(1, bits_of(V ? V - 1 : 0));
     const bool lds_rows = HIST_BYTES + (size_t)V * 8 + 16 <= LDS_BUDGET - 4096;
     if (p->kp.lat32) {
@@ -1054,22 +1403,7 @@ srt_status tight_csr_shard_t(srt_plan *p, unsigned long long *d_stats, bool *sha
     p->t_edges = total;
     p->t_packed = true;
     if ((st = ensure_edge_arrays(p, err)) != SRT_OK) return st;
-    const uint64_t slots = C * W;
-    const uint32_t lblocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, (slots + 255) / 256));
-    (void)hipMemsetAsync(p->d_tcnt, 0, (size_t)V * 4, M);
-    if (p->loss_push)
-        hipLaunchKernelGGL(tight_list_count_kernel<true>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tcnt);
-    else
-        hipLaunchKernelGGL(tight_list_count_kernel<false>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tcnt);
-    hipLaunchKernelGGL(tight_scan_kernel, dim3(1), dim3(1024), 0, M, p->d_tcnt, p->d_tptr, V);
-    if (p->loss_push)
-        hipLaunchKernelGGL(tight_list_fill_kernel<true>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tptr,
-                           p->d_tcnt, p->d_tpk2, ubits);
-    else
-        hipLaunchKernelGGL(tight_list_fill_kernel<false>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tptr,
-                           p->d_tcnt, p->d_tpk2, ubits);
-    p->t_push = p->loss_push;
-    if ((st = sort_packed(p, ubits, maxw, err)) != SRT_OK) return st;
+    if ((st = build_tight_rows(p, C * W, ubits, maxw, err)) != SRT_OK) return st;
     *sharded = true;
     return SRT_OK;
 }
@@ -1191,21 +1525,7 @@ srt_status loss_emulated_t(srt_plan *p, unsigned long long *d_stats, srt_err *er
     p->t_edges = total;
     p->t_packed = true;
     if ((st = ensure_edge_arrays(p, err)) != SRT_OK) return st;
-    const uint32_t lblocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, (slots + 255) / 256));
-    (void)hipMemsetAsync(p->d_tcnt, 0, (size_t)V * 4, M);
-    if (p->loss_push)
-        hipLaunchKernelGGL(tight_list_count_kernel<true>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tcnt);
-    else
-        hipLaunchKernelGGL(tight_list_count_kernel<false>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tcnt);
-    hipLaunchKernelGGL(tight_scan_kernel, dim3(1), dim3(1024), 0, M, p->d_tcnt, p->d_tptr, V);
-    if (p->loss_push)
-        hipLaunchKernelGGL(tight_list_fill_kernel<true>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tptr,
-                           p->d_tcnt, p->d_tpk2, ubits);
-    else
-        hipLaunchKernelGGL(tight_list_fill_kernel<false>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tptr,
-                           p->d_tcnt, p->d_tpk2, ubits);
-    p->t_push = p->loss_push;
-    if ((st = sort_packed(p, ubits, maxw, err)) != SRT_OK) return st;
+    if ((st = build_tight_rows(p, slots, ubits, maxw, err)) != SRT_OK) return st;
     const size_t chunk = (size_t)p->lrow_max * p->n;
     p->stage16 = p->key_type == KEY_U16;
     const size_t lb = p->stage16 ? 2 : 4;  // bytes per staged latency

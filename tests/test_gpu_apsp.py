@@ -327,3 +327,56 @@ def test_piece_upload_errors_in_reference_order(small_upload_pieces):
     with pytest.raises(_lib.SrtError) as e:
         g.compute_shortest_paths(np.arange(n, dtype=np.uint32))
     assert e.value.code == _lib.SRT_ERR_NO_EDGE and str(e.value) == "No edge connecting node 8 to 8"
+
+
+def _plan_table(g, nodes, algo=_lib.SRT_ALGO_FW):
+    from shadow_amd.plan import RoutingPlan
+    plan = RoutingPlan(g, nodes, algo=algo).run()
+    return plan, plan.fetch()
+
+
+@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("directed", [False, True])
+def test_level_fold_equals_scan_fold(monkeypatch, seed, directed):
+    """The level fold (tight edges grouped by exact weight class, each class
+    walked from the smaller of its two latency levels: push from N_{l-w} or
+    pull into N_l, srt_loss.hip level_loss_kernel) and the single-direction
+    push scan (SRT_LOSS_LEVEL=0) both give the oracle's bits, on tie-heavy
+    graphs (latencies 1..6 units) both directed and undirected; the plan
+    reports which fold ran."""
+    n = 100 + 29 * seed
+    src, dst, lat, loss = synth.random_graph(n, 300 + seed, p_edge=0.2, directed=directed, lat_range_ns=(1, 6),
+                                             loss_max=0.05)
+    nodes = np.random.default_rng(seed).permutation(n).astype(np.uint32)
+    elat, eloss = O.compute_shortest_paths(O.Graph(directed, np.arange(n), src, dst, lat, loss), nodes)
+    for level in (1, 0):
+        monkeypatch.setenv("SRT_LOSS_LEVEL", str(level))
+        g = NetworkGraph.from_edges(n, src, dst, lat, loss, directed=directed)
+        plan, t = _plan_table(g, nodes)
+        assert plan.timing()["loss_fold"] == level
+        assert np.array_equal(t.latency_ns, elat)
+        assert np.array_equal(t.packet_loss.view(np.uint32), eloss.view(np.uint32)), f"level={level}"
+
+
+@pytest.mark.parametrize("lat_hi,level", [(15, 1), (40, 0)])
+def test_level_fold_weight_class_limit(lat_hi, level):
+    """Tight edges heavier than the 15 exact weight classes send the build to
+    the scan fold; at the limit it stays on the level fold; bits as the oracle."""
+    n = 140
+    src, dst, lat, loss = synth.random_graph(n, 77, p_edge=0.08, directed=False, lat_range_ns=(1, lat_hi),
+                                             loss_max=0.05)
+    # make sure a tight edge of the top weight exists: a pendant vertex
+    src = np.append(src, np.uint32(n - 1)).astype(np.uint32)
+    dst = np.append(dst, np.uint32(0)).astype(np.uint32)
+    keep = ~(((src == n - 1) | (dst == n - 1)) & (src != dst))
+    keep[-1] = True
+    src, dst = src[keep], dst[keep]
+    lat = np.append(lat, np.uint64(lat_hi))[keep]
+    loss = np.append(loss, np.float32(0.01))[keep]
+    nodes = np.arange(n, dtype=np.uint32)
+    elat, eloss = O.compute_shortest_paths(O.Graph(False, np.arange(n), src, dst, lat, loss), nodes)
+    g = NetworkGraph.from_edges(n, src, dst, lat, loss, directed=False)
+    plan, t = _plan_table(g, nodes)
+    assert plan.timing()["loss_fold"] == level
+    assert np.array_equal(t.latency_ns, elat)
+    assert np.array_equal(t.packet_loss.view(np.uint32), eloss.view(np.uint32))

@@ -72,6 +72,7 @@ def test_c3_16k_rows_vs_oracle_and_symmetry():
     nodes = np.arange(n, dtype=np.uint32)
     plan = RoutingPlan(g, nodes).run()
     assert plan.describe().startswith("fw:f16key")  # complete graph: lmax = the longest edge (300 units < 1024)
+    assert plan.timing()["loss_fold"] == 1  # tight weights <= 15 units, latencies < 2048: the level fold
     plan.fetch(table=False)  # every pair reachable (else DISCONNECTED), min latency
     L, P = _device_table(plan)
     assert torch.equal(L, L.t()), "undirected latency table must be symmetric"
