@@ -1113,6 +1113,121 @@ __device__ __forceinline__ void relax_pairs_f16(uint32_t (&acc)[4], uint32_t a, 
         : "v"(a), "v"(b0.x), "v"(b0.y), "v"(b0.z), "v"(b0.w), "v"(b1.x), "v"(b1.y), "v"(b1.z), "v"(b1.w));
 }
 
+// Phase 1 for u16 / f16 keys, two FW steps per barrier.  Steps k and k+1
+// (k even) both follow from row/column k and row/column k+1 as they stood
+// before step k: with a = D[i][k], b = D[k][j], c = D[i][k+1], d = D[k+1][j],
+//     c' = min(c, a + D[k][k+1]),   d' = min(d, D[k+1][k] + b)
+// are the step-k values of column / row k+1, and two sequential steps give
+//     D[i][j] <- min(D[i][j], a + b, c' + d')
+// (for i = k+1 or j = k+1 the third term never wins: D'[k+1][k+1] >= 0).
+// So the owners publish rows k, k+1 and columns k, k+1 together, each thread
+// forms d' for its 4 column pairs and c' for its rows, and one barrier covers
+// two steps: 64 instead of 128 on the look-ahead chain.  F16: the three-way
+// min is one v_pk_minimum3_f16 per pair (relax_pairs_f16); u16: two
+// v_pk_min_u16.  Same layout as fw_phase1_u16pk_kernel (P1R even).
+template <int P1R, bool F16 = false>
+__global__ __launch_bounds__(16 * (B / P1R)) void fw_phase1_pk2_kernel(uint16_t *__restrict__ D, uint32_t Vp,
+                                                                      uint32_t kb) {
+    static_assert(P1R % 2 == 0, "rows k and k+1 must share a thread-row");
+    __shared__ us2 rowbuf[2][2][B / 2];   // [buffer][row k, row k+1][column pair]
+    __shared__ uint16_t colbuf[2][2][B];  // [buffer][column k, column k+1][row]
+    __builtin_amdgcn_s_setprio(3);        // critical path of the look-ahead chain
+    const int tid = threadIdx.x, tx = tid % 16, ty = tid / 16;
+    const uint64_t k0 = (uint64_t)kb * B;
+    us2 p[P1R][4];
+#pragma unroll
+    for (int i = 0; i < P1R; ++i) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(D + (k0 + ty * P1R + i) * Vp + k0 + tx * 8);
+        p[i][0] = __builtin_bit_cast(us2, v.x);
+        p[i][1] = __builtin_bit_cast(us2, v.y);
+        p[i][2] = __builtin_bit_cast(us2, v.z);
+        p[i][3] = __builtin_bit_cast(us2, v.w);
+    }
+    // double step k = 8g + 2e (e < 4): rows k, k+1 in thread-row k / P1R at
+    // elements k % P1R and +1; columns k, k+1 in thread-column g, pair e
+    auto publish = [&](int g, int e, int buf) {
+        const int k = 8 * g + 2 * e;
+        if (ty == k / P1R) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                rowbuf[buf][0][tx * 4 + q] = p[k % P1R][q];
+                rowbuf[buf][1][tx * 4 + q] = p[k % P1R + 1][q];
+            }
+        }
+        if (tx == g) {
+#pragma unroll
+            for (int i = 0; i < P1R; ++i) {
+                colbuf[buf][0][ty * P1R + i] = p[i][e][0];
+                colbuf[buf][1][ty * P1R + i] = p[i][e][1];
+            }
+        }
+    };
+    publish(0, 0, 0);
+    __syncthreads();
+#pragma unroll 1
+    for (int g = 0; g < B / 8; ++g) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int cur = e & 1;
+            const int k = 8 * g + 2 * e;
+            us2 b0[4], d1[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                b0[q] = rowbuf[cur][0][tx * 4 + q];
+                d1[q] = rowbuf[cur][1][tx * 4 + q];
+            }
+            const uint16_t s01 = rowbuf[cur][0][k / 2][1];  // D[k][k+1]
+            const uint16_t s10 = rowbuf[cur][1][k / 2][0];  // D[k+1][k]
+            const us2 s10p = {s10, s10};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) d1[q] = __builtin_elementwise_min(d1[q], add_keys2<F16>(s10p, b0[q]));
+#pragma unroll
+            for (int i = 0; i < P1R; ++i) {
+                const uint16_t a = colbuf[cur][0][ty * P1R + i], c = colbuf[cur][1][ty * P1R + i];
+                const us2 s01p = {s01, (uint16_t)0};
+                // (a, c') with c' = min(c, a + D[k][k+1]) (the low half of a + s01 is a + D[k][k+1])
+                const us2 sum = add_keys2<F16>(us2{a, a}, s01p);
+                const us2 acp = {a, c < sum[0] ? c : sum[0]};
+                if constexpr (F16) {
+                    uint32_t acc[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) acc[q] = __builtin_bit_cast(uint32_t, p[i][q]);
+                    u32x4 B0, B1;
+                    B0.x = __builtin_bit_cast(uint32_t, b0[0]);
+                    B0.y = __builtin_bit_cast(uint32_t, b0[1]);
+                    B0.z = __builtin_bit_cast(uint32_t, b0[2]);
+                    B0.w = __builtin_bit_cast(uint32_t, b0[3]);
+                    B1.x = __builtin_bit_cast(uint32_t, d1[0]);
+                    B1.y = __builtin_bit_cast(uint32_t, d1[1]);
+                    B1.z = __builtin_bit_cast(uint32_t, d1[2]);
+                    B1.w = __builtin_bit_cast(uint32_t, d1[3]);
+                    relax_pairs_f16(acc, __builtin_bit_cast(uint32_t, acp), B0, B1);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) p[i][q] = __builtin_bit_cast(us2, acc[q]);
+                } else {
+                    const us2 a2 = {acp[0], acp[0]}, c2 = {acp[1], acp[1]};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        p[i][q] = __builtin_elementwise_min(__builtin_elementwise_min(p[i][q], a2 + b0[q]),
+                                                            c2 + d1[q]);
+                }
+            }
+            if (e < 3) publish(g, e + 1, cur ^ 1);
+            else if (g + 1 < B / 8) publish(g + 1, 0, cur ^ 1);
+            __syncthreads();
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < P1R; ++i) {
+        uint4 v;
+        v.x = __builtin_bit_cast(uint32_t, p[i][0]);
+        v.y = __builtin_bit_cast(uint32_t, p[i][1]);
+        v.z = __builtin_bit_cast(uint32_t, p[i][2]);
+        v.w = __builtin_bit_cast(uint32_t, p[i][3]);
+        *reinterpret_cast<uint4 *>(D + (k0 + ty * P1R + i) * Vp + k0 + tx * 8) = v;
+    }
+}
+
 template <int s, bool F16>
 __device__ __forceinline__ void chunk_steps16(uint32_t (&acc)[8][4], StepOps16 (&o)[2], uint32_t abase,
                                               uint32_t bbase) {
@@ -1692,11 +1807,25 @@ template <int P1R>
 auto p1k(bool f16) {
     return f16 ? &fw_phase1_u16pk_kernel<P1R, true> : &fw_phase1_u16pk_kernel<P1R, false>;
 }
+template <int P1R>
+auto p1k2(bool f16) {
+    return f16 ? &fw_phase1_pk2_kernel<P1R, true> : &fw_phase1_pk2_kernel<P1R, false>;
+}
 
+// two: u16 / f16 keys, two FW steps per barrier (fw_phase1_pk2_kernel)
 template <typename K>
-void launch_p1(int rows, hipStream_t s, K *D, uint32_t Vp, uint32_t kb, bool f16 = false) {
+void launch_p1(int rows, hipStream_t s, K *D, uint32_t Vp, uint32_t kb, bool f16 = false, bool two = false) {
     if constexpr (sizeof(K) == 2) {
         uint16_t *D16 = reinterpret_cast<uint16_t *>(D);
+        if (two) {
+            if (rows == 2)
+                hipLaunchKernelGGL(p1k2<2>(f16), dim3(1), dim3(16 * (B / 2)), 0, s, D16, Vp, kb);
+            else if (rows == 4)
+                hipLaunchKernelGGL(p1k2<4>(f16), dim3(1), dim3(16 * (B / 4)), 0, s, D16, Vp, kb);
+            else
+                hipLaunchKernelGGL(p1k2<8>(f16), dim3(1), dim3(16 * (B / 8)), 0, s, D16, Vp, kb);
+            return;
+        }
         if (rows == 2)
             hipLaunchKernelGGL(p1k<2>(f16), dim3(1), dim3(16 * (B / 2)), 0, s, D16, Vp, kb);
         else if (rows == 4)
@@ -1910,7 +2039,7 @@ srt_status fw_rounds_sym_sharded(srt_plan *p, int p1r, srt_err *err) {
             launch_mirror<uint16_t, 1>(p, s, k, row);
     };
     // prologue: pivot 0 on every rank (the same full initial D)
-    launch_p1<uint16_t>(p1r, M, D, p->Vp, 0u, p->fw_f16);
+    launch_p1<uint16_t>(p1r, M, D, p->Vp, 0u, p->fw_f16, p->fw_p1_two);
     p2row_mirror(M, 0);
     hipEventRecord(p->ev_cross, M);
     hipEvent_t rest_done = p->ev_cross;
@@ -1947,7 +2076,7 @@ srt_status fw_rounds_sym_sharded(srt_plan *p, int p1r, srt_err *err) {
         hipLaunchKernelGGL(unpack_row16_kernel, dim3(nblk), dim3(256), 0, S,
                            emu ? p->d_fbuf : D + (uint64_t)k1 * B * p->Vp, p->Vp, k1, N, S_t,
                            (const uint16_t *)p->d_rowslots);
-        launch_p1<uint16_t>(p1r, S, D, p->Vp, k1, p->fw_f16);
+        launch_p1<uint16_t>(p1r, S, D, p->Vp, k1, p->fw_f16, p->fw_p1_two);
         p2row_mirror(S, k1);
         hipEventRecord(p->ev_pivot, S);
     }
@@ -2050,7 +2179,7 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
     srt_status st = SRT_OK;
     // prologue: pivot 0
     if (own(0)) {
-        launch_p1<K>(p1r, M, D, p->Vp, 0u, p->fw_f16);
+        launch_p1<K>(p1r, M, D, p->Vp, 0u, p->fw_f16, p->fw_p1_two);
         launch_tiles<K, 1>(p, M, 0, Rect{make_span(0, 1), make_span(0, nblk, 0)}, none);
     }
     if (sharded && (st = comm_bcast(p->comm, D, pivot_bytes, 0, M, err)) != SRT_OK) return st;
@@ -2103,7 +2232,7 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
             Rect row = own(k1) ? Rect{make_span(k1, k1 + 1), make_span(0, nblk, kb)} : none;
             launch_tiles<K, 4>(p, S, kb, col, row);
             if (own(k1)) {
-                launch_p1<K>(p1r, S, D, p->Vp, k1, p->fw_f16);
+                launch_p1<K>(p1r, S, D, p->Vp, k1, p->fw_f16, p->fw_p1_two);
                 launch_tiles<K, 1>(p, S, k1, Rect{make_span(k1, k1 + 1), make_span(0, nblk, k1)}, none);
             }
             // pivot-row broadcast on the comm stream C: the owner's chain goes
@@ -2210,7 +2339,7 @@ srt_status fw_rounds_group_t(srt_plan *p, int p1r, uint32_t g) {
     const bool symc = p->fw_sym && sizeof(K) == 2 && !p->fw_small_chain;
     auto pivots = [&](hipStream_t s, uint32_t a) {
         for (uint32_t r = a; r < a + g; ++r) {
-            launch_p1<K>(p1r, s, D, p->Vp, r, p->fw_f16);
+            launch_p1<K>(p1r, s, D, p->Vp, r, p->fw_f16, p->fw_p1_two);
             if (symc) {
                 launch_mirror<K, 1>(p, s, r, Rect{make_span(r, r + 1), make_span(0, nblk, r)});
                 if (r + 1 < a + g)
@@ -2355,7 +2484,7 @@ srt_status fw_rounds_group_sharded_t(srt_plan *p, int p1r, uint32_t g, uint32_t 
         const bool o = own(a);
         for (uint32_t r = a; r < a + g; ++r) {
             if (o) {
-                launch_p1<K>(p1r, s, D, p->Vp, r, p->fw_f16);
+                launch_p1<K>(p1r, s, D, p->Vp, r, p->fw_f16, p->fw_p1_two);
                 launch_tiles<K, 1>(p, s, r, Rect{make_span(r, r + 1), make_span(0, nblk, r)}, none);
             }
             if (sharded || emu_bcast_ticks) {

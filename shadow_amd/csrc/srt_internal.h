@@ -78,6 +78,7 @@ struct srt_plan {
     int key_type = srt::KEY_F64;  // closure keys: u32 / f64 (exact integers < 2^53) / u64
     bool fw_glds = true;   // FW tiles staged by LDS-DMA (false: register staging)
     bool fw_f16 = false;   // u16-stored keys relaxed as f16 integers (every finite distance < 1024 units)
+    bool fw_p1_two = true; // u16/f16 phase 1 at two FW steps per barrier (knob SRT_FW_P1_TWO=0: one)
     bool fw_small_chain = false;  // quarter-tile kernels for the look-ahead chain (sharded)
     bool fw_unique_edges = false; // no parallel edges: FW init stores instead of atomic min
     bool fw_sym = false;          // D symmetric (fw_sym_check): rest launches run the triangle

@@ -741,7 +741,7 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
     const uint64_t *__restrict__ ce_out, const uint64_t *__restrict__ ce_in, uint64_t g,
     const uint64_t *__restrict__ sl_lat, const float *__restrict__ sl_loss, uint64_t *__restrict__ out_lat,
     float *__restrict__ out_loss, unsigned long long *stats, const uint32_t *__restrict__ row_list,
-    void *__restrict__ out32, float *__restrict__ out32_loss, bool stage16) {
+    void *__restrict__ out32, float *__restrict__ out32_loss, bool stage16, uint32_t diag) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ uint64_t red[16];
     __shared__ unsigned long long red_min[16], red_cnt[16];
@@ -827,7 +827,9 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
         __syncthreads();
         // hist[l] is now the end of level l (its start: hist[l-1], or 0)
         // 3. levels in increasing latency, every weight class from its smaller end
-        for (uint32_t l = 1; l <= mx; ++l) {
+        // (diag, timing-only knob SRT_LOSS_DIAG, wrong tables: bit 0 skips the
+        // level walks, bit 1 the row output)
+        for (uint32_t l = 1; l <= ((diag & 1u) ? 0u : mx); ++l) {
             const uint32_t lo = hist[l - 1], cnt_l = hist[l] - lo;
             if (!cnt_l) continue;  // uniform
             if (tid == 0) {
@@ -896,7 +898,7 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
         uint32_t *o32 = out32 && !stage16 ? reinterpret_cast<uint32_t *>(out32) + (uint64_t)k * n : nullptr;
         uint16_t *o16 = out32 && stage16 ? reinterpret_cast<uint16_t *>(out32) + (uint64_t)k * n : nullptr;
         float *o32p = out32 ? out32_loss + (uint64_t)k * n : nullptr;
-        for (uint32_t j = tid; j < n; j += nt) {
+        for (uint32_t j = tid; j < ((diag & 2u) ? 0u : n); j += nt) {
             uint64_t latv;
             float lossv;
             if (j == i) {
@@ -1215,7 +1217,8 @@ srt_status launch_level(srt_plan *p, unsigned long long *d_stats, const RowJob &
                        p->d_nodes, p->n, job.list ? 0u : job.range ? job.r0 : p->row0,
                        job.list ? job.count : job.range ? job.r1 : p->row1, p->d_tcls, (uint64_t)V * CLS + 1,
                        p->d_tpk, p->d_tpk2, p->kp.g, p->d_sl_lat, p->d_sl_loss, p->d_out_lat, p->d_out_loss, d_stats,
-                       job.list, job.out32, job.out32_loss, p->stage16);
+                       job.list, job.out32, job.out32_loss, p->stage16,
+                       std::getenv("SRT_LOSS_DIAG") ? (uint32_t)std::atoi(std::getenv("SRT_LOSS_DIAG")) : 0u);
     return SRT_OK;
 }
 

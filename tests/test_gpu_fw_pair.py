@@ -274,3 +274,33 @@ def test_eccentricity_proof_needs_strong_connectivity():
         assert plan.describe().startswith("fw:u16key") and "(V-1)" in plan.describe(), plan.describe()
     finally:
         plan.close()
+
+
+@pytest.mark.parametrize("key", ["f16", "u16"])
+@pytest.mark.parametrize("rows", ["2", "4", "8"])
+def test_phase1_two_steps_per_barrier(monkeypatch, key, rows):
+    """Phase 1 at two FW steps per barrier (fw_phase1_pk2_kernel: rows and
+    columns k, k+1 published together, column/row k+1 advanced by step k in
+    registers) gives the one-step kernel's bits and the oracle's, for f16 and
+    u16 keys and every rows-per-thread layout."""
+    monkeypatch.setenv("SRT_FW_P1_ROWS", rows)
+    if key == "u16":
+        monkeypatch.setenv("SRT_FW_KEY", "u16")
+    n = 700
+    src, dst, lat, loss = synth.complete_graph(n, 40 + int(rows))
+    g = NetworkGraph.from_edges(n, src, dst, lat, loss)
+    nodes = np.arange(n, dtype=np.uint32)
+    tabs = {}
+    for two in ("1", "0"):
+        monkeypatch.setenv("SRT_FW_P1_TWO", two)
+        plan = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_FW)
+        try:
+            assert plan.describe().startswith(f"fw:{key}key"), plan.describe()
+            tabs[two] = plan.run().fetch()
+        finally:
+            plan.close()
+    from oracle import oracle as O
+    elat, eloss = O.compute_shortest_paths(O.Graph(False, nodes, src, dst, lat, loss), nodes)
+    for two, t in tabs.items():
+        assert np.array_equal(t.latency_ns, elat), two
+        assert np.array_equal(t.packet_loss.view(np.uint32), eloss.view(np.uint32)), two

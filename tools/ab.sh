@@ -22,6 +22,6 @@ for rep in 1 2; do
   for knobs in "$@"; do
     i=$((i + 1))
     env $knobs timeout -k 10 400 python -u bench.py $BARGS --no-cpu-baseline > $O/run${i}_$rep.json 2> $O/run${i}_$rep.err || { tail -5 $O/run${i}_$rep.err; exit 1; }
-    python -c "import json; d=json.loads(open('$O/run${i}_$rep.json').read().strip().splitlines()[-1]); print('[$knobs]', round(d['ms_per_step'],2), d['config'].get('plan',''))"
+    python -c "import json; d=json.loads(open('$O/run${i}_$rep.json').read().strip().splitlines()[-1]); cf=d['config'] if isinstance(d.get('config'),dict) else {}; ph=cf.get('phases_last_build') or {}; print('[$knobs]', round(d['ms_per_step'],2), 'loss', round(ph.get('exact_loss_pass_ms',d.get('tail_ms_last',0)),2), 'rest', round(ph.get('dominant_ms',d.get('rest_ms_per_step',0)),2), cf.get('plan','')[:60])"
   done
 done
