@@ -1125,19 +1125,21 @@ __device__ __forceinline__ void relax_pairs_f16(uint32_t (&acc)[4], uint32_t a, 
 // two steps: 64 instead of 128 on the look-ahead chain.  F16: the three-way
 // min is one v_pk_minimum3_f16 per pair (relax_pairs_f16); u16: two
 // v_pk_min_u16.  Same layout as fw_phase1_u16pk_kernel (P1R even).
-template <int P1R, bool F16 = false>
-__global__ __launch_bounds__(16 * (B / P1R)) void fw_phase1_pk2_kernel(uint16_t *__restrict__ D, uint32_t Vp,
-                                                                      uint32_t kb) {
+// The body reads the pivot block from src (row stride ss) and writes the
+// closure to dst (row stride ds): D's diagonal block, or (unpack_p1_kernel)
+// the block as the row all-gather delivered it.
+template <int P1R, bool F16>
+__device__ __forceinline__ void phase1_pk2_body(const uint16_t *__restrict__ src, uint64_t ss,
+                                                uint16_t *__restrict__ dst, uint64_t ds) {
     static_assert(P1R % 2 == 0, "rows k and k+1 must share a thread-row");
     __shared__ us2 rowbuf[2][2][B / 2];   // [buffer][row k, row k+1][column pair]
     __shared__ uint16_t colbuf[2][2][B];  // [buffer][column k, column k+1][row]
     __builtin_amdgcn_s_setprio(3);        // critical path of the look-ahead chain
     const int tid = threadIdx.x, tx = tid % 16, ty = tid / 16;
-    const uint64_t k0 = (uint64_t)kb * B;
     us2 p[P1R][4];
 #pragma unroll
     for (int i = 0; i < P1R; ++i) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(D + (k0 + ty * P1R + i) * Vp + k0 + tx * 8);
+        const uint4 v = *reinterpret_cast<const uint4 *>(src + (ty * P1R + i) * ss + tx * 8);
         p[i][0] = __builtin_bit_cast(us2, v.x);
         p[i][1] = __builtin_bit_cast(us2, v.y);
         p[i][2] = __builtin_bit_cast(us2, v.z);
@@ -1224,7 +1226,39 @@ __global__ __launch_bounds__(16 * (B / P1R)) void fw_phase1_pk2_kernel(uint16_t 
         v.y = __builtin_bit_cast(uint32_t, p[i][1]);
         v.z = __builtin_bit_cast(uint32_t, p[i][2]);
         v.w = __builtin_bit_cast(uint32_t, p[i][3]);
-        *reinterpret_cast<uint4 *>(D + (k0 + ty * P1R + i) * Vp + k0 + tx * 8) = v;
+        *reinterpret_cast<uint4 *>(dst + (ty * P1R + i) * ds + tx * 8) = v;
+    }
+}
+
+template <int P1R, bool F16 = false>
+__global__ __launch_bounds__(16 * (B / P1R)) void fw_phase1_pk2_kernel(uint16_t *__restrict__ D, uint32_t Vp,
+                                                                      uint32_t kb) {
+    uint16_t *blk = D + (uint64_t)kb * B * Vp + (uint64_t)kb * B;
+    phase1_pk2_body<P1R, F16>(blk, Vp, blk, Vp);
+}
+
+// The symmetric sharded chain after the row all-gather, one launch: block 0
+// closes pivot block (k, k) straight from its slot (emu: from D) into D;
+// block 1 + c copies tile (k, c) of row k from rank (k + c) mod N's slot into
+// row (D's block-row k, or the emulation's scratch), except the pivot block.
+template <int P1R, bool F16>
+__global__ __launch_bounds__(16 * (B / P1R)) void unpack_p1_kernel(uint16_t *__restrict__ D, uint32_t Vp, uint32_t k,
+                                                                  uint32_t N, uint32_t S,
+                                                                  const uint16_t *__restrict__ slots,
+                                                                  uint16_t *__restrict__ row, bool emu) {
+    const uint64_t diag = (uint64_t)k * B * Vp + (uint64_t)k * B;
+    if (blockIdx.x == 0) {
+        const uint16_t *src = emu ? D + diag : slots + ((uint64_t)((2 * k) % N) * S + k / N) * B * B;
+        phase1_pk2_body<P1R, F16>(src, emu ? Vp : B, D + diag, Vp);
+        return;
+    }
+    const uint32_t c = blockIdx.x - 1;
+    if (c == k && !emu) return;
+    const uint16_t *src = slots + ((uint64_t)((k + c) % N) * S + c / N) * B * B;
+    uint16_t *dst = row + (uint64_t)c * B;
+    for (uint32_t e = threadIdx.x; e < B * B / 8; e += blockDim.x) {
+        const uint32_t r = e / (B / 8), cc = (e % (B / 8)) * 8;
+        *reinterpret_cast<u32x4 *>(dst + (uint64_t)r * Vp + cc) = *reinterpret_cast<const u32x4 *>(src + r * B + cc);
     }
 }
 
@@ -1617,10 +1651,14 @@ __global__ __launch_bounds__(256) void minplus_small_kernel(K *__restrict__ D, u
 // rows or columns r1.r.x0 / r1.r.x1 skipped), mirrored; MODE 1: the rect r1,
 // mirrored; MODE 0: the rects r1 then r2, not mirrored (the look-ahead chain
 // of one GPU at chain-bound sizes and of the row-sharded schedule).  F16: f16
-// integer keys (see relax_pairs_f16).
+// integer keys (see relax_pairs_f16).  slot (MODE 2, the symmetric sharded
+// cross): every result tile in row or column prow also goes, in row-prow
+// orientation, to this rank's all-gather slot -- tile (prow, c) at slot index
+// c / N (the pack of fw_rounds_sym_sharded, fused).
 template <int TAG, int MODE, bool F16>
 __global__ __launch_bounds__(256) void minplus_q16_kernel(uint16_t *__restrict__ D, uint32_t Vp, uint32_t kb, Rect r1,
-                                                          Rect r2) {
+                                                          Rect r2, uint16_t *__restrict__ slot, uint32_t prow,
+                                                          uint32_t N) {
     constexpr int QK = 32;
     __shared__ uint16_t As[2][SQ][QK + 2];  // [row][k]
     __shared__ us2 Bs[2][QK][SQ / 2];        // [k][column pair]
@@ -1633,7 +1671,37 @@ __global__ __launch_bounds__(256) void minplus_q16_kernel(uint16_t *__restrict__
         const uint32_t e = tl[t];
         bi = e >> 16;
         bj = e & 0xffffu;
-        if (bi == r1.r.x0 || bj == r1.r.x0 || bi == r1.r.x1 || bj == r1.r.x1) return;
+        if (bi == r1.r.x0 || bj == r1.r.x0 || bi == r1.r.x1 || bj == r1.r.x1) {
+            // a skipped tile of row / column prow is current already: into the slot as it is
+            if (slot && (bi == prow || bj == prow)) {
+                const uint64_t si0 = (uint64_t)bi * B + (q >> 1) * SQ, sj0 = (uint64_t)bj * B + (q & 1) * SQ;
+                const int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
+                if (bi == prow) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        *reinterpret_cast<uint2 *>(slot + (uint64_t)(bj / N) * B * B +
+                                                   ((q >> 1) * SQ + ty * 4 + i) * B + (q & 1) * SQ + tx * 4) =
+                            *reinterpret_cast<const uint2 *>(D + (si0 + ty * 4 + i) * Vp + sj0 + tx * 4);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int c = 0; c < 4; ++c)
+                            T[tx * 4 + c][ty * 4 + i] = D[(si0 + ty * 4 + i) * Vp + sj0 + tx * 4 + c];
+                    __syncthreads();
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int r = ty * 4 + i;
+                        uint2 v;
+                        v.x = (uint32_t)T[r][tx * 4] | ((uint32_t)T[r][tx * 4 + 1] << 16);
+                        v.y = (uint32_t)T[r][tx * 4 + 2] | ((uint32_t)T[r][tx * 4 + 3] << 16);
+                        *reinterpret_cast<uint2 *>(slot + (uint64_t)(bi / N) * B * B + ((q & 1) * SQ + r) * B +
+                                                   (q >> 1) * SQ + tx * 4) = v;
+                    }
+                }
+            }
+            return;
+        }
     } else {
         const uint32_t n1 = r1.r.n * r1.c.n;
         if (MODE == 1 || t < n1) {
@@ -1700,6 +1768,10 @@ __global__ __launch_bounds__(256) void minplus_q16_kernel(uint16_t *__restrict__
         v.x = __builtin_bit_cast(uint32_t, acc[i][0]);
         v.y = __builtin_bit_cast(uint32_t, acc[i][1]);
         *reinterpret_cast<uint2 *>(D + (i0 + ty * 4 + i) * Vp + j0 + tx * 4) = v;
+        // the slot takes the quarter as computed when it is row prow's
+        if (MODE == 2 && slot && bi == prow)
+            *reinterpret_cast<uint2 *>(slot + (uint64_t)(bj / N) * B * B + ((q >> 1) * SQ + ty * 4 + i) * B +
+                                       (q & 1) * SQ + tx * 4) = v;
     }
     if (MODE != 0 && bi != bj) {
 #pragma unroll
@@ -1714,6 +1786,10 @@ __global__ __launch_bounds__(256) void minplus_q16_kernel(uint16_t *__restrict__
             v.x = (uint32_t)T[r][tx * 4] | ((uint32_t)T[r][tx * 4 + 1] << 16);
             v.y = (uint32_t)T[r][tx * 4 + 2] | ((uint32_t)T[r][tx * 4 + 3] << 16);
             *reinterpret_cast<uint2 *>(D + (j0 + r) * Vp + i0 + tx * 4) = v;
+            // ... or transposed, when it is column prow's (tile (bi, prow) = mirror (prow, bi))
+            if (MODE == 2 && slot && bj == prow)
+                *reinterpret_cast<uint2 *>(slot + (uint64_t)(bi / N) * B * B + ((q & 1) * SQ + r) * B +
+                                           (q >> 1) * SQ + tx * 4) = v;
         }
     }
 }
@@ -1849,7 +1925,7 @@ void launch_tiles(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1, const
     if (TAG != 0 && p->fw_small_chain) {  // look-ahead chain: quarter tiles, lower latency
         if constexpr (sizeof(K) == 2)
             hipLaunchKernelGGL((q16k<TAG, 0>(p->fw_f16)), dim3(4 * n), dim3(256), 0, s,
-                               reinterpret_cast<uint16_t *>(p->d_D), p->Vp, kb, r1, r2);
+                               reinterpret_cast<uint16_t *>(p->d_D), p->Vp, kb, r1, r2, (uint16_t *)nullptr, 0u, 1u);
         else
             hipLaunchKernelGGL((minplus_small_kernel<K, TAG>), dim3(4 * n), dim3(256), 0, s,
                                reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2);
@@ -2030,11 +2106,19 @@ srt_status fw_rounds_sym_sharded(srt_plan *p, int p1r, srt_err *err) {
     // the round's critical path; knob SRT_FW_SYM_SMALL=0/1 for A/B
     bool small = p->tl_own < 4096;
     if (const char *e = std::getenv("SRT_FW_SYM_SMALL")) small = std::atoi(e) != 0;
+    // the quarter-tile cross also packs row k1 into the slot (knob
+    // SRT_FW_FUSE_PACK=0: the separate pack kernel, for A/B)
+    bool fuse_pack = true;
+    if (const char *e = std::getenv("SRT_FW_FUSE_PACK")) fuse_pack = std::atoi(e) != 0;
+    // ... and the unpack of row k1 runs beside p1(k1) in one launch (two-step
+    // phase 1; knob SRT_FW_FUSE_P1=0: separate launches)
+    bool fuse_p1 = p->fw_p1_two;
+    if (const char *e = std::getenv("SRT_FW_FUSE_P1")) fuse_p1 = fuse_p1 && std::atoi(e) != 0;
     auto p2row_mirror = [&](hipStream_t s, uint32_t k) {
         const Rect row{make_span(k, k + 1), make_span(0, nblk, k)};
         if (small)
             hipLaunchKernelGGL((q16k<1, 1>(p->fw_f16)), dim3(4 * row.c.n), dim3(256), 0, s, D, p->Vp, k, row,
-                               Rect{make_span(0, 0), make_span(0, 0)});
+                               Rect{make_span(0, 0), make_span(0, 0)}, (uint16_t *)nullptr, 0u, 1u);
         else
             launch_mirror<uint16_t, 1>(p, s, k, row);
     };
@@ -2062,21 +2146,33 @@ srt_status fw_rounds_sym_sharded(srt_plan *p, int p1r, srt_err *err) {
             Span skip{0, 0, kb, NONE, 0};
             const uint64_t addr = reinterpret_cast<uint64_t>(cl);
             Span ptr{(uint32_t)addr, (uint32_t)(addr >> 32), NONE, NONE, 0};
+            // cross(kb) and the pack of row k1 into this rank's slot, one launch
             hipLaunchKernelGGL((q16k<4, 2>(p->fw_f16)), dim3(4 * cn), dim3(256), 0, S, D, p->Vp, kb,
-                               Rect{skip, skip}, Rect{ptr, ptr});
+                               Rect{skip, skip}, Rect{ptr, ptr}, fuse_pack ? myslot : (uint16_t *)nullptr, k1, N);
+            if (!fuse_pack)
+                hipLaunchKernelGGL(pack_row16_kernel, dim3(cn), dim3(256), 0, S, D, p->Vp, cl, k1, N, myslot);
         } else {
             launch_list16(S, D, p->Vp, kb, cl, cn, kb, NONE, p->fw_f16);
+            if (cn) hipLaunchKernelGGL(pack_row16_kernel, dim3(cn), dim3(256), 0, S, D, p->Vp, cl, k1, N, myslot);
         }
-        if (cn) hipLaunchKernelGGL(pack_row16_kernel, dim3(cn), dim3(256), 0, S, D, p->Vp, cl, k1, N, myslot);
         // the row all-gather on S itself: nothing else waits on S meanwhile,
         // and two cross-stream event hops (~13 us each) fewer per round
         if ((st = gather(p->d_rowslots, (size_t)S_t * B * B * 2, S)) != SRT_OK) return st;
         // emulation: the other slots hold no real rows, so the unpack (same
         // volume) goes to scratch and the closed D stays as it is
-        hipLaunchKernelGGL(unpack_row16_kernel, dim3(nblk), dim3(256), 0, S,
-                           emu ? p->d_fbuf : D + (uint64_t)k1 * B * p->Vp, p->Vp, k1, N, S_t,
-                           (const uint16_t *)p->d_rowslots);
-        launch_p1<uint16_t>(p1r, S, D, p->Vp, k1, p->fw_f16, p->fw_p1_two);
+        uint16_t *rowdst = emu ? p->d_fbuf : D + (uint64_t)k1 * B * p->Vp;
+        if (fuse_p1 && (p1r == 2 || p1r == 4 || p1r == 8)) {
+            // unpack of row k1 and p1(k1) from its slot, one launch
+            auto kern = p1r == 2 ? (p->fw_f16 ? &unpack_p1_kernel<2, true> : &unpack_p1_kernel<2, false>)
+                        : p1r == 4 ? (p->fw_f16 ? &unpack_p1_kernel<4, true> : &unpack_p1_kernel<4, false>)
+                                   : (p->fw_f16 ? &unpack_p1_kernel<8, true> : &unpack_p1_kernel<8, false>);
+            hipLaunchKernelGGL(kern, dim3(nblk + 1), dim3(16 * (B / p1r)), 0, S, D, p->Vp, k1, N, S_t,
+                               (const uint16_t *)p->d_rowslots, rowdst, emu);
+        } else {
+            hipLaunchKernelGGL(unpack_row16_kernel, dim3(nblk), dim3(256), 0, S, rowdst, p->Vp, k1, N, S_t,
+                               (const uint16_t *)p->d_rowslots);
+            launch_p1<uint16_t>(p1r, S, D, p->Vp, k1, p->fw_f16, p->fw_p1_two);
+        }
         p2row_mirror(S, k1);
         hipEventRecord(p->ev_pivot, S);
     }
@@ -2160,7 +2256,10 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
         return fw_rounds_group_t<K>(p, p1r, grp);
     // symmetric D on several ranks: the triangle dealt by (i + j) mod N
     if constexpr (sizeof(K) == 2)
-        if ((sharded || emu) && p->fw_sym && p->fw_glds) return fw_rounds_sym_sharded(p, p1r, err);
+        if ((sharded || emu) && p->fw_sym && p->fw_glds) {
+            p->fw_full_d = true;  // the final tile exchange leaves the whole closure on every rank
+            return fw_rounds_sym_sharded(p, p1r, err);
+        }
     // sharded: groups of 2 when a rank holds >= 32 block-rows (rest-bound)
     // that split into whole groups (one owner per group) and there are >= 2
     // groups.  Emulated C3 (16k, u16 keys), g = 1 / 2 / 4: 2 ranks 82.7 / 80.6
@@ -2713,6 +2812,7 @@ srt_status fw_gather_keys(srt_plan *p, srt_err *err) {
 }
 
 srt_status fw_rounds(srt_plan *p, srt_err *err) {
+    p->fw_full_d = false;
     if (p->key_type == KEY_U16) {
         // f16 plans: D to f16 keys and back around the closure, on the main
         // stream (every schedule's last kernel runs there, or joins it)

@@ -238,6 +238,9 @@ struct srt_plan {
     uint32_t *d_slat = nullptr;            // nranks * lrow_max * n: latency units (~0: unreachable),
                                            // u16 when stage16 (u16 keys), else u32
     bool stage16 = false;
+    bool fw_full_d = false;                // the closure left the whole D on every rank (symmetric sharded)
+    bool stage_loss_only = false;          // ... so the tail stages and exchanges only the loss; the
+                                           // latencies come from D (expand_rows_kernel)
     float *d_sloss = nullptr;              // nranks * lrow_max * n
     uint4 *d_tlist = nullptr;              // tlist_cap allocated slots of tight edges {v, u, w, 1-e bits} (v = ~0: pad)
     uint64_t tlist_cap = 0;

@@ -208,9 +208,13 @@ __global__ void tight_list_fill_kernel(const uint4 *__restrict__ list, uint64_t 
 // Sharded tail: every rank's staged rows into the table.  slot s = r * lrow_max
 // + k holds table row lrows[s] (~0: padding) as latency units (~0:
 // unreachable) and loss.
+// Dfull (u16 keys, the symmetric sharded closure on every rank): the staging
+// holds only the loss; latencies come from D (the diagonal: the self-loop).
 __global__ void expand_rows_kernel(const uint32_t *__restrict__ lrows, uint32_t slots, uint32_t n,
                                    const void *__restrict__ slat, bool lat16, const float *__restrict__ sloss,
-                                   uint64_t g, uint64_t *__restrict__ out_lat, float *__restrict__ out_loss) {
+                                   uint64_t g, uint64_t *__restrict__ out_lat, float *__restrict__ out_loss,
+                                   const uint16_t *__restrict__ Dfull, uint32_t Vp, const uint32_t *__restrict__ nodes,
+                                   const uint64_t *__restrict__ sl_lat) {
     for (uint32_t sl = blockIdx.x; sl < slots; sl += gridDim.x) {
         const uint32_t i = lrows[sl];
         if (i == ~0u) continue;
@@ -219,9 +223,13 @@ __global__ void expand_rows_kernel(const uint32_t *__restrict__ lrows, uint32_t 
         const float *sp = sloss + (uint64_t)sl * n;
         uint64_t *ol = out_lat + (uint64_t)i * n;
         float *op = out_loss + (uint64_t)i * n;
+        const uint16_t *Drow = Dfull ? Dfull + (uint64_t)nodes[i] * Vp : nullptr;
         for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
             uint64_t l;
-            if (lat16) {
+            if (Drow) {
+                const uint32_t x = Drow[nodes[j]];
+                l = j == i ? sl_lat[i] : x >= KEY16_INF ? ~0ull : (uint64_t)x * g;
+            } else if (lat16) {
                 const uint32_t x = s16[j];
                 l = x == 0xffffu ? ~0ull : (uint64_t)x * g;
             } else {
@@ -632,7 +640,7 @@ __global__ __launch_bounds__(LOSS_NT) void tight_loss_kernel(
         // or u32, ~0 = unreachable
         uint32_t *o32 = out32 && !stage16 ? reinterpret_cast<uint32_t *>(out32) + (uint64_t)k * n : nullptr;
         uint16_t *o16 = out32 && stage16 ? reinterpret_cast<uint16_t *>(out32) + (uint64_t)k * n : nullptr;
-        float *o32p = out32 ? out32_loss + (uint64_t)k * n : nullptr;
+        float *o32p = out32_loss ? out32_loss + (uint64_t)k * n : nullptr;  // staging (loss only if !out32)
         for (uint32_t j = tid; j < ((diag & 2u) ? 0u : n); j += nt) {
             uint64_t latv;
             float lossv;
@@ -651,11 +659,9 @@ __global__ __launch_bounds__(LOSS_NT) void tight_loss_kernel(
                     lossv = prow[v];
                 }
             }
-            if (o16) {
-                o16[j] = latv == ~0ull ? (uint16_t)0xffffu : (uint16_t)(latv / g);
-                o32p[j] = lossv;
-            } else if (o32) {
-                o32[j] = latv == ~0ull ? ~0u : (uint32_t)(latv / g);
+            if (o32p) {
+                if (o16) o16[j] = latv == ~0ull ? (uint16_t)0xffffu : (uint16_t)(latv / g);
+                else if (o32) o32[j] = latv == ~0ull ? ~0u : (uint32_t)(latv / g);
                 o32p[j] = lossv;
             } else {
                 ol[j] = latv;
@@ -897,7 +903,7 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
         float *op = out_loss + (uint64_t)i * n;
         uint32_t *o32 = out32 && !stage16 ? reinterpret_cast<uint32_t *>(out32) + (uint64_t)k * n : nullptr;
         uint16_t *o16 = out32 && stage16 ? reinterpret_cast<uint16_t *>(out32) + (uint64_t)k * n : nullptr;
-        float *o32p = out32 ? out32_loss + (uint64_t)k * n : nullptr;
+        float *o32p = out32_loss ? out32_loss + (uint64_t)k * n : nullptr;  // staging (loss only if !out32)
         for (uint32_t j = tid; j < ((diag & 2u) ? 0u : n); j += nt) {
             uint64_t latv;
             float lossv;
@@ -916,11 +922,9 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
                     lossv = __uint_as_float(prow[v]);
                 }
             }
-            if (o16) {
-                o16[j] = latv == ~0ull ? (uint16_t)0xffffu : (uint16_t)(latv / g);
-                o32p[j] = lossv;
-            } else if (o32) {
-                o32[j] = latv == ~0ull ? ~0u : (uint32_t)(latv / g);
+            if (o32p) {
+                if (o16) o16[j] = latv == ~0ull ? (uint16_t)0xffffu : (uint16_t)(latv / g);
+                else if (o32) o32[j] = latv == ~0ull ? ~0u : (uint32_t)(latv / g);
                 o32p[j] = lossv;
             } else {
                 ol[j] = latv;
@@ -1425,6 +1429,9 @@ srt_status loss_sharded_t(srt_plan *p, unsigned long long *d_stats, srt_err *err
     const uint32_t W = (uint32_t)p->comm->nranks, r = (uint32_t)p->comm->rank;
     const size_t chunk = (size_t)p->lrow_max * p->n;
     p->stage16 = p->key_type == KEY_U16;
+    // every rank holds the whole closure: exchange the loss only (knob
+    // SRT_TAIL_LAT=1 stages the latencies too, for A/B)
+    p->stage_loss_only = p->fw_full_d && p->stage16 && !std::getenv("SRT_TAIL_LAT");
     const size_t lb = p->stage16 ? 2 : 4;  // bytes per staged latency
     if (!p->d_slat) {
         void *a = nullptr, *b = nullptr;
@@ -1449,14 +1456,15 @@ srt_status loss_sharded_t(srt_plan *p, unsigned long long *d_stats, srt_err *err
         RowJob job;
         job.list = p->d_lrows + slot;
         job.count = p->lrow_cnt[r] > c * cr ? std::min(cr, p->lrow_cnt[r] - c * cr) : 0u;
-        job.out32 = reinterpret_cast<uint8_t *>(p->d_slat) + slot * p->n * lb;
+        job.out32 = p->stage_loss_only ? nullptr : reinterpret_cast<uint8_t *>(p->d_slat) + slot * p->n * lb;
         job.out32_loss = p->d_sloss + slot * p->n;
         if ((st = fold(p, d_stats, job, err)) != SRT_OK) return st;
         (void)hipEventRecord(p->ev_tail[c], M);
         (void)hipStreamWaitEvent(C, p->ev_tail[c], 0);
         const size_t base = (size_t)c * W * cr * p->n;
-        if ((st = comm_allgather_inplace(p->comm, reinterpret_cast<uint8_t *>(p->d_slat) + base * lb, lbytes, C,
-                                         err)) != SRT_OK ||
+        if ((!p->stage_loss_only &&
+             (st = comm_allgather_inplace(p->comm, reinterpret_cast<uint8_t *>(p->d_slat) + base * lb, lbytes, C,
+                                          err)) != SRT_OK) ||
             (st = comm_allgather_inplace(p->comm, p->d_sloss + base, cbytes, C, err)) != SRT_OK)
             return st;
     }
@@ -1531,7 +1539,8 @@ srt_status loss_emulated_t(srt_plan *p, unsigned long long *d_stats, srt_err *er
     if ((st = build_tight_rows(p, slots, ubits, maxw, err)) != SRT_OK) return st;
     const size_t chunk = (size_t)p->lrow_max * p->n;
     p->stage16 = p->key_type == KEY_U16;
-    const size_t lb = p->stage16 ? 2 : 4;  // bytes per staged latency
+    p->stage_loss_only = p->fw_full_d && p->stage16 && !std::getenv("SRT_TAIL_LAT");
+    const size_t lb = p->stage_loss_only ? 0 : p->stage16 ? 2 : 4;  // bytes per staged latency
     if (!p->d_slat) {
         void *a = nullptr, *b = nullptr;
         e = hipMalloc(&a, std::max<size_t>(chunk * W, 1) * 4);
@@ -1550,7 +1559,7 @@ srt_status loss_emulated_t(srt_plan *p, unsigned long long *d_stats, srt_err *er
         RowJob job;
         job.list = p->d_lrows + slot;
         job.count = p->lrow_cnt[0] > c * cr ? std::min(cr, p->lrow_cnt[0] - c * cr) : 0u;
-        job.out32 = reinterpret_cast<uint8_t *>(p->d_slat) + slot * p->n * lb;
+        job.out32 = p->stage_loss_only ? nullptr : reinterpret_cast<uint8_t *>(p->d_slat) + slot * p->n * lb;
         job.out32_loss = p->d_sloss + slot * p->n;
         if ((st = fold(p, d_stats, job, err)) != SRT_OK) return st;
         (void)hipEventRecord(p->ev_tail[c], M);
@@ -1571,7 +1580,8 @@ void expand_shard_rows(srt_plan *p, int nranks) {
     if (!slots || !p->n) return;
     hipLaunchKernelGGL(expand_rows_kernel, dim3(std::min<uint32_t>(slots, 4096)), dim3(256), 0, p->stream, p->d_lrows,
                        slots, p->n, (const void *)p->d_slat, p->stage16, p->d_sloss, p->kp.g, p->d_out_lat,
-                       p->d_out_loss);
+                       p->d_out_loss, p->stage_loss_only ? reinterpret_cast<const uint16_t *>(p->d_D) : nullptr,
+                       p->Vp, p->d_nodes, p->d_sl_lat);
 }
 
 srt_status fw_loss(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
