@@ -85,6 +85,10 @@ def parse_args():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the CPUs this process may use")
     ap.add_argument("--cpu-sources", type=int, default=0, help="0 = auto (~10-30 s of CPU work)")
     ap.add_argument("--no-e2e", dest="e2e", action="store_false", default=True)
+    ap.add_argument("--no-cold", dest="cold", action="store_false", default=True,
+                    help="skip the cold first-call legs (fresh processes) of the dense configs")
+    ap.add_argument("--cold-child", dest="cold_child", default="", choices=["", "plain", "init"],
+                    help=argparse.SUPPRESS)
     ap.add_argument("--emulate-ranks", dest="emulate_ranks", type=int, default=0,
                     help="measurement only (dense FW, 1 GPU): time one rank of an N-rank run -- 1/N of the "
                          "block-rows plus the pivot owner's chain every round, no collectives; the table "
@@ -256,6 +260,72 @@ def e2e_build(g, nodes, reps=3):
                     "validation, CSR upload, build, table download and plan teardown included"}
 
 
+def routing_info_builds(g, nodes, reps=3):
+    """generate_routing_info as Shadow calls it (sim_config.rs:424-461):
+    srt_routing_info_build from the host CSR to the RoutingInfo (the table kept
+    in its downloaded record form, decoded per path()).  Best of `reps`."""
+    from shadow_amd import RoutingInfo
+    times = []
+    rb = 0
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        ri = RoutingInfo.build(g, nodes)
+        times.append((time.perf_counter() - t0) * 1e3)
+        rb = ri.record_bytes()
+        ri.close()
+    return {"ms": min(times), "call_ms": [round(x, 2) for x in times], "record_bytes": rb,
+            "span": "srt_routing_info_build: host CSR -> RoutingInfo (validation, upload, build, download of the "
+                    "table's records, plan teardown)"}
+
+
+def cold_child(args):
+    """One fresh process, one first call (the bench's --cold-child mode): 'init'
+    calls srt_init_async first thing -- Shadow would, before its config and GML
+    parsing -- and the graph is built meanwhile; 'plain' does not, so the call
+    pays the HIP runtime start, the kernels' code-object loads and the pinning
+    of the transfer staging."""
+    t_start = time.perf_counter()
+    import shadow_amd
+    if args.cold_child == "init":
+        shadow_amd.init_async(0)
+    from shadow_amd import NetworkGraph, RoutingInfo, synth
+    cfg = CONFIGS[args.config]
+    n = args.nodes or cfg["nodes"]
+    seed = cfg["seed"] if args.seed < 0 else args.seed
+    if cfg["kind"] == "dense":
+        row_ptr, col, lat, loss = synth.dense_csr(n, synth.dense_graph(n, seed, drop=cfg["drop"]))
+    else:
+        row_ptr, col, lat, loss = synth.complete_csr(n, seed)
+    g = NetworkGraph(n, np.arange(n, dtype=np.uint32), row_ptr, col, lat, loss, directed=False)
+    nodes = np.arange(n, dtype=np.uint32)
+    t1 = time.perf_counter()
+    ri = RoutingInfo.build(g, nodes)
+    t2 = time.perf_counter()
+    print(json.dumps({"mode": args.cold_child, "first_call_ms": (t2 - t1) * 1e3,
+                      "graph_build_s": t1 - t_start, "record_bytes": ri.record_bytes(),
+                      "smallest_latency_ns": ri.get_smallest_latency_ns()}), flush=True)
+    ri.close()
+
+
+def cold_calls(args):
+    """The cold first call in fresh processes, without and with srt_init_async."""
+    out = {}
+    for mode in ("plain", "init"):
+        cmd = [sys.executable, os.path.abspath(__file__), "--cold-child", mode, "--config", args.config]
+        if args.nodes:
+            cmd += ["--nodes", str(args.nodes)]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+        if r.returncode != 0 or not line:
+            raise SystemExit(f"cold child ({mode}) failed: {r.stderr[-2000:]}")
+        out[mode] = json.loads(line[-1])
+    return {"plain_first_call_ms": out["plain"]["first_call_ms"], "init_first_call_ms": out["init"]["first_call_ms"],
+            "graph_build_s": out["init"]["graph_build_s"], "record_bytes": out["init"]["record_bytes"],
+            "what": "srt_routing_info_build as the first GPU call of a fresh process: 'plain' pays HIP start-up, "
+                    "code-object loads and the pinning of the transfer staging; 'init' called srt_init_async "
+                    "at process start, overlapped with building the graph (Shadow: config + GML parsing)"}
+
+
 def gml_graph(n_nodes, seed):
     from shadow_amd import synth
     src, dst, lat, loss = synth.complete_graph(n_nodes, seed)
@@ -385,8 +455,11 @@ def bench_graph(args, cfg, D):
     plan.close()
     n = len(nodes)
     e2e = None
-    if args.e2e and D.world == 1 and cfg["kind"] == "complete":
+    if args.e2e and D.world == 1 and cfg["kind"] in ("complete", "dense"):
         e2e = e2e_build(g, nodes)
+        e2e["routing_info"] = routing_info_builds(g, nodes)
+        if args.cold:
+            e2e["cold"] = cold_calls(args)
     out = None
     if D.rank == 0:
         pairs = n * n
@@ -604,6 +677,9 @@ def spawn_ranks(args):
 
 def main():
     args = parse_args()
+    if args.cold_child:
+        cold_child(args)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 and world == 1:
         sys.exit(spawn_ranks(args))

@@ -284,9 +284,36 @@ int srt_routing_info_smallest_latency_ns(const srt_routing_info *ri, uint64_t *o
 /* table row of a GML id (the srt_pkt src_row / dst_row of its host), -1 if not in use */
 int64_t srt_routing_info_row(const srt_routing_info *ri, uint32_t gml_id);
 uint32_t srt_routing_info_size(const srt_routing_info *ri);
-/* the dense table, row-major size x size, rows in in-use order (read-only) */
+/* Storage of the table.  srt_routing_info_build keeps the dense build's table
+ * in the record form it was downloaded in and decodes in path(): 6 bytes a
+ * pair (latency / g as u16 + f32 loss) for u16-key closures (C1-C3: 1.6 GB
+ * at 16k nodes instead of 4.3 GB of srt_path), 8 bytes (u32 + f32) for other
+ * closures whose latencies fit u32 units, else srt_path; the diagonal (the
+ * raw self-loops) is kept apart. */
+#define SRT_RI_PATH16 16  /* srt_path records */
+#define SRT_RI_REC8 8     /* {latency / g u32, loss f32} */
+#define SRT_RI_REC6 6     /* latency / g u16 array + loss f32 array */
+int srt_routing_info_record_bytes(const srt_routing_info *ri);
+/* the dense table as srt_path, row-major size x size, rows in in-use order
+ * (read-only) -- only for SRT_RI_PATH16 storage, else NULL (use path() or
+ * srt_routing_info_copy_table) */
 const srt_path *srt_routing_info_table(const srt_routing_info *ri);
+/* the whole table decoded into out[size * size] (any storage) */
+void srt_routing_info_copy_table(const srt_routing_info *ri, srt_path *out);
 void srt_routing_info_destroy(srt_routing_info *ri);
+
+/* --------------------------------------------------------------- start-up */
+/* Shadow builds the routing info once, at setup (sim_config.rs:136-140 ->
+ * generate_routing_info, sim_config.rs:424-461), so that one call is a cold
+ * one: it would pay the HIP runtime start, the load of this library's kernels
+ * and the pinning of the transfer staging on top of the build.  srt_init does
+ * those three on `device` (-1: the current device) and returns when done;
+ * srt_init_async starts it on a library thread and returns at once, so the
+ * simulator can call it first thing in main and parse its config and GML
+ * graph meanwhile.  Every build (and srt_init) waits for a pending init.
+ * Idempotent; errors of an async init surface in the next srt_init call. */
+srt_status srt_init(int device, srt_err *err);
+void srt_init_async(int device);
 
 /* --------------------------------------------------------------- GML ingest */
 /* Parses Shadow GML text (gml-parser grammar + NetworkGraph validation) into a

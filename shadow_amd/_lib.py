@@ -118,6 +118,10 @@ SIGNATURES = {
     "srt_routing_info_row": (C.c_int64, [_vp, C.c_uint32]),
     "srt_routing_info_size": (C.c_uint32, [_vp]),
     "srt_routing_info_table": (C.POINTER(SrtPath), [_vp]),
+    "srt_routing_info_record_bytes": (C.c_int, [_vp]),
+    "srt_routing_info_copy_table": (None, [_vp, C.POINTER(SrtPath)]),
+    "srt_init": (C.c_int, [C.c_int, _errp]),
+    "srt_init_async": (None, [C.c_int]),
     "srt_routing_info_destroy": (None, [_vp]),
     "srt_gml_parse": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(_vp), _errp]),
     "srt_gml_csr": (C.c_int, [_vp, C.POINTER(SrtCsr)]),
@@ -154,6 +158,18 @@ def lib():
 def check(rc: int, err: SrtErr):
     if rc != SRT_OK:
         raise SrtError(rc, err.msg.decode(errors="replace"), err.a_id, err.b_id)
+
+
+def init(device: int = -1) -> None:
+    """srt_init: HIP runtime, kernel code objects and pinned staging, ahead of
+    the first build (the cold-start work of generate_routing_info)."""
+    err = SrtErr()
+    check(lib().srt_init(int(device), C.byref(err)), err)
+
+
+def init_async(device: int = -1) -> None:
+    """srt_init_async: the same on a library thread; the next build waits for it."""
+    lib().srt_init_async(int(device))
 
 
 def require_device():

@@ -11,6 +11,7 @@
 //      SRT_ERR_DISCONNECTED.
 #include <hip/hip_runtime.h>
 #include <immintrin.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <chrono>
@@ -654,6 +655,7 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         (void)hipEventCreateWithFlags(&p->ev_pivot, sync_fl);
         (void)hipEventCreateWithFlags(&p->ev_row, sync_fl);
         (void)hipEventCreateWithFlags(&p->ev_bcast, sync_fl);
+        tr.mark("create: streams + events");
         srt_status st;
         if ((st = dmalloc(&p->d_row_ptr, (size_t)g->n_nodes + 1, err)) != SRT_OK ||
             (st = dmalloc(&p->d_col, g->n_adj, err)) != SRT_OK || (st = dmalloc(&p->d_lat, g->n_adj, err)) != SRT_OK ||
@@ -661,6 +663,7 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
             (st = dmalloc(&p->d_sl_lat, n, err)) != SRT_OK || (st = dmalloc(&p->d_sl_loss, n, err)) != SRT_OK ||
             (st = dmalloc(&p->d_stats, 2, err)) != SRT_OK || (st = dmalloc(&p->d_rstats, 2, err)) != SRT_OK)
             return st;
+        tr.mark("create: CSR device buffers");
         auto up = [&](void *dst, const void *src, size_t bytes) -> hipError_t {
             if (!bytes) return hipSuccess;
             return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, p->stream);
@@ -891,10 +894,12 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         }
     }
 #undef PLAN_TRY
-    if ((n && (e = hipMemcpyAsync(p->d_sl_lat, sl_lat.data(), (size_t)n * 8, hipMemcpyHostToDevice, p->stream)) !=
-                  hipSuccess) ||
-        (n && (e = hipMemcpyAsync(p->d_sl_loss, sl_loss.data(), (size_t)n * 4, hipMemcpyHostToDevice, p->stream)) !=
-                  hipSuccess) ||
+    p->h_sl_lat = std::move(sl_lat);
+    p->h_sl_loss = std::move(sl_loss);
+    if ((n && (e = hipMemcpyAsync(p->d_sl_lat, p->h_sl_lat.data(), (size_t)n * 8, hipMemcpyHostToDevice,
+                                  p->stream)) != hipSuccess) ||
+        (n && (e = hipMemcpyAsync(p->d_sl_loss, p->h_sl_loss.data(), (size_t)n * 4, hipMemcpyHostToDevice,
+                                  p->stream)) != hipSuccess) ||
         (e = hipStreamSynchronize(p->stream)) != hipSuccess) {
         srt_plan_destroy(p);
         return hip_fail(err, e, "upload");
@@ -1255,13 +1260,57 @@ void fetch_geometry(uint64_t *piece, int *depth) {
     if (const char *k = std::getenv("SRT_FETCH_DEPTH")) *depth = std::max(2, std::min(DEPTH_MAX, std::atoi(k)));
 }
 
+// The RoutingInfo's record arrays for an n x n table (2 MB aligned, on
+// transparent huge pages) touched on T host threads: the first touch of fresh
+// memory (page faults + the kernel's zeroing, ~1.6 GB for C3) costs more than
+// the download itself, so srt_routing_info_build runs this while the closure
+// is on the GPU and the download then copies into warm pages.
+bool ct_alloc(srt::CompactTable *ct, uint32_t n, uint64_t g, bool rec6, int T) {
+    ct->release();
+    ct->n = n;
+    ct->g = g;
+    ct->bytes = rec6 ? SRT_RI_REC6 : SRT_RI_REC8;
+    const uint64_t nn = std::max<uint64_t>((uint64_t)n * n, 1);
+    auto big = [](uint64_t bytes) -> void * {
+        const uint64_t HP = 2ull << 20, b = (bytes + HP - 1) / HP * HP;
+        void *q = std::aligned_alloc(HP, b);
+        if (q) (void)madvise(q, b, MADV_HUGEPAGE);
+        return q;
+    };
+    if (rec6) {
+        ct->lat16 = static_cast<uint16_t *>(big(nn * 2));
+        ct->loss = static_cast<float *>(big(nn * 4));
+    } else {
+        ct->rec8 = static_cast<uint2 *>(big(nn * 8));
+    }
+    if ((rec6 && (!ct->lat16 || !ct->loss)) || (!rec6 && !ct->rec8)) {
+        ct->release();
+        return false;
+    }
+    auto touch = [](void *q, uint64_t bytes, int w, int T) {
+        const uint64_t a = bytes * w / T, b = bytes * (w + 1) / T;
+        std::memset(static_cast<uint8_t *>(q) + a, 0, b - a);
+    };
+    std::vector<std::thread> pool;
+    for (int w = 0; w < T; ++w)
+        pool.emplace_back([&, w] {
+            if (ct->lat16) touch(ct->lat16, nn * 2, w, T);
+            if (ct->loss) touch(ct->loss, nn * 4, w, T);
+            if (ct->rec8) touch(ct->rec8, nn * 8, w, T);
+        });
+    for (auto &t : pool) t.join();
+    return true;
+}
+
 // End-to-end download of a kp.lat32 table in 8-byte records (latency / g as
 // u32 + loss bits: half the PCIe bytes of srt_path), pipelined three ways:
 // the device packs and copies piece c + 1 into one pinned buffer while host
-// threads expand piece c from the other into the caller's srt_path table, and
-// the fold of later rows still runs on the main stream.  Piece c waits for the
-// fold chunk holding its last entry (ev_fold).
-srt_status fetch_pipelined8(srt_plan *p, srt_path *out, uint8_t *pinned, srt_err *err) {
+// threads move piece c from the other into its destination, and the fold of
+// later rows still runs on the main stream.  Piece c waits for the fold chunk
+// holding its last entry (ev_fold).  Destination: the caller's srt_path table
+// (expanded; the diagonal then rewritten from the host self-loops, which need
+// not fit a record's latency field), or ct (the records kept as they are).
+srt_status fetch_pipelined8(srt_plan *p, srt_path *out, srt::CompactTable *ct, uint8_t *pinned, srt_err *err) {
     Trace tr;
     const uint64_t nn = (uint64_t)p->n * p->n, per_fold = (uint64_t)p->fold_chunk_rows * p->n;
     uint64_t PIECE;
@@ -1272,6 +1321,12 @@ srt_status fetch_pipelined8(srt_plan *p, srt_path *out, uint8_t *pinned, srt_err
     const bool rec6 = p->key_type == srt::KEY_U16 && !std::getenv("SRT_FETCH8");
     auto loss_off = [](uint64_t cnt) { return (cnt * 2 + 15) & ~15ull; };
     const uint32_t np = (uint32_t)((nn + PIECE - 1) / PIECE);
+    // the record arrays: prepared (and touched) while the closure ran, else now
+    if (ct && !(ct->n == p->n && ct->bytes == (rec6 ? SRT_RI_REC6 : SRT_RI_REC8) && (rec6 ? ct->lat16 != nullptr : ct->rec8 != nullptr)) &&
+        !ct_alloc(ct, p->n, p->kp.g, rec6, host_threads(nn))) {
+        set_err(err, SRT_ERR_OOM, "out of host memory (routing table)");
+        return SRT_ERR_OOM;
+    }
     if (!p->d_pack8) HIP_TRY(hipMalloc(&p->d_pack8, PIECE * 8 * DEPTH), "hipMalloc(pack8)");
     uint2 *h[DEPTH_MAX];
     hipEvent_t ev[DEPTH_MAX];
@@ -1299,10 +1354,23 @@ srt_status fetch_pipelined8(srt_plan *p, srt_path *out, uint8_t *pinned, srt_err
     // expansion of entries [a, b) of piece c into the caller's table: one
     // 16-byte non-temporal store per entry when the table is 16-byte aligned
     // (no read-for-ownership of the destination lines)
-    const bool nt = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+    const bool nt = out && (reinterpret_cast<uintptr_t>(out) & 15) == 0;
     auto expand_range = [&](uint32_t c, uint64_t a, uint64_t b) {
         const uint64_t first = (uint64_t)c * PIECE;
         const uint2 *src = h[c % DEPTH];
+        if (ct) {  // the records as they are
+            if (b <= a) return;
+            if (rec6) {
+                const uint64_t cnt = std::min(PIECE, nn - first);
+                std::memcpy(ct->lat16 + first + a, reinterpret_cast<const uint16_t *>(src) + a, (b - a) * 2);
+                std::memcpy(ct->loss + first + a,
+                            reinterpret_cast<const float *>(reinterpret_cast<const uint8_t *>(src) + loss_off(cnt)) + a,
+                            (b - a) * 4);
+            } else {
+                std::memcpy(ct->rec8 + first + a, src + a, (b - a) * 8);
+            }
+            return;
+        }
         srt_path *dst = out + first;
         if (rec6) {
             const uint64_t cnt = std::min(PIECE, nn - first);
@@ -1374,18 +1442,28 @@ srt_status fetch_pipelined8(srt_plan *p, srt_path *out, uint8_t *pinned, srt_err
     stop.store(1);
     for (auto &th : pool) th.join();
     if (tr.on)
-        std::fprintf(stderr, "[srt] fetch8: %u pieces of %d-byte records, %d threads, nt=%d: waited %.1f ms on DMA, "
-                     "%.1f ms expanding\n", np, rec6 ? 6 : 8, T, (int)nt, wait_dma, wait_expand);
+        std::fprintf(stderr, "[srt] fetch8: %u pieces of %d-byte records, %d threads, nt=%d, %s: waited %.1f ms on DMA, "
+                     "%.1f ms expanding\n", np, rec6 ? 6 : 8, T, (int)nt, ct ? "kept" : "expanded", wait_dma,
+                     wait_expand);
     tr.mark("fetch8: pieces downloaded + expanded");
     for (int i = 0; i < DEPTH; ++i) (void)hipEventDestroy(ev[i]);
     if (e != hipSuccess) return hip_fail(err, e, "compact download");
+    // the diagonal: the raw self-loops (mod.rs:210-217), from the host
+    if (ct) {
+        ct->diag.resize(p->n);
+        for (uint32_t i = 0; i < p->n; ++i) ct->diag[i] = srt_path{p->h_sl_lat[i], p->h_sl_loss[i], 0u};
+    } else {
+        for (uint32_t i = 0; i < p->n; ++i) out[(uint64_t)i * p->n + i] = srt_path{p->h_sl_lat[i], p->h_sl_loss[i], 0u};
+    }
     return SRT_OK;
 }
 
 // End-to-end download behind the chunked fold (fw_loss with fold_chunk_rows):
 // chunk c's rows are packed and copied to the host on the comm stream (idle
 // on one GPU) once ev_fold[c] fires, while the fold of chunk c + 1 runs.
-srt_status fetch_pipelined(srt_plan *p, srt_path *out, uint64_t *min_latency_ns, srt_err *err) {
+// ct: keep compact records (kp.lat32 plans) -- else ct gets an srt_path table.
+srt_status fetch_pipelined(srt_plan *p, srt_path *out, srt::CompactTable *ct, uint64_t *min_latency_ns,
+                           srt_err *err) {
     const uint64_t nn = (uint64_t)p->n * p->n, per = (uint64_t)p->fold_chunk_rows * p->n;
     const uint32_t nc = (uint32_t)((nn + per - 1) / per);
     if (!p->d_pack) {
@@ -1405,12 +1483,23 @@ srt_status fetch_pipelined(srt_plan *p, srt_path *out, uint64_t *min_latency_ns,
             int depth;
             fetch_geometry(&piece, &depth);
             if (pp.ensure(std::max<size_t>(PINNED_BYTES, (size_t)depth * piece * 8))) {
-                srt_status s = fetch_pipelined8(p, out, reinterpret_cast<uint8_t *>(pp.buf), err);
+                srt_status s = fetch_pipelined8(p, out, ct, reinterpret_cast<uint8_t *>(pp.buf), err);
                 if (s == SRT_OK) s = srt_plan_sync(p, err);
                 if (s == SRT_OK) s = srt_plan_fetch(p, nullptr, min_latency_ns, err);
                 return s;
             }
         }
+    }
+    if (ct) {
+        ct->release();
+        ct->n = p->n;
+        ct->bytes = SRT_RI_PATH16;
+        ct->full = static_cast<srt_path *>(std::malloc(std::max<uint64_t>(nn, 1) * sizeof(srt_path)));
+        if (!ct->full) {
+            set_err(err, SRT_ERR_OOM, "out of host memory (routing table)");
+            return SRT_ERR_OOM;
+        }
+        out = ct->full;
     }
     for (uint32_t c = 0; c < nc; ++c) {
         const uint64_t first = (uint64_t)c * per, cnt = std::min(per, nn - first);
@@ -1423,13 +1512,17 @@ srt_status fetch_pipelined(srt_plan *p, srt_path *out, uint64_t *min_latency_ns,
     srt_status s = srt_plan_sync(p, err);
     // connectivity (the reference's assert) and the min latency; the table is home
     if (s == SRT_OK) s = srt_plan_fetch(p, nullptr, min_latency_ns, err);
+    if (s == SRT_OK && ct) {
+        ct->diag.resize(p->n);
+        for (uint32_t i = 0; i < p->n; ++i) ct->diag[i] = out[(uint64_t)i * p->n + i];
+    }
     return s;
 }
-}  // namespace
 
-srt_status srt_compute_shortest_paths(const srt_csr *g, const uint32_t *nodes, uint32_t n,
-                                      srt_path *out, uint64_t *min_latency_ns,
-                                      const srt_opts *opts, srt_err *err) {
+// srt_compute_shortest_paths' end-to-end build into `out` (srt_path) or `ct`
+srt_status build_e2e(const srt_csr *g, const uint32_t *nodes, uint32_t n, srt_path *out, srt::CompactTable *ct,
+                     uint64_t *min_latency_ns, const srt_opts *opts, srt_err *err) {
+    srt::init_wait();
     srt_plan *p = nullptr;
     Trace tr;
     srt_status s = plan_create_impl(g, nodes, n, opts, &p, err, true);
@@ -1437,34 +1530,178 @@ srt_status srt_compute_shortest_paths(const srt_csr *g, const uint32_t *nodes, u
     if (s != SRT_OK) return s;
     // one-GPU dense build with a table wanted: the fold runs in chunks of <= 64
     // Mi entries whose downloads overlap the next chunk's fold
-    const bool pipe = out && p->n && p->algo == SRT_ALGO_FW && !p->comm && p->emulate_ranks <= 1;
+    const bool pipe = (out || ct) && p->n && p->algo == SRT_ALGO_FW && !p->comm && p->emulate_ranks <= 1;
     if (pipe)
         p->fold_chunk_rows = (uint32_t)std::max<uint64_t>(
             1, std::min<uint64_t>((uint64_t)p->n * p->n, 1ull << 26) / p->n);
     s = run_closure(p, err);
     tr.mark("e2e: closure enqueued");
     // the pinned staging of the compact download, pinned while the closure
-    // runs (first call of the process: ~1 ms per MB, too slow to pay inline)
-    std::thread pinner;
+    // runs (first call of the process without srt_init: ~1 ms per MB, too
+    // slow to pay inline)
+    std::thread pinner, prefault;
     if (s == SRT_OK && pipe && p->kp.lat32 && g_pinned.bytes < PINNED_BYTES)
         pinner = std::thread([] {
             std::lock_guard<std::mutex> lk(g_pinned.m);
             (void)g_pinned.ensure(PINNED_BYTES);
         });
+    // RoutingInfo records: allocated and touched while the closure runs
+    if (s == SRT_OK && pipe && ct && p->kp.lat32 && !std::getenv("SRT_FETCH16")) {
+        const bool rec6 = p->key_type == srt::KEY_U16 && !std::getenv("SRT_FETCH8");
+        const int T = host_threads((uint64_t)p->n * p->n);
+        prefault = std::thread([ct, p, rec6, T] { (void)ct_alloc(ct, p->n, p->kp.g, rec6, T); });
+    }
     if (s == SRT_OK) s = run_tail(p, err);  // the deferred loss upload overlaps the closure
     tr.mark("e2e: loss upload + tail enqueued");
     if (pinner.joinable()) pinner.join();
     tr.mark("e2e: pinned staging ready");
+    if (prefault.joinable()) prefault.join();
+    tr.mark("e2e: routing records touched");
     if (s == SRT_OK && pipe) {
-        s = fetch_pipelined(p, out, min_latency_ns, err);
+        s = fetch_pipelined(p, out, ct, min_latency_ns, err);
     } else if (s == SRT_OK) {
         s = srt_plan_sync(p, err);
+        if (s == SRT_OK && ct) {
+            ct->release();
+            ct->n = p->n;
+            ct->bytes = SRT_RI_PATH16;
+            ct->full = static_cast<srt_path *>(std::malloc(std::max<uint64_t>((uint64_t)p->n * p->n, 1) *
+                                                           sizeof(srt_path)));
+            if (!ct->full) {
+                srt_plan_destroy(p);
+                set_err(err, SRT_ERR_OOM, "out of host memory (routing table)");
+                return SRT_ERR_OOM;
+            }
+            out = ct->full;
+        }
         if (s == SRT_OK) s = srt_plan_fetch(p, out, min_latency_ns, err);
+        if (s == SRT_OK && ct) {
+            ct->diag.resize(p->n);
+            for (uint32_t i = 0; i < p->n; ++i) ct->diag[i] = out[(uint64_t)i * p->n + i];
+        }
     }
     tr.mark("e2e: build + fetch");
     srt_plan_destroy(p);
     tr.mark("e2e: destroy");
     return s;
+}
+
+// srt_init: the HIP runtime on the device, the library's code objects (one
+// kernel of each translation unit, which loads that unit's whole code object)
+// and the pinned transfer staging
+struct InitState {
+    std::mutex m;
+    std::thread th;
+    bool pending = false;
+    std::vector<int> done_dev;  // devices initialised
+    srt_status last = SRT_OK;
+    std::string msg;
+};
+InitState g_init;
+
+srt_status init_device(int device, std::string *msg) {
+    int dev = device;
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
+    hipError_t e = hipSetDevice(dev);
+    if (e == hipSuccess) e = hipFree(nullptr);  // creates the context
+    if (e == hipSuccess) e = srt::preload_kernels();
+    // the hardware queues behind a plan's streams (one normal, two high
+    // priority): the runtime creates them on first use (~0.1 s) and keeps
+    // them for later streams of the same priority
+    if (e == hipSuccess) {
+        int lo = 0, hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+        hipStream_t s[3] = {nullptr, nullptr, nullptr};
+        void *scratch = nullptr;
+        e = hipMalloc(&scratch, 4096);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&s[0], hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(&s[1], hipStreamNonBlocking, hi);
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(&s[2], hipStreamNonBlocking, hi);
+        for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipMemsetAsync(scratch, 0, 4096, s[i]);
+        for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipStreamSynchronize(s[i]);
+        for (int i = 0; i < 3; ++i)
+            if (s[i]) (void)hipStreamDestroy(s[i]);
+        if (scratch) (void)hipFree(scratch);
+    }
+    if (e == hipSuccess) {
+        std::lock_guard<std::mutex> lk(g_pinned.m);
+        if (!g_pinned.ensure(PINNED_BYTES)) e = hipErrorOutOfMemory;
+    }
+    if (e != hipSuccess) {
+        *msg = std::string("srt_init: ") + hipGetErrorString(e);
+        return SRT_ERR_HIP;
+    }
+    return SRT_OK;
+}
+}  // namespace
+
+}  // extern "C"
+
+namespace srt {
+void init_wait() {
+    std::thread t;
+    {
+        std::lock_guard<std::mutex> lk(g_init.m);
+        if (!g_init.pending) return;
+        t = std::move(g_init.th);
+        g_init.pending = false;
+    }
+    if (t.joinable()) t.join();
+}
+
+srt_status routing_build(const srt_csr *g, const uint32_t *nodes, uint32_t n, const srt_opts *opts, CompactTable *t,
+                         uint64_t *min_latency, srt_err *err) {
+    return build_e2e(g, nodes, n, nullptr, t, min_latency, opts, err);
+}
+}  // namespace srt
+
+extern "C" {
+
+srt_status srt_compute_shortest_paths(const srt_csr *g, const uint32_t *nodes, uint32_t n,
+                                      srt_path *out, uint64_t *min_latency_ns,
+                                      const srt_opts *opts, srt_err *err) {
+    return build_e2e(g, nodes, n, out, nullptr, min_latency_ns, opts, err);
+}
+
+srt_status srt_init(int device, srt_err *err) {
+    clear_err(err);
+    srt::init_wait();
+    std::lock_guard<std::mutex> lk(g_init.m);
+    int dev = device;
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (g_init.last != SRT_OK) {  // a failed async init
+        const srt_status s = g_init.last;
+        set_err(err, s, g_init.msg.c_str());
+        g_init.last = SRT_OK;
+        return s;
+    }
+    if (std::find(g_init.done_dev.begin(), g_init.done_dev.end(), dev) != g_init.done_dev.end()) return SRT_OK;
+    std::string msg;
+    const srt_status s = init_device(dev, &msg);
+    if (s != SRT_OK) {
+        set_err(err, s, msg.c_str());
+        return s;
+    }
+    g_init.done_dev.push_back(dev);
+    return SRT_OK;
+}
+
+void srt_init_async(int device) {
+    std::lock_guard<std::mutex> lk(g_init.m);
+    if (g_init.pending) return;
+    g_init.pending = true;
+    g_init.th = std::thread([device] {
+        std::string msg;
+        int dev = device;
+        if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
+        const srt_status s = init_device(dev, &msg);
+        std::lock_guard<std::mutex> lk2(g_init.m);
+        if (s == SRT_OK) g_init.done_dev.push_back(dev);
+        else {
+            g_init.last = s;
+            g_init.msg = msg;
+        }
+    });
 }
 
 }  // extern "C"

@@ -90,6 +90,14 @@ struct DevBuf {
 
 }  // namespace
 
+namespace srt {
+// srt_init: loads this unit's code object (srt::preload_kernels)
+hipError_t preload_direct() {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&direct_init_stats));
+}
+}  // namespace srt
+
 extern "C" srt_status srt_get_direct_paths(const srt_csr *g, const uint32_t *nodes, uint32_t n,
                                            srt_path *out, uint64_t *min_latency_ns,
                                            const srt_opts *opts, srt_err *err) {

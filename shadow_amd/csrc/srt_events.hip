@@ -192,6 +192,14 @@ int bit_width(uint32_t x) {
 
 }  // namespace
 
+namespace srt {
+// srt_init: loads this unit's code object (srt::preload_kernels)
+hipError_t preload_events() {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&event_id_kernel));
+}
+}  // namespace srt
+
 extern "C" srt_status srt_packet_events(srt_plan *plan, const uint32_t *d_host_pkt_ptr, uint32_t n_hosts,
                                         uint64_t n_pkts, const uint32_t *d_flags, const uint64_t *d_deliver,
                                         const uint32_t *d_dst_host, uint32_t n_dst_hosts, uint64_t *d_event_base,

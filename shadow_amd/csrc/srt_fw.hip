@@ -2850,4 +2850,25 @@ void pack_paths(srt_plan *p, uint64_t first, uint64_t count, srt_path *dst, hipS
                        count);
 }
 
+// srt_init: loads this unit's code object (srt::preload_kernels)
+hipError_t preload_fw() {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&fill_kernel<uint16_t>));
+}
+
+hipError_t preload_loss();
+hipError_t preload_sssp();
+hipError_t preload_packet();
+hipError_t preload_direct();
+hipError_t preload_events();
+hipError_t preload_kernels() {
+    hipError_t e = preload_fw();
+    if (e == hipSuccess) e = preload_loss();
+    if (e == hipSuccess) e = preload_sssp();
+    if (e == hipSuccess) e = preload_packet();
+    if (e == hipSuccess) e = preload_direct();
+    if (e == hipSuccess) e = preload_events();
+    return e;
+}
+
 }  // namespace srt

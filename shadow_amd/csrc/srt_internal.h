@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -126,6 +127,8 @@ struct srt_plan {
     float *d_out_loss = nullptr;
     uint64_t *d_sl_lat = nullptr;
     float *d_sl_loss = nullptr;
+    std::vector<uint64_t> h_sl_lat;  // the self-loops on the host too (the compact downloads'
+    std::vector<float> h_sl_loss;    // diagonal: a self-loop need not fit their latency field)
     unsigned long long *d_stats = nullptr;  // [0] min latency, [1] unreachable pairs
     srt_path *d_pack = nullptr;             // AoS staging for fetch
     void *d_pack8 = nullptr;                // 8-byte staging of the compact end-to-end download
@@ -250,6 +253,56 @@ struct srt_plan {
 };
 
 namespace srt {
+// A host routing table in the record form of its download (srt_routing.cpp
+// decodes it per path() call): SRT_RI_REC6 = lat16[n*n] (latency / g, 0xFFFF
+// unreachable) + loss[n*n]; SRT_RI_REC8 = rec8[n*n] {latency / g (~0:
+// unreachable), loss bits}; SRT_RI_PATH16 = full[n*n].  The diagonal (the raw
+// self-loops, mod.rs:210-217) is diag[n] in every form.
+struct CompactTable {
+    int bytes = SRT_RI_PATH16;
+    uint32_t n = 0;
+    uint64_t g = 1;
+    uint16_t *lat16 = nullptr;
+    float *loss = nullptr;
+    uint2 *rec8 = nullptr;
+    srt_path *full = nullptr;
+    std::vector<srt_path> diag;
+    srt_path at(uint64_t i, uint64_t j) const {
+        if (i == j) return diag[i];
+        const uint64_t e = i * n + j;
+        srt_path q{};
+        if (bytes == SRT_RI_REC6) {
+            q.latency_ns = lat16[e] == 0xffffu ? ~0ull : (uint64_t)lat16[e] * g;
+            q.packet_loss = loss[e];
+        } else if (bytes == SRT_RI_REC8) {
+            const uint2 r = rec8[e];
+            q.latency_ns = r.x == 0xffffffffu ? ~0ull : (uint64_t)r.x * g;
+            q.packet_loss = __builtin_bit_cast(float, r.y);
+        } else {
+            q = full[e];
+        }
+        return q;
+    }
+    void release() {
+        std::free(lat16);
+        std::free(loss);
+        std::free(rec8);
+        std::free(full);
+        lat16 = nullptr;
+        loss = nullptr;
+        rec8 = nullptr;
+        full = nullptr;
+    }
+};
+// generate_routing_info's shortest-path build straight into a CompactTable
+// (srt_api.cpp): the end-to-end build of srt_compute_shortest_paths with the
+// downloaded records kept as they are; *min_latency as that function's
+srt_status routing_build(const srt_csr *g, const uint32_t *nodes, uint32_t n, const srt_opts *opts, CompactTable *t,
+                         uint64_t *min_latency, srt_err *err);
+// waits for a pending srt_init_async (srt_api.cpp)
+void init_wait();
+// loads the code object of every kernel translation unit (srt_init)
+hipError_t preload_kernels();
 // collectives (srt_comm.cpp)
 srt_status comm_bcast(srt_comm *c, void *buf, size_t bytes, int root, hipStream_t s, srt_err *err);
 srt_status comm_allgather_inplace(srt_comm *c, void *buf, size_t bytes_per_rank, hipStream_t s,

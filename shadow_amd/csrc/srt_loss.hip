@@ -180,6 +180,93 @@ __global__ void tight_list_kernel(uint32_t u0, uint32_t u1, const uint64_t *__re
     }
 }
 
+// One GPU, packed forms: the tight edges of adjacency rows [0, V) straight
+// into the list, one wave per row in two passes -- pass 1 tests each 64-entry
+// chunk (w * g == lat and w == D[u][v]) and keeps its ballot in LDS (chunks
+// past TR_CH are tested again in pass 2), one atomic takes the row's range,
+// pass 2 writes the records of the set lanes.  No flag array: against the
+// flag + list kernels (1.16 + 0.74 ms on C3) the adjacency is read once and
+// the second pass touches only the tight entries.  Writes only when the whole
+// row fits below cap (list slots); total and max w are always counted, so a
+// run with cap 0 (or too small a list) counts and the caller runs it again.
+constexpr uint32_t TR_CH = 256;  // chunks (64 entries) a wave keeps in LDS: rows up to 16,384 entries
+template <typename K>
+__global__ __launch_bounds__(256) void tight_rows_kernel(const K *__restrict__ D, uint32_t Vp, uint32_t V,
+                                                         const uint64_t *__restrict__ row_ptr,
+                                                         const uint32_t *__restrict__ col,
+                                                         const uint64_t *__restrict__ lat,
+                                                         const float *__restrict__ loss, uint64_t g,
+                                                         uint4 *__restrict__ list, uint64_t cap,
+                                                         unsigned long long *cursor, unsigned long long *maxw,
+                                                         unsigned long long *total) {
+    __shared__ uint64_t bal[4][TR_CH];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    uint64_t mw = 0, tot = 0;
+    auto test = [&](uint32_t u, const K *Du, uint64_t k, uint64_t e) -> bool {
+        if (k >= e) return false;
+        const uint32_t v = col[k];
+        if (v == u) return false;
+        const K d = Du[v];
+        const uint64_t w = KeyLat<K>::lat(d);
+        return !KeyLat<K>::inf(d) && w * g == lat[k];
+    };
+    for (uint32_t u = wave; u < V; u += nwaves) {
+        const K *Du = D + (uint64_t)u * Vp;
+        const uint64_t b = row_ptr[u], e = row_ptr[u + 1];
+        const uint32_t nch = (uint32_t)((e - b + 63) / 64);
+        uint32_t cnt = 0;
+        // 4 chunks per step: their col / lat loads, then their D loads, in flight together
+        for (uint32_t c0 = 0; c0 < nch; c0 += 4) {
+            uint32_t v[4];
+            uint64_t l[4];
+            K d[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint64_t k = b + 64ull * (c0 + q) + lane;
+                v[q] = k < e ? col[k] : u;
+                l[q] = k < e ? lat[k] : 0;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) d[q] = Du[v[q]];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint64_t w = KeyLat<K>::lat(d[q]);
+                const bool f = v[q] != u && !KeyLat<K>::inf(d[q]) && w * g == l[q];
+                const uint64_t m = __ballot(f);
+                if (f) mw = w > mw ? w : mw;
+                if (c0 + q < TR_CH && lane == 0) bal[wv][c0 + q] = m;
+                cnt += (uint32_t)__popcll(m);
+            }
+        }
+        if (!cnt) continue;
+        tot += cnt;
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(cursor, (unsigned long long)cnt);
+        base = __shfl(base, 0);
+        if (base + cnt > cap) continue;  // uniform: the caller grows the list and runs again
+        for (uint32_t c = 0; c < nch; ++c) {
+            const uint64_t k = b + 64ull * c + lane;
+            const uint64_t m = c < TR_CH ? bal[wv][c] : __ballot(test(u, Du, k, e));
+            if (!m) continue;  // uniform
+            if ((m >> lane) & 1ull) {
+                const uint64_t pos = base + __popcll(m & ((1ull << lane) - 1ull));
+                const float eb = 1.0f - loss[k];  // the reference's (1f32 - other.packet_loss), mod.rs:328
+                list[pos] = make_uint4(col[k], u, (uint32_t)(lat[k] / g), __float_as_uint(eb));
+            }
+            base += __popcll(m);
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(mw, off);
+        mw = o > mw ? o : mw;
+    }
+    // tot is uniform per wave (ballot counts)
+    if (lane == 0 && mw) atomicMax(maxw, (unsigned long long)mw);
+    if (lane == 0 && tot) atomicAdd(total, (unsigned long long)tot);
+}
+
 // Per-row counts of a tight-edge list (v = ~0: padding): rows by target v
 // (pull CSR) or, BY_SRC, by source u (push CSR)
 template <bool BY_SRC>
@@ -752,6 +839,7 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
     __shared__ uint64_t red[16];
     __shared__ unsigned long long red_min[16], red_cnt[16];
     __shared__ uint32_t plan_end[WC + 1];  // inclusive prefix of the class item counts
+    __shared__ uint32_t wcnt[16][32];      // few-level sort: per-wave level counts, then bases
     __shared__ uint32_t plan_push;         // bit w: class w pushes from N_{l-w}
     uint32_t *hist = reinterpret_cast<uint32_t *>(smem);
     uint16_t *lrow = reinterpret_cast<uint16_t *>(smem + HIST_BYTES);
@@ -789,14 +877,59 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
         __syncthreads();
         mx = 0;
         for (int q = 0; q < nw; ++q) mx = red[q] > mx ? (uint32_t)red[q] : mx;
-        const bool few = mx < 64;  // uniform: aggregate the LDS atomics per wave
-        // 2. counting sort of the reachable vertices (s at level 0) by level
+        // 2. counting sort of the reachable vertices (s at level 0) by level.
+        // Few levels (mx < 32, C3: ~6): one ballot per level and 64-vertex
+        // chunk, a wave's count of level l in lane l; the per-wave counts are
+        // scanned level-major, so every wave places its chunks' vertices at
+        // its own bases without atomics.  Else LDS atomics per distinct level.
+        if (mx < 32) {
+            uint32_t mine = 0;  // lane l: this wave's vertices at level l
+            for (uint32_t base = 0; base < V; base += nt) {
+                const uint32_t v = base + tid;
+                const uint16_t l = v < V ? lrow[v] : LINF;
+                for (uint32_t q = 0; q <= mx; ++q) {
+                    const uint64_t m = __ballot(l == q);
+                    if (lane == (int)q) mine += (uint32_t)__popcll(m);
+                }
+            }
+            if (lane < 32) wcnt[wv][lane] = lane <= (int)mx ? mine : 0u;
+            __syncthreads();
+            if (wv == 0 && lane < 32) {
+                uint32_t tot = 0;
+                for (int q = 0; q < nw; ++q) tot += wcnt[q][lane];
+                uint32_t x = tot;  // inclusive scan over the levels (lanes 0..31)
+                for (int off = 1; off < 32; off <<= 1) {
+                    const uint32_t y = __shfl_up(x, off, 32);
+                    if (lane >= off) x += y;
+                }
+                uint32_t run = x - tot;  // start of level `lane`
+                for (int q = 0; q < nw; ++q) {
+                    const uint32_t c = wcnt[q][lane];
+                    wcnt[q][lane] = run;
+                    run += c;
+                }
+                if (lane <= (int)mx) hist[lane] = x;  // end of level `lane`
+            }
+            __syncthreads();
+            uint32_t at = wcnt[wv][lane & 31];  // lane l: where this wave's next level-l vertex goes
+            for (uint32_t base = 0; base < V; base += nt) {
+                const uint32_t v = base + tid;
+                const uint16_t l = v < V ? lrow[v] : LINF;
+                for (uint32_t q = 0; q <= mx; ++q) {
+                    const uint64_t m = __ballot(l == q);
+                    if (!m) continue;  // uniform
+                    const uint32_t b = __builtin_amdgcn_readlane(at, q);
+                    if (l == q) mem[b + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)v;
+                    if (lane == (int)q) at += (uint32_t)__popcll(m);
+                }
+            }
+            __syncthreads();
+        } else {
         for (uint32_t base = 0; base < V; base += nt) {
             const uint32_t v = base + tid;
             const uint16_t l = v < V ? lrow[v] : LINF;
             const bool ok = l != LINF;
-            if (few) agg_inc(hist, ok ? l : 0u, ok);
-            else if (ok) atomicAdd(&hist[l], 1u);
+            if (ok) atomicAdd(&hist[l], 1u);
         }
         __syncthreads();
         {  // exclusive scan of hist[0, NBK): each thread a contiguous run
@@ -825,12 +958,10 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
             const uint32_t v = base + tid;
             const uint16_t l = v < V ? lrow[v] : LINF;
             const bool ok = l != LINF;
-            uint32_t pos = 0;
-            if (few) pos = agg_inc(hist, ok ? l : 0u, ok);
-            else if (ok) pos = atomicAdd(&hist[l], 1u);
-            if (ok) mem[pos] = (uint16_t)v;
+            if (ok) mem[atomicAdd(&hist[l], 1u)] = (uint16_t)v;
         }
         __syncthreads();
+        }
         // hist[l] is now the end of level l (its start: hist[l-1], or 0)
         // 3. levels in increasing latency, every weight class from its smaller end
         // (diag, timing-only knob SRT_LOSS_DIAG, wrong tables: bit 0 skips the
@@ -854,15 +985,25 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
             }
             __syncthreads();
             const uint32_t T = plan_end[WC], pm = plan_push;
-            for (uint32_t t = grp; t < T; t += ngrp) {
-                uint32_t w = 1;
+            // item t -> (class w, member x, its edge range); the next item's
+            // range is loaded while the current one is walked
+            auto item = [&](uint32_t t, uint32_t &w, uint32_t &x, uint32_t &e0, uint32_t &e1) {
+                w = 1;
                 while (t >= plan_end[w]) ++w;
                 const uint32_t m = t - (w > 1 ? plan_end[w - 1] : 0u), j = l - w;
                 const bool push = (pm >> w) & 1u;
-                const uint32_t x = mem[(push ? (j ? hist[j - 1] : 0u) : lo) + m];
+                x = mem[(push ? (j ? hist[j - 1] : 0u) : lo) + m];
                 const uint32_t *cl = push ? cls_out : cls_in;
+                e0 = cl[(uint64_t)x * CLS + w - 1];
+                e1 = cl[(uint64_t)x * CLS + w];
+            };
+            uint32_t nw_ = 1, nx = 0, ne0 = 0, ne1 = 0;
+            if (grp < T) item(grp, nw_, nx, ne0, ne1);
+            for (uint32_t t = grp; t < T; t += ngrp) {
+                const uint32_t w = nw_, x = nx, e0 = ne0, e1 = ne1, j = l - w;
+                if (t + ngrp < T) item(t + ngrp, nw_, nx, ne0, ne1);
+                const bool push = (pm >> w) & 1u;
                 const uint64_t *ce = push ? ce_out : ce_in;
-                const uint32_t e0 = cl[(uint64_t)x * CLS + w - 1], e1 = cl[(uint64_t)x * CLS + w];
                 // push: x in N_j, its class-w out-edges x -> v, v in N_l;
                 // pull: x in N_l, its class-w in-edges u -> x, u in N_j
                 const uint16_t want = (uint16_t)(push ? l : j);
@@ -1240,25 +1381,33 @@ srt_status tight_csr_push_t(srt_plan *p, unsigned long long *d_stats, bool *done
         (st = grow(&p->d_tcursor, &cap_cur, 1, err, "hipMalloc(tight cursor)")) != SRT_OK)
         return st;
     hipLaunchKernelGGL(loss_stats_init_kernel, dim3(1), dim3(1), 0, M, d_stats, (unsigned long long *)p->d_tmaxw);
-    (void)hipMemsetAsync(p->d_tinfo, 0, 2 * sizeof(unsigned long long), M);
-    (void)hipMemsetAsync(p->d_tcursor, 0, sizeof(unsigned long long), M);
     const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(8192, (V + 3) / 4));
-    hipLaunchKernelGGL(tight_flag_kernel<K>, dim3(blocks), dim3(256), 0, M, reinterpret_cast<const K *>(p->d_D),
-                       p->Vp, 0u, V, p->d_row_ptr, p->d_col, p->d_lat, p->kp.g, p->d_tflag, (uint32_t *)nullptr,
-                       (unsigned long long *)p->d_tmaxw, p->d_tinfo);
-    (void)hipMemcpyAsync(p->h_tcount, p->d_tinfo, sizeof(uint64_t), hipMemcpyDeviceToHost, M);
-    (void)hipMemcpyAsync(p->h_tcount + 1, p->d_tmaxw, sizeof(uint64_t), hipMemcpyDeviceToHost, M);
-    hipError_t e = hipStreamSynchronize(M);
-    if (e != hipSuccess) return fail(err, e, "tight-edge count");
+    // the list straight from the adjacency (tight_rows_kernel) into the list
+    // the last run sized; a first run (or a larger count) counts, grows the
+    // list and runs again
+    auto rows = [&]() {
+        (void)hipMemsetAsync(p->d_tinfo, 0, 2 * sizeof(unsigned long long), M);
+        (void)hipMemsetAsync(p->d_tcursor, 0, sizeof(unsigned long long), M);
+        hipLaunchKernelGGL(tight_rows_kernel<K>, dim3(blocks), dim3(256), 0, M, reinterpret_cast<const K *>(p->d_D),
+                           p->Vp, V, p->d_row_ptr, p->d_col, p->d_lat, p->d_loss, p->kp.g, p->d_tlist,
+                           p->d_tlist ? p->tlist_cap : 0ull, p->d_tcursor, (unsigned long long *)p->d_tmaxw,
+                           p->d_tinfo);
+        (void)hipMemcpyAsync(p->h_tcount, p->d_tinfo, sizeof(uint64_t), hipMemcpyDeviceToHost, M);
+        (void)hipMemcpyAsync(p->h_tcount + 1, p->d_tmaxw, sizeof(uint64_t), hipMemcpyDeviceToHost, M);
+        return hipStreamSynchronize(M);
+    };
+    hipError_t e = rows();
+    if (e != hipSuccess) return fail(err, e, "tight-edge list");
     const uint64_t total = p->h_tcount[0], maxw = p->h_tcount[1];
     const uint32_t ubits = (uint32_t)std::max(1, bits_of(V ? V - 1 : 0));
     if (!(p->kp.lat32 && ubits + bits_of(maxw) <= 32 && total < (1ull << 32))) return SRT_OK;
     p->t_edges = total;
     if ((st = ensure_edge_arrays(p, err)) != SRT_OK) return st;
     const uint64_t C = std::max<uint64_t>(total, 1);
-    if ((st = ensure_tlist(p, C + C / 4 + 64, C, err)) != SRT_OK) return st;
-    hipLaunchKernelGGL(tight_list_kernel, dim3(blocks), dim3(256), 0, M, 0u, V, p->d_row_ptr, p->d_col, p->d_lat,
-                       p->d_loss, p->kp.g, p->d_tflag, p->d_tlist, p->d_tcursor);
+    if (!p->d_tlist || total > p->tlist_cap) {
+        if ((st = ensure_tlist(p, C + C / 4 + 64, C, err)) != SRT_OK) return st;
+        if ((e = rows()) != hipSuccess) return fail(err, e, "tight-edge list");
+    }
     if ((st = build_tight_rows(p, total, ubits, maxw, err)) != SRT_OK) return st;
     p->t_packed = true;
     *done = true;
@@ -1639,6 +1788,12 @@ srt_status fw_loss(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     }
     (void)hipEventRecord(p->ev_loss1, p->stream);
     return SRT_OK;
+}
+
+// srt_init: loads this unit's code object (srt::preload_kernels)
+hipError_t preload_loss() {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&loss_stats_init_kernel));
 }
 
 }  // namespace srt

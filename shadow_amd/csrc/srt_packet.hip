@@ -160,6 +160,14 @@ __global__ __launch_bounds__(1024) void stats_kernel(const unsigned long long *_
 
 }  // namespace
 
+namespace srt {
+// srt_init: loads this unit's code object (srt::preload_kernels)
+hipError_t preload_packet() {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&decide_kernel));
+}
+}  // namespace srt
+
 extern "C" srt_status srt_packet_batch(srt_plan *plan, const srt_pkt *d_pkts,
                                        const uint32_t *d_host_pkt_ptr, uint32_t n_hosts,
                                        uint64_t n_pkts, uint64_t *d_rng, const srt_round *round,

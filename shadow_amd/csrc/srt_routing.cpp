@@ -9,7 +9,10 @@
 // srt_path mirror of PathProperties), one GML id -> row map replaces the N^2
 // re-keying (a direct array when the ids are dense, else a sorted array with
 // binary search), and the packet counters are a dense array of atomics with
-// the reference's saturating add -- no lock on the send path.
+// the reference's saturating add -- no lock on the send path.  The shortest-
+// path table is kept in the record form the build downloaded it in (6 or 8
+// bytes a pair, srt::CompactTable) and decoded per path() call: no n^2
+// expansion into srt_path (4.3 GB at 16k nodes) on the host.
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
@@ -22,7 +25,7 @@
 
 struct srt_routing_info {
     uint32_t n = 0;
-    srt_path *table = nullptr;               // n * n
+    srt::CompactTable t;                     // n * n paths (compact records or srt_path)
     std::atomic<uint64_t> *counters = nullptr;  // n * n, calloc'd: untouched pairs cost no memory
     std::vector<int32_t> dense;              // id -> row when ids are dense (-1: not in use)
     std::vector<std::pair<uint32_t, uint32_t>> sorted;  // (id, row) otherwise
@@ -53,9 +56,8 @@ srt_status make_info(uint32_t n, const uint32_t *ids, srt_routing_info **out, sr
     }
     ri->n = n;
     const size_t nn = (size_t)n * n;
-    ri->table = static_cast<srt_path *>(std::malloc(std::max<size_t>(nn, 1) * sizeof(srt_path)));
     ri->counters = static_cast<std::atomic<uint64_t> *>(std::calloc(std::max<size_t>(nn, 1), sizeof(uint64_t)));
-    if (!ri->table || !ri->counters) {
+    if (!ri->counters) {
         srt_routing_info_destroy(ri);
         rerr(err, SRT_ERR_OOM, "out of host memory (routing table)");
         return SRT_ERR_OOM;
@@ -72,6 +74,24 @@ srt_status make_info(uint32_t n, const uint32_t *ids, srt_routing_info **out, sr
     }
     *out = ri;
     return SRT_OK;
+}
+
+// an srt_path table of n * n entries for ri->t (direct paths, plans)
+srt_status full_table(srt_routing_info *ri, srt_err *err) {
+    ri->t.release();
+    ri->t.n = ri->n;
+    ri->t.bytes = SRT_RI_PATH16;
+    ri->t.full = static_cast<srt_path *>(std::malloc(std::max<size_t>((size_t)ri->n * ri->n, 1) * sizeof(srt_path)));
+    if (!ri->t.full) {
+        rerr(err, SRT_ERR_OOM, "out of host memory (routing table)");
+        return SRT_ERR_OOM;
+    }
+    return SRT_OK;
+}
+
+void diag_from_full(srt_routing_info *ri) {
+    ri->t.diag.resize(ri->n);
+    for (uint32_t i = 0; i < ri->n; ++i) ri->t.diag[i] = ri->t.full[(size_t)i * ri->n + i];
 }
 
 std::vector<uint32_t> gml_ids(const srt_csr *g, const uint32_t *nodes, uint32_t n) {
@@ -105,8 +125,13 @@ srt_status srt_routing_info_build(const srt_csr *g, const uint32_t *nodes, uint3
     srt_status st = make_info(n, ids.data(), &ri, err);
     if (st != SRT_OK) return st;
     uint64_t mn = ~0ull;
-    st = use_shortest_paths ? srt_compute_shortest_paths(g, nodes, n, ri->table, &mn, opts, err)
-                            : srt_get_direct_paths(g, nodes, n, ri->table, &mn, opts, err);
+    if (use_shortest_paths) {
+        st = srt::routing_build(g, nodes, n, opts, &ri->t, &mn, err);
+    } else {
+        st = full_table(ri, err);
+        if (st == SRT_OK) st = srt_get_direct_paths(g, nodes, n, ri->t.full, &mn, opts, err);
+        if (st == SRT_OK) diag_from_full(ri);
+    }
     if (st != SRT_OK) {
         srt_routing_info_destroy(ri);
         return st;
@@ -131,7 +156,9 @@ srt_status srt_routing_info_from_plan(srt_plan *plan, srt_routing_info **out, sr
     srt_status st = make_info(plan->n, ids.data(), &ri, err);
     if (st != SRT_OK) return st;
     uint64_t mn = ~0ull;
-    st = srt_plan_fetch(plan, ri->table, &mn, err);
+    st = full_table(ri, err);
+    if (st == SRT_OK) st = srt_plan_fetch(plan, ri->t.full, &mn, err);
+    if (st == SRT_OK) diag_from_full(ri);
     if (st != SRT_OK) {
         srt_routing_info_destroy(ri);
         return st;
@@ -146,7 +173,7 @@ srt_status srt_routing_info_path(const srt_routing_info *ri, uint32_t src_id, ui
     if (!ri || !out) return SRT_ERR_INVALID;
     const int64_t i = ri->row(src_id), j = ri->row(dst_id);
     if (i < 0 || j < 0) return SRT_ERR_INVALID;
-    *out = ri->table[(size_t)i * ri->n + (size_t)j];
+    *out = ri->t.at((uint64_t)i, (uint64_t)j);
     return SRT_OK;
 }
 
@@ -192,11 +219,21 @@ int64_t srt_routing_info_row(const srt_routing_info *ri, uint32_t gml_id) { retu
 
 uint32_t srt_routing_info_size(const srt_routing_info *ri) { return ri ? ri->n : 0; }
 
-const srt_path *srt_routing_info_table(const srt_routing_info *ri) { return ri ? ri->table : nullptr; }
+int srt_routing_info_record_bytes(const srt_routing_info *ri) { return ri ? ri->t.bytes : 0; }
+
+const srt_path *srt_routing_info_table(const srt_routing_info *ri) {
+    return ri && ri->t.bytes == SRT_RI_PATH16 ? ri->t.full : nullptr;
+}
+
+void srt_routing_info_copy_table(const srt_routing_info *ri, srt_path *out) {
+    if (!ri || !out) return;
+    for (uint64_t i = 0; i < ri->n; ++i)
+        for (uint64_t j = 0; j < ri->n; ++j) out[i * ri->n + j] = ri->t.at(i, j);
+}
 
 void srt_routing_info_destroy(srt_routing_info *ri) {
     if (!ri) return;
-    std::free(ri->table);
+    ri->t.release();
     std::free(ri->counters);
     delete ri;
 }

@@ -1269,4 +1269,10 @@ void reduce_rank_stats(srt_plan *p, int nranks) {
                        (const unsigned long long *)p->d_rstats, nranks, p->d_stats);
 }
 
+// srt_init: loads this unit's code object (srt::preload_kernels)
+hipError_t preload_sssp() {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&sssp_init_kernel));
+}
+
 }  // namespace srt

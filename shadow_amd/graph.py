@@ -303,12 +303,18 @@ class RoutingInfo:
         v = C.c_uint64()
         return int(v.value) if _lib.lib().srt_routing_info_smallest_latency_ns(self._h, C.byref(v)) else None
 
+    def record_bytes(self) -> int:
+        """Bytes a pair of the stored table: 6 / 8 (compact records decoded by
+        path()) or 16 (srt_path)."""
+        return int(_lib.lib().srt_routing_info_record_bytes(self._h))
+
     def table(self):
-        """(latency_ns u64[n,n], packet_loss f32[n,n]) copies of the dense table."""
+        """(latency_ns u64[n,n], packet_loss f32[n,n]) copies of the dense table
+        (srt_routing_info_copy_table: any storage)."""
         n = len(self)
-        ptr = _lib.lib().srt_routing_info_table(self._h)
-        raw = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint8)), shape=(max(n * n, 1) * 16,))
-        rec = raw.view(np.dtype([("lat", "<u8"), ("loss", "<f4"), ("pad", "<u4")]))[:n * n]
+        rec = np.empty(max(n * n, 1), np.dtype([("lat", "<u8"), ("loss", "<f4"), ("pad", "<u4")]))
+        _lib.lib().srt_routing_info_copy_table(self._h, rec.ctypes.data_as(C.POINTER(_lib.SrtPath)))
+        rec = rec[:n * n]
         return rec["lat"].reshape(n, n).copy(), rec["loss"].reshape(n, n).copy()
 
     def close(self):

@@ -97,3 +97,74 @@ def test_empty_in_use_set():
     ri = generate_routing_info(g, set())
     assert len(ri) == 0 and ri.get_smallest_latency_ns() is None
     ri.close()
+
+
+@pytest.mark.parametrize("key,rec", [(None, 6), ("u32", 8)])
+def test_compact_storage_matches_oracle(monkeypatch, key, rec):
+    """srt_routing_info_build keeps the dense build's table as downloaded --
+    6-byte records (u16 latency units + f32 loss) for u16/f16-key closures, 8
+    bytes (u32 units + loss) for u32 keys -- and path() decodes them: every
+    pair equals the oracle's bits, the diagonal is the raw self-loop."""
+    from shadow_amd import _lib
+    if key:
+        monkeypatch.setenv("SRT_FW_KEY", key)
+    n = 600
+    src, dst, lat, loss = synth.complete_graph(n, 25)
+    ids = (np.arange(n) * 3 + 7).astype(np.uint32)
+    g = NetworkGraph.from_edges(n, src, dst, lat, loss, node_ids=ids)
+    nodes = np.arange(n, dtype=np.uint32)
+    ri = RoutingInfo.build(g, nodes, algo=_lib.SRT_ALGO_FW)
+    assert ri.record_bytes() == rec
+    L, P = ri.table()
+    elat, eloss = O.compute_shortest_paths(O.Graph(False, ids, src, dst, lat, loss), nodes)
+    assert np.array_equal(L, elat)
+    assert np.array_equal(P.view(np.uint32), eloss.view(np.uint32))
+    p = ri.path(int(ids[5]), int(ids[5]))
+    assert p.latency_ns == int(elat[5, 5])
+    ri.close()
+
+
+def test_self_loop_beyond_the_record_field():
+    """A non-complete graph whose key width comes from the eccentricity proof
+    (path latencies < 1024 units: f16 keys, 6-byte records) but with one
+    self-loop of 200 s (200,000 units, past the u16 field): the diagonal is the
+    raw self-loop in both the end-to-end srt_path table and the compact
+    RoutingInfo -- it travels beside the records, not in them."""
+    from shadow_amd import _lib
+    n = 300
+    src, dst, lat, loss = synth.dense_graph(n, 26, drop=0.4)
+    lat = lat.copy()
+    big = np.nonzero((src == dst) & (src == 17))[0][0]
+    lat[big] = np.uint64(200_000) * np.uint64(synth.MS)
+    g = NetworkGraph.from_edges(n, src, dst, lat, loss)
+    nodes = np.arange(n, dtype=np.uint32)
+    elat, eloss = O.compute_shortest_paths(O.Graph(False, np.arange(n), src, dst, lat, loss), nodes)
+    t = g.compute_shortest_paths(nodes, algo=_lib.SRT_ALGO_FW)
+    assert np.array_equal(t.latency_ns, elat)
+    assert np.array_equal(t.packet_loss.view(np.uint32), eloss.view(np.uint32))
+    ri = RoutingInfo.build(g, nodes, algo=_lib.SRT_ALGO_FW)
+    assert ri.record_bytes() == 6
+    assert ri.path(17, 17).latency_ns == 200_000 * synth.MS
+    L, P = ri.table()
+    assert np.array_equal(L, elat) and np.array_equal(P.view(np.uint32), eloss.view(np.uint32))
+    ri.close()
+
+
+def test_init_then_build():
+    """srt_init (HIP runtime, kernel code objects, pinned staging) and
+    srt_init_async ahead of a build: idempotent, and the build that follows
+    waits for a pending init and matches the oracle."""
+    import shadow_amd
+    shadow_amd.init_async(0)
+    shadow_amd.init(0)
+    shadow_amd.init(0)
+    shadow_amd.init_async(0)
+    n = 120
+    src, dst, lat, loss = synth.complete_graph(n, 27)
+    g = NetworkGraph.from_edges(n, src, dst, lat, loss)
+    nodes = np.arange(n, dtype=np.uint32)
+    ri = RoutingInfo.build(g, nodes)
+    L, P = ri.table()
+    elat, eloss = O.compute_shortest_paths(O.Graph(False, np.arange(n), src, dst, lat, loss), nodes)
+    assert np.array_equal(L, elat) and np.array_equal(P.view(np.uint32), eloss.view(np.uint32))
+    ri.close()
