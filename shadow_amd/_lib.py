@@ -105,6 +105,7 @@ SIGNATURES = {
     "srt_plan_bind_comm": (C.c_int, [_vp, _vp, _errp]),
     "srt_packet_batch": (C.c_int, [_vp, _vp, _vp, C.c_uint32, C.c_uint64, _vp, C.POINTER(SrtRound), _vp, _vp, _vp,
                                    _vp, _errp]),
+    "srt_packet_events_status": (C.c_int, [_vp, _errp]),
     "srt_packet_events": (C.c_int, [_vp, _vp, C.c_uint32, C.c_uint64, _vp, _vp, _vp, C.c_uint32, _vp, _vp, _vp,
                                     _vp, _errp]),
     "srt_routing_info_build": (C.c_int, [C.POINTER(SrtCsr), _u32p, C.c_uint32, C.c_int, C.POINTER(SrtOpts),

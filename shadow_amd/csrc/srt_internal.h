@@ -136,6 +136,15 @@ struct srt_plan {
     uint64_t *d_draws = nullptr;            // packet stage: one RNG draw per packet
     uint64_t draws_cap = 0;
     void *d_ev_scratch = nullptr;           // packet events: sort keys + rocPRIM temp
+    uint32_t *d_ev_bad = nullptr;    // srt_packet_events: bit 0 a destination out of range, bit 1 time span
+    struct EvCall {                  // the last srt_packet_events call (exact fallback)
+        const uint32_t *flags;
+        const uint64_t *deliver;
+        const uint32_t *dst;
+        uint32_t n_dst;
+        uint32_t *order, *dst_ptr;
+        uint32_t n;
+    } ev_last{};
     size_t ev_scratch_cap = 0;
 
     // host copies needed after create

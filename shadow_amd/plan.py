@@ -114,7 +114,7 @@ class RoutingPlan:
 
     # ---------------------------------------------------------------- packets
     def packet_events(self, host_ptr, flags, deliver, dst_host, n_dst_hosts: int, event_base, event_id, order,
-                      dst_ptr):
+                      dst_ptr, check: bool = True):
         """srt_packet_events (worker.rs:629-639 + event.rs:85-150) on torch CUDA
         tensors of this plan's device: host_ptr int32 [n_hosts+1], flags int32,
         deliver int64, dst_host int32 [n_pkts], event_base int64 [n_hosts]
@@ -131,6 +131,12 @@ class RoutingPlan:
             dst_host.data_ptr(), n_dst_hosts, event_base.data_ptr(), event_id.data_ptr(), order.data_ptr(),
             dst_ptr.data_ptr(), C.byref(err)), err)
         cur.wait_stream(ps)  # torch-side consumers see the outputs (device-side ordering)
+        if check:  # the asynchronous call's destination check (synchronises the plan's stream)
+            self.packet_events_status()
+
+    def packet_events_status(self):
+        err = _lib.SrtErr()
+        _lib.check(_lib.lib().srt_packet_events_status(self._h, C.byref(err)), err)
 
     def packet_batch(self, pkts, host_ptr, rng, round_end_ns: int, bootstrap_end_ns: int, sim_end_ns: int,
                      flags, deliver, counters=None, stats=None, sync: bool = True):
