@@ -369,15 +369,20 @@ def bench_gml(args, cfg, D):
             parse_s = time.perf_counter() - t1
             cpu = cpu_baseline(og, nodes, threads, 0, "C1", full=True)
             cpu["sample"] += f"; plus the oracle's GML parse ({parse_s:.2f} s, not in value)"
+        # the closure's key type, from a plan over the same graph (not timed)
+        from shadow_amd.plan import RoutingPlan
+        probe = RoutingPlan(NetworkGraph.parse(text), nodes, device=D.dev)
+        desc = probe.describe()
+        probe.close()
         out = {
             "metric": "APSP pairs/sec (routing-table build from GML text, 1k-node graph)",
             "value": D.world * n_nodes * n_nodes / per, "unit": "pairs/s", "n_gpus": D.world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": per * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u16",
+            "scaling": "weak", "vs_baseline": None, "dtype": desc.split(":")[1][:3] if desc.startswith("fw") else "u64",
             "data": "synthetic (seeded complete GML graph, latency U{1..300} ms, loss U[0,0.01])",
             "config": {"workload": f"C1: {n_nodes}-node complete undirected GML graph, use_shortest_path=true: "
                                    f"GML text -> srt_gml_parse -> srt_compute_shortest_paths -> host table",
-                       "nodes": n_nodes, "pairs": n_nodes * n_nodes, "gml_bytes": len(text),
+                       "nodes": n_nodes, "pairs": n_nodes * n_nodes, "gml_bytes": len(text), "plan": desc,
                        "parallelism": "replicas" if D.world > 1 else "single"},
             "roofline": None,
             "cpu_baseline": cpu,
