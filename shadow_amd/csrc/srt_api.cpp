@@ -780,7 +780,7 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         // tuning knob (measurement only): SRT_FW_STAGE=reg selects register staging
         if (const char *e = std::getenv("SRT_FW_STAGE")) p->fw_glds = std::strcmp(e, "reg") != 0;
         p->fw_f16 = f16 && p->fw_glds;
-        if (const char *e = std::getenv("SRT_FW_P1_TWO")) p->fw_p1_two = std::atoi(e) != 0;
+        if (const char *e = std::getenv("SRT_FW_P1")) p->fw_p1 = std::atoi(e);
         if (const char *e = std::getenv("SRT_FW_EMULATE_RANKS")) p->emulate_ranks = (uint32_t)std::atoi(e);
         if (p->emulate_ranks > 1) {
             // emulated rank 0 owns the first max(1, blocks / N) block-rows (fw_rounds_t)

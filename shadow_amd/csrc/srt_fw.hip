@@ -1237,28 +1237,120 @@ __global__ __launch_bounds__(16 * (B / P1R)) void fw_phase1_pk2_kernel(uint16_t 
     phase1_pk2_body<P1R, F16>(blk, Vp, blk, Vp);
 }
 
-// The symmetric sharded chain after the row all-gather, one launch: block 0
-// closes pivot block (k, k) straight from its slot (emu: from D) into D;
-// block 1 + c copies tile (k, c) of row k from rank (k + c) mod N's slot into
-// row (D's block-row k, or the emulation's scratch), except the pivot block.
-template <int P1R, bool F16>
-__global__ __launch_bounds__(16 * (B / P1R)) void unpack_p1_kernel(uint16_t *__restrict__ D, uint32_t Vp, uint32_t k,
-                                                                  uint32_t N, uint32_t S,
+// Phase 1 for u16 / f16 keys by min-plus squaring: M <- min(M, M (x) M)
+// until nothing changes (at most 7 times: a shortest path inside the block
+// has <= 127 hops and the t-th square covers every walk of <= 2^t).  A
+// fixpoint M holds walk lengths, stays <= the input and satisfies the
+// triangle inequality, so it is the closure -- the same keys as the 128
+// sequential FW steps, bit for bit.  Pivot blocks close in 2-4 squares
+// (few hops inside a block), each one a dense 128^3 min-plus product of one
+// workgroup out of LDS (M row-major in pairs, and pair-transposed for the A
+// operand), instead of 64 barrier-bound double steps: the critical path of
+// the symmetric sharded chain.  512 threads, each 4 rows x 8 columns (the
+// pk2 layout).  Reads src (row stride ss), writes dst (row stride ds).
+template <bool F16>
+__device__ __forceinline__ void closure_sq_body(const uint16_t *__restrict__ src, uint64_t ss,
+                                                uint16_t *__restrict__ dst, uint64_t ds) {
+    __shared__ __attribute__((aligned(16))) uint32_t M2[B][B / 2];       // M2[i][kp] = (M[i][2kp], M[i][2kp+1])
+    __shared__ __attribute__((aligned(16))) uint32_t MT2[B / 2][B + 4];  // MT2[kp][i] = M2[i][kp]
+    __builtin_amdgcn_s_setprio(3);  // critical path of the look-ahead chain
+    const int tid = threadIdx.x, tx = tid % 16, ty = tid / 16;
+    uint32_t acc[4][4];  // rows ty*4 + i, column pairs tx*4 + q
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(src + (ty * 4 + i) * ss + tx * 8);
+        acc[i][0] = v.x;
+        acc[i][1] = v.y;
+        acc[i][2] = v.z;
+        acc[i][3] = v.w;
+    }
+    auto stash = [&]() {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            *reinterpret_cast<uint4 *>(&M2[ty * 4 + i][tx * 4]) = make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            *reinterpret_cast<uint4 *>(&MT2[tx * 4 + q][ty * 4]) = make_uint4(acc[0][q], acc[1][q], acc[2][q], acc[3][q]);
+    };
+    stash();
+    __syncthreads();
+#pragma unroll 1
+    for (int it = 0; it < 7; ++it) {
+        uint32_t old[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) old[i][q] = acc[i][q];
+#pragma unroll 4
+        for (int kp = 0; kp < B / 2; ++kp) {
+            const uint4 a = *reinterpret_cast<const uint4 *>(&MT2[kp][ty * 4]);
+            const uint4 b0v = *reinterpret_cast<const uint4 *>(&M2[2 * kp][tx * 4]);
+            const uint4 b1v = *reinterpret_cast<const uint4 *>(&M2[2 * kp + 1][tx * 4]);
+            const u32x4 b0 = {b0v.x, b0v.y, b0v.z, b0v.w}, b1 = {b1v.x, b1v.y, b1v.z, b1v.w};
+            const uint32_t av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if constexpr (F16) {
+                    relax_pairs_f16(acc[i], av[i], b0, b1);
+                } else {
+                    relax_pairs16<0>(acc[i], av[i], b0);
+                    relax_pairs16<1>(acc[i], av[i], b1);
+                }
+            }
+        }
+        int changed = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) changed |= acc[i][q] != old[i][q];
+        if (!__syncthreads_or(changed)) break;  // also: every read of this square is done
+        stash();
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<uint4 *>(dst + (ty * 4 + i) * ds + tx * 8) =
+            make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+}
+
+template <bool F16>
+__global__ __launch_bounds__(512) void fw_phase1_sq_kernel(uint16_t *__restrict__ D, uint32_t Vp, uint32_t kb) {
+    uint16_t *blk = D + (uint64_t)kb * B * Vp + (uint64_t)kb * B;
+    closure_sq_body<F16>(blk, Vp, blk, Vp);
+}
+
+// The symmetric sharded chain after the row all-gather, one launch: rows
+// [p0, p0 + np) (one round, or a group's) arrive; block 0 closes pivot block
+// (p0, p0) straight from its slot (emu: from D) into D when p1 is set; block
+// 1 + (r - p0) * nblk + c copies tile (r, c) from rank (r + c) mod N's slot
+// (np * S tiles a rank: index (r - p0) * S + c / N) into rows (row r at
+// rows + (r - p0) * B * Vp: D's block-rows, or the emulation's scratch),
+// except the pivot block p1 closes.
+template <int P1R, bool F16, bool SQ = false>
+__global__ __launch_bounds__(16 * (B / P1R)) void unpack_p1_kernel(uint16_t *__restrict__ D, uint32_t Vp, uint32_t p0,
+                                                                  uint32_t np, uint32_t N, uint32_t S,
                                                                   const uint16_t *__restrict__ slots,
-                                                                  uint16_t *__restrict__ row, bool emu) {
-    const uint64_t diag = (uint64_t)k * B * Vp + (uint64_t)k * B;
+                                                                  uint16_t *__restrict__ rows, bool emu, bool p1) {
+    const uint64_t diag = (uint64_t)p0 * B * Vp + (uint64_t)p0 * B;
     if (blockIdx.x == 0) {
-        const uint16_t *src = emu ? D + diag : slots + ((uint64_t)((2 * k) % N) * S + k / N) * B * B;
-        phase1_pk2_body<P1R, F16>(src, emu ? Vp : B, D + diag, Vp);
+        if (!p1) return;
+        const uint16_t *src = emu ? D + diag : slots + ((uint64_t)((2 * p0) % N) * np * S + p0 / N) * B * B;
+        if constexpr (SQ) {
+            static_assert(P1R == 4, "the squaring body runs 512 threads");
+            closure_sq_body<F16>(src, emu ? Vp : B, D + diag, Vp);
+        } else {
+            phase1_pk2_body<P1R, F16>(src, emu ? Vp : B, D + diag, Vp);
+        }
         return;
     }
-    const uint32_t c = blockIdx.x - 1;
-    if (c == k && !emu) return;
-    const uint16_t *src = slots + ((uint64_t)((k + c) % N) * S + c / N) * B * B;
-    uint16_t *dst = row + (uint64_t)c * B;
+    const uint32_t nblk = Vp / B, t = blockIdx.x - 1, r = p0 + t / nblk, c = t % nblk;
+    if (p1 && r == p0 && c == p0 && !emu) return;
+    const uint16_t *src = slots + ((uint64_t)((r + c) % N) * np * S + (uint64_t)(r - p0) * S + c / N) * B * B;
+    uint16_t *dst = rows + (uint64_t)(r - p0) * B * Vp + (uint64_t)c * B;
     for (uint32_t e = threadIdx.x; e < B * B / 8; e += blockDim.x) {
-        const uint32_t r = e / (B / 8), cc = (e % (B / 8)) * 8;
-        *reinterpret_cast<u32x4 *>(dst + (uint64_t)r * Vp + cc) = *reinterpret_cast<const u32x4 *>(src + r * B + cc);
+        const uint32_t rr = e / (B / 8), cc = (e % (B / 8)) * 8;
+        *reinterpret_cast<u32x4 *>(dst + (uint64_t)rr * Vp + cc) =
+            *reinterpret_cast<const u32x4 *>(src + rr * B + cc);
     }
 }
 
@@ -1357,14 +1449,14 @@ __global__ __launch_bounds__(NT3, 2) void minplus_u16_kernel(uint16_t *__restric
             return;  // workgroup-uniform, before any barrier
     } else if constexpr (SYM == 3) {
         // tile list (symmetric sharded schedule): the list's device address in
-        // r2.r.lo / r2.r.hi, entries (i << 16) | j; tiles in row or column
-        // r1.r.x0 or r1.r.x1 (this round's pivot and look-ahead) are skipped;
-        // results are also stored mirrored (below)
+        // r2.r.lo / r2.r.hi, entries (i << 16) | j; tiles in a row or column of
+        // [r1.r.x0, r1.r.x1) (this group's pivots and the look-ahead group's)
+        // are skipped; results are also stored mirrored (below)
         const uint32_t *tl = reinterpret_cast<const uint32_t *>(((uint64_t)r2.r.hi << 32) | r2.r.lo);
         const uint32_t e = tl[blockIdx.x];
         bi = e >> 16;
         bj = e & 0xffffu;
-        if (bi == r1.r.x0 || bj == r1.r.x0 || bi == r1.r.x1 || bj == r1.r.x1) return;
+        if (bi - r1.r.x0 < r1.r.x1 - r1.r.x0 || bj - r1.r.x0 < r1.r.x1 - r1.r.x0) return;
     } else {
         tile_of(blockIdx.x, r1, r2, ng, bi, bj);
     }
@@ -1651,14 +1743,24 @@ __global__ __launch_bounds__(256) void minplus_small_kernel(K *__restrict__ D, u
 // rows or columns r1.r.x0 / r1.r.x1 skipped), mirrored; MODE 1: the rect r1,
 // mirrored; MODE 0: the rects r1 then r2, not mirrored (the look-ahead chain
 // of one GPU at chain-bound sizes and of the row-sharded schedule).  F16: f16
-// integer keys (see relax_pairs_f16).  slot (MODE 2, the symmetric sharded
-// cross): every result tile in row or column prow also goes, in row-prow
-// orientation, to this rank's all-gather slot -- tile (prow, c) at slot index
-// c / N (the pack of fw_rounds_sym_sharded, fused).
+// integer keys (see relax_pairs_f16).  nr rounds (k from kb * B to (kb + nr)
+// * B: a grouped cross).  pk.slot (MODE 2, the symmetric sharded cross):
+// every result tile in a row or column r of [pk.p0, pk.p0 + pk.np) also goes,
+// in row-r orientation, to this rank's all-gather slot -- tile (r, c) at slot
+// index (r - p0) * S + c / N (the pack of fw_rounds_sym_sharded, fused).
+struct PackSpec {
+    uint16_t *slot;
+    uint32_t p0, np, N, S;
+};
 template <int TAG, int MODE, bool F16>
 __global__ __launch_bounds__(256) void minplus_q16_kernel(uint16_t *__restrict__ D, uint32_t Vp, uint32_t kb, Rect r1,
-                                                          Rect r2, uint16_t *__restrict__ slot, uint32_t prow,
-                                                          uint32_t N) {
+                                                          Rect r2, uint32_t nr, PackSpec pk) {
+    uint16_t *__restrict__ slot = pk.slot;
+    const uint32_t N = pk.N;
+    auto in_pack = [&](uint32_t b) { return b - pk.p0 < pk.np; };
+    auto slot_tile = [&](uint32_t r, uint32_t c) {
+        return slot + ((uint64_t)(r - pk.p0) * pk.S + c / N) * B * B;
+    };
     constexpr int QK = 32;
     __shared__ uint16_t As[2][SQ][QK + 2];  // [row][k]
     __shared__ us2 Bs[2][QK][SQ / 2];        // [k][column pair]
@@ -1671,18 +1773,19 @@ __global__ __launch_bounds__(256) void minplus_q16_kernel(uint16_t *__restrict__
         const uint32_t e = tl[t];
         bi = e >> 16;
         bj = e & 0xffffu;
-        if (bi == r1.r.x0 || bj == r1.r.x0 || bi == r1.r.x1 || bj == r1.r.x1) {
-            // a skipped tile of row / column prow is current already: into the slot as it is
-            if (slot && (bi == prow || bj == prow)) {
+        if (bi - r1.r.x0 < r1.r.x1 - r1.r.x0 || bj - r1.r.x0 < r1.r.x1 - r1.r.x0) {  // skipped range [x0, x1)
+            // a skipped tile of a packed row / column is current already: into the slot as it is
+            if (slot && (in_pack(bi) || in_pack(bj))) {
                 const uint64_t si0 = (uint64_t)bi * B + (q >> 1) * SQ, sj0 = (uint64_t)bj * B + (q & 1) * SQ;
                 const int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
-                if (bi == prow) {
+                if (in_pack(bi)) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
-                        *reinterpret_cast<uint2 *>(slot + (uint64_t)(bj / N) * B * B +
-                                                   ((q >> 1) * SQ + ty * 4 + i) * B + (q & 1) * SQ + tx * 4) =
+                        *reinterpret_cast<uint2 *>(slot_tile(bi, bj) + ((q >> 1) * SQ + ty * 4 + i) * B +
+                                                   (q & 1) * SQ + tx * 4) =
                             *reinterpret_cast<const uint2 *>(D + (si0 + ty * 4 + i) * Vp + sj0 + tx * 4);
-                } else {
+                }
+                if (in_pack(bj) && bi != bj) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1695,8 +1798,8 @@ __global__ __launch_bounds__(256) void minplus_q16_kernel(uint16_t *__restrict__
                         uint2 v;
                         v.x = (uint32_t)T[r][tx * 4] | ((uint32_t)T[r][tx * 4 + 1] << 16);
                         v.y = (uint32_t)T[r][tx * 4 + 2] | ((uint32_t)T[r][tx * 4 + 3] << 16);
-                        *reinterpret_cast<uint2 *>(slot + (uint64_t)(bi / N) * B * B + ((q & 1) * SQ + r) * B +
-                                                   (q >> 1) * SQ + tx * 4) = v;
+                        *reinterpret_cast<uint2 *>(slot_tile(bj, bi) + ((q & 1) * SQ + r) * B + (q >> 1) * SQ +
+                                                   tx * 4) = v;
                     }
                 }
             }
@@ -1716,6 +1819,7 @@ __global__ __launch_bounds__(256) void minplus_q16_kernel(uint16_t *__restrict__
     const uint64_t i0 = (uint64_t)bi * B + (q >> 1) * SQ, j0 = (uint64_t)bj * B + (q & 1) * SQ;
     const uint64_t k0 = (uint64_t)kb * B;
     const int tid = threadIdx.x, tx = tid % 16, ty = tid / 16;
+    const int NCH = (int)nr * (B / 32);  // K chunks of 32 over the nr rounds
     us2 acc[4][2];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1743,7 +1847,6 @@ __global__ __launch_bounds__(256) void minplus_q16_kernel(uint16_t *__restrict__
     fetch(0);
     stash(0);
     __syncthreads();
-    constexpr int NCH = B / QK;
 #pragma unroll 1
     for (int ch = 0; ch < NCH; ++ch) {
         const int cur = ch & 1;
@@ -1768,10 +1871,10 @@ __global__ __launch_bounds__(256) void minplus_q16_kernel(uint16_t *__restrict__
         v.x = __builtin_bit_cast(uint32_t, acc[i][0]);
         v.y = __builtin_bit_cast(uint32_t, acc[i][1]);
         *reinterpret_cast<uint2 *>(D + (i0 + ty * 4 + i) * Vp + j0 + tx * 4) = v;
-        // the slot takes the quarter as computed when it is row prow's
-        if (MODE == 2 && slot && bi == prow)
-            *reinterpret_cast<uint2 *>(slot + (uint64_t)(bj / N) * B * B + ((q >> 1) * SQ + ty * 4 + i) * B +
-                                       (q & 1) * SQ + tx * 4) = v;
+        // the slot takes the quarter as computed when it is a packed row's
+        if (MODE == 2 && slot && in_pack(bi))
+            *reinterpret_cast<uint2 *>(slot_tile(bi, bj) + ((q >> 1) * SQ + ty * 4 + i) * B + (q & 1) * SQ +
+                                       tx * 4) = v;
     }
     if (MODE != 0 && bi != bj) {
 #pragma unroll
@@ -1786,10 +1889,10 @@ __global__ __launch_bounds__(256) void minplus_q16_kernel(uint16_t *__restrict__
             v.x = (uint32_t)T[r][tx * 4] | ((uint32_t)T[r][tx * 4 + 1] << 16);
             v.y = (uint32_t)T[r][tx * 4 + 2] | ((uint32_t)T[r][tx * 4 + 3] << 16);
             *reinterpret_cast<uint2 *>(D + (j0 + r) * Vp + i0 + tx * 4) = v;
-            // ... or transposed, when it is column prow's (tile (bi, prow) = mirror (prow, bi))
-            if (MODE == 2 && slot && bj == prow)
-                *reinterpret_cast<uint2 *>(slot + (uint64_t)(bi / N) * B * B + ((q & 1) * SQ + r) * B +
-                                           (q >> 1) * SQ + tx * 4) = v;
+            // ... or transposed, when it is a packed column's (tile (bi, r) = mirror (r, bi))
+            if (MODE == 2 && slot && in_pack(bj))
+                *reinterpret_cast<uint2 *>(slot_tile(bj, bi) + ((q & 1) * SQ + r) * B + (q >> 1) * SQ + tx * 4) =
+                    v;
         }
     }
 }
@@ -1890,10 +1993,15 @@ auto p1k2(bool f16) {
 
 // two: u16 / f16 keys, two FW steps per barrier (fw_phase1_pk2_kernel)
 template <typename K>
-void launch_p1(int rows, hipStream_t s, K *D, uint32_t Vp, uint32_t kb, bool f16 = false, bool two = false) {
+void launch_p1(int rows, hipStream_t s, K *D, uint32_t Vp, uint32_t kb, bool f16 = false, int mode = 0) {
     if constexpr (sizeof(K) == 2) {
         uint16_t *D16 = reinterpret_cast<uint16_t *>(D);
-        if (two) {
+        if (mode == 2) {
+            hipLaunchKernelGGL(f16 ? &fw_phase1_sq_kernel<true> : &fw_phase1_sq_kernel<false>, dim3(1), dim3(512), 0,
+                               s, D16, Vp, kb);
+            return;
+        }
+        if (mode == 1) {
             if (rows == 2)
                 hipLaunchKernelGGL(p1k2<2>(f16), dim3(1), dim3(16 * (B / 2)), 0, s, D16, Vp, kb);
             else if (rows == 4)
@@ -1925,7 +2033,8 @@ void launch_tiles(srt_plan *p, hipStream_t s, uint32_t kb, const Rect &r1, const
     if (TAG != 0 && p->fw_small_chain) {  // look-ahead chain: quarter tiles, lower latency
         if constexpr (sizeof(K) == 2)
             hipLaunchKernelGGL((q16k<TAG, 0>(p->fw_f16)), dim3(4 * n), dim3(256), 0, s,
-                               reinterpret_cast<uint16_t *>(p->d_D), p->Vp, kb, r1, r2, (uint16_t *)nullptr, 0u, 1u);
+                               reinterpret_cast<uint16_t *>(p->d_D), p->Vp, kb, r1, r2, 1u,
+                               PackSpec{nullptr, 0u, 0u, 1u, 1u});
         else
             hipLaunchKernelGGL((minplus_small_kernel<K, TAG>), dim3(4 * n), dim3(256), 0, s,
                                reinterpret_cast<K *>(p->d_D), p->Vp, kb, r1, r2);
@@ -2006,9 +2115,22 @@ srt_status fw_rounds_group_sharded_t(srt_plan *p, int p1r, uint32_t g, uint32_t 
 // one all-gather of ceil(nblk/N) tiles a round instead of a broadcast of
 // nblk.  The prologue needs no exchange: every rank starts from the same
 // full initial D.
-srt_status sym_sharded_setup(srt_plan *p, uint32_t N, uint32_t r, srt_err *err) {
-    if (p->d_tl_all) return SRT_OK;
-    const uint32_t nblk = p->Vp / B;
+// Groups of g rounds (fw_rounds_sym_grouped; g = 1: fw_rounds_sym_sharded):
+// tl_cross_off[a] .. [a + 1] = the own tiles with a row or column in group a,
+// d_rowslots = N slots of g * ceil(nblk / N) tiles.
+srt_status sym_sharded_setup(srt_plan *p, uint32_t N, uint32_t r, uint32_t g, srt_err *err) {
+    if (p->d_tl_all && p->sym_g == g) return SRT_OK;
+    if (p->d_tl_all) {  // another group size: rebuild
+        hipFree(p->d_tl_all);
+        hipFree(p->d_tl_cnt);
+        hipFree(p->d_tl_cross);
+        hipFree(p->d_rowslots);
+        hipFree(p->d_fbuf);
+        p->d_tl_all = p->d_tl_cnt = p->d_tl_cross = nullptr;
+        p->d_rowslots = p->d_fbuf = nullptr;
+    }
+    p->sym_g = g;
+    const uint32_t nblk = p->Vp / B, ngrp = (nblk + g - 1) / g;
     std::vector<std::vector<uint32_t>> lists(N);
     for (uint32_t i = 0; i < nblk; ++i)
         for (uint32_t j = i; j < nblk; ++j) lists[(i + j) % N].push_back((i << 16) | j);
@@ -2020,21 +2142,22 @@ srt_status sym_sharded_setup(srt_plan *p, uint32_t N, uint32_t r, srt_err *err) 
         std::copy(lists[q].begin(), lists[q].end(), all.begin() + (size_t)q * tmax);
     }
     std::vector<uint32_t> cross;
-    p->tl_cross_off.assign(nblk + 1, 0);
-    for (uint32_t k = 0; k < nblk; ++k) {
-        p->tl_cross_off[k] = (uint32_t)cross.size();
+    p->tl_cross_off.assign(ngrp + 1, 0);
+    for (uint32_t a = 0; a < ngrp; ++a) {
+        p->tl_cross_off[a] = (uint32_t)cross.size();
         for (uint32_t e : lists[r])
-            if ((e >> 16) == k || (e & 0xffffu) == k) cross.push_back(e);
+            if ((e >> 16) / g == a || (e & 0xffffu) / g == a) cross.push_back(e);
     }
-    p->tl_cross_off[nblk] = (uint32_t)cross.size();
+    p->tl_cross_off[ngrp] = (uint32_t)cross.size();
     p->tl_max = tmax;
     p->tl_own = cnt[r];
     const uint32_t S = (nblk + N - 1) / N;
     hipError_t e = hipMalloc(&p->d_tl_all, all.size() * 4);
     if (e == hipSuccess) e = hipMalloc(&p->d_tl_cnt, N * 4);
     if (e == hipSuccess) e = hipMalloc(&p->d_tl_cross, std::max<size_t>(cross.size(), 1) * 4);
-    if (e == hipSuccess) e = hipMalloc(&p->d_rowslots, (size_t)N * S * B * B * 2);
-    if (e == hipSuccess) e = hipMalloc(&p->d_fbuf, (size_t)N * tmax * B * B * 2);
+    if (e == hipSuccess) e = hipMalloc(&p->d_rowslots, (size_t)N * g * S * B * B * 2);
+    // the final exchange; also the emulation's scratch rows (g block-rows)
+    if (e == hipSuccess) e = hipMalloc(&p->d_fbuf, std::max<size_t>((size_t)N * tmax, (size_t)g * nblk) * B * B * 2);
     if (e == hipSuccess) e = hipMemcpy(p->d_tl_all, all.data(), all.size() * 4, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->d_tl_cnt, cnt.data(), N * 4, hipMemcpyHostToDevice);
     if (e == hipSuccess && !cross.empty())
@@ -2049,16 +2172,29 @@ srt_status sym_sharded_setup(srt_plan *p, uint32_t N, uint32_t r, srt_err *err) 
     return SRT_OK;
 }
 
-// a list launch of the SYM == 3 rest kernel: n entries at tl, skipping rows /
-// columns a and b
+// the fused row unpack + phase 1 kernel for a phase-1 form: the squaring body
+// (512 threads) or the two-step body at p1r rows a thread
+struct UnpackP1 {
+    void (*fn)(uint16_t *, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, const uint16_t *, uint16_t *, bool, bool);
+    uint32_t threads;
+};
+UnpackP1 unpack_p1_for(int p1r, bool f16, bool sq) {
+    if (sq) return {f16 ? &unpack_p1_kernel<4, true, true> : &unpack_p1_kernel<4, false, true>, 512u};
+    if (p1r == 2) return {f16 ? &unpack_p1_kernel<2, true> : &unpack_p1_kernel<2, false>, 16u * (B / 2)};
+    if (p1r == 4) return {f16 ? &unpack_p1_kernel<4, true> : &unpack_p1_kernel<4, false>, 16u * (B / 4)};
+    return {f16 ? &unpack_p1_kernel<8, true> : &unpack_p1_kernel<8, false>, 16u * (B / 8)};
+}
+
+// a list launch of the SYM == 3 rest kernel: n entries at tl, ng rounds from
+// kb, skipping tiles in a row or column of [a, b)
 void launch_list16(hipStream_t s, uint16_t *D, uint32_t Vp, uint32_t kb, const uint32_t *tl, uint32_t n, uint32_t a,
-                   uint32_t b, bool f16) {
+                   uint32_t b, bool f16, uint32_t ng = 1) {
     if (!n) return;
     Span skip{0, 0, a, b, 0};
     const uint64_t addr = reinterpret_cast<uint64_t>(tl);
     Span ptr{(uint32_t)addr, (uint32_t)(addr >> 32), NONE, NONE, 0};
     hipLaunchKernelGGL((u16k<0, 3>(f16)), dim3(n), dim3(NT3), 0, s, D, Vp, kb, Rect{skip, skip},
-                       Rect{ptr, ptr}, 1u);
+                       Rect{ptr, ptr}, ng);
 }
 
 // Emulation (measurement only, SRT_FW_EMULATE_RANKS=N, one GPU, D already
@@ -2067,16 +2203,17 @@ void launch_list16(hipStream_t s, uint16_t *D, uint32_t Vp, uint32_t kb, const u
 // goes to scratch (the other ranks' slots hold no real rows) and the final
 // unpack writes rank 0's tiles N times (every rank's volume), so D stays the
 // closure for the loss tail that follows.
-srt_status fw_rounds_sym_sharded(srt_plan *p, int p1r, srt_err *err) {
-    const bool emu = p->comm == nullptr;
-    const uint32_t N = emu ? p->emulate_ranks : (uint32_t)p->comm->nranks, r = emu ? 0u : (uint32_t)p->comm->rank;
-    if (srt_status st = sym_sharded_setup(p, N, r, err); st != SRT_OK) return st;
-    uint16_t *D = reinterpret_cast<uint16_t *>(p->d_D);
-    const uint32_t nblk = p->Vp / B;
-    const uint32_t S_t = (nblk + N - 1) / N;
+// the all-gather of the symmetric sharded schedules: RCCL in place, or the
+// emulation's stand-in wait (latency + bytes / bandwidth, see below)
+struct SymGather {
+    srt_plan *p;
+    srt_err *err;
+    bool emu;
+    uint32_t N;
     long long ag_lat = 0;
     double ag_per_byte = 0.0;
-    if (emu) {
+    SymGather(srt_plan *p_, uint32_t N_, srt_err *e) : p(p_), err(e), emu(p_->comm == nullptr), N(N_) {
+        if (!emu) return;
         int khz = 100000;
         (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, p->device);
         const double lat_us = std::getenv("SRT_FW_EMU_AG_US") ? std::atof(std::getenv("SRT_FW_EMU_AG_US")) : 25.0;
@@ -2084,12 +2221,50 @@ srt_status fw_rounds_sym_sharded(srt_plan *p, int p1r, srt_err *err) {
         ag_lat = (long long)(lat_us * khz / 1000.0);
         ag_per_byte = (double)(N - 1) / (gbps * 1e3) * khz / 1000.0;  // ticks per byte a rank sends
     }
-    auto gather = [&](void *buf, size_t bytes_per_rank, hipStream_t s) -> srt_status {
+    srt_status operator()(void *buf, size_t bytes_per_rank, hipStream_t s) const {
         if (!emu) return comm_allgather_inplace(p->comm, buf, bytes_per_rank, s, err);
         hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, s, ag_lat + (long long)(bytes_per_rank * ag_per_byte));
         return SRT_OK;
-    };
-    hipStream_t M = p->stream, S = p->side_stream, C = p->comm_stream;
+    }
+};
+
+// the final exchange of the symmetric sharded schedules: every rank's tiles,
+// written with their mirrors (after M's last rest)
+srt_status sym_final_exchange(srt_plan *p, uint32_t N, uint32_t r, const SymGather &gather) {
+    uint16_t *D = reinterpret_cast<uint16_t *>(p->d_D);
+    hipStream_t M = p->stream, C = p->comm_stream;
+    const uint32_t *own = p->d_tl_all + (size_t)r * p->tl_max;
+    if (p->tl_own)
+        hipLaunchKernelGGL(pack_list16_kernel, dim3(p->tl_own), dim3(256), 0, M, D, p->Vp, own,
+                           p->d_fbuf + (size_t)r * p->tl_max * B * B);
+    hipEventRecord(p->ev_row, M);
+    hipStreamWaitEvent(C, p->ev_row, 0);
+    if (srt_status st = gather(p->d_fbuf, (size_t)p->tl_max * B * B * 2, C); st != SRT_OK) return st;
+    hipEventRecord(p->ev_bcast, C);
+    hipStreamWaitEvent(M, p->ev_bcast, 0);
+    hipLaunchKernelGGL(unpack_list16_kernel, dim3(p->tl_max, N), dim3(256), 0, M, D, p->Vp,
+                       (const uint32_t *)p->d_tl_all, (const uint32_t *)p->d_tl_cnt, p->tl_max,
+                       (const uint16_t *)p->d_fbuf, gather.emu ? 1u : 0u);
+    return SRT_OK;
+}
+
+srt_status fw_rounds_sym_grouped(srt_plan *p, int p1r, uint32_t g, srt_err *err);
+
+srt_status fw_rounds_sym_sharded(srt_plan *p, int p1r, srt_err *err) {
+    const bool emu = p->comm == nullptr;
+    const uint32_t N = emu ? p->emulate_ranks : (uint32_t)p->comm->nranks, r = emu ? 0u : (uint32_t)p->comm->rank;
+    const uint32_t nblk = p->Vp / B;
+    {
+        uint32_t g = p->fw_sym_group;
+        if (const char *e = std::getenv("SRT_FW_SYM_GROUP")) g = (uint32_t)std::max(1, std::atoi(e));
+        g = std::min<uint32_t>(g, std::max<uint32_t>(1, nblk / 2));
+        if (g > 1 && (p1r == 2 || p1r == 4 || p1r == 8)) return fw_rounds_sym_grouped(p, p1r, g, err);
+    }
+    if (srt_status st = sym_sharded_setup(p, N, r, 1u, err); st != SRT_OK) return st;
+    uint16_t *D = reinterpret_cast<uint16_t *>(p->d_D);
+    const uint32_t S_t = (nblk + N - 1) / N;
+    const SymGather gather(p, N, err);
+    hipStream_t M = p->stream, S = p->side_stream;
     const uint32_t *own = p->d_tl_all + (size_t)r * p->tl_max;
     uint16_t *myslot = p->d_rowslots + (size_t)r * S_t * B * B;
     p->p3_launches = 0;
@@ -2112,18 +2287,18 @@ srt_status fw_rounds_sym_sharded(srt_plan *p, int p1r, srt_err *err) {
     if (const char *e = std::getenv("SRT_FW_FUSE_PACK")) fuse_pack = std::atoi(e) != 0;
     // ... and the unpack of row k1 runs beside p1(k1) in one launch (two-step
     // phase 1; knob SRT_FW_FUSE_P1=0: separate launches)
-    bool fuse_p1 = p->fw_p1_two;
+    bool fuse_p1 = p->fw_p1 >= 1;
     if (const char *e = std::getenv("SRT_FW_FUSE_P1")) fuse_p1 = fuse_p1 && std::atoi(e) != 0;
     auto p2row_mirror = [&](hipStream_t s, uint32_t k) {
         const Rect row{make_span(k, k + 1), make_span(0, nblk, k)};
         if (small)
             hipLaunchKernelGGL((q16k<1, 1>(p->fw_f16)), dim3(4 * row.c.n), dim3(256), 0, s, D, p->Vp, k, row,
-                               Rect{make_span(0, 0), make_span(0, 0)}, (uint16_t *)nullptr, 0u, 1u);
+                               Rect{make_span(0, 0), make_span(0, 0)}, 1u, PackSpec{nullptr, 0u, 0u, 1u, 1u});
         else
             launch_mirror<uint16_t, 1>(p, s, k, row);
     };
     // prologue: pivot 0 on every rank (the same full initial D)
-    launch_p1<uint16_t>(p1r, M, D, p->Vp, 0u, p->fw_f16, p->fw_p1_two);
+    launch_p1<uint16_t>(p1r, M, D, p->Vp, 0u, p->fw_f16, p->fw_p1);
     p2row_mirror(M, 0);
     hipEventRecord(p->ev_cross, M);
     hipEvent_t rest_done = p->ev_cross;
@@ -2133,7 +2308,7 @@ srt_status fw_rounds_sym_sharded(srt_plan *p, int p1r, srt_err *err) {
         if (nxt) hipStreamWaitEvent(S, rest_done, 0);
         if (kb) hipStreamWaitEvent(M, p->ev_pivot, 0);
         hipEventRecord(p->ev[2 * p->p3_launches], M);
-        launch_list16(M, D, p->Vp, kb, own, p->tl_own, kb, nxt ? k1 : NONE, p->fw_f16);
+        launch_list16(M, D, p->Vp, kb, own, p->tl_own, kb, nxt ? k1 + 1 : k1, p->fw_f16);
         rest_done = p->ev[2 * p->p3_launches + 1];
         hipEventRecord(rest_done, M);
         p->p3_launches++;
@@ -2143,16 +2318,17 @@ srt_status fw_rounds_sym_sharded(srt_plan *p, int p1r, srt_err *err) {
         const uint32_t *cl = p->d_tl_cross + p->tl_cross_off[k1];
         const uint32_t cn = p->tl_cross_off[k1 + 1] - p->tl_cross_off[k1];
         if (small && cn) {
-            Span skip{0, 0, kb, NONE, 0};
+            Span skip{0, 0, kb, kb + 1, 0};
             const uint64_t addr = reinterpret_cast<uint64_t>(cl);
             Span ptr{(uint32_t)addr, (uint32_t)(addr >> 32), NONE, NONE, 0};
             // cross(kb) and the pack of row k1 into this rank's slot, one launch
             hipLaunchKernelGGL((q16k<4, 2>(p->fw_f16)), dim3(4 * cn), dim3(256), 0, S, D, p->Vp, kb,
-                               Rect{skip, skip}, Rect{ptr, ptr}, fuse_pack ? myslot : (uint16_t *)nullptr, k1, N);
+                               Rect{skip, skip}, Rect{ptr, ptr}, 1u,
+                               PackSpec{fuse_pack ? myslot : (uint16_t *)nullptr, k1, 1u, N, S_t});
             if (!fuse_pack)
                 hipLaunchKernelGGL(pack_row16_kernel, dim3(cn), dim3(256), 0, S, D, p->Vp, cl, k1, N, myslot);
         } else {
-            launch_list16(S, D, p->Vp, kb, cl, cn, kb, NONE, p->fw_f16);
+            launch_list16(S, D, p->Vp, kb, cl, cn, kb, kb + 1, p->fw_f16);
             if (cn) hipLaunchKernelGGL(pack_row16_kernel, dim3(cn), dim3(256), 0, S, D, p->Vp, cl, k1, N, myslot);
         }
         // the row all-gather on S itself: nothing else waits on S meanwhile,
@@ -2163,32 +2339,121 @@ srt_status fw_rounds_sym_sharded(srt_plan *p, int p1r, srt_err *err) {
         uint16_t *rowdst = emu ? p->d_fbuf : D + (uint64_t)k1 * B * p->Vp;
         if (fuse_p1 && (p1r == 2 || p1r == 4 || p1r == 8)) {
             // unpack of row k1 and p1(k1) from its slot, one launch
-            auto kern = p1r == 2 ? (p->fw_f16 ? &unpack_p1_kernel<2, true> : &unpack_p1_kernel<2, false>)
-                        : p1r == 4 ? (p->fw_f16 ? &unpack_p1_kernel<4, true> : &unpack_p1_kernel<4, false>)
-                                   : (p->fw_f16 ? &unpack_p1_kernel<8, true> : &unpack_p1_kernel<8, false>);
-            hipLaunchKernelGGL(kern, dim3(nblk + 1), dim3(16 * (B / p1r)), 0, S, D, p->Vp, k1, N, S_t,
-                               (const uint16_t *)p->d_rowslots, rowdst, emu);
+            const UnpackP1 u = unpack_p1_for(p1r, p->fw_f16, p->fw_p1 == 2);
+            hipLaunchKernelGGL(u.fn, dim3(nblk + 1), dim3(u.threads), 0, S, D, p->Vp, k1, 1u, N, S_t,
+                               (const uint16_t *)p->d_rowslots, rowdst, emu, true);
         } else {
             hipLaunchKernelGGL(unpack_row16_kernel, dim3(nblk), dim3(256), 0, S, rowdst, p->Vp, k1, N, S_t,
                                (const uint16_t *)p->d_rowslots);
-            launch_p1<uint16_t>(p1r, S, D, p->Vp, k1, p->fw_f16, p->fw_p1_two);
+            launch_p1<uint16_t>(p1r, S, D, p->Vp, k1, p->fw_f16, p->fw_p1);
         }
         p2row_mirror(S, k1);
         hipEventRecord(p->ev_pivot, S);
     }
-    // final exchange: every rank's tiles, written with their mirrors
-    if (p->tl_own)
-        hipLaunchKernelGGL(pack_list16_kernel, dim3(p->tl_own), dim3(256), 0, M, D, p->Vp, own,
-                           p->d_fbuf + (size_t)r * p->tl_max * B * B);
-    hipEventRecord(p->ev_row, M);
-    hipStreamWaitEvent(C, p->ev_row, 0);
-    if ((st = gather(p->d_fbuf, (size_t)p->tl_max * B * B * 2, C)) != SRT_OK) return st;
-    hipEventRecord(p->ev_bcast, C);
-    hipStreamWaitEvent(M, p->ev_bcast, 0);
-    hipLaunchKernelGGL(unpack_list16_kernel, dim3(p->tl_max, N), dim3(256), 0, M, D, p->Vp,
-                       (const uint32_t *)p->d_tl_all, (const uint32_t *)p->d_tl_cnt, p->tl_max,
-                       (const uint16_t *)p->d_fbuf, emu ? 1u : 0u);
-    return SRT_OK;
+    return sym_final_exchange(p, N, r, gather);
+}
+
+// The symmetric sharded schedule in groups of g rounds: one row all-gather
+// per group instead of per round.  Group a = blocks [a g, a g + g) (the last
+// one shorter); A = group a, Bn = group a + 1.  Invariant at group a: the
+// panel of A (its block-rows and, mirrored, block-columns) is closed through
+// A's last round on every rank; own tiles elsewhere are current through the
+// rounds before A.  Per group:
+//   M: rest(A) = own tiles outside the rows / columns of A and Bn, the |A|
+//      rounds of A in one pass (they read only A's closed panel);
+//   S: cross(A) = own tiles in a row or column of Bn (outside A's), the |A|
+//      rounds of A, each result of rows Bn also packed into this rank's slot
+//      (g ceil(nblk / N) tiles); the all-gather; the unpack of rows Bn and
+//      p1(Bn.lo) in one launch; then Bn's panel closed round by round on every
+//      rank: p1(q), p2row(q) with its mirror, and round q on the other rows
+//      of Bn (mirrored).
+// rest(A) and the chain of Bn touch disjoint tiles, as in the one-round
+// schedule; S waits for rest(A - 1) (the rows of Bn took A - 1's rounds there)
+// and M for Bn's panel.  Relaxations as the one-round schedule, g times fewer
+// all-gathers, p1 / p2row / cross launches, and stream hops.
+srt_status fw_rounds_sym_grouped(srt_plan *p, int p1r, uint32_t g, srt_err *err) {
+    const bool emu = p->comm == nullptr;
+    const uint32_t N = emu ? p->emulate_ranks : (uint32_t)p->comm->nranks, r = emu ? 0u : (uint32_t)p->comm->rank;
+    if (srt_status st = sym_sharded_setup(p, N, r, g, err); st != SRT_OK) return st;
+    uint16_t *D = reinterpret_cast<uint16_t *>(p->d_D);
+    const uint32_t nblk = p->Vp / B, ngrp = (nblk + g - 1) / g;
+    const uint32_t S_t = (nblk + N - 1) / N;
+    const SymGather gather(p, N, err);
+    hipStream_t M = p->stream, S = p->side_stream;
+    const uint32_t *own = p->d_tl_all + (size_t)r * p->tl_max;
+    p->p3_launches = 0;
+    p->p3_work = 0.0;
+    p->p3_tiles = 0;
+    while (p->ev.size() < 2 * (size_t)ngrp + 2) {
+        hipEvent_t e;
+        hipEventCreateWithFlags(&e, (unsigned)hipEventDisableSystemFence);
+        p->ev.push_back(e);
+    }
+    const bool f16 = p->fw_f16;
+    const Rect none{make_span(0, 0), make_span(0, 0)};
+    const PackSpec nopack{nullptr, 0u, 0u, 1u, 1u};
+    auto lo = [&](uint32_t a) { return a * g; };
+    auto hi = [&](uint32_t a) { return std::min(nblk, a * g + g); };
+    // Bn's panel after rows Bn arrived: round q on row q (mirrored), then on
+    // the other rows of Bn (mirrored; column q is p2row's mirror, row q and
+    // column q are the operands); p1(q) before each but the first when first
+    // is set (the unpack closed it)
+    auto close_panel = [&](hipStream_t s, uint32_t a, bool first_done) {
+        const uint32_t b0 = lo(a), b1 = hi(a);
+        for (uint32_t q = b0; q < b1; ++q) {
+            if (q > b0 || !first_done) launch_p1<uint16_t>(p1r, s, D, p->Vp, q, f16, p->fw_p1);
+            const Rect row{make_span(q, q + 1), make_span(0, nblk, q)};
+            hipLaunchKernelGGL((q16k<1, 1>(f16)), dim3(4 * row.c.n), dim3(256), 0, s, D, p->Vp, q, row, none, 1u,
+                               nopack);
+            if (b1 - b0 > 1) {
+                const Rect pan{make_span(b0, b1, q), make_span(0, nblk, q)};
+                hipLaunchKernelGGL((q16k<1, 1>(f16)), dim3(4 * pan.r.n * pan.c.n), dim3(256), 0, s, D, p->Vp, q,
+                                   pan, none, 1u, nopack);
+            }
+        }
+    };
+    // prologue: group 0's panel on every rank (the same full initial D)
+    close_panel(M, 0, false);
+    hipEventRecord(p->ev_cross, M);
+    hipEvent_t rest_done = p->ev_cross;
+    srt_status st = SRT_OK;
+    for (uint32_t a = 0; a < ngrp; ++a) {
+        const bool nxt = a + 1 < ngrp;
+        const uint32_t A0 = lo(a), A1 = hi(a), na = A1 - A0;
+        if (nxt) hipStreamWaitEvent(S, rest_done, 0);
+        if (a) hipStreamWaitEvent(M, p->ev_pivot, 0);
+        hipEventRecord(p->ev[2 * p->p3_launches], M);
+        launch_list16(M, D, p->Vp, A0, own, p->tl_own, A0, nxt ? hi(a + 1) : A1, f16, na);
+        rest_done = p->ev[2 * p->p3_launches + 1];
+        hipEventRecord(rest_done, M);
+        p->p3_launches++;
+        p->p3_work += (double)p->tl_own * B * B * B * na;  // minus the skipped row/col tiles
+        p->p3_tiles += p->tl_own;
+        if (!nxt) break;
+        const uint32_t B0 = lo(a + 1), nb = hi(a + 1) - B0;
+        const uint32_t *cl = p->d_tl_cross + p->tl_cross_off[a + 1];
+        const uint32_t cn = p->tl_cross_off[a + 2] - p->tl_cross_off[a + 1];
+        uint16_t *myslot = p->d_rowslots + (size_t)r * nb * S_t * B * B;
+        if (cn) {
+            Span skip{0, 0, A0, A1, 0};
+            const uint64_t addr = reinterpret_cast<uint64_t>(cl);
+            Span ptr{(uint32_t)addr, (uint32_t)(addr >> 32), NONE, NONE, 0};
+            // cross(A) and the pack of rows Bn into this rank's slot, one launch
+            hipLaunchKernelGGL((q16k<4, 2>(f16)), dim3(4 * cn), dim3(256), 0, S, D, p->Vp, A0, Rect{skip, skip},
+                               Rect{ptr, ptr}, na, PackSpec{myslot, B0, nb, N, S_t});
+        }
+        if ((st = gather(p->d_rowslots, (size_t)nb * S_t * B * B * 2, S)) != SRT_OK) return st;
+        // emulation: the other slots hold no real rows, so the unpack (same
+        // volume) goes to scratch and the closed D stays as it is
+        uint16_t *rowdst = emu ? p->d_fbuf : D + (uint64_t)B0 * B * p->Vp;
+        const bool p1 = p->fw_p1 >= 1;  // the fused p1: the squaring or the two-step body
+        const UnpackP1 u = unpack_p1_for(p1r, f16, p->fw_p1 == 2);
+        hipLaunchKernelGGL(u.fn, dim3(1 + nb * nblk), dim3(u.threads), 0, S, D, p->Vp, B0, nb, N, S_t,
+                           (const uint16_t *)p->d_rowslots, rowdst, emu, p1);
+        close_panel(S, a + 1, p1);
+        hipEventRecord(p->ev_pivot, S);
+    }
+    return sym_final_exchange(p, N, r, gather);
 }
 
 template <typename K>
@@ -2278,7 +2543,7 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
     srt_status st = SRT_OK;
     // prologue: pivot 0
     if (own(0)) {
-        launch_p1<K>(p1r, M, D, p->Vp, 0u, p->fw_f16, p->fw_p1_two);
+        launch_p1<K>(p1r, M, D, p->Vp, 0u, p->fw_f16, p->fw_p1);
         launch_tiles<K, 1>(p, M, 0, Rect{make_span(0, 1), make_span(0, nblk, 0)}, none);
     }
     if (sharded && (st = comm_bcast(p->comm, D, pivot_bytes, 0, M, err)) != SRT_OK) return st;
@@ -2331,7 +2596,7 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
             Rect row = own(k1) ? Rect{make_span(k1, k1 + 1), make_span(0, nblk, kb)} : none;
             launch_tiles<K, 4>(p, S, kb, col, row);
             if (own(k1)) {
-                launch_p1<K>(p1r, S, D, p->Vp, k1, p->fw_f16, p->fw_p1_two);
+                launch_p1<K>(p1r, S, D, p->Vp, k1, p->fw_f16, p->fw_p1);
                 launch_tiles<K, 1>(p, S, k1, Rect{make_span(k1, k1 + 1), make_span(0, nblk, k1)}, none);
             }
             // pivot-row broadcast on the comm stream C: the owner's chain goes
@@ -2438,7 +2703,7 @@ srt_status fw_rounds_group_t(srt_plan *p, int p1r, uint32_t g) {
     const bool symc = p->fw_sym && sizeof(K) == 2 && !p->fw_small_chain;
     auto pivots = [&](hipStream_t s, uint32_t a) {
         for (uint32_t r = a; r < a + g; ++r) {
-            launch_p1<K>(p1r, s, D, p->Vp, r, p->fw_f16, p->fw_p1_two);
+            launch_p1<K>(p1r, s, D, p->Vp, r, p->fw_f16, p->fw_p1);
             if (symc) {
                 launch_mirror<K, 1>(p, s, r, Rect{make_span(r, r + 1), make_span(0, nblk, r)});
                 if (r + 1 < a + g)
@@ -2583,7 +2848,7 @@ srt_status fw_rounds_group_sharded_t(srt_plan *p, int p1r, uint32_t g, uint32_t 
         const bool o = own(a);
         for (uint32_t r = a; r < a + g; ++r) {
             if (o) {
-                launch_p1<K>(p1r, s, D, p->Vp, r, p->fw_f16, p->fw_p1_two);
+                launch_p1<K>(p1r, s, D, p->Vp, r, p->fw_f16, p->fw_p1);
                 launch_tiles<K, 1>(p, s, r, Rect{make_span(r, r + 1), make_span(0, nblk, r)}, none);
             }
             if (sharded || emu_bcast_ticks) {

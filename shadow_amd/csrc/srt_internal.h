@@ -79,9 +79,15 @@ struct srt_plan {
     int key_type = srt::KEY_F64;  // closure keys: u32 / f64 (exact integers < 2^53) / u64
     bool fw_glds = true;   // FW tiles staged by LDS-DMA (false: register staging)
     bool fw_f16 = false;   // u16-stored keys relaxed as f16 integers (every finite distance < 1024 units)
-    bool fw_p1_two = true; // u16/f16 phase 1 at two FW steps per barrier (knob SRT_FW_P1_TWO=0: one)
+    // u16/f16 phase 1 (the pivot block's closure): 2 = min-plus squaring to
+    // the fixpoint (closure_sq_body), 1 = two FW steps per barrier, 0 = one
+    // (knob SRT_FW_P1 for A/B)
+    int fw_p1 = 2;
     bool fw_small_chain = false;  // quarter-tile kernels for the look-ahead chain (sharded)
     bool fw_unique_edges = false; // no parallel edges: FW init stores instead of atomic min
+    // rounds per row all-gather of the symmetric sharded schedule (knob
+    // SRT_FW_SYM_GROUP; 1 = fw_rounds_sym_sharded's one-round chain)
+    uint32_t fw_sym_group = 1;
     bool fw_sym = false;          // D symmetric (fw_sym_check): rest launches run the triangle
     bool fw_sym_known = false;
     uint32_t *d_flag32 = nullptr; // device scratch flag (symmetry check)
@@ -91,6 +97,7 @@ struct srt_plan {
     uint32_t *d_tl_cnt = nullptr;      // N counts
     uint32_t *d_tl_cross = nullptr;    // own tiles with i == k or j == k, concatenated over k
     std::vector<uint32_t> tl_cross_off;
+    uint32_t sym_g = 0;  // the group size the lists and slots above are laid out for
     uint32_t tl_max = 0, tl_own = 0;
     uint16_t *d_rowslots = nullptr;    // N x ceil(nblk / N) tiles: the per-round row exchange
     uint16_t *d_fbuf = nullptr;        // N x tl_max tiles: the final exchange

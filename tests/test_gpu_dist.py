@@ -32,14 +32,20 @@ def _port():
     (3, 400, 7, "fw", True, None),
     # symmetric graphs: triangle tiles dealt by (i + j) mod N, a row all-gather per round
     (2, 300, 12, "fw", "undirected", None), (3, 520, 13, "fw", "undirected", None),
-    (8, 1100, 14, "fw", "undirected", None), (3, 200, 15, "sssp", "undirected", None)])
+    (8, 1100, 14, "fw", "undirected", None), (3, 200, 15, "sssp", "undirected", None),
+    # ... in groups of g rounds, one row all-gather per group ("s<g>:<rest launches>"; a sharded
+    # plan pads to whole block-rows a rank: 8 ranks 16 block-rows, the last group of 3 ragged)
+    (2, 1000, 16, "fw", "undirected", "s2:4"), (3, 1300, 17, "fw", "undirected", "s4:3"),
+    (8, 1100, 18, "fw", "undirected", "s2:8"), (8, 1500, 19, "fw", "undirected", "s3:6")])
 def test_sharded_build_matches_oracle(world, n, seed, algo, wide, group):
     """Dense builds assert the sharded tail ran (or, "wide", the replicated
     fallback) and, for undirected graphs, the symmetric schedule; every rank's
     table equals the oracle's bit for bit."""
     port = _port()
     env = dict(os.environ)
-    if group:  # "g:rest launches"
+    if group and group.startswith("s"):  # symmetric schedule, "s<g>:<rest launches>"
+        env["SRT_FW_SYM_GROUP"], env["SRT_TEST_EXPECT_RESTS"] = group[1:].split(":")
+    elif group:  # "g:rest launches"
         env["SRT_FW_SHARD_GROUP"], env["SRT_TEST_EXPECT_RESTS"] = group.split(":")
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker.py"), str(r), str(world), str(port),
                                str(n), str(seed), "torch", algo] +

@@ -281,8 +281,9 @@ def test_eccentricity_proof_needs_strong_connectivity():
 def test_phase1_two_steps_per_barrier(monkeypatch, key, rows):
     """Phase 1 at two FW steps per barrier (fw_phase1_pk2_kernel: rows and
     columns k, k+1 published together, column/row k+1 advanced by step k in
-    registers) gives the one-step kernel's bits and the oracle's, for f16 and
-    u16 keys and every rows-per-thread layout."""
+    registers) and by min-plus squaring (closure_sq_body, the default) give
+    the one-step kernel's bits and the oracle's, for f16 and u16 keys and
+    every rows-per-thread layout."""
     monkeypatch.setenv("SRT_FW_P1_ROWS", rows)
     if key == "u16":
         monkeypatch.setenv("SRT_FW_KEY", "u16")
@@ -291,8 +292,8 @@ def test_phase1_two_steps_per_barrier(monkeypatch, key, rows):
     g = NetworkGraph.from_edges(n, src, dst, lat, loss)
     nodes = np.arange(n, dtype=np.uint32)
     tabs = {}
-    for two in ("1", "0"):
-        monkeypatch.setenv("SRT_FW_P1_TWO", two)
+    for two in ("2", "1", "0"):
+        monkeypatch.setenv("SRT_FW_P1", two)
         plan = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_FW)
         try:
             assert plan.describe().startswith(f"fw:{key}key"), plan.describe()
@@ -304,3 +305,45 @@ def test_phase1_two_steps_per_barrier(monkeypatch, key, rows):
     for two, t in tabs.items():
         assert np.array_equal(t.latency_ns, elat), two
         assert np.array_equal(t.packet_loss.view(np.uint32), eloss.view(np.uint32)), two
+
+
+@pytest.mark.parametrize("key", ["f16", "u16"])
+@pytest.mark.parametrize("directed", [False, True])
+def test_phase1_squaring_long_paths(monkeypatch, key, directed):
+    """Pivot blocks whose shortest paths run through ~127 hops inside the block
+    (a path graph over consecutive ids, plus a few chords): the squaring phase
+    1 needs all 7 squares there, and must still equal the FW steps and the
+    oracle."""
+    if key == "u16":
+        monkeypatch.setenv("SRT_FW_KEY", "u16")
+    n = 390
+    rng = np.random.default_rng(7)
+    ids = np.arange(n - 1, dtype=np.uint32)
+    chords = rng.integers(0, n, size=(12, 2)).astype(np.uint32)
+    src = np.concatenate([ids, chords[:, 0], np.arange(n, dtype=np.uint32)])
+    dst = np.concatenate([ids + 1, chords[:, 1], np.arange(n, dtype=np.uint32)])
+    m = len(src)
+    lat = (rng.integers(1, 3, size=m) * 1_000_000).astype(np.uint64)
+    lat[m - n:] = 1_000_000  # self-loops
+    lat[n - 1:m - n] = 900_000_000  # long chords: the path stays the shortest way
+    loss = np.round(rng.uniform(0.0, 0.01, size=m), 6).astype(np.float32)
+    if directed:  # both directions, different weights: a directed graph with paths both ways
+        src, dst = np.concatenate([src, dst]), np.concatenate([dst, src])
+        lat = np.concatenate([lat, lat[::-1].copy()])
+        loss = np.concatenate([loss, loss])
+    g = NetworkGraph.from_edges(n, src, dst, lat, loss, directed=directed)
+    nodes = np.arange(n, dtype=np.uint32)
+    tabs = {}
+    for mode in ("2", "1"):
+        monkeypatch.setenv("SRT_FW_P1", mode)
+        plan = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_FW)
+        try:
+            assert plan.describe().startswith(f"fw:{key}key"), plan.describe()
+            tabs[mode] = plan.run().fetch()
+        finally:
+            plan.close()
+    from oracle import oracle as O
+    elat, eloss = O.compute_shortest_paths(O.Graph(directed, nodes, src, dst, lat, loss), nodes)
+    for mode, t in tabs.items():
+        assert np.array_equal(t.latency_ns, elat), mode
+        assert np.array_equal(t.packet_loss.view(np.uint32), eloss.view(np.uint32)), mode

@@ -6,7 +6,7 @@ R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
 cd /tmp
 for n in ${@:-8}; do
-  timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/emu_trace$n -o run --output-format csv -- \
-    python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --emulate-ranks $n > $R/gpurun_out/emu_trace$n.log 2>&1 || exit 1
-  tail -1 $R/gpurun_out/emu_trace$n.log
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/emu_trace$n${EMU_TAG} -o run --output-format csv -- \
+    python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-cold --no-e2e --emulate-ranks $n > $R/gpurun_out/emu_trace$n${EMU_TAG}.log 2>&1 || exit 1
+  tail -1 $R/gpurun_out/emu_trace$n${EMU_TAG}.log
 done
