@@ -1132,8 +1132,9 @@ template <int P1R, bool F16>
 __device__ __forceinline__ void phase1_pk2_body(const uint16_t *__restrict__ src, uint64_t ss,
                                                 uint16_t *__restrict__ dst, uint64_t ds) {
     static_assert(P1R % 2 == 0, "rows k and k+1 must share a thread-row");
-    __shared__ us2 rowbuf[2][2][B / 2];   // [buffer][row k, row k+1][column pair]
-    __shared__ uint16_t colbuf[2][2][B];  // [buffer][column k, column k+1][row]
+    __shared__ us2 rowbuf[2][2][B / 2];  // [buffer][row k, row k+1][column pair]
+    // [buffer][row]: (D[row][k], D[row][k+1]) -- the owner's register pair as is
+    __shared__ __attribute__((aligned(16))) uint32_t colbuf2[2][B];
     __builtin_amdgcn_s_setprio(3);        // critical path of the look-ahead chain
     const int tid = threadIdx.x, tx = tid % 16, ty = tid / 16;
     us2 p[P1R][4];
@@ -1158,10 +1159,7 @@ __device__ __forceinline__ void phase1_pk2_body(const uint16_t *__restrict__ src
         }
         if (tx == g) {
 #pragma unroll
-            for (int i = 0; i < P1R; ++i) {
-                colbuf[buf][0][ty * P1R + i] = p[i][e][0];
-                colbuf[buf][1][ty * P1R + i] = p[i][e][1];
-            }
+            for (int i = 0; i < P1R; ++i) colbuf2[buf][ty * P1R + i] = __builtin_bit_cast(uint32_t, p[i][e]);
         }
     };
     publish(0, 0, 0);
@@ -1183,13 +1181,34 @@ __device__ __forceinline__ void phase1_pk2_body(const uint16_t *__restrict__ src
             const us2 s10p = {s10, s10};
 #pragma unroll
             for (int q = 0; q < 4; ++q) d1[q] = __builtin_elementwise_min(d1[q], add_keys2<F16>(s10p, b0[q]));
+            uint32_t cp[P1R];  // (a, c) = (D[i][k], D[i][k+1]) per row
+#pragma unroll
+            for (int i = 0; i < P1R; i += 2) {
+                const uint2 v = *reinterpret_cast<const uint2 *>(&colbuf2[cur][ty * P1R + i]);
+                cp[i] = v.x;
+                cp[i + 1] = v.y;
+            }
+            // f16: (a, c') = min((a, c), (a + 2048, a + D[k][k+1])) in two packed
+            // ops (a + 2048 <= 3072 is exact and > a)
+            const uint32_t kk = 0x6800u | ((uint32_t)s01 << 16);
 #pragma unroll
             for (int i = 0; i < P1R; ++i) {
-                const uint16_t a = colbuf[cur][0][ty * P1R + i], c = colbuf[cur][1][ty * P1R + i];
-                const us2 s01p = {s01, (uint16_t)0};
-                // (a, c') with c' = min(c, a + D[k][k+1]) (the low half of a + s01 is a + D[k][k+1])
-                const us2 sum = add_keys2<F16>(us2{a, a}, s01p);
-                const us2 acp = {a, c < sum[0] ? c : sum[0]};
+                us2 acp;
+                if constexpr (F16) {
+                    uint32_t t, r;
+                    asm volatile(
+                        "v_pk_add_f16 %0, %2, %3 op_sel_hi:[0,1]\n\t"
+                        "v_pk_min_u16 %1, %2, %0"
+                        : "=&v"(t), "=v"(r)
+                        : "v"(cp[i]), "v"(kk));
+                    acp = __builtin_bit_cast(us2, r);
+                } else {
+                    const us2 ac = __builtin_bit_cast(us2, cp[i]);
+                    const uint16_t a = ac[0], c = ac[1];
+                    // (a, c') with c' = min(c, a + D[k][k+1])
+                    const uint16_t sum = (uint16_t)(a + s01);
+                    acp = us2{a, c < sum ? c : sum};
+                }
                 if constexpr (F16) {
                     uint32_t acc[4];
 #pragma unroll
@@ -1237,88 +1256,6 @@ __global__ __launch_bounds__(16 * (B / P1R)) void fw_phase1_pk2_kernel(uint16_t 
     phase1_pk2_body<P1R, F16>(blk, Vp, blk, Vp);
 }
 
-// Phase 1 for u16 / f16 keys by min-plus squaring: M <- min(M, M (x) M)
-// until nothing changes (at most 7 times: a shortest path inside the block
-// has <= 127 hops and the t-th square covers every walk of <= 2^t).  A
-// fixpoint M holds walk lengths, stays <= the input and satisfies the
-// triangle inequality, so it is the closure -- the same keys as the 128
-// sequential FW steps, bit for bit.  Pivot blocks close in 2-4 squares
-// (few hops inside a block), each one a dense 128^3 min-plus product of one
-// workgroup out of LDS (M row-major in pairs, and pair-transposed for the A
-// operand), instead of 64 barrier-bound double steps: the critical path of
-// the symmetric sharded chain.  512 threads, each 4 rows x 8 columns (the
-// pk2 layout).  Reads src (row stride ss), writes dst (row stride ds).
-template <bool F16>
-__device__ __forceinline__ void closure_sq_body(const uint16_t *__restrict__ src, uint64_t ss,
-                                                uint16_t *__restrict__ dst, uint64_t ds) {
-    __shared__ __attribute__((aligned(16))) uint32_t M2[B][B / 2];       // M2[i][kp] = (M[i][2kp], M[i][2kp+1])
-    __shared__ __attribute__((aligned(16))) uint32_t MT2[B / 2][B + 4];  // MT2[kp][i] = M2[i][kp]
-    __builtin_amdgcn_s_setprio(3);  // critical path of the look-ahead chain
-    const int tid = threadIdx.x, tx = tid % 16, ty = tid / 16;
-    uint32_t acc[4][4];  // rows ty*4 + i, column pairs tx*4 + q
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(src + (ty * 4 + i) * ss + tx * 8);
-        acc[i][0] = v.x;
-        acc[i][1] = v.y;
-        acc[i][2] = v.z;
-        acc[i][3] = v.w;
-    }
-    auto stash = [&]() {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            *reinterpret_cast<uint4 *>(&M2[ty * 4 + i][tx * 4]) = make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-            *reinterpret_cast<uint4 *>(&MT2[tx * 4 + q][ty * 4]) = make_uint4(acc[0][q], acc[1][q], acc[2][q], acc[3][q]);
-    };
-    stash();
-    __syncthreads();
-#pragma unroll 1
-    for (int it = 0; it < 7; ++it) {
-        uint32_t old[4][4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) old[i][q] = acc[i][q];
-#pragma unroll 4
-        for (int kp = 0; kp < B / 2; ++kp) {
-            const uint4 a = *reinterpret_cast<const uint4 *>(&MT2[kp][ty * 4]);
-            const uint4 b0v = *reinterpret_cast<const uint4 *>(&M2[2 * kp][tx * 4]);
-            const uint4 b1v = *reinterpret_cast<const uint4 *>(&M2[2 * kp + 1][tx * 4]);
-            const u32x4 b0 = {b0v.x, b0v.y, b0v.z, b0v.w}, b1 = {b1v.x, b1v.y, b1v.z, b1v.w};
-            const uint32_t av[4] = {a.x, a.y, a.z, a.w};
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                if constexpr (F16) {
-                    relax_pairs_f16(acc[i], av[i], b0, b1);
-                } else {
-                    relax_pairs16<0>(acc[i], av[i], b0);
-                    relax_pairs16<1>(acc[i], av[i], b1);
-                }
-            }
-        }
-        int changed = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) changed |= acc[i][q] != old[i][q];
-        if (!__syncthreads_or(changed)) break;  // also: every read of this square is done
-        stash();
-        __syncthreads();
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-        *reinterpret_cast<uint4 *>(dst + (ty * 4 + i) * ds + tx * 8) =
-            make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
-}
-
-template <bool F16>
-__global__ __launch_bounds__(512) void fw_phase1_sq_kernel(uint16_t *__restrict__ D, uint32_t Vp, uint32_t kb) {
-    uint16_t *blk = D + (uint64_t)kb * B * Vp + (uint64_t)kb * B;
-    closure_sq_body<F16>(blk, Vp, blk, Vp);
-}
-
 // The symmetric sharded chain after the row all-gather, one launch: rows
 // [p0, p0 + np) (one round, or a group's) arrive; block 0 closes pivot block
 // (p0, p0) straight from its slot (emu: from D) into D when p1 is set; block
@@ -1326,7 +1263,7 @@ __global__ __launch_bounds__(512) void fw_phase1_sq_kernel(uint16_t *__restrict_
 // (np * S tiles a rank: index (r - p0) * S + c / N) into rows (row r at
 // rows + (r - p0) * B * Vp: D's block-rows, or the emulation's scratch),
 // except the pivot block p1 closes.
-template <int P1R, bool F16, bool SQ = false>
+template <int P1R, bool F16>
 __global__ __launch_bounds__(16 * (B / P1R)) void unpack_p1_kernel(uint16_t *__restrict__ D, uint32_t Vp, uint32_t p0,
                                                                   uint32_t np, uint32_t N, uint32_t S,
                                                                   const uint16_t *__restrict__ slots,
@@ -1335,12 +1272,7 @@ __global__ __launch_bounds__(16 * (B / P1R)) void unpack_p1_kernel(uint16_t *__r
     if (blockIdx.x == 0) {
         if (!p1) return;
         const uint16_t *src = emu ? D + diag : slots + ((uint64_t)((2 * p0) % N) * np * S + p0 / N) * B * B;
-        if constexpr (SQ) {
-            static_assert(P1R == 4, "the squaring body runs 512 threads");
-            closure_sq_body<F16>(src, emu ? Vp : B, D + diag, Vp);
-        } else {
-            phase1_pk2_body<P1R, F16>(src, emu ? Vp : B, D + diag, Vp);
-        }
+        phase1_pk2_body<P1R, F16>(src, emu ? Vp : B, D + diag, Vp);
         return;
     }
     const uint32_t nblk = Vp / B, t = blockIdx.x - 1, r = p0 + t / nblk, c = t % nblk;
@@ -1762,8 +1694,8 @@ __global__ __launch_bounds__(256) void minplus_q16_kernel(uint16_t *__restrict__
         return slot + ((uint64_t)(r - pk.p0) * pk.S + c / N) * B * B;
     };
     constexpr int QK = 32;
-    __shared__ uint16_t As[2][SQ][QK + 2];  // [row][k]
-    __shared__ us2 Bs[2][QK][SQ / 2];        // [k][column pair]
+    __shared__ __attribute__((aligned(16))) uint32_t At2[2][QK / 2][SQ + 4];  // [k pair][row]: (A[row][2kp], A[row][2kp+1])
+    __shared__ __attribute__((aligned(16))) us2 Bs[2][QK][SQ / 2];           // [k][column pair]
     __shared__ uint16_t T[SQ][SQ + 1];
     __builtin_amdgcn_s_setprio(2);
     uint32_t t = blockIdx.x >> 2, bi, bj;
@@ -1827,43 +1759,89 @@ __global__ __launch_bounds__(256) void minplus_q16_kernel(uint16_t *__restrict__
         acc[i][0] = __builtin_bit_cast(us2, v.x);
         acc[i][1] = __builtin_bit_cast(us2, v.y);
     }
-    // a chunk: A = 64 rows x 32 k (8 keys a thread), B = 32 k x 64 columns (8 keys)
-    uint4 ra, rb;
-    auto fetch = [&](int kc) {
-        ra = *reinterpret_cast<const uint4 *>(D + (i0 + tid / 4) * Vp + k0 + kc + (tid % 4) * 8);
-        rb = *reinterpret_cast<const uint4 *>(D + (k0 + kc + tid / 8) * Vp + j0 + (tid % 8) * 8);
+    // a chunk: A = 64 rows x 32 k (8 keys a thread), B = 32 k x 64 columns (8
+    // keys).  Chunks are fetched PF ahead into a register ring, so a launch
+    // of one round (4 chunks) waits on global memory once, not per chunk:
+    // these launches are latency-bound chain steps
+    constexpr int PF = 4;
+    uint4 ra[PF], rb[PF];
+    auto fetch = [&](int slot, int kc) {
+        ra[slot] = *reinterpret_cast<const uint4 *>(D + (i0 + tid / 4) * Vp + k0 + kc + (tid % 4) * 8);
+        rb[slot] = *reinterpret_cast<const uint4 *>(D + (k0 + kc + tid / 8) * Vp + j0 + (tid % 8) * 8);
     };
-    auto stash = [&](int buf) {
-        uint16_t *a = &As[buf][tid / 4][(tid % 4) * 8];
-        const uint16_t *ra16 = reinterpret_cast<const uint16_t *>(&ra);
+    auto stash = [&](int slot, int buf) {
+        // the thread's 8 keys of row tid / 4 = 4 k pairs, at k pairs (tid % 4) * 4 ..
+        const uint32_t *r = reinterpret_cast<const uint32_t *>(&ra[slot]);
 #pragma unroll
-        for (int x = 0; x < 8; ++x) a[x] = ra16[x];
+        for (int x = 0; x < 4; ++x) At2[buf][(tid % 4) * 4 + x][tid / 4] = r[x];
         us2 *b = &Bs[buf][tid / 8][(tid % 8) * 4];
-        b[0] = __builtin_bit_cast(us2, rb.x);
-        b[1] = __builtin_bit_cast(us2, rb.y);
-        b[2] = __builtin_bit_cast(us2, rb.z);
-        b[3] = __builtin_bit_cast(us2, rb.w);
+        b[0] = __builtin_bit_cast(us2, rb[slot].x);
+        b[1] = __builtin_bit_cast(us2, rb[slot].y);
+        b[2] = __builtin_bit_cast(us2, rb[slot].z);
+        b[3] = __builtin_bit_cast(us2, rb[slot].w);
     };
-    fetch(0);
-    stash(0);
-    __syncthreads();
-#pragma unroll 1
-    for (int ch = 0; ch < NCH; ++ch) {
-        const int cur = ch & 1;
-        if (ch + 1 < NCH) fetch((ch + 1) * QK);
-#pragma unroll 8
-        for (int k = 0; k < QK; ++k) {
-            const us2 b0 = Bs[cur][k][tx * 2], b1 = Bs[cur][k][tx * 2 + 1];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uint16_t a = As[cur][ty * 4 + i][k];
-                const us2 a2 = {a, a};
-                acc[i][0] = __builtin_elementwise_min(acc[i][0], add_keys2<F16>(a2, b0));
-                acc[i][1] = __builtin_elementwise_min(acc[i][1], add_keys2<F16>(a2, b1));
+    for (int c = 0; c < PF; ++c) fetch(c, c * QK);  // NCH is a multiple of 4 = PF
+    stash(0, 0);
+    __syncthreads();
+    uint32_t ac[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        ac[i][0] = __builtin_bit_cast(uint32_t, acc[i][0]);
+        ac[i][1] = __builtin_bit_cast(uint32_t, acc[i][1]);
+    }
+#pragma unroll 1
+    for (int c0 = 0; c0 < NCH; c0 += PF) {
+#pragma unroll
+        for (int j = 0; j < PF; ++j) {
+            const int ch = c0 + j, cur = j & 1;
+            // two k a step: per row and column pair, acc <- min(acc, a_k + b_k,
+            // a_k+1 + b_k+1) -- f16: 2 v_pk_add_f16 + 1 v_pk_minimum3_f16 (A's
+            // pair broadcast by op_sel, as relax_pairs_f16); u16: 2 adds + 2 mins
+#pragma unroll 4
+            for (int kp = 0; kp < QK / 2; ++kp) {
+                const uint4 a4 = *reinterpret_cast<const uint4 *>(&At2[cur][kp][ty * 4]);
+                const uint2 b0 = *reinterpret_cast<const uint2 *>(&Bs[cur][2 * kp][tx * 2]);
+                const uint2 b1 = *reinterpret_cast<const uint2 *>(&Bs[cur][2 * kp + 1][tx * 2]);
+                const uint32_t av[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    uint32_t t0, t1, t2, t3;
+                    if constexpr (F16)
+                        asm volatile(
+                            "v_pk_add_f16 %0, %6, %7 op_sel_hi:[0,1]\n\t"
+                            "v_pk_add_f16 %1, %6, %9 op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+                            "v_pk_add_f16 %2, %6, %8 op_sel_hi:[0,1]\n\t"
+                            "v_pk_add_f16 %3, %6, %10 op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+                            "v_pk_minimum3_f16 %4, %4, %0, %1\n\t"
+                            "v_pk_minimum3_f16 %5, %5, %2, %3"
+                            : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "+v"(ac[i][0]), "+v"(ac[i][1])
+                            : "v"(av[i]), "v"(b0.x), "v"(b0.y), "v"(b1.x), "v"(b1.y));
+                    else
+                        asm volatile(
+                            "v_pk_add_u16 %0, %6, %7 op_sel_hi:[0,1]\n\t"
+                            "v_pk_add_u16 %1, %6, %9 op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+                            "v_pk_add_u16 %2, %6, %8 op_sel_hi:[0,1]\n\t"
+                            "v_pk_add_u16 %3, %6, %10 op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+                            "v_pk_min_u16 %4, %4, %0\n\t"
+                            "v_pk_min_u16 %5, %5, %2\n\t"
+                            "v_pk_min_u16 %4, %4, %1\n\t"
+                            "v_pk_min_u16 %5, %5, %3"
+                            : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "+v"(ac[i][0]), "+v"(ac[i][1])
+                            : "v"(av[i]), "v"(b0.x), "v"(b0.y), "v"(b1.x), "v"(b1.y));
+                }
             }
+            if (ch + 1 < NCH) {
+                stash((j + 1) % PF, cur ^ 1);  // the other buffer's readers passed the last barrier
+                if (ch + 1 + PF - 1 < NCH) fetch(j, (ch + PF) * QK);  // slot j is free again
+            }
+            __syncthreads();
         }
-        if (ch + 1 < NCH) stash(cur ^ 1);  // the other buffer's readers passed the last barrier
-        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        acc[i][0] = __builtin_bit_cast(us2, ac[i][0]);
+        acc[i][1] = __builtin_bit_cast(us2, ac[i][1]);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1996,11 +1974,6 @@ template <typename K>
 void launch_p1(int rows, hipStream_t s, K *D, uint32_t Vp, uint32_t kb, bool f16 = false, int mode = 0) {
     if constexpr (sizeof(K) == 2) {
         uint16_t *D16 = reinterpret_cast<uint16_t *>(D);
-        if (mode == 2) {
-            hipLaunchKernelGGL(f16 ? &fw_phase1_sq_kernel<true> : &fw_phase1_sq_kernel<false>, dim3(1), dim3(512), 0,
-                               s, D16, Vp, kb);
-            return;
-        }
         if (mode == 1) {
             if (rows == 2)
                 hipLaunchKernelGGL(p1k2<2>(f16), dim3(1), dim3(16 * (B / 2)), 0, s, D16, Vp, kb);
@@ -2172,14 +2145,12 @@ srt_status sym_sharded_setup(srt_plan *p, uint32_t N, uint32_t r, uint32_t g, sr
     return SRT_OK;
 }
 
-// the fused row unpack + phase 1 kernel for a phase-1 form: the squaring body
-// (512 threads) or the two-step body at p1r rows a thread
+// the fused row unpack + (two-step) phase 1 kernel at p1r rows a thread
 struct UnpackP1 {
     void (*fn)(uint16_t *, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, const uint16_t *, uint16_t *, bool, bool);
     uint32_t threads;
 };
-UnpackP1 unpack_p1_for(int p1r, bool f16, bool sq) {
-    if (sq) return {f16 ? &unpack_p1_kernel<4, true, true> : &unpack_p1_kernel<4, false, true>, 512u};
+UnpackP1 unpack_p1_for(int p1r, bool f16) {
     if (p1r == 2) return {f16 ? &unpack_p1_kernel<2, true> : &unpack_p1_kernel<2, false>, 16u * (B / 2)};
     if (p1r == 4) return {f16 ? &unpack_p1_kernel<4, true> : &unpack_p1_kernel<4, false>, 16u * (B / 4)};
     return {f16 ? &unpack_p1_kernel<8, true> : &unpack_p1_kernel<8, false>, 16u * (B / 8)};
@@ -2339,7 +2310,7 @@ srt_status fw_rounds_sym_sharded(srt_plan *p, int p1r, srt_err *err) {
         uint16_t *rowdst = emu ? p->d_fbuf : D + (uint64_t)k1 * B * p->Vp;
         if (fuse_p1 && (p1r == 2 || p1r == 4 || p1r == 8)) {
             // unpack of row k1 and p1(k1) from its slot, one launch
-            const UnpackP1 u = unpack_p1_for(p1r, p->fw_f16, p->fw_p1 == 2);
+            const UnpackP1 u = unpack_p1_for(p1r, p->fw_f16);
             hipLaunchKernelGGL(u.fn, dim3(nblk + 1), dim3(u.threads), 0, S, D, p->Vp, k1, 1u, N, S_t,
                                (const uint16_t *)p->d_rowslots, rowdst, emu, true);
         } else {
@@ -2446,8 +2417,8 @@ srt_status fw_rounds_sym_grouped(srt_plan *p, int p1r, uint32_t g, srt_err *err)
         // emulation: the other slots hold no real rows, so the unpack (same
         // volume) goes to scratch and the closed D stays as it is
         uint16_t *rowdst = emu ? p->d_fbuf : D + (uint64_t)B0 * B * p->Vp;
-        const bool p1 = p->fw_p1 >= 1;  // the fused p1: the squaring or the two-step body
-        const UnpackP1 u = unpack_p1_for(p1r, f16, p->fw_p1 == 2);
+        const bool p1 = p->fw_p1 >= 1;  // the fused p1 is the two-step body
+        const UnpackP1 u = unpack_p1_for(p1r, f16);
         hipLaunchKernelGGL(u.fn, dim3(1 + nb * nblk), dim3(u.threads), 0, S, D, p->Vp, B0, nb, N, S_t,
                            (const uint16_t *)p->d_rowslots, rowdst, emu, p1);
         close_panel(S, a + 1, p1);

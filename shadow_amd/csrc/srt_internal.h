@@ -79,10 +79,12 @@ struct srt_plan {
     int key_type = srt::KEY_F64;  // closure keys: u32 / f64 (exact integers < 2^53) / u64
     bool fw_glds = true;   // FW tiles staged by LDS-DMA (false: register staging)
     bool fw_f16 = false;   // u16-stored keys relaxed as f16 integers (every finite distance < 1024 units)
-    // u16/f16 phase 1 (the pivot block's closure): 2 = min-plus squaring to
-    // the fixpoint (closure_sq_body), 1 = two FW steps per barrier, 0 = one
-    // (knob SRT_FW_P1 for A/B)
-    int fw_p1 = 2;
+    // u16/f16 phase 1 (the pivot block's closure): 1 = two FW steps per
+    // barrier, 0 = one (knob SRT_FW_P1 for A/B).  (Min-plus squaring to the
+    // fixpoint was tried: 1 CU does a whole 128^3 product per square, real
+    // blocks need 2-4 squares, and its 66 KB of LDS waited behind the rest
+    // launch for a CU -- median 44 us, tail 1.2 ms, against 33 us.)
+    int fw_p1 = 1;
     bool fw_small_chain = false;  // quarter-tile kernels for the look-ahead chain (sharded)
     bool fw_unique_edges = false; // no parallel edges: FW init stores instead of atomic min
     // rounds per row all-gather of the symmetric sharded schedule (knob

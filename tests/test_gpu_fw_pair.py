@@ -281,9 +281,8 @@ def test_eccentricity_proof_needs_strong_connectivity():
 def test_phase1_two_steps_per_barrier(monkeypatch, key, rows):
     """Phase 1 at two FW steps per barrier (fw_phase1_pk2_kernel: rows and
     columns k, k+1 published together, column/row k+1 advanced by step k in
-    registers) and by min-plus squaring (closure_sq_body, the default) give
-    the one-step kernel's bits and the oracle's, for f16 and u16 keys and
-    every rows-per-thread layout."""
+    registers) gives the one-step kernel's bits and the oracle's, for f16 and
+    u16 keys and every rows-per-thread layout."""
     monkeypatch.setenv("SRT_FW_P1_ROWS", rows)
     if key == "u16":
         monkeypatch.setenv("SRT_FW_KEY", "u16")
@@ -292,7 +291,7 @@ def test_phase1_two_steps_per_barrier(monkeypatch, key, rows):
     g = NetworkGraph.from_edges(n, src, dst, lat, loss)
     nodes = np.arange(n, dtype=np.uint32)
     tabs = {}
-    for two in ("2", "1", "0"):
+    for two in ("1", "0"):
         monkeypatch.setenv("SRT_FW_P1", two)
         plan = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_FW)
         try:
@@ -309,32 +308,34 @@ def test_phase1_two_steps_per_barrier(monkeypatch, key, rows):
 
 @pytest.mark.parametrize("key", ["f16", "u16"])
 @pytest.mark.parametrize("directed", [False, True])
-def test_phase1_squaring_long_paths(monkeypatch, key, directed):
+def test_phase1_long_paths(monkeypatch, key, directed):
     """Pivot blocks whose shortest paths run through ~127 hops inside the block
-    (a path graph over consecutive ids, plus a few chords): the squaring phase
-    1 needs all 7 squares there, and must still equal the FW steps and the
-    oracle."""
+    (a path graph over consecutive ids, plus a few chords): both phase-1 forms
+    equal the oracle."""
     if key == "u16":
         monkeypatch.setenv("SRT_FW_KEY", "u16")
     n = 390
     rng = np.random.default_rng(7)
     ids = np.arange(n - 1, dtype=np.uint32)
-    chords = rng.integers(0, n, size=(12, 2)).astype(np.uint32)
-    src = np.concatenate([ids, chords[:, 0], np.arange(n, dtype=np.uint32)])
-    dst = np.concatenate([ids + 1, chords[:, 1], np.arange(n, dtype=np.uint32)])
+    pairs = {(min(a, b), max(a, b)) for a, b in rng.integers(0, n, size=(24, 2)) if abs(int(a) - int(b)) > 1}
+    ch = np.array(sorted(pairs), np.uint32)[:12]
+    if directed:  # the path both ways (own weights), chords one way
+        src = np.concatenate([ids, ids + 1, ch[:, 0], np.arange(n, dtype=np.uint32)])
+        dst = np.concatenate([ids + 1, ids, ch[:, 1], np.arange(n, dtype=np.uint32)])
+        npath = 2 * (n - 1)
+    else:
+        src = np.concatenate([ids, ch[:, 0], np.arange(n, dtype=np.uint32)])
+        dst = np.concatenate([ids + 1, ch[:, 1], np.arange(n, dtype=np.uint32)])
+        npath = n - 1
     m = len(src)
-    lat = (rng.integers(1, 3, size=m) * 1_000_000).astype(np.uint64)
+    lat = (rng.choice([1, 2], size=m, p=[0.85, 0.15]) * 1_000_000).astype(np.uint64)
+    lat[npath:npath + len(ch)] = 900_000_000  # long chords: the path stays the shortest way
     lat[m - n:] = 1_000_000  # self-loops
-    lat[n - 1:m - n] = 900_000_000  # long chords: the path stays the shortest way
     loss = np.round(rng.uniform(0.0, 0.01, size=m), 6).astype(np.float32)
-    if directed:  # both directions, different weights: a directed graph with paths both ways
-        src, dst = np.concatenate([src, dst]), np.concatenate([dst, src])
-        lat = np.concatenate([lat, lat[::-1].copy()])
-        loss = np.concatenate([loss, loss])
     g = NetworkGraph.from_edges(n, src, dst, lat, loss, directed=directed)
     nodes = np.arange(n, dtype=np.uint32)
     tabs = {}
-    for mode in ("2", "1"):
+    for mode in ("1", "0"):
         monkeypatch.setenv("SRT_FW_P1", mode)
         plan = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_FW)
         try:
