@@ -88,8 +88,11 @@ struct srt_plan {
     bool fw_small_chain = false;  // quarter-tile kernels for the look-ahead chain (sharded)
     bool fw_unique_edges = false; // no parallel edges: FW init stores instead of atomic min
     // rounds per row all-gather of the symmetric sharded schedule (knob
-    // SRT_FW_SYM_GROUP; 1 = fw_rounds_sym_sharded's one-round chain)
-    uint32_t fw_sym_group = 1;
+    // SRT_FW_SYM_GROUP; 1 = fw_rounds_sym_sharded's one-round chain).
+    // Emulated C3, g = 1 / 2 / 4: 8 ranks 21.9 / 20.0 / 22.4 ms, 4 ranks 24.2 /
+    // 22.6 / 26.0, 2 ranks 37.3 / 34.5 (stream-memory hand-offs instead of
+    // events measured the same: 19.8 / 22.8 / 34.4)
+    uint32_t fw_sym_group = 2;
     bool fw_sym = false;          // D symmetric (fw_sym_check): rest launches run the triangle
     bool fw_sym_known = false;
     uint32_t *d_flag32 = nullptr; // device scratch flag (symmetry check)
