@@ -30,9 +30,11 @@ def _port():
     (2, 1000, 11, "fw", False, "2:4"),
     # u64 keys: replicated loss pass after the key all-gather
     (3, 400, 7, "fw", True, None),
-    # symmetric graphs: triangle tiles dealt by (i + j) mod N, a row all-gather per round
+    # symmetric graphs: triangle tiles dealt by (i + j) mod N, a row all-gather per 2 rounds
+    # (the default; 300 nodes = 3 block-rows: one round a group), and per round ("s1:...")
     (2, 300, 12, "fw", "undirected", None), (3, 520, 13, "fw", "undirected", None),
     (8, 1100, 14, "fw", "undirected", None), (3, 200, 15, "sssp", "undirected", None),
+    (2, 1000, 20, "fw", "undirected", "s1:8"), (8, 1100, 21, "fw", "undirected", "s1:16"),
     # ... in groups of g rounds, one row all-gather per group ("s<g>:<rest launches>"; a sharded
     # plan pads to whole block-rows a rank: 8 ranks 16 block-rows, the last group of 3 ragged)
     (2, 1000, 16, "fw", "undirected", "s2:4"), (3, 1300, 17, "fw", "undirected", "s4:3"),
@@ -68,9 +70,11 @@ def test_sharded_build_matches_oracle(world, n, seed, algo, wide, group):
 def test_symmetric_sharded_full_tile_chain():
     """The symmetric schedule's chain with full-tile cross / p2row launches
     (SRT_FW_SYM_SMALL=0; the default at >= 4096 own tiles a rank, i.e. 2 ranks
-    at 16k) -- small graphs otherwise take the packed quarter-tile chain."""
+    at 16k) -- small graphs otherwise take the packed quarter-tile chain; one
+    round per all-gather (SRT_FW_SYM_GROUP=1: the grouped schedule always runs
+    the quarter-tile chain)."""
     port = _port()
-    env = dict(os.environ, SRT_FW_SYM_SMALL="0")
+    env = dict(os.environ, SRT_FW_SYM_SMALL="0", SRT_FW_SYM_GROUP="1")
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker.py"), str(r), "2", str(port), "400",
                                "16", "torch", "fw", "undirected"], env=env, stdout=subprocess.PIPE,
                               stderr=subprocess.STDOUT, text=True) for r in range(2)]
