@@ -154,9 +154,7 @@ typedef struct {
     uint32_t sharded_tail;      /* dense, comm bound: 1 = the loss pass ran on this rank's own
                                    closure rows (no key all-gather; tight-edge lists and
                                    u32 + f32 table rows exchanged), 0 = replicated */
-    uint32_t sparse_split;      /* sparse: 1 = the split sweep's table (u16 latency sweep, then the
-                                   loss sweep over tight edges), 0 = the fused u64 sweep (the split
-                                   one saturated or is turned off) */
+    uint32_t sparse_split;      /* reserved, 0 (an earlier split latency/loss sweep, removed) */
     uint64_t sparse_sweeps;     /* sparse: sweep launches of the last run, summed over its source
                                    launches (each covers every group in flight) */
     uint32_t loss_fold;         /* dense: 1 = the level fold (tight edges walked by weight class

@@ -471,7 +471,7 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_in_ptr);
     hipFree(p->d_in_edge);
     hipFree(p->d_sD);
-    hipFree(p->d_scl);
+    hipFree(p->d_spend);
     hipFree(p->d_smask);
     hipFree(p->d_sflag);
     hipFree(p->d_sact);
@@ -829,10 +829,6 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b)
             budget_mb = std::max<uint64_t>(64, std::min<uint64_t>(budget_mb, (free_b >> 20) / 8));
         if (const char *e = std::getenv("SRT_SSSP_MB")) budget_mb = (uint64_t)std::atoll(e);
-        // the sweep variants and their knobs (measurement / A-B parity only):
-        // SRT_SSSP_CL=1 the compact-list sweep, SRT_SSSP_SPLIT=1 the split sweep
-        if (const char *ev = std::getenv("SRT_SSSP_SPLIT")) p->sssp_split = std::atoi(ev) != 0;
-        if (const char *ev = std::getenv("SRT_SSSP_CL")) p->sssp_cl = std::atoi(ev) != 0;
         const uint32_t R = (rmax >= 4 && words >= 4) ? 4 : (rmax >= 2 && words >= 2) ? 2 : 1;
         const uint64_t per_group = (uint64_t)p->V * 64 * 8 * R;
         uint64_t G = std::max<uint64_t>(1, (budget_mb << 20) / std::max<uint64_t>(per_group, 1));
@@ -841,9 +837,7 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         p->sssp_r = R;
         p->sssp_nb = (uint32_t)(G * R);
         p->n_in_edges = n_in;
-        std::snprintf(d, sizeof d, "sssp:lat32|f32 g=%llu V=%u n=%u E_in=%llu R=%u groups=%u state=%s",
-                      (unsigned long long)p->sssp_g, p->V, n, (unsigned long long)n_in, p->sssp_r,
-                      p->sssp_nb / p->sssp_r, p->sssp_cl ? "planes+lists" : "keys");
+        d[0] = '\0';  // named once the bucket width is known (below)
     }
     p->desc = d;
     tr.mark("create: key/algo choice");
@@ -873,15 +867,27 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         PLAN_TRY(dmalloc(&p->d_sD, (size_t)p->sssp_nb * p->V * 64, err));
         PLAN_TRY(dmalloc(&p->d_smask, (size_t)2 * p->sssp_nb * p->V, err));
         PLAN_TRY(dmalloc(&p->d_sflag, (size_t)3 * p->sssp_nb, err));
-        if (const char *ev = std::getenv("SRT_SSSP_LOSS_ACT")) p->sssp_loss_act = std::atoi(ev) != 0;
-        if (const char *ev = std::getenv("SRT_SSSP_TB")) p->sssp_tb = std::atoi(ev) != 0;
-        if (const char *ev = std::getenv("SRT_SSSP_ALT")) p->sssp_alt = std::atoi(ev) != 0;
+        PLAN_TRY(dmalloc(&p->d_spend, (size_t)p->sssp_nb * p->V, err));
+        {
+            // delta: a quarter of the mean in-edge latency (units of g), knob
+            // SRT_SSSP_DELTA = another factor (0: ungated sweeps)
+            double f = 0.25;
+            if (const char *ev = std::getenv("SRT_SSSP_DELTA")) f = std::atof(ev);
+            double sum = 0.0;
+            for (const srt::InEdge &ie : in_edge) sum += ie.w;
+            const double mean = in_edge.empty() ? 0.0 : sum / (double)in_edge.size();
+            p->sssp_delta = f > 0.0 ? (uint32_t)std::max(1.0, std::min(mean * f, 1e9)) : 0u;
+        }
+        char dd[256];
+        std::snprintf(dd, sizeof dd, "sssp:lat32|f32 g=%llu V=%u n=%u E_in=%llu R=%u groups=%u delta=%u",
+                      (unsigned long long)p->sssp_g, p->V, p->n, (unsigned long long)p->n_in_edges, p->sssp_r,
+                      p->sssp_nb / p->sssp_r, p->sssp_delta);
+        p->desc = dd;
         if (const char *ev = std::getenv("SRT_SSSP_ACT")) {
             const int k = std::atoi(ev);
             p->sssp_act_on = k != 0;
             p->sssp_act_from = k > 1 ? (uint32_t)k : 0u;
         }
-        if (p->sssp_cl) PLAN_TRY(dmalloc(&p->d_scl, (size_t)2 * p->sssp_nb * p->V * 64, err));
         if (p->sssp_act_on) PLAN_TRY(dmalloc(&p->d_sact, (size_t)3 * (p->sssp_nb / p->sssp_r) * p->V, err));
         if ((e = hipHostMalloc((void **)&p->h_sflag, (size_t)p->sssp_nb * sizeof(uint32_t), 0)) != hipSuccess) {
             srt_plan_destroy(p);
@@ -1099,7 +1105,7 @@ srt_status srt_plan_timing(const srt_plan *p, srt_timing *o) {
     o->loss_ms = p->loss_ms;
     o->tight_edges = p->algo == SRT_ALGO_FW ? p->t_edges : 0;
     o->sharded_tail = p->algo == SRT_ALGO_FW && p->shard_tail ? 1u : 0u;
-    o->sparse_split = p->algo == SRT_ALGO_SSSP && p->sssp_used_split ? 1u : 0u;
+    o->sparse_split = 0u;  // the split sweep was removed (reserved)
     o->sparse_sweeps = p->algo == SRT_ALGO_SSSP ? p->sssp_sweeps : 0;
     o->loss_fold = p->algo == SRT_ALGO_FW && p->t_level ? 1u : 0u;
     o->reserved0 = 0;

@@ -196,16 +196,11 @@ struct srt_plan {
     uint32_t sssp_r = 1;                 // 64-source words per lane (group = 64 * sssp_r sources)
     uint64_t sssp_g = 1;                 // latency unit
     uint64_t sssp_sweeps = 0;            // sweeps of the last run (all groups)
-    uint64_t sssp_loss_sweeps = 0;       // split: loss sweeps of the last run
-    bool sssp_split = false;             // u16 latency sweep + loss sweep (knob SRT_SSSP_SPLIT=1; C4: 1.88 s vs
-                                         // 1.51 s fused -- the loss sweeps are as many as the latency ones)
-    bool sssp_used_split = false;        // the last run's table came from the split sweep
-    bool sssp_loss_act = true;           // split: target activation in the loss sweeps (SRT_SSSP_LOSS_ACT=0 off)
-    bool sssp_tb = true;                 // split: precomputed tight bits for the loss sweeps (SRT_SSSP_TB=0 off)
-    bool sssp_alt = false;               // sweeps alternate target order (SRT_SSSP_ALT=1; C4: no gain)
-    bool sssp_cl = false;                // fused sweep reads changed keys from compact lists (SRT_SSSP_CL=1;
-                                         // C4: FETCH -32%, same time -- see srt_sssp.hip)
-    uint64_t *d_scl = nullptr;           // compact lists: 2 (parity) * sssp_nb * V * 64 keys
+    // delta-stepping bucket width in latency units (0: ungated sweeps); host
+    // default = a quarter of the mean in-edge latency (knob SRT_SSSP_DELTA =
+    // the factor, 0 off)
+    uint32_t sssp_delta = 0;
+    uint64_t *d_spend = nullptr;         // sssp_nb * V pending-key masks (delta-stepping)
     // table rows this rank computes ([0, n) single-GPU); the table is allocated
     // with rows_alloc >= n rows so the row all-gather has equal chunks
     uint32_t row0 = 0, row1 = 0, rows_alloc = 0;

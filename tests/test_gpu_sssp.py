@@ -17,19 +17,18 @@ pytestmark = pytest.mark.gpu
 SSSP = _lib.SRT_ALGO_SSSP
 
 
-@pytest.fixture(autouse=True, params=["split", "fused", "lists"])
+@pytest.fixture(autouse=True, params=["delta", "ungated", "fine"])
 def sweep_mode(request, monkeypatch):
-    """Every test runs the three sparse sweeps: the fused sweep over u64 keys
-    (the default, and the split sweep's fallback), the fused sweep with
-    latency / loss planes and compact change lists (SRT_SSSP_CL=1) and the
-    split one (SRT_SSSP_SPLIT=1: u16 latency sweep, then the loss sweep over
-    tight edges)."""
-    monkeypatch.delenv("SRT_SSSP_SPLIT", raising=False)
-    monkeypatch.delenv("SRT_SSSP_CL", raising=False)
-    if request.param == "split":
-        monkeypatch.setenv("SRT_SSSP_SPLIT", "1")
-    elif request.param == "lists":
-        monkeypatch.setenv("SRT_SSSP_CL", "1")
+    """Every test runs the sweep three ways: delta-stepping at the default
+    bucket width (a quarter of the mean in-edge latency), ungated
+    (SRT_SSSP_DELTA=0: every improved key moves on at once) and with very
+    narrow buckets (factor 0.01: most keys wait in the pending masks for
+    many sweeps).  All three must give the same bits."""
+    monkeypatch.delenv("SRT_SSSP_DELTA", raising=False)
+    if request.param == "ungated":
+        monkeypatch.setenv("SRT_SSSP_DELTA", "0")
+    elif request.param == "fine":
+        monkeypatch.setenv("SRT_SSSP_DELTA", "0.01")
     return request.param
 
 
@@ -187,10 +186,9 @@ def test_target_activation_bit_exact(monkeypatch, act, directed):
     _check(edges, nodes, directed, n)
 
 
-def test_split_saturation_falls_back(sweep_mode):
-    """Path latencies past the split sweep's u16 range (a 90-node ring of
-    1,000-2,000 ns edges, gcd 1: the far side is ~67k units away) saturate it;
-    the rows are rebuilt by the fused u64 sweep, bit-exact."""
+def test_long_ring(sweep_mode):
+    """A 90-node ring of 1,000-2,000 ns edges (gcd 1: the far side is ~67k
+    latency units away, thousands of narrow buckets deep), bit-exact."""
     n = 90
     rng = np.random.default_rng(5)
     src = np.concatenate([np.arange(n), np.arange(n)]).astype(np.uint32)
@@ -199,26 +197,14 @@ def test_split_saturation_falls_back(sweep_mode):
     loss = rng.uniform(0, 0.05, 2 * n).astype(np.float32)
     nodes = np.arange(n, dtype=np.uint32)
     _check((src, dst, lat, loss), nodes, False, n)
-    g = NetworkGraph.from_edges(n, src, dst, lat, loss, directed=False)
-    plan = RoutingPlan(g, nodes, algo=SSSP).run()
-    assert plan.timing()["sparse_split"] == 0
-    plan.close()
 
 
-def test_split_sweep_is_used(sweep_mode):
-    src, dst, lat, loss = synth.barabasi_albert(3000, 4, 4)
-    g = NetworkGraph.from_edges(3000, src, dst, lat, loss)
-    plan = RoutingPlan(g, np.arange(300, dtype=np.uint32), algo=SSSP).run()
-    assert plan.timing()["sparse_split"] == (1 if sweep_mode == "split" else 0)
-    plan.close()
-
-
-def test_state_layout_is_reported(sweep_mode):
-    """The plan names the fused sweep's state layout: u64 keys by default, two
-    planes + compact change lists under SRT_SSSP_CL=1."""
+def test_delta_is_reported(sweep_mode):
+    """The plan names its bucket width: 0 when ungated, else >= 1 unit."""
     src, dst, lat, loss = synth.barabasi_albert(500, 3, 9)
     g = NetworkGraph.from_edges(500, src, dst, lat, loss)
     plan = RoutingPlan(g, np.arange(100, dtype=np.uint32), algo=SSSP)
-    want = "state=planes+lists" if sweep_mode == "lists" else "state=keys"
-    assert want in plan.describe()
+    delta = int(plan.describe().split(" delta=")[1].split()[0])
+    assert (delta == 0) == (sweep_mode == "ungated"), plan.describe()
     plan.close()
+
