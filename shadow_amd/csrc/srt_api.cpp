@@ -866,17 +866,25 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         PLAN_TRY(dmalloc(&p->d_in_edge, in_edge.size(), err));
         PLAN_TRY(dmalloc(&p->d_sD, (size_t)p->sssp_nb * p->V * 64, err));
         PLAN_TRY(dmalloc(&p->d_smask, (size_t)2 * p->sssp_nb * p->V, err));
-        PLAN_TRY(dmalloc(&p->d_sflag, (size_t)3 * p->sssp_nb, err));
+        PLAN_TRY(dmalloc(&p->d_sflag, (size_t)12 * p->sssp_nb, err));  // flags + delta-stepping ring
         PLAN_TRY(dmalloc(&p->d_spend, (size_t)p->sssp_nb * p->V, err));
         {
-            // delta: a quarter of the mean in-edge latency (units of g), knob
-            // SRT_SSSP_DELTA = another factor (0: ungated sweeps)
-            double f = 0.25;
+            // delta-stepping bucket width = SRT_SSSP_DELTA x the mean in-edge
+            // latency (units of g); default 0 = ungated sweeps, the faster on
+            // C4 (100k BA, one GPU: ungated 1.60 s, factor 0.25 / 1.0 1.68 s --
+            // fewer relaxations but not fewer gathered lines)
+            double f = 0.0;
             if (const char *ev = std::getenv("SRT_SSSP_DELTA")) f = std::atof(ev);
             double sum = 0.0;
             for (const srt::InEdge &ie : in_edge) sum += ie.w;
             const double mean = in_edge.empty() ? 0.0 : sum / (double)in_edge.size();
             p->sssp_delta = f > 0.0 ? (uint32_t)std::max(1.0, std::min(mean * f, 1e9)) : 0u;
+            // sweep bound: V + 2 Bellman-Ford sweeps once the threshold passes
+            // the longest simple path, plus the sweeps it takes to get there
+            uint64_t wmax = 0;
+            for (const srt::InEdge &ie : in_edge) wmax = std::max<uint64_t>(wmax, ie.w);
+            p->sssp_tmax = (uint64_t)p->V + 4;
+            if (p->sssp_delta) p->sssp_tmax += (uint64_t)p->V * wmax / p->sssp_delta + 2;
         }
         char dd[256];
         std::snprintf(dd, sizeof dd, "sssp:lat32|f32 g=%llu V=%u n=%u E_in=%llu R=%u groups=%u delta=%u",

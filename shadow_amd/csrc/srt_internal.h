@@ -187,7 +187,7 @@ struct srt_plan {
     uint64_t n_in_edges = 0;
     uint64_t *d_sD = nullptr;            // sssp_nb * V * 64 keys
     uint64_t *d_smask = nullptr;         // 2 * sssp_nb * V change masks
-    uint32_t *d_sflag = nullptr;         // 3 * sssp_nb convergence flags
+    uint32_t *d_sflag = nullptr;         // 12 * sssp_nb: convergence flags + delta ring (srt_sssp.hip)
     uint8_t *d_sact = nullptr;           // 3 * groups * V target-activation bytes (tail sweeps)
     bool sssp_act_on = true;             // knob SRT_SSSP_ACT=0 turns target activation off
     uint32_t sssp_act_from = 0;          // knob SRT_SSSP_ACT=k>1: from sweep k (0: from the last launch)
@@ -196,10 +196,10 @@ struct srt_plan {
     uint32_t sssp_r = 1;                 // 64-source words per lane (group = 64 * sssp_r sources)
     uint64_t sssp_g = 1;                 // latency unit
     uint64_t sssp_sweeps = 0;            // sweeps of the last run (all groups)
-    // delta-stepping bucket width in latency units (0: ungated sweeps); host
-    // default = a quarter of the mean in-edge latency (knob SRT_SSSP_DELTA =
-    // the factor, 0 off)
+    // delta-stepping bucket width in latency units (0: ungated sweeps, the
+    // default); knob SRT_SSSP_DELTA = the factor of the mean in-edge latency
     uint32_t sssp_delta = 0;
+    uint64_t sssp_tmax = 0;              // sweep count past which the sweep reports non-convergence
     uint64_t *d_spend = nullptr;         // sssp_nb * V pending-key masks (delta-stepping)
     // table rows this rank computes ([0, n) single-GPU); the table is allocated
     // with rows_alloc >= n rows so the row all-gather has equal chunks

@@ -62,7 +62,8 @@ __global__ void sssp_init_kernel(uint64_t *__restrict__ D, uint64_t *__restrict_
         D[e] = SKEY_INF;
         if (e < nM) mask[e] = 0;
         if (e < nM / 2) pend[e] = 0;
-        if (e < 3ull * G) flag[e] = 0;
+        // flags, thresholds and prop flags 0, pending minima ~0 (srt_sweep_kernel)
+        if (e < 12ull * G) flag[e] = (e >= 6ull * G && e < 9ull * G) ? ~0u : 0u;
     }
 }
 
@@ -106,6 +107,15 @@ constexpr uint32_t ACT_USE = 1, ACT_SET = 2;
 // key moves it to the change mask.  The fixpoint -- and so every key -- is
 // the one of the ungated sweep: a key still pending keeps the group's flag
 // set, and the threshold grows without bound.
+//
+// Empty buckets are skipped: flag[] holds, after the 3 convergence slots, per
+// ring slot and group the threshold the sweep used (theta), the smallest
+// pending latency it left (pmin, one atomicMin a wave) and whether it moved
+// any key on (prop).  theta_0 = 2 delta; theta_t = theta_{t-1} + delta, or, if
+// sweep t-1 moved nothing, at least pmin_{t-1} + delta -- so the next pending
+// key moves at once instead of after (pmin - theta) / delta idle sweeps.  Every
+// wave derives theta_t from the same slot values; block 0 stores it.
+
 template <int R>
 __global__ __launch_bounds__(SWP_WAVES * 64) void sssp_sweep_kernel(
     const uint64_t *__restrict__ in_ptr, const InEdge *__restrict__ in_edge, uint32_t V,
@@ -113,8 +123,26 @@ __global__ __launch_bounds__(SWP_WAVES * 64) void sssp_sweep_kernel(
     uint32_t *flag, uint32_t t, uint32_t delta, const uint64_t *__restrict__ row_ptr,
     const uint32_t *__restrict__ col, uint8_t *act, uint32_t act_mode) {
     const uint32_t g = blockIdx.y, G = gridDim.y;
-    if (blockIdx.x == 0 && threadIdx.x == 0) flag[((t + 1) % 3) * G + g] = 0;  // for sweep t+1
-    if (t > 0 && flag[((t + 2) % 3) * G + g] == 0) return;                     // converged
+    uint32_t *theta = flag + 3 * G, *pmin = flag + 6 * G, *prop = flag + 9 * G;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // slots of sweep t+1
+        flag[((t + 1) % 3) * G + g] = 0;
+        pmin[((t + 1) % 3) * G + g] = ~0u;
+        prop[((t + 1) % 3) * G + g] = 0;
+    }
+    if (t > 0 && flag[((t + 2) % 3) * G + g] == 0) return;  // converged
+    // this sweep's threshold (see above); saturates below the u32 latency range
+    uint64_t th = ~0ull;
+    if (delta) {
+        if (t == 0) {
+            th = 2ull * delta;
+        } else {
+            const uint32_t ps = ((t + 2) % 3) * G + g;
+            th = (uint64_t)theta[ps] + delta;
+            if (prop[ps] == 0 && pmin[ps] != ~0u) th = th > (uint64_t)pmin[ps] + delta ? th : (uint64_t)pmin[ps] + delta;
+            th = th < 0xFFFFFFFFull ? th : 0xFFFFFFFFull;
+        }
+        if (blockIdx.x == 0 && threadIdx.x == 0) theta[(t % 3) * G + g] = (uint32_t)th;
+    }
     const int lane = threadIdx.x & 63;
     // Plain block order on purpose: an XCD-contiguous remap (each XCD sweeping
     // its own run of vertices) measured 2x slower on C4 (1.52 -> 2.9 s) -- all
@@ -124,11 +152,22 @@ __global__ __launch_bounds__(SWP_WAVES * 64) void sssp_sweep_kernel(
     const uint32_t v = vi;
     const uint64_t base = (uint64_t)g * V;  // first vertex row of the group
     const uint64_t aslot = (uint64_t)G * V;  // bytes per ring slot
+    bool skip_walk = false;
     if (act_mode & (ACT_USE | ACT_SET)) {
         if (lane == 0) act[((t + 2) % 3) * aslot + base + v] = 0;
         if ((act_mode & ACT_USE) && act[(t % 3) * aslot + base + v] == 0) {
-            if (lane < R) mask_next[(base + v) * R + lane] = 0;
-            return;
+            // no in-neighbour changed: only pending keys (delta-stepping) can
+            // move on, which needs no in-edge walk
+            bool pend_only = false;
+            if (delta) {
+                uint64_t pw = lane < R ? pend[(base + v) * R + lane] : 0ull;
+                pend_only = __ballot(pw != 0) != 0;
+            }
+            if (!pend_only) {
+                if (lane < R) mask_next[(base + v) * R + lane] = 0;
+                return;
+            }
+            skip_walk = true;
         }
     }
     const uint64_t *Dg = D + base * R * 64;
@@ -136,7 +175,7 @@ __global__ __launch_bounds__(SWP_WAVES * 64) void sssp_sweep_kernel(
     uint64_t best[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) best[r] = SKEY_INF;
-    const uint64_t e0 = in_ptr[v], e1 = in_ptr[v + 1];
+    const uint64_t e0 = in_ptr[v], e1 = skip_walk ? e0 : in_ptr[v + 1];
     for (uint64_t c0 = e0; c0 < e1; c0 += 64) {
         const uint64_t k = c0 + lane;
         uint32_t eu = 0, ew = 0;
@@ -196,25 +235,28 @@ __global__ __launch_bounds__(SWP_WAVES * 64) void sssp_sweep_kernel(
         }
     }
     uint64_t *Dv = D + ((base + v) * R) * 64 + lane;
-    // the threshold of sweep t + 1 (saturating: no wrap for long sweeps)
-    const uint64_t th = delta ? (uint64_t)(t + 2) * delta : ~0ull;
     bool prop_any = false, pend_any = false;
+    uint32_t pl = ~0u;  // smallest pending latency of this lane
     uint64_t m_out[R], p_out[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         bool imp = false;
-        uint64_t cur = Dv[r * 64];
+        // pending keys of this word (one broadcast load; none without delta)
+        const uint64_t pw = delta ? pend[(base + v) * R + r] : 0ull;
+        const bool pb = (pw >> lane) & 1ull;
+        // own key: only lanes with a candidate or a pending key read it
+        uint64_t cur = SKEY_INF;
+        if (best[r] != SKEY_INF || pb) cur = Dv[r * 64];
         if (best[r] != SKEY_INF && best[r] < cur) {
             Dv[r * 64] = best[r];
             cur = best[r];
             imp = true;
         }
-        // pending keys of this word (one broadcast load; none without delta)
-        const uint64_t pw = delta ? pend[(base + v) * R + r] : 0ull;
-        const bool cand = imp || ((pw >> lane) & 1ull);
+        const bool cand = imp || pb;
         const bool go = cand && (cur >> 32) < th;
         m_out[r] = __ballot(go);
         p_out[r] = __ballot(cand && !go);
+        if (cand && !go) pl = (uint32_t)(cur >> 32) < pl ? (uint32_t)(cur >> 32) : pl;
         prop_any |= m_out[r] != 0;
         pend_any |= p_out[r] != 0;
     }
@@ -224,15 +266,27 @@ __global__ __launch_bounds__(SWP_WAVES * 64) void sssp_sweep_kernel(
             mask_next[(base + v) * R + r] = m_out[r];
             if (delta) pend[(base + v) * R + r] = p_out[r];
         }
-        if (prop_any || pend_any) flag[(t % 3) * G + g] = 1;  // idempotent store, no atomic
+        // idempotent stores, no atomics; every wave of the group hits the same
+        // word, so read first and write only while it is still 0 (a hot line
+        // written by every wave serialises in its L2 channel)
+        uint32_t *fl = &flag[(t % 3) * G + g], *pr = &prop[(t % 3) * G + g];
+        if ((prop_any || pend_any) && __builtin_nontemporal_load(fl) == 0) *fl = 1;
+        if (prop_any && __builtin_nontemporal_load(pr) == 0) *pr = 1;
+    }
+    if (pend_any) {
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint32_t o = __shfl_xor(pl, off);
+            pl = o < pl ? o : pl;
+        }
+        uint32_t *pm = &pmin[(t % 3) * G + g];
+        if (lane == 0 && pl < __builtin_nontemporal_load(pm)) atomicMin(pm, pl);
     }
     if (act_mode & ACT_SET) {
         uint8_t *nxt = act + ((t + 1) % 3) * aslot + base;
-        if (pend_any && lane == 0) nxt[v] = 1;  // visit v again: its pending keys
         if (prop_any) {
             for (uint64_t k = row_ptr[v] + lane; k < row_ptr[v + 1]; k += 64) {
                 const uint32_t w = col[k];
-                if (w != v) nxt[w] = 1;
+                if (w != v && nxt[w] == 0) nxt[w] = 1;  // hubs: read before the store (hot lines)
             }
         }
     }
@@ -358,7 +412,7 @@ srt_status sweep_until_converged(srt_plan *p, uint32_t G, uint32_t chunk, F swee
         bool any = false;
         for (uint32_t b = 0; b < G; ++b) any |= p->h_sflag[b] != 0;
         if (!any) break;
-        if (t > p->V + 2) {  // Bellman-Ford bound: cannot happen with positive latencies
+        if (t > p->sssp_tmax) {  // Bellman-Ford + bucket bound: cannot happen with positive latencies
             if (err) {
                 err->code = SRT_ERR_INVALID;
                 std::snprintf(err->msg, sizeof err->msg, "sssp did not converge after %u sweeps", t);

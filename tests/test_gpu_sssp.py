@@ -17,16 +17,16 @@ pytestmark = pytest.mark.gpu
 SSSP = _lib.SRT_ALGO_SSSP
 
 
-@pytest.fixture(autouse=True, params=["delta", "ungated", "fine"])
+@pytest.fixture(autouse=True, params=["ungated", "delta", "fine"])
 def sweep_mode(request, monkeypatch):
-    """Every test runs the sweep three ways: delta-stepping at the default
-    bucket width (a quarter of the mean in-edge latency), ungated
-    (SRT_SSSP_DELTA=0: every improved key moves on at once) and with very
-    narrow buckets (factor 0.01: most keys wait in the pending masks for
-    many sweeps).  All three must give the same bits."""
+    """Every test runs the sweep three ways: ungated (the default: every
+    improved key moves on at once), delta-stepping at a quarter of the mean
+    in-edge latency (SRT_SSSP_DELTA=0.25) and with very narrow buckets (factor
+    0.01: most keys wait in the pending masks for many sweeps, and empty
+    buckets are skipped).  All three must give the same bits."""
     monkeypatch.delenv("SRT_SSSP_DELTA", raising=False)
-    if request.param == "ungated":
-        monkeypatch.setenv("SRT_SSSP_DELTA", "0")
+    if request.param == "delta":
+        monkeypatch.setenv("SRT_SSSP_DELTA", "0.25")
     elif request.param == "fine":
         monkeypatch.setenv("SRT_SSSP_DELTA", "0.01")
     return request.param
