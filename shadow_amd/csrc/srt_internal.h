@@ -247,6 +247,7 @@ struct srt_plan {
     // table rows travel as u32 latency units + f32 loss and are expanded into
     // the table on every rank
     bool shard_tail = false;               // this run used the sharded tail
+    bool tail_expanded = false;            // ... and expanded its chunks behind their all-gathers
     std::vector<uint32_t> lrow_cnt;        // per rank: loss-pass rows
     uint32_t lrow_max = 0;                 // staging rows per rank (tail_q chunks of tail_cr rows)
     uint32_t tail_q = 1, tail_cr = 0;      // the fold runs in tail_q chunks; chunk c's all-gather

@@ -1564,6 +1564,31 @@ srt_status tight_csr_shard_t(srt_plan *p, unsigned long long *d_stats, bool *sha
     return SRT_OK;
 }
 
+// staged slots [s0, s0 + slots) into the table, on the main stream
+void expand_slots(srt_plan *p, size_t s0, uint32_t slots) {
+    if (!slots || !p->n) return;
+    const size_t lb = p->stage16 ? 2 : 4;
+    hipLaunchKernelGGL(expand_rows_kernel, dim3(std::min<uint32_t>(slots, 4096)), dim3(256), 0, p->stream,
+                       p->d_lrows + s0, slots, p->n,
+                       (const void *)(reinterpret_cast<const uint8_t *>(p->d_slat) + s0 * p->n * lb), p->stage16,
+                       p->d_sloss + s0 * p->n, p->kp.g, p->d_out_lat, p->d_out_loss,
+                       p->stage_loss_only ? reinterpret_cast<const uint16_t *>(p->d_D) : nullptr, p->Vp, p->d_nodes,
+                       p->d_sl_lat);
+}
+
+// chunk c of the staging into the table as soon as its all-gather is done
+// (ev_tail[q + c]): the expansion of chunk c overlaps the all-gathers of the
+// later chunks (emulated C3, 8 ranks: the 1.4 ms expansion was serial after
+// the last all-gather)
+void expand_chunks_behind(srt_plan *p, uint32_t W) {
+    const uint32_t q = p->tail_q, cr = p->tail_cr;
+    for (uint32_t c = 0; c < q; ++c) {
+        (void)hipStreamWaitEvent(p->stream, p->ev_tail[q + c], 0);
+        expand_slots(p, (size_t)c * W * cr, W * cr);
+    }
+    p->tail_expanded = true;
+}
+
 template <typename K>
 srt_status loss_sharded_t(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     bool sharded = false;
@@ -1616,9 +1641,9 @@ srt_status loss_sharded_t(srt_plan *p, unsigned long long *d_stats, srt_err *err
                                           err)) != SRT_OK) ||
             (st = comm_allgather_inplace(p->comm, p->d_sloss + base, cbytes, C, err)) != SRT_OK)
             return st;
+        (void)hipEventRecord(p->ev_tail[q + c], C);
     }
-    (void)hipEventRecord(p->ev_tail[q], C);
-    (void)hipStreamWaitEvent(M, p->ev_tail[q], 0);
+    expand_chunks_behind(p, W);
     p->shard_tail = true;
     return SRT_OK;
 }
@@ -1714,9 +1739,9 @@ srt_status loss_emulated_t(srt_plan *p, unsigned long long *d_stats, srt_err *er
         (void)hipEventRecord(p->ev_tail[c], M);
         (void)hipStreamWaitEvent(Cs, p->ev_tail[c], 0);
         allgather_on((double)cr * p->n * (4.0 + lb), Cs);  // latency units + loss
+        (void)hipEventRecord(p->ev_tail[q + c], Cs);
     }
-    (void)hipEventRecord(p->ev_tail[q], Cs);
-    (void)hipStreamWaitEvent(M, p->ev_tail[q], 0);
+    expand_chunks_behind(p, W);  // emulation: the others' slots are stale (same volume)
     allgather(16.0);  // rank stats
     p->shard_tail = true;
     return SRT_OK;
@@ -1724,14 +1749,7 @@ srt_status loss_emulated_t(srt_plan *p, unsigned long long *d_stats, srt_err *er
 
 }  // namespace
 
-void expand_shard_rows(srt_plan *p, int nranks) {
-    const uint32_t slots = (uint32_t)nranks * p->lrow_max;
-    if (!slots || !p->n) return;
-    hipLaunchKernelGGL(expand_rows_kernel, dim3(std::min<uint32_t>(slots, 4096)), dim3(256), 0, p->stream, p->d_lrows,
-                       slots, p->n, (const void *)p->d_slat, p->stage16, p->d_sloss, p->kp.g, p->d_out_lat,
-                       p->d_out_loss, p->stage_loss_only ? reinterpret_cast<const uint16_t *>(p->d_D) : nullptr,
-                       p->Vp, p->d_nodes, p->d_sl_lat);
-}
+void expand_shard_rows(srt_plan *p, int nranks) { expand_slots(p, 0, (uint32_t)nranks * p->lrow_max); }
 
 srt_status fw_loss(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     if (!p->ev_loss0) {
@@ -1741,6 +1759,7 @@ srt_status fw_loss(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     (void)hipEventRecord(p->ev_loss0, p->stream);
     srt_status st;
     p->shard_tail = false;
+    p->tail_expanded = false;
     if (p->comm) {
         if (p->key_type == KEY_U16) st = loss_sharded_t<uint16_t>(p, d_stats, err);
         else if (p->key_type == KEY_U32) st = loss_sharded_t<uint32_t>(p, d_stats, err);
