@@ -241,19 +241,20 @@ srt_status srt_packet_batch(srt_plan *plan, const srt_pkt *d_pkts, const uint32_
  * packet (UINT64_MAX for packets not sent); order[0 .. n_sent): the sent
  * packets' indices grouped by destination host, each group in pop order;
  * dst_ptr[0 .. n_dst_hosts]: group offsets (dst_ptr[n_dst_hosts] = n_sent).
- * Asynchronous on the plan's stream (it never waits for the device): the sort
- * key holds deliver - (the batch's earliest) in 48 - ceil(log2(n_dst_hosts+1))
- * bits (10k hosts: 34 bits, 17 s); a batch spanning more, or a sent packet
- * whose destination is out of range, is flagged: call srt_packet_events_status
- * before reading the results (it redoes a wide batch exactly). */
+ * Asynchronous on the plan's stream (it never waits for the device): each
+ * destination's group is sorted in on-chip memory; a group of more than 1024
+ * events, or a sent packet whose destination is out of range, is flagged:
+ * call srt_packet_events_status before reading the results (it redoes a batch
+ * with a big group exactly).  The unsent tail of order[] is unspecified. */
 srt_status srt_packet_events(srt_plan *plan, const uint32_t *d_host_pkt_ptr, uint32_t n_hosts, uint64_t n_pkts,
                              const uint32_t *d_flags, const uint64_t *d_deliver, const uint32_t *d_dst_host,
                              uint32_t n_dst_hosts, uint64_t *d_event_base, uint64_t *d_event_id,
                              uint32_t *d_order, uint32_t *d_dst_ptr, srt_err *err);
 /* Synchronises the plan's stream: SRT_ERR_INVALID ("destination host index
  * out of range") if an srt_packet_events call since the last check met one;
- * if the last call's deliver times overflowed the key, redoes that call's sort
- * exactly (its arrays must still be valid) and returns SRT_OK; else SRT_OK. */
+ * if the last call had a destination group too big for the on-chip sort,
+ * redoes that call's sort exactly (its arrays must still be valid) and
+ * returns SRT_OK; else SRT_OK. */
 srt_status srt_packet_events_status(srt_plan *plan, srt_err *err);
 
 /* ------------------------------------------------------------- RoutingInfo */

@@ -147,8 +147,8 @@ struct srt_plan {
     uint32_t *d_up32 = nullptr;             // u32 latency slots of the piece-pipelined upload
     uint64_t *d_draws = nullptr;            // packet stage: one RNG draw per packet
     uint64_t draws_cap = 0;
-    void *d_ev_scratch = nullptr;           // packet events: sort keys + rocPRIM temp
-    uint32_t *d_ev_bad = nullptr;    // srt_packet_events: bit 0 a destination out of range, bit 1 time span
+    void *d_ev_scratch = nullptr;           // packet events: per-destination counts + cursors
+    uint32_t *d_ev_bad = nullptr;    // srt_packet_events: bit 0 a destination out of range, bit 2 a group over EV_CAP
     struct EvCall {                  // the last srt_packet_events call (exact fallback)
         const uint32_t *flags;
         const uint64_t *deliver;

@@ -71,9 +71,11 @@ def _plan():
 
 
 @gpu
-@pytest.mark.parametrize("seed", [1, 2])
-def test_gpu_events_random_batch(seed):
-    host_ptr, flags, deliver, dst, n_dst, base = _random_batch(seed, n_hosts=300, n_pkts=50_000, n_dst=200)
+@pytest.mark.parametrize("seed,n_dst", [(1, 200), (2, 200), (3, 20_000)])
+def test_gpu_events_random_batch(seed, n_dst):
+    """200 destinations: the chunked LDS count / scatter; 20,000 (more than
+    its LDS histogram holds): the global-atomic count / scatter."""
+    host_ptr, flags, deliver, dst, n_dst, base = _random_batch(seed, n_hosts=300, n_pkts=50_000, n_dst=n_dst)
     plan = _plan()
     ob = base.copy()
     eid_o, ord_o, ptr_o = O.packet_events(host_ptr, flags, deliver, dst, n_dst, ob)
@@ -140,9 +142,26 @@ def test_gpu_events_edge_cases():
 
 
 @gpu
+def test_gpu_events_big_group():
+    """one destination receives far more than the on-chip group sort holds
+    (1024 events): the call flags it and the status check redoes the batch
+    with the exact two-sort path; the small groups beside it stay exact."""
+    host_ptr, flags, deliver, dst, n_dst, base = _random_batch(5, n_hosts=60, n_pkts=12_000, n_dst=30)
+    dst = dst.copy()
+    dst[::2] = 7  # ~4,200 sent events to destination 7
+    plan = _plan()
+    ob = base.copy()
+    eid_o, ord_o, ptr_o = O.packet_events(host_ptr, flags, deliver, dst, n_dst, ob)
+    eid, order, ptr, nb = _gpu_events(plan, host_ptr, flags, deliver, dst, n_dst, base)
+    assert ptr_o[8] - ptr_o[7] > 1024
+    assert np.array_equal(eid, eid_o) and np.array_equal(order, ord_o) and np.array_equal(ptr, ptr_o)
+    assert np.array_equal(nb, ob)
+
+
+@gpu
 def test_gpu_events_wide_time_span():
-    """deliver times spanning ~2^60 ns with 40 destinations: the time and
-    destination bits exceed 64, so the two-sort path runs."""
+    """deliver times spanning ~2^60 ns: the group sort compares full 64-bit
+    deliver times (no time-field width)."""
     host_ptr, flags, deliver, dst, n_dst, base = _random_batch(4, n_hosts=50, n_pkts=20_000, n_dst=40)
     rng = np.random.default_rng(4)
     deliver = (rng.integers(0, 8, size=len(deliver)).astype(np.uint64) << np.uint64(57)) + deliver
