@@ -469,6 +469,7 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_fbuf);
     hipFree(p->d_draws);
     hipFree(p->d_in_ptr);
+    hipFree(p->d_sperm);
     hipFree(p->d_in_edge);
     hipFree(p->d_sD);
     hipFree(p->d_spend);
@@ -539,6 +540,41 @@ void build_in_edges(const srt_csr *g, uint64_t gunit, uint64_t n_in, std::vector
             e.pad = 0;
             (*edges)[fill[v]++] = e;
         }
+}
+
+// Breadth-first discovery rank of every vertex over the adjacency, from the
+// highest-degree vertex (then from the lowest-numbered unvisited one): the
+// sparse sweep puts table rows in this order into its 64-source words, so a
+// word's sources are graph neighbours / siblings whose labels change at the
+// same vertices in the same sweeps (fewer 128-B lines gathered per change).
+std::vector<uint32_t> bfs_rank(const srt_csr *g) {
+    const uint32_t V = g->n_nodes;
+    std::vector<uint32_t> rank(V, ~0u), q;
+    q.reserve(V);
+    uint32_t start = 0;
+    uint64_t best = 0;
+    for (uint32_t u = 0; u < V; ++u)
+        if (g->row_ptr[u + 1] - g->row_ptr[u] > best) best = g->row_ptr[u + 1] - g->row_ptr[u], start = u;
+    uint32_t next = 0;
+    for (uint32_t root = start, scan = 0; next < V;) {
+        if (rank[root] == ~0u) {
+            rank[root] = next++;
+            q.push_back(root);
+            for (size_t h = q.size() - 1; h < q.size(); ++h) {
+                const uint32_t u = q[h];
+                for (uint64_t k = g->row_ptr[u]; k < g->row_ptr[u + 1]; ++k) {
+                    const uint32_t v = g->col[k];
+                    if (v < V && rank[v] == ~0u) {
+                        rank[v] = next++;
+                        q.push_back(v);
+                    }
+                }
+            }
+        }
+        while (scan < V && rank[scan] != ~0u) ++scan;
+        root = scan;
+    }
+    return rank;
 }
 
 }  // namespace
@@ -620,25 +656,7 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         p->device = dev;
         hipError_t e = hipSetDevice(dev);
         if (e != hipSuccess) return hip_fail(err, e, "hipSetDevice");
-        // measurement knob SRT_FW_CHAIN_CUS=c: the main stream (phase-3 rest) is
-        // kept off c CUs so the look-ahead chain on the side stream never waits
-        // for a CU slot (SRT_FW_CHAIN_CU_STRIDE=1: reserved CUs spread evenly
-        // over the mask, else the last c bits)
-        if (const char *ce = std::getenv("SRT_FW_CHAIN_CUS"); ce && std::atoi(ce) > 0) {
-            hipDeviceProp_t prop;
-            int ncu = 256;
-            if (hipGetDeviceProperties(&prop, dev) == hipSuccess) ncu = prop.multiProcessorCount;
-            const int c = std::min(std::atoi(ce), ncu - 1);
-            const bool stride = std::getenv("SRT_FW_CHAIN_CU_STRIDE") != nullptr;
-            std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-            for (int i = 0; i < ncu; ++i) {
-                const bool reserved = stride ? (i % (ncu / c) == 0 && i / (ncu / c) < c) : i >= ncu - c;
-                if (!reserved) mask[i / 32] |= 1u << (i % 32);
-            }
-            e = hipExtStreamCreateWithCUMask(&p->stream, (uint32_t)mask.size(), mask.data());
-        } else {
-            e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
-        }
+        e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
         if (e != hipSuccess) return hip_fail(err, e, "hipStreamCreate");
         p->own_stream = true;
         int lo = 0, hi = 0;
@@ -648,10 +666,9 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         if (e != hipSuccess) return hip_fail(err, e, "hipStreamCreateWithPriority");
         (void)hipEventCreate(&p->ev_begin);
         (void)hipEventCreate(&p->ev_end);
-        // knob SRT_FW_SYNC_FENCE=dev (measurement): the stream-to-stream events
-        // of the look-ahead schedule skip the system-scope fence (same device)
-        const unsigned sync_fl =
-            hipEventDisableTiming | (std::getenv("SRT_FW_SYNC_FENCE") ? hipEventDisableSystemFence : 0u);
+        // the stream-to-stream events of the look-ahead schedule (the
+        // system-scope fence is kept: skipping it measured no faster)
+        const unsigned sync_fl = hipEventDisableTiming;
         (void)hipEventCreateWithFlags(&p->ev_cross, sync_fl);
         (void)hipEventCreateWithFlags(&p->ev_pivot, sync_fl);
         (void)hipEventCreateWithFlags(&p->ev_row, sync_fl);
@@ -793,15 +810,11 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         }
         if (const char *e = std::getenv("SRT_FW_BAND")) p->fw_band = e[0] == '1';
         if (const char *e = std::getenv("SRT_FW_XCD")) p->fw_xcd = e[0] != '0';
-        if (const char *e = std::getenv("SRT_FW_SQ_XCD")) p->fw_sq_xcd = e[0] == '1';
         if (const char *e = std::getenv("SRT_FW_BAND_H")) {
             const int h = std::atoi(e);
             p->fw_band_h = 1;
             while (p->fw_band_h * 2 <= (uint32_t)std::min(h, 64)) p->fw_band_h *= 2;
         }
-        if (const char *e = std::getenv("SRT_FW_RELAX")) p->fw_relax = std::atoi(e);
-        if (const char *e = std::getenv("SRT_LOSS_PUSH")) p->loss_push = std::atoi(e) != 0;
-        if (const char *e = std::getenv("SRT_FW_ABLATE")) p->fw_ablate = (uint32_t)std::atoi(e) & 15u;
         std::snprintf(d, sizeof d, "fw:%s B=%d g=%llu lmax=%llu%s V=%u n=%u stage=%s band=%d loss=tight-dag%s",
                       p->fw_f16                     ? "f16key"
                       : p->key_type == srt::KEY_U16 ? "u16key"
@@ -862,6 +875,9 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         std::vector<uint64_t> in_ptr;
         std::vector<srt::InEdge> in_edge;
         build_in_edges(g, p->sssp_g, n_in, &in_ptr, &in_edge);
+        // source order of the sweep's words (knob SRT_SSSP_ORDER=0: table order)
+        if (!(std::getenv("SRT_SSSP_ORDER") && std::atoi(std::getenv("SRT_SSSP_ORDER")) == 0))
+            p->h_bfs_rank = bfs_rank(g);
         PLAN_TRY(dmalloc(&p->d_in_ptr, in_ptr.size(), err));
         PLAN_TRY(dmalloc(&p->d_in_edge, in_edge.size(), err));
         PLAN_TRY(dmalloc(&p->d_sD, (size_t)p->sssp_nb * p->V * 64, err));

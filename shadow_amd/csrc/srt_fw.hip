@@ -821,63 +821,19 @@ __device__ __forceinline__ void relax_quad32(uint32_t &c0, uint32_t &c1, uint32_
           "v"(b1.w));
 }
 
-// 8 adds t[c] = a + b0[c] / b1[c] (c < 4) into 8 temporaries
-__device__ __forceinline__ void add8_32(uint32_t (&t)[8], uint32_t a, u32x4 b0, u32x4 b1) {
-    asm volatile(
-        "v_add_u32 %0, %8, %9\n\t"
-        "v_add_u32 %1, %8, %10\n\t"
-        "v_add_u32 %2, %8, %11\n\t"
-        "v_add_u32 %3, %8, %12\n\t"
-        "v_add_u32 %4, %8, %13\n\t"
-        "v_add_u32 %5, %8, %14\n\t"
-        "v_add_u32 %6, %8, %15\n\t"
-        "v_add_u32 %7, %8, %16"
-        : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "=&v"(t[5]), "=&v"(t[6]), "=&v"(t[7])
-        : "v"(a), "v"(b0.x), "v"(b0.y), "v"(b0.z), "v"(b0.w), "v"(b1.x), "v"(b1.y), "v"(b1.z), "v"(b1.w));
-}
-
-// acc[c] = min3(acc[c], t[c], u[c]), c < 8
-__device__ __forceinline__ void min8_32(uint32_t (&acc)[8], const uint32_t (&t)[8], const uint32_t (&u)[8]) {
-    asm volatile(
-        "v_min3_u32 %0, %0, %8, %16\n\t"
-        "v_min3_u32 %1, %1, %9, %17\n\t"
-        "v_min3_u32 %2, %2, %10, %18\n\t"
-        "v_min3_u32 %3, %3, %11, %19\n\t"
-        "v_min3_u32 %4, %4, %12, %20\n\t"
-        "v_min3_u32 %5, %5, %13, %21\n\t"
-        "v_min3_u32 %6, %6, %14, %22\n\t"
-        "v_min3_u32 %7, %7, %15, %23"
-        : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[6]),
-          "+v"(acc[7])
-        : "v"(t[0]), "v"(t[1]), "v"(t[2]), "v"(t[3]), "v"(t[4]), "v"(t[5]), "v"(t[6]), "v"(t[7]), "v"(u[0]),
-          "v"(u[1]), "v"(u[2]), "v"(u[3]), "v"(u[4]), "v"(u[5]), "v"(u[6]), "v"(u[7]));
-}
-
-template <int s, int RV>
+template <int s>
 __device__ __forceinline__ void chunk_steps32(uint32_t (&acc)[8][8], StepOps32 (&o)[2], uint32_t abase,
                                               uint32_t bbase) {
     if constexpr (s < KC32 / 2) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if constexpr (s + 1 < KC32 / 2) lds_step32<s + 1>(o[(s + 1) & 1], abase, bbase);
         const StepOps32 &c = o[s & 1];
-        if constexpr (RV == 0) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                relax_quad32(acc[i][0], acc[i][1], acc[i][2], acc[i][3], c.a[i].x, c.a[i].y, c.b[0], c.b[2]);
-                relax_quad32(acc[i][4], acc[i][5], acc[i][6], acc[i][7], c.a[i].x, c.a[i].y, c.b[1], c.b[3]);
-            }
-        } else {
-            // a row's 16 adds (k, k+1) before its 8 min3: each min3 reads
-            // sums produced >= 8 instructions earlier
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                uint32_t t[8], u[8];
-                add8_32(t, c.a[i].x, c.b[0], c.b[1]);
-                add8_32(u, c.a[i].y, c.b[2], c.b[3]);
-                min8_32(acc[i], t, u);
-            }
+        for (int i = 0; i < 8; ++i) {
+            relax_quad32(acc[i][0], acc[i][1], acc[i][2], acc[i][3], c.a[i].x, c.a[i].y, c.b[0], c.b[2]);
+            relax_quad32(acc[i][4], acc[i][5], acc[i][6], acc[i][7], c.a[i].x, c.a[i].y, c.b[1], c.b[3]);
         }
-        chunk_steps32<s + 1, RV>(acc, o, abase, bbase);
+        chunk_steps32<s + 1>(acc, o, abase, bbase);
     }
 }
 
@@ -887,7 +843,7 @@ __device__ __forceinline__ void tile_of(uint32_t t, const Rect &r1, const Rect &
                                         uint32_t &bj) {
     const uint32_t n1 = r1.r.n * r1.c.n;
     if (t < n1) {
-        if (gridDim.x == n1 && n1 >= 64 && !(ng & (1u << 26))) {  // bit 26: no remap (plan field fw_sq_xcd)
+        if (gridDim.x == n1 && n1 >= 64 && !(ng & (1u << 26))) {  // bit 26: no remap (rest launches)
             const uint32_t q = n1 / 8, rr = n1 % 8, xcd = t % 8;
             t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + t / 8;
         }
@@ -907,7 +863,7 @@ __device__ __forceinline__ void tile_of(uint32_t t, const Rect &r1, const Rect &
     }
 }
 
-template <int TAG, int RV = 0>
+template <int TAG>
 __global__ __launch_bounds__(NT3, 2) void minplus_u32_kernel(uint32_t *__restrict__ D, uint32_t Vp, uint32_t kb,
                                                                Rect r1, Rect r2, uint32_t ng) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[2 * GBUF32];
@@ -930,19 +886,11 @@ __global__ __launch_bounds__(NT3, 2) void minplus_u32_kernel(uint32_t *__restric
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int tx = tid % 16, ty = tid / 16;
 
-    // measurement-only ablations (bits 20.., knob SRT_FW_ABLATE; the closure
-    // is wrong with any of them): 1 no C load, 2 no C store, 4 no chunk
-    // staging after the first, 8 no per-chunk wait + barrier
-    const uint32_t abl = ng >> 20;
     uint32_t acc[8][8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const uint32_t *src = D + (i0 + ty + 16 * i) * Vp + j0 + tx * 4;
-        u32x4 lo = {0x3fffffffu, 0x3fffffffu, 0x3fffffffu, 0x3fffffffu}, hi = lo;
-        if (!(abl & 1)) {
-            lo = *reinterpret_cast<const u32x4 *>(src);
-            hi = *reinterpret_cast<const u32x4 *>(src + 64);
-        }
+        const u32x4 lo = *reinterpret_cast<const u32x4 *>(src), hi = *reinterpret_cast<const u32x4 *>(src + 64);
         acc[i][0] = lo.x;
         acc[i][1] = lo.y;
         acc[i][2] = lo.z;
@@ -978,20 +926,17 @@ __global__ __launch_bounds__(NT3, 2) void minplus_u32_kernel(uint32_t *__restric
 #pragma unroll 1
     for (int ch = ch0; ch < ch1; ++ch) {
         const int cur = (ch - ch0) & 1;
-        if (ch + 1 < ch1 && !(abl & 4)) stage(ch + 1, cur ^ 1);  // the other buffer's readers passed the last barrier
+        if (ch + 1 < ch1 ) stage(ch + 1, cur ^ 1);  // the other buffer's readers passed the last barrier
         const uint32_t *As = lds + cur * GBUF32 + ty * KC32;      // row ty of piece 0
         const uint32_t *Bs = lds + cur * GBUF32 + AIMG32 + tx * 4;  // columns tx*4 of k-row 0
         const uint32_t abase = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t *)As;
         const uint32_t bbase = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t *)Bs;
         StepOps32 o[2];
         lds_step32<0>(o[0], abase, bbase);
-        chunk_steps32<0, RV>(acc, o, abase, bbase);
-        if (!(abl & 8)) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-        }
+        chunk_steps32<0>(acc, o, abase, bbase);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
     }
-    if (abl & 2) return;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         uint32_t *dst = D + (i0 + ty + 16 * i) * Vp + j0 + tx * 4;
@@ -1407,13 +1352,11 @@ __global__ __launch_bounds__(NT3, 2) void minplus_u16_kernel(uint16_t *__restric
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int tx = tid % 16, ty = tid / 16;
-    const uint32_t abl = ng >> 20;  // measurement-only ablations, as the u32 kernel
 
     uint32_t acc[8][4];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        u32x4 v = {0x3fff3fffu, 0x3fff3fffu, 0x3fff3fffu, 0x3fff3fffu};
-        if (!(abl & 1)) v = *reinterpret_cast<const u32x4 *>(D + (i0 + ty + 16 * i) * Vp + j0 + tx * 8);
+        const u32x4 v = *reinterpret_cast<const u32x4 *>(D + (i0 + ty + 16 * i) * Vp + j0 + tx * 8);
         acc[i][0] = v.x;
         acc[i][1] = v.y;
         acc[i][2] = v.z;
@@ -1445,7 +1388,7 @@ __global__ __launch_bounds__(NT3, 2) void minplus_u16_kernel(uint16_t *__restric
 #pragma unroll 1
     for (int ch = ch0; ch < ch1; ++ch) {
         const int cur = (ch - ch0) & 1;
-        if (ch + 1 < ch1 && !(abl & 4)) stage(ch + 1, cur ^ 1);  // the other buffer's readers passed the last barrier
+        if (ch + 1 < ch1 ) stage(ch + 1, cur ^ 1);  // the other buffer's readers passed the last barrier
         const uint16_t *As = lds + cur * GBUF16 + ty * KC16;      // row ty of piece 0
         const uint16_t *Bs = lds + cur * GBUF16 + AIMG16 + tx * 8;  // columns tx*8 of k-row 0
         const uint32_t abase = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint16_t *)As;
@@ -1453,12 +1396,9 @@ __global__ __launch_bounds__(NT3, 2) void minplus_u16_kernel(uint16_t *__restric
         StepOps16 o[2];
         lds_step16<0>(o[0], abase, bbase);
         chunk_steps16<0, F16>(acc, o, abase, bbase);
-        if (!(abl & 8)) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
     }
-    if (abl & 2) return;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         u32x4 v;
@@ -2460,8 +2400,8 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
     const size_t need = 2 * (size_t)nblk + 2;
     while (p->ev.size() < need) {
         hipEvent_t e;
-        // timing-only events: no system-scope fence (knob SRT_FW_TIMING_FENCE=sys restores it)
-        hipEventCreateWithFlags(&e, std::getenv("SRT_FW_TIMING_FENCE") ? 0u : (unsigned)hipEventDisableSystemFence);
+        // timing-only events: no system-scope fence
+        hipEventCreateWithFlags(&e, (unsigned)hipEventDisableSystemFence);
         p->ev.push_back(e);
     }
     // phase-1 rows per thread (knob SRT_FW_P1_ROWS in {2,4,8}, measurement only)
@@ -2632,8 +2572,8 @@ void launch_group(srt_plan *p, hipStream_t s, uint32_t a, uint32_t g, const Rect
     // bit 16: banded tile order (plan knob SRT_FW_BAND=0 turns it off for A/B timing)
     // bit 24: XCD remap of the triangle order (knob SRT_FW_XCD=1, A/B timing)
     const uint32_t arg = g | (p->fw_band ? 0x10000u : 0u) | band_bits(p->fw_band_h) |
-                         (chain ? 0u : p->fw_ablate << 20) | (p->fw_xcd ? 1u << 24 : 0u) |
-                         (p->fw_sq_xcd || chain ? 0u : 1u << 26);
+                         (p->fw_xcd ? 1u << 24 : 0u) |
+                         (chain ? 0u : 1u << 26);
     if constexpr (sizeof(K) == 2) {
         if (chain && p->fw_sym)  // r1 only; its transposes are r2 (fw_rounds_group_t)
             hipLaunchKernelGGL((u16k<5, 2>(p->fw_f16)), dim3(r1.r.n * r1.c.n), dim3(NT3), 0, s, D, p->Vp, a, r1,
@@ -2648,8 +2588,6 @@ void launch_group(srt_plan *p, hipStream_t s, uint32_t a, uint32_t g, const Rect
     } else if constexpr (sizeof(K) == 4) {
         if (chain)
             hipLaunchKernelGGL((minplus_u32_kernel<5>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
-        else if (p->fw_relax)
-            hipLaunchKernelGGL((minplus_u32_kernel<0, 1>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
         else
             hipLaunchKernelGGL((minplus_u32_kernel<0>), dim3(n), dim3(NT3), 0, s, D, p->Vp, a, r1, r2, arg);
     } else {
@@ -2694,7 +2632,7 @@ srt_status fw_rounds_group_t(srt_plan *p, int p1r, uint32_t g) {
     const size_t need = 2 * (nblk / g) + 2;
     while (p->ev.size() < need) {
         hipEvent_t e;
-        hipEventCreateWithFlags(&e, std::getenv("SRT_FW_TIMING_FENCE") ? 0u : (unsigned)hipEventDisableSystemFence);
+        hipEventCreateWithFlags(&e, (unsigned)hipEventDisableSystemFence);
         p->ev.push_back(e);
     }
     pivots(M, 0);
@@ -2812,7 +2750,7 @@ srt_status fw_rounds_group_sharded_t(srt_plan *p, int p1r, uint32_t g, uint32_t 
     const size_t need = 2 * (nblk / g) + 2;
     while (p->ev.size() < need) {
         hipEvent_t e;
-        hipEventCreateWithFlags(&e, std::getenv("SRT_FW_TIMING_FENCE") ? 0u : (unsigned)hipEventDisableSystemFence);
+        hipEventCreateWithFlags(&e, (unsigned)hipEventDisableSystemFence);
         p->ev.push_back(e);
     }
     auto chain = [&](hipStream_t s, uint32_t a) -> srt_status {

@@ -106,14 +106,11 @@ struct srt_plan {
     uint32_t tl_max = 0, tl_own = 0;
     uint16_t *d_rowslots = nullptr;    // N x ceil(nblk / N) tiles: the per-round row exchange
     uint16_t *d_fbuf = nullptr;        // N x tl_max tiles: the final exchange
-    int fw_relax = 0;             // u32 rest kernel relax order (SRT_FW_RELAX, A/B)
-    uint32_t fw_ablate = 0;       // measurement only: u32 rest-kernel ablations (SRT_FW_ABLATE, see the kernel)
     bool fw_xcd = false;          // triangle rest: XCD remap of the order (knob SRT_FW_XCD=1, A/B timing)
     // square rest order: plain row-major, dealt round-robin over the XCDs, by
     // default -- C3 forced square (SRT_FW_SYM=0), rest per build: remapped +
     // banded 119.3 ms, remapped 120.5, neither 117.9 (the remap concentrates
     // the group's short tiles on one XCD; see the triangle order in srt_fw.hip)
-    bool fw_sq_xcd = false;       // square rest: XCD remap of the order (knob SRT_FW_SQ_XCD=1, A/B timing)
     uint32_t fw_band_h = 1;       // triangle rest: rows per band (power of 2, knob SRT_FW_BAND_H, read at create)
     bool fw_band = false;         // grouped launches: banded tile order (knob SRT_FW_BAND=1, read at create)
     uint32_t emulate_ranks = 0;   // measurement only, see fw_rounds_t
@@ -183,6 +180,9 @@ struct srt_plan {
 
     // sparse SSSP (algo == SRT_ALGO_SSSP, srt_sssp.hip)
     uint64_t *d_in_ptr = nullptr;        // V + 1
+    std::vector<uint32_t> h_bfs_rank;    // BFS discovery rank per vertex (empty: table order)
+    uint32_t *d_sperm = nullptr;         // n: sweep slot q -> table row (rows [sperm_r0, sperm_r1) permuted)
+    uint32_t sperm_r0 = 0, sperm_r1 = 0;
     srt::InEdge *d_in_edge = nullptr;    // n_in_edges (self-loops dropped)
     uint64_t n_in_edges = 0;
     uint64_t *d_sD = nullptr;            // sssp_nb * V * 64 keys
@@ -222,7 +222,6 @@ struct srt_plan {
     uint64_t *d_tmaxw = nullptr;     // max latency (units) of a tight edge
     uint64_t t_cap = 0, t_edges = 0; // capacity / tight edges of the last run
     bool t_packed = false;           // the last run used the packed, w-sorted form
-    bool loss_push = true;           // fold in push form over tight OUT-edges (knob SRT_LOSS_PUSH=0: pull)
     bool t_push = false;             // the last run's CSR is the push form (rows by source)
     uint64_t *h_tcount = nullptr;    // pinned: [0] total tight edges, [1] max tight latency
     // level fold (srt_loss.hip level_loss_kernel): the tight edges grouped by

@@ -1333,18 +1333,13 @@ srt_status build_tight_rows(srt_plan *p, uint64_t slots, uint32_t ubits, uint64_
         return SRT_OK;
     }
     (void)hipMemsetAsync(p->d_tcnt, 0, (size_t)V * 4, M);
-    if (p->loss_push)
-        hipLaunchKernelGGL(tight_list_count_kernel<true>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tcnt);
-    else
-        hipLaunchKernelGGL(tight_list_count_kernel<false>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tcnt);
+    // push form: CSR over tight OUT-edges (the pull form over in-edges
+    // measured slower and was removed)
+    hipLaunchKernelGGL(tight_list_count_kernel<true>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tcnt);
     hipLaunchKernelGGL(tight_scan_kernel, dim3(1), dim3(1024), 0, M, p->d_tcnt, p->d_tptr, V);
-    if (p->loss_push)
-        hipLaunchKernelGGL(tight_list_fill_kernel<true>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tptr,
-                           p->d_tcnt, p->d_tpk2, ubits);
-    else
-        hipLaunchKernelGGL(tight_list_fill_kernel<false>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tptr,
-                           p->d_tcnt, p->d_tpk2, ubits);
-    p->t_push = p->loss_push;
+    hipLaunchKernelGGL(tight_list_fill_kernel<true>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tptr,
+                       p->d_tcnt, p->d_tpk2, ubits);
+    p->t_push = true;
     return sort_packed(p, ubits, maxw, err);
 }
 
@@ -1432,7 +1427,7 @@ srt_status tight_csr_t(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     }
     p->t_push = false;
     p->t_level = false;
-    if (p->loss_push && V && !std::getenv("SRT_LOSS_UNPACKED")) {
+    if (V && !std::getenv("SRT_LOSS_UNPACKED")) {
         bool done = false;
         if ((st = tight_csr_push_t<K>(p, d_stats, &done, err)) != SRT_OK || done) return st;
     }

@@ -69,14 +69,15 @@ __global__ void sssp_init_kernel(uint64_t *__restrict__ D, uint64_t *__restrict_
 
 // source row row0 + q (q = (g*R + r)*64 + s) -> group g, word r, lane s:
 // D[g][v][r][s], mask[g][v][r]
+// (perm: sweep slot -> table row, the BFS source order; null = identity)
 __global__ void sssp_seed_kernel(uint64_t *__restrict__ D, uint64_t *__restrict__ mask,
-                                 const uint32_t *__restrict__ nodes, uint32_t V, uint32_t row0,
-                                 uint32_t row1, uint32_t nbat, uint32_t R) {
+                                 const uint32_t *__restrict__ nodes, const uint32_t *__restrict__ perm, uint32_t V,
+                                 uint32_t row0, uint32_t row1, uint32_t nbat, uint32_t R) {
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nbat * 64) return;
     const uint32_t g = q / (64 * R), r = (q / 64) % R, s = q % 64;
     if (row0 + q >= row1) return;
-    const uint32_t src = nodes[row0 + q];
+    const uint32_t src = nodes[perm ? perm[row0 + q] : row0 + q];
     const uint64_t row = (uint64_t)g * V + src;
     D[(row * R + r) * 64 + s] = 0ull;  // (0 ns, 0.0 loss): petgraph's zero score
     mask[row * R + r] = 1ull << s;     // sources within a word are distinct nodes
@@ -299,8 +300,9 @@ __global__ __launch_bounds__(SWP_WAVES * 64) void sssp_sweep_kernel(
 // and unreachable count (the assert at mod.rs:219) are block-reduced into
 // stats[0] (min) / stats[1] (count).  blockIdx.y = g*R + r.
 __global__ __launch_bounds__(256) void sssp_emit_kernel(
-    const uint64_t *__restrict__ D, uint32_t V, uint32_t R, const uint32_t *__restrict__ nodes, uint32_t n,
-    uint32_t row0, uint32_t row1, uint64_t gunit, const uint64_t *__restrict__ sl_lat,
+    const uint64_t *__restrict__ D, uint32_t V, uint32_t R, const uint32_t *__restrict__ nodes,
+    const uint32_t *__restrict__ perm, uint32_t n, uint32_t row0, uint32_t row1, uint64_t gunit,
+    const uint64_t *__restrict__ sl_lat,
     const float *__restrict__ sl_loss, uint64_t *__restrict__ out_lat, float *__restrict__ out_loss,
     unsigned long long *stats) {
     __shared__ uint64_t tile[64][65];
@@ -320,8 +322,9 @@ __global__ __launch_bounds__(256) void sssp_emit_kernel(
     unsigned long long unreach = 0;
     for (int idx = tid; idx < 64 * 64; idx += 256) {
         const int s = idx / 64, jj = idx % 64;
-        const uint32_t j = j0 + jj, row = row0 + b * 64 + s;
-        if (j >= n || row >= row1) continue;
+        const uint32_t j = j0 + jj, q = row0 + b * 64 + s;
+        if (j >= n || q >= row1) continue;
+        const uint32_t row = perm ? perm[q] : q;
         uint64_t lat;
         float loss;
         if (row == j) {
@@ -434,6 +437,29 @@ srt_status sssp_pass(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     p->p3_launches = 0;
     p->p3_work = 0.0;
     p->sssp_sweeps = 0;
+    // the BFS source order of this rank's rows (built once per row range)
+    const uint32_t *perm = nullptr;
+    if (!p->h_bfs_rank.empty() && p->row1 > p->row0) {
+        if (!p->d_sperm || p->sperm_r0 != p->row0 || p->sperm_r1 != p->row1) {
+            std::vector<uint32_t> pm(p->n);
+            for (uint32_t i = 0; i < p->n; ++i) pm[i] = i;
+            std::stable_sort(pm.begin() + p->row0, pm.begin() + p->row1, [&](uint32_t a, uint32_t b) {
+                return p->h_bfs_rank[p->nodes[a]] < p->h_bfs_rank[p->nodes[b]];
+            });
+            hipError_t e = p->d_sperm ? hipSuccess : hipMalloc(&p->d_sperm, (size_t)p->n * 4);
+            if (e == hipSuccess) e = hipMemcpy(p->d_sperm, pm.data(), (size_t)p->n * 4, hipMemcpyHostToDevice);
+            if (e != hipSuccess) {
+                if (err) {
+                    err->code = SRT_ERR_HIP;
+                    std::snprintf(err->msg, sizeof err->msg, "sssp source order: %s", hipGetErrorString(e));
+                }
+                return SRT_ERR_HIP;
+            }
+            p->sperm_r0 = p->row0;
+            p->sperm_r1 = p->row1;
+        }
+        perm = p->d_sperm;
+    }
     hipLaunchKernelGGL(sssp_stats_init_kernel, dim3(1), dim3(1), 0, M, d_stats);
     const uint32_t launches = (p->row1 - p->row0 + per_launch - 1) / per_launch;
     while (p->ev.size() < 2 * (size_t)launches) {
@@ -450,7 +476,7 @@ srt_status sssp_pass(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
         hipLaunchKernelGGL(sssp_init_kernel, dim3(4096), dim3(256), 0, M, p->d_sD, p->d_smask, p->d_spend, p->d_sflag,
                            V, G * R, G);
         hipLaunchKernelGGL(sssp_seed_kernel, dim3((nbat * 64 + 255) / 256), dim3(256), 0, M, p->d_sD, p->d_smask,
-                           p->d_nodes, V, g0, g0 + rows, nbat, R);
+                           p->d_nodes, perm, V, g0, g0 + rows, nbat, R);
         if (p->sssp_act_on) (void)hipMemsetAsync(p->d_sact, 0, 3ull * G * V, M);
         (void)hipEventRecord(p->ev[2 * li], M);
         const dim3 grid((V + SWP_WAVES - 1) / SWP_WAVES, G);
@@ -476,7 +502,7 @@ srt_status sssp_pass(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
         (void)hipEventRecord(p->ev[2 * li + 1], M);
         p->p3_launches++;
         hipLaunchKernelGGL(sssp_emit_kernel, dim3((p->n + 63) / 64, G * R), dim3(256), 0, M, p->d_sD, V, R,
-                           p->d_nodes, p->n, g0, g0 + rows, p->sssp_g, p->d_sl_lat, p->d_sl_loss, p->d_out_lat,
+                           p->d_nodes, perm, p->n, g0, g0 + rows, p->sssp_g, p->d_sl_lat, p->d_sl_loss, p->d_out_lat,
                            p->d_out_loss, d_stats);
     }
     // algorithmic bytes: 12 B per in-edge + 12 B per vertex, per source

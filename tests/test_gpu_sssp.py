@@ -25,8 +25,10 @@ def sweep_mode(request, monkeypatch):
     0.01: most keys wait in the pending masks for many sweeps, and empty
     buckets are skipped).  All three must give the same bits."""
     monkeypatch.delenv("SRT_SSSP_DELTA", raising=False)
+    monkeypatch.delenv("SRT_SSSP_ORDER", raising=False)
     if request.param == "delta":
         monkeypatch.setenv("SRT_SSSP_DELTA", "0.25")
+        monkeypatch.setenv("SRT_SSSP_ORDER", "0")  # sources in table order (default: BFS order)
     elif request.param == "fine":
         monkeypatch.setenv("SRT_SSSP_DELTA", "0.01")
     return request.param
