@@ -508,7 +508,8 @@ def bench_graph(args, cfg, D):
             launches_per_step = k_launches // max(args.steps, 1)
             sweeps_per_launch = timing["sparse_sweeps"] / max(launches_per_step, 1)
             state = desc.split("state=")[1].split()[0] if "state=" in desc else "keys"
-            schedule = {"state": state, "words_per_lane": int(desc.split(" R=")[1].split()[0]) if " R=" in desc else 0}
+            schedule = {"state": state, "words_per_lane": int(desc.split(" R=")[1].split()[0]) if " R=" in desc else 0,
+                        "source_order": "bfs" if "order=bfs" in desc else "table"}
             per_sweep, traffic_src = measured_traffic(args, "(sssp_sweep)", schedule)
             roofline = {
                 "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",

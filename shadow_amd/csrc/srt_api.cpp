@@ -903,9 +903,9 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
             if (p->sssp_delta) p->sssp_tmax += (uint64_t)p->V * wmax / p->sssp_delta + 2;
         }
         char dd[256];
-        std::snprintf(dd, sizeof dd, "sssp:lat32|f32 g=%llu V=%u n=%u E_in=%llu R=%u groups=%u delta=%u",
+        std::snprintf(dd, sizeof dd, "sssp:lat32|f32 g=%llu V=%u n=%u E_in=%llu R=%u groups=%u delta=%u order=%s",
                       (unsigned long long)p->sssp_g, p->V, p->n, (unsigned long long)p->n_in_edges, p->sssp_r,
-                      p->sssp_nb / p->sssp_r, p->sssp_delta);
+                      p->sssp_nb / p->sssp_r, p->sssp_delta, p->h_bfs_rank.empty() ? "table" : "bfs");
         p->desc = dd;
         if (const char *ev = std::getenv("SRT_SSSP_ACT")) {
             const int k = std::atoi(ev);
