@@ -182,9 +182,7 @@ __global__ __launch_bounds__(1024) void event_chunk_scatter_kernel(const uint32_
                                                                    const uint32_t *__restrict__ loc,
                                                                    const uint32_t *__restrict__ part,
                                                                    uint32_t *__restrict__ dst_ptr,
-                                                                   const uint64_t *__restrict__ deliver,
-                                                                   uint32_t *__restrict__ order,
-                                                                   uint64_t *__restrict__ gkey) {
+                                                                   uint32_t *__restrict__ order) {
     extern __shared__ uint32_t c[];  // n_dst cursors, then the block prefixes
     const uint32_t nparts = (n_dst + 63) / 64;
     uint32_t *pbase = c + n_dst;
@@ -216,11 +214,7 @@ __global__ __launch_bounds__(1024) void event_chunk_scatter_kernel(const uint32_
     for (uint32_t p = p0 + threadIdx.x; p < p1; p += blockDim.x)
         if (flags[p] == SRT_PDS_INET_SENT) {
             const uint32_t d = dst[p];
-            if (d < n_dst) {
-                const uint32_t pos = atomicAdd(&c[d], 1u);
-                order[pos] = p;
-                gkey[pos] = deliver[p];  // coalesced read; the group sort then reads its keys contiguously
-            }
+            if (d < n_dst) order[atomicAdd(&c[d], 1u)] = p;
         }
 }
 
@@ -228,16 +222,11 @@ __global__ __launch_bounds__(1024) void event_chunk_scatter_kernel(const uint32_
 // global-atomic form, for more than EV_LDS_DST destinations)
 __global__ void event_scatter_kernel(const uint32_t *__restrict__ flags, const uint32_t *__restrict__ dst,
                                      uint32_t n_dst, uint32_t n, uint32_t *__restrict__ cur,
-                                     const uint64_t *__restrict__ deliver, uint32_t *__restrict__ order,
-                                     uint64_t *__restrict__ gkey) {
+                                     uint32_t *__restrict__ order) {
     for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
         if (flags[p] != SRT_PDS_INET_SENT) continue;
         const uint32_t d = dst[p];
-        if (d < n_dst) {
-            const uint32_t pos = atomicAdd(&cur[d], 1u);
-            order[pos] = p;
-            gkey[pos] = deliver[p];
-        }
+        if (d < n_dst) order[atomicAdd(&cur[d], 1u)] = p;
     }
 }
 
@@ -251,11 +240,12 @@ __global__ void event_scatter_kernel(const uint32_t *__restrict__ flags, const u
 constexpr uint32_t EV_SMALL = 256;
 
 template <uint32_t CAP>
-__device__ __forceinline__ void group_rank_sort(uint32_t b, uint32_t m, const uint64_t *__restrict__ gkey,
+__device__ __forceinline__ void group_rank_sort(uint32_t b, uint32_t m, const uint64_t *__restrict__ deliver,
                                                 uint32_t *__restrict__ order, uint64_t *key, uint32_t *idx) {
-    for (uint32_t i = threadIdx.x; i < m; i += 64) {  // gkey[b + i] = deliver[order[b + i]] (the scatter wrote it)
-        idx[i] = order[b + i];
-        key[i] = gkey[b + i];
+    for (uint32_t i = threadIdx.x; i < m; i += 64) {
+        const uint32_t p = order[b + i];
+        idx[i] = p;
+        key[i] = deliver[p];
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < m; i += 64) {
@@ -273,7 +263,7 @@ __device__ __forceinline__ void group_rank_sort(uint32_t b, uint32_t m, const ui
 // one single-wave workgroup per destination (four destinations per 256-lane
 // workgroup measured slower: 24.4 against 21.0 us on C5)
 __global__ __launch_bounds__(64) void event_group_sort_kernel(const uint32_t *__restrict__ dst_ptr,
-                                                              const uint64_t *__restrict__ gkey,
+                                                              const uint64_t *__restrict__ deliver,
                                                               uint32_t *__restrict__ order, uint32_t *__restrict__ big) {
     __shared__ uint64_t key[EV_SMALL];
     __shared__ uint32_t idx[EV_SMALL];
@@ -283,11 +273,11 @@ __global__ __launch_bounds__(64) void event_group_sort_kernel(const uint32_t *__
         if (threadIdx.x == 0) big[1 + atomicAdd(&big[0], 1u)] = d;
         return;
     }
-    group_rank_sort<EV_SMALL>(b, m, gkey, order, key, idx);
+    group_rank_sort<EV_SMALL>(b, m, deliver, order, key, idx);
 }
 
 __global__ __launch_bounds__(64) void event_big_group_sort_kernel(const uint32_t *__restrict__ dst_ptr,
-                                                                  const uint64_t *__restrict__ gkey,
+                                                                  const uint64_t *__restrict__ deliver,
                                                                   uint32_t *__restrict__ order,
                                                                   const uint32_t *__restrict__ big,
                                                                   uint32_t *__restrict__ bad) {
@@ -300,7 +290,7 @@ __global__ __launch_bounds__(64) void event_big_group_sort_kernel(const uint32_t
             if (threadIdx.x == 0) atomicOr(bad, 4u);
             continue;
         }
-        group_rank_sort<EV_CAP>(b, m, gkey, order, key, idx);
+        group_rank_sort<EV_CAP>(b, m, deliver, order, key, idx);
         __syncthreads();  // LDS reused by the next group
     }
 }
@@ -395,7 +385,7 @@ extern "C" srt_status srt_packet_events(srt_plan *plan, const uint32_t *d_host_p
     // count the per-chunk rows
     const uint32_t chunks = (n + EV_CHUNK - 1) / EV_CHUNK;
     const bool chunked = n && n_dst_hosts && n_dst_hosts <= EV_LDS_DST && (uint64_t)chunks * n_dst_hosts <= (64u << 20);
-    const size_t need = 8ull * n + 12ull * ((size_t)n_dst_hosts + 1) + (chunked ? 4ull * chunks * n_dst_hosts : 0);
+    const size_t need = 12ull * ((size_t)n_dst_hosts + 1) + (chunked ? 4ull * chunks * n_dst_hosts : 0);
     if (need > plan->ev_scratch_cap) {
         if (plan->d_ev_scratch) (void)hipFree(plan->d_ev_scratch);
         plan->d_ev_scratch = nullptr;
@@ -406,10 +396,8 @@ extern "C" srt_status srt_packet_events(srt_plan *plan, const uint32_t *d_host_p
         }
         plan->ev_scratch_cap = need;
     }
-    // the group keys (deliver times in scatter order), cnt, cur, the
-    // big-group list (count + ids), the chunk rows
-    uint64_t *gkey = (uint64_t *)plan->d_ev_scratch;
-    uint32_t *cnt = (uint32_t *)(gkey + n), *cur = cnt + n_dst_hosts + 1, *big = cur + n_dst_hosts + 1;
+    // cnt, cur, the big-group list (count + ids), the chunk rows
+    uint32_t *cnt = (uint32_t *)plan->d_ev_scratch, *cur = cnt + n_dst_hosts + 1, *big = cur + n_dst_hosts + 1;
     uint32_t *hist = big + n_dst_hosts + 1;
     if (!chunked) {
         (void)hipMemsetAsync(cnt, 0, 4ull * (n_dst_hosts + 1), s);
@@ -436,16 +424,15 @@ extern "C" srt_status srt_packet_events(srt_plan *plan, const uint32_t *d_host_p
             hipLaunchKernelGGL(event_chunk_scatter_kernel, dim3(chunks), dim3(1024),
                                lds + 4ull * ((n_dst_hosts + 63) / 64), s, d_flags, d_dst_host, n_dst_hosts, n,
                                (const uint32_t *)hist, (const uint32_t *)cnt, (const uint32_t *)cur, d_dst_ptr,
-                               d_deliver, d_order, gkey);
+                               d_order);
         else
             hipLaunchKernelGGL(event_scatter_kernel, dim3(blocks), dim3(256), 0, s, d_flags, d_dst_host, n_dst_hosts, n,
-                               cur, d_deliver, d_order, gkey);
+                               cur, d_order);
         if (n_dst_hosts) {
             hipLaunchKernelGGL(event_group_sort_kernel, dim3(n_dst_hosts), dim3(64), 0, s, (const uint32_t *)d_dst_ptr,
-                               (const uint64_t *)gkey, d_order, big);
+                               d_deliver, d_order, big);
             hipLaunchKernelGGL(event_big_group_sort_kernel, dim3(std::min<uint32_t>(n_dst_hosts, 512)), dim3(64), 0, s,
-                               (const uint32_t *)d_dst_ptr, (const uint64_t *)gkey, d_order, (const uint32_t *)big,
-                               plan->d_ev_bad);
+                               (const uint32_t *)d_dst_ptr, d_deliver, d_order, (const uint32_t *)big, plan->d_ev_bad);
         }
     }
     // the call, for srt_packet_events_status's exact fallback
