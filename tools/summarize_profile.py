@@ -25,6 +25,12 @@ LABELS = {
     "minplus_u16_kernel<0>": "phase 3 rest",
     "minplus_u16_kernel<0, 1>": "phase 3 rest",
     "minplus_u16_kernel<0, 3>": "phase 3 rest",
+    "minplus_u16_kernel<0, 0, true>": "phase 3 rest",
+    "minplus_u16_kernel<0, 1, true>": "phase 3 rest",
+    "minplus_u16_kernel<0, 3, true>": "phase 3 rest",
+    "minplus_u16_kernel<0, 0, false>": "phase 3 rest",
+    "minplus_u16_kernel<0, 1, false>": "phase 3 rest",
+    "minplus_u16_kernel<0, 3, false>": "phase 3 rest",
     "minplus_u16_kernel<5>": "phase 3 look-ahead (grouped)",
     "minplus_u32_kernel<0>": "phase 3 rest",
     "minplus_u32_kernel<5>": "phase 3 look-ahead (grouped)",
