@@ -907,7 +907,6 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
                       (unsigned long long)p->sssp_g, p->V, p->n, (unsigned long long)p->n_in_edges, p->sssp_r,
                       p->sssp_nb / p->sssp_r, p->sssp_delta, p->h_bfs_rank.empty() ? "table" : "bfs");
         p->desc = dd;
-        if (const char *ev = std::getenv("SRT_SSSP_WGCAP")) p->sssp_wgcap = (uint32_t)std::atoi(ev);
         if (const char *ev = std::getenv("SRT_SSSP_ACT")) {
             const int k = std::atoi(ev);
             p->sssp_act_on = k != 0;

@@ -199,8 +199,7 @@ struct srt_plan {
     // delta-stepping bucket width in latency units (0: ungated sweeps, the
     // default); knob SRT_SSSP_DELTA = the factor of the mean in-edge latency
     uint32_t sssp_delta = 0;
-    uint64_t sssp_tmax = 0;
-    uint32_t sssp_wgcap = 0;             // sweep workgroups per group cap (SRT_SSSP_WGCAP; 0: one wave per vertex)              // sweep count past which the sweep reports non-convergence
+    uint64_t sssp_tmax = 0;              // sweep count past which the sweep reports non-convergence
     uint64_t *d_spend = nullptr;         // sssp_nb * V pending-key masks (delta-stepping)
     // table rows this rank computes ([0, n) single-GPU); the table is allocated
     // with rows_alloc >= n rows so the row all-gather has equal chunks

@@ -152,149 +152,146 @@ __global__ __launch_bounds__(SWP_WAVES * 64) void sssp_sweep_kernel(
     // Plain block order on purpose: an XCD-contiguous remap (each XCD sweeping
     // its own run of vertices) measured 2x slower on C4 (1.52 -> 2.9 s) -- all
     // XCDs on neighbouring vertices keep the gathered rows in the Infinity Cache.
-    // each wave walks vertices v0, v0 + stride, ... (a capped grid: a light
-    // sweep's inactive vertices cost a loop iteration, not a workgroup dispatch)
-    const uint32_t v0 = __builtin_amdgcn_readfirstlane(blockIdx.x * SWP_WAVES + (threadIdx.x >> 6));
-    const uint32_t vstride = gridDim.x * SWP_WAVES;
-    for (uint32_t v = v0; v < V; v += vstride) {
-        const uint64_t base = (uint64_t)g * V;  // first vertex row of the group
-        const uint64_t aslot = (uint64_t)G * V;  // bytes per ring slot
-        bool skip_walk = false;
-        if (act_mode & (ACT_USE | ACT_SET)) {
-            if (lane == 0) act[((t + 2) % 3) * aslot + base + v] = 0;
-            if ((act_mode & ACT_USE) && act[(t % 3) * aslot + base + v] == 0) {
-                // no in-neighbour changed: only pending keys (delta-stepping) can
-                // move on, which needs no in-edge walk
-                bool pend_only = false;
-                if (delta) {
-                    uint64_t pw = lane < R ? pend[(base + v) * R + lane] : 0ull;
-                    pend_only = __ballot(pw != 0) != 0;
-                }
-                if (!pend_only) {
-                    if (lane < R) mask_next[(base + v) * R + lane] = 0;
-                    continue;
-                }
-                skip_walk = true;
+    const uint32_t vi = __builtin_amdgcn_readfirstlane(blockIdx.x * SWP_WAVES + (threadIdx.x >> 6));
+    if (vi >= V) return;
+    const uint32_t v = vi;
+    const uint64_t base = (uint64_t)g * V;  // first vertex row of the group
+    const uint64_t aslot = (uint64_t)G * V;  // bytes per ring slot
+    bool skip_walk = false;
+    if (act_mode & (ACT_USE | ACT_SET)) {
+        if (lane == 0) act[((t + 2) % 3) * aslot + base + v] = 0;
+        if ((act_mode & ACT_USE) && act[(t % 3) * aslot + base + v] == 0) {
+            // no in-neighbour changed: only pending keys (delta-stepping) can
+            // move on, which needs no in-edge walk
+            bool pend_only = false;
+            if (delta) {
+                uint64_t pw = lane < R ? pend[(base + v) * R + lane] : 0ull;
+                pend_only = __ballot(pw != 0) != 0;
             }
+            if (!pend_only) {
+                if (lane < R) mask_next[(base + v) * R + lane] = 0;
+                return;
+            }
+            skip_walk = true;
         }
-        const uint64_t *Dg = D + base * R * 64;
-        const uint64_t *mc = mask_cur + base * R;
-        uint64_t best[R];
-    #pragma unroll
-        for (int r = 0; r < R; ++r) best[r] = SKEY_INF;
-        const uint64_t e0 = in_ptr[v], e1 = skip_walk ? e0 : in_ptr[v + 1];
-        for (uint64_t c0 = e0; c0 < e1; c0 += 64) {
-            const uint64_t k = c0 + lane;
-            uint32_t eu = 0, ew = 0;
-            float eeb = 0.f;
-            uint64_t em[R];
-            bool any = false;
-    #pragma unroll
-            for (int r = 0; r < R; ++r) em[r] = 0;
-            if (k < e1) {
-                const InEdge e = in_edge[k];
-                eu = e.u;
-                ew = e.w;
-                eeb = e.eb;
-    #pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    em[r] = mc[(uint64_t)eu * R + r];
-                    any |= em[r] != 0;
-                }
-            }
-            uint64_t act = __ballot(any);
-            while (act) {
-                uint64_t du[4][R];
-                uint32_t w[4];
-                float eb[4];
-    #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    w[q] = 0;
-                    eb[q] = 0.f;
-    #pragma unroll
-                    for (int r = 0; r < R; ++r) du[q][r] = SKEY_INF;
-                    if (act) {
-                        const int j = __builtin_ctzll(act);
-                        act &= act - 1;
-                        const uint32_t u = __builtin_amdgcn_readlane(eu, j);
-                        w[q] = __builtin_amdgcn_readlane(ew, j);
-                        eb[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(eeb), j));
-                        const uint64_t *Du = Dg + (uint64_t)u * R * 64 + lane;
-    #pragma unroll
-                        for (int r = 0; r < R; ++r) {
-                            const uint32_t mlo = __builtin_amdgcn_readlane((uint32_t)em[r], j);
-                            const uint32_t mhi = __builtin_amdgcn_readlane((uint32_t)(em[r] >> 32), j);
-                            const uint32_t bit = lane < 32 ? (mlo >> lane) : (mhi >> (lane - 32));
-                            if (bit & 1u) du[q][r] = Du[r * 64];
-                        }
-                    }
-                }
-    #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-    #pragma unroll
-                    for (int r = 0; r < R; ++r) {
-                        if (du[q][r] != SKEY_INF) {
-                            const uint64_t c = relax(du[q][r], w[q], eb[q]);
-                            best[r] = c < best[r] ? c : best[r];
-                        }
-                    }
-                }
-            }
-        }
-        uint64_t *Dv = D + ((base + v) * R) * 64 + lane;
-        bool prop_any = false, pend_any = false;
-        uint32_t pl = ~0u;  // smallest pending latency of this lane
-        uint64_t m_out[R], p_out[R];
-    #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            bool imp = false;
-            // pending keys of this word (one broadcast load; none without delta)
-            const uint64_t pw = delta ? pend[(base + v) * R + r] : 0ull;
-            const bool pb = (pw >> lane) & 1ull;
-            // own key: only lanes with a candidate or a pending key read it
-            uint64_t cur = SKEY_INF;
-            if (best[r] != SKEY_INF || pb) cur = Dv[r * 64];
-            if (best[r] != SKEY_INF && best[r] < cur) {
-                Dv[r * 64] = best[r];
-                cur = best[r];
-                imp = true;
-            }
-            const bool cand = imp || pb;
-            const bool go = cand && (cur >> 32) < th;
-            m_out[r] = __ballot(go);
-            p_out[r] = __ballot(cand && !go);
-            if (cand && !go) pl = (uint32_t)(cur >> 32) < pl ? (uint32_t)(cur >> 32) : pl;
-            prop_any |= m_out[r] != 0;
-            pend_any |= p_out[r] != 0;
-        }
-        if (lane == 0) {
-    #pragma unroll
+    }
+    const uint64_t *Dg = D + base * R * 64;
+    const uint64_t *mc = mask_cur + base * R;
+    uint64_t best[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) best[r] = SKEY_INF;
+    const uint64_t e0 = in_ptr[v], e1 = skip_walk ? e0 : in_ptr[v + 1];
+    for (uint64_t c0 = e0; c0 < e1; c0 += 64) {
+        const uint64_t k = c0 + lane;
+        uint32_t eu = 0, ew = 0;
+        float eeb = 0.f;
+        uint64_t em[R];
+        bool any = false;
+#pragma unroll
+        for (int r = 0; r < R; ++r) em[r] = 0;
+        if (k < e1) {
+            const InEdge e = in_edge[k];
+            eu = e.u;
+            ew = e.w;
+            eeb = e.eb;
+#pragma unroll
             for (int r = 0; r < R; ++r) {
-                mask_next[(base + v) * R + r] = m_out[r];
-                if (delta) pend[(base + v) * R + r] = p_out[r];
+                em[r] = mc[(uint64_t)eu * R + r];
+                any |= em[r] != 0;
             }
-            // idempotent stores, no atomics; every wave of the group hits the same
-            // word, so read first and write only while it is still 0 (a hot line
-            // written by every wave serialises in its L2 channel)
-            uint32_t *fl = &flag[(t % 3) * G + g], *pr = &prop[(t % 3) * G + g];
-            if ((prop_any || pend_any) && __builtin_nontemporal_load(fl) == 0) *fl = 1;
-            if (prop_any && __builtin_nontemporal_load(pr) == 0) *pr = 1;
         }
-        if (pend_any) {
-            for (int off = 32; off > 0; off >>= 1) {
-                const uint32_t o = __shfl_xor(pl, off);
-                pl = o < pl ? o : pl;
-            }
-            uint32_t *pm = &pmin[(t % 3) * G + g];
-            if (lane == 0 && pl < __builtin_nontemporal_load(pm)) atomicMin(pm, pl);
-        }
-        if (act_mode & ACT_SET) {
-            uint8_t *nxt = act + ((t + 1) % 3) * aslot + base;
-            if (prop_any) {
-                for (uint64_t k = row_ptr[v] + lane; k < row_ptr[v + 1]; k += 64) {
-                    const uint32_t w = col[k];
-                    if (w != v && nxt[w] == 0) nxt[w] = 1;  // hubs: read before the store (hot lines)
+        uint64_t act = __ballot(any);
+        while (act) {
+            uint64_t du[4][R];
+            uint32_t w[4];
+            float eb[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                w[q] = 0;
+                eb[q] = 0.f;
+#pragma unroll
+                for (int r = 0; r < R; ++r) du[q][r] = SKEY_INF;
+                if (act) {
+                    const int j = __builtin_ctzll(act);
+                    act &= act - 1;
+                    const uint32_t u = __builtin_amdgcn_readlane(eu, j);
+                    w[q] = __builtin_amdgcn_readlane(ew, j);
+                    eb[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(eeb), j));
+                    const uint64_t *Du = Dg + (uint64_t)u * R * 64 + lane;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const uint32_t mlo = __builtin_amdgcn_readlane((uint32_t)em[r], j);
+                        const uint32_t mhi = __builtin_amdgcn_readlane((uint32_t)(em[r] >> 32), j);
+                        const uint32_t bit = lane < 32 ? (mlo >> lane) : (mhi >> (lane - 32));
+                        if (bit & 1u) du[q][r] = Du[r * 64];
+                    }
                 }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if (du[q][r] != SKEY_INF) {
+                        const uint64_t c = relax(du[q][r], w[q], eb[q]);
+                        best[r] = c < best[r] ? c : best[r];
+                    }
+                }
+            }
+        }
+    }
+    uint64_t *Dv = D + ((base + v) * R) * 64 + lane;
+    bool prop_any = false, pend_any = false;
+    uint32_t pl = ~0u;  // smallest pending latency of this lane
+    uint64_t m_out[R], p_out[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        bool imp = false;
+        // pending keys of this word (one broadcast load; none without delta)
+        const uint64_t pw = delta ? pend[(base + v) * R + r] : 0ull;
+        const bool pb = (pw >> lane) & 1ull;
+        // own key: only lanes with a candidate or a pending key read it
+        uint64_t cur = SKEY_INF;
+        if (best[r] != SKEY_INF || pb) cur = Dv[r * 64];
+        if (best[r] != SKEY_INF && best[r] < cur) {
+            Dv[r * 64] = best[r];
+            cur = best[r];
+            imp = true;
+        }
+        const bool cand = imp || pb;
+        const bool go = cand && (cur >> 32) < th;
+        m_out[r] = __ballot(go);
+        p_out[r] = __ballot(cand && !go);
+        if (cand && !go) pl = (uint32_t)(cur >> 32) < pl ? (uint32_t)(cur >> 32) : pl;
+        prop_any |= m_out[r] != 0;
+        pend_any |= p_out[r] != 0;
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            mask_next[(base + v) * R + r] = m_out[r];
+            if (delta) pend[(base + v) * R + r] = p_out[r];
+        }
+        // idempotent stores, no atomics; every wave of the group hits the same
+        // word, so read first and write only while it is still 0 (a hot line
+        // written by every wave serialises in its L2 channel)
+        uint32_t *fl = &flag[(t % 3) * G + g], *pr = &prop[(t % 3) * G + g];
+        if ((prop_any || pend_any) && __builtin_nontemporal_load(fl) == 0) *fl = 1;
+        if (prop_any && __builtin_nontemporal_load(pr) == 0) *pr = 1;
+    }
+    if (pend_any) {
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint32_t o = __shfl_xor(pl, off);
+            pl = o < pl ? o : pl;
+        }
+        uint32_t *pm = &pmin[(t % 3) * G + g];
+        if (lane == 0 && pl < __builtin_nontemporal_load(pm)) atomicMin(pm, pl);
+    }
+    if (act_mode & ACT_SET) {
+        uint8_t *nxt = act + ((t + 1) % 3) * aslot + base;
+        if (prop_any) {
+            for (uint64_t k = row_ptr[v] + lane; k < row_ptr[v + 1]; k += 64) {
+                const uint32_t w = col[k];
+                if (w != v && nxt[w] == 0) nxt[w] = 1;  // hubs: read before the store (hot lines)
             }
         }
     }
@@ -486,10 +483,7 @@ srt_status sssp_pass(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
                            p->d_nodes, perm, V, g0, g0 + rows, nbat, R);
         if (p->sssp_act_on) (void)hipMemsetAsync(p->d_sact, 0, 3ull * G * V, M);
         (void)hipEventRecord(p->ev[2 * li], M);
-        // workgroups per group: capped (knob SRT_SSSP_WGCAP, 0 = one wave per vertex)
-        uint32_t wg = (V + SWP_WAVES - 1) / SWP_WAVES;
-        if (p->sssp_wgcap) wg = std::min<uint32_t>(wg, p->sssp_wgcap);
-        const dim3 grid(wg, G);
+        const dim3 grid((V + SWP_WAVES - 1) / SWP_WAVES, G);
         // activation starts where the previous launch's sweeps thinned out
         // (SRT_SSSP_ACT: knob; the first launch has no history)
         uint32_t t_on = 0;
