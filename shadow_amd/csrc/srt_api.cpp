@@ -476,6 +476,14 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_smask);
     hipFree(p->d_sflag);
     hipFree(p->d_sact);
+    hipFree(p->d_fl);
+    hipFree(p->d_fp);
+    hipFree(p->d_ftight);
+    hipFree(p->d_fchg);
+    hipFree(p->d_fact);
+    hipFree(p->d_fdone);
+    hipFree(p->d_fimp);
+    if (p->h_fimp) hipHostFree(p->h_fimp);
     hipFree(p->d_rstats);
     hipFree(p->d_ev_scratch);
     hipFree(p->d_tflag);
@@ -540,6 +548,44 @@ void build_in_edges(const srt_csr *g, uint64_t gunit, uint64_t n_in, std::vector
             e.pad = 0;
             (*edges)[fill[v]++] = e;
         }
+}
+
+// Is the latency adjacency symmetric (every u -> v of latency w has a v -> u of
+// latency w, as multisets -- petgraph undirected graphs are)?  Then every
+// shortest latency is symmetric, L(s, v) = L(v, s), which the frontier sweeps
+// use to seed a launch from the rows of the earlier ones.  Per vertex: the
+// in-edges (u, w) against the out-row (col, lat / g), both sorted; host threads
+// over vertex ranges.
+bool latency_symmetric(const srt_csr *g, const std::vector<uint64_t> &in_ptr, const std::vector<srt::InEdge> &in_edge,
+                       uint64_t gunit) {
+    const uint32_t V = g->n_nodes;
+    const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<uint8_t> bad(nt, 0);
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            std::vector<uint64_t> a, b;
+            for (uint32_t v = (uint32_t)((uint64_t)V * t / nt); v < (uint32_t)((uint64_t)V * (t + 1) / nt) && !bad[t];
+                 ++v) {
+                a.clear();
+                b.clear();
+                for (uint64_t k = in_ptr[v]; k < in_ptr[v + 1]; ++k)
+                    a.push_back((uint64_t)in_edge[k].u << 32 | in_edge[k].w);
+                for (uint64_t k = g->row_ptr[v]; k < g->row_ptr[v + 1]; ++k)
+                    if (g->col[k] != v) b.push_back((uint64_t)g->col[k] << 32 | (uint32_t)(g->lat_ns[k] / gunit));
+                if (a.size() != b.size()) {
+                    bad[t] = 1;
+                    break;
+                }
+                std::sort(a.begin(), a.end());
+                std::sort(b.begin(), b.end());
+                if (a != b) bad[t] = 1;
+            }
+        });
+    for (auto &x : th) x.join();
+    for (uint8_t x : bad)
+        if (x) return false;
+    return true;
 }
 
 // Breadth-first discovery rank of every vertex over the adjacency, from the
@@ -741,8 +787,11 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         const bool dense_likely = want0 == SRT_ALGO_FW ||
                                   (want0 == SRT_ALGO_AUTO && (double)p->Vp * p->Vp * p->Vp / 1.2e13 <
                                                                  (double)n * ((double)nin + p->V) * 64.0 / 3e12);
-        if (!cs.complete && dense_likely && (unsigned __int128)(p->V ? p->V - 1 : 0) * maxu >= 1024 &&
-            !std::getenv("SRT_FW_NO_ECC")) {
+        // sparse plans need it too: the frontier sweeps keep u16 latencies
+        // when every finite distance is below 0xFFFF units (srt_frontier.hip)
+        const bool sparse_u16 = !dense_likely && (unsigned __int128)(p->V ? p->V - 1 : 0) * maxu >= 0xffff;
+        if (!cs.complete && (dense_likely || sparse_u16) &&
+            (unsigned __int128)(p->V ? p->V - 1 : 0) * maxu >= 1024 && !std::getenv("SRT_FW_NO_ECC")) {
             uint64_t b = ~0ull;
             srt_err e2{};
             if (srt::fw_ecc_bound(p, 512, &b, &ecc_sweeps, &e2) != SRT_OK) {
@@ -880,10 +929,23 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
             p->h_bfs_rank = bfs_rank(g);
         PLAN_TRY(dmalloc(&p->d_in_ptr, in_ptr.size(), err));
         PLAN_TRY(dmalloc(&p->d_in_edge, in_edge.size(), err));
-        PLAN_TRY(dmalloc(&p->d_sD, (size_t)p->sssp_nb * p->V * 64, err));
-        PLAN_TRY(dmalloc(&p->d_smask, (size_t)2 * p->sssp_nb * p->V, err));
-        PLAN_TRY(dmalloc(&p->d_sflag, (size_t)12 * p->sssp_nb, err));  // flags + delta-stepping ring
-        PLAN_TRY(dmalloc(&p->d_spend, (size_t)p->sssp_nb * p->V, err));
+        // latency-first frontier sweeps (srt_frontier.hip) when every finite
+        // distance fits u16 units: the proved bound (eccentricity, or (V-1) *
+        // max edge) below 0xFFFF.  Knob SRT_SSSP_KEY=64 keeps the packed-key
+        // sweep (A/B, tests).
+        {
+            const uint64_t maxu = cs.maxlat / cs.gcd;
+            const unsigned __int128 lb = ecc_units != ~0ull ? (unsigned __int128)ecc_units
+                                                            : (unsigned __int128)(p->V ? p->V - 1 : 0) * maxu;
+            const char *kk = std::getenv("SRT_SSSP_KEY");
+            p->sssp_frontier = lb < 0xffff && !(kk && std::atoi(kk) == 64);
+        }
+        if (!p->sssp_frontier) {
+            PLAN_TRY(dmalloc(&p->d_sD, (size_t)p->sssp_nb * p->V * 64, err));
+            PLAN_TRY(dmalloc(&p->d_smask, (size_t)2 * p->sssp_nb * p->V, err));
+            PLAN_TRY(dmalloc(&p->d_sflag, (size_t)12 * p->sssp_nb, err));  // flags + delta-stepping ring
+            PLAN_TRY(dmalloc(&p->d_spend, (size_t)p->sssp_nb * p->V, err));
+        }
         {
             // delta-stepping bucket width = SRT_SSSP_DELTA x the mean in-edge
             // latency (units of g); default 0 = ungated sweeps, the faster on
@@ -912,7 +974,56 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
             p->sssp_act_on = k != 0;
             p->sssp_act_from = k > 1 ? (uint32_t)k : 0u;
         }
-        if (p->sssp_act_on) PLAN_TRY(dmalloc(&p->d_sact, (size_t)3 * (p->sssp_nb / p->sssp_r) * p->V, err));
+        if (p->sssp_frontier) {
+            // blocks in flight: as many as half the free HBM holds (C4: ~0.7 GB a
+            // block, capped at 64 = 32k sources), never more than the rows need;
+            // knob SRT_SSSP_FR_NB (measurement)
+            const uint64_t bb = srt::frontier_block_bytes(p->V, n_in);
+            size_t free_b = 0, total_b = 0;
+            uint64_t nb = 64;
+            if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b)
+                nb = std::min<uint64_t>(nb, std::max<uint64_t>(1, (free_b / 2) / std::max<uint64_t>(bb, 1)));
+            if (const char *ev = std::getenv("SRT_SSSP_FR_NB")) nb = std::max<uint64_t>(1, std::atoll(ev));
+            nb = std::min<uint64_t>(nb, std::max<uint32_t>(1, (n + 511) / 512));
+            p->fr_nb = (uint32_t)nb;
+            int cus = 256;
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device);
+            p->fr_grid = (uint32_t)std::max(1, cus) * 8;
+            if (const char *ev = std::getenv("SRT_SSSP_FR_GRID")) p->fr_grid = (uint32_t)std::max(1, std::atoi(ev));
+            // undirected (latency-symmetric) graphs: L(s, v) = L(v, s), so every
+            // launch starts from the exact columns of the earlier launches' rows
+            // (srt_frontier.hip fr_sym_copy_kernel) -- which needs the latencies
+            // of all rows resident: n * V * 2 B (C4: 20 GB), if a quarter of the
+            // free HBM holds them.  Knob SRT_SSSP_SYM=0 (A/B, tests).
+            const uint64_t all_blocks = std::max<uint32_t>(1, (n + 511) / 512);
+            const char *ks = std::getenv("SRT_SSSP_SYM");
+            p->fr_sym = !(ks && std::atoi(ks) == 0) && all_blocks > nb &&
+                        all_blocks * p->V * 1024ull <= (uint64_t)free_b / 4 && latency_symmetric(g, in_ptr, in_edge, cs.gcd);
+            p->fr_lblocks = p->fr_sym ? (uint32_t)all_blocks : (uint32_t)nb;
+            PLAN_TRY(dmalloc(&p->d_fl, (size_t)p->fr_lblocks * p->V * 512, err));
+            PLAN_TRY(dmalloc(&p->d_fp, (size_t)nb * p->V * 512, err));
+            PLAN_TRY(dmalloc(&p->d_ftight, (size_t)nb * std::max<uint64_t>(n_in, 1) * 64, err));
+            PLAN_TRY(dmalloc(reinterpret_cast<uint8_t **>(&p->d_fchg), (size_t)nb * p->V * srt::frontier_chg_bytes(), err));
+            PLAN_TRY(dmalloc(&p->d_fact, (size_t)nb * p->V, err));
+            PLAN_TRY(dmalloc(&p->d_fimp, 1, err));
+            if ((e = hipMemsetAsync(p->d_fchg, 0, (size_t)nb * p->V * srt::frontier_chg_bytes(), p->stream)) != hipSuccess ||
+                (e = hipMemsetAsync(p->d_fact, 0, (size_t)nb * p->V * 4, p->stream)) != hipSuccess ||
+                (e = hipMemsetAsync(p->d_fimp, 0, 4, p->stream)) != hipSuccess ||
+                (e = hipHostMalloc((void **)&p->h_fimp, 4, 0)) != hipSuccess) {
+                srt_plan_destroy(p);
+                return hip_fail(err, e, "sparse frontier buffers");
+            }
+            p->fr_t = 1;
+            char df[160];
+            std::snprintf(df, sizeof df,
+                          "sssp:frontier u16|f32 g=%llu lmax=%llu%s V=%u n=%u E_in=%llu blocks=%u order=%s seed=%s",
+                          (unsigned long long)p->sssp_g, (unsigned long long)(ecc_units != ~0ull ? ecc_units : 0),
+                          ecc_units != ~0ull ? "(ecc)" : "(V-1)", p->V, p->n, (unsigned long long)p->n_in_edges,
+                          p->fr_nb, p->h_bfs_rank.empty() ? "table" : "bfs", p->fr_sym ? "sym" : "none");
+            p->desc = df;
+        }
+        if (p->sssp_act_on && !p->sssp_frontier)
+            PLAN_TRY(dmalloc(&p->d_sact, (size_t)3 * (p->sssp_nb / p->sssp_r) * p->V, err));
         if ((e = hipHostMalloc((void **)&p->h_sflag, (size_t)p->sssp_nb * sizeof(uint32_t), 0)) != hipSuccess) {
             srt_plan_destroy(p);
             return hip_fail(err, e, "hipHostMalloc");

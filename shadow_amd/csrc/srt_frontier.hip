@@ -1,0 +1,669 @@
+// srt_frontier.hip -- latency-first batched sparse SSSP over a ballot-compacted
+// frontier, gfx950.
+//
+// Replaces NetworkGraph::compute_shortest_paths (src/main/network/graph/mod.rs:183-228)
+// for sparse graphs (config C4: 100k-node AS-like graph, average degree 8) when
+// every finite shortest latency is below 0xFFFF units of g (the eccentricity
+// proof, srt_fw.hip fw_ecc_bound; C4: ~750 units).  The reference runs one
+// petgraph Dijkstra per in-use source (mod.rs:195-198); here 512 sources
+// ("a block") move together through two label-correcting phases:
+//
+//  1. Latency.  L[b][v][512] u16: one 128-B line holds a 64-source word of one
+//     vertex, so a gather along an in-edge costs one line per changed word (the
+//     packed u64 (latency, loss) key of srt_sssp.hip cost four).  Relaxation
+//     is v_pk_add_u16 (clamp) + v_pk_min_u16, 8 sources a lane.
+//  2. Tightness.  One pass stores, per (in-edge, lane), the 8-bit mask of the
+//     lane's sources for which the edge ends a shortest path: L(s,u) + w ==
+//     L(s,v) (the loss of a pair is the left fold along tight
+//     edges only).
+//  3. Loss.  P[b][v][512] f32 from 2.0 ("not reached"), sources 0:
+//     P(s,v) = min over tight in-edges of 1 - (1 - P(s,u)) * (1 - e), one
+//     rounding per op (mod.rs:322-331, __fmul_rn, -ffp-contract=off), folded
+//     only from reached parents (P <= 1).  The fold is monotone in P(s,u), so
+//     the label-correcting fixpoint over the tight DAG is petgraph's
+//     lexicographic (latency, loss) minimum bit for bit; and since a parent is
+//     reached only with its final loss when it has one tight parent itself
+//     (1.007 tight in-edges per pair at C4), most pairs are written once.
+//
+// Frontier.  Items are (block, vertex).  act[b][v] holds the sweep that must
+// process the item; a wave that improves (b, v) in sweep t stores t + 1 into
+// act[b][x] of every out-neighbour x.  Sweep t's waves scan act in 64-item
+// chunks, ballot the entries >= t (a mark for t + 1 may have overwritten one
+// for t during the sweep: the item is then processed in both) and process only
+// those -- the grid is capped at a few workgroups per CU, so a sweep costs its
+// active items plus one coalesced 256-B scan per chunk, not a dispatch per
+// vertex.  chg[b][v] = (sweep << 8) | changed words: a reader in sweep t
+// gathers word w of u only if u changed it in sweep t - 1 or t (Gauss-Seidel:
+// values written earlier in the same sweep may be read; every write also marks
+// the readers for the next sweep).  Sweep stamps only grow (across phases,
+// launches and builds), so neither array is ever cleared.
+//
+// Order: items are block-major, so the waves of a sweep work through one or
+// two blocks at a time and the rows they gather (100 MB a block at C4) stay
+// in the Infinity Cache; sources enter blocks in BFS order (srt_api.cpp
+// bfs_rank), so a word's sources change at the same vertices in the same
+// sweeps.
+#include <algorithm>
+#include <cstdio>
+
+#include "srt_internal.h"
+
+namespace srt {
+
+namespace {
+
+constexpr uint32_t FR_SRC = 512;     // sources per block (8 words of 64)
+constexpr int FR_WAVES = 4;          // waves per sweep workgroup
+constexpr int FR_EB = 8;             // edges gathered per batch (loads in flight per lane)
+constexpr uint32_t L16_INF = 0xffffu;
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pk_add_sat(uint32_t x, uint32_t w2) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_add_sat(__builtin_bit_cast(u16x2, x),
+                                                                      __builtin_bit_cast(u16x2, w2)));
+}
+__device__ __forceinline__ uint32_t pk_min(uint32_t x, uint32_t y) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, x),
+                                                                  __builtin_bit_cast(u16x2, y)));
+}
+__device__ __forceinline__ uint4 relax8(uint4 best, uint4 x, uint32_t w2) {
+    best.x = pk_min(best.x, pk_add_sat(x.x, w2));
+    best.y = pk_min(best.y, pk_add_sat(x.y, w2));
+    best.z = pk_min(best.z, pk_add_sat(x.z, w2));
+    best.w = pk_min(best.w, pk_add_sat(x.w, w2));
+    return best;
+}
+// bit i of the result: source i of the lane's 8 -- (x_i + w == own_i), both finite
+__device__ __forceinline__ uint32_t tight8(uint4 x, uint4 own, uint32_t w) {
+    const uint32_t xs[4] = {x.x, x.y, x.z, x.w}, os[4] = {own.x, own.y, own.z, own.w};
+    uint32_t m = 0;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t a = (xs[h] >> (16 * k)) & 0xffffu, o = (os[h] >> (16 * k)) & 0xffffu;
+            if (a != L16_INF && o != L16_INF && a + w == o) m |= 1u << (2 * h + k);
+        }
+    }
+    return m;
+}
+// the fold of mod.rs:322-331 with eb = 1 - edge loss (rounded once, f32)
+__device__ __forceinline__ float fold(float a, float eb) { return 1.0f - __fmul_rn(1.0f - a, eb); }
+
+
+// Change record of (b, v): the sweep that last improved it and the lanes
+// whose sources improved (a lane = 8 sources), one 16-B store so a reader
+// sees a consistent pair.
+struct Chg {
+    uint32_t stamp, pad;
+    uint64_t lanes;
+};
+constexpr uint32_t ACT_FINAL = 0xffffffffu;  // (b, v) exact from the start (symmetric seeding)
+
+// After (b, v) improved lanes `im` in sweep t: its change record (keeping the
+// lanes of sweep t - 1, which readers of this sweep may still need), the
+// phase's last-improvement stamp, and the marks of its out-neighbours for
+// sweep t + 1 (raise only: a final item keeps ACT_FINAL).
+__device__ __forceinline__ void publish(Chg *chg_bv, uint32_t *act_b, uint32_t *last, uint32_t v, uint64_t im,
+                                        uint32_t t, const uint64_t *__restrict__ row_ptr,
+                                        const uint32_t *__restrict__ col, int lane) {
+    if (lane == 0) {
+        const Chg old = *chg_bv;
+        Chg c;
+        c.stamp = t;
+        c.pad = 0;
+        c.lanes = im | (old.stamp + 1 == t ? old.lanes : 0ull);
+        *chg_bv = c;
+        if (__builtin_nontemporal_load(last) != t) *last = t;  // hot word: read first
+    }
+    for (uint64_t k = row_ptr[v] + lane; k < row_ptr[v + 1]; k += 64) {
+        const uint32_t x = col[k];
+        if (x != v && act_b[x] < t + 1) act_b[x] = t + 1;  // hubs: read before the store
+    }
+}
+
+// the lanes of u that changed in sweep t - 1 or t (0 if none)
+__device__ __forceinline__ uint64_t changed_lanes(const Chg *chg_b, uint32_t u, uint32_t t) {
+    const Chg c = chg_b[u];
+    return c.stamp + 1 >= t ? c.lanes : 0ull;
+}
+
+// -------------------------------------------------------------- seeds
+// slot q of the launch (q < nsrc): block q / 512, source q % 512 of it; the
+// table row is perm[q0 + q] (perm null: q0 + q), the source vertex nodes[row].
+// Phase 1 (L given): L = 0; phase 3: P = 0.  Either way the source's lane is
+// marked changed in sweep t0 and its out-neighbours marked for t0 + 1.
+__global__ void fr_seed_kernel(uint16_t *__restrict__ L, float *__restrict__ P, Chg *chg, uint32_t *act,
+                               const uint32_t *__restrict__ nodes, const uint32_t *__restrict__ perm, uint32_t V,
+                               uint32_t q0, uint32_t nsrc, uint32_t t0, const uint64_t *__restrict__ row_ptr,
+                               const uint32_t *__restrict__ col) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nsrc) return;
+    const uint32_t b = q / FR_SRC, i = q % FR_SRC;
+    const uint32_t src = nodes[perm ? perm[q0 + q] : q0 + q];
+    const uint64_t row = (uint64_t)b * V + src;
+    if (L) L[row * FR_SRC + i] = 0;
+    else P[row * FR_SRC + i] = 0.0f;
+    Chg c;
+    c.stamp = t0;
+    c.pad = 0;
+    c.lanes = 1ull << (i / 8);  // sources of a launch are distinct vertices
+    chg[row] = c;
+    uint32_t *act_b = act + (uint64_t)b * V;
+    for (uint64_t k = row_ptr[src]; k < row_ptr[src + 1]; ++k) {
+        const uint32_t x = col[k];
+        if (x != src && act_b[x] < t0 + 1) act_b[x] = t0 + 1;
+    }
+}
+
+// Symmetric seeding (undirected graphs: L(s, v) = L(v, s)).  The rows of
+// earlier launches are exact, so for every source s_i of this launch and
+// every source v of an earlier block b', L[b][v][i] = L[b'][s_i][i'] -- a
+// 64 x 64 tile transpose through LDS per (block pair, chunk pair).
+// blockIdx.x: (b - B0) * 8 + chunk of i; blockIdx.y: b' * 8 + chunk of i'.
+__global__ __launch_bounds__(256) void fr_sym_copy_kernel(uint16_t *L, const uint32_t *__restrict__ nodes,
+                                                          const uint32_t *__restrict__ perm, uint32_t V,
+                                                          uint32_t row0, uint32_t row1, uint32_t B0) {
+    __shared__ uint16_t tile[64][66];
+    __shared__ uint32_t sv[64], dv[64];
+    const uint32_t b = B0 + blockIdx.x / 8, i0 = (blockIdx.x % 8) * 64;
+    const uint32_t bp = blockIdx.y / 8, j0 = (blockIdx.y % 8) * 64;
+    const int tid = threadIdx.x;
+    if (tid < 64) {
+        const uint32_t qa = row0 + b * FR_SRC + i0 + tid, qb = row0 + bp * FR_SRC + j0 + tid;
+        sv[tid] = qa < row1 ? nodes[perm ? perm[qa] : qa] : ~0u;  // this launch's sources s_i
+        dv[tid] = qb < row1 ? nodes[perm ? perm[qb] : qb] : ~0u;  // earlier sources v_j
+    }
+    __syncthreads();
+    // read: row s_i of block b', entries j0 .. j0+63 (128 B, 2 B a thread)
+    for (int idx = tid; idx < 64 * 64; idx += 256) {
+        const int ii = idx / 64, jj = idx % 64;
+        uint16_t x = L16_INF;
+        if (sv[ii] != ~0u) x = L[((uint64_t)bp * V + sv[ii]) * FR_SRC + j0 + jj];
+        tile[jj][ii] = x;
+    }
+    __syncthreads();
+    for (int idx = tid; idx < 64 * 64; idx += 256) {
+        const int jj = idx / 64, ii = idx % 64;
+        if (dv[jj] != ~0u) L[((uint64_t)b * V + dv[jj]) * FR_SRC + i0 + ii] = tile[jj][ii];
+    }
+}
+
+// Symmetric seeding, activity: an item (b, v) whose v is a source of an
+// earlier block (done[v] < B0) is final -- ACT_FINAL, changed in every lane
+// in sweep t0; every other item is active in sweep t0 + 1.
+__global__ void fr_sym_act_kernel(uint32_t *act, Chg *chg, const uint32_t *__restrict__ done, uint32_t V, uint32_t NB,
+                                  uint32_t B0, uint32_t t0) {
+    const uint64_t n = (uint64_t)NB * V;
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < n; e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t v = (uint32_t)(e % V);
+        if (done[v] < B0) {
+            act[e] = ACT_FINAL;
+            Chg c;
+            c.stamp = t0;
+            c.pad = 0;
+            c.lanes = ~0ull;
+            chg[e] = c;
+        } else {
+            act[e] = t0 + 1;
+        }
+    }
+}
+
+// ------------------------------------------------------- latency sweep
+// One wave per active item (b, v): the 8 sources of lane l are 8l .. 8l+7.
+// Per 64 in-edges: one edge and its source's changed lanes per lane, a ballot
+// of the edges whose source changed in sweep t-1 or t, then batches of FR_EB
+// gathers (16 B a lane, only the lanes whose sources changed) and the packed
+// relaxation.  The own row is loaded first (independent of the chain).
+__global__ __launch_bounds__(FR_WAVES * 64) void fr_lat_sweep_kernel(
+    const uint64_t *__restrict__ in_ptr, const InEdge *__restrict__ in_edge, uint32_t V, uint32_t NB,
+    uint16_t *L, Chg *chg, uint32_t *act, uint32_t *last, uint32_t t, const uint64_t *__restrict__ row_ptr,
+    const uint32_t *__restrict__ col) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = blockIdx.x * FR_WAVES + (threadIdx.x >> 6), nwaves = gridDim.x * FR_WAVES;
+    const uint32_t cpb = (V + 63) / 64, nchunks = cpb * NB;
+    for (uint32_t c = __builtin_amdgcn_readfirstlane(wave); c < nchunks; c += nwaves) {
+        const uint32_t b = c / cpb, v0 = (c % cpb) * 64;
+        uint32_t *act_b = act + (uint64_t)b * V;
+        const uint32_t a = v0 + lane < V ? act_b[v0 + lane] : 0u;
+        uint64_t items = __ballot(a >= t && a != ACT_FINAL);
+        uint4 *Lb = reinterpret_cast<uint4 *>(L + (uint64_t)b * V * FR_SRC);
+        Chg *chg_b = chg + (uint64_t)b * V;
+        while (items) {
+            const uint32_t v = v0 + __builtin_ctzll(items);
+            items &= items - 1;
+            const uint4 own = Lb[(uint64_t)v * 64 + lane];
+            uint4 best = own;
+            const uint64_t e0 = in_ptr[v], e1 = in_ptr[v + 1];
+            for (uint64_t c0 = e0; c0 < e1; c0 += 64) {
+                const uint64_t k = c0 + lane;
+                uint32_t eu = 0, ew = 0;
+                uint64_t m = 0;
+                if (k < e1) {
+                    const InEdge e = in_edge[k];
+                    eu = e.u;
+                    ew = e.w < L16_INF ? e.w : L16_INF;
+                    m = changed_lanes(chg_b, eu, t);
+                }
+                uint64_t am = __ballot(m != 0);
+                while (am) {
+                    uint4 x[FR_EB];
+                    uint32_t w2[FR_EB];
+#pragma unroll
+                    for (int q = 0; q < FR_EB; ++q) {
+                        x[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
+                        w2[q] = 0;
+                        if (am) {
+                            const int j = __builtin_ctzll(am);
+                            am &= am - 1;
+                            const uint32_t u = __builtin_amdgcn_readlane(eu, j);
+                            const uint32_t w = __builtin_amdgcn_readlane(ew, j);
+                            const uint32_t mlo = __builtin_amdgcn_readlane((uint32_t)m, j);
+                            const uint32_t mhi = __builtin_amdgcn_readlane((uint32_t)(m >> 32), j);
+                            w2[q] = w | (w << 16);
+                            if (((lane < 32 ? mlo : mhi) >> (lane & 31)) & 1u) x[q] = Lb[(uint64_t)u * 64 + lane];
+                        }
+                    }
+#pragma unroll
+                    for (int q = 0; q < FR_EB; ++q) best = relax8(best, x[q], w2[q]);
+                }
+            }
+            const bool imp = best.x != own.x || best.y != own.y || best.z != own.z || best.w != own.w;
+            const uint64_t im = __ballot(imp);
+            if (im) {
+                if (imp) Lb[(uint64_t)v * 64 + lane] = best;
+                publish(chg_b + v, act_b, last, v, im, t, row_ptr, col, lane);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------- tight pass
+// Every item (b, v), every in-edge k of v: tight[(b * E + k) * 64 + lane] =
+// the lane's 8-bit mask of sources s with L(s,u) + w == L(s,v).
+__global__ __launch_bounds__(FR_WAVES * 64) void fr_tight_kernel(const uint64_t *__restrict__ in_ptr,
+                                                                 const InEdge *__restrict__ in_edge, uint32_t V,
+                                                                 uint32_t NB, uint64_t E,
+                                                                 const uint16_t *__restrict__ L,
+                                                                 uint8_t *__restrict__ tight) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = blockIdx.x * FR_WAVES + (threadIdx.x >> 6), nwaves = gridDim.x * FR_WAVES;
+    const uint64_t nitems = (uint64_t)V * NB;
+    for (uint64_t it = __builtin_amdgcn_readfirstlane(wave); it < nitems; it += nwaves) {
+        const uint32_t b = (uint32_t)(it / V), v = (uint32_t)(it % V);
+        const uint4 *Lb = reinterpret_cast<const uint4 *>(L + (uint64_t)b * V * FR_SRC);
+        const uint4 own = Lb[(uint64_t)v * 64 + lane];
+        uint8_t *tb = tight + (uint64_t)b * E * 64 + lane;
+        const uint64_t e0 = in_ptr[v], e1 = in_ptr[v + 1];
+        for (uint64_t c0 = e0; c0 < e1; c0 += 64) {
+            const uint64_t k = c0 + lane;
+            uint32_t eu = 0, ew = 0;
+            if (k < e1) {
+                const InEdge e = in_edge[k];
+                eu = e.u;
+                ew = e.w;
+            }
+            const uint32_t cnt = e1 - c0 < 64 ? (uint32_t)(e1 - c0) : 64u;
+            for (uint32_t j0 = 0; j0 < cnt; j0 += FR_EB) {
+                uint4 x[FR_EB];
+                uint32_t w[FR_EB];
+#pragma unroll
+                for (int q = 0; q < FR_EB; ++q) {
+                    w[q] = 0;
+                    x[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
+                    if (j0 + q < cnt) {
+                        const uint32_t u = __builtin_amdgcn_readlane(eu, j0 + q);
+                        w[q] = __builtin_amdgcn_readlane(ew, j0 + q);
+                        x[q] = Lb[(uint64_t)u * 64 + lane];
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < FR_EB; ++q)
+                    if (j0 + q < cnt) tb[(c0 + j0 + q) * 64] = (uint8_t)tight8(x[q], own, w[q]);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------- loss sweep
+// As the latency sweep, over tight lanes only: for a changed in-neighbour u,
+// lane l loads its tight byte of the edge and, if any of its 8 sources is
+// tight and u changed the lane's sources, u's 8 losses (32 B), and folds the
+// reached ones (P <= 1; 2.0 = not reached yet).
+constexpr int FR_EBL = 4;  // loss gathers per batch (2 x 16 B a lane each)
+__global__ __launch_bounds__(FR_WAVES * 64) void fr_loss_sweep_kernel(
+    const uint64_t *__restrict__ in_ptr, const InEdge *__restrict__ in_edge, uint32_t V, uint32_t NB, uint64_t E,
+    const uint8_t *__restrict__ tight, float *P, Chg *chg, uint32_t *act, uint32_t *last, uint32_t t,
+    const uint64_t *__restrict__ row_ptr, const uint32_t *__restrict__ col) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = blockIdx.x * FR_WAVES + (threadIdx.x >> 6), nwaves = gridDim.x * FR_WAVES;
+    const uint32_t cpb = (V + 63) / 64, nchunks = cpb * NB;
+    for (uint32_t c = __builtin_amdgcn_readfirstlane(wave); c < nchunks; c += nwaves) {
+        const uint32_t b = c / cpb, v0 = (c % cpb) * 64;
+        uint32_t *act_b = act + (uint64_t)b * V;
+        const uint32_t a = v0 + lane < V ? act_b[v0 + lane] : 0u;
+        uint64_t items = __ballot(a >= t);
+        float4 *Pb = reinterpret_cast<float4 *>(P + (uint64_t)b * V * FR_SRC);
+        const uint8_t *tb = tight + (uint64_t)b * E * 64 + lane;
+        Chg *chg_b = chg + (uint64_t)b * V;
+        while (items) {
+            const uint32_t v = v0 + __builtin_ctzll(items);
+            items &= items - 1;
+            const float4 o0 = Pb[(uint64_t)v * 128 + 2 * lane], o1 = Pb[(uint64_t)v * 128 + 2 * lane + 1];
+            float best[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+            const uint64_t e0 = in_ptr[v], e1 = in_ptr[v + 1];
+            for (uint64_t c0 = e0; c0 < e1; c0 += 64) {
+                const uint64_t k = c0 + lane;
+                uint32_t eu = 0;
+                uint64_t m = 0;
+                float eeb = 0.f;
+                if (k < e1) {
+                    const InEdge e = in_edge[k];
+                    eu = e.u;
+                    eeb = e.eb;
+                    m = changed_lanes(chg_b, eu, t);
+                }
+                uint64_t am = __ballot(m != 0);
+                while (am) {
+                    float4 x0[FR_EBL], x1[FR_EBL];
+                    uint32_t tm[FR_EBL];
+                    float eb[FR_EBL];
+#pragma unroll
+                    for (int q = 0; q < FR_EBL; ++q) {
+                        tm[q] = 0;
+                        eb[q] = 0.f;
+                        x0[q] = x1[q] = make_float4(2.f, 2.f, 2.f, 2.f);
+                        if (am) {
+                            const int j = __builtin_ctzll(am);
+                            am &= am - 1;
+                            const uint32_t u = __builtin_amdgcn_readlane(eu, j);
+                            const uint32_t mlo = __builtin_amdgcn_readlane((uint32_t)m, j);
+                            const uint32_t mhi = __builtin_amdgcn_readlane((uint32_t)(m >> 32), j);
+                            eb[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(eeb), j));
+                            if (((lane < 32 ? mlo : mhi) >> (lane & 31)) & 1u) {
+                                tm[q] = tb[(c0 + j) * 64];
+                                if (tm[q]) {
+                                    x0[q] = Pb[(uint64_t)u * 128 + 2 * lane];
+                                    x1[q] = Pb[(uint64_t)u * 128 + 2 * lane + 1];
+                                }
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int q = 0; q < FR_EBL; ++q) {
+                        const float xs[8] = {x0[q].x, x0[q].y, x0[q].z, x0[q].w, x1[q].x, x1[q].y, x1[q].z, x1[q].w};
+#pragma unroll
+                        for (int i = 0; i < 8; ++i)
+                            if (((tm[q] >> i) & 1u) && xs[i] <= 1.0f) {  // u reached (not the 2.0 init)
+                                const float cnd = fold(xs[i], eb[q]);
+                                best[i] = cnd < best[i] ? cnd : best[i];
+                            }
+                    }
+                }
+            }
+            const bool imp = best[0] < o0.x || best[1] < o0.y || best[2] < o0.z || best[3] < o0.w ||
+                             best[4] < o1.x || best[5] < o1.y || best[6] < o1.z || best[7] < o1.w;
+            const uint64_t im = __ballot(imp);
+            if (im) {
+                if (imp) {
+                    Pb[(uint64_t)v * 128 + 2 * lane] = make_float4(best[0], best[1], best[2], best[3]);
+                    Pb[(uint64_t)v * 128 + 2 * lane + 1] = make_float4(best[4], best[5], best[6], best[7]);
+                }
+                publish(chg_b + v, act_b, last, v, im, t, row_ptr, col, lane);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- emit
+// Table rows of the launch: slot q -> row perm[q0 + q].  A 64 x 64 (slots x
+// columns) tile through LDS: each column's 64 slots are one 128-B run of L
+// and one 256-B run of P; the rows are stored coalesced.  Diagonal = the raw
+// self-loop (mod.rs:210-217); min latency (mod.rs:474-476) and unreachable
+// count (the assert at mod.rs:219) block-reduced into stats.
+__global__ __launch_bounds__(256) void fr_emit_kernel(const uint16_t *__restrict__ L, const float *__restrict__ P,
+                                                      uint32_t V, const uint32_t *__restrict__ nodes,
+                                                      const uint32_t *__restrict__ perm, uint32_t n, uint32_t q0,
+                                                      uint32_t nsrc, uint64_t gunit,
+                                                      const uint64_t *__restrict__ sl_lat,
+                                                      const float *__restrict__ sl_loss, uint64_t *__restrict__ out_lat,
+                                                      float *__restrict__ out_loss, unsigned long long *stats) {
+    __shared__ uint16_t tl[64][66];
+    __shared__ float tp[64][65];
+    __shared__ unsigned long long red_min[4], red_cnt[4];
+    const uint32_t s0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
+    const uint32_t b = s0 / FR_SRC, o = s0 % FR_SRC;
+    const int tid = threadIdx.x;
+    for (int idx = tid; idx < 64 * 64; idx += 256) {
+        const int jj = idx / 64, s = idx % 64;
+        const uint32_t j = j0 + jj;
+        uint16_t l = L16_INF;
+        float pl = 1.0f;
+        if (j < n) {
+            const uint64_t r = ((uint64_t)b * V + nodes[j]) * FR_SRC + o + s;
+            l = L[r];
+            pl = P[r];
+        }
+        tl[jj][s] = l;
+        tp[jj][s] = pl;
+    }
+    __syncthreads();
+    uint64_t mn = ~0ull;
+    unsigned long long unreach = 0;
+    for (int idx = tid; idx < 64 * 64; idx += 256) {
+        const int s = idx / 64, jj = idx % 64;
+        const uint32_t j = j0 + jj, q = s0 + s;
+        if (j >= n || q >= nsrc) continue;
+        const uint32_t row = perm ? perm[q0 + q] : q0 + q;
+        uint64_t lat;
+        float loss;
+        if (row == j) {
+            lat = sl_lat[j];
+            loss = sl_loss[j];
+        } else if (tl[jj][s] == L16_INF) {
+            ++unreach;
+            lat = ~0ull;
+            loss = 1.0f;
+        } else {
+            lat = (uint64_t)tl[jj][s] * gunit;
+            loss = tp[jj][s];
+        }
+        out_lat[(uint64_t)row * n + j] = lat;
+        out_loss[(uint64_t)row * n + j] = loss;
+        mn = lat < mn ? lat : mn;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t x = __shfl_xor(mn, off);
+        mn = x < mn ? x : mn;
+        unreach += __shfl_xor(unreach, off);
+    }
+    const int w = tid >> 6;
+    if ((tid & 63) == 0) {
+        red_min[w] = mn;
+        red_cnt[w] = unreach;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long m = red_min[0], cnt = red_cnt[0];
+        for (int k = 1; k < 4; ++k) {
+            m = red_min[k] < m ? red_min[k] : m;
+            cnt += red_cnt[k];
+        }
+        atomicMin(&stats[0], m);
+        if (cnt) atomicAdd(&stats[1], cnt);
+    }
+}
+
+__global__ void fr_stats_init_kernel(unsigned long long *stats) {
+    stats[0] = ~0ull;
+    stats[1] = 0ull;
+}
+
+srt_status hip_err(srt_err *err, hipError_t e, const char *what) {
+    if (err) {
+        err->code = SRT_ERR_HIP;
+        std::snprintf(err->msg, sizeof err->msg, "%s: %s", what, hipGetErrorString(e));
+    }
+    return SRT_ERR_HIP;
+}
+
+// Sweeps t0 + 1, t0 + 2, ... of one phase until one improves nothing.  The
+// host reads the phase's last-improvement stamp after each chunk of sweeps
+// (sweeps past convergence find no marked item and cost one act scan).
+// Returns the last sweep enqueued in *t_end and the productive count in *n.
+template <typename F>
+srt_status run_phase(srt_plan *p, uint32_t t0, uint32_t chunk, F sweep, uint32_t *t_end, uint32_t *n, srt_err *err) {
+    hipStream_t M = p->stream;
+    uint32_t t = t0;
+    for (;;) {
+        for (uint32_t c = 0; c < chunk; ++c) sweep(++t);
+        hipError_t e = hipMemcpyAsync(p->h_fimp, p->d_fimp, 4, hipMemcpyDeviceToHost, M);
+        if (e == hipSuccess) e = hipStreamSynchronize(M);
+        if (e != hipSuccess) return hip_err(err, e, "sparse frontier sweep");
+        const uint32_t last = *p->h_fimp;
+        if (last < t) {  // sweep t improved nothing (nor did any later than `last`)
+            *t_end = t;
+            *n = last > t0 ? last - t0 : 0;
+            return SRT_OK;
+        }
+        if (t - t0 > p->sssp_tmax) {  // Bellman-Ford bound: cannot happen with positive latencies
+            if (err) {
+                err->code = SRT_ERR_INVALID;
+                std::snprintf(err->msg, sizeof err->msg, "sssp did not converge after %u sweeps", t - t0);
+            }
+            return SRT_ERR_INVALID;
+        }
+        chunk = 2;
+    }
+}
+
+}  // namespace
+
+// One pass over this rank's table rows [row0, row1), fr_nb blocks of 512
+// sources a launch.  Returns with the stream drained up to the last emit.
+srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
+    hipStream_t M = p->stream;
+    const uint32_t V = p->V, per_launch = p->fr_nb * FR_SRC;
+    const uint64_t E = p->n_in_edges;
+    Chg *chg = reinterpret_cast<Chg *>(p->d_fchg);
+    p->p3_launches = 0;
+    p->p3_work = 0.0;
+    p->sssp_sweeps = 0;
+    p->fr_lat_sweeps = p->fr_loss_sweeps = 0;
+    hipError_t e;
+    const uint32_t rows = p->row1 - p->row0;
+    // symmetric seeding needs every block of this rank's rows resident
+    const bool sym = p->fr_sym && p->fr_lblocks * FR_SRC >= rows;
+    // the BFS source order of this rank's rows and, per vertex, the block in
+    // which it is a source (built once per row range), uploaded on the plan's
+    // stream from host copies the plan keeps
+    const uint32_t *perm = nullptr;
+    if (p->row1 > p->row0 && (!p->d_fdone || p->sperm_r0 != p->row0 || p->sperm_r1 != p->row1)) {
+        const bool bfs = !p->h_bfs_rank.empty();
+        if (bfs) {
+            p->h_sperm.resize(p->n);
+            for (uint32_t i = 0; i < p->n; ++i) p->h_sperm[i] = i;
+            std::stable_sort(p->h_sperm.begin() + p->row0, p->h_sperm.begin() + p->row1, [&](uint32_t a, uint32_t b) {
+                return p->h_bfs_rank[p->nodes[a]] < p->h_bfs_rank[p->nodes[b]];
+            });
+        }
+        p->h_fdone.assign(V, ~0u);
+        for (uint32_t q = 0; q < rows; ++q)
+            p->h_fdone[p->nodes[bfs ? p->h_sperm[p->row0 + q] : p->row0 + q]] = q / FR_SRC;
+        e = hipSuccess;
+        if (bfs && !p->d_sperm) e = hipMalloc(&p->d_sperm, (size_t)p->n * 4);
+        if (e == hipSuccess && !p->d_fdone) e = hipMalloc(&p->d_fdone, (size_t)std::max<uint32_t>(V, 1) * 4);
+        if (e == hipSuccess && bfs)
+            e = hipMemcpyAsync(p->d_sperm, p->h_sperm.data(), (size_t)p->n * 4, hipMemcpyHostToDevice, M);
+        if (e == hipSuccess) e = hipMemcpyAsync(p->d_fdone, p->h_fdone.data(), (size_t)V * 4, hipMemcpyHostToDevice, M);
+        if (e != hipSuccess) return hip_err(err, e, "sssp source order");
+        p->sperm_r0 = p->row0;
+        p->sperm_r1 = p->row1;
+    }
+    if (!p->h_bfs_rank.empty()) perm = p->d_sperm;
+    // sweep stamps: start over (zeroed) long before they wrap
+    if (p->fr_t > (1u << 30)) {
+        if ((e = hipMemsetAsync(p->d_fchg, 0, (size_t)p->fr_nb * V * sizeof(Chg), M)) != hipSuccess ||
+            (e = hipMemsetAsync(p->d_fact, 0, (size_t)p->fr_nb * V * 4, M)) != hipSuccess)
+            return hip_err(err, e, "sssp stamps");
+        p->fr_t = 1;
+    }
+    hipLaunchKernelGGL(fr_stats_init_kernel, dim3(1), dim3(1), 0, M, d_stats);
+    const uint32_t launches = (rows + per_launch - 1) / per_launch;
+    while (p->ev.size() < 2 * (size_t)launches) {
+        hipEvent_t ev;
+        (void)hipEventCreateWithFlags(&ev, 0);
+        p->ev.push_back(ev);
+    }
+    const dim3 sgrid(p->fr_grid), sblk(FR_WAVES * 64);
+    uint32_t chunk_lat = 12, chunk_loss = 12;
+    for (uint32_t li = 0; li < launches; ++li) {
+        const uint32_t q0 = p->row0 + li * per_launch;
+        const uint32_t nsrc = std::min<uint32_t>(per_launch, p->row1 - q0);
+        const uint32_t NB = (nsrc + FR_SRC - 1) / FR_SRC, B0 = li * p->fr_nb;
+        uint16_t *L = p->d_fl + (sym ? (uint64_t)B0 * V * FR_SRC : 0);
+        const dim3 seed_grid((nsrc + 255) / 256);
+        (void)hipEventRecord(p->ev[2 * li], M);
+        // 1. latency: INF, the exact columns of earlier launches (symmetric
+        //    graphs), the sources
+        if ((e = hipMemsetAsync(L, 0xff, (size_t)NB * V * FR_SRC * 2, M)) != hipSuccess)
+            return hip_err(err, e, "sssp init");
+        uint32_t t0 = ++p->fr_t;
+        if (sym && B0 > 0) {
+            hipLaunchKernelGGL(fr_sym_copy_kernel, dim3(NB * 8, B0 * 8), dim3(256), 0, M, p->d_fl, p->d_nodes, perm, V,
+                               p->row0, p->row1, B0);
+            hipLaunchKernelGGL(fr_sym_act_kernel, dim3(2048), dim3(256), 0, M, p->d_fact, chg, p->d_fdone, V, NB, B0,
+                               t0);
+        } else if ((e = hipMemsetAsync(p->d_fact, 0, (size_t)NB * V * 4, M)) != hipSuccess) {
+            return hip_err(err, e, "sssp init");
+        }
+        hipLaunchKernelGGL(fr_seed_kernel, seed_grid, dim3(256), 0, M, L, nullptr, chg, p->d_fact, p->d_nodes, perm, V,
+                           q0, nsrc, t0, p->d_row_ptr, p->d_col);
+        uint32_t t_end = 0, nsw = 0;
+        srt_status st = run_phase(p, t0, chunk_lat, [&](uint32_t t) {
+            hipLaunchKernelGGL(fr_lat_sweep_kernel, sgrid, sblk, 0, M, p->d_in_ptr, p->d_in_edge, V, NB, L, chg,
+                               p->d_fact, p->d_fimp, t, p->d_row_ptr, p->d_col);
+        }, &t_end, &nsw, err);
+        if (st != SRT_OK) return st;
+        p->fr_lat_sweeps += nsw;
+        p->sssp_sweeps += nsw;
+        chunk_lat = std::max<uint32_t>(nsw + 1, 4);
+        // 2. tight masks
+        hipLaunchKernelGGL(fr_tight_kernel, sgrid, sblk, 0, M, p->d_in_ptr, p->d_in_edge, V, NB, E, L, p->d_ftight);
+        // 3. loss (stamps from t_end + 2: nothing of the latency phase is read;
+        //    activity cleared of the final marks)
+        if ((e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p->d_fp), 0x40000000u, (size_t)NB * V * FR_SRC,
+                                   M)) != hipSuccess ||
+            (e = hipMemsetAsync(p->d_fact, 0, (size_t)NB * V * 4, M)) != hipSuccess)
+            return hip_err(err, e, "sssp loss init");
+        t0 = t_end + 2;
+        hipLaunchKernelGGL(fr_seed_kernel, seed_grid, dim3(256), 0, M, nullptr, p->d_fp, chg, p->d_fact, p->d_nodes,
+                           perm, V, q0, nsrc, t0, p->d_row_ptr, p->d_col);
+        st = run_phase(p, t0, chunk_loss, [&](uint32_t t) {
+            hipLaunchKernelGGL(fr_loss_sweep_kernel, sgrid, sblk, 0, M, p->d_in_ptr, p->d_in_edge, V, NB, E,
+                               p->d_ftight, p->d_fp, chg, p->d_fact, p->d_fimp, t, p->d_row_ptr, p->d_col);
+        }, &t_end, &nsw, err);
+        if (st != SRT_OK) return st;
+        p->fr_loss_sweeps += nsw;
+        p->sssp_sweeps += nsw;
+        chunk_loss = std::max<uint32_t>(nsw + 1, 4);
+        p->fr_t = t_end + 2;
+        (void)hipEventRecord(p->ev[2 * li + 1], M);
+        p->p3_launches++;
+        hipLaunchKernelGGL(fr_emit_kernel, dim3((p->n + 63) / 64, (nsrc + 63) / 64), dim3(256), 0, M, L, p->d_fp, V,
+                           p->d_nodes, perm, p->n, q0, nsrc, p->sssp_g, p->d_sl_lat, p->d_sl_loss, p->d_out_lat,
+                           p->d_out_loss, d_stats);
+    }
+    // algorithmic bytes: 12 B per in-edge + 12 B per vertex, per source
+    p->p3_work = (double)rows * 12.0 * ((double)E + (double)V);
+    return SRT_OK;
+}
+
+// device bytes of one 512-source block in flight: L (1 KB) + P (2 KB) + change
+// record (16 B) + activity (4 B) per vertex, the tight masks (64 B) per in-edge
+uint64_t frontier_block_bytes(uint32_t V, uint64_t E) { return (uint64_t)V * (1024 + 2048 + 20) + E * 64; }
+size_t frontier_chg_bytes() { return sizeof(Chg); }
+
+}  // namespace srt

@@ -201,6 +201,25 @@ struct srt_plan {
     uint32_t sssp_delta = 0;
     uint64_t sssp_tmax = 0;              // sweep count past which the sweep reports non-convergence
     uint64_t *d_spend = nullptr;         // sssp_nb * V pending-key masks (delta-stepping)
+    // latency-first frontier sweeps (srt_frontier.hip), the sparse default when
+    // every finite distance is < 0xFFFF units (eccentricity proof)
+    bool sssp_frontier = false;
+    uint32_t fr_nb = 0;                  // 512-source blocks per launch
+    uint32_t fr_grid = 0;                // sweep workgroups (a few per CU; waves loop over the items)
+    bool fr_sym = false;                 // latency-symmetric graph: launches seed from earlier rows
+    uint32_t fr_lblocks = 0;             // blocks of d_fl (every block of the rows when fr_sym, else fr_nb)
+    uint16_t *d_fl = nullptr;            // fr_lblocks * V * 512 u16 latencies (units of g)
+    float *d_fp = nullptr;               // fr_nb * V * 512 f32 losses
+    uint8_t *d_ftight = nullptr;         // fr_nb * n_in_edges * 64 tight-source bytes
+    void *d_fchg = nullptr;              // fr_nb * V change records (srt_frontier.hip Chg, 16 B)
+    uint32_t *d_fact = nullptr;          // fr_nb * V activation stamps
+    uint32_t *d_fdone = nullptr;         // V: block (of this rank's rows) in which the vertex is a source, ~0 none
+    std::vector<uint32_t> h_fdone;
+    uint32_t *d_fimp = nullptr;          // last sweep that improved anything
+    uint32_t *h_fimp = nullptr;          // pinned copy
+    uint32_t fr_t = 1;                   // sweep stamp counter (grows across launches and builds)
+    uint64_t fr_lat_sweeps = 0, fr_loss_sweeps = 0;  // productive sweeps of the last run
+    std::vector<uint32_t> h_sperm;       // host copy of d_sperm (kept alive for the async upload)
     // table rows this rank computes ([0, n) single-GPU); the table is allocated
     // with rows_alloc >= n rows so the row all-gather has equal chunks
     uint32_t row0 = 0, row1 = 0, rows_alloc = 0;
@@ -351,5 +370,9 @@ void iota_rows(uint32_t *dst, uint64_t count, uint32_t V, hipStream_t s);
 void pack_paths6(srt_plan *p, uint64_t first, uint64_t count, void *dst, uint64_t loss_off, hipStream_t s);
 // kernels (srt_sssp.hip)
 srt_status sssp_run(srt_plan *p, unsigned long long *d_stats, srt_err *err);
+// kernels (srt_frontier.hip): the latency-first frontier sweeps
+srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err);
+uint64_t frontier_block_bytes(uint32_t V, uint64_t E);
+size_t frontier_chg_bytes();
 void reduce_rank_stats(srt_plan *p, int nranks);
 }  // namespace srt

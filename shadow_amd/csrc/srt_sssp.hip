@@ -516,7 +516,9 @@ srt_status sssp_pass(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
 }  // namespace
 
 // Whole build for this rank's table rows.
-srt_status sssp_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) { return sssp_pass(p, d_stats, err); }
+srt_status sssp_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
+    return p->sssp_frontier ? frontier_run(p, d_stats, err) : sssp_pass(p, d_stats, err);
+}
 
 void reduce_rank_stats(srt_plan *p, int nranks) {
     hipLaunchKernelGGL(reduce_rank_stats_kernel, dim3(1), dim3(1), 0, p->stream,

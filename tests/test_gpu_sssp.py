@@ -1,4 +1,4 @@
-"""GPU parity of the sparse routing build (srt_sssp.hip, SRT_ALGO_SSSP) against
+"""GPU parity of the sparse routing build (srt_frontier.hip / srt_sssp.hip, SRT_ALGO_SSSP) against
 the oracle's restatement of petgraph's Dijkstra.
 
 Bar: latency bit-exact AND packet_loss bit-exact -- the sweep folds loss with
@@ -17,19 +17,34 @@ pytestmark = pytest.mark.gpu
 SSSP = _lib.SRT_ALGO_SSSP
 
 
-@pytest.fixture(autouse=True, params=["ungated", "delta", "fine"])
+@pytest.fixture(autouse=True, params=["frontier", "frontier-small", "frontier-nosym", "packed", "packed-delta", "packed-fine"])
 def sweep_mode(request, monkeypatch):
-    """Every test runs the sweep three ways: ungated (the default: every
-    improved key moves on at once), delta-stepping at a quarter of the mean
-    in-edge latency (SRT_SSSP_DELTA=0.25) and with very narrow buckets (factor
-    0.01: most keys wait in the pending masks for many sweeps, and empty
-    buckets are skipped).  All three must give the same bits."""
-    monkeypatch.delenv("SRT_SSSP_DELTA", raising=False)
-    monkeypatch.delenv("SRT_SSSP_ORDER", raising=False)
-    if request.param == "delta":
+    """Every test runs the sparse build five ways, all of which must give the
+    same bits: the latency-first frontier sweeps (srt_frontier.hip, the default
+    when every distance fits u16 units), the same with one 512-source block a
+    launch, a 3-workgroup sweep grid and sources in table order (several
+    launches share the sweep stamps; waves loop over many chunks; undirected
+    graphs seed each launch from the earlier rows' columns), the same without
+    that symmetric seeding, and the
+    packed-key sweep (srt_sssp.hip, SRT_SSSP_KEY=64) ungated, with
+    delta-stepping at a quarter of the mean in-edge latency and with very narrow
+    buckets (factor 0.01: most keys wait in the pending masks)."""
+    for k in ("SRT_SSSP_DELTA", "SRT_SSSP_ORDER", "SRT_SSSP_KEY", "SRT_SSSP_FR_NB", "SRT_SSSP_FR_GRID",
+              "SRT_SSSP_SYM"):
+        monkeypatch.delenv(k, raising=False)
+    if request.param == "frontier-nosym":
+        monkeypatch.setenv("SRT_SSSP_FR_NB", "1")
+        monkeypatch.setenv("SRT_SSSP_SYM", "0")
+    if request.param == "frontier-small":
+        monkeypatch.setenv("SRT_SSSP_FR_NB", "1")
+        monkeypatch.setenv("SRT_SSSP_FR_GRID", "3")
+        monkeypatch.setenv("SRT_SSSP_ORDER", "0")
+    elif request.param.startswith("packed"):
+        monkeypatch.setenv("SRT_SSSP_KEY", "64")
+    if request.param == "packed-delta":
         monkeypatch.setenv("SRT_SSSP_DELTA", "0.25")
         monkeypatch.setenv("SRT_SSSP_ORDER", "0")  # sources in table order (default: BFS order)
-    elif request.param == "fine":
+    elif request.param == "packed-fine":
         monkeypatch.setenv("SRT_SSSP_DELTA", "0.01")
     return request.param
 
@@ -201,12 +216,56 @@ def test_long_ring(sweep_mode):
     _check((src, dst, lat, loss), nodes, False, n)
 
 
-def test_delta_is_reported(sweep_mode):
-    """The plan names its bucket width: 0 when ungated, else >= 1 unit."""
+def test_sweep_family_is_reported(sweep_mode):
+    """The plan names its sweep: the frontier sweeps (u16 latencies) unless the
+    packed-key sweep is forced, which names its bucket width (0 = ungated)."""
     src, dst, lat, loss = synth.barabasi_albert(500, 3, 9)
     g = NetworkGraph.from_edges(500, src, dst, lat, loss)
     plan = RoutingPlan(g, np.arange(100, dtype=np.uint32), algo=SSSP)
-    delta = int(plan.describe().split(" delta=")[1].split()[0])
-    assert (delta == 0) == (sweep_mode == "ungated"), plan.describe()
+    d = plan.describe()
+    if sweep_mode.startswith("frontier"):
+        assert d.startswith("sssp:frontier u16") and "(ecc)" in d, d
+    else:
+        delta = int(d.split(" delta=")[1].split()[0])
+        assert (delta == 0) == (sweep_mode == "packed"), d
     plan.close()
 
+
+def test_wide_latencies_fall_back_to_packed_keys(sweep_mode):
+    """A 90-node ring at ns resolution (gcd 1): the far side is ~67k units away,
+    past the frontier's u16 latencies, so the plan keeps the packed u64 keys."""
+    n = 90
+    rng = np.random.default_rng(5)
+    src = np.concatenate([np.arange(n), np.arange(n)]).astype(np.uint32)
+    dst = np.concatenate([np.arange(n), (np.arange(n) + 1) % n]).astype(np.uint32)
+    lat = rng.integers(1000, 2000, 2 * n).astype(np.uint64) | np.uint64(1)
+    g = NetworkGraph.from_edges(n, src, dst, lat, np.zeros(2 * n, np.float32))
+    plan = RoutingPlan(g, np.arange(n, dtype=np.uint32), algo=SSSP)
+    assert plan.describe().startswith("sssp:lat32"), plan.describe()
+    plan.close()
+
+
+def test_repeated_runs_same_bits(sweep_mode):
+    """Sweep stamps grow across launches and runs and are never cleared: a plan
+    run three times returns the same table (several launches per run in the
+    small-block mode)."""
+    n = 1300
+    src, dst, lat, loss = synth.barabasi_albert(n, 3, 21)
+    g = NetworkGraph.from_edges(n, src, dst, lat, loss)
+    nodes = np.arange(0, n, 1, dtype=np.uint32)
+    plan = RoutingPlan(g, nodes, algo=SSSP)
+    if sweep_mode == "frontier-small":
+        assert "seed=sym" in plan.describe(), plan.describe()
+    ref = None
+    for _ in range(3):
+        plan.run()
+        t = plan.fetch()
+        if ref is None:
+            ref = t
+            elat, eloss = O.compute_shortest_paths(O.Graph(False, np.arange(n), src, dst, lat, loss), nodes)
+            assert np.array_equal(t.latency_ns, elat)
+            assert np.array_equal(_bits(t.packet_loss), _bits(eloss))
+        else:
+            assert np.array_equal(t.latency_ns, ref.latency_ns)
+            assert np.array_equal(_bits(t.packet_loss), _bits(ref.packet_loss))
+    plan.close()

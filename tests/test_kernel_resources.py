@@ -38,7 +38,7 @@ def _resources(src):
 
 
 @pytest.mark.skipif(shutil.which(HIPCC) is None and not os.path.exists(HIPCC), reason="hipcc not available")
-@pytest.mark.parametrize("src", ["srt_fw.hip", "srt_sssp.hip", "srt_packet.hip", "srt_direct.hip", "srt_loss.hip"])
+@pytest.mark.parametrize("src", ["srt_fw.hip", "srt_sssp.hip", "srt_frontier.hip", "srt_packet.hip", "srt_direct.hip", "srt_loss.hip"])
 def test_no_scratch_spills(src):
     ks = _resources(src)
     assert ks, "no kernels reported"
