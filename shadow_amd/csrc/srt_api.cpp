@@ -482,6 +482,7 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_fchg);
     hipFree(p->d_fact);
     hipFree(p->d_fdone);
+    hipFree(p->d_fsbits);
     hipFree(p->d_fimp);
     if (p->h_fimp) hipHostFree(p->h_fimp);
     hipFree(p->d_rstats);
@@ -651,6 +652,7 @@ namespace {
 srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n, const srt_opts *opts,
                             srt_plan **plan_out, srt_err *err, bool defer_loss) {
     clear_err(err);
+    srt::init_wait();  // a pending srt_init_async finishes before any device work
     Trace tr;
     if (!g || !plan_out || (n && !nodes) || !g->row_ptr || (g->n_adj && (!g->col || !g->lat_ns || !g->loss))) {
         set_err(err, SRT_ERR_INVALID, "null argument");
@@ -1005,6 +1007,7 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
             PLAN_TRY(dmalloc(&p->d_ftight, (size_t)nb * std::max<uint64_t>(n_in, 1) * 64, err));
             PLAN_TRY(dmalloc(reinterpret_cast<uint8_t **>(&p->d_fchg), (size_t)nb * p->V * srt::frontier_chg_bytes(), err));
             PLAN_TRY(dmalloc(&p->d_fact, (size_t)nb * p->V, err));
+            PLAN_TRY(dmalloc(&p->d_fsbits, (size_t)nb * p->V * 64, err));
             PLAN_TRY(dmalloc(&p->d_fimp, 1, err));
             if ((e = hipMemsetAsync(p->d_fchg, 0, (size_t)nb * p->V * srt::frontier_chg_bytes(), p->stream)) != hipSuccess ||
                 (e = hipMemsetAsync(p->d_fact, 0, (size_t)nb * p->V * 4, p->stream)) != hipSuccess ||
@@ -1743,6 +1746,12 @@ struct InitState {
 };
 InitState g_init;
 
+// The async init's thread is joined before the process's HIP runtime is torn
+// down: srt_init_async starts the runtime on the caller's thread first, then
+// registers this handler (atexit handlers run before the destructors of statics
+// constructed earlier), so a process that never builds still exits cleanly.
+void join_init_at_exit() { srt::init_wait(); }
+
 srt_status init_device(int device, std::string *msg) {
     int dev = device;
     if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
@@ -1831,6 +1840,12 @@ srt_status srt_init(int device, srt_err *err) {
 }
 
 void srt_init_async(int device) {
+    static std::once_flag reg;
+    std::call_once(reg, [] {
+        int count = 0;
+        (void)hipGetDeviceCount(&count);
+        std::atexit(join_init_at_exit);
+    });
     std::lock_guard<std::mutex> lk(g_init.m);
     if (g_init.pending) return;
     g_init.pending = true;

@@ -101,6 +101,7 @@ hipError_t preload_direct() {
 extern "C" srt_status srt_get_direct_paths(const srt_csr *g, const uint32_t *nodes, uint32_t n,
                                            srt_path *out, uint64_t *min_latency_ns,
                                            const srt_opts *opts, srt_err *err) {
+    srt::init_wait();  // a pending srt_init_async finishes first
     if (err) std::memset(err, 0, sizeof *err);
     auto fail = [&](int code, const char *msg) {
         if (err) {

@@ -356,11 +356,21 @@ hipError_t preload_events() {
 }
 }  // namespace srt
 
+namespace {
+// start of a batch: an unchecked big-group flag of the previous batch (bit 2)
+// moves to bit 3 ("an earlier batch is wrong and can no longer be redone")
+__global__ void event_carry_kernel(uint32_t *bad) {
+    const uint32_t b = *bad;
+    if (b & 4u) *bad = (b & ~4u) | 8u;
+}
+}  // namespace
+
 extern "C" srt_status srt_packet_events(srt_plan *plan, const uint32_t *d_host_pkt_ptr, uint32_t n_hosts,
                                         uint64_t n_pkts, const uint32_t *d_flags, const uint64_t *d_deliver,
                                         const uint32_t *d_dst_host, uint32_t n_dst_hosts, uint64_t *d_event_base,
                                         uint64_t *d_event_id, uint32_t *d_order, uint32_t *d_dst_ptr,
                                         srt_err *err) {
+    srt::init_wait();  // a pending srt_init_async finishes first
     if (err) std::memset(err, 0, sizeof *err);
     if (!plan || !d_host_pkt_ptr || !d_dst_ptr || (n_hosts && !d_event_base) ||
         (n_pkts && (!d_flags || !d_deliver || !d_dst_host || !d_event_id || !d_order))) {
@@ -380,6 +390,11 @@ extern "C" srt_status srt_packet_events(srt_plan *plan, const uint32_t *d_host_p
             return SRT_ERR_OOM;
         }
         (void)hipMemsetAsync(plan->d_ev_bad, 0, 4, s);
+    } else {
+        // a big group of an earlier, unchecked batch cannot be redone any more
+        // (only the last call's arrays are kept): bit 2 becomes bit 3, which
+        // srt_packet_events_status reports as an error
+        hipLaunchKernelGGL(event_carry_kernel, dim3(1), dim3(1), 0, s, plan->d_ev_bad);
     }
     // scratch: per destination a count and a scatter cursor; for the chunked
     // count the per-chunk rows
@@ -458,6 +473,12 @@ extern "C" srt_status srt_packet_events_status(srt_plan *plan, srt_err *err) {
         (void)hipMemsetAsync(plan->d_ev_bad, 0, 4, plan->stream);
         if (bad & 1u) {
             set_err(err, SRT_ERR_INVALID, "destination host index out of range");
+            return SRT_ERR_INVALID;
+        }
+        if (bad & 8u) {
+            set_err(err, SRT_ERR_INVALID,
+                    "packet events: an earlier batch had a destination group over 1024 events and was not checked "
+                    "(call srt_packet_events_status after every batch that may hold one)");
             return SRT_ERR_INVALID;
         }
         // a destination group of the last batch was too big for the LDS

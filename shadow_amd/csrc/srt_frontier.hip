@@ -134,17 +134,21 @@ __device__ __forceinline__ uint64_t changed_lanes(const Chg *chg_b, uint32_t u, 
 // table row is perm[q0 + q] (perm null: q0 + q), the source vertex nodes[row].
 // Phase 1 (L given): L = 0; phase 3: P = 0.  Either way the source's lane is
 // marked changed in sweep t0 and its out-neighbours marked for t0 + 1.
-__global__ void fr_seed_kernel(uint16_t *__restrict__ L, float *__restrict__ P, Chg *chg, uint32_t *act,
-                               const uint32_t *__restrict__ nodes, const uint32_t *__restrict__ perm, uint32_t V,
-                               uint32_t q0, uint32_t nsrc, uint32_t t0, const uint64_t *__restrict__ row_ptr,
-                               const uint32_t *__restrict__ col) {
+__global__ void fr_seed_kernel(uint16_t *__restrict__ L, float *__restrict__ P, uint8_t *__restrict__ sbits, Chg *chg,
+                               uint32_t *act, const uint32_t *__restrict__ nodes, const uint32_t *__restrict__ perm,
+                               uint32_t V, uint32_t q0, uint32_t nsrc, uint32_t t0,
+                               const uint64_t *__restrict__ row_ptr, const uint32_t *__restrict__ col) {
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nsrc) return;
     const uint32_t b = q / FR_SRC, i = q % FR_SRC;
     const uint32_t src = nodes[perm ? perm[q0 + q] : q0 + q];
     const uint64_t row = (uint64_t)b * V + src;
-    if (L) L[row * FR_SRC + i] = 0;
-    else P[row * FR_SRC + i] = 0.0f;
+    if (L) {
+        L[row * FR_SRC + i] = 0;
+    } else {
+        P[row * FR_SRC + i] = 0.0f;
+        sbits[row * 64 + i / 8] = (uint8_t)(1u << (i % 8));  // the source's own change bit
+    }
     Chg c;
     c.stamp = t0;
     c.pad = 0;
@@ -335,7 +339,7 @@ __global__ __launch_bounds__(FR_WAVES * 64) void fr_tight_kernel(const uint64_t 
 constexpr int FR_EBL = 4;  // loss gathers per batch (2 x 16 B a lane each)
 __global__ __launch_bounds__(FR_WAVES * 64) void fr_loss_sweep_kernel(
     const uint64_t *__restrict__ in_ptr, const InEdge *__restrict__ in_edge, uint32_t V, uint32_t NB, uint64_t E,
-    const uint8_t *__restrict__ tight, float *P, Chg *chg, uint32_t *act, uint32_t *last, uint32_t t,
+    const uint8_t *__restrict__ tight, float *P, uint8_t *sbits, Chg *chg, uint32_t *act, uint32_t *last, uint32_t t,
     const uint64_t *__restrict__ row_ptr, const uint32_t *__restrict__ col) {
     const int lane = threadIdx.x & 63;
     const uint32_t wave = blockIdx.x * FR_WAVES + (threadIdx.x >> 6), nwaves = gridDim.x * FR_WAVES;
@@ -347,6 +351,7 @@ __global__ __launch_bounds__(FR_WAVES * 64) void fr_loss_sweep_kernel(
         uint64_t items = __ballot(a >= t);
         float4 *Pb = reinterpret_cast<float4 *>(P + (uint64_t)b * V * FR_SRC);
         const uint8_t *tb = tight + (uint64_t)b * E * 64 + lane;
+        uint8_t *sb = sbits + (uint64_t)b * V * 64 + lane;
         Chg *chg_b = chg + (uint64_t)b * V;
         while (items) {
             const uint32_t v = v0 + __builtin_ctzll(items);
@@ -383,8 +388,10 @@ __global__ __launch_bounds__(FR_WAVES * 64) void fr_loss_sweep_kernel(
                             const uint32_t mhi = __builtin_amdgcn_readlane((uint32_t)(m >> 32), j);
                             eb[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(eeb), j));
                             if (((lane < 32 ? mlo : mhi) >> (lane & 31)) & 1u) {
+                                // gather only when one of the lane's sources is
+                                // tight on this edge AND changed at u
                                 tm[q] = tb[(c0 + j) * 64];
-                                if (tm[q]) {
+                                if (tm[q] & sb[(uint64_t)u * 64]) {
                                     x0[q] = Pb[(uint64_t)u * 128 + 2 * lane];
                                     x1[q] = Pb[(uint64_t)u * 128 + 2 * lane + 1];
                                 }
@@ -403,14 +410,20 @@ __global__ __launch_bounds__(FR_WAVES * 64) void fr_loss_sweep_kernel(
                     }
                 }
             }
-            const bool imp = best[0] < o0.x || best[1] < o0.y || best[2] < o0.z || best[3] < o0.w ||
-                             best[4] < o1.x || best[5] < o1.y || best[6] < o1.z || best[7] < o1.w;
-            const uint64_t im = __ballot(imp);
+            const float ov[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+            uint32_t ib = 0;  // the lane's improved sources
+#pragma unroll
+            for (int i = 0; i < 8; ++i) ib |= best[i] < ov[i] ? 1u << i : 0u;
+            const uint64_t im = __ballot(ib != 0);
             if (im) {
-                if (imp) {
+                if (ib) {
                     Pb[(uint64_t)v * 128 + 2 * lane] = make_float4(best[0], best[1], best[2], best[3]);
                     Pb[(uint64_t)v * 128 + 2 * lane + 1] = make_float4(best[4], best[5], best[6], best[7]);
                 }
+                // per-source change bits (kept from sweep t - 1 as the lanes are), before the record
+                const uint32_t st = chg_b[v].stamp;
+                const uint32_t keep = st + 1 == t ? sb[(uint64_t)v * 64] : 0u;
+                if (ib || keep) sb[(uint64_t)v * 64] = (uint8_t)(ib | keep);
                 publish(chg_b + v, act_b, last, v, im, t, row_ptr, col, lane);
             }
         }
@@ -619,8 +632,8 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
         } else if ((e = hipMemsetAsync(p->d_fact, 0, (size_t)NB * V * 4, M)) != hipSuccess) {
             return hip_err(err, e, "sssp init");
         }
-        hipLaunchKernelGGL(fr_seed_kernel, seed_grid, dim3(256), 0, M, L, nullptr, chg, p->d_fact, p->d_nodes, perm, V,
-                           q0, nsrc, t0, p->d_row_ptr, p->d_col);
+        hipLaunchKernelGGL(fr_seed_kernel, seed_grid, dim3(256), 0, M, L, nullptr, nullptr, chg, p->d_fact, p->d_nodes,
+                           perm, V, q0, nsrc, t0, p->d_row_ptr, p->d_col);
         uint32_t t_end = 0, nsw = 0;
         srt_status st = run_phase(p, t0, chunk_lat, [&](uint32_t t) {
             hipLaunchKernelGGL(fr_lat_sweep_kernel, sgrid, sblk, 0, M, p->d_in_ptr, p->d_in_edge, V, NB, L, chg,
@@ -639,11 +652,12 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
             (e = hipMemsetAsync(p->d_fact, 0, (size_t)NB * V * 4, M)) != hipSuccess)
             return hip_err(err, e, "sssp loss init");
         t0 = t_end + 2;
-        hipLaunchKernelGGL(fr_seed_kernel, seed_grid, dim3(256), 0, M, nullptr, p->d_fp, chg, p->d_fact, p->d_nodes,
-                           perm, V, q0, nsrc, t0, p->d_row_ptr, p->d_col);
+        hipLaunchKernelGGL(fr_seed_kernel, seed_grid, dim3(256), 0, M, nullptr, p->d_fp, p->d_fsbits, chg, p->d_fact,
+                           p->d_nodes, perm, V, q0, nsrc, t0, p->d_row_ptr, p->d_col);
         st = run_phase(p, t0, chunk_loss, [&](uint32_t t) {
             hipLaunchKernelGGL(fr_loss_sweep_kernel, sgrid, sblk, 0, M, p->d_in_ptr, p->d_in_edge, V, NB, E,
-                               p->d_ftight, p->d_fp, chg, p->d_fact, p->d_fimp, t, p->d_row_ptr, p->d_col);
+                               p->d_ftight, p->d_fp, p->d_fsbits, chg, p->d_fact, p->d_fimp, t, p->d_row_ptr,
+                               p->d_col);
         }, &t_end, &nsw, err);
         if (st != SRT_OK) return st;
         p->fr_loss_sweeps += nsw;
@@ -662,8 +676,9 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
 }
 
 // device bytes of one 512-source block in flight: L (1 KB) + P (2 KB) + change
-// record (16 B) + activity (4 B) per vertex, the tight masks (64 B) per in-edge
-uint64_t frontier_block_bytes(uint32_t V, uint64_t E) { return (uint64_t)V * (1024 + 2048 + 20) + E * 64; }
+// record (16 B) + per-source change bits (64 B) + activity (4 B) per vertex,
+// the tight masks (64 B) per in-edge
+uint64_t frontier_block_bytes(uint32_t V, uint64_t E) { return (uint64_t)V * (1024 + 2048 + 84) + E * 64; }
 size_t frontier_chg_bytes() { return sizeof(Chg); }
 
 }  // namespace srt

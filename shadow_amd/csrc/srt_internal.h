@@ -213,6 +213,7 @@ struct srt_plan {
     uint8_t *d_ftight = nullptr;         // fr_nb * n_in_edges * 64 tight-source bytes
     void *d_fchg = nullptr;              // fr_nb * V change records (srt_frontier.hip Chg, 16 B)
     uint32_t *d_fact = nullptr;          // fr_nb * V activation stamps
+    uint8_t *d_fsbits = nullptr;         // fr_nb * V * 64 per-source change bits (loss sweeps)
     uint32_t *d_fdone = nullptr;         // V: block (of this rank's rows) in which the vertex is a source, ~0 none
     std::vector<uint32_t> h_fdone;
     uint32_t *d_fimp = nullptr;          // last sweep that improved anything

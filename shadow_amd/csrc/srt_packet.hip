@@ -173,6 +173,7 @@ extern "C" srt_status srt_packet_batch(srt_plan *plan, const srt_pkt *d_pkts,
                                        uint64_t n_pkts, uint64_t *d_rng, const srt_round *round,
                                        uint32_t *d_flags, uint64_t *d_deliver,
                                        uint64_t *d_counters, uint64_t *d_stats, srt_err *err) {
+    srt::init_wait();  // a pending srt_init_async finishes first
     if (err) std::memset(err, 0, sizeof *err);
     if (!plan || !round || (n_pkts && (!d_pkts || !d_flags || !d_deliver)) || !d_host_pkt_ptr ||
         (n_hosts && !d_rng)) {

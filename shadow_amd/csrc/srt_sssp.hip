@@ -102,8 +102,9 @@ __global__ void sssp_seed_kernel(uint64_t *__restrict__ D, uint64_t *__restrict_
 constexpr uint32_t ACT_USE = 1, ACT_SET = 2;
 //
 // Delta-stepping (delta > 0, in latency units g): sweep t propagates only keys
-// whose latency is below the threshold theta_t = (t + 1) * delta -- the
-// buckets [0, delta), [delta, 2 delta), ... are settled in order, so a key is
+// whose latency is below the threshold theta_t (theta_0 = 2 delta, then + delta
+// a sweep, or at least the smallest pending latency + delta after a sweep that
+// moved nothing; see below) -- the buckets are settled in order, so a key is
 // far more often final when it moves on (C4: fewer re-relaxations per
 // (vertex, source) and fewer gathered lines).  A wave whose closing compare
 // leaves a key at or above the next threshold (improved now, or pending from
@@ -445,13 +446,18 @@ srt_status sssp_pass(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     const uint32_t *perm = nullptr;
     if (!p->h_bfs_rank.empty() && p->row1 > p->row0) {
         if (!p->d_sperm || p->sperm_r0 != p->row0 || p->sperm_r1 != p->row1) {
-            std::vector<uint32_t> pm(p->n);
+            // the host copy stays alive in the plan; the upload is ordered on
+            // the plan's stream after the previous pass's emit (which reads it)
+            std::vector<uint32_t> &pm = p->h_sperm;
+            pm.resize(p->n);
             for (uint32_t i = 0; i < p->n; ++i) pm[i] = i;
             std::stable_sort(pm.begin() + p->row0, pm.begin() + p->row1, [&](uint32_t a, uint32_t b) {
                 return p->h_bfs_rank[p->nodes[a]] < p->h_bfs_rank[p->nodes[b]];
             });
             hipError_t e = p->d_sperm ? hipSuccess : hipMalloc(&p->d_sperm, (size_t)p->n * 4);
-            if (e == hipSuccess) e = hipMemcpy(p->d_sperm, pm.data(), (size_t)p->n * 4, hipMemcpyHostToDevice);
+            if (e == hipSuccess) e = hipStreamSynchronize(M);  // the previous emit is done with the old order
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(p->d_sperm, pm.data(), (size_t)p->n * 4, hipMemcpyHostToDevice, M);
             if (e != hipSuccess) {
                 if (err) {
                     err->code = SRT_ERR_HIP;

@@ -3,6 +3,7 @@ the reference's generate_routing_info + RoutingInfo (sim_config.rs:424-461,
 graph/mod.rs:428-477) restated over the oracle's table: path() keyed by GML
 ids (None for ids that are not in use), get_smallest_latency_ns, packet
 counters with saturating add, and the direct-path mode."""
+import os
 import numpy as np
 import pytest
 
@@ -168,3 +169,24 @@ def test_init_then_build():
     elat, eloss = O.compute_shortest_paths(O.Graph(False, np.arange(n), src, dst, lat, loss), nodes)
     assert np.array_equal(L, elat) and np.array_equal(P.view(np.uint32), eloss.view(np.uint32))
     ri.close()
+
+
+@pytest.mark.gpu
+def test_init_async_then_exit_without_building():
+    """srt_init_async, then the process exits at once: the library joins its
+    init thread before the HIP runtime goes away (no std::terminate, no abort),
+    and a plan created right after the call waits for the init first."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = "import shadow_amd; shadow_amd.init_async(0)"
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    code = ("import numpy as np, shadow_amd; from shadow_amd import synth, NetworkGraph; "
+            "from shadow_amd.plan import RoutingPlan; shadow_amd.init_async(0); "
+            "s, d, l, p = synth.complete_graph(8, 1); "
+            "pl = RoutingPlan(NetworkGraph.from_edges(8, s, d, l, p), np.arange(8, dtype=np.uint32)).run(); "
+            "print(pl.fetch().latency_ns[0, 1])")
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip(), r.stderr[-2000:]

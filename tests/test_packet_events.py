@@ -171,3 +171,38 @@ def test_gpu_events_wide_time_span():
     eid, order, ptr, nb = _gpu_events(plan, host_ptr, flags, deliver, dst, n_dst, base)
     assert np.array_equal(eid, eid_o) and np.array_equal(order, ord_o) and np.array_equal(ptr, ptr_o)
     assert np.array_equal(nb, ob)
+
+
+@gpu
+def test_gpu_events_unchecked_big_group_is_reported():
+    """A batch with a group over the on-chip sort's 1024 events, then another
+    batch before any status check: the first batch can no longer be redone, so
+    the status check reports it instead of returning OK (the second batch's own
+    bits are still exact)."""
+    from shadow_amd import _lib
+
+    host_ptr, flags, deliver, dst, n_dst, base = _random_batch(5, n_hosts=60, n_pkts=12_000, n_dst=30)
+    big = dst.copy()
+    big[::2] = 7
+    plan = _plan()
+    import torch
+
+    dev = torch.device("cuda:0")
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt).copy()).to(dev)  # noqa: E731
+    n = len(flags)
+    outs = lambda: (torch.zeros(n, dtype=torch.int64, device=dev), torch.zeros(n, dtype=torch.int32, device=dev),  # noqa
+                    torch.zeros(n_dst + 1, dtype=torch.int32, device=dev))
+    e1, o1, p1 = outs()
+    plan.packet_events(t(host_ptr, np.int32), t(flags, np.int32), t(deliver, np.int64), t(big, np.int32), n_dst,
+                       t(base, np.int64), e1, o1, p1, check=False)
+    e2, o2, p2 = outs()
+    plan.packet_events(t(host_ptr, np.int32), t(flags, np.int32), t(deliver, np.int64), t(dst, np.int32), n_dst,
+                       t(base, np.int64), e2, o2, p2, check=False)
+    with pytest.raises(_lib.SrtError, match="not checked"):
+        plan.packet_events_status()
+    plan.packet_events_status()  # the flags were cleared with the report
+    ob = base.copy()
+    _, ord_o, ptr_o = O.packet_events(host_ptr, flags, deliver, dst, n_dst, ob)
+    ptr = p2.cpu().numpy().view(np.uint32)
+    assert np.array_equal(ptr, ptr_o)
+    assert np.array_equal(o2.cpu().numpy().view(np.uint32)[:ptr[-1]], ord_o)
