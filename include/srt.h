@@ -87,10 +87,14 @@ typedef enum { SRT_ALGO_AUTO = 0, SRT_ALGO_FW = 1, SRT_ALGO_SSSP = 2 } srt_algo;
 
 typedef struct {
     uint32_t algo;   /* srt_algo */
-    int32_t device;  /* HIP device ordinal, -1 = current */
-    uint32_t flags;  /* reserved, 0 */
-    uint32_t reserved;
+    int32_t device;  /* HIP device ordinal (the first one when n_gpus > 1), -1 = current */
+    uint32_t flags;  /* SRT_OPT_* */
+    uint32_t n_gpus; /* 0 or 1: one GPU; N > 1: the build (srt_compute_shortest_paths,
+                        srt_routing_info_build) shards over devices device .. device+N-1
+                        with one host thread each in the calling process (srt_comm_init_local) */
 } srt_opts;
+/* flags: every one of the n_gpus ranks on `device` (tests the multi-GPU schedules on one GPU) */
+#define SRT_OPT_SAME_DEVICE 1u
 
 /* ------------------------------------------------------------------ info */
 int srt_abi_version(void);
@@ -189,6 +193,14 @@ typedef int (*srt_allgather_fn)(void *user, void *d_buf, uint64_t bytes_per_rank
 srt_status srt_comm_init_callbacks(int nranks, int rank, srt_bcast_fn bcast,
                                    srt_allgather_fn allgather, void *user, srt_comm **comm,
                                    srt_err *err);
+/* In-process transport: nranks communicators (comms[0 .. nranks)) for nranks
+ * host threads of THIS process, rank r on devices[r] (NULL: device r; a device
+ * may repeat -- several ranks on one GPU, for testing the schedules).  Every
+ * rank's plan is driven by its own thread; collectives stay stream-ordered
+ * (events + one peer-read kernel, peer access enabled between the devices).
+ * Up to 16 ranks.  srt_comm_abort releases the other ranks of a failed one. */
+srt_status srt_comm_init_local(int nranks, const int32_t *devices, srt_comm **comms, srt_err *err);
+void srt_comm_abort(srt_comm *comm);
 /* Binds the plan to a communicator: from now on srt_plan_run computes only
  * this rank's block-rows of the closure, broadcasts each round's pivot
  * block-row from its owner and all-gathers the path keys at the end, so every

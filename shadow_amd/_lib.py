@@ -22,6 +22,7 @@ SRT_ERR_UNSUPPORTED = 7
 SRT_ERR_COMM = 8
 
 SRT_ALGO_AUTO, SRT_ALGO_FW, SRT_ALGO_SSSP = 0, 1, 2
+SRT_OPT_SAME_DEVICE = 1  # srt_opts.flags: every n_gpus rank on `device` (tests)
 PDS_NONE, PDS_INET_SENT, PDS_INET_DROPPED = 0, 1 << 8, 1 << 9
 
 
@@ -47,7 +48,7 @@ class SrtPath(C.Structure):
 
 
 class SrtOpts(C.Structure):
-    _fields_ = [("algo", C.c_uint32), ("device", C.c_int32), ("flags", C.c_uint32), ("reserved", C.c_uint32)]
+    _fields_ = [("algo", C.c_uint32), ("device", C.c_int32), ("flags", C.c_uint32), ("n_gpus", C.c_uint32)]
 
 
 class SrtTiming(C.Structure):
@@ -102,6 +103,8 @@ SIGNATURES = {
     "srt_comm_init": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(_vp), _errp]),
     "srt_comm_destroy": (None, [_vp]),
     "srt_comm_init_callbacks": (C.c_int, [C.c_int, C.c_int, _vp, _vp, _vp, C.POINTER(_vp), _errp]),
+    "srt_comm_init_local": (C.c_int, [C.c_int, C.POINTER(C.c_int32), C.POINTER(_vp), _errp]),
+    "srt_comm_abort": (None, [_vp]),
     "srt_plan_bind_comm": (C.c_int, [_vp, _vp, _errp]),
     "srt_packet_batch": (C.c_int, [_vp, _vp, _vp, C.c_uint32, C.c_uint64, _vp, C.POINTER(SrtRound), _vp, _vp, _vp,
                                    _vp, _errp]),

@@ -482,7 +482,13 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_fchg);
     hipFree(p->d_fact);
     hipFree(p->d_fdone);
-    hipFree(p->d_fsbits);
+    hipFree(p->d_fmul);
+    hipFree(p->d_fmm);
+    hipFree(p->d_fpushed);
+    hipFree(p->d_fnp);
+    hipFree(p->d_fout_ptr);
+    hipFree(p->d_fout_edge);
+    hipFree(p->d_fin2out);
     hipFree(p->d_fimp);
     if (p->h_fimp) hipHostFree(p->h_fimp);
     hipFree(p->d_rstats);
@@ -549,6 +555,32 @@ void build_in_edges(const srt_csr *g, uint64_t gunit, uint64_t n_in, std::vector
             e.pad = 0;
             (*edges)[fill[v]++] = e;
         }
+}
+
+// Out-edge list of the frontier's loss push (srt_frontier.hip): the CSR minus
+// self-loops, {far end, 1 - loss as f32 bits} (8 B), row offsets, and for every
+// in-edge slot of build_in_edges the out-edge it is (so the tight pass, which
+// walks in-edges, stores its masks in out-edge order for the push).
+void build_out_edges(const srt_csr *g, const std::vector<uint64_t> &in_ptr, std::vector<uint64_t> *out_ptr,
+                     std::vector<uint2> *out_edge, std::vector<uint32_t> *in2out) {
+    const uint32_t V = g->n_nodes;
+    out_ptr->assign((size_t)V + 1, 0);
+    const uint64_t E = in_ptr.empty() ? 0 : in_ptr[V];
+    out_edge->resize(std::max<uint64_t>(E, 1));
+    in2out->resize(std::max<uint64_t>(E, 1));
+    std::vector<uint64_t> fill(in_ptr.begin(), in_ptr.end() - 1);
+    uint64_t o = 0;
+    for (uint32_t u = 0; u < V; ++u) {
+        for (uint64_t k = g->row_ptr[u]; k < g->row_ptr[u + 1]; ++k) {
+            const uint32_t v = g->col[k];
+            if (v == u) continue;
+            const float eb = 1.0f - g->loss[k];
+            (*out_edge)[o] = make_uint2(v, __builtin_bit_cast(uint32_t, eb));
+            (*in2out)[fill[v]++] = (uint32_t)o;
+            ++o;
+        }
+        (*out_ptr)[u + 1] = o;
+    }
 }
 
 // Is the latency adjacency symmetric (every u -> v of latency w has a v -> u of
@@ -940,7 +972,10 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
             const unsigned __int128 lb = ecc_units != ~0ull ? (unsigned __int128)ecc_units
                                                             : (unsigned __int128)(p->V ? p->V - 1 : 0) * maxu;
             const char *kk = std::getenv("SRT_SSSP_KEY");
-            p->sssp_frontier = lb < 0xffff && !(kk && std::atoi(kk) == 64);
+            uint64_t maxdeg = 0;
+            for (uint32_t v = 0; v < p->V; ++v) maxdeg = std::max<uint64_t>(maxdeg, in_ptr[v + 1] - in_ptr[v]);
+            // (the loss push counts a pair's tight parents in u16)
+            p->sssp_frontier = lb < 0xffff && maxdeg < 0xffff && !(kk && std::atoi(kk) == 64);
         }
         if (!p->sssp_frontier) {
             PLAN_TRY(dmalloc(&p->d_sD, (size_t)p->sssp_nb * p->V * 64, err));
@@ -1007,7 +1042,31 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
             PLAN_TRY(dmalloc(&p->d_ftight, (size_t)nb * std::max<uint64_t>(n_in, 1) * 64, err));
             PLAN_TRY(dmalloc(reinterpret_cast<uint8_t **>(&p->d_fchg), (size_t)nb * p->V * srt::frontier_chg_bytes(), err));
             PLAN_TRY(dmalloc(&p->d_fact, (size_t)nb * p->V, err));
-            PLAN_TRY(dmalloc(&p->d_fsbits, (size_t)nb * p->V * 64, err));
+            // the loss push: out-edges, tight / multi-parent bytes in out-edge
+            // order, per item the multi-parent mask, pushed mask and (multi
+            // pairs) remaining-parent counts
+            PLAN_TRY(dmalloc(&p->d_fmul, (size_t)nb * std::max<uint64_t>(n_in, 1) * 64, err));
+            PLAN_TRY(dmalloc(&p->d_fmm, (size_t)nb * p->V * 64, err));
+            PLAN_TRY(dmalloc(&p->d_fpushed, (size_t)nb * p->V * 64, err));
+            PLAN_TRY(dmalloc(&p->d_fnp, (size_t)nb * p->V * 512, err));
+            {
+                std::vector<uint64_t> out_ptr;
+                std::vector<uint2> out_edge;
+                std::vector<uint32_t> in2out;
+                build_out_edges(g, in_ptr, &out_ptr, &out_edge, &in2out);
+                PLAN_TRY(dmalloc(&p->d_fout_ptr, out_ptr.size(), err));
+                PLAN_TRY(dmalloc(&p->d_fout_edge, out_edge.size(), err));
+                PLAN_TRY(dmalloc(&p->d_fin2out, in2out.size(), err));
+                if ((e = hipMemcpy(p->d_fout_ptr, out_ptr.data(), out_ptr.size() * 8, hipMemcpyHostToDevice)) !=
+                        hipSuccess ||
+                    (e = hipMemcpy(p->d_fout_edge, out_edge.data(), out_edge.size() * 8, hipMemcpyHostToDevice)) !=
+                        hipSuccess ||
+                    (e = hipMemcpy(p->d_fin2out, in2out.data(), in2out.size() * 4, hipMemcpyHostToDevice)) !=
+                        hipSuccess) {
+                    srt_plan_destroy(p);
+                    return hip_fail(err, e, "sparse frontier out-edges");
+                }
+            }
             PLAN_TRY(dmalloc(&p->d_fimp, 1, err));
             if ((e = hipMemsetAsync(p->d_fchg, 0, (size_t)nb * p->V * srt::frontier_chg_bytes(), p->stream)) != hipSuccess ||
                 (e = hipMemsetAsync(p->d_fact, 0, (size_t)nb * p->V * 4, p->stream)) != hipSuccess ||
@@ -1666,10 +1725,88 @@ srt_status fetch_pipelined(srt_plan *p, srt_path *out, srt::CompactTable *ct, ui
     return s;
 }
 
+// The multi-GPU build inside the caller's process (srt_opts.n_gpus > 1): one
+// host thread and one plan per device, bound to an in-process communicator
+// (srt_comm_init_local), every sharded schedule unchanged; rank 0's plan holds
+// the whole table after the row all-gather and is the one fetched.  This is
+// how Shadow's single process -- generate_routing_info runs once, on its main
+// thread (sim_config.rs:136-140, 424-461) -- reaches every GPU of the node.
+srt_status build_multi(const srt_csr *g, const uint32_t *nodes, uint32_t n, srt_path *out, srt::CompactTable *ct,
+                       uint64_t *min_latency_ns, const srt_opts *opts, srt_err *err) {
+    const int N = (int)opts->n_gpus;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
+        set_err(err, SRT_ERR_HIP, "no HIP device");
+        return SRT_ERR_HIP;
+    }
+    const bool same = (opts->flags & SRT_OPT_SAME_DEVICE) != 0;
+    int first = opts->device;
+    if (first < 0 && hipGetDevice(&first) != hipSuccess) first = 0;
+    if (N > srt::MAX_LOCAL_RANKS || (!same && (N > ndev || first + N > ndev))) {
+        set_err(err, SRT_ERR_INVALID, "srt_opts.n_gpus exceeds the visible devices (or 16)");
+        return SRT_ERR_INVALID;
+    }
+    std::vector<int32_t> devs(N);
+    for (int r = 0; r < N; ++r) devs[r] = same ? first : first + r;
+    std::vector<srt_comm *> comms(N, nullptr);
+    if (srt_status s = srt_comm_init_local(N, devs.data(), comms.data(), err); s != SRT_OK) return s;
+    std::vector<srt_plan *> plans(N, nullptr);
+    std::vector<srt_status> sts(N, SRT_OK);
+    std::vector<srt_err> errs(N);
+    std::vector<std::thread> th;
+    for (int r = 0; r < N; ++r)
+        th.emplace_back([&, r] {
+            srt_opts o = *opts;
+            o.device = devs[r];
+            o.n_gpus = 1;
+            o.flags &= ~(uint32_t)SRT_OPT_SAME_DEVICE;
+            std::memset(&errs[r], 0, sizeof errs[r]);
+            srt_status s = plan_create_impl(g, nodes, n, &o, &plans[r], &errs[r], false);
+            if (s == SRT_OK) s = srt_plan_bind_comm(plans[r], comms[r], &errs[r]);
+            if (s == SRT_OK) s = srt_plan_run(plans[r], &errs[r]);
+            if (s != SRT_OK) srt_comm_abort(comms[r]);  // releases the others' collectives
+            sts[r] = s;
+        });
+    for (auto &t : th) t.join();
+    // the first rank's own failure (graph errors are found by every rank
+    // alike); a rank released by another's abort reports SRT_ERR_COMM
+    srt_status s = SRT_OK;
+    for (int r = 0; r < N && s == SRT_OK; ++r)
+        if (sts[r] != SRT_OK && sts[r] != SRT_ERR_COMM) {
+            s = sts[r];
+            if (err) *err = errs[r];
+        }
+    for (int r = 0; r < N && s == SRT_OK; ++r)
+        if (sts[r] != SRT_OK) {
+            s = sts[r];
+            if (err) *err = errs[r];
+        }
+    if (s == SRT_OK && ct) {
+        ct->release();
+        ct->n = n;
+        ct->bytes = SRT_RI_PATH16;
+        ct->full = static_cast<srt_path *>(std::malloc(std::max<uint64_t>((uint64_t)n * n, 1) * sizeof(srt_path)));
+        if (!ct->full) {
+            s = SRT_ERR_OOM;
+            set_err(err, SRT_ERR_OOM, "out of host memory (routing table)");
+        }
+        out = ct->full;
+    }
+    if (s == SRT_OK) s = srt_plan_fetch(plans[0], out, min_latency_ns, err);
+    if (s == SRT_OK && ct) {
+        ct->diag.resize(n);
+        for (uint32_t i = 0; i < n; ++i) ct->diag[i] = out[(uint64_t)i * n + i];
+    }
+    for (int r = 0; r < N; ++r) srt_plan_destroy(plans[r]);
+    for (int r = 0; r < N; ++r) srt_comm_destroy(comms[r]);
+    return s;
+}
+
 // srt_compute_shortest_paths' end-to-end build into `out` (srt_path) or `ct`
 srt_status build_e2e(const srt_csr *g, const uint32_t *nodes, uint32_t n, srt_path *out, srt::CompactTable *ct,
                      uint64_t *min_latency_ns, const srt_opts *opts, srt_err *err) {
     srt::init_wait();
+    if (opts && opts->n_gpus > 1) return build_multi(g, nodes, n, out, ct, min_latency_ns, opts, err);
     srt_plan *p = nullptr;
     Trace tr;
     srt_status s = plan_create_impl(g, nodes, n, opts, &p, err, true);

@@ -2,16 +2,20 @@
 //
 // The reference has no collective at all: compute_shortest_paths fans sources
 // out over a rayon pool inside one process (src/main/network/graph/mod.rs:190-208).
-// Here source rows are sharded over the GPUs of one node (one process per GPU)
-// and the two real exchange steps of the blocked closure go over xGMI:
-//   - per round: broadcast of the pivot block-row from its owner;
-//   - at the end: in-place all-gather of the path-key rows.
-// Transport: RCCL (native, on the plan's stream) or host callbacks.
+// Here source rows are sharded over the GPUs of one node and the exchange
+// steps of the blocked closure go over xGMI (pivot-row broadcasts, row / tile
+// all-gathers).  Transports: RCCL (one process per GPU, on the plan's stream),
+// in-process (one host thread per GPU of one process: the way Shadow's single
+// process reaches every GPU, srt_opts.n_gpus), or host callbacks (any
+// host-side collective, e.g. torch.distributed/gloo in tests).
 #include <rccl/rccl.h>
 
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <new>
+#include <vector>
 
 #include "srt_internal.h"
 
@@ -26,7 +30,102 @@ void set_err(srt_err *err, int code, const char *msg) {
 
 namespace srt {
 
+// In-process transport (srt_comm_init_local): the N ranks are N host threads
+// of one process, one per device (or several on one device, for tests).  A
+// collective is stream-ordered like RCCL's, with no host synchronisation of
+// the device:
+//   1. every rank records `ready` on its stream and publishes its buffer;
+//   2. host barrier (every rank has enqueued its record and published);
+//   3. each rank's stream waits for the other ranks' `ready` events and one
+//      kernel (srt_peer.hip) reads their slots straight out of their buffers
+//      (xGMI peer reads; peer access enabled at init);
+//   4. every rank records `done`; host barrier; each stream waits for every
+//      `done`, so no rank overwrites its slot while another still reads it.
+// A failed rank aborts the group: the others' barriers return an error
+// instead of waiting for it.
+struct LocalGroup {
+    int n = 0;
+    std::vector<int> dev;
+    std::vector<hipEvent_t> ready, done;
+    std::vector<const uint8_t *> ptr;
+    std::mutex m;
+    std::condition_variable cv;
+    int arrived = 0, refs = 0;
+    uint64_t gen = 0;
+    bool aborted = false;
+
+    bool barrier() {
+        std::unique_lock<std::mutex> lk(m);
+        if (aborted) return false;
+        const uint64_t g = gen;
+        if (++arrived == n) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+            return true;
+        }
+        cv.wait(lk, [&] { return gen != g || aborted; });
+        return !aborted;
+    }
+    void abort() {
+        std::lock_guard<std::mutex> lk(m);
+        aborted = true;
+        cv.notify_all();
+    }
+};
+
+namespace {
+// one in-process collective: rank c->rank contributes `own` (published as the
+// base of its buffer) and gathers into dst; root >= 0: a broadcast from root
+srt_status local_collective(srt_comm *c, uint8_t *buf, uint64_t bytes, int root, hipStream_t s, srt_err *err) {
+    LocalGroup *G = c->local;
+    const int r = c->rank, N = G->n;
+    hipError_t e = hipEventRecord(G->ready[r], s);
+    if (e != hipSuccess) {
+        G->abort();
+        set_err(err, SRT_ERR_HIP, "local collective: hipEventRecord");
+        return SRT_ERR_HIP;
+    }
+    G->ptr[r] = buf;
+    if (!G->barrier()) {
+        set_err(err, SRT_ERR_COMM, "local collective: another rank failed");
+        return SRT_ERR_COMM;
+    }
+    const bool receive = root < 0 || root != r;
+    if (receive) {
+        PeerSrcs src{};
+        for (int q = 0; q < N; ++q) {
+            src.p[q] = G->ptr[q];
+            if (q != r && (root < 0 || q == root)) (void)hipStreamWaitEvent(s, G->ready[q], 0);
+        }
+        peer_gather(buf, src, bytes, N, r, root, s);
+    }
+    e = hipEventRecord(G->done[r], s);
+    if (e != hipSuccess) {
+        G->abort();
+        set_err(err, SRT_ERR_HIP, "local collective: hipEventRecord");
+        return SRT_ERR_HIP;
+    }
+    if (!G->barrier()) {
+        set_err(err, SRT_ERR_COMM, "local collective: another rank failed");
+        return SRT_ERR_COMM;
+    }
+    // every reader of this rank's slot is done before its stream moves on (a
+    // broadcast's root waits for all; a receiver only for itself)
+    if (root < 0 || root == r)
+        for (int q = 0; q < N; ++q)
+            if (q != r) (void)hipStreamWaitEvent(s, G->done[q], 0);
+    if (hipGetLastError() != hipSuccess) {
+        G->abort();
+        set_err(err, SRT_ERR_HIP, "local collective: copy launch failed");
+        return SRT_ERR_HIP;
+    }
+    return SRT_OK;
+}
+}  // namespace
+
 srt_status comm_bcast(srt_comm *c, void *buf, size_t bytes, int root, hipStream_t s, srt_err *err) {
+    if (c->local) return local_collective(c, (uint8_t *)buf, bytes, root, s, err);
     if (c->nccl) {
         ncclResult_t r = ncclBroadcast(buf, buf, bytes, ncclUint8, root, (ncclComm_t)c->nccl, s);
         if (r != ncclSuccess) {
@@ -50,6 +149,7 @@ srt_status comm_bcast(srt_comm *c, void *buf, size_t bytes, int root, hipStream_
 
 srt_status comm_allgather_inplace(srt_comm *c, void *buf, size_t bytes_per_rank, hipStream_t s,
                                   srt_err *err) {
+    if (c->local) return local_collective(c, (uint8_t *)buf, bytes_per_rank, -1, s, err);
     if (c->nccl) {
         char *base = (char *)buf;
         ncclResult_t r = ncclAllGather(base + (size_t)c->rank * bytes_per_rank, base, bytes_per_rank,
@@ -150,9 +250,96 @@ srt_status srt_comm_init_callbacks(int nranks, int rank, srt_bcast_fn bcast,
     return SRT_OK;
 }
 
+srt_status srt_comm_init_local(int nranks, const int32_t *devices, srt_comm **comms, srt_err *err) {
+    if (!comms || nranks < 1 || nranks > srt::MAX_LOCAL_RANKS) {
+        set_err(err, SRT_ERR_INVALID, "bad communicator arguments (1 to 16 local ranks)");
+        return SRT_ERR_INVALID;
+    }
+    srt::LocalGroup *G = new (std::nothrow) srt::LocalGroup();
+    if (!G) {
+        set_err(err, SRT_ERR_OOM, "out of host memory");
+        return SRT_ERR_OOM;
+    }
+    G->n = nranks;
+    G->ptr.assign(nranks, nullptr);
+    G->ready.assign(nranks, nullptr);
+    G->done.assign(nranks, nullptr);
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    hipError_t e = hipSuccess;
+    for (int r = 0; r < nranks && e == hipSuccess; ++r) {
+        const int d = devices ? devices[r] : r;
+        G->dev.push_back(d);
+        e = hipSetDevice(d);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&G->ready[r], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&G->done[r], hipEventDisableTiming);
+    }
+    // peer access between every pair of distinct devices (xGMI reads)
+    for (int a = 0; a < nranks && e == hipSuccess; ++a)
+        for (int b = 0; b < nranks && e == hipSuccess; ++b) {
+            if (G->dev[a] == G->dev[b]) continue;
+            int ok = 0;
+            if (hipDeviceCanAccessPeer(&ok, G->dev[a], G->dev[b]) != hipSuccess || !ok) {
+                e = hipErrorPeerAccessUnsupported;
+                break;
+            }
+            if ((e = hipSetDevice(G->dev[a])) != hipSuccess) break;
+            e = hipDeviceEnablePeerAccess(G->dev[b], 0);
+            if (e == hipErrorPeerAccessAlreadyEnabled) {
+                (void)hipGetLastError();
+                e = hipSuccess;
+            }
+        }
+    (void)hipSetDevice(cur);
+    if (e != hipSuccess) {
+        for (hipEvent_t ev : G->ready)
+            if (ev) (void)hipEventDestroy(ev);
+        for (hipEvent_t ev : G->done)
+            if (ev) (void)hipEventDestroy(ev);
+        char m[200];
+        std::snprintf(m, sizeof m, "srt_comm_init_local: %s", hipGetErrorString(e));
+        set_err(err, SRT_ERR_HIP, m);
+        delete G;
+        return SRT_ERR_HIP;
+    }
+    for (int r = 0; r < nranks; ++r) {
+        srt_comm *c = new (std::nothrow) srt_comm();
+        if (!c) {
+            for (int q = 0; q < r; ++q) srt_comm_destroy(comms[q]);
+            set_err(err, SRT_ERR_OOM, "out of host memory");
+            return SRT_ERR_OOM;
+        }
+        c->nranks = nranks;
+        c->rank = r;
+        c->local = G;
+        comms[r] = c;
+    }
+    G->refs = nranks;
+    if (err) std::memset(err, 0, sizeof *err);
+    return SRT_OK;
+}
+
+void srt_comm_abort(srt_comm *comm) {
+    if (comm && comm->local) comm->local->abort();
+}
+
 void srt_comm_destroy(srt_comm *comm) {
     if (!comm) return;
     if (comm->nccl) ncclCommDestroy((ncclComm_t)comm->nccl);
+    if (srt::LocalGroup *G = comm->local) {
+        bool last;
+        {
+            std::lock_guard<std::mutex> lk(G->m);
+            last = --G->refs == 0;
+        }
+        if (last) {
+            for (hipEvent_t ev : G->ready)
+                if (ev) (void)hipEventDestroy(ev);
+            for (hipEvent_t ev : G->done)
+                if (ev) (void)hipEventDestroy(ev);
+            delete G;
+        }
+    }
     delete comm;
 }
 

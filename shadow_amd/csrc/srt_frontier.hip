@@ -132,9 +132,10 @@ __device__ __forceinline__ uint64_t changed_lanes(const Chg *chg_b, uint32_t u, 
 // -------------------------------------------------------------- seeds
 // slot q of the launch (q < nsrc): block q / 512, source q % 512 of it; the
 // table row is perm[q0 + q] (perm null: q0 + q), the source vertex nodes[row].
-// Phase 1 (L given): L = 0; phase 3: P = 0.  Either way the source's lane is
-// marked changed in sweep t0 and its out-neighbours marked for t0 + 1.
-__global__ void fr_seed_kernel(uint16_t *__restrict__ L, float *__restrict__ P, uint8_t *__restrict__ sbits, Chg *chg,
+// Phase 1 (L given): L = 0, the source's lane marked changed in sweep t0 and
+// its out-neighbours marked for t0 + 1.  Phase 3: P = 0, the source's own item
+// marked for t0 + 1 (it pushes first).
+__global__ void fr_seed_kernel(uint16_t *__restrict__ L, float *__restrict__ P, Chg *chg,
                                uint32_t *act, const uint32_t *__restrict__ nodes, const uint32_t *__restrict__ perm,
                                uint32_t V, uint32_t q0, uint32_t nsrc, uint32_t t0,
                                const uint64_t *__restrict__ row_ptr, const uint32_t *__restrict__ col) {
@@ -143,18 +144,18 @@ __global__ void fr_seed_kernel(uint16_t *__restrict__ L, float *__restrict__ P, 
     const uint32_t b = q / FR_SRC, i = q % FR_SRC;
     const uint32_t src = nodes[perm ? perm[q0 + q] : q0 + q];
     const uint64_t row = (uint64_t)b * V + src;
-    if (L) {
-        L[row * FR_SRC + i] = 0;
-    } else {
+    uint32_t *act_b = act + (uint64_t)b * V;
+    if (!L) {  // loss push: the source pair is final at 0; its item pushes in sweep t0 + 1
         P[row * FR_SRC + i] = 0.0f;
-        sbits[row * 64 + i / 8] = (uint8_t)(1u << (i % 8));  // the source's own change bit
+        act_b[src] = t0 + 1;
+        return;
     }
+    L[row * FR_SRC + i] = 0;
     Chg c;
     c.stamp = t0;
     c.pad = 0;
     c.lanes = 1ull << (i / 8);  // sources of a launch are distinct vertices
     chg[row] = c;
-    uint32_t *act_b = act + (uint64_t)b * V;
     for (uint64_t k = row_ptr[src]; k < row_ptr[src + 1]; ++k) {
         const uint32_t x = col[k];
         if (x != src && act_b[x] < t0 + 1) act_b[x] = t0 + 1;
@@ -285,13 +286,17 @@ __global__ __launch_bounds__(FR_WAVES * 64) void fr_lat_sweep_kernel(
 }
 
 // ---------------------------------------------------------- tight pass
-// Every item (b, v), every in-edge k of v: tight[(b * E + k) * 64 + lane] =
-// the lane's 8-bit mask of sources s with L(s,u) + w == L(s,v).
-__global__ __launch_bounds__(FR_WAVES * 64) void fr_tight_kernel(const uint64_t *__restrict__ in_ptr,
-                                                                 const InEdge *__restrict__ in_edge, uint32_t V,
-                                                                 uint32_t NB, uint64_t E,
-                                                                 const uint16_t *__restrict__ L,
-                                                                 uint8_t *__restrict__ tight) {
+// Every item (b, v), every in-edge k = (u -> v) of v, stored at its out-edge
+// index o = in2out[k]: tight[(b * E + o) * 64 + lane] = the lane's 8-bit mask
+// of sources s with L(s,u) + w == L(s,v) -- the edges the loss push walks.
+// Per source the tight parents are counted; the sources with two or more
+// (ties, ~0.7% of pairs at C4) are marked in mm[b][v][lane], their counts
+// stored in np[b][v][s], and a second walk stores their edges' bits in mul
+// (the push takes the atomic path for exactly those).
+__global__ __launch_bounds__(FR_WAVES * 64) void fr_tight_kernel(
+    const uint64_t *__restrict__ in_ptr, const InEdge *__restrict__ in_edge, const uint32_t *__restrict__ in2out,
+    uint32_t V, uint32_t NB, uint64_t E, const uint16_t *__restrict__ L, uint8_t *__restrict__ tight,
+    uint8_t *__restrict__ mul, uint8_t *__restrict__ mm, uint16_t *__restrict__ np) {
     const int lane = threadIdx.x & 63;
     const uint32_t wave = blockIdx.x * FR_WAVES + (threadIdx.x >> 6), nwaves = gridDim.x * FR_WAVES;
     const uint64_t nitems = (uint64_t)V * NB;
@@ -300,47 +305,77 @@ __global__ __launch_bounds__(FR_WAVES * 64) void fr_tight_kernel(const uint64_t 
         const uint4 *Lb = reinterpret_cast<const uint4 *>(L + (uint64_t)b * V * FR_SRC);
         const uint4 own = Lb[(uint64_t)v * 64 + lane];
         uint8_t *tb = tight + (uint64_t)b * E * 64 + lane;
+        uint32_t cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         const uint64_t e0 = in_ptr[v], e1 = in_ptr[v + 1];
         for (uint64_t c0 = e0; c0 < e1; c0 += 64) {
             const uint64_t k = c0 + lane;
-            uint32_t eu = 0, ew = 0;
+            uint32_t eu = 0, ew = 0, eo = 0;
             if (k < e1) {
                 const InEdge e = in_edge[k];
                 eu = e.u;
                 ew = e.w;
+                eo = in2out[k];
             }
-            const uint32_t cnt = e1 - c0 < 64 ? (uint32_t)(e1 - c0) : 64u;
-            for (uint32_t j0 = 0; j0 < cnt; j0 += FR_EB) {
+            const uint32_t n = e1 - c0 < 64 ? (uint32_t)(e1 - c0) : 64u;
+            for (uint32_t j0 = 0; j0 < n; j0 += FR_EB) {
                 uint4 x[FR_EB];
-                uint32_t w[FR_EB];
+                uint32_t w[FR_EB], o[FR_EB];
 #pragma unroll
                 for (int q = 0; q < FR_EB; ++q) {
                     w[q] = 0;
+                    o[q] = 0;
                     x[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
-                    if (j0 + q < cnt) {
+                    if (j0 + q < n) {
                         const uint32_t u = __builtin_amdgcn_readlane(eu, j0 + q);
                         w[q] = __builtin_amdgcn_readlane(ew, j0 + q);
+                        o[q] = __builtin_amdgcn_readlane(eo, j0 + q);
                         x[q] = Lb[(uint64_t)u * 64 + lane];
                     }
                 }
 #pragma unroll
                 for (int q = 0; q < FR_EB; ++q)
-                    if (j0 + q < cnt) tb[(c0 + j0 + q) * 64] = (uint8_t)tight8(x[q], own, w[q]);
+                    if (j0 + q < n) {
+                        const uint32_t tm = tight8(x[q], own, w[q]);
+                        tb[(uint64_t)o[q] * 64] = (uint8_t)tm;
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) cnt[i] += (tm >> i) & 1u;
+                    }
             }
+        }
+        uint32_t multi = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) multi |= cnt[i] >= 2 ? 1u << i : 0u;
+        mm[((uint64_t)b * V + v) * 64 + lane] = (uint8_t)multi;
+        if (__ballot(multi != 0) == 0) continue;
+        uint16_t *npv = np + ((uint64_t)b * V + v) * FR_SRC + lane * 8;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if ((multi >> i) & 1u) npv[i] = (uint16_t)cnt[i];
+        // second walk: the multi-parent sources' bits of every tight in-edge
+        uint8_t *mb = mul + (uint64_t)b * E * 64 + lane;
+        for (uint64_t k = e0; k < e1; ++k) {
+            const uint32_t o = in2out[k];  // wave-uniform
+            const uint32_t m = multi & tb[(uint64_t)o * 64];
+            if (m) mb[(uint64_t)o * 64] = (uint8_t)m;
         }
     }
 }
 
-// ---------------------------------------------------------- loss sweep
-// As the latency sweep, over tight lanes only: for a changed in-neighbour u,
-// lane l loads its tight byte of the edge and, if any of its 8 sources is
-// tight and u changed the lane's sources, u's 8 losses (32 B), and folds the
-// reached ones (P <= 1; 2.0 = not reached yet).
-constexpr int FR_EBL = 4;  // loss gathers per batch (2 x 16 B a lane each)
-__global__ __launch_bounds__(FR_WAVES * 64) void fr_loss_sweep_kernel(
-    const uint64_t *__restrict__ in_ptr, const InEdge *__restrict__ in_edge, uint32_t V, uint32_t NB, uint64_t E,
-    const uint8_t *__restrict__ tight, float *P, uint8_t *sbits, Chg *chg, uint32_t *act, uint32_t *last, uint32_t t,
-    const uint64_t *__restrict__ row_ptr, const uint32_t *__restrict__ col) {
+// ----------------------------------------------------------- loss push
+// Loss over the tight DAG, pushed once per pair: sweep t processes the items
+// (b, u) marked for it; a source s of u is final when its loss is -- single
+// tight parent: P <= 1 (the parent's store; 2.0 = not yet), two or more:
+// every parent has arrived (np == 0, values min-combined atomically).  The
+// lane's newly final sources (not in pushed) go along every out-edge o = (u
+// -> x): for the sources whose edge is tight (tight byte), P(s,x) = 1 - (1 -
+// P(s,u)) * (1 - e) -- a plain store for a single-parent pair, else atomicMin
+// on the f32 bits (non-negative floats order as their bits) then a fence and
+// the decrement of x's count -- and x is marked for sweep t + 1.  Every pair
+// is pushed once; the fold is the reference's (mod.rs:322-331).
+__global__ __launch_bounds__(FR_WAVES * 64) void fr_loss_push_kernel(
+    const uint64_t *__restrict__ out_ptr, const uint2 *__restrict__ out_edge, uint32_t V, uint32_t NB, uint64_t E,
+    const uint8_t *__restrict__ tight, const uint8_t *__restrict__ mul, const uint8_t *__restrict__ mm,
+    uint8_t *pushed, uint16_t *np, float *P, uint32_t *act, uint32_t *last, uint32_t t) {
     const int lane = threadIdx.x & 63;
     const uint32_t wave = blockIdx.x * FR_WAVES + (threadIdx.x >> 6), nwaves = gridDim.x * FR_WAVES;
     const uint32_t cpb = (V + 63) / 64, nchunks = cpb * NB;
@@ -349,82 +384,84 @@ __global__ __launch_bounds__(FR_WAVES * 64) void fr_loss_sweep_kernel(
         uint32_t *act_b = act + (uint64_t)b * V;
         const uint32_t a = v0 + lane < V ? act_b[v0 + lane] : 0u;
         uint64_t items = __ballot(a >= t);
-        float4 *Pb = reinterpret_cast<float4 *>(P + (uint64_t)b * V * FR_SRC);
+        float *Pb = P + (uint64_t)b * V * FR_SRC;
         const uint8_t *tb = tight + (uint64_t)b * E * 64 + lane;
-        uint8_t *sb = sbits + (uint64_t)b * V * 64 + lane;
-        Chg *chg_b = chg + (uint64_t)b * V;
+        const uint8_t *mb = mul + (uint64_t)b * E * 64 + lane;
         while (items) {
-            const uint32_t v = v0 + __builtin_ctzll(items);
+            const uint32_t u = v0 + __builtin_ctzll(items);
             items &= items - 1;
-            const float4 o0 = Pb[(uint64_t)v * 128 + 2 * lane], o1 = Pb[(uint64_t)v * 128 + 2 * lane + 1];
-            float best[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
-            const uint64_t e0 = in_ptr[v], e1 = in_ptr[v + 1];
+            const uint64_t iu = (uint64_t)b * V + u;
+            float *pu = Pb + (uint64_t)u * FR_SRC + lane * 8;
+            const float4 o0 = reinterpret_cast<const float4 *>(pu)[0], o1 = reinterpret_cast<const float4 *>(pu)[1];
+            float p[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+            const uint32_t pb = pushed[iu * 64 + lane], multi = mm[iu * 64 + lane];
+            uint32_t fin = 0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                if ((multi >> i) & 1u) {
+                    // arrivals are atomics at the memory side: read count and
+                    // value past this CU's caches
+                    const uint32_t idx = (uint32_t)(iu * FR_SRC + lane * 8 + i);
+                    const uint32_t cw = __hip_atomic_load(reinterpret_cast<uint32_t *>(np) + idx / 2, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+                    if (((cw >> (16 * (idx & 1))) & 0xffffu) == 0) {
+                        fin |= 1u << i;
+                        p[i] = __uint_as_float(__hip_atomic_load(reinterpret_cast<uint32_t *>(pu) + i, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT));
+                    }
+                } else if (p[i] <= 1.0f) {
+                    fin |= 1u << i;
+                }
+            }
+            const uint32_t newly = fin & ~pb;
+            if (__ballot(newly != 0) == 0) continue;
+            if (newly) pushed[iu * 64 + lane] = (uint8_t)(pb | newly);
+            if (lane == 0 && __builtin_nontemporal_load(last) != t) *last = t;
+            const uint64_t e0 = out_ptr[u], e1 = out_ptr[u + 1];
             for (uint64_t c0 = e0; c0 < e1; c0 += 64) {
                 const uint64_t k = c0 + lane;
-                uint32_t eu = 0;
-                uint64_t m = 0;
-                float eeb = 0.f;
-                if (k < e1) {
-                    const InEdge e = in_edge[k];
-                    eu = e.u;
-                    eeb = e.eb;
-                    m = changed_lanes(chg_b, eu, t);
-                }
-                uint64_t am = __ballot(m != 0);
-                while (am) {
-                    float4 x0[FR_EBL], x1[FR_EBL];
-                    uint32_t tm[FR_EBL];
-                    float eb[FR_EBL];
+                uint2 oe = make_uint2(0, 0);
+                if (k < e1) oe = out_edge[k];
+                const uint32_t n = e1 - c0 < 64 ? (uint32_t)(e1 - c0) : 64u;
+                for (uint32_t j0 = 0; j0 < n; j0 += FR_EB) {
+                    uint32_t m[FR_EB], ml[FR_EB];
 #pragma unroll
-                    for (int q = 0; q < FR_EBL; ++q) {
-                        tm[q] = 0;
-                        eb[q] = 0.f;
-                        x0[q] = x1[q] = make_float4(2.f, 2.f, 2.f, 2.f);
-                        if (am) {
-                            const int j = __builtin_ctzll(am);
-                            am &= am - 1;
-                            const uint32_t u = __builtin_amdgcn_readlane(eu, j);
-                            const uint32_t mlo = __builtin_amdgcn_readlane((uint32_t)m, j);
-                            const uint32_t mhi = __builtin_amdgcn_readlane((uint32_t)(m >> 32), j);
-                            eb[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(eeb), j));
-                            if (((lane < 32 ? mlo : mhi) >> (lane & 31)) & 1u) {
-                                // gather only when one of the lane's sources is
-                                // tight on this edge AND changed at u
-                                tm[q] = tb[(c0 + j) * 64];
-                                if (tm[q] & sb[(uint64_t)u * 64]) {
-                                    x0[q] = Pb[(uint64_t)u * 128 + 2 * lane];
-                                    x1[q] = Pb[(uint64_t)u * 128 + 2 * lane + 1];
-                                }
-                            }
+                    for (int q = 0; q < FR_EB; ++q) {
+                        m[q] = 0;
+                        ml[q] = 0;
+                        if (j0 + q < n && newly) {
+                            m[q] = tb[(c0 + j0 + q) * 64] & newly;
+                            if (m[q]) ml[q] = mb[(c0 + j0 + q) * 64];
                         }
                     }
 #pragma unroll
-                    for (int q = 0; q < FR_EBL; ++q) {
-                        const float xs[8] = {x0[q].x, x0[q].y, x0[q].z, x0[q].w, x1[q].x, x1[q].y, x1[q].z, x1[q].w};
+                    for (int q = 0; q < FR_EB; ++q) {
+                        if (j0 + q >= n) break;
+                        const uint32_t x = __builtin_amdgcn_readlane(oe.x, j0 + q);
+                        const float eb = __uint_as_float(__builtin_amdgcn_readlane(oe.y, j0 + q));
+                        if (m[q]) {
+                            float *px = Pb + (uint64_t)x * FR_SRC + lane * 8;
+                            const uint32_t base = (uint32_t)(((uint64_t)b * V + x) * FR_SRC + lane * 8);
 #pragma unroll
-                        for (int i = 0; i < 8; ++i)
-                            if (((tm[q] >> i) & 1u) && xs[i] <= 1.0f) {  // u reached (not the 2.0 init)
-                                const float cnd = fold(xs[i], eb[q]);
-                                best[i] = cnd < best[i] ? cnd : best[i];
+                            for (int i = 0; i < 8; ++i) {
+                                if (!((m[q] >> i) & 1u)) continue;
+                                const float val = fold(p[i], eb);
+                                if ((ml[q] >> i) & 1u) {
+                                    atomicMin(reinterpret_cast<uint32_t *>(px) + i, __float_as_uint(val));
+                                    __threadfence();
+                                    atomicSub(reinterpret_cast<uint32_t *>(np) + (base + i) / 2,
+                                              1u << (16 * ((base + i) & 1)));
+                                } else {
+                                    px[i] = val;
+                                }
                             }
+                        }
+                        if (__ballot(m[q] != 0) && lane == 0) {
+                            uint32_t *ax = act_b + x;
+                            if (*ax < t + 1) *ax = t + 1;
+                        }
                     }
                 }
-            }
-            const float ov[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
-            uint32_t ib = 0;  // the lane's improved sources
-#pragma unroll
-            for (int i = 0; i < 8; ++i) ib |= best[i] < ov[i] ? 1u << i : 0u;
-            const uint64_t im = __ballot(ib != 0);
-            if (im) {
-                if (ib) {
-                    Pb[(uint64_t)v * 128 + 2 * lane] = make_float4(best[0], best[1], best[2], best[3]);
-                    Pb[(uint64_t)v * 128 + 2 * lane + 1] = make_float4(best[4], best[5], best[6], best[7]);
-                }
-                // per-source change bits (kept from sweep t - 1 as the lanes are), before the record
-                const uint32_t st = chg_b[v].stamp;
-                const uint32_t keep = st + 1 == t ? sb[(uint64_t)v * 64] : 0u;
-                if (ib || keep) sb[(uint64_t)v * 64] = (uint8_t)(ib | keep);
-                publish(chg_b + v, act_b, last, v, im, t, row_ptr, col, lane);
             }
         }
     }
@@ -632,8 +669,8 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
         } else if ((e = hipMemsetAsync(p->d_fact, 0, (size_t)NB * V * 4, M)) != hipSuccess) {
             return hip_err(err, e, "sssp init");
         }
-        hipLaunchKernelGGL(fr_seed_kernel, seed_grid, dim3(256), 0, M, L, nullptr, nullptr, chg, p->d_fact, p->d_nodes,
-                           perm, V, q0, nsrc, t0, p->d_row_ptr, p->d_col);
+        hipLaunchKernelGGL(fr_seed_kernel, seed_grid, dim3(256), 0, M, L, nullptr, chg, p->d_fact, p->d_nodes, perm, V,
+                           q0, nsrc, t0, p->d_row_ptr, p->d_col);
         uint32_t t_end = 0, nsw = 0;
         srt_status st = run_phase(p, t0, chunk_lat, [&](uint32_t t) {
             hipLaunchKernelGGL(fr_lat_sweep_kernel, sgrid, sblk, 0, M, p->d_in_ptr, p->d_in_edge, V, NB, L, chg,
@@ -643,21 +680,24 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
         p->fr_lat_sweeps += nsw;
         p->sssp_sweeps += nsw;
         chunk_lat = std::max<uint32_t>(nsw + 1, 4);
-        // 2. tight masks
-        hipLaunchKernelGGL(fr_tight_kernel, sgrid, sblk, 0, M, p->d_in_ptr, p->d_in_edge, V, NB, E, L, p->d_ftight);
-        // 3. loss (stamps from t_end + 2: nothing of the latency phase is read;
-        //    activity cleared of the final marks)
+        // 2. tight masks (out-edge order) and the multi-parent pairs
+        if ((e = hipMemsetAsync(p->d_fmul, 0, (size_t)NB * E * 64, M)) != hipSuccess)
+            return hip_err(err, e, "sssp tight init");
+        hipLaunchKernelGGL(fr_tight_kernel, sgrid, sblk, 0, M, p->d_in_ptr, p->d_in_edge, p->d_fin2out, V, NB, E, L,
+                           p->d_ftight, p->d_fmul, p->d_fmm, p->d_fnp);
+        // 3. loss push (stamps from t_end + 2; activity cleared of the final marks)
         if ((e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p->d_fp), 0x40000000u, (size_t)NB * V * FR_SRC,
                                    M)) != hipSuccess ||
-            (e = hipMemsetAsync(p->d_fact, 0, (size_t)NB * V * 4, M)) != hipSuccess)
+            (e = hipMemsetAsync(p->d_fact, 0, (size_t)NB * V * 4, M)) != hipSuccess ||
+            (e = hipMemsetAsync(p->d_fpushed, 0, (size_t)NB * V * 64, M)) != hipSuccess)
             return hip_err(err, e, "sssp loss init");
         t0 = t_end + 2;
-        hipLaunchKernelGGL(fr_seed_kernel, seed_grid, dim3(256), 0, M, nullptr, p->d_fp, p->d_fsbits, chg, p->d_fact,
-                           p->d_nodes, perm, V, q0, nsrc, t0, p->d_row_ptr, p->d_col);
+        hipLaunchKernelGGL(fr_seed_kernel, seed_grid, dim3(256), 0, M, nullptr, p->d_fp, chg, p->d_fact, p->d_nodes,
+                           perm, V, q0, nsrc, t0, p->d_row_ptr, p->d_col);
         st = run_phase(p, t0, chunk_loss, [&](uint32_t t) {
-            hipLaunchKernelGGL(fr_loss_sweep_kernel, sgrid, sblk, 0, M, p->d_in_ptr, p->d_in_edge, V, NB, E,
-                               p->d_ftight, p->d_fp, p->d_fsbits, chg, p->d_fact, p->d_fimp, t, p->d_row_ptr,
-                               p->d_col);
+            hipLaunchKernelGGL(fr_loss_push_kernel, sgrid, sblk, 0, M, p->d_fout_ptr, p->d_fout_edge, V, NB, E,
+                               p->d_ftight, p->d_fmul, p->d_fmm, p->d_fpushed, p->d_fnp, p->d_fp, p->d_fact,
+                               p->d_fimp, t);
         }, &t_end, &nsw, err);
         if (st != SRT_OK) return st;
         p->fr_loss_sweeps += nsw;
@@ -675,10 +715,10 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
     return SRT_OK;
 }
 
-// device bytes of one 512-source block in flight: L (1 KB) + P (2 KB) + change
-// record (16 B) + per-source change bits (64 B) + activity (4 B) per vertex,
-// the tight masks (64 B) per in-edge
-uint64_t frontier_block_bytes(uint32_t V, uint64_t E) { return (uint64_t)V * (1024 + 2048 + 84) + E * 64; }
+// device bytes of one 512-source block in flight: L (1 KB) + P (2 KB) + parent
+// counts (1 KB) + change record (16 B) + multi / pushed masks (128 B) +
+// activity (4 B) per vertex, the tight and multi masks (128 B) per edge
+uint64_t frontier_block_bytes(uint32_t V, uint64_t E) { return (uint64_t)V * (1024 + 2048 + 1024 + 148) + E * 128; }
 size_t frontier_chg_bytes() { return sizeof(Chg); }
 
 }  // namespace srt

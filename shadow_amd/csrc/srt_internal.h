@@ -57,9 +57,23 @@ struct InEdge {
 
 }  // namespace srt
 
+namespace srt {
+struct LocalGroup;  // srt_comm.cpp: the ranks of one process (srt_comm_init_local)
+constexpr int MAX_LOCAL_RANKS = 16;
+// source buffers of one in-process collective, by rank (a kernel argument)
+struct PeerSrcs {
+    const uint8_t *p[MAX_LOCAL_RANKS];
+};
+// all-gather (only < 0): dst's slots [q * bytes, ...) <- src.p[q]'s, q != skip;
+// broadcast (only = root): dst[0, bytes) <- src.p[root][0, bytes); on stream s
+// (srt_peer.hip)
+void peer_gather(uint8_t *dst, const PeerSrcs &src, uint64_t bytes, int nranks, int skip, int only, hipStream_t s);
+}  // namespace srt
+
 struct srt_comm {
     int nranks = 1;
     int rank = 0;
+    srt::LocalGroup *local = nullptr;  // in-process transport (one host thread per rank)
     void *nccl = nullptr;  // ncclComm_t when the RCCL transport is used
     srt_bcast_fn bcast = nullptr;
     srt_allgather_fn allgather = nullptr;
@@ -213,7 +227,13 @@ struct srt_plan {
     uint8_t *d_ftight = nullptr;         // fr_nb * n_in_edges * 64 tight-source bytes
     void *d_fchg = nullptr;              // fr_nb * V change records (srt_frontier.hip Chg, 16 B)
     uint32_t *d_fact = nullptr;          // fr_nb * V activation stamps
-    uint8_t *d_fsbits = nullptr;         // fr_nb * V * 64 per-source change bits (loss sweeps)
+    uint8_t *d_fmul = nullptr;           // fr_nb * n_in_edges * 64: tight bytes of multi-parent pairs (out order)
+    uint8_t *d_fmm = nullptr;            // fr_nb * V * 64: per item and lane, the sources with >= 2 tight parents
+    uint8_t *d_fpushed = nullptr;        // fr_nb * V * 64: per item and lane, the sources already pushed
+    uint16_t *d_fnp = nullptr;           // fr_nb * V * 512: tight parents still to arrive (multi-parent pairs)
+    uint64_t *d_fout_ptr = nullptr;      // V + 1: out-edge rows (CSR minus self-loops)
+    uint2 *d_fout_edge = nullptr;        // {far end, 1 - loss f32 bits} per out-edge
+    uint32_t *d_fin2out = nullptr;       // per in-edge slot: its out-edge index
     uint32_t *d_fdone = nullptr;         // V: block (of this rank's rows) in which the vertex is a source, ~0 none
     std::vector<uint32_t> h_fdone;
     uint32_t *d_fimp = nullptr;          // last sweep that improved anything

@@ -141,3 +141,61 @@ def bind(plan, rank: int, world: int, device: int, transport: str = "rccl") -> C
     plan.bind_comm(comm.handle)
     plan._comm = comm
     return comm
+
+
+def local_comms(devices) -> list:
+    """srt_comm_init_local: one communicator per rank of THIS process (rank r
+    on devices[r]; a device may repeat).  Each rank's plan must be driven by
+    its own thread (see local_build)."""
+    L = _lib.lib()
+    n = len(devices)
+    devs = (C.c_int32 * n)(*devices)
+    hs = (_lib._vp * n)()
+    err = _lib.SrtErr()
+    _lib.check(L.srt_comm_init_local(n, devs, hs, C.byref(err)), err)
+    return [Comm(C.c_void_p(hs[r])) for r in range(n)]
+
+
+def local_build(graph, nodes, devices, algo: int = _lib.SRT_ALGO_AUTO):
+    """The in-process sharded build (what srt_opts.n_gpus does inside the
+    library), from Python so tests can inspect every rank's plan: one plan and
+    one thread per rank, collectives over srt_comm_init_local.  Returns rank
+    0's table and every rank's plan description and timing."""
+    import threading
+
+    from .plan import RoutingPlan
+
+    comms = local_comms(devices)
+    plans = [None] * len(devices)
+    errors = [None] * len(devices)
+
+    def rank(r):
+        try:
+            p = RoutingPlan(graph, nodes, algo=algo, device=devices[r])
+            plans[r] = p
+            p.bind_comm(comms[r].handle)
+            p.run()
+        except BaseException as e:  # noqa: BLE001 -- re-raised below
+            errors[r] = e
+            _lib.lib().srt_comm_abort(comms[r].handle)
+
+    ts = [threading.Thread(target=rank, args=(r,)) for r in range(len(devices))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    try:
+        for e in errors:
+            if e is not None and not (isinstance(e, _lib.SrtError) and e.code == _lib.SRT_ERR_COMM):
+                raise e
+        for e in errors:
+            if e is not None:
+                raise e
+        table = plans[0].fetch()
+        return table, [p.describe() for p in plans], [p.timing() for p in plans]
+    finally:
+        for p in plans:
+            if p is not None:
+                p.close()
+        for c in comms:
+            c.close()

@@ -177,7 +177,7 @@ class NetworkGraph:
         c.node_ids = self.node_ids.ctypes.data_as(C.POINTER(C.c_uint32))
         return c
 
-    def _run(self, fn_name: str, nodes, algo: int, device: int) -> PathTable:
+    def _run(self, fn_name: str, nodes, algo: int, device: int, n_gpus: int = 1, same_device: bool = False) -> PathTable:
         L = _lib.lib()
         _lib.require_device()
         nodes = np.ascontiguousarray(np.asarray(list(nodes) if not isinstance(nodes, np.ndarray) else nodes),
@@ -185,7 +185,7 @@ class NetworkGraph:
         n = len(nodes)
         out = (_lib.SrtPath * max(n * n, 1))()
         mn = C.c_uint64()
-        opts = _lib.SrtOpts(algo, device, 0, 0)
+        opts = _lib.SrtOpts(algo, device, _lib.SRT_OPT_SAME_DEVICE if same_device else 0, n_gpus)
         err = _lib.SrtErr()
         csr = self.csr()
         rc = getattr(L, fn_name)(C.byref(csr), nodes.ctypes.data_as(C.POINTER(C.c_uint32)), n, out, C.byref(mn),
@@ -195,11 +195,13 @@ class NetworkGraph:
         return PathTable(nodes, raw["lat"].reshape(n, n).copy(), raw["loss"].reshape(n, n).copy(), mn.value)
 
     def compute_shortest_paths(self, nodes: Iterable[int], algo: int = _lib.SRT_ALGO_AUTO,
-                               device: int = -1) -> PathTable:
+                               device: int = -1, n_gpus: int = 1, same_device: bool = False) -> PathTable:
         """mod.rs:183-228 on the GPU. Raises NetGraphError(code=NO_EDGE/MULTI_EDGE)
         for a missing/duplicate self-loop and code=DISCONNECTED where the
-        reference panics on an unreachable pair."""
-        return self._run("srt_compute_shortest_paths", nodes, algo, device)
+        reference panics on an unreachable pair.  n_gpus > 1: sharded over
+        devices device .. device + n_gpus - 1 from this process (one library
+        thread per device); same_device puts every rank on `device` (tests)."""
+        return self._run("srt_compute_shortest_paths", nodes, algo, device, n_gpus, same_device)
 
     def get_direct_paths(self, nodes: Iterable[int], device: int = -1) -> PathTable:
         """mod.rs:230-252 on the GPU."""
@@ -254,14 +256,14 @@ class RoutingInfo:
 
     @classmethod
     def build(cls, graph: "NetworkGraph", nodes, use_shortest_paths: bool = True, algo: int = _lib.SRT_ALGO_AUTO,
-              device: int = -1) -> "RoutingInfo":
+              device: int = -1, n_gpus: int = 1, same_device: bool = False) -> "RoutingInfo":
         L = _lib.lib()
         _lib.require_device()
         nodes = np.ascontiguousarray(np.asarray(list(nodes) if not isinstance(nodes, np.ndarray) else nodes),
                                      np.uint32)
         h = C.c_void_p()
         err = _lib.SrtErr()
-        opts = _lib.SrtOpts(algo, device, 0, 0)
+        opts = _lib.SrtOpts(algo, device, _lib.SRT_OPT_SAME_DEVICE if same_device else 0, n_gpus)
         csr = graph.csr()
         _lib.check(L.srt_routing_info_build(C.byref(csr), nodes.ctypes.data_as(C.POINTER(C.c_uint32)), len(nodes),
                                             int(bool(use_shortest_paths)), C.byref(opts), C.byref(h), C.byref(err)),
