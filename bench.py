@@ -64,6 +64,9 @@ CONFIGS = {
     # longest edge
     "c2nc": dict(kind="dense", nodes=4096, seed=2, drop=0.3),
     "c3": dict(kind="complete", nodes=16384, seed=3),
+    # C3 with ns-resolution latencies (a sub-ms offset on every edge): g = 1 ns,
+    # so the closure runs u32 keys and the loss pass the scan fold
+    "c3ns": dict(kind="complete", nodes=16384, seed=3, ns=True),
     "c4": dict(kind="ba", nodes=100_000, seed=4, m=4),
     "c5": dict(kind="packets", nodes=1000, seed=5, hosts=10_000, packets=1_000_000),
 }
@@ -295,7 +298,8 @@ def cold_child(args):
     if cfg["kind"] == "dense":
         row_ptr, col, lat, loss = synth.dense_csr(n, synth.dense_graph(n, seed, drop=cfg["drop"]))
     else:
-        row_ptr, col, lat, loss = synth.complete_csr(n, seed)
+        row_ptr, col, lat, loss = synth.complete_csr(n, seed, edges=synth.complete_graph_ns(n, seed)
+                                                     if cfg.get("ns") else None)
     g = NetworkGraph(n, np.arange(n, dtype=np.uint32), row_ptr, col, lat, loss, directed=False)
     nodes = np.arange(n, dtype=np.uint32)
     t1 = time.perf_counter()
@@ -397,13 +401,19 @@ def bench_graph(args, cfg, D):
     n_nodes = args.nodes or cfg["nodes"]
     seed = cfg["seed"] if args.seed < 0 else args.seed
     if cfg["kind"] == "complete":
-        row_ptr, col, lat, loss = synth.complete_csr(n_nodes, seed)
+        edges = synth.complete_graph_ns(n_nodes, seed) if cfg.get("ns") else None
+        row_ptr, col, lat, loss = synth.complete_csr(n_nodes, seed, edges=edges)
         g = NetworkGraph(n_nodes, np.arange(n_nodes, dtype=np.uint32), row_ptr, col, lat, loss, directed=False)
         nodes = np.arange(n_nodes, dtype=np.uint32)
-        label = (f"{args.config.upper()}: {n_nodes}-node complete undirected graph (CSR built directly; the same "
-                 f"values as the GML text of synth.gml_text, GML ingest not in this step)")
-        data = "synthetic (seeded complete graph, latency U{1..300} ms, loss U[0,0.01])"
-        og_args = None
+        if cfg.get("ns"):
+            label = (f"{args.config.upper()}: {n_nodes}-node complete undirected graph, latencies in ns (the C3 "
+                     f"ms values plus a seeded sub-ms offset: g = 1 ns), CSR built directly")
+            data = "synthetic (seeded complete graph, latency U{1..300} ms + U{0..999999} ns, loss U[0,0.01])"
+        else:
+            label = (f"{args.config.upper()}: {n_nodes}-node complete undirected graph (CSR built directly; the "
+                     f"same values as the GML text of synth.gml_text, GML ingest not in this step)")
+            data = "synthetic (seeded complete graph, latency U{1..300} ms, loss U[0,0.01])"
+        og_args = edges
         del row_ptr, col, lat, loss
     elif cfg["kind"] == "dense":
         edges = synth.dense_graph(n_nodes, seed, drop=cfg["drop"])

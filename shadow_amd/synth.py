@@ -25,6 +25,17 @@ def complete_graph(n: int, seed: int, lat_ms=(1, 300), loss_max=0.01, self_loops
     return iu.astype(np.uint32), ju.astype(np.uint32), lat, loss
 
 
+def complete_graph_ns(n: int, seed: int, lat_ms=(1, 300), loss_max=0.01):
+    """complete_graph(n, seed) with every latency given in ns plus a seeded
+    sub-ms offset U{0..999_999} ns: the gcd of the latencies is 1 ns, so the
+    closure carries ns units (u32 keys at 16k: the longest edge is < 3.01e8
+    units) and the loss pass's tight weights exceed the level fold's classes
+    (units.rs:377-388: Shadow reads latencies as any time unit down to ns)."""
+    src, dst, lat, loss = complete_graph(n, seed, lat_ms, loss_max)
+    off = np.random.default_rng(seed + 7).integers(0, MS, size=len(lat), dtype=np.uint64)
+    return src, dst, lat + off, loss
+
+
 def complete_csr(n: int, seed: int, lat_ms=(1, 300), loss_max=0.01, edges=None):
     """CSR (petgraph adjacency of the undirected complete graph) built directly,
     without the O(n^2) edge-list sort: row u lists all v (self-loop once).

@@ -92,6 +92,37 @@ def test_c3_16k_rows_vs_oracle_and_symmetry():
     plan.close()
 
 
+def test_c3ns_16k_u32_keys_rows_vs_oracle():
+    """C3 with ns latencies (bench --config c3ns): g = 1 ns, so the closure
+    runs u32 keys and the loss pass the scan fold; 16 seeded rows bit-exact
+    against the oracle, symmetry over the device table."""
+    import torch
+
+    n = 16384
+    edges = synth.complete_graph_ns(n, 3)
+    row_ptr, col, lat, loss = synth.complete_csr(n, 3, edges=edges)
+    g = NetworkGraph(n, np.arange(n, dtype=np.uint32), row_ptr, col, lat, loss, directed=False)
+    nodes = np.arange(n, dtype=np.uint32)
+    plan = RoutingPlan(g, nodes).run()
+    d = plan.describe()
+    assert d.startswith("fw:u32key g=1 "), d
+    assert plan.timing()["loss_fold"] == 0  # tight weights in ns units: the scan fold
+    plan.fetch(table=False)
+    L, P = _device_table(plan)
+    assert torch.equal(L, L.t())
+    rows = np.random.default_rng(33).choice(n, 16, replace=False)
+    order = np.concatenate([rows, np.setdiff1d(nodes, rows)]).astype(np.uint32)
+    og = O.Graph(False, nodes, *edges)
+    del row_ptr, col
+    elat, eloss = O.compute_shortest_paths(og, order, src_count=16, mode=1)
+    inv = np.empty(n, np.int64)
+    inv[order] = np.arange(n)
+    sl_l = lat.reshape(n, n).diagonal().copy()
+    sl_p = loss.reshape(n, n).diagonal().copy()
+    _check_rows(L, P, rows, nodes, elat[:16][:, inv], eloss[:16][:, inv], sl_l, sl_p)
+    plan.close()
+
+
 def test_c4_100k_all_in_use():
     import torch
 

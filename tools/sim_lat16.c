@@ -250,11 +250,40 @@ int main(int argc, char **argv) {
                 if (d != UINT32_MAX && d + iw[k] == L[(uint64_t)v * 64 + s]) ++tight;
             }
     printf("tight (edge, lane) pairs per (vertex, lane): %.3f\n", (double)tight / ((double)V * 64));
+    /* loss-phase vertex order (argv[6]): 0 = vertex id, 1 = latency from the
+       word's first source, 2 = hops from it */
+    const int LORD = argc > 6 ? atoi(argv[6]) : 0;
+    uint32_t *lord = malloc(4 * V);
+    for (uint32_t v = 0; v < V; ++v) lord[v] = v;
+    if (LORD) {
+        uint64_t *key = malloc(8 * V);
+        uint32_t *hop = malloc(4 * V), *qq = malloc(4 * V), h0 = 0, h1 = 0;
+        for (uint32_t v = 0; v < V; ++v) hop[v] = UINT32_MAX;
+        hop[srcs[0]] = 0;
+        qq[h1++] = srcs[0];
+        while (h0 < h1) {
+            const uint32_t x = qq[h0++];
+            for (uint64_t k = ptr[x]; k < ptr[x + 1]; ++k)
+                if (hop[iu[k]] == UINT32_MAX) {
+                    hop[iu[k]] = hop[x] + 1;
+                    qq[h1++] = iu[k];
+                }
+        }
+        for (uint32_t v = 0; v < V; ++v)
+            key[v] = ((uint64_t)(LORD == 1 ? L[(uint64_t)v * 64] : hop[v]) << 32) | v;
+        int cmp(const void *a, const void *b) {
+            const uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
+            return x < y ? -1 : x > y;
+        }
+        qsort(key, V, 8, cmp);
+        for (uint32_t i = 0; i < V; ++i) lord[i] = (uint32_t)key[i];
+    }
     uint32_t tl = 0;
     uint64_t ltot = 0;
     for (;;) {
         uint64_t lines = 0, act = 0, impv = 0;
-        for (uint32_t v = 0; v < V; ++v) {
+        for (uint32_t vi = 0; vi < V; ++vi) {
+            const uint32_t v = lord[vi];
             int a = 0;
             float best[64];
             for (int s = 0; s < 64; ++s) best[s] = 2.0f;
