@@ -482,13 +482,11 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_fchg);
     hipFree(p->d_fact);
     hipFree(p->d_fdone);
-    hipFree(p->d_fmul);
-    hipFree(p->d_fmm);
-    hipFree(p->d_fpushed);
-    hipFree(p->d_fnp);
-    hipFree(p->d_fout_ptr);
-    hipFree(p->d_fout_edge);
-    hipFree(p->d_fin2out);
+    hipFree(p->d_fsb);
+    hipFree(p->d_ffin);
+    hipFree(p->d_fnodes);
+    hipFree(p->d_frow_ptr);
+    hipFree(p->d_fcol);
     hipFree(p->d_fimp);
     if (p->h_fimp) hipHostFree(p->h_fimp);
     hipFree(p->d_rstats);
@@ -555,32 +553,6 @@ void build_in_edges(const srt_csr *g, uint64_t gunit, uint64_t n_in, std::vector
             e.pad = 0;
             (*edges)[fill[v]++] = e;
         }
-}
-
-// Out-edge list of the frontier's loss push (srt_frontier.hip): the CSR minus
-// self-loops, {far end, 1 - loss as f32 bits} (8 B), row offsets, and for every
-// in-edge slot of build_in_edges the out-edge it is (so the tight pass, which
-// walks in-edges, stores its masks in out-edge order for the push).
-void build_out_edges(const srt_csr *g, const std::vector<uint64_t> &in_ptr, std::vector<uint64_t> *out_ptr,
-                     std::vector<uint2> *out_edge, std::vector<uint32_t> *in2out) {
-    const uint32_t V = g->n_nodes;
-    out_ptr->assign((size_t)V + 1, 0);
-    const uint64_t E = in_ptr.empty() ? 0 : in_ptr[V];
-    out_edge->resize(std::max<uint64_t>(E, 1));
-    in2out->resize(std::max<uint64_t>(E, 1));
-    std::vector<uint64_t> fill(in_ptr.begin(), in_ptr.end() - 1);
-    uint64_t o = 0;
-    for (uint32_t u = 0; u < V; ++u) {
-        for (uint64_t k = g->row_ptr[u]; k < g->row_ptr[u + 1]; ++k) {
-            const uint32_t v = g->col[k];
-            if (v == u) continue;
-            const float eb = 1.0f - g->loss[k];
-            (*out_edge)[o] = make_uint2(v, __builtin_bit_cast(uint32_t, eb));
-            (*in2out)[fill[v]++] = (uint32_t)o;
-            ++o;
-        }
-        (*out_ptr)[u + 1] = o;
-    }
 }
 
 // Is the latency adjacency symmetric (every u -> v of latency w has a v -> u of
@@ -972,10 +944,7 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
             const unsigned __int128 lb = ecc_units != ~0ull ? (unsigned __int128)ecc_units
                                                             : (unsigned __int128)(p->V ? p->V - 1 : 0) * maxu;
             const char *kk = std::getenv("SRT_SSSP_KEY");
-            uint64_t maxdeg = 0;
-            for (uint32_t v = 0; v < p->V; ++v) maxdeg = std::max<uint64_t>(maxdeg, in_ptr[v + 1] - in_ptr[v]);
-            // (the loss push counts a pair's tight parents in u16)
-            p->sssp_frontier = lb < 0xffff && maxdeg < 0xffff && !(kk && std::atoi(kk) == 64);
+            p->sssp_frontier = lb < 0xffff && !(kk && std::atoi(kk) == 64);
         }
         if (!p->sssp_frontier) {
             PLAN_TRY(dmalloc(&p->d_sD, (size_t)p->sssp_nb * p->V * 64, err));
@@ -1034,39 +1003,17 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
             // free HBM holds them.  Knob SRT_SSSP_SYM=0 (A/B, tests).
             const uint64_t all_blocks = std::max<uint32_t>(1, (n + 511) / 512);
             const char *ks = std::getenv("SRT_SSSP_SYM");
+            p->fr_symg = latency_symmetric(g, in_ptr, in_edge, cs.gcd);
             p->fr_sym = !(ks && std::atoi(ks) == 0) && all_blocks > nb &&
-                        all_blocks * p->V * 1024ull <= (uint64_t)free_b / 4 && latency_symmetric(g, in_ptr, in_edge, cs.gcd);
+                        all_blocks * p->V * 1024ull <= (uint64_t)free_b / 4 && p->fr_symg;
             p->fr_lblocks = p->fr_sym ? (uint32_t)all_blocks : (uint32_t)nb;
             PLAN_TRY(dmalloc(&p->d_fl, (size_t)p->fr_lblocks * p->V * 512, err));
             PLAN_TRY(dmalloc(&p->d_fp, (size_t)nb * p->V * 512, err));
             PLAN_TRY(dmalloc(&p->d_ftight, (size_t)nb * std::max<uint64_t>(n_in, 1) * 64, err));
             PLAN_TRY(dmalloc(reinterpret_cast<uint8_t **>(&p->d_fchg), (size_t)nb * p->V * srt::frontier_chg_bytes(), err));
             PLAN_TRY(dmalloc(&p->d_fact, (size_t)nb * p->V, err));
-            // the loss push: out-edges, tight / multi-parent bytes in out-edge
-            // order, per item the multi-parent mask, pushed mask and (multi
-            // pairs) remaining-parent counts
-            PLAN_TRY(dmalloc(&p->d_fmul, (size_t)nb * std::max<uint64_t>(n_in, 1) * 64, err));
-            PLAN_TRY(dmalloc(&p->d_fmm, (size_t)nb * p->V * 64, err));
-            PLAN_TRY(dmalloc(&p->d_fpushed, (size_t)nb * p->V * 64, err));
-            PLAN_TRY(dmalloc(&p->d_fnp, (size_t)nb * p->V * 512, err));
-            {
-                std::vector<uint64_t> out_ptr;
-                std::vector<uint2> out_edge;
-                std::vector<uint32_t> in2out;
-                build_out_edges(g, in_ptr, &out_ptr, &out_edge, &in2out);
-                PLAN_TRY(dmalloc(&p->d_fout_ptr, out_ptr.size(), err));
-                PLAN_TRY(dmalloc(&p->d_fout_edge, out_edge.size(), err));
-                PLAN_TRY(dmalloc(&p->d_fin2out, in2out.size(), err));
-                if ((e = hipMemcpy(p->d_fout_ptr, out_ptr.data(), out_ptr.size() * 8, hipMemcpyHostToDevice)) !=
-                        hipSuccess ||
-                    (e = hipMemcpy(p->d_fout_edge, out_edge.data(), out_edge.size() * 8, hipMemcpyHostToDevice)) !=
-                        hipSuccess ||
-                    (e = hipMemcpy(p->d_fin2out, in2out.data(), in2out.size() * 4, hipMemcpyHostToDevice)) !=
-                        hipSuccess) {
-                    srt_plan_destroy(p);
-                    return hip_fail(err, e, "sparse frontier out-edges");
-                }
-            }
+            PLAN_TRY(dmalloc(&p->d_fsb, (size_t)2 * nb * p->V * 64, err));
+            PLAN_TRY(dmalloc(&p->d_ffin, (size_t)nb * p->V, err));
             PLAN_TRY(dmalloc(&p->d_fimp, 1, err));
             if ((e = hipMemsetAsync(p->d_fchg, 0, (size_t)nb * p->V * srt::frontier_chg_bytes(), p->stream)) != hipSuccess ||
                 (e = hipMemsetAsync(p->d_fact, 0, (size_t)nb * p->V * 4, p->stream)) != hipSuccess ||
@@ -1089,6 +1036,69 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         if ((e = hipHostMalloc((void **)&p->h_sflag, (size_t)p->sssp_nb * sizeof(uint32_t), 0)) != hipSuccess) {
             srt_plan_destroy(p);
             return hip_fail(err, e, "hipHostMalloc");
+        }
+        if (p->sssp_frontier) {
+            // Hub-spreading vertex order for the frontier sweeps: a wave works
+            // through a 64-vertex chunk item by item, so a chunk of hubs (BA
+            // graphs number them first: C4's vertices 0..63 have ~1000
+            // in-edges each) would keep one wave busy for the whole sweep
+            // (measured: C4 1.71 s -> 1.07 s with the hubs dealt out).  The
+            // cpb highest in-degree vertices go to slot 0 of the cpb chunks,
+            // one each; every other vertex keeps its relative order (BA graphs'
+            // id locality: neighbours of similar age gather similar rows).
+            const uint32_t V = p->V, cpb = (V + 63) / 64;
+            std::vector<uint32_t> order(V), pi(V, ~0u);
+            for (uint32_t v = 0; v < V; ++v) order[v] = v;
+            std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+                return in_ptr[a + 1] - in_ptr[a] > in_ptr[b + 1] - in_ptr[b];
+            });
+            const uint32_t H = V >= 64 * cpb ? cpb : (V > cpb ? cpb - 1 : 0);  // chunks with a full slot 0
+            std::vector<uint8_t> hub(V, 0);
+            for (uint32_t h = 0; h < H; ++h) {
+                pi[order[h]] = h * 64;
+                hub[order[h]] = 1;
+            }
+            for (uint32_t v = 0, pos = 0; v < V; ++v) {
+                if (hub[v]) continue;
+                while (pos % 64 == 0 && pos / 64 < H) ++pos;  // slot 0 of a hub chunk
+                pi[v] = pos++;
+            }
+            std::vector<uint64_t> ip(V + 1, 0), op(V + 1, 0);
+            for (uint32_t v = 0; v < V; ++v) {
+                ip[pi[v] + 1] = in_ptr[v + 1] - in_ptr[v];
+                uint64_t d = 0;
+                for (uint64_t k = g->row_ptr[v]; k < g->row_ptr[v + 1]; ++k) d += g->col[k] != v;
+                op[pi[v] + 1] = d;
+            }
+            for (uint32_t v = 0; v < V; ++v) {
+                ip[v + 1] += ip[v];
+                op[v + 1] += op[v];
+            }
+            std::vector<srt::InEdge> ie(in_edge.size());
+            std::vector<uint32_t> oc(std::max<uint64_t>(op[V], 1));
+            for (uint32_t v = 0; v < V; ++v) {
+                uint64_t o = ip[pi[v]];
+                for (uint64_t k = in_ptr[v]; k < in_ptr[v + 1]; ++k, ++o) {
+                    ie[o] = in_edge[k];
+                    ie[o].u = pi[in_edge[k].u];
+                }
+                o = op[pi[v]];
+                for (uint64_t k = g->row_ptr[v]; k < g->row_ptr[v + 1]; ++k)
+                    if (g->col[k] != v) oc[o++] = pi[g->col[k]];
+            }
+            in_ptr.swap(ip);
+            in_edge.swap(ie);
+            p->h_fnodes.resize(n);
+            for (uint32_t i = 0; i < n; ++i) p->h_fnodes[i] = pi[nodes[i]];
+            PLAN_TRY(dmalloc(&p->d_fnodes, std::max<uint32_t>(n, 1), err));
+            PLAN_TRY(dmalloc(&p->d_frow_ptr, op.size(), err));
+            PLAN_TRY(dmalloc(&p->d_fcol, oc.size(), err));
+            if ((e = hipMemcpy(p->d_fnodes, p->h_fnodes.data(), (size_t)n * 4, hipMemcpyHostToDevice)) != hipSuccess ||
+                (e = hipMemcpy(p->d_frow_ptr, op.data(), op.size() * 8, hipMemcpyHostToDevice)) != hipSuccess ||
+                (e = hipMemcpy(p->d_fcol, oc.data(), oc.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) {
+                srt_plan_destroy(p);
+                return hip_fail(err, e, "upload frontier graph");
+            }
         }
         if ((e = hipMemcpy(p->d_in_ptr, in_ptr.data(), in_ptr.size() * 8, hipMemcpyHostToDevice)) != hipSuccess ||
             (e = hipMemcpy(p->d_in_edge, in_edge.data(), in_edge.size() * sizeof(srt::InEdge),

@@ -55,6 +55,7 @@ namespace {
 constexpr uint32_t FR_SRC = 512;     // sources per block (8 words of 64)
 constexpr int FR_WAVES = 4;          // waves per sweep workgroup
 constexpr int FR_EB = 8;             // edges gathered per batch (loads in flight per lane)
+constexpr int FR_EBL = 4;            // loss sweep: edges per batch (2 x 16 B gathered a lane each)
 constexpr uint32_t L16_INF = 0xffffu;
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -99,28 +100,33 @@ struct Chg {
     uint32_t stamp, pad;
     uint64_t lanes;
 };
-constexpr uint32_t ACT_FINAL = 0xffffffffu;  // (b, v) exact from the start (symmetric seeding)
 
-// After (b, v) improved lanes `im` in sweep t: its change record (keeping the
-// lanes of sweep t - 1, which readers of this sweep may still need), the
-// phase's last-improvement stamp, and the marks of its out-neighbours for
-// sweep t + 1 (raise only: a final item keeps ACT_FINAL).
-__device__ __forceinline__ void publish(Chg *chg_bv, uint32_t *act_b, uint32_t *last, uint32_t v, uint64_t im,
-                                        uint32_t t, const uint64_t *__restrict__ row_ptr,
-                                        const uint32_t *__restrict__ col, int lane) {
-    if (lane == 0) {
-        const Chg old = *chg_bv;
-        Chg c;
-        c.stamp = t;
-        c.pad = 0;
-        c.lanes = im | (old.stamp + 1 == t ? old.lanes : 0ull);
-        *chg_bv = c;
-        if (__builtin_nontemporal_load(last) != t) *last = t;  // hot word: read first
+// The marks of v's out-neighbours for sweep t + 1, plain stores (stamps only
+// grow, and final items are flagged apart, so a mark never lowers anything and
+// needs no read first).  Latency-symmetric graphs: the out-neighbours are the
+// in-edge sources, already in the lanes' registers (eu_last: the last in-edge
+// chunk, the only one at <= 64 in-edges); else the CSR row.
+__device__ __forceinline__ void mark(uint32_t *act_b, uint32_t v, uint32_t t, bool sym, const InEdge *in_edge,
+                                     uint32_t eu_last, uint64_t e0, uint64_t e1, const uint64_t *__restrict__ row_ptr,
+                                     const uint32_t *__restrict__ col, int lane) {
+    if (sym) {
+        if (e1 - e0 <= 64) {
+            if (e0 + lane < e1) act_b[eu_last] = t + 1;
+        } else {
+            for (uint64_t k = e0 + lane; k < e1; k += 64) act_b[in_edge[k].u] = t + 1;
+        }
+    } else {
+        for (uint64_t k = row_ptr[v] + lane; k < row_ptr[v + 1]; k += 64) {
+            const uint32_t x = col[k];
+            if (x != v) act_b[x] = t + 1;
+        }
     }
-    for (uint64_t k = row_ptr[v] + lane; k < row_ptr[v + 1]; k += 64) {
-        const uint32_t x = col[k];
-        if (x != v && act_b[x] < t + 1) act_b[x] = t + 1;  // hubs: read before the store
-    }
+}
+
+// the phase's last-improvement stamp, once per wave at the end of a sweep
+// (every improving wave stores the same value: read first, a hot word)
+__device__ __forceinline__ void note_improved(uint32_t *last, uint32_t t, bool any, int lane) {
+    if (__ballot(any) && lane == 0 && __builtin_nontemporal_load(last) != t) *last = t;
 }
 
 // the lanes of u that changed in sweep t - 1 or t (0 if none)
@@ -132,10 +138,10 @@ __device__ __forceinline__ uint64_t changed_lanes(const Chg *chg_b, uint32_t u, 
 // -------------------------------------------------------------- seeds
 // slot q of the launch (q < nsrc): block q / 512, source q % 512 of it; the
 // table row is perm[q0 + q] (perm null: q0 + q), the source vertex nodes[row].
-// Phase 1 (L given): L = 0, the source's lane marked changed in sweep t0 and
-// its out-neighbours marked for t0 + 1.  Phase 3: P = 0, the source's own item
-// marked for t0 + 1 (it pushes first).
-__global__ void fr_seed_kernel(uint16_t *__restrict__ L, float *__restrict__ P, Chg *chg,
+// Phase 1 (L given): L = 0 and the source's lane marked changed in sweep t0;
+// phase 3: P = 0 and the source's change bit set.  Either way its
+// out-neighbours are marked for sweep t0 + 1.
+__global__ void fr_seed_kernel(uint16_t *__restrict__ L, float *__restrict__ P, uint8_t *__restrict__ sbits, Chg *chg,
                                uint32_t *act, const uint32_t *__restrict__ nodes, const uint32_t *__restrict__ perm,
                                uint32_t V, uint32_t q0, uint32_t nsrc, uint32_t t0,
                                const uint64_t *__restrict__ row_ptr, const uint32_t *__restrict__ col) {
@@ -145,20 +151,20 @@ __global__ void fr_seed_kernel(uint16_t *__restrict__ L, float *__restrict__ P, 
     const uint32_t src = nodes[perm ? perm[q0 + q] : q0 + q];
     const uint64_t row = (uint64_t)b * V + src;
     uint32_t *act_b = act + (uint64_t)b * V;
-    if (!L) {  // loss push: the source pair is final at 0; its item pushes in sweep t0 + 1
+    if (L) {
+        L[row * FR_SRC + i] = 0;
+        Chg c;
+        c.stamp = t0;
+        c.pad = 0;
+        c.lanes = 1ull << (i / 8);  // sources of a launch are distinct vertices
+        chg[row] = c;
+    } else {
         P[row * FR_SRC + i] = 0.0f;
-        act_b[src] = t0 + 1;
-        return;
+        sbits[row * 64 + i / 8] = (uint8_t)(1u << (i % 8));  // the source's own change bit
     }
-    L[row * FR_SRC + i] = 0;
-    Chg c;
-    c.stamp = t0;
-    c.pad = 0;
-    c.lanes = 1ull << (i / 8);  // sources of a launch are distinct vertices
-    chg[row] = c;
     for (uint64_t k = row_ptr[src]; k < row_ptr[src + 1]; ++k) {
         const uint32_t x = col[k];
-        if (x != src && act_b[x] < t0 + 1) act_b[x] = t0 + 1;
+        if (x != src) act_b[x] = t0 + 1;
     }
 }
 
@@ -196,22 +202,22 @@ __global__ __launch_bounds__(256) void fr_sym_copy_kernel(uint16_t *L, const uin
 }
 
 // Symmetric seeding, activity: an item (b, v) whose v is a source of an
-// earlier block (done[v] < B0) is final -- ACT_FINAL, changed in every lane
-// in sweep t0; every other item is active in sweep t0 + 1.
-__global__ void fr_sym_act_kernel(uint32_t *act, Chg *chg, const uint32_t *__restrict__ done, uint32_t V, uint32_t NB,
-                                  uint32_t B0, uint32_t t0) {
+// earlier block (done[v] < B0) is final -- fin = 1, changed in every lane in
+// sweep t0; every other item is active in sweep t0 + 1.
+__global__ void fr_sym_act_kernel(uint32_t *act, uint8_t *fin, Chg *chg, const uint32_t *__restrict__ done, uint32_t V,
+                                  uint32_t NB, uint32_t B0, uint32_t t0) {
     const uint64_t n = (uint64_t)NB * V;
     for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < n; e += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t v = (uint32_t)(e % V);
-        if (done[v] < B0) {
-            act[e] = ACT_FINAL;
+        const bool f = done[v] < B0;
+        fin[e] = f;
+        act[e] = t0 + 1;
+        if (f) {
             Chg c;
             c.stamp = t0;
             c.pad = 0;
             c.lanes = ~0ull;
             chg[e] = c;
-        } else {
-            act[e] = t0 + 1;
         }
     }
 }
@@ -224,28 +230,34 @@ __global__ void fr_sym_act_kernel(uint32_t *act, Chg *chg, const uint32_t *__res
 // relaxation.  The own row is loaded first (independent of the chain).
 __global__ __launch_bounds__(FR_WAVES * 64) void fr_lat_sweep_kernel(
     const uint64_t *__restrict__ in_ptr, const InEdge *__restrict__ in_edge, uint32_t V, uint32_t NB,
-    uint16_t *L, Chg *chg, uint32_t *act, uint32_t *last, uint32_t t, const uint64_t *__restrict__ row_ptr,
-    const uint32_t *__restrict__ col) {
+    uint16_t *L, Chg *chg, uint32_t *act, const uint8_t *__restrict__ fin, uint32_t *last, uint32_t t, bool sym,
+    const uint64_t *__restrict__ row_ptr, const uint32_t *__restrict__ col) {
     const int lane = threadIdx.x & 63;
     const uint32_t wave = blockIdx.x * FR_WAVES + (threadIdx.x >> 6), nwaves = gridDim.x * FR_WAVES;
     const uint32_t cpb = (V + 63) / 64, nchunks = cpb * NB;
+    bool any_imp = false;
     for (uint32_t c = __builtin_amdgcn_readfirstlane(wave); c < nchunks; c += nwaves) {
         const uint32_t b = c / cpb, v0 = (c % cpb) * 64;
         uint32_t *act_b = act + (uint64_t)b * V;
-        const uint32_t a = v0 + lane < V ? act_b[v0 + lane] : 0u;
-        uint64_t items = __ballot(a >= t && a != ACT_FINAL);
+        const bool in = v0 + lane < V;
+        const uint32_t a = in ? act_b[v0 + lane] : 0u;
+        const bool f = in && fin[(uint64_t)b * V + v0 + lane];
+        uint64_t items = __ballot(a >= t && !f);
         uint4 *Lb = reinterpret_cast<uint4 *>(L + (uint64_t)b * V * FR_SRC);
         Chg *chg_b = chg + (uint64_t)b * V;
         while (items) {
             const uint32_t v = v0 + __builtin_ctzll(items);
             items &= items - 1;
             const uint4 own = Lb[(uint64_t)v * 64 + lane];
+            const Chg old = chg_b[v];  // own record, for the kept lanes (loaded beside the row)
             uint4 best = own;
             const uint64_t e0 = in_ptr[v], e1 = in_ptr[v + 1];
+            uint32_t eu = 0;
             for (uint64_t c0 = e0; c0 < e1; c0 += 64) {
                 const uint64_t k = c0 + lane;
-                uint32_t eu = 0, ew = 0;
+                uint32_t ew = 0;
                 uint64_t m = 0;
+                eu = 0;
                 if (k < e1) {
                     const InEdge e = in_edge[k];
                     eu = e.u;
@@ -277,26 +289,31 @@ __global__ __launch_bounds__(FR_WAVES * 64) void fr_lat_sweep_kernel(
             }
             const bool imp = best.x != own.x || best.y != own.y || best.z != own.z || best.w != own.w;
             const uint64_t im = __ballot(imp);
-            if (im) {
-                if (imp) Lb[(uint64_t)v * 64 + lane] = best;
-                publish(chg_b + v, act_b, last, v, im, t, row_ptr, col, lane);
+            if (!im) continue;
+            any_imp = true;
+            if (imp) Lb[(uint64_t)v * 64 + lane] = best;
+            if (lane == 0) {  // this sweep's lanes, and those of sweep t - 1 that readers may still need
+                Chg cnew;
+                cnew.stamp = t;
+                cnew.pad = 0;
+                cnew.lanes = im | (old.stamp + 1 == t ? old.lanes : 0ull);
+                chg_b[v] = cnew;
             }
+            mark(act_b, v, t, sym, in_edge, eu, e0, e1, row_ptr, col, lane);
         }
     }
+    note_improved(last, t, any_imp, lane);
 }
 
 // ---------------------------------------------------------- tight pass
-// Every item (b, v), every in-edge k = (u -> v) of v, stored at its out-edge
-// index o = in2out[k]: tight[(b * E + o) * 64 + lane] = the lane's 8-bit mask
-// of sources s with L(s,u) + w == L(s,v) -- the edges the loss push walks.
-// Per source the tight parents are counted; the sources with two or more
-// (ties, ~0.7% of pairs at C4) are marked in mm[b][v][lane], their counts
-// stored in np[b][v][s], and a second walk stores their edges' bits in mul
-// (the push takes the atomic path for exactly those).
-__global__ __launch_bounds__(FR_WAVES * 64) void fr_tight_kernel(
-    const uint64_t *__restrict__ in_ptr, const InEdge *__restrict__ in_edge, const uint32_t *__restrict__ in2out,
-    uint32_t V, uint32_t NB, uint64_t E, const uint16_t *__restrict__ L, uint8_t *__restrict__ tight,
-    uint8_t *__restrict__ mul, uint8_t *__restrict__ mm, uint16_t *__restrict__ np) {
+// Every item (b, v), every in-edge k = (u -> v) of v:
+// tight[(b * E + k) * 64 + lane] = the lane's 8-bit mask of sources s with
+// L(s,u) + w == L(s,v) -- the only edges the loss sweeps read along.
+__global__ __launch_bounds__(FR_WAVES * 64) void fr_tight_kernel(const uint64_t *__restrict__ in_ptr,
+                                                                 const InEdge *__restrict__ in_edge, uint32_t V,
+                                                                 uint32_t NB, uint64_t E,
+                                                                 const uint16_t *__restrict__ L,
+                                                                 uint8_t *__restrict__ tight) {
     const int lane = threadIdx.x & 63;
     const uint32_t wave = blockIdx.x * FR_WAVES + (threadIdx.x >> 6), nwaves = gridDim.x * FR_WAVES;
     const uint64_t nitems = (uint64_t)V * NB;
@@ -305,166 +322,134 @@ __global__ __launch_bounds__(FR_WAVES * 64) void fr_tight_kernel(
         const uint4 *Lb = reinterpret_cast<const uint4 *>(L + (uint64_t)b * V * FR_SRC);
         const uint4 own = Lb[(uint64_t)v * 64 + lane];
         uint8_t *tb = tight + (uint64_t)b * E * 64 + lane;
-        uint32_t cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         const uint64_t e0 = in_ptr[v], e1 = in_ptr[v + 1];
         for (uint64_t c0 = e0; c0 < e1; c0 += 64) {
             const uint64_t k = c0 + lane;
-            uint32_t eu = 0, ew = 0, eo = 0;
+            uint32_t eu = 0, ew = 0;
             if (k < e1) {
                 const InEdge e = in_edge[k];
                 eu = e.u;
                 ew = e.w;
-                eo = in2out[k];
             }
             const uint32_t n = e1 - c0 < 64 ? (uint32_t)(e1 - c0) : 64u;
             for (uint32_t j0 = 0; j0 < n; j0 += FR_EB) {
                 uint4 x[FR_EB];
-                uint32_t w[FR_EB], o[FR_EB];
+                uint32_t w[FR_EB];
 #pragma unroll
                 for (int q = 0; q < FR_EB; ++q) {
                     w[q] = 0;
-                    o[q] = 0;
                     x[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
                     if (j0 + q < n) {
                         const uint32_t u = __builtin_amdgcn_readlane(eu, j0 + q);
                         w[q] = __builtin_amdgcn_readlane(ew, j0 + q);
-                        o[q] = __builtin_amdgcn_readlane(eo, j0 + q);
                         x[q] = Lb[(uint64_t)u * 64 + lane];
                     }
                 }
 #pragma unroll
                 for (int q = 0; q < FR_EB; ++q)
-                    if (j0 + q < n) {
-                        const uint32_t tm = tight8(x[q], own, w[q]);
-                        tb[(uint64_t)o[q] * 64] = (uint8_t)tm;
-#pragma unroll
-                        for (int i = 0; i < 8; ++i) cnt[i] += (tm >> i) & 1u;
-                    }
+                    if (j0 + q < n) tb[(c0 + j0 + q) * 64] = (uint8_t)tight8(x[q], own, w[q]);
             }
-        }
-        uint32_t multi = 0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) multi |= cnt[i] >= 2 ? 1u << i : 0u;
-        mm[((uint64_t)b * V + v) * 64 + lane] = (uint8_t)multi;
-        if (__ballot(multi != 0) == 0) continue;
-        uint16_t *npv = np + ((uint64_t)b * V + v) * FR_SRC + lane * 8;
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-            if ((multi >> i) & 1u) npv[i] = (uint16_t)cnt[i];
-        // second walk: the multi-parent sources' bits of every tight in-edge
-        uint8_t *mb = mul + (uint64_t)b * E * 64 + lane;
-        for (uint64_t k = e0; k < e1; ++k) {
-            const uint32_t o = in2out[k];  // wave-uniform
-            const uint32_t m = multi & tb[(uint64_t)o * 64];
-            if (m) mb[(uint64_t)o * 64] = (uint8_t)m;
         }
     }
 }
 
-// ----------------------------------------------------------- loss push
-// Loss over the tight DAG, pushed once per pair: sweep t processes the items
-// (b, u) marked for it; a source s of u is final when its loss is -- single
-// tight parent: P <= 1 (the parent's store; 2.0 = not yet), two or more:
-// every parent has arrived (np == 0, values min-combined atomically).  The
-// lane's newly final sources (not in pushed) go along every out-edge o = (u
-// -> x): for the sources whose edge is tight (tight byte), P(s,x) = 1 - (1 -
-// P(s,u)) * (1 - e) -- a plain store for a single-parent pair, else atomicMin
-// on the f32 bits (non-negative floats order as their bits) then a fence and
-// the decrement of x's count -- and x is marked for sweep t + 1.  Every pair
-// is pushed once; the fold is the reference's (mod.rs:322-331).
-__global__ __launch_bounds__(FR_WAVES * 64) void fr_loss_push_kernel(
-    const uint64_t *__restrict__ out_ptr, const uint2 *__restrict__ out_edge, uint32_t V, uint32_t NB, uint64_t E,
-    const uint8_t *__restrict__ tight, const uint8_t *__restrict__ mul, const uint8_t *__restrict__ mm,
-    uint8_t *pushed, uint16_t *np, float *P, uint32_t *act, uint32_t *last, uint32_t t) {
+// ---------------------------------------------------------- loss sweep
+// Pull over tight in-edges with per-source change bits, double-buffered:
+// sb_cur[b][u][lane] = the lane's sources of u whose loss changed in sweep
+// t - 1, sb_next = those of sweep t (cleared before it; read as well, so a
+// change made earlier in the same sweep is picked up at once, Gauss-Seidel).
+// Per in-edge the lane loads its tight byte (in-edge order: the item's edges
+// are contiguous) and u's two change bytes; only where they meet does it
+// gather u's 8 losses (32 B) and fold the tight ones that are reached (P <= 1;
+// 2.0 = not yet).  Chain per item: in-edges -> (tight, change bytes) ->
+// gather, the own losses loaded beside the in-edges; marks from registers.
+__global__ __launch_bounds__(FR_WAVES * 64) void fr_loss_sweep_kernel(
+    const uint64_t *__restrict__ in_ptr, const InEdge *__restrict__ in_edge, uint32_t V, uint32_t NB, uint64_t E,
+    const uint8_t *__restrict__ tight, float *P, const uint8_t *__restrict__ sb_cur, uint8_t *sb_next,
+    uint32_t *act, uint32_t *last, uint32_t t, bool sym, const uint64_t *__restrict__ row_ptr,
+    const uint32_t *__restrict__ col) {
     const int lane = threadIdx.x & 63;
     const uint32_t wave = blockIdx.x * FR_WAVES + (threadIdx.x >> 6), nwaves = gridDim.x * FR_WAVES;
     const uint32_t cpb = (V + 63) / 64, nchunks = cpb * NB;
+    bool any_imp = false;
     for (uint32_t c = __builtin_amdgcn_readfirstlane(wave); c < nchunks; c += nwaves) {
         const uint32_t b = c / cpb, v0 = (c % cpb) * 64;
         uint32_t *act_b = act + (uint64_t)b * V;
         const uint32_t a = v0 + lane < V ? act_b[v0 + lane] : 0u;
         uint64_t items = __ballot(a >= t);
-        float *Pb = P + (uint64_t)b * V * FR_SRC;
+        float4 *Pb = reinterpret_cast<float4 *>(P + (uint64_t)b * V * FR_SRC);
         const uint8_t *tb = tight + (uint64_t)b * E * 64 + lane;
-        const uint8_t *mb = mul + (uint64_t)b * E * 64 + lane;
+        const uint8_t *sbc = sb_cur + (uint64_t)b * V * 64 + lane;
+        uint8_t *sbn = sb_next + (uint64_t)b * V * 64 + lane;
         while (items) {
-            const uint32_t u = v0 + __builtin_ctzll(items);
+            const uint32_t v = v0 + __builtin_ctzll(items);
             items &= items - 1;
-            const uint64_t iu = (uint64_t)b * V + u;
-            float *pu = Pb + (uint64_t)u * FR_SRC + lane * 8;
-            const float4 o0 = reinterpret_cast<const float4 *>(pu)[0], o1 = reinterpret_cast<const float4 *>(pu)[1];
-            float p[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
-            const uint32_t pb = pushed[iu * 64 + lane], multi = mm[iu * 64 + lane];
-            uint32_t fin = 0;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                if ((multi >> i) & 1u) {
-                    // arrivals are atomics at the memory side: read count and
-                    // value past this CU's caches
-                    const uint32_t idx = (uint32_t)(iu * FR_SRC + lane * 8 + i);
-                    const uint32_t cw = __hip_atomic_load(reinterpret_cast<uint32_t *>(np) + idx / 2, __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT);
-                    if (((cw >> (16 * (idx & 1))) & 0xffffu) == 0) {
-                        fin |= 1u << i;
-                        p[i] = __uint_as_float(__hip_atomic_load(reinterpret_cast<uint32_t *>(pu) + i, __ATOMIC_RELAXED,
-                                                                 __HIP_MEMORY_SCOPE_AGENT));
-                    }
-                } else if (p[i] <= 1.0f) {
-                    fin |= 1u << i;
-                }
-            }
-            const uint32_t newly = fin & ~pb;
-            if (__ballot(newly != 0) == 0) continue;
-            if (newly) pushed[iu * 64 + lane] = (uint8_t)(pb | newly);
-            if (lane == 0 && __builtin_nontemporal_load(last) != t) *last = t;
-            const uint64_t e0 = out_ptr[u], e1 = out_ptr[u + 1];
+            float4 *pv = Pb + (uint64_t)v * 128 + 2 * lane;
+            const float4 o0 = pv[0], o1 = pv[1];
+            float best[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+            const uint64_t e0 = in_ptr[v], e1 = in_ptr[v + 1];
+            uint32_t eu = 0;
             for (uint64_t c0 = e0; c0 < e1; c0 += 64) {
                 const uint64_t k = c0 + lane;
-                uint2 oe = make_uint2(0, 0);
-                if (k < e1) oe = out_edge[k];
+                float eeb = 0.f;
+                eu = 0;
+                if (k < e1) {
+                    const InEdge e = in_edge[k];
+                    eu = e.u;
+                    eeb = e.eb;
+                }
                 const uint32_t n = e1 - c0 < 64 ? (uint32_t)(e1 - c0) : 64u;
-                for (uint32_t j0 = 0; j0 < n; j0 += FR_EB) {
-                    uint32_t m[FR_EB], ml[FR_EB];
+                for (uint32_t j0 = 0; j0 < n; j0 += FR_EBL) {
+                    uint32_t m[FR_EBL], u[FR_EBL];
+                    float eb[FR_EBL];
 #pragma unroll
-                    for (int q = 0; q < FR_EB; ++q) {
+                    for (int q = 0; q < FR_EBL; ++q) {
                         m[q] = 0;
-                        ml[q] = 0;
-                        if (j0 + q < n && newly) {
-                            m[q] = tb[(c0 + j0 + q) * 64] & newly;
-                            if (m[q]) ml[q] = mb[(c0 + j0 + q) * 64];
+                        u[q] = 0;
+                        eb[q] = 0.f;
+                        if (j0 + q < n) {
+                            u[q] = __builtin_amdgcn_readlane(eu, j0 + q);
+                            eb[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(eeb), j0 + q));
+                            m[q] = tb[(c0 + j0 + q) * 64] & (sbc[(uint64_t)u[q] * 64] | sbn[(uint64_t)u[q] * 64]);
+                        }
+                    }
+                    float4 x0[FR_EBL], x1[FR_EBL];
+#pragma unroll
+                    for (int q = 0; q < FR_EBL; ++q) {
+                        x0[q] = x1[q] = make_float4(2.f, 2.f, 2.f, 2.f);
+                        if (m[q]) {
+                            x0[q] = Pb[(uint64_t)u[q] * 128 + 2 * lane];
+                            x1[q] = Pb[(uint64_t)u[q] * 128 + 2 * lane + 1];
                         }
                     }
 #pragma unroll
-                    for (int q = 0; q < FR_EB; ++q) {
-                        if (j0 + q >= n) break;
-                        const uint32_t x = __builtin_amdgcn_readlane(oe.x, j0 + q);
-                        const float eb = __uint_as_float(__builtin_amdgcn_readlane(oe.y, j0 + q));
-                        if (m[q]) {
-                            float *px = Pb + (uint64_t)x * FR_SRC + lane * 8;
-                            const uint32_t base = (uint32_t)(((uint64_t)b * V + x) * FR_SRC + lane * 8);
+                    for (int q = 0; q < FR_EBL; ++q) {
+                        const float xs[8] = {x0[q].x, x0[q].y, x0[q].z, x0[q].w, x1[q].x, x1[q].y, x1[q].z, x1[q].w};
 #pragma unroll
-                            for (int i = 0; i < 8; ++i) {
-                                if (!((m[q] >> i) & 1u)) continue;
-                                const float val = fold(p[i], eb);
-                                if ((ml[q] >> i) & 1u) {
-                                    atomicMin(reinterpret_cast<uint32_t *>(px) + i, __float_as_uint(val));
-                                    __threadfence();
-                                    atomicSub(reinterpret_cast<uint32_t *>(np) + (base + i) / 2,
-                                              1u << (16 * ((base + i) & 1)));
-                                } else {
-                                    px[i] = val;
-                                }
+                        for (int i = 0; i < 8; ++i)
+                            if (((m[q] >> i) & 1u) && xs[i] <= 1.0f) {  // u reached (not the 2.0 init)
+                                const float cnd = fold(xs[i], eb[q]);
+                                best[i] = cnd < best[i] ? cnd : best[i];
                             }
-                        }
-                        if (__ballot(m[q] != 0) && lane == 0) {
-                            uint32_t *ax = act_b + x;
-                            if (*ax < t + 1) *ax = t + 1;
-                        }
                     }
                 }
             }
+            const float ov[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+            uint32_t ib = 0;  // the lane's improved sources
+#pragma unroll
+            for (int i = 0; i < 8; ++i) ib |= best[i] < ov[i] ? 1u << i : 0u;
+            const uint64_t im = __ballot(ib != 0);
+            if (!im) continue;
+            any_imp = true;
+            if (ib) {
+                pv[0] = make_float4(best[0], best[1], best[2], best[3]);
+                pv[1] = make_float4(best[4], best[5], best[6], best[7]);
+                sbn[(uint64_t)v * 64] = (uint8_t)ib;  // only this wave writes v's byte this sweep
+            }
+            mark(act_b, v, t, sym, in_edge, eu, e0, e1, row_ptr, col, lane);
         }
     }
+    note_improved(last, t, any_imp, lane);
 }
 
 // ---------------------------------------------------------------- emit
@@ -621,7 +606,7 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
         }
         p->h_fdone.assign(V, ~0u);
         for (uint32_t q = 0; q < rows; ++q)
-            p->h_fdone[p->nodes[bfs ? p->h_sperm[p->row0 + q] : p->row0 + q]] = q / FR_SRC;
+            p->h_fdone[p->h_fnodes[bfs ? p->h_sperm[p->row0 + q] : p->row0 + q]] = q / FR_SRC;
         e = hipSuccess;
         if (bfs && !p->d_sperm) e = hipMalloc(&p->d_sperm, (size_t)p->n * 4);
         if (e == hipSuccess && !p->d_fdone) e = hipMalloc(&p->d_fdone, (size_t)std::max<uint32_t>(V, 1) * 4);
@@ -662,42 +647,45 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
             return hip_err(err, e, "sssp init");
         uint32_t t0 = ++p->fr_t;
         if (sym && B0 > 0) {
-            hipLaunchKernelGGL(fr_sym_copy_kernel, dim3(NB * 8, B0 * 8), dim3(256), 0, M, p->d_fl, p->d_nodes, perm, V,
+            hipLaunchKernelGGL(fr_sym_copy_kernel, dim3(NB * 8, B0 * 8), dim3(256), 0, M, p->d_fl, p->d_fnodes, perm, V,
                                p->row0, p->row1, B0);
-            hipLaunchKernelGGL(fr_sym_act_kernel, dim3(2048), dim3(256), 0, M, p->d_fact, chg, p->d_fdone, V, NB, B0,
-                               t0);
-        } else if ((e = hipMemsetAsync(p->d_fact, 0, (size_t)NB * V * 4, M)) != hipSuccess) {
+            hipLaunchKernelGGL(fr_sym_act_kernel, dim3(2048), dim3(256), 0, M, p->d_fact, p->d_ffin, chg, p->d_fdone, V,
+                               NB, B0, t0);
+        } else if ((e = hipMemsetAsync(p->d_fact, 0, (size_t)NB * V * 4, M)) != hipSuccess ||
+                   (e = hipMemsetAsync(p->d_ffin, 0, (size_t)NB * V, M)) != hipSuccess) {
             return hip_err(err, e, "sssp init");
         }
-        hipLaunchKernelGGL(fr_seed_kernel, seed_grid, dim3(256), 0, M, L, nullptr, chg, p->d_fact, p->d_nodes, perm, V,
-                           q0, nsrc, t0, p->d_row_ptr, p->d_col);
+        hipLaunchKernelGGL(fr_seed_kernel, seed_grid, dim3(256), 0, M, L, nullptr, nullptr, chg, p->d_fact, p->d_fnodes,
+                           perm, V, q0, nsrc, t0, p->d_frow_ptr, p->d_fcol);
         uint32_t t_end = 0, nsw = 0;
         srt_status st = run_phase(p, t0, chunk_lat, [&](uint32_t t) {
             hipLaunchKernelGGL(fr_lat_sweep_kernel, sgrid, sblk, 0, M, p->d_in_ptr, p->d_in_edge, V, NB, L, chg,
-                               p->d_fact, p->d_fimp, t, p->d_row_ptr, p->d_col);
+                               p->d_fact, p->d_ffin, p->d_fimp, t, p->fr_symg, p->d_frow_ptr, p->d_fcol);
         }, &t_end, &nsw, err);
         if (st != SRT_OK) return st;
         p->fr_lat_sweeps += nsw;
         p->sssp_sweeps += nsw;
         chunk_lat = std::max<uint32_t>(nsw + 1, 4);
-        // 2. tight masks (out-edge order) and the multi-parent pairs
-        if ((e = hipMemsetAsync(p->d_fmul, 0, (size_t)NB * E * 64, M)) != hipSuccess)
-            return hip_err(err, e, "sssp tight init");
-        hipLaunchKernelGGL(fr_tight_kernel, sgrid, sblk, 0, M, p->d_in_ptr, p->d_in_edge, p->d_fin2out, V, NB, E, L,
-                           p->d_ftight, p->d_fmul, p->d_fmm, p->d_fnp);
-        // 3. loss push (stamps from t_end + 2; activity cleared of the final marks)
+        // 2. tight masks
+        hipLaunchKernelGGL(fr_tight_kernel, sgrid, sblk, 0, M, p->d_in_ptr, p->d_in_edge, V, NB, E, L, p->d_ftight);
+        // 3. loss (activity cleared of the final marks; change bits double-buffered)
+        const size_t sbytes = (size_t)NB * V * 64;
         if ((e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p->d_fp), 0x40000000u, (size_t)NB * V * FR_SRC,
                                    M)) != hipSuccess ||
             (e = hipMemsetAsync(p->d_fact, 0, (size_t)NB * V * 4, M)) != hipSuccess ||
-            (e = hipMemsetAsync(p->d_fpushed, 0, (size_t)NB * V * 64, M)) != hipSuccess)
+            (e = hipMemsetAsync(p->d_fsb, 0, sbytes, M)) != hipSuccess)
             return hip_err(err, e, "sssp loss init");
         t0 = t_end + 2;
-        hipLaunchKernelGGL(fr_seed_kernel, seed_grid, dim3(256), 0, M, nullptr, p->d_fp, chg, p->d_fact, p->d_nodes,
-                           perm, V, q0, nsrc, t0, p->d_row_ptr, p->d_col);
+        hipLaunchKernelGGL(fr_seed_kernel, seed_grid, dim3(256), 0, M, nullptr, p->d_fp, p->d_fsb, chg, p->d_fact,
+                           p->d_fnodes, perm, V, q0, nsrc, t0, p->d_frow_ptr, p->d_fcol);
         st = run_phase(p, t0, chunk_loss, [&](uint32_t t) {
-            hipLaunchKernelGGL(fr_loss_push_kernel, sgrid, sblk, 0, M, p->d_fout_ptr, p->d_fout_edge, V, NB, E,
-                               p->d_ftight, p->d_fmul, p->d_fmm, p->d_fpushed, p->d_fnp, p->d_fp, p->d_fact,
-                               p->d_fimp, t);
+            // sweep t reads the bits of sweep t - 1 (slot (t - t0 - 1) & 1; the
+            // seeds are slot 0) and writes slot (t - t0) & 1, cleared first
+            uint8_t *cur = p->d_fsb + ((t - t0 - 1) & 1) * sbytes, *nxt = p->d_fsb + ((t - t0) & 1) * sbytes;
+            (void)hipMemsetAsync(nxt, 0, sbytes, M);
+            hipLaunchKernelGGL(fr_loss_sweep_kernel, sgrid, sblk, 0, M, p->d_in_ptr, p->d_in_edge, V, NB, E,
+                               p->d_ftight, p->d_fp, cur, nxt, p->d_fact, p->d_fimp, t, p->fr_symg, p->d_frow_ptr,
+                               p->d_fcol);
         }, &t_end, &nsw, err);
         if (st != SRT_OK) return st;
         p->fr_loss_sweeps += nsw;
@@ -707,7 +695,7 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
         (void)hipEventRecord(p->ev[2 * li + 1], M);
         p->p3_launches++;
         hipLaunchKernelGGL(fr_emit_kernel, dim3((p->n + 63) / 64, (nsrc + 63) / 64), dim3(256), 0, M, L, p->d_fp, V,
-                           p->d_nodes, perm, p->n, q0, nsrc, p->sssp_g, p->d_sl_lat, p->d_sl_loss, p->d_out_lat,
+                           p->d_fnodes, perm, p->n, q0, nsrc, p->sssp_g, p->d_sl_lat, p->d_sl_loss, p->d_out_lat,
                            p->d_out_loss, d_stats);
     }
     // algorithmic bytes: 12 B per in-edge + 12 B per vertex, per source
@@ -715,10 +703,10 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
     return SRT_OK;
 }
 
-// device bytes of one 512-source block in flight: L (1 KB) + P (2 KB) + parent
-// counts (1 KB) + change record (16 B) + multi / pushed masks (128 B) +
-// activity (4 B) per vertex, the tight and multi masks (128 B) per edge
-uint64_t frontier_block_bytes(uint32_t V, uint64_t E) { return (uint64_t)V * (1024 + 2048 + 1024 + 148) + E * 128; }
+// device bytes of one 512-source block in flight: L (1 KB) + P (2 KB) + change
+// record (16 B) + 2 x per-source change bits (128 B) + activity (4 B) per
+// vertex, the tight masks (64 B) per in-edge
+uint64_t frontier_block_bytes(uint32_t V, uint64_t E) { return (uint64_t)V * (1024 + 2048 + 148) + E * 64; }
 size_t frontier_chg_bytes() { return sizeof(Chg); }
 
 }  // namespace srt

@@ -227,13 +227,16 @@ struct srt_plan {
     uint8_t *d_ftight = nullptr;         // fr_nb * n_in_edges * 64 tight-source bytes
     void *d_fchg = nullptr;              // fr_nb * V change records (srt_frontier.hip Chg, 16 B)
     uint32_t *d_fact = nullptr;          // fr_nb * V activation stamps
-    uint8_t *d_fmul = nullptr;           // fr_nb * n_in_edges * 64: tight bytes of multi-parent pairs (out order)
-    uint8_t *d_fmm = nullptr;            // fr_nb * V * 64: per item and lane, the sources with >= 2 tight parents
-    uint8_t *d_fpushed = nullptr;        // fr_nb * V * 64: per item and lane, the sources already pushed
-    uint16_t *d_fnp = nullptr;           // fr_nb * V * 512: tight parents still to arrive (multi-parent pairs)
-    uint64_t *d_fout_ptr = nullptr;      // V + 1: out-edge rows (CSR minus self-loops)
-    uint2 *d_fout_edge = nullptr;        // {far end, 1 - loss f32 bits} per out-edge
-    uint32_t *d_fin2out = nullptr;       // per in-edge slot: its out-edge index
+    uint8_t *d_ffin = nullptr;           // fr_nb * V: item exact from the start (symmetric seeding)
+    // the frontier's vertex order (hubs spread over the 64-vertex chunks):
+    // in-use nodes, out-CSR (self-loops dropped) renumbered; d_in_ptr /
+    // d_in_edge of a frontier plan are in this order too
+    uint32_t *d_fnodes = nullptr;
+    uint64_t *d_frow_ptr = nullptr;
+    uint32_t *d_fcol = nullptr;
+    std::vector<uint32_t> h_fnodes;
+    bool fr_symg = false;                // latency-symmetric adjacency: out-neighbours = in-edge sources
+    uint8_t *d_fsb = nullptr;            // 2 x fr_nb * V * 64: per-source loss change bits (double-buffered)
     uint32_t *d_fdone = nullptr;         // V: block (of this rank's rows) in which the vertex is a source, ~0 none
     std::vector<uint32_t> h_fdone;
     uint32_t *d_fimp = nullptr;          // last sweep that improved anything
