@@ -180,6 +180,24 @@ def measured_traffic(args, kernel_tag, schedule):
     return None, None
 
 
+def frontier_traffic(args, schedule, launches):
+    """HBM bytes per launch of the frontier path: every fr_* kernel's bytes per
+    dispatch x its dispatches, over the run's launches, from the newest committed
+    PMC summary of this workload and schedule (see measured_traffic)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    for f in reversed(files):
+        d = json.load(open(f))
+        cfg = d.get("config", "")
+        if not cfg.startswith(args.config.upper() + " ") or d.get("schedule") != schedule:
+            continue
+        tot = sum(v["hbm_bytes_per_launch"] * v["dispatches"] for k, v in d.get("kernels", {}).items()
+                  if k.startswith("fr_") and not k.startswith("fr_emit"))
+        if tot:
+            return tot / max(d.get("launches", launches), 1), os.path.relpath(f, ROOT)
+    return None, None
+
+
 class Dist:
     def __init__(self):
         import torch
@@ -517,26 +535,38 @@ def bench_graph(args, cfg, D):
             achieved = work_per_launch / avg_launch_s
             launches_per_step = k_launches // max(args.steps, 1)
             sweeps_per_launch = timing["sparse_sweeps"] / max(launches_per_step, 1)
-            state = desc.split("state=")[1].split()[0] if "state=" in desc else "keys"
-            schedule = {"state": state, "words_per_lane": int(desc.split(" R=")[1].split()[0]) if " R=" in desc else 0,
-                        "source_order": "bfs" if "order=bfs" in desc else "table"}
-            per_sweep, traffic_src = measured_traffic(args, "(sssp_sweep)", schedule)
+            frontier = desc.startswith("sssp:frontier")
+            if frontier:
+                schedule = {"state": "frontier-u16", "blocks": int(desc.split(" blocks=")[1].split()[0]),
+                            "seed": desc.split(" seed=")[1].split()[0],
+                            "source_order": "bfs" if "order=bfs" in desc else "table"}
+                traffic, traffic_src = frontier_traffic(args, schedule, launches_per_step)
+                kernel = ("fr_lat_sweep_kernel + fr_tight_kernel + fr_loss_sweep_kernel: every sweep of one launch "
+                          "(its blocks of 512 sources)")
+                algo = "latency-first frontier sweeps (u16 latencies, then f32 loss over the tight DAG)"
+            else:
+                state = desc.split("state=")[1].split()[0] if "state=" in desc else "keys"
+                schedule = {"state": state,
+                            "words_per_lane": int(desc.split(" R=")[1].split()[0]) if " R=" in desc else 0,
+                            "source_order": "bfs" if "order=bfs" in desc else "table"}
+                per_sweep, traffic_src = measured_traffic(args, "(sssp_sweep)", schedule)
+                traffic = per_sweep * sweeps_per_launch if per_sweep else None
+                kernel = "sssp_sweep_kernel (all sweeps of one launch)"
+                algo = "batched sparse sweep"
             roofline = {
                 "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK,
-                # one "launch" = every sweep of the groups in flight (groups x 64 R sources)
-                "traffic": per_sweep * sweeps_per_launch if per_sweep else None,
-                "traffic_unit": "HBM bytes per launch (PMC bytes per sweep dispatch x this run's sweeps per launch)",
+                "traffic": traffic,
+                "traffic_unit": "HBM bytes per launch (PMC bytes of the launch's kernels, per launch)",
                 "traffic_source": (f"{traffic_src}: committed rocprofv3 PMC summary of this workload and layout, "
                                    f"not measured in this run" if traffic_src else
                                    "no committed PMC summary for this workload/layout"),
                 "schedule": schedule,
-                "kernel": "sssp_sweep_kernel (all sweeps of one launch)",
+                "kernel": kernel,
                 "avg_launch_ms": avg_launch_s * 1e3, "launches_per_step": launches_per_step,
                 "sweeps_per_launch": sweeps_per_launch,
                 "algorithmic_bytes_per_launch": work_per_launch,
                 "basis": "12 B x (E_in + V) per source (SURVEY.md 8(d)), E_in = in-edges without self-loops"}
-            algo = "batched sparse sweep"
         cpu = cpu_opt = None
         if args.cpu_baseline and D.world == 1:
             from oracle import oracle as O

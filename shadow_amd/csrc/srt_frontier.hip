@@ -465,49 +465,87 @@ __global__ __launch_bounds__(256) void fr_emit_kernel(const uint16_t *__restrict
                                                       const uint64_t *__restrict__ sl_lat,
                                                       const float *__restrict__ sl_loss, uint64_t *__restrict__ out_lat,
                                                       float *__restrict__ out_loss, unsigned long long *stats) {
-    __shared__ uint16_t tl[64][66];
+    __shared__ uint16_t tl[64][66];  // [column][slot]
     __shared__ float tp[64][65];
+    __shared__ uint32_t rows[64], cols[64];
     __shared__ unsigned long long red_min[4], red_cnt[4];
     const uint32_t s0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
     const uint32_t b = s0 / FR_SRC, o = s0 % FR_SRC;
     const int tid = threadIdx.x;
-    for (int idx = tid; idx < 64 * 64; idx += 256) {
-        const int jj = idx / 64, s = idx % 64;
-        const uint32_t j = j0 + jj;
-        uint16_t l = L16_INF;
-        float pl = 1.0f;
-        if (j < n) {
-            const uint64_t r = ((uint64_t)b * V + nodes[j]) * FR_SRC + o + s;
-            l = L[r];
-            pl = P[r];
-        }
-        tl[jj][s] = l;
-        tp[jj][s] = pl;
+    if (tid < 64) {
+        const uint32_t j = j0 + tid, q = s0 + tid;
+        cols[tid] = j < n ? nodes[j] : ~0u;
+        rows[tid] = q < nsrc ? (perm ? perm[q0 + q] : q0 + q) : ~0u;
     }
     __syncthreads();
+    // 1. each column's 64 slots: 128 B of L (8 x 16 B) and 256 B of P (16 x 16 B)
+    for (int idx = tid; idx < 64 * 8; idx += 256) {
+        const int jj = idx / 8, part = idx % 8;
+        uint4 x = make_uint4(~0u, ~0u, ~0u, ~0u);
+        if (cols[jj] != ~0u)
+            x = *reinterpret_cast<const uint4 *>(L + ((uint64_t)b * V + cols[jj]) * FR_SRC + o + part * 8);
+        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            tl[jj][part * 8 + 2 * h] = (uint16_t)w[h];
+            tl[jj][part * 8 + 2 * h + 1] = (uint16_t)(w[h] >> 16);
+        }
+    }
+    for (int idx = tid; idx < 64 * 16; idx += 256) {
+        const int jj = idx / 16, part = idx % 16;
+        float4 x = make_float4(1.f, 1.f, 1.f, 1.f);
+        if (cols[jj] != ~0u)
+            x = *reinterpret_cast<const float4 *>(P + ((uint64_t)b * V + cols[jj]) * FR_SRC + o + part * 4);
+        tp[jj][part * 4] = x.x;
+        tp[jj][part * 4 + 1] = x.y;
+        tp[jj][part * 4 + 2] = x.z;
+        tp[jj][part * 4 + 3] = x.w;
+    }
+    __syncthreads();
+    // 2. rows: latency as 2 columns (16 B) a lane, loss as 4 (16 B) a lane
     uint64_t mn = ~0ull;
     unsigned long long unreach = 0;
-    for (int idx = tid; idx < 64 * 64; idx += 256) {
-        const int s = idx / 64, jj = idx % 64;
-        const uint32_t j = j0 + jj, q = s0 + s;
-        if (j >= n || q >= nsrc) continue;
-        const uint32_t row = perm ? perm[q0 + q] : q0 + q;
-        uint64_t lat;
-        float loss;
-        if (row == j) {
-            lat = sl_lat[j];
-            loss = sl_loss[j];
-        } else if (tl[jj][s] == L16_INF) {
-            ++unreach;
-            lat = ~0ull;
-            loss = 1.0f;
-        } else {
-            lat = (uint64_t)tl[jj][s] * gunit;
-            loss = tp[jj][s];
+    for (int idx = tid; idx < 64 * 32; idx += 256) {
+        const int s = idx / 32, jj = (idx % 32) * 2;
+        const uint32_t row = rows[s];
+        if (row == ~0u || j0 + jj >= n) continue;
+        uint64_t v2[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t j = j0 + jj + k;
+            const uint16_t l = tl[jj + k][s];
+            uint64_t lat = row == j ? sl_lat[j] : l == L16_INF ? ~0ull : (uint64_t)l * gunit;
+            if (j >= n) lat = ~0ull;
+            else {
+                unreach += (row != j && l == L16_INF);
+                mn = lat < mn ? lat : mn;
+            }
+            v2[k] = lat;
         }
-        out_lat[(uint64_t)row * n + j] = lat;
-        out_loss[(uint64_t)row * n + j] = loss;
-        mn = lat < mn ? lat : mn;
+        uint64_t *dst = out_lat + (uint64_t)row * n + j0 + jj;
+        if (j0 + jj + 1 < n && ((uintptr_t)dst & 15) == 0) {
+            *reinterpret_cast<ulonglong2 *>(dst) = make_ulonglong2(v2[0], v2[1]);
+        } else {
+            dst[0] = v2[0];
+            if (j0 + jj + 1 < n) dst[1] = v2[1];
+        }
+    }
+    for (int idx = tid; idx < 64 * 16; idx += 256) {
+        const int s = idx / 16, jj = (idx % 16) * 4;
+        const uint32_t row = rows[s];
+        if (row == ~0u || j0 + jj >= n) continue;
+        float v4[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t j = j0 + jj + k;
+            v4[k] = j >= n ? 1.0f : row == j ? sl_loss[j] : tl[jj + k][s] == L16_INF ? 1.0f : tp[jj + k][s];
+        }
+        float *dst = out_loss + (uint64_t)row * n + j0 + jj;
+        if (j0 + jj + 3 < n && ((uintptr_t)dst & 15) == 0) {
+            *reinterpret_cast<float4 *>(dst) = make_float4(v4[0], v4[1], v4[2], v4[3]);
+        } else {
+            for (int k = 0; k < 4 && j0 + jj + k < n; ++k) dst[k] = v4[k];
+        }
     }
     for (int off = 32; off > 0; off >>= 1) {
         const uint64_t x = __shfl_xor(mn, off);

@@ -19,18 +19,63 @@
 #include <string>
 #include <thread>
 #include <string_view>
+#include <sys/mman.h>
 #include <unordered_map>
 #include <vector>
 
 #include "srt_internal.h"
 
+namespace {
+// vectors whose resize() leaves elements uninitialised: the big arrays of the
+// ingest are written in full by the parallel phases, so their pages are first
+// touched there, on every thread, instead of zeroed by one thread
+// Big ones (>= 4 MiB) are mapped directly and advised onto transparent huge
+// pages: an ingest at C3 scale allocates several GB, and 4-KiB page faults
+// (each one a kernel zero-fill) were a large part of a cold parse.
+template <typename T>
+struct NoInit : std::allocator<T> {
+    template <typename U>
+    struct rebind {
+        using other = NoInit<U>;
+    };
+    NoInit() = default;
+    template <typename U>
+    NoInit(const NoInit<U> &) noexcept {}
+    static constexpr size_t BIG = 4u << 20, HUGE = 2u << 20;
+    T *allocate(size_t n) {
+        const size_t bytes = n * sizeof(T);
+        if (bytes < BIG) return std::allocator<T>::allocate(n);
+        const size_t len = (bytes + HUGE - 1) & ~(HUGE - 1);
+        void *p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (p == MAP_FAILED) throw std::bad_alloc();
+        (void)madvise(p, len, MADV_HUGEPAGE);
+        return static_cast<T *>(p);
+    }
+    void deallocate(T *p, size_t n) noexcept {
+        const size_t bytes = n * sizeof(T);
+        if (bytes < BIG) return std::allocator<T>::deallocate(p, n);
+        munmap(p, (bytes + HUGE - 1) & ~(HUGE - 1));
+    }
+    template <typename U>
+    void construct(U *p) noexcept {
+        ::new (static_cast<void *>(p)) U;
+    }
+    template <typename U, typename... A>
+    void construct(U *p, A &&...a) {
+        ::new (static_cast<void *>(p)) U(std::forward<A>(a)...);
+    }
+};
+template <typename T>
+using uvec = std::vector<T, NoInit<T>>;
+}  // namespace
+
 struct srt_gml {
     bool directed = false;
     std::vector<uint32_t> ids;
     std::vector<uint64_t> row_ptr;
-    std::vector<uint32_t> col;
-    std::vector<uint64_t> lat;
-    std::vector<float> loss;
+    uvec<uint32_t> col;
+    uvec<uint64_t> lat;
+    uvec<float> loss;
 };
 
 namespace {
@@ -112,7 +157,10 @@ class Lexer {
                 if (x > INT32_MAX) ovf = true, x = INT32_MAX + 1ll;
                 ++p_;
             }
-            if (!ovf && newline()) {
+            // a '.', 'e' or 'E' right after the digits fails the int's newline:
+            // straight to the float alternative
+            const bool fl = p_ < e_ && (*p_ == '.' || *p_ == 'e' || *p_ == 'E');
+            if (!ovf && !fl && newline()) {
                 v->t = VT::Int;
                 v->i = (int32_t)x;
                 return true;
@@ -341,7 +389,10 @@ const char *parse_time(std::string_view s, uint64_t *ns, uint64_t *value) {
     uint64_t mag = 0;
     if (u.empty()) mag = 1000000000ull;
     for (const auto &t : tab)
-        if (u == t.first) mag = t.second;
+        if (u == t.first) {
+            mag = t.second;  // the units are distinct: the first match is the only one
+            break;
+        }
     if (!mag) return "Unit was not one of (ns|nanosecond|...|h|hr|hrs|hour|hours)";
     uint64_t x;
     if (!parse_u64(v, &x)) return "invalid digit found in string";
@@ -384,12 +435,12 @@ bool bits_per_sec_ok(std::string_view s) {  // BitsPerSec<SiPrefixUpper>
 // node/edge validation (gml_parser::parse runs before NetworkGraph::parse),
 // then nodes are validated in order, then edges (first failing edge wins).
 
-struct EdgeRec {
-    int32_t s = 0, t = 0;
-    uint64_t ns = 0;
-    float loss = 0.f;
-    uint8_t err = 0;   // first failing ShadowEdge::try_from check (0 = ok)
-    uint8_t sub = 0;   // which Time error text
+struct EdgeRec {  // trivially constructible: check_edge fills every field
+    int32_t s, t;
+    uint64_t ns;
+    float loss;
+    uint8_t err;  // first failing ShadowEdge::try_from check (0 = ok)
+    uint8_t sub;  // which Time error text
 };
 
 const char *time_err_text(uint8_t sub) {
@@ -410,7 +461,7 @@ uint8_t time_err_code(const char *e) {
 // ShadowEdge::try_from (mod.rs:72-111) on one parsed block, minus the id
 // lookups (done once every node is known)
 EdgeRec check_edge(const std::vector<KV> &b) {
-    EdgeRec r;
+    EdgeRec r{0, 0, 0, 0.f, 0, 0};
     const Val *s = get(b, "source"), *t = get(b, "target");
     if (s && s->t != VT::Int) return r.err = 1, r;
     if (!s) return r.err = 2, r;
@@ -478,8 +529,8 @@ void parallel_for(size_t n, unsigned T, F &&f);
 // contiguous chunks; per-chunk row counts give every chunk its own write
 // offsets (chunk T-1 first, since the order is reverse insertion), so the
 // fill runs in parallel and lands exactly where the sequential fill would.
-void build_csr(srt_gml *g, size_t V, const std::vector<uint32_t> &es, const std::vector<uint32_t> &ed,
-               const std::vector<uint64_t> &el, const std::vector<float> &eo, unsigned T = 1) {
+void build_csr(srt_gml *g, size_t V, const uvec<uint32_t> &es, const uvec<uint32_t> &ed, const uvec<uint64_t> &el,
+               const uvec<float> &eo, unsigned T = 1) {
     const size_t m = es.size();
     if (m < 4 * (size_t)T || T < 2) T = 1;
     const bool und = !g->directed;
@@ -585,9 +636,9 @@ void parse_sequential(std::string_view text, srt_gml *g) {
         id_map[g->ids[i]] = (uint32_t)i;
     }
     const size_t m = edges.size();
-    std::vector<uint32_t> es(m), ed(m);
-    std::vector<uint64_t> el(m);
-    std::vector<float> eo(m);
+    uvec<uint32_t> es(m), ed(m);
+    uvec<uint64_t> el(m);
+    uvec<float> eo(m);
     for (size_t i = 0; i < m; ++i) {
         EdgeRec r = check_edge(edges[i]);
         if (!r.err) {
@@ -660,11 +711,27 @@ void parse_parallel(std::string_view text, srt_gml *g, unsigned T) {
             bool in_str = q & 1;
             const char *p = base + cb[c], *end = base + cb[c + 1];
             std::vector<uint64_t> &out = st[c];
+            out.reserve((size_t)(end - p) / 32 + 16);  // ~2 structural bytes per ~90-byte block
+            // 8 bytes a step: a word with none of '"' '[' ']' is skipped whole
+            // (SWAR zero-byte test on the XOR with each broadcast character)
+            constexpr uint64_t ONES = 0x0101010101010101ull, HIGH = 0x8080808080808080ull;
+            constexpr uint64_t QQ = ONES * '"', LB = ONES * '[', RB = ONES * ']';
+            auto has0 = [](uint64_t x) { return (x - ONES) & ~x & HIGH; };
             while (p < end) {
-                const char x = *p;
-                if (x == '"') in_str = !in_str;
-                else if (!in_str && (x == '[' || x == ']')) out.push_back((uint64_t)(p - base));
-                ++p;
+                if (end - p >= 8) {
+                    uint64_t w;
+                    std::memcpy(&w, p, 8);
+                    if (!(has0(w ^ QQ) | has0(w ^ LB) | has0(w ^ RB))) {
+                        p += 8;
+                        continue;
+                    }
+                }
+                const char *stop = std::min(p + 8, end);
+                for (; p < stop; ++p) {
+                    const char x = *p;
+                    if (x == '"') in_str = !in_str;
+                    else if (!in_str && (x == '[' || x == ']')) out.push_back((uint64_t)(p - base));
+                }
             }
         }
     });
@@ -676,7 +743,7 @@ void parse_parallel(std::string_view text, srt_gml *g, unsigned T) {
     // check the alternation before it and pair the entries, chunk-parallel.
     std::vector<size_t> off(nch + 1, 0);
     for (size_t c = 0; c < nch; ++c) off[c + 1] = off[c] + st[c].size();
-    std::vector<uint64_t> E(off[nch]);
+    uvec<uint64_t> E(off[nch]);
     parallel_for(nch, T, [&](size_t b, size_t e, unsigned) {
         for (size_t c = b; c < e; ++c) std::copy(st[c].begin(), st[c].end(), E.begin() + (ptrdiff_t)off[c]);
     });
@@ -706,7 +773,7 @@ void parse_parallel(std::string_view text, srt_gml *g, unsigned T) {
         if ((i & 1) == 1 && base[E[i]] == '[') throw Bad{};
     const uint64_t gend = E[gi];
     const size_t nb = gi / 2;
-    std::vector<std::pair<uint64_t, uint64_t>> blocks(nb);
+    uvec<std::pair<uint64_t, uint64_t>> blocks(nb);
     parallel_for(nb, T, [&](size_t b, size_t e, unsigned) {
         for (size_t j = b; j < e; ++j) blocks[j] = {E[2 * j], E[2 * j + 1]};
     });
@@ -715,12 +782,11 @@ void parse_parallel(std::string_view text, srt_gml *g, unsigned T) {
     tick("blocks");
     // 4. parse gaps (before block i: [prev_end+1, blocks[i].first); the last
     // gap ends at the graph's ']') and blocks, in parallel
-    std::vector<uint8_t> kind(nb);  // 1 node, 2 edge
+    uvec<uint8_t> kind(nb);  // 1 node, 2 edge (every gap sets its block's)
     std::vector<std::vector<KV>> gap_others(T), nodes_kv;
     std::vector<int> gap_directed(T, 0);
     std::vector<int> directed_val(T, -1);
-    std::vector<EdgeRec> recs;
-    std::vector<uint32_t> node_of(nb, UINT32_MAX);
+    uvec<EdgeRec> recs;
     // gaps first (they say which blocks are nodes), in order per thread
     auto parse_gap = [&](size_t i, unsigned t) {  // gap before block i (i == nb: the tail)
         const size_t b = i == 0 ? h : blocks[i - 1].second + 1;
@@ -768,7 +834,7 @@ void parse_parallel(std::string_view text, srt_gml *g, unsigned T) {
             if (others[i].k == others[j].k) throw Bad{};
     tick("gaps");
     // node / edge numbering in file order
-    std::vector<uint32_t> idx(nb);
+    uvec<uint32_t> idx(nb);
     uint32_t nn = 0, ne = 0;
     for (size_t i = 0; i < nb; ++i) idx[i] = kind[i] == 1 ? nn++ : ne++;
     nodes_kv.resize(nn);
@@ -793,9 +859,9 @@ void parse_parallel(std::string_view text, srt_gml *g, unsigned T) {
         id_map[g->ids[i]] = i;
     }
     nodes_kv.clear();
-    std::vector<uint32_t> es(ne), ed(ne);
-    std::vector<uint64_t> el(ne);
-    std::vector<float> eo(ne);
+    uvec<uint32_t> es(ne), ed(ne);
+    uvec<uint64_t> el(ne);
+    uvec<float> eo(ne);
     std::vector<size_t> first_bad(T, SIZE_MAX);
     parallel_for(ne, T, [&](size_t b, size_t e, unsigned t) {
         for (size_t i = b; i < e; ++i) {

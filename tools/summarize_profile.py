@@ -43,6 +43,10 @@ LABELS = {
     "minplus_glds_kernel<double, 2>": "phase 2 col",
     "minplus_tile_kernel<double, 0>": "phase 3 rest",
     "sssp_sweep_kernel": "sssp_sweep",
+    "fr_lat_sweep_kernel": "frontier latency sweep",
+    "fr_tight_kernel": "frontier tight pass",
+    "fr_loss_sweep_kernel": "frontier loss sweep",
+    "fr_emit_kernel": "frontier emit",
     "decide_kernel": "packet decide",
     "draw_kernel": "packet draw",
 }
@@ -52,7 +56,9 @@ LABELS = {
 # 16-B/lane streaming reads, global_load and buffer_load ... lds alike).  The
 # u16 / u32 tile kernels read C tiles and panels 16 B per lane; others as recorded
 # (the f64 tile kernels' 8-B/lane C loads were calibrated 1:1 in r01).
-FETCH_CORR = {"minplus_u32_kernel": 2.0, "minplus_u16_kernel": 2.0}
+FETCH_CORR = {"minplus_u32_kernel": 2.0, "minplus_u16_kernel": 2.0,
+              # frontier sweeps: 128-B rows gathered 16 B a lane (8 lanes a line)
+              "fr_lat_sweep_kernel": 2.0, "fr_tight_kernel": 2.0, "fr_loss_sweep_kernel": 2.0, "fr_emit_kernel": 2.0}
 
 
 def short(name):
@@ -96,7 +102,9 @@ def main():
         kernels[key] = {"dispatches": max(fn, wn), "FETCH_SIZE_KB_per_launch": fkb / max(fn, 1),
                         "WRITE_SIZE_KB_per_launch": wkb / max(wn, 1), "fetch_correction": corr,
                         "hbm_bytes_per_launch": 1024.0 * (corr * fkb / max(fn, 1) + wkb / max(wn, 1))}
-    doc = {"round": tag, "config": config,
+    # the PMC passes run one step without warmup: the frontier's launches of one step
+    launches = (json.loads(bench).get("roofline") or {}).get("launches_per_step")
+    doc = {"round": tag, "config": config, "launches": launches,
            "schedule": json.loads(sys.argv[4]) if len(sys.argv) > 4 else None,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (MI355X_MICROARCH.md "
                      "HBM section), KB per dispatch averaged over the dispatches of each kernel. "
