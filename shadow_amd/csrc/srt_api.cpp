@@ -105,6 +105,10 @@ struct CsrStats {
     uint64_t gcd = 0, maxlat = 0, selfloops = 0;
     uint64_t zero_k = ~0ull, badloss_k = ~0ull, badcol_k = ~0ull;
     bool unique = true, complete = true;
+    // symmetry fingerprint for the family price: sums over entries (u, v, l)
+    // of u*v*v + l*u and of v*u*u + l*v (mod 2^64) -- equal for every graph
+    // whose entry multiset is closed under (u, v, l) -> (v, u, l)
+    uint64_t sym_a = 0, sym_b = 0;
     std::vector<uint32_t> sl_cnt;    // per node: self-loop entries
     std::vector<uint64_t> sl_first;  // per node: first self-loop entry
 };
@@ -125,7 +129,7 @@ int host_threads(uint64_t work) {
 void scan_rows(const srt_csr *g, uint32_t r0, uint32_t r1, CsrStats &st, CsrStats *out, uint32_t *lat32 = nullptr,
                uint64_t k_base = 0, bool *lat_over = nullptr, bool *identity = nullptr) {
     const uint32_t V = g->n_nodes;
-    uint64_t gcd = st.gcd, maxlat = st.maxlat, selfl = st.selfloops;
+    uint64_t gcd = st.gcd, maxlat = st.maxlat, selfl = st.selfloops, sa = st.sym_a, sb = st.sym_b;
     bool ident = true, over = false;
     for (uint32_t u = r0; u < r1; ++u) {
         const uint64_t b = g->row_ptr[u], e = g->row_ptr[u + 1];
@@ -141,6 +145,8 @@ void scan_rows(const srt_csr *g, uint32_t r0, uint32_t r1, CsrStats &st, CsrStat
             if (l == 0 && st.zero_k == ~0ull) st.zero_k = k;
             if (!(q >= 0.0f && q <= 1.0f) && st.badloss_k == ~0ull) st.badloss_k = k;
             maxlat = l > maxlat ? l : maxlat;
+            sa += (uint64_t)u * c * c + l * u;
+            sb += (uint64_t)c * u * u + l * c;
             if (lat32) {
                 over |= l > 0xffffffffull;
                 lat32[k - k_base] = (uint32_t)l;
@@ -177,6 +183,8 @@ void scan_rows(const srt_csr *g, uint32_t r0, uint32_t r1, CsrStats &st, CsrStat
     st.gcd = gcd;
     st.maxlat = maxlat;
     st.selfloops = selfl;
+    st.sym_a = sa;
+    st.sym_b = sb;
     if (lat_over && over) *lat_over = true;
     if (identity && !ident) *identity = false;
 }
@@ -188,6 +196,8 @@ void merge_stats(const std::vector<CsrStats> &part, uint32_t V, CsrStats *out) {
         out->gcd = std::gcd(out->gcd, st.gcd);
         out->maxlat = std::max(out->maxlat, st.maxlat);
         out->selfloops += st.selfloops;
+        out->sym_a += st.sym_a;
+        out->sym_b += st.sym_b;
         out->zero_k = std::min(out->zero_k, st.zero_k);
         out->badloss_k = std::min(out->badloss_k, st.badloss_k);
         out->badcol_k = std::min(out->badcol_k, st.badcol_k);
@@ -249,7 +259,7 @@ constexpr size_t PINNED_BYTES = 3ull * (1ull << 23) * 8;  // 3 pieces of 8 Mi 8-
 // self-loops, as Shadow's atlas graphs) uploads no col at all: a kernel writes
 // it.  A piece with a latency >= 2^32 ns, or irregular rows, sends that array
 // from the caller's memory as before.  C3 (16k complete): 3.2 GB -> 1.07 GB
-// over PCIe.  Knobs (tests / A-B): SRT_UPLOAD_PIPE=0 off, SRT_UPLOAD_PIECE=
+// over PCIe.  Knob (tests): SRT_UPLOAD_PIECE=
 // log2 entries per piece (also forces the pipeline on small graphs).
 struct PieceUpload {
     static constexpr int DEPTH = 3;
@@ -271,7 +281,6 @@ struct PieceUpload {
     bool init(const srt_csr *g_, CsrStats *cs) {
         g = g_;
         const char *pe = std::getenv("SRT_UPLOAD_PIECE");
-        if (const char *k = std::getenv("SRT_UPLOAD_PIPE"); k && std::atoi(k) == 0) return false;
         if (pe) PE = 1ull << std::max(4, std::min(24, std::atoi(pe)));
         else if (g->n_adj < PE) return false;
         const uint32_t V = g->n_nodes;
@@ -527,6 +536,31 @@ bool sssp_params(const CsrStats &cs, uint32_t V, std::string *why) {
         return false;
     }
     return true;
+}
+
+// Family prices for AUTO, seconds on one MI355X, from the measured rates of
+// DESIGN.md 4 (rest launches by key type, r03 profiles; sparse builds r04).
+// Dense: Vp^3 relaxations (half on the triangle schedule: 2-byte keys on a
+// symmetric graph), at least ~80 us a 128-pivot round (the chain: C2 4k), plus
+// the exact-loss fold (C3: 7.0 ms for 16k x 16k pairs).  Sparse: one unit per
+// (source, in-edge or vertex) visited, at the C4 rate of the frontier sweeps
+// (u16 latencies) or of the packed-key sweeps, at least ~1 ms a launch of
+// sources (its ~60 dependent sweeps).
+double price_fw(uint32_t Vp, uint32_t n, uint32_t V, int key_type, bool f16, bool sym) {
+    const double rate = f16                          ? 4.3e13   // C3 rest: 1.45 ms / 6.26e10
+                        : key_type == srt::KEY_U16 ? 3.3e13     // 1.90 ms (r02)
+                        : key_type == srt::KEY_U32 ? 1.25e13    // 4.82-5.19 ms
+                        : key_type == srt::KEY_F64 ? 8e12       // ~half the u32 mix, not profiled
+                                                   : 4e12;      // u64: ~1/3 of u32's mix, not profiled
+    const bool tri = sym && (f16 || key_type == srt::KEY_U16);
+    const double relax = (double)Vp * Vp * Vp * (tri ? 0.5 : 1.0);
+    return std::max(relax / rate, (double)(Vp / 128) * 80e-6) + (double)n * V * 2.6e-11;
+}
+double price_sparse(uint32_t n, uint64_t n_in, uint32_t V, bool frontier) {
+    const double units = (double)n * ((double)n_in + V);
+    const double per = frontier ? 1.19e-11 : 1.73e-11;  // C4: 9e10 units in 1.07 s / 1.56 s
+    const double launches = std::ceil((double)n / (frontier ? 8192.0 : 4096.0));
+    return std::max(units * per, launches * 1e-3);
 }
 
 // Pull-form adjacency for the sweep: for every v, the entries u -> v of every
@@ -790,9 +824,11 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         const uint64_t maxu = cs.maxlat / cs.gcd;
         const uint64_t nin = g->n_adj - cs.selfloops;
         const uint32_t want0 = opts ? opts->algo : (uint32_t)SRT_ALGO_AUTO;
+        // priced as if the proof gave 2-byte keys (it decides whether to run it)
+        const bool sym = cs.sym_a == cs.sym_b;
         const bool dense_likely = want0 == SRT_ALGO_FW ||
-                                  (want0 == SRT_ALGO_AUTO && (double)p->Vp * p->Vp * p->Vp / 1.2e13 <
-                                                                 (double)n * ((double)nin + p->V) * 64.0 / 3e12);
+                                  (want0 == SRT_ALGO_AUTO && price_fw(p->Vp, n, p->V, srt::KEY_U16, true, sym) <
+                                                                 price_sparse(n, nin, p->V, true));
         // sparse plans need it too: the frontier sweeps keep u16 latencies
         // when every finite distance is below 0xFFFF units (srt_frontier.hip)
         const bool sparse_u16 = !dense_likely && (unsigned __int128)(p->V ? p->V - 1 : 0) * maxu >= 0xffff;
@@ -811,10 +847,8 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     (void)ecc_sweeps;
     tr.mark("create: eccentricity sweeps");
 
-    // 3. kernel family.  Dense closure (FW) costs Vp^3 relaxations at
-    // ~1.2e13/s; the batched sparse sweep costs ~n * (E_in + V) row gathers of
-    // 8 B with a few re-activations per row, priced at ~64 B per (source,
-    // in-edge) at ~3e12 B/s.  AUTO takes the cheaper representable one.
+    // 3. kernel family: AUTO takes the cheaper representable one at the
+    //    measured rates (price_fw, price_sparse)
     std::string why_fw, why_sssp;
     bool f16 = false;
     const bool fw_ok = choose_key_params(cs, p->V, ecc_units, &p->kp, &p->key_type, &f16, &why_fw);
@@ -825,13 +859,21 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     p->sssp_g = cs.gcd;
     const uint32_t want = opts ? opts->algo : (uint32_t)SRT_ALGO_AUTO;
     int algo = -1;
+    std::string auto_note;
     if (want == SRT_ALGO_FW) {
         if (fw_ok) algo = SRT_ALGO_FW;
     } else if (want == SRT_ALGO_SSSP) {
         if (sssp_ok) algo = SRT_ALGO_SSSP;
     } else if (want == SRT_ALGO_AUTO) {
-        const double t_fw = fw_ok ? (double)p->Vp * p->Vp * p->Vp / 1.2e13 : 1e300;
-        const double t_sssp = sssp_ok ? (double)n * ((double)n_in + p->V) * 64.0 / 3e12 : 1e300;
+        const uint64_t maxu = cs.maxlat / cs.gcd;
+        const unsigned __int128 lb = ecc_units != ~0ull ? (unsigned __int128)ecc_units
+                                                        : (unsigned __int128)(p->V ? p->V - 1 : 0) * maxu;
+        const double t_fw = fw_ok ? price_fw(p->Vp, n, p->V, p->key_type, f16, cs.sym_a == cs.sym_b) : 1e300;
+        const double t_sssp = sssp_ok ? price_sparse(n, n_in, p->V, lb < 0xffff) : 1e300;
+        char pr[96];
+        std::snprintf(pr, sizeof pr, " auto-price=fw:%.3gms,sparse:%.3gms", t_fw < 1e299 ? t_fw * 1e3 : -1.0,
+                      t_sssp < 1e299 ? t_sssp * 1e3 : -1.0);
+        auto_note = pr;
         if (fw_ok || sssp_ok) algo = t_sssp < t_fw ? SRT_ALGO_SSSP : SRT_ALGO_FW;
     } else {
         return fail(SRT_ERR_INVALID, "unknown srt_opts.algo");
@@ -849,8 +891,6 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     p->rows_alloc = n;
     char d[200];
     if (algo == SRT_ALGO_FW) {
-        // tuning knob (measurement only): SRT_FW_STAGE=reg selects register staging
-        if (const char *e = std::getenv("SRT_FW_STAGE")) p->fw_glds = std::strcmp(e, "reg") != 0;
         p->fw_f16 = f16 && p->fw_glds;
         if (const char *e = std::getenv("SRT_FW_P1")) p->fw_p1 = std::atoi(e);
         if (const char *e = std::getenv("SRT_FW_EMULATE_RANKS")) p->emulate_ranks = (uint32_t)std::atoi(e);
@@ -864,12 +904,6 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
             }
         }
         if (const char *e = std::getenv("SRT_FW_BAND")) p->fw_band = e[0] == '1';
-        if (const char *e = std::getenv("SRT_FW_XCD")) p->fw_xcd = e[0] != '0';
-        if (const char *e = std::getenv("SRT_FW_BAND_H")) {
-            const int h = std::atoi(e);
-            p->fw_band_h = 1;
-            while (p->fw_band_h * 2 <= (uint32_t)std::min(h, 64)) p->fw_band_h *= 2;
-        }
         std::snprintf(d, sizeof d, "fw:%s B=%d g=%llu lmax=%llu%s V=%u n=%u stage=%s band=%d loss=tight-dag%s",
                       p->fw_f16                     ? "f16key"
                       : p->key_type == srt::KEY_U16 ? "u16key"
@@ -888,16 +922,12 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         // Many groups in flight amortise each sweep's launch and latency chain
         // and the convergence tail (C4, measured: 192 MB of path state 3.0 s,
         // 1.6 GB 1.73 s, 6.4 GB 1.53 s, 12.8 GB 1.49 s), capped at 1/8 of the
-        // free HBM.  Tuning knobs (measurement only): SRT_SSSP_R in {1,2,4},
-        // SRT_SSSP_MB = path-state budget.
-        uint32_t rmax = 4;
-        if (const char *e = std::getenv("SRT_SSSP_R")) rmax = (uint32_t)std::atoi(e);
+        // free HBM.
         uint64_t budget_mb = 6400;
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b)
             budget_mb = std::max<uint64_t>(64, std::min<uint64_t>(budget_mb, (free_b >> 20) / 8));
-        if (const char *e = std::getenv("SRT_SSSP_MB")) budget_mb = (uint64_t)std::atoll(e);
-        const uint32_t R = (rmax >= 4 && words >= 4) ? 4 : (rmax >= 2 && words >= 2) ? 2 : 1;
+        const uint32_t R = words >= 4 ? 4 : words >= 2 ? 2 : 1;
         const uint64_t per_group = (uint64_t)p->V * 64 * 8 * R;
         uint64_t G = std::max<uint64_t>(1, (budget_mb << 20) / std::max<uint64_t>(per_group, 1));
         G = std::min<uint64_t>(G, (words + R - 1) / R);
@@ -1119,6 +1149,7 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         return hip_fail(err, e, "upload");
     }
     tr.mark("create: upload");
+    p->desc += auto_note;
     *plan_out = p;
     return SRT_OK;
 }
@@ -1357,12 +1388,10 @@ srt_status build_loss_rows(srt_plan *p, int W, uint32_t rows_per, srt_err *err) 
         p->lrow_cnt[r] = (uint32_t)lists[r].size();
         most = std::max(most, p->lrow_cnt[r]);
     }
-    // chunks of >= 64 rows, 8 by default (knob SRT_TAIL_CHUNKS, 1..16; each
-    // chunk's all-gather runs behind the next chunk's fold and its expansion
-    // behind the next all-gather: emulated C3 8 ranks 19.2 ms at 4, 18.9 at 8)
-    uint32_t q = 8;
-    if (const char *e = std::getenv("SRT_TAIL_CHUNKS")) q = (uint32_t)std::max(1, std::min(16, std::atoi(e)));
-    q = std::max<uint32_t>(1, std::min<uint32_t>(q, most / 64));
+    // chunks of >= 64 rows, 8 at most (each chunk's all-gather runs behind
+    // the next chunk's fold and its expansion behind the next all-gather:
+    // emulated C3 8 ranks 19.2 ms at 4 chunks, 18.9 at 8)
+    const uint32_t q = std::max<uint32_t>(1, std::min<uint32_t>(8, most / 64));
     p->tail_q = q;
     p->tail_cr = (most + q - 1) / q;
     p->lrow_max = q * p->tail_cr;
@@ -1468,12 +1497,9 @@ constexpr int DEPTH_MAX = 4;
 // table on the host 42-44 ms after the fold starts; 2 in flight measured
 // bimodal (45 or 80 ms: the DMA idles whenever the host is still expanding
 // the piece whose buffer it needs next); 4 Mi or 16 Mi pieces no better.
-// Knobs (measurement): SRT_FETCH_PIECE = log2 entries, SRT_FETCH_DEPTH.
 void fetch_geometry(uint64_t *piece, int *depth) {
     *piece = 1ull << 23;
     *depth = 3;
-    if (const char *k = std::getenv("SRT_FETCH_PIECE")) *piece = 1ull << std::max(16, std::min(24, std::atoi(k)));
-    if (const char *k = std::getenv("SRT_FETCH_DEPTH")) *depth = std::max(2, std::min(DEPTH_MAX, std::atoi(k)));
 }
 
 // The RoutingInfo's record arrays for an n x n table (2 MB aligned, on

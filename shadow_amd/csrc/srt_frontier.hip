@@ -245,24 +245,45 @@ __global__ __launch_bounds__(FR_WAVES * 64) void fr_lat_sweep_kernel(
         uint64_t items = __ballot(a >= t && !f);
         uint4 *Lb = reinterpret_cast<uint4 *>(L + (uint64_t)b * V * FR_SRC);
         Chg *chg_b = chg + (uint64_t)b * V;
-        while (items) {
-            const uint32_t v = v0 + __builtin_ctzll(items);
-            items &= items - 1;
+        if (!items) continue;
+        // software-pipelined like the loss sweep: the next item's head (row
+        // bounds, first 64 in-edges and their sources' change records) is
+        // loaded while the current item's gathers are in flight.  A record
+        // read early may miss a change of this sweep; its writer marked v for
+        // sweep t + 1 anyway.
+        uint32_t v = v0 + __builtin_ctzll(items);
+        items &= items - 1;
+        uint64_t e0 = in_ptr[v], e1 = in_ptr[v + 1];
+        uint32_t eu = 0, ew = 0;
+        uint64_t m = 0;
+        if (e0 + lane < e1) {
+            const InEdge e = in_edge[e0 + lane];
+            eu = e.u;
+            ew = e.w < L16_INF ? e.w : L16_INF;
+            m = changed_lanes(chg_b, eu, t);
+        }
+        for (;;) {
+            const bool more = items != 0;
+            const uint32_t vn = more ? v0 + __builtin_ctzll(items) : v;
+            if (more) items &= items - 1;
             const uint4 own = Lb[(uint64_t)v * 64 + lane];
             const Chg old = chg_b[v];  // own record, for the kept lanes (loaded beside the row)
             uint4 best = own;
-            const uint64_t e0 = in_ptr[v], e1 = in_ptr[v + 1];
-            uint32_t eu = 0;
+            uint64_t ne0 = 0, ne1 = 0, nm = 0;
+            uint32_t neu = 0, new_ = 0;
+            bool pre = !more;
             for (uint64_t c0 = e0; c0 < e1; c0 += 64) {
-                const uint64_t k = c0 + lane;
-                uint32_t ew = 0;
-                uint64_t m = 0;
-                eu = 0;
-                if (k < e1) {
-                    const InEdge e = in_edge[k];
-                    eu = e.u;
-                    ew = e.w < L16_INF ? e.w : L16_INF;
-                    m = changed_lanes(chg_b, eu, t);
+                if (c0 != e0) {  // chunks past the head
+                    const uint64_t k = c0 + lane;
+                    eu = 0;
+                    ew = 0;
+                    m = 0;
+                    if (k < e1) {
+                        const InEdge e = in_edge[k];
+                        eu = e.u;
+                        ew = e.w < L16_INF ? e.w : L16_INF;
+                        m = changed_lanes(chg_b, eu, t);
+                    }
                 }
                 uint64_t am = __ballot(m != 0);
                 while (am) {
@@ -283,23 +304,52 @@ __global__ __launch_bounds__(FR_WAVES * 64) void fr_lat_sweep_kernel(
                             if (((lane < 32 ? mlo : mhi) >> (lane & 31)) & 1u) x[q] = Lb[(uint64_t)u * 64 + lane];
                         }
                     }
+                    if (!pre) {  // the next item's head, behind this batch's gathers
+                        pre = true;
+                        ne0 = in_ptr[vn];
+                        ne1 = in_ptr[vn + 1];
+                        if (ne0 + lane < ne1) {
+                            const InEdge e = in_edge[ne0 + lane];
+                            neu = e.u;
+                            new_ = e.w < L16_INF ? e.w : L16_INF;
+                            nm = changed_lanes(chg_b, neu, t);
+                        }
+                    }
 #pragma unroll
                     for (int q = 0; q < FR_EB; ++q) best = relax8(best, x[q], w2[q]);
                 }
             }
+            if (!pre) {  // nothing gathered for v
+                ne0 = in_ptr[vn];
+                ne1 = in_ptr[vn + 1];
+                if (ne0 + lane < ne1) {
+                    const InEdge e = in_edge[ne0 + lane];
+                    neu = e.u;
+                    new_ = e.w < L16_INF ? e.w : L16_INF;
+                    nm = changed_lanes(chg_b, neu, t);
+                }
+            }
             const bool imp = best.x != own.x || best.y != own.y || best.z != own.z || best.w != own.w;
             const uint64_t im = __ballot(imp);
-            if (!im) continue;
-            any_imp = true;
-            if (imp) Lb[(uint64_t)v * 64 + lane] = best;
-            if (lane == 0) {  // this sweep's lanes, and those of sweep t - 1 that readers may still need
-                Chg cnew;
-                cnew.stamp = t;
-                cnew.pad = 0;
-                cnew.lanes = im | (old.stamp + 1 == t ? old.lanes : 0ull);
-                chg_b[v] = cnew;
+            if (im) {
+                any_imp = true;
+                if (imp) Lb[(uint64_t)v * 64 + lane] = best;
+                if (lane == 0) {  // this sweep's lanes, and those of sweep t - 1 that readers may still need
+                    Chg cnew;
+                    cnew.stamp = t;
+                    cnew.pad = 0;
+                    cnew.lanes = im | (old.stamp + 1 == t ? old.lanes : 0ull);
+                    chg_b[v] = cnew;
+                }
+                mark(act_b, v, t, sym, in_edge, eu, e0, e1, row_ptr, col, lane);
             }
-            mark(act_b, v, t, sym, in_edge, eu, e0, e1, row_ptr, col, lane);
+            if (!more) break;
+            v = vn;
+            e0 = ne0;
+            e1 = ne1;
+            eu = neu;
+            ew = new_;
+            m = nm;
         }
     }
     note_improved(last, t, any_imp, lane);
@@ -381,22 +431,41 @@ __global__ __launch_bounds__(FR_WAVES * 64) void fr_loss_sweep_kernel(
         const uint8_t *tb = tight + (uint64_t)b * E * 64 + lane;
         const uint8_t *sbc = sb_cur + (uint64_t)b * V * 64 + lane;
         uint8_t *sbn = sb_next + (uint64_t)b * V * 64 + lane;
-        while (items) {
-            const uint32_t v = v0 + __builtin_ctzll(items);
-            items &= items - 1;
+        if (!items) continue;
+        // items are software-pipelined: the next item's in-edge head (row
+        // bounds and first 64 in-edges) is loaded while the current one's
+        // change bytes are in flight
+        uint32_t v = v0 + __builtin_ctzll(items);
+        items &= items - 1;
+        uint64_t e0 = in_ptr[v], e1 = in_ptr[v + 1];
+        uint32_t eu = 0;
+        float eeb = 0.f;
+        if (e0 + lane < e1) {
+            const InEdge e = in_edge[e0 + lane];
+            eu = e.u;
+            eeb = e.eb;
+        }
+        for (;;) {
+            const bool more = items != 0;
+            const uint32_t vn = more ? v0 + __builtin_ctzll(items) : v;
+            if (more) items &= items - 1;
             float4 *pv = Pb + (uint64_t)v * 128 + 2 * lane;
             const float4 o0 = pv[0], o1 = pv[1];
             float best[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
-            const uint64_t e0 = in_ptr[v], e1 = in_ptr[v + 1];
-            uint32_t eu = 0;
+            uint64_t ne0 = 0, ne1 = 0;
+            uint32_t neu = 0;
+            float neeb = 0.f;
+            bool pre = !more;
             for (uint64_t c0 = e0; c0 < e1; c0 += 64) {
-                const uint64_t k = c0 + lane;
-                float eeb = 0.f;
-                eu = 0;
-                if (k < e1) {
-                    const InEdge e = in_edge[k];
-                    eu = e.u;
-                    eeb = e.eb;
+                if (c0 != e0) {  // chunks past the head
+                    const uint64_t k = c0 + lane;
+                    eu = 0;
+                    eeb = 0.f;
+                    if (k < e1) {
+                        const InEdge e = in_edge[k];
+                        eu = e.u;
+                        eeb = e.eb;
+                    }
                 }
                 const uint32_t n = e1 - c0 < 64 ? (uint32_t)(e1 - c0) : 64u;
                 for (uint32_t j0 = 0; j0 < n; j0 += FR_EBL) {
@@ -411,6 +480,16 @@ __global__ __launch_bounds__(FR_WAVES * 64) void fr_loss_sweep_kernel(
                             u[q] = __builtin_amdgcn_readlane(eu, j0 + q);
                             eb[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(eeb), j0 + q));
                             m[q] = tb[(c0 + j0 + q) * 64] & (sbc[(uint64_t)u[q] * 64] | sbn[(uint64_t)u[q] * 64]);
+                        }
+                    }
+                    if (!pre) {  // the next item's head, behind this batch's loads
+                        pre = true;
+                        ne0 = in_ptr[vn];
+                        ne1 = in_ptr[vn + 1];
+                        if (ne0 + lane < ne1) {
+                            const InEdge e = in_edge[ne0 + lane];
+                            neu = e.u;
+                            neeb = e.eb;
                         }
                     }
                     float4 x0[FR_EBL], x1[FR_EBL];
@@ -434,19 +513,34 @@ __global__ __launch_bounds__(FR_WAVES * 64) void fr_loss_sweep_kernel(
                     }
                 }
             }
+            if (!pre) {  // v has no in-edge
+                ne0 = in_ptr[vn];
+                ne1 = in_ptr[vn + 1];
+                if (ne0 + lane < ne1) {
+                    const InEdge e = in_edge[ne0 + lane];
+                    neu = e.u;
+                    neeb = e.eb;
+                }
+            }
             const float ov[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
             uint32_t ib = 0;  // the lane's improved sources
 #pragma unroll
             for (int i = 0; i < 8; ++i) ib |= best[i] < ov[i] ? 1u << i : 0u;
-            const uint64_t im = __ballot(ib != 0);
-            if (!im) continue;
-            any_imp = true;
-            if (ib) {
-                pv[0] = make_float4(best[0], best[1], best[2], best[3]);
-                pv[1] = make_float4(best[4], best[5], best[6], best[7]);
-                sbn[(uint64_t)v * 64] = (uint8_t)ib;  // only this wave writes v's byte this sweep
+            if (__ballot(ib != 0)) {
+                any_imp = true;
+                if (ib) {
+                    pv[0] = make_float4(best[0], best[1], best[2], best[3]);
+                    pv[1] = make_float4(best[4], best[5], best[6], best[7]);
+                    sbn[(uint64_t)v * 64] = (uint8_t)ib;  // only this wave writes v's byte this sweep
+                }
+                mark(act_b, v, t, sym, in_edge, eu, e0, e1, row_ptr, col, lane);
             }
-            mark(act_b, v, t, sym, in_edge, eu, e0, e1, row_ptr, col, lane);
+            if (!more) break;
+            v = vn;
+            e0 = ne0;
+            e1 = ne1;
+            eu = neu;
+            eeb = neeb;
         }
     }
     note_improved(last, t, any_imp, lane);

@@ -1264,7 +1264,7 @@ __device__ __forceinline__ void chunk_steps16(uint32_t (&acc)[8][4], StepOps16 (
 // triangle, no exits) without the XCD remap of tile_of is the default: C3
 // rest per build, same box, with the remap, h = 32 / 16 / 8 / 4 / 2 / 1:
 // 74.9 / 66.4 / 63.5 / 62.9 / 62.4 / 62.2 ms; without it h = 4 / 2 / 1:
-// 62.2 / 61.1 / 60.9 ms (knobs SRT_FW_BAND_H, SRT_FW_XCD=1; taller bands'
+// 62.2 / 61.1 / 60.9 ms (band heights and the XCD remap, since removed; taller bands'
 // L2 reuse does not pay -- the launch is VALU-bound, not fetch-bound -- and
 // the remap puts a band's short in-group tiles all on one XCD, which then
 // idles in the launch's tail; a group-last order measured 62.1).  The
@@ -2192,14 +2192,11 @@ srt_status fw_rounds_sym_sharded(srt_plan *p, int p1r, srt_err *err) {
     // the round's critical path; knob SRT_FW_SYM_SMALL=0/1 for A/B
     bool small = p->tl_own < 4096;
     if (const char *e = std::getenv("SRT_FW_SYM_SMALL")) small = std::atoi(e) != 0;
-    // the quarter-tile cross also packs row k1 into the slot (knob
-    // SRT_FW_FUSE_PACK=0: the separate pack kernel, for A/B)
-    bool fuse_pack = true;
-    if (const char *e = std::getenv("SRT_FW_FUSE_PACK")) fuse_pack = std::atoi(e) != 0;
+    // the quarter-tile cross also packs row k1 into the slot ...
+    const bool fuse_pack = true;
     // ... and the unpack of row k1 runs beside p1(k1) in one launch (two-step
-    // phase 1; knob SRT_FW_FUSE_P1=0: separate launches)
-    bool fuse_p1 = p->fw_p1 >= 1;
-    if (const char *e = std::getenv("SRT_FW_FUSE_P1")) fuse_p1 = fuse_p1 && std::atoi(e) != 0;
+    // phase 1)
+    const bool fuse_p1 = p->fw_p1 >= 1;
     auto p2row_mirror = [&](hipStream_t s, uint32_t k) {
         const Rect row{make_span(k, k + 1), make_span(0, nblk, k)};
         if (small)
@@ -2393,10 +2390,8 @@ srt_status fw_rounds_t(srt_plan *p, srt_err *err) {
     const Rect none{make_span(0, 0), make_span(0, 0)};
     p->p3_launches = 0;
     p->p3_work = 0.0;
-    // phase-3 launches bracketed by timing events (kernel_stats): every
-    // ev_every-th round (knob SRT_FW_EVENT_EVERY, measurement only)
-    uint32_t ev_every = 1;
-    if (const char *e = std::getenv("SRT_FW_EVENT_EVERY")) ev_every = std::max(1, std::atoi(e));
+    // phase-3 launches bracketed by timing events (kernel_stats), every round
+    const uint32_t ev_every = 1;
     const size_t need = 2 * (size_t)nblk + 2;
     while (p->ev.size() < need) {
         hipEvent_t e;
@@ -2570,7 +2565,7 @@ void launch_group(srt_plan *p, hipStream_t s, uint32_t a, uint32_t g, const Rect
     if (!n) return;
     K *D = reinterpret_cast<K *>(p->d_D);
     // bit 16: banded tile order (plan knob SRT_FW_BAND=0 turns it off for A/B timing)
-    // bit 24: XCD remap of the triangle order (knob SRT_FW_XCD=1, A/B timing)
+    // bit 24: XCD remap of the triangle order (measured no faster; plan field fw_xcd off)
     const uint32_t arg = g | (p->fw_band ? 0x10000u : 0u) | band_bits(p->fw_band_h) |
                          (p->fw_xcd ? 1u << 24 : 0u) |
                          (chain ? 0u : 1u << 26);

@@ -120,12 +120,12 @@ struct srt_plan {
     uint32_t tl_max = 0, tl_own = 0;
     uint16_t *d_rowslots = nullptr;    // N x ceil(nblk / N) tiles: the per-round row exchange
     uint16_t *d_fbuf = nullptr;        // N x tl_max tiles: the final exchange
-    bool fw_xcd = false;          // triangle rest: XCD remap of the order (knob SRT_FW_XCD=1, A/B timing)
+    bool fw_xcd = false;          // triangle rest: XCD remap of the order (measured no faster: off)
     // square rest order: plain row-major, dealt round-robin over the XCDs, by
     // default -- C3 forced square (SRT_FW_SYM=0), rest per build: remapped +
     // banded 119.3 ms, remapped 120.5, neither 117.9 (the remap concentrates
     // the group's short tiles on one XCD; see the triangle order in srt_fw.hip)
-    uint32_t fw_band_h = 1;       // triangle rest: rows per band (power of 2, knob SRT_FW_BAND_H, read at create)
+    uint32_t fw_band_h = 1;       // triangle rest: rows per band (power of 2; 1 measured best)
     bool fw_band = false;         // grouped launches: banded tile order (knob SRT_FW_BAND=1, read at create)
     uint32_t emulate_ranks = 0;   // measurement only, see fw_rounds_t
     bool emu_closed = false;

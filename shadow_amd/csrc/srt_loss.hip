@@ -536,8 +536,7 @@ __global__ __launch_bounds__(LOSS_NT) void tight_loss_kernel(
     uint64_t *__restrict__ out_lat, float *__restrict__ out_loss, unsigned long long *stats,
     uint4 *__restrict__ ord_all, LatT *lat_all, float *loss_all, const uint64_t *__restrict__ row_ptr,
     const uint32_t *__restrict__ col, const uint64_t *__restrict__ elat, const float *__restrict__ eloss,
-    const uint32_t *__restrict__ row_list, void *__restrict__ out32, float *__restrict__ out32_loss, bool stage16,
-    uint32_t diag) {
+    const uint32_t *__restrict__ row_list, void *__restrict__ out32, float *__restrict__ out32_loss, bool stage16) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ uint64_t red[16];
     __shared__ unsigned long long red_min[16], red_cnt[16];
@@ -590,12 +589,10 @@ __global__ __launch_bounds__(LOSS_NT) void tight_loss_kernel(
         for (int k = 0; k < nw; ++k) mx = red[k] > mx ? red[k] : mx;
         int shift = 0;
         while ((mx >> shift) >= (uint64_t)NBK) ++shift;
-        // diag (timing-only knob SRT_LOSS_DIAG, wrong tables): bit 0 skips the
-        // bucket scans, bit 1 the row output, bit 2 the counting sort
-        const uint32_t nb = (diag & 5u) ? 0u : (uint32_t)(mx >> shift) + 1;
+        const uint32_t nb = (uint32_t)(mx >> shift) + 1;
         const bool few = nb <= 64;  // uniform: aggregate the LDS atomics per wave
         // 2. counting sort of the reachable vertices (s excluded) by bucket
-        for (uint32_t base = 0; base < ((diag & 4u) ? 0u : V); base += nt) {
+        for (uint32_t base = 0; base < V; base += nt) {
             const uint32_t v = base + tid;
             const LatT l = v < V ? lrow[v] : LINF;
             const bool ok = v < V && v != s && l != LINF;
@@ -651,7 +648,7 @@ __global__ __launch_bounds__(LOSS_NT) void tight_loss_kernel(
             }
         }
         __syncthreads();
-        for (uint32_t base = 0; base < ((diag & 4u) ? 0u : V); base += nt) {
+        for (uint32_t base = 0; base < V; base += nt) {
             const uint32_t v = base + tid;
             const LatT l = v < V ? lrow[v] : LINF;
             const bool ok = v < V && v != s && l != LINF;
@@ -728,7 +725,7 @@ __global__ __launch_bounds__(LOSS_NT) void tight_loss_kernel(
         uint32_t *o32 = out32 && !stage16 ? reinterpret_cast<uint32_t *>(out32) + (uint64_t)k * n : nullptr;
         uint16_t *o16 = out32 && stage16 ? reinterpret_cast<uint16_t *>(out32) + (uint64_t)k * n : nullptr;
         float *o32p = out32_loss ? out32_loss + (uint64_t)k * n : nullptr;  // staging (loss only if !out32)
-        for (uint32_t j = tid; j < ((diag & 2u) ? 0u : n); j += nt) {
+        for (uint32_t j = tid; j < n; j += nt) {
             uint64_t latv;
             float lossv;
             if (j == i) {
@@ -834,7 +831,7 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
     const uint64_t *__restrict__ ce_out, const uint64_t *__restrict__ ce_in, uint64_t g,
     const uint64_t *__restrict__ sl_lat, const float *__restrict__ sl_loss, uint64_t *__restrict__ out_lat,
     float *__restrict__ out_loss, unsigned long long *stats, const uint32_t *__restrict__ row_list,
-    void *__restrict__ out32, float *__restrict__ out32_loss, bool stage16, uint32_t diag) {
+    void *__restrict__ out32, float *__restrict__ out32_loss, bool stage16) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ uint64_t red[16];
     __shared__ unsigned long long red_min[16], red_cnt[16];
@@ -964,9 +961,7 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
         }
         // hist[l] is now the end of level l (its start: hist[l-1], or 0)
         // 3. levels in increasing latency, every weight class from its smaller end
-        // (diag, timing-only knob SRT_LOSS_DIAG, wrong tables: bit 0 skips the
-        // level walks, bit 1 the row output)
-        for (uint32_t l = 1; l <= ((diag & 1u) ? 0u : mx); ++l) {
+        for (uint32_t l = 1; l <= mx; ++l) {
             const uint32_t lo = hist[l - 1], cnt_l = hist[l] - lo;
             if (!cnt_l) continue;  // uniform
             if (tid == 0) {
@@ -1045,7 +1040,7 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
         uint32_t *o32 = out32 && !stage16 ? reinterpret_cast<uint32_t *>(out32) + (uint64_t)k * n : nullptr;
         uint16_t *o16 = out32 && stage16 ? reinterpret_cast<uint16_t *>(out32) + (uint64_t)k * n : nullptr;
         float *o32p = out32_loss ? out32_loss + (uint64_t)k * n : nullptr;  // staging (loss only if !out32)
-        for (uint32_t j = tid; j < ((diag & 2u) ? 0u : n); j += nt) {
+        for (uint32_t j = tid; j < n; j += nt) {
             uint64_t latv;
             float lossv;
             if (j == i) {
@@ -1187,7 +1182,7 @@ srt_status launch_fold(srt_plan *p, unsigned long long *d_stats, uint32_t ubits,
                            job.list ? job.count : job.range ? job.r1 : p->row1, p->d_tptr, p->d_tu,
                            reinterpret_cast<const LatT *>(p->d_tw), p->d_teb, p->d_tpk, ubits, p->kp.g, p->d_sl_lat,
                            p->d_sl_loss, p->d_out_lat, p->d_out_loss, d_stats, ord, lat_all, loss_all, p->d_row_ptr,
-                           p->d_col, p->d_lat, p->d_loss, job.list, job.out32, job.out32_loss, p->stage16, std::getenv("SRT_LOSS_DIAG") ? (uint32_t)std::atoi(std::getenv("SRT_LOSS_DIAG")) : 0u);
+                           p->d_col, p->d_lat, p->d_loss, job.list, job.out32, job.out32_loss, p->stage16);
     return SRT_OK;
 }
 
@@ -1199,18 +1194,11 @@ srt_status launch_fold_lpt(srt_plan *p, unsigned long long *d_stats, uint32_t ub
     const double avg = p->V ? (double)p->t_edges / p->V : 0.0;
     if constexpr (PACKED) {
         if (p->t_push) {
-            const char *k = std::getenv("SRT_LOSS_LPT");  // lanes per pushing member (A/B)
-            if (k && std::atoi(k) == 8) return launch_fold<LatT, LROWS, 8, true, true>(p, d_stats, ubits, job, err);
-            if (k && std::atoi(k) == 2) return launch_fold<LatT, LROWS, 2, true, true>(p, d_stats, ubits, job, err);
-            if ((k && std::atoi(k) == 4) || avg > 10.0)
-                return launch_fold<LatT, LROWS, 4, true, true>(p, d_stats, ubits, job, err);
+            if (avg > 10.0) return launch_fold<LatT, LROWS, 4, true, true>(p, d_stats, ubits, job, err);
             return launch_fold<LatT, LROWS, 2, true, true>(p, d_stats, ubits, job, err);
         }
         // 4 lanes x 8 edges per target (C3, same box: 4 / 8 / 16 lanes ->
-        // 31.9 / 33.0 / 36.5 ms for the pass; knob SRT_LOSS_LPT = 8 / 16)
-        const char *k = std::getenv("SRT_LOSS_LPT");
-        if (k && std::atoi(k) == 8) return launch_fold<LatT, LROWS, 8, PACKED, false>(p, d_stats, ubits, job, err);
-        if (k && std::atoi(k) == 16) return launch_fold<LatT, LROWS, 16, PACKED, false>(p, d_stats, ubits, job, err);
+        // 31.9 / 33.0 / 36.5 ms for the pass)
         if (avg > 10.0) return launch_fold<LatT, LROWS, 4, PACKED, false>(p, d_stats, ubits, job, err);
         return launch_fold<LatT, LROWS, 2, PACKED, false>(p, d_stats, ubits, job, err);
     }
@@ -1357,8 +1345,7 @@ srt_status launch_level(srt_plan *p, unsigned long long *d_stats, const RowJob &
                        p->d_nodes, p->n, job.list ? 0u : job.range ? job.r0 : p->row0,
                        job.list ? job.count : job.range ? job.r1 : p->row1, p->d_tcls, (uint64_t)V * CLS + 1,
                        p->d_tpk, p->d_tpk2, p->kp.g, p->d_sl_lat, p->d_sl_loss, p->d_out_lat, p->d_out_loss, d_stats,
-                       job.list, job.out32, job.out32_loss, p->stage16,
-                       std::getenv("SRT_LOSS_DIAG") ? (uint32_t)std::atoi(std::getenv("SRT_LOSS_DIAG")) : 0u);
+                       job.list, job.out32, job.out32_loss, p->stage16);
     return SRT_OK;
 }
 
@@ -1475,12 +1462,7 @@ srt_status tight_csr_t(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
 srt_status fold(srt_plan *p, unsigned long long *d_stats, const RowJob &job, srt_err *err) {
     const uint32_t V = p->V;
     if (p->t_level) {
-        // lanes per class walk (knob SRT_LOSS_LPT = 2 / 4 / 8 for A/B)
-        const char *k = std::getenv("SRT_LOSS_LPT");
-        const int lpt = k ? std::atoi(k) : 4;
-        if (lpt == 2) return launch_level<2>(p, d_stats, job);
-        if (lpt == 8) return launch_level<8>(p, d_stats, job);
-        return launch_level<4>(p, d_stats, job);
+        return launch_level<4>(p, d_stats, job);  // 4 lanes per class walk (2 and 8 measured slower)
     }
     const uint32_t ubits = (uint32_t)std::max(1, bits_of(V ? V - 1 : 0));
     const bool lds_rows = HIST_BYTES + (size_t)V * 8 + 16 <= LDS_BUDGET - 4096;
@@ -1600,7 +1582,7 @@ srt_status loss_sharded_t(srt_plan *p, unsigned long long *d_stats, srt_err *err
     p->stage16 = p->key_type == KEY_U16;
     // every rank holds the whole closure: exchange the loss only (knob
     // SRT_TAIL_LAT=1 stages the latencies too, for A/B)
-    p->stage_loss_only = p->fw_full_d && p->stage16 && !std::getenv("SRT_TAIL_LAT");
+    p->stage_loss_only = p->fw_full_d && p->stage16;
     const size_t lb = p->stage16 ? 2 : 4;  // bytes per staged latency
     if (!p->d_slat) {
         void *a = nullptr, *b = nullptr;
@@ -1708,7 +1690,7 @@ srt_status loss_emulated_t(srt_plan *p, unsigned long long *d_stats, srt_err *er
     if ((st = build_tight_rows(p, slots, ubits, maxw, err)) != SRT_OK) return st;
     const size_t chunk = (size_t)p->lrow_max * p->n;
     p->stage16 = p->key_type == KEY_U16;
-    p->stage_loss_only = p->fw_full_d && p->stage16 && !std::getenv("SRT_TAIL_LAT");
+    p->stage_loss_only = p->fw_full_d && p->stage16;
     const size_t lb = p->stage_loss_only ? 0 : p->stage16 ? 2 : 4;  // bytes per staged latency
     if (!p->d_slat) {
         void *a = nullptr, *b = nullptr;

@@ -210,23 +210,10 @@ extern "C" srt_status srt_packet_batch(srt_plan *plan, const srt_pkt *d_pkts,
     unsigned long long *partial = (unsigned long long *)(plan->d_draws + n_pkts);
     hipStream_t s = plan->stream;
     if (n_hosts) {
-        // knob SRT_PKT_DRAW (measurement only): "256x16", "64x16", "64x32", "256x32"
-        static const char *knob = std::getenv("SRT_PKT_DRAW");
-        const bool wide = knob && knob[0] == '2';
-        // default 64 x 16 (C5: 103 us/round vs 137 at 256 threads; PF 16 == 32)
-        const bool pf32 = knob && std::strstr(knob, "x32");
-        if (wide && pf32)
-            hipLaunchKernelGGL((draw_kernel<256, 32>), dim3((n_hosts + 255) / 256), dim3(256), 0, s, d_pkts,
-                               d_host_pkt_ptr, n_hosts, d_rng, round->sim_end_ns, plan->d_draws);
-        else if (wide)
-            hipLaunchKernelGGL((draw_kernel<256, 16>), dim3((n_hosts + 255) / 256), dim3(256), 0, s, d_pkts,
-                               d_host_pkt_ptr, n_hosts, d_rng, round->sim_end_ns, plan->d_draws);
-        else if (pf32)
-            hipLaunchKernelGGL((draw_kernel<64, 32>), dim3((n_hosts + 63) / 64), dim3(64), 0, s, d_pkts,
-                               d_host_pkt_ptr, n_hosts, d_rng, round->sim_end_ns, plan->d_draws);
-        else
-            hipLaunchKernelGGL((draw_kernel<64, 16>), dim3((n_hosts + 63) / 64), dim3(64), 0, s, d_pkts,
-                               d_host_pkt_ptr, n_hosts, d_rng, round->sim_end_ns, plan->d_draws);
+        // 64 threads x 16 packets in flight a host (C5: 103 us/round vs 137
+        // at 256 threads; 32 in flight no faster)
+        hipLaunchKernelGGL((draw_kernel<64, 16>), dim3((n_hosts + 63) / 64), dim3(64), 0, s, d_pkts,
+                           d_host_pkt_ptr, n_hosts, d_rng, round->sim_end_ns, plan->d_draws);
     }
     if (n_pkts) {
         uint64_t blocks = (n_pkts + DECIDE_THREADS - 1) / DECIDE_THREADS;
