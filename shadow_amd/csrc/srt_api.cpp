@@ -19,6 +19,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <atomic>
+#include <condition_variable>
+#include <deque>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -29,8 +31,14 @@
 #include <vector>
 
 #include "srt_internal.h"
+#include "srt_scan.h"
 
+using srt::CsrStats;
 using srt::KeyParams;
+using srt::csr_scan;
+using srt::host_threads;
+using srt::merge_stats;
+using srt::scan_rows;
 
 namespace {
 
@@ -89,146 +97,6 @@ srt_status edge_error(srt_err *err, int c, uint32_t a_id, uint32_t b_id) {
     return SRT_ERR_MULTI_EDGE;
 }
 
-// One pass over the borrowed CSR: the edge-attribute checks of
-// ShadowEdge::try_from that the ABI cannot assume (mod.rs:72-111: latency != 0,
-// loss in [0, 1]), endpoints in range, the self-loops of every node
-// (mod.rs:210-217, 256-293), and the statistics the key proofs need (gcd and
-// max of the latencies, completeness, parallel edges).  Rows are split over
-// host threads (the CPU share of the job: OMP_NUM_THREADS, else up to 32) by
-// equal adjacency counts; it runs while the main thread sets up the device
-// and uploads the CSR.  A row counts as free of parallel edges when its
-// far endpoints are strictly monotone (petgraph lists a node's edges in
-// reverse insertion order, so a GML graph written in node order is); any
-// other row is treated as possibly parallel, which only costs the FW init an
-// atomic min and the key proof its completeness shortcut.
-struct CsrStats {
-    uint64_t gcd = 0, maxlat = 0, selfloops = 0;
-    uint64_t zero_k = ~0ull, badloss_k = ~0ull, badcol_k = ~0ull;
-    bool unique = true, complete = true;
-    // symmetry fingerprint for the family price: sums over entries (u, v, l)
-    // of u*v*v + l*u and of v*u*u + l*v (mod 2^64) -- equal for every graph
-    // whose entry multiset is closed under (u, v, l) -> (v, u, l)
-    uint64_t sym_a = 0, sym_b = 0;
-    std::vector<uint32_t> sl_cnt;    // per node: self-loop entries
-    std::vector<uint64_t> sl_first;  // per node: first self-loop entry
-};
-
-int host_threads(uint64_t work) {
-    if (work < (1ull << 20)) return 1;
-    int t = (int)std::thread::hardware_concurrency();
-    if (const char *e = std::getenv("OMP_NUM_THREADS")) t = std::atoi(e);
-    if (const char *e = std::getenv("SRT_HOST_THREADS")) t = std::atoi(e);
-    return std::max(1, std::min(t, 32));
-}
-
-// Rows [r0, r1) into the thread's accumulator st (sl_cnt / sl_first of the
-// rows go to out).  Optional, for the piece-pipelined upload: lat32 (the
-// rows' latencies as u32, indexed from entry k_base; *lat_over set when one
-// does not fit) and *identity (cleared unless every row is exactly the
-// entries 0 .. V-1 in order, so col need not be uploaded).
-void scan_rows(const srt_csr *g, uint32_t r0, uint32_t r1, CsrStats &st, CsrStats *out, uint32_t *lat32 = nullptr,
-               uint64_t k_base = 0, bool *lat_over = nullptr, bool *identity = nullptr) {
-    const uint32_t V = g->n_nodes;
-    uint64_t gcd = st.gcd, maxlat = st.maxlat, selfl = st.selfloops, sa = st.sym_a, sb = st.sym_b;
-    bool ident = true, over = false;
-    for (uint32_t u = r0; u < r1; ++u) {
-        const uint64_t b = g->row_ptr[u], e = g->row_ptr[u + 1];
-        uint32_t cnt = 0, prev = 0;
-        uint64_t first = ~0ull;
-        bool inc = true, dec = true;
-        if (identity) ident &= e - b == V;
-        for (uint64_t k = b; k < e; ++k) {
-            const uint32_t c = g->col[k];
-            const uint64_t l = g->lat_ns[k];
-            const float q = g->loss[k];
-            if (c >= V && st.badcol_k == ~0ull) st.badcol_k = k;
-            if (l == 0 && st.zero_k == ~0ull) st.zero_k = k;
-            if (!(q >= 0.0f && q <= 1.0f) && st.badloss_k == ~0ull) st.badloss_k = k;
-            maxlat = l > maxlat ? l : maxlat;
-            sa += (uint64_t)u * c * c + l * u;
-            sb += (uint64_t)c * u * u + l * c;
-            if (lat32) {
-                over |= l > 0xffffffffull;
-                lat32[k - k_base] = (uint32_t)l;
-            }
-            if (identity) ident &= c == (uint32_t)(k - b);
-            if (gcd != 1 && l) {
-                // divisibility by the running gcd: exact in f64 below 2^53
-                bool divides;
-                if (gcd && l < (1ull << 53) && gcd < (1ull << 53)) {
-                    const uint64_t qi = (uint64_t)((double)l / (double)gcd);
-                    divides = qi * gcd == l;
-                } else {
-                    divides = gcd && l % gcd == 0;
-                }
-                if (!divides) gcd = std::gcd(gcd, l);
-            }
-            if (c == u) {
-                if (!cnt) first = k;
-                ++cnt;
-            }
-            if (k > b) {
-                inc &= c > prev;
-                dec &= c < prev;
-            }
-            prev = c;
-        }
-        out->sl_cnt[u] = cnt;
-        out->sl_first[u] = first;
-        selfl += cnt;
-        const bool uniq = inc || dec;
-        st.unique &= uniq;
-        st.complete &= uniq && (e - b - cnt) == (uint64_t)V - 1;
-    }
-    st.gcd = gcd;
-    st.maxlat = maxlat;
-    st.selfloops = selfl;
-    st.sym_a = sa;
-    st.sym_b = sb;
-    if (lat_over && over) *lat_over = true;
-    if (identity && !ident) *identity = false;
-}
-
-// per-thread accumulators into out
-void merge_stats(const std::vector<CsrStats> &part, uint32_t V, CsrStats *out) {
-    out->complete = V > 0;
-    for (const CsrStats &st : part) {
-        out->gcd = std::gcd(out->gcd, st.gcd);
-        out->maxlat = std::max(out->maxlat, st.maxlat);
-        out->selfloops += st.selfloops;
-        out->sym_a += st.sym_a;
-        out->sym_b += st.sym_b;
-        out->zero_k = std::min(out->zero_k, st.zero_k);
-        out->badloss_k = std::min(out->badloss_k, st.badloss_k);
-        out->badcol_k = std::min(out->badcol_k, st.badcol_k);
-        out->unique &= st.unique;
-        out->complete &= st.complete;
-    }
-    if (out->gcd == 0) out->gcd = 1;
-}
-
-void csr_scan(const srt_csr *g, CsrStats *out) {
-    const uint32_t V = g->n_nodes;
-    out->sl_cnt.assign(V, 0);
-    out->sl_first.assign(V, ~0ull);
-    const int T = host_threads(g->n_adj);
-    std::vector<CsrStats> part(T);
-    auto work = [&](int t, uint32_t r0, uint32_t r1) { scan_rows(g, r0, r1, part[t], out); };
-    // row ranges with about n_adj / T entries each
-    std::vector<uint32_t> cut(T + 1, V);
-    cut[0] = 0;
-    for (int t = 1; t < T; ++t) {
-        const uint64_t target = g->n_adj * (uint64_t)t / T;
-        cut[t] = (uint32_t)(std::lower_bound(g->row_ptr, g->row_ptr + V + 1, target) - g->row_ptr);
-        cut[t] = std::max(std::min(cut[t], V), cut[t - 1]);
-    }
-    std::vector<std::thread> pool;
-    for (int t = 1; t < T; ++t) pool.emplace_back(work, t, cut[t], cut[t + 1]);
-    work(0, cut[0], cut[1]);
-    for (auto &th : pool) th.join();
-    merge_stats(part, V, out);
-}
-
 // Pinned host staging of the piece-pipelined upload and download, kept for
 // the process (pinning 192 MB costs tens of milliseconds, more than the
 // transfers it speeds up), one user at a time (a concurrent build takes the
@@ -277,9 +145,11 @@ struct PieceUpload {
     uint32_t *slot[DEPTH] = {};
     hipEvent_t ev[DEPTH] = {};
     bool on = false;
+    bool check_loss = true;
 
-    bool init(const srt_csr *g_, CsrStats *cs) {
+    bool init(const srt_csr *g_, CsrStats *cs, bool check_loss_) {
         g = g_;
+        check_loss = check_loss_;
         const char *pe = std::getenv("SRT_UPLOAD_PIECE");
         if (pe) PE = 1ull << std::max(4, std::min(24, std::atoi(pe)));
         else if (g->n_adj < PE) return false;
@@ -321,7 +191,7 @@ struct PieceUpload {
             const uint32_t a = w == 0 ? cut[c] : row_at(k0 + (k1 - k0) * w / T);
             const uint32_t b = w == T - 1 ? cut[c + 1] : row_at(k0 + (k1 - k0) * (w + 1) / T);
             bool ov = false, id = true;
-            if (a < b) scan_rows(g, a, b, part[w], cs, slot[c % DEPTH], k0, &ov, &id);
+            if (a < b) scan_rows(g, a, b, part[w], cs, slot[c % DEPTH], k0, &ov, &id, check_loss);
             over[(size_t)c * T + w] = ov;
             ident[(size_t)c * T + w] = id;
             done[c].fetch_add(1, std::memory_order_acq_rel);
@@ -378,6 +248,84 @@ struct PieceUpload {
             ready.store((int)P);
             for (auto &th : pool) th.join();
         }
+    }
+};
+
+// End-to-end builds: the edge losses uploaded while the closure runs, through
+// the pinned staging in 64 MB pieces (host threads copy a piece into a slot,
+// 3 in flight, the DMA runs at the link rate instead of the pageable ~21 GB/s:
+// C3's 1 GB 48 ms -> ~25, under the 46 ms closure), then range-checked on the
+// device (srt::loss_check; the host scan skipped the losses).  Falls back to
+// one pageable copy when the staging is busy.
+struct LossUpload {
+    static constexpr int DEPTH = 3;
+    static constexpr uint64_t PE = 1ull << 24;  // floats a piece
+    const float *src = nullptr;
+    uint64_t m = 0;
+    uint32_t P = 0;
+    int T = 1;
+    std::unique_ptr<std::atomic<int>[]> done;
+    std::atomic<int> ready{-1};
+    std::vector<std::thread> pool;
+    float *slot[DEPTH] = {};
+    hipEvent_t ev[DEPTH] = {};
+
+    void work(int w) {
+        for (uint32_t c = 0; c < P; ++c) {
+            while (ready.load(std::memory_order_acquire) < (int)c) std::this_thread::yield();
+            const uint64_t k0 = (uint64_t)c * PE, cnt = std::min(PE, m - k0);
+            const uint64_t a = cnt * w / T, b = cnt * (w + 1) / T;
+            std::memcpy(slot[c % DEPTH] + a, src + k0 + a, (b - a) * 4);
+            done[c].fetch_add(1, std::memory_order_acq_rel);
+        }
+    }
+    // on stream `up`; the check's result goes to p->d_lossbad
+    srt_status run(srt_plan *p, hipStream_t up, srt_err *err) {
+        std::unique_lock<std::mutex> lk(g_pinned.m, std::try_to_lock);
+        if (!lk.owns_lock() || g_pinned.bytes < DEPTH * PE * 4) {
+            HIP_TRY(hipMemcpyAsync(p->d_loss, src, m * 4, hipMemcpyHostToDevice, up), "upload (loss)");
+            srt::loss_check(p->d_loss, m, 0, p->d_lossbad, up);
+            return SRT_OK;
+        }
+        for (int i = 0; i < DEPTH; ++i) slot[i] = reinterpret_cast<float *>(g_pinned.buf) + (uint64_t)i * PE;
+        P = (uint32_t)((m + PE - 1) / PE);
+        T = std::min(16, host_threads(m));
+        done.reset(new std::atomic<int>[P]);
+        for (uint32_t c = 0; c < P; ++c) done[c].store(0);
+        ready.store(std::min<int>(DEPTH, (int)P) - 1);
+        for (int w = 1; w < T; ++w) pool.emplace_back([this, w] { work(w); });
+        srt_status st = SRT_OK;
+        hipError_t e = hipSuccess;
+        for (int i = 0; i < DEPTH && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
+        for (uint32_t c = 0; c < P && e == hipSuccess; ++c) {
+            // this thread copies its share too, then queues the piece
+            {
+                while (ready.load(std::memory_order_acquire) < (int)c) std::this_thread::yield();
+                const uint64_t k0 = (uint64_t)c * PE, cnt = std::min(PE, m - k0);
+                std::memcpy(slot[c % DEPTH], src + k0, (cnt / T) * 4);
+                done[c].fetch_add(1, std::memory_order_acq_rel);
+            }
+            while (done[c].load(std::memory_order_acquire) < T) std::this_thread::yield();
+            const uint64_t k0 = (uint64_t)c * PE, cnt = std::min(PE, m - k0);
+            e = hipMemcpyAsync(p->d_loss + k0, slot[c % DEPTH], cnt * 4, hipMemcpyHostToDevice, up);
+            if (e == hipSuccess) e = hipEventRecord(ev[c % DEPTH], up);
+            if (e == hipSuccess && c + DEPTH < P) {
+                e = hipEventSynchronize(ev[c % DEPTH]);  // slot c's copy done: piece c + DEPTH may fill it
+                ready.store((int)(c + DEPTH), std::memory_order_release);
+            }
+        }
+        ready.store((int)P);  // release the workers on any error
+        for (auto &th : pool) th.join();
+        // one check behind all the copies: a kernel queued between them would
+        // wait for CUs the closure holds, and the next copy with it
+        if (e == hipSuccess) srt::loss_check(p->d_loss, m, 0, p->d_lossbad, up);
+        for (int i = 0; i < DEPTH; ++i)
+            if (ev[i]) {
+                (void)hipEventSynchronize(ev[i]);  // the staging is free for the download
+                (void)hipEventDestroy(ev[i]);
+            }
+        if (e != hipSuccess) st = hip_fail(err, e, "upload (loss pieces)");
+        return st;
     }
 };
 
@@ -446,10 +394,72 @@ bool choose_key_params(const CsrStats &cs, uint32_t V, uint64_t ecc_units, KeyPa
     return false;
 }
 
+// Teardown of the one-call builds' plans behind their return (C3: ~6 ms of
+// stream syncs and hipFree of ~5 GB): one worker thread, plans queued; an
+// allocation that fails drains the queue and retries; joined at exit.
+struct Reaper {
+    std::mutex m;
+    std::condition_variable cv, idle;
+    std::deque<srt_plan *> q;
+    std::thread th;
+    bool busy = false, stop = false;
+};
+Reaper g_reap;
+
+void reap_worker() {
+    std::unique_lock<std::mutex> lk(g_reap.m);
+    for (;;) {
+        g_reap.cv.wait(lk, [] { return g_reap.stop || !g_reap.q.empty(); });
+        if (g_reap.q.empty()) return;  // stopping, nothing left
+        srt_plan *p = g_reap.q.front();
+        g_reap.q.pop_front();
+        g_reap.busy = true;
+        lk.unlock();
+        srt_plan_destroy(p);
+        lk.lock();
+        g_reap.busy = false;
+        if (g_reap.q.empty()) g_reap.idle.notify_all();
+    }
+}
+
+// every queued plan destroyed
+void reap_drain() {
+    std::unique_lock<std::mutex> lk(g_reap.m);
+    g_reap.idle.wait(lk, [] { return g_reap.q.empty() && !g_reap.busy; });
+}
+
+// registered after the HIP runtime started, so it runs before its teardown
+void reap_stop_at_exit() {
+    {
+        std::lock_guard<std::mutex> lk(g_reap.m);
+        g_reap.stop = true;
+    }
+    g_reap.cv.notify_all();
+    if (g_reap.th.joinable()) g_reap.th.join();
+}
+
+void reap_async(srt_plan *p) {
+    static std::once_flag once;
+    std::call_once(once, [] {
+        g_reap.th = std::thread(reap_worker);
+        std::atexit(reap_stop_at_exit);
+    });
+    {
+        std::lock_guard<std::mutex> lk(g_reap.m);
+        g_reap.q.push_back(p);
+    }
+    g_reap.cv.notify_one();
+}
+
 template <typename T>
 srt_status dmalloc(T **p, size_t count, srt_err *err) {
     void *ptr = nullptr;
     hipError_t e = hipMalloc(&ptr, std::max<size_t>(count, 1) * sizeof(T));
+    if (e == hipErrorOutOfMemory) {  // plans still being torn down: wait for them once
+        (void)hipGetLastError();
+        reap_drain();
+        e = hipMalloc(&ptr, std::max<size_t>(count, 1) * sizeof(T));
+    }
     if (e != hipSuccess) return hip_fail(err, e, "hipMalloc");
     *p = (T *)ptr;
     return SRT_OK;
@@ -498,6 +508,8 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_fcol);
     hipFree(p->d_fimp);
     if (p->h_fimp) hipHostFree(p->h_fimp);
+    if (p->d_lossbad) hipFree(p->d_lossbad);
+    if (p->h_lossbad) hipHostFree(p->h_lossbad);
     hipFree(p->d_rstats);
     hipFree(p->d_ev_scratch);
     hipFree(p->d_tflag);
@@ -731,9 +743,9 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     //    thread sets up the device and uploads the CSR
     CsrStats cs;
     PieceUpload pu;
-    const bool piped = pu.init(g, &cs);
+    const bool piped = pu.init(g, &cs, !defer_loss);
     std::thread scanner;
-    if (!piped) scanner = std::thread([&] { csr_scan(g, &cs); });
+    if (!piped) scanner = std::thread([&] { csr_scan(g, &cs, !defer_loss); });
     srt_err derr{};
     const srt_status dst = [&]() -> srt_status {
         srt_err *err = &derr;
@@ -803,6 +815,9 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     for (uint32_t i = 0; i < n; ++i) {
         const uint32_t u = nodes[i], c = cs.sl_cnt[u];
         if (c != 1) {
+            // the losses were left to the device: the parse-time error first
+            if (defer_loss && srt::first_bad_loss(g) != ~0ull)
+                return fail(SRT_ERR_INVALID, "Edge 'packet_loss' is not in the range [0,1]");
             srt_plan_destroy(p);
             return edge_error(err, (int)c, node_id(g, u), node_id(g, u));
         }
@@ -885,7 +900,11 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     p->algo = algo;
     // SSSP plans read their in-edges (with loss) from the host-built list, never
     // d_loss: drop the deferred upload so run_tail does not copy it
-    if (algo == SRT_ALGO_SSSP) p->h_loss_defer = nullptr;
+    if (algo == SRT_ALGO_SSSP) {
+        p->h_loss_defer = nullptr;
+        if (defer_loss && srt::first_bad_loss(g) != ~0ull)  // no device check on this path
+            return fail(SRT_ERR_INVALID, "Edge 'packet_loss' is not in the range [0,1]");
+    }
     p->row0 = 0;
     p->row1 = n;
     p->rows_alloc = n;
@@ -1183,15 +1202,27 @@ srt_status run_tail(srt_plan *p, srt_err *err) {
     const int rank = p->comm ? p->comm->rank : 0, nranks = p->comm ? p->comm->nranks : 1;
     unsigned long long *rstats = p->comm ? p->d_rstats + 2 * rank : p->d_stats;
     if (p->h_loss_defer) {
-        // end-to-end build: the edge losses, uploaded while the closure runs.
-        // The pageable copy runs on the host thread once its stream reaches
-        // it, so it goes on the comm stream (idle on one GPU; the closure is
-        // all on the main and side streams) and the main stream waits for it
-        // before the loss pass -- on the main stream it would queue behind the
-        // closure (measured: C3 +19 ms, the 1 GB at ~55 GB/s, serial).
+        // end-to-end build: the edge losses, uploaded while the closure runs
+        // and range-checked on the device (LossUpload).  The copies run on
+        // the host thread once their stream reaches them, so they go on the
+        // comm stream (idle on one GPU; the closure is all on the main and
+        // side streams) and the main stream waits for them before the loss
+        // pass -- on the main stream they would queue behind the closure
+        // (measured: C3 +19 ms, serial).
         hipStream_t up = p->comm ? p->stream : p->comm_stream;
-        HIP_TRY(hipMemcpyAsync(p->d_loss, p->h_loss_defer, p->n_adj * 4, hipMemcpyHostToDevice, up),
-                "upload (loss)");
+        if (!p->d_lossbad) {
+            HIP_TRY(hipMalloc(&p->d_lossbad, 8), "hipMalloc(loss check)");
+            HIP_TRY(hipHostMalloc((void **)&p->h_lossbad, 8, 0), "hipHostMalloc(loss check)");
+        }
+        *p->h_lossbad = ~0ull;
+        HIP_TRY(hipMemsetAsync(p->d_lossbad, 0xff, 8, up), "memset (loss check)");
+        {
+            LossUpload lu;
+            lu.src = p->h_loss_defer;
+            lu.m = p->n_adj;
+            if (srt_status s2 = lu.run(p, up, err); s2 != SRT_OK) return s2;
+        }
+        HIP_TRY(hipMemcpyAsync(p->h_lossbad, p->d_lossbad, 8, hipMemcpyDeviceToHost, up), "download (loss check)");
         if (up != p->stream) {
             if (!p->ev_upload) HIP_TRY(hipEventCreateWithFlags(&p->ev_upload, hipEventDisableTiming), "event");
             HIP_TRY(hipEventRecord(p->ev_upload, up), "event record");
@@ -1901,8 +1932,17 @@ srt_status build_e2e(const srt_csr *g, const uint32_t *nodes, uint32_t n, srt_pa
         }
     }
     tr.mark("e2e: build + fetch");
-    srt_plan_destroy(p);
-    tr.mark("e2e: destroy");
+    // the device's loss range check (the host scan skipped it): a parse-time
+    // error, so it wins over any error of the build itself
+    if (p->h_lossbad && s != SRT_ERR_HIP) {
+        (void)hipStreamSynchronize(p->comm_stream);
+        if (*p->h_lossbad != ~0ull) {
+            s = SRT_ERR_INVALID;
+            set_err(err, SRT_ERR_INVALID, "Edge 'packet_loss' is not in the range [0,1]");
+        }
+    }
+    reap_async(p);  // teardown behind the return
+    tr.mark("e2e: destroy queued");
     return s;
 }
 

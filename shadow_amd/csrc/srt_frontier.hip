@@ -55,8 +55,13 @@ namespace {
 constexpr uint32_t FR_SRC = 512;     // sources per block (8 words of 64)
 constexpr int FR_WAVES = 4;          // waves per sweep workgroup
 constexpr int FR_EB = 8;             // edges gathered per batch (loads in flight per lane)
-constexpr int FR_EBL = 4;            // loss sweep: edges per batch (2 x 16 B gathered a lane each)
+constexpr int FR_EBL = 2;            // loss sweep: edges per batch (2 x 16 B gathered a lane each)
 constexpr uint32_t L16_INF = 0xffffu;
+
+// The sweeps are latency-bound chains of dependent gathers: 8 waves a SIMD
+// (<= 64 VGPRs, a few bytes of spill) beat fewer, fatter waves -- C4 1.03 s
+// at 5 waves/SIMD (92 VGPRs, 4 loss edges a batch) -> 0.79 s.
+#define FR_OCC __attribute__((amdgpu_waves_per_eu(8, 8)))
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
@@ -228,7 +233,7 @@ __global__ void fr_sym_act_kernel(uint32_t *act, uint8_t *fin, Chg *chg, const u
 // of the edges whose source changed in sweep t-1 or t, then batches of FR_EB
 // gathers (16 B a lane, only the lanes whose sources changed) and the packed
 // relaxation.  The own row is loaded first (independent of the chain).
-__global__ __launch_bounds__(FR_WAVES * 64) void fr_lat_sweep_kernel(
+__global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_lat_sweep_kernel(
     const uint64_t *__restrict__ in_ptr, const InEdge *__restrict__ in_edge, uint32_t V, uint32_t NB,
     uint16_t *L, Chg *chg, uint32_t *act, const uint8_t *__restrict__ fin, uint32_t *last, uint32_t t, bool sym,
     const uint64_t *__restrict__ row_ptr, const uint32_t *__restrict__ col) {
@@ -413,7 +418,7 @@ __global__ __launch_bounds__(FR_WAVES * 64) void fr_tight_kernel(const uint64_t 
 // gather u's 8 losses (32 B) and fold the tight ones that are reached (P <= 1;
 // 2.0 = not yet).  Chain per item: in-edges -> (tight, change bytes) ->
 // gather, the own losses loaded beside the in-edges; marks from registers.
-__global__ __launch_bounds__(FR_WAVES * 64) void fr_loss_sweep_kernel(
+__global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
     const uint64_t *__restrict__ in_ptr, const InEdge *__restrict__ in_edge, uint32_t V, uint32_t NB, uint64_t E,
     const uint8_t *__restrict__ tight, float *P, const uint8_t *__restrict__ sb_cur, uint8_t *sb_next,
     uint32_t *act, uint32_t *last, uint32_t t, bool sym, const uint64_t *__restrict__ row_ptr,
@@ -452,6 +457,7 @@ __global__ __launch_bounds__(FR_WAVES * 64) void fr_loss_sweep_kernel(
             float4 *pv = Pb + (uint64_t)v * 128 + 2 * lane;
             const float4 o0 = pv[0], o1 = pv[1];
             float best[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+            uint32_t ib = 0;  // the lane's improved sources
             uint64_t ne0 = 0, ne1 = 0;
             uint32_t neu = 0;
             float neeb = 0.f;
@@ -508,7 +514,10 @@ __global__ __launch_bounds__(FR_WAVES * 64) void fr_loss_sweep_kernel(
                         for (int i = 0; i < 8; ++i)
                             if (((m[q] >> i) & 1u) && xs[i] <= 1.0f) {  // u reached (not the 2.0 init)
                                 const float cnd = fold(xs[i], eb[q]);
-                                best[i] = cnd < best[i] ? cnd : best[i];
+                                if (cnd < best[i]) {
+                                    best[i] = cnd;
+                                    ib |= 1u << i;
+                                }
                             }
                     }
                 }
@@ -522,10 +531,6 @@ __global__ __launch_bounds__(FR_WAVES * 64) void fr_loss_sweep_kernel(
                     neeb = e.eb;
                 }
             }
-            const float ov[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
-            uint32_t ib = 0;  // the lane's improved sources
-#pragma unroll
-            for (int i = 0; i < 8; ++i) ib |= best[i] < ov[i] ? 1u << i : 0u;
             if (__ballot(ib != 0)) {
                 any_imp = true;
                 if (ib) {

@@ -1860,6 +1860,17 @@ __global__ void widen_u32_kernel(uint64_t *__restrict__ dst, const uint32_t *__r
         dst[e] = src[e];
 }
 
+// ShadowEdge::try_from's loss range (mod.rs:72-111) on the device, over the
+// losses as the end-to-end build uploads them: the first entry (k0 + index)
+// outside [0, 1] (or NaN; -0.0 is valid) atomic-min'ed into *first
+__global__ void loss_check_kernel(const uint32_t *__restrict__ bits, uint64_t count, uint64_t k0,
+                                  unsigned long long *first) {
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < count; e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t q = bits[e];
+        if (q > 0x3f800000u && q != 0x80000000u) atomicMin(first, (unsigned long long)(k0 + e));
+    }
+}
+
 __global__ void iota_rows_kernel(uint32_t *__restrict__ dst, uint64_t count, uint32_t V) {
     for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < count; e += (uint64_t)gridDim.x * blockDim.x)
         dst[e] = (uint32_t)(e % V);
@@ -3003,6 +3014,12 @@ void pack_paths8(srt_plan *p, uint64_t first, uint64_t count, void *dst, hipStre
 
 void widen_u32(uint64_t *dst, const uint32_t *src, uint64_t count, hipStream_t s) {
     hipLaunchKernelGGL(widen_u32_kernel, dim3(2048), dim3(256), 0, s, dst, src, count);
+}
+
+void loss_check(const float *d_loss, uint64_t count, uint64_t k0, unsigned long long *d_first, hipStream_t s) {
+    if (count)
+        hipLaunchKernelGGL(loss_check_kernel, dim3(2048), dim3(256), 0, s, reinterpret_cast<const uint32_t *>(d_loss),
+                           count, k0, d_first);
 }
 
 void iota_rows(uint32_t *dst, uint64_t count, uint32_t V, hipStream_t s) {

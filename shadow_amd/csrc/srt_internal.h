@@ -133,6 +133,9 @@ struct srt_plan {
     // while the closure runs, and the fold runs in chunks of fold_chunk_rows
     // table rows (ev_fold after each) so their download overlaps the next
     const float *h_loss_defer = nullptr;
+    // end-to-end builds: the losses are range-checked on the device as they
+    // are uploaded; the first bad entry (~0 if none) lands in h_lossbad
+    unsigned long long *d_lossbad = nullptr, *h_lossbad = nullptr;
     uint32_t fold_chunk_rows = 0;
     std::vector<hipEvent_t> ev_fold;      // emulation: D holds the closure (first run done)
     uint64_t emu_tight = 0, emu_maxw = 0;  // emulation: tight edges / max latency of the closure
@@ -390,6 +393,8 @@ void pack_paths8(srt_plan *p, uint64_t first, uint64_t count, void *dst, hipStre
 // piece-pipelined upload: dst[i] = src[i] (u32 -> u64); dst[k] = k % V (identity rows)
 void widen_u32(uint64_t *dst, const uint32_t *src, uint64_t count, hipStream_t s);
 void iota_rows(uint32_t *dst, uint64_t count, uint32_t V, hipStream_t s);
+// first loss entry outside [0, 1] of [k0, k0 + count) atomic-min'ed into *d_first
+void loss_check(const float *d_loss, uint64_t count, uint64_t k0, unsigned long long *d_first, hipStream_t s);
 // u16-key plans: u16 latency units, then the f32 losses at byte offset loss_off
 void pack_paths6(srt_plan *p, uint64_t first, uint64_t count, void *dst, uint64_t loss_off, hipStream_t s);
 // kernels (srt_sssp.hip)

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle as O
-from shadow_amd import NetworkGraph, _lib, synth
+from shadow_amd import NetworkGraph, RoutingInfo, _lib, synth
 
 pytestmark = pytest.mark.gpu
 
@@ -380,3 +380,63 @@ def test_level_fold_weight_class_limit(lat_hi, level):
     assert plan.timing()["loss_fold"] == level
     assert np.array_equal(t.latency_ns, elat)
     assert np.array_equal(t.packet_loss.view(np.uint32), eloss.view(np.uint32))
+
+
+@pytest.mark.parametrize("bad", [1.5, -0.5, float("nan")])
+def test_loss_out_of_range_rejected(bad):
+    """ShadowEdge::try_from's loss range (mod.rs:72-111): the one-call entry
+    points check it on the device as the losses upload (the host scan skips
+    them), srt_plan_create on the host, the sparse family on the host; all
+    report the reference's text.  -0.0 is in range (IEEE -0.0 >= 0)."""
+    from shadow_amd.plan import RoutingPlan
+    g = NetworkGraph.from_edges(3, [0, 1, 2, 0, 1], [0, 1, 2, 1, 2], [5, 5, 5, 7, 9], [0.0, 0.0, 0.0, 0.1, bad],
+                                directed=False)
+    for algo in (_lib.SRT_ALGO_FW, _lib.SRT_ALGO_SSSP):
+        with pytest.raises(_lib.SrtError) as e:
+            g.compute_shortest_paths([0, 1, 2], algo=algo)
+        assert e.value.code == _lib.SRT_ERR_INVALID and str(e.value) == "Edge 'packet_loss' is not in the range [0,1]"
+        with pytest.raises(_lib.SrtError) as e:
+            RoutingPlan(g, np.arange(3, dtype=np.uint32), algo=algo, device=0)
+        assert e.value.code == _lib.SRT_ERR_INVALID and "packet_loss" in str(e.value)
+    with pytest.raises(_lib.SrtError) as e:
+        RoutingInfo.build(g, [0, 1, 2])
+    assert "packet_loss" in str(e.value)
+    ok = NetworkGraph.from_edges(3, [0, 1, 2, 0, 1], [0, 1, 2, 1, 2], [5, 5, 5, 7, 9], [0.0, 0.0, 0.0, 0.1, -0.0],
+                                 directed=False)
+    t = ok.compute_shortest_paths([0, 1, 2])
+    assert t.latency_ns[0, 2] == 16
+
+
+def test_loss_error_precedes_self_loop_error():
+    """A bad loss and a missing self-loop: the parse-time loss error wins
+    (mod.rs:72-111 before 210-217), although the end-to-end scan left the
+    losses to the device."""
+    g = NetworkGraph.from_edges(3, [0, 1, 0, 1], [0, 1, 1, 2], [5, 5, 7, 9], [0.0, 0.0, 2.0, 0.0], directed=False)
+    with pytest.raises(_lib.SrtError) as e:
+        g.compute_shortest_paths([0, 1, 2])
+    assert str(e.value) == "Edge 'packet_loss' is not in the range [0,1]"
+    g2 = NetworkGraph.from_edges(3, [0, 1, 0, 1], [0, 1, 1, 2], [5, 5, 7, 9], [0.0, 0.0, 0.5, 0.0], directed=False)
+    with pytest.raises(_lib.SrtError) as e:
+        g2.compute_shortest_paths([0, 1, 2])
+    assert str(e.value) == "No edge connecting node 2 to 2"
+
+
+def test_loss_checked_on_device_in_pieces():
+    """4,200-node complete graph (17.6 Mi entries: two 16 Mi upload pieces):
+    a bad loss in the second piece's last row is found by the device check;
+    the clean graph then builds."""
+    n = 4200
+    row_ptr, col, lat, loss = synth.complete_csr(n, 23)
+    loss = loss.copy()
+    k = len(loss) - 3
+    keep = loss[k]
+    loss[k] = np.float32(1.25)
+    g = NetworkGraph(n, np.arange(n, dtype=np.uint32), row_ptr, col, lat, loss, directed=False)
+    with pytest.raises(_lib.SrtError) as e:
+        RoutingInfo.build(g, np.arange(n, dtype=np.uint32))
+    assert str(e.value) == "Edge 'packet_loss' is not in the range [0,1]"
+    loss[k] = keep
+    g = NetworkGraph(n, np.arange(n, dtype=np.uint32), row_ptr, col, lat, loss, directed=False)
+    nodes = np.arange(0, n, 7, dtype=np.uint32)
+    t = g.compute_shortest_paths(nodes)
+    assert t.latency_ns.shape == (len(nodes), len(nodes)) and (t.latency_ns > 0).all()
