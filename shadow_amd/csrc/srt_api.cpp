@@ -284,6 +284,7 @@ struct LossUpload {
         std::unique_lock<std::mutex> lk(g_pinned.m, std::try_to_lock);
         if (!lk.owns_lock() || g_pinned.bytes < DEPTH * PE * 4) {
             HIP_TRY(hipMemcpyAsync(p->d_loss, src, m * 4, hipMemcpyHostToDevice, up), "upload (loss)");
+            HIP_TRY(hipMemsetAsync(p->d_lossbad, 0xff, 8, up), "memset (loss check)");
             srt::loss_check(p->d_loss, m, 0, p->d_lossbad, up);
             return SRT_OK;
         }
@@ -296,6 +297,9 @@ struct LossUpload {
         for (int w = 1; w < T; ++w) pool.emplace_back([this, w] { work(w); });
         srt_status st = SRT_OK;
         hipError_t e = hipSuccess;
+        using clk = std::chrono::steady_clock;
+        double w_copy = 0, w_dma = 0;  // SRT_TRACE: waits on the host copies / on the DMA
+        const auto t_start = clk::now();
         for (int i = 0; i < DEPTH && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
         for (uint32_t c = 0; c < P && e == hipSuccess; ++c) {
             // this thread copies its share too, then queues the piece
@@ -305,20 +309,31 @@ struct LossUpload {
                 std::memcpy(slot[c % DEPTH], src + k0, (cnt / T) * 4);
                 done[c].fetch_add(1, std::memory_order_acq_rel);
             }
+            auto t0 = clk::now();
             while (done[c].load(std::memory_order_acquire) < T) std::this_thread::yield();
+            w_copy += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
             const uint64_t k0 = (uint64_t)c * PE, cnt = std::min(PE, m - k0);
             e = hipMemcpyAsync(p->d_loss + k0, slot[c % DEPTH], cnt * 4, hipMemcpyHostToDevice, up);
             if (e == hipSuccess) e = hipEventRecord(ev[c % DEPTH], up);
             if (e == hipSuccess && c + DEPTH < P) {
+                t0 = clk::now();
                 e = hipEventSynchronize(ev[c % DEPTH]);  // slot c's copy done: piece c + DEPTH may fill it
+                w_dma += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
                 ready.store((int)(c + DEPTH), std::memory_order_release);
             }
         }
         ready.store((int)P);  // release the workers on any error
         for (auto &th : pool) th.join();
-        // one check behind all the copies: a kernel queued between them would
-        // wait for CUs the closure holds, and the next copy with it
+        // one check behind all the copies: a kernel (the memset's fill kernel
+        // too) queued before or between them waits for CUs the closure holds,
+        // and every later copy with it (measured: the 1 GB took the closure's
+        // 48 ms)
+        if (e == hipSuccess) e = hipMemsetAsync(p->d_lossbad, 0xff, 8, up);
         if (e == hipSuccess) srt::loss_check(p->d_loss, m, 0, p->d_lossbad, up);
+        if (std::getenv("SRT_TRACE"))
+            std::fprintf(stderr, "[srt] loss pieces: %u x %llu MB, %d threads, %.1f ms: waited %.1f ms on copies, %.1f on DMA\n",
+                         P, (unsigned long long)(PE * 4 >> 20), T,
+                         std::chrono::duration<double, std::milli>(clk::now() - t_start).count(), w_copy, w_dma);
         for (int i = 0; i < DEPTH; ++i)
             if (ev[i]) {
                 (void)hipEventSynchronize(ev[i]);  // the staging is free for the download
@@ -449,6 +464,69 @@ void reap_async(srt_plan *p) {
         g_reap.q.push_back(p);
     }
     g_reap.cv.notify_one();
+}
+
+// Streams and events of destroyed plans, kept for the next plan on the same
+// device: creating a plan's 3 streams, 6 events and the ~2 per 128-pivot
+// round timing events of the closure cost ~4-6 ms (C3).  At most 4 sets.
+struct StreamSet {
+    int device = -1;
+    hipStream_t stream = nullptr, side = nullptr, comm = nullptr;
+    hipEvent_t begin = nullptr, end = nullptr, cross = nullptr, pivot = nullptr, row = nullptr, bcast = nullptr;
+    std::vector<hipEvent_t> ev, ev_tail;
+};
+struct StreamPool {
+    std::mutex m;
+    std::vector<StreamSet> sets;
+};
+StreamPool g_streams;
+
+bool take_stream_set(int device, srt_plan *p) {
+    std::lock_guard<std::mutex> lk(g_streams.m);
+    for (size_t i = 0; i < g_streams.sets.size(); ++i)
+        if (g_streams.sets[i].device == device) {
+            StreamSet &x = g_streams.sets[i];
+            p->stream = x.stream;
+            p->side_stream = x.side;
+            p->comm_stream = x.comm;
+            p->ev_begin = x.begin;
+            p->ev_end = x.end;
+            p->ev_cross = x.cross;
+            p->ev_pivot = x.pivot;
+            p->ev_row = x.row;
+            p->ev_bcast = x.bcast;
+            p->ev.swap(x.ev);
+            p->ev_tail.swap(x.ev_tail);
+            g_streams.sets.erase(g_streams.sets.begin() + i);
+            return true;
+        }
+    return false;
+}
+
+// the plan's (synchronised) streams and events into the pool; false: full
+bool give_stream_set(srt_plan *p) {
+    if (!p->own_stream || !p->stream || !p->side_stream || !p->comm_stream || !p->ev_begin || !p->ev_end ||
+        !p->ev_cross || !p->ev_pivot || !p->ev_row || !p->ev_bcast)
+        return false;
+    std::lock_guard<std::mutex> lk(g_streams.m);
+    if (g_streams.sets.size() >= 4) return false;
+    StreamSet x;
+    x.device = p->device;
+    x.stream = p->stream;
+    x.side = p->side_stream;
+    x.comm = p->comm_stream;
+    x.begin = p->ev_begin;
+    x.end = p->ev_end;
+    x.cross = p->ev_cross;
+    x.pivot = p->ev_pivot;
+    x.row = p->ev_row;
+    x.bcast = p->ev_bcast;
+    x.ev.swap(p->ev);
+    x.ev_tail.swap(p->ev_tail);
+    g_streams.sets.push_back(std::move(x));
+    p->stream = p->side_stream = p->comm_stream = nullptr;
+    p->ev_begin = p->ev_end = p->ev_cross = p->ev_pivot = p->ev_row = p->ev_bcast = nullptr;
+    return true;
 }
 
 template <typename T>
@@ -754,23 +832,25 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         p->device = dev;
         hipError_t e = hipSetDevice(dev);
         if (e != hipSuccess) return hip_fail(err, e, "hipSetDevice");
-        e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
-        if (e != hipSuccess) return hip_fail(err, e, "hipStreamCreate");
         p->own_stream = true;
-        int lo = 0, hi = 0;
-        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-        e = hipStreamCreateWithPriority(&p->side_stream, hipStreamNonBlocking, hi);
-        if (e == hipSuccess) e = hipStreamCreateWithPriority(&p->comm_stream, hipStreamNonBlocking, hi);
-        if (e != hipSuccess) return hip_fail(err, e, "hipStreamCreateWithPriority");
-        (void)hipEventCreate(&p->ev_begin);
-        (void)hipEventCreate(&p->ev_end);
-        // the stream-to-stream events of the look-ahead schedule (the
-        // system-scope fence is kept: skipping it measured no faster)
-        const unsigned sync_fl = hipEventDisableTiming;
-        (void)hipEventCreateWithFlags(&p->ev_cross, sync_fl);
-        (void)hipEventCreateWithFlags(&p->ev_pivot, sync_fl);
-        (void)hipEventCreateWithFlags(&p->ev_row, sync_fl);
-        (void)hipEventCreateWithFlags(&p->ev_bcast, sync_fl);
+        if (!take_stream_set(dev, p)) {
+            e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
+            if (e != hipSuccess) return hip_fail(err, e, "hipStreamCreate");
+            int lo = 0, hi = 0;
+            (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+            e = hipStreamCreateWithPriority(&p->side_stream, hipStreamNonBlocking, hi);
+            if (e == hipSuccess) e = hipStreamCreateWithPriority(&p->comm_stream, hipStreamNonBlocking, hi);
+            if (e != hipSuccess) return hip_fail(err, e, "hipStreamCreateWithPriority");
+            (void)hipEventCreate(&p->ev_begin);
+            (void)hipEventCreate(&p->ev_end);
+            // the stream-to-stream events of the look-ahead schedule (the
+            // system-scope fence is kept: skipping it measured no faster)
+            const unsigned sync_fl = hipEventDisableTiming;
+            (void)hipEventCreateWithFlags(&p->ev_cross, sync_fl);
+            (void)hipEventCreateWithFlags(&p->ev_pivot, sync_fl);
+            (void)hipEventCreateWithFlags(&p->ev_row, sync_fl);
+            (void)hipEventCreateWithFlags(&p->ev_bcast, sync_fl);
+        }
         tr.mark("create: streams + events");
         srt_status st;
         if ((st = dmalloc(&p->d_row_ptr, (size_t)g->n_nodes + 1, err)) != SRT_OK ||
@@ -1101,6 +1181,7 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
             std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
                 return in_ptr[a + 1] - in_ptr[a] > in_ptr[b + 1] - in_ptr[b];
             });
+            // (measured, C4: no hubs dealt 1.30 s, the top 64 0.95 s, one per chunk 0.80 s)
             const uint32_t H = V >= 64 * cpb ? cpb : (V > cpb ? cpb - 1 : 0);  // chunks with a full slot 0
             std::vector<uint8_t> hub(V, 0);
             for (uint32_t h = 0; h < H; ++h) {
@@ -1215,7 +1296,6 @@ srt_status run_tail(srt_plan *p, srt_err *err) {
             HIP_TRY(hipHostMalloc((void **)&p->h_lossbad, 8, 0), "hipHostMalloc(loss check)");
         }
         *p->h_lossbad = ~0ull;
-        HIP_TRY(hipMemsetAsync(p->d_lossbad, 0xff, 8, up), "memset (loss check)");
         {
             LossUpload lu;
             lu.src = p->h_loss_defer;
@@ -1394,6 +1474,7 @@ void srt_plan_destroy(srt_plan *p) {
     if (p->side_stream) hipStreamSynchronize(p->side_stream);
     if (p->comm_stream) hipStreamSynchronize(p->comm_stream);
     free_plan_buffers(p);
+    (void)give_stream_set(p);  // synchronised above: reusable by the next plan
     for (hipEvent_t e : p->ev) hipEventDestroy(e);
     for (hipEvent_t e : p->ev_tail) hipEventDestroy(e);
     for (hipEvent_t e : {p->ev_begin, p->ev_end, p->ev_cross, p->ev_pivot, p->ev_row, p->ev_bcast, p->ev_loss0,

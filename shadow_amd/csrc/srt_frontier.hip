@@ -54,7 +54,7 @@ namespace {
 
 constexpr uint32_t FR_SRC = 512;     // sources per block (8 words of 64)
 constexpr int FR_WAVES = 4;          // waves per sweep workgroup
-constexpr int FR_EB = 8;             // edges gathered per batch (loads in flight per lane)
+constexpr int FR_EB = 8;              // edges gathered per batch (loads in flight per lane)
 constexpr int FR_EBL = 2;            // loss sweep: edges per batch (2 x 16 B gathered a lane each)
 constexpr uint32_t L16_INF = 0xffffu;
 
@@ -363,7 +363,11 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_lat_sweep_kernel(
 // ---------------------------------------------------------- tight pass
 // Every item (b, v), every in-edge k = (u -> v) of v:
 // tight[(b * E + k) * 64 + lane] = the lane's 8-bit mask of sources s with
-// L(s,u) + w == L(s,v) -- the only edges the loss sweeps read along.
+// L(s,u) + w == L(s,v) -- the only edges the loss sweeps read along.  A wave
+// takes 64-vertex chunks, as the sweeps do: every chunk holds one hub (slot
+// 0, srt_api.cpp's vertex order), so the waves stay balanced -- striding
+// single items by the wave count (a multiple of 64) put every hub on the same
+// few waves (C4: 33 -> 90 ms).
 __global__ __launch_bounds__(FR_WAVES * 64) void fr_tight_kernel(const uint64_t *__restrict__ in_ptr,
                                                                  const InEdge *__restrict__ in_edge, uint32_t V,
                                                                  uint32_t NB, uint64_t E,
@@ -371,9 +375,10 @@ __global__ __launch_bounds__(FR_WAVES * 64) void fr_tight_kernel(const uint64_t 
                                                                  uint8_t *__restrict__ tight) {
     const int lane = threadIdx.x & 63;
     const uint32_t wave = blockIdx.x * FR_WAVES + (threadIdx.x >> 6), nwaves = gridDim.x * FR_WAVES;
-    const uint64_t nitems = (uint64_t)V * NB;
-    for (uint64_t it = __builtin_amdgcn_readfirstlane(wave); it < nitems; it += nwaves) {
-        const uint32_t b = (uint32_t)(it / V), v = (uint32_t)(it % V);
+    const uint32_t cpb = (V + 63) / 64, nchunks = cpb * NB;
+    for (uint32_t c = __builtin_amdgcn_readfirstlane(wave); c < nchunks; c += nwaves)
+    for (uint32_t v = (c % cpb) * 64, vend = std::min(V, v + 64); v < vend; ++v) {
+        const uint32_t b = c / cpb;
         const uint4 *Lb = reinterpret_cast<const uint4 *>(L + (uint64_t)b * V * FR_SRC);
         const uint4 own = Lb[(uint64_t)v * 64 + lane];
         uint8_t *tb = tight + (uint64_t)b * E * 64 + lane;
