@@ -55,7 +55,8 @@ namespace {
 constexpr uint32_t FR_SRC = 512;     // sources per block (8 words of 64)
 constexpr int FR_WAVES = 4;          // waves per sweep workgroup
 constexpr int FR_EB = 8;              // edges gathered per batch (loads in flight per lane)
-constexpr int FR_EBL = 2;            // loss sweep: edges per batch (2 x 16 B gathered a lane each)
+constexpr int FR_EBL = 2;            // loss sweep: edges gathered per batch (2 x 16 B a lane each)
+constexpr int FR_MG = 8;             // loss sweep: in-edges whose masks load together (multiple of 4)
 constexpr uint32_t L16_INF = 0xffffu;
 
 // The sweeps are latency-bound chains of dependent gathers: 8 waves a SIMD
@@ -271,9 +272,12 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_lat_sweep_kernel(
             const bool more = items != 0;
             const uint32_t vn = more ? v0 + __builtin_ctzll(items) : v;
             if (more) items &= items - 1;
-            const uint4 own = Lb[(uint64_t)v * 64 + lane];
-            const Chg old = chg_b[v];  // own record, for the kept lanes (loaded beside the row)
-            uint4 best = own;
+            // candidates only; the own row is read at the end by the lanes
+            // that gathered anything (most lanes of an active item gather
+            // nothing: reading every row cost 1 KB an item a sweep)
+            uint4 best = make_uint4(~0u, ~0u, ~0u, ~0u);
+            bool gat = false;
+            const Chg old = chg_b[v];  // own record, for the kept lanes
             uint64_t ne0 = 0, ne1 = 0, nm = 0;
             uint32_t neu = 0, new_ = 0;
             bool pre = !more;
@@ -306,7 +310,10 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_lat_sweep_kernel(
                             const uint32_t mlo = __builtin_amdgcn_readlane((uint32_t)m, j);
                             const uint32_t mhi = __builtin_amdgcn_readlane((uint32_t)(m >> 32), j);
                             w2[q] = w | (w << 16);
-                            if (((lane < 32 ? mlo : mhi) >> (lane & 31)) & 1u) x[q] = Lb[(uint64_t)u * 64 + lane];
+                            if (((lane < 32 ? mlo : mhi) >> (lane & 31)) & 1u) {
+                                x[q] = Lb[(uint64_t)u * 64 + lane];
+                                gat = true;
+                            }
                         }
                     }
                     if (!pre) {  // the next item's head, behind this batch's gathers
@@ -334,7 +341,15 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_lat_sweep_kernel(
                     nm = changed_lanes(chg_b, neu, t);
                 }
             }
-            const bool imp = best.x != own.x || best.y != own.y || best.z != own.z || best.w != own.w;
+            uint4 own = make_uint4(0u, 0u, 0u, 0u);
+            if (gat) {
+                own = Lb[(uint64_t)v * 64 + lane];
+                best.x = pk_min(best.x, own.x);
+                best.y = pk_min(best.y, own.y);
+                best.z = pk_min(best.z, own.z);
+                best.w = pk_min(best.w, own.w);
+            }
+            const bool imp = gat && (best.x != own.x || best.y != own.y || best.z != own.z || best.w != own.w);
             const uint64_t im = __ballot(imp);
             if (im) {
                 any_imp = true;
@@ -460,9 +475,12 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
             const uint32_t vn = more ? v0 + __builtin_ctzll(items) : v;
             if (more) items &= items - 1;
             float4 *pv = Pb + (uint64_t)v * 128 + 2 * lane;
-            const float4 o0 = pv[0], o1 = pv[1];
-            float best[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
-            uint32_t ib = 0;  // the lane's improved sources
+            // candidates; the own row is read only by the lanes with a tight,
+            // changed parent, beside their first gathers (2 KB an item a
+            // sweep for every lane otherwise)
+            float best[8] = {2.f, 2.f, 2.f, 2.f, 2.f, 2.f, 2.f, 2.f};
+            float4 o0 = make_float4(2.f, 2.f, 2.f, 2.f), o1 = o0;
+            bool own = false;
             uint64_t ne0 = 0, ne1 = 0;
             uint32_t neu = 0;
             float neeb = 0.f;
@@ -479,21 +497,39 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
                     }
                 }
                 const uint32_t n = e1 - c0 < 64 ? (uint32_t)(e1 - c0) : 64u;
-                for (uint32_t j0 = 0; j0 < n; j0 += FR_EBL) {
-                    uint32_t m[FR_EBL], u[FR_EBL];
-                    float eb[FR_EBL];
+                // groups of FR_MG in-edges: every lane's tight & changed mask of
+                // the group in one round of loads, then gathers along the edges
+                // some lane needs only (the masks of a group packed 4 a register)
+                for (uint32_t j0 = 0; j0 < n; j0 += FR_MG) {
+                    uint32_t mk[FR_MG / 4];
+                    uint32_t amask = 0;  // wave-uniform: the group's edges some lane needs
+                    {
+                        uint32_t mq[FR_MG];
 #pragma unroll
-                    for (int q = 0; q < FR_EBL; ++q) {
-                        m[q] = 0;
-                        u[q] = 0;
-                        eb[q] = 0.f;
-                        if (j0 + q < n) {
-                            u[q] = __builtin_amdgcn_readlane(eu, j0 + q);
-                            eb[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(eeb), j0 + q));
-                            m[q] = tb[(c0 + j0 + q) * 64] & (sbc[(uint64_t)u[q] * 64] | sbn[(uint64_t)u[q] * 64]);
+                        for (int q = 0; q < FR_MG; ++q) {
+                            mq[q] = 0;
+                            if (j0 + q < n) {
+                                const uint32_t u = __builtin_amdgcn_readlane(eu, j0 + q);
+                                mq[q] = tb[(c0 + j0 + q) * 64] & (sbc[(uint64_t)u * 64] | sbn[(uint64_t)u * 64]);
+                            }
+                        }
+#pragma unroll
+                        for (int q = 0; q < FR_MG; ++q) amask |= __ballot(mq[q] != 0) ? 1u << q : 0u;
+#pragma unroll
+                        for (int r = 0; r < FR_MG / 4; ++r)
+                            mk[r] = mq[4 * r] | mq[4 * r + 1] << 8 | mq[4 * r + 2] << 16 | mq[4 * r + 3] << 24;
+                    }
+                    if (!own) {
+                        uint32_t any = 0;
+#pragma unroll
+                        for (int r = 0; r < FR_MG / 4; ++r) any |= mk[r];
+                        if (any) {
+                            o0 = pv[0];
+                            o1 = pv[1];
+                            own = true;
                         }
                     }
-                    if (!pre) {  // the next item's head, behind this batch's loads
+                    if (!pre) {  // the next item's head, behind this group's loads
                         pre = true;
                         ne0 = in_ptr[vn];
                         ne1 = in_ptr[vn + 1];
@@ -503,27 +539,41 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
                             neeb = e.eb;
                         }
                     }
-                    float4 x0[FR_EBL], x1[FR_EBL];
+                    while (amask) {
+                        uint32_t m[FR_EBL];
+                        float eb[FR_EBL];
+                        float4 x0[FR_EBL], x1[FR_EBL];
 #pragma unroll
-                    for (int q = 0; q < FR_EBL; ++q) {
-                        x0[q] = x1[q] = make_float4(2.f, 2.f, 2.f, 2.f);
-                        if (m[q]) {
-                            x0[q] = Pb[(uint64_t)u[q] * 128 + 2 * lane];
-                            x1[q] = Pb[(uint64_t)u[q] * 128 + 2 * lane + 1];
-                        }
-                    }
+                        for (int q = 0; q < FR_EBL; ++q) {
+                            m[q] = 0;
+                            eb[q] = 0.f;
+                            x0[q] = x1[q] = make_float4(2.f, 2.f, 2.f, 2.f);
+                            if (amask) {
+                                const uint32_t jq = __builtin_ctz(amask);
+                                amask &= amask - 1;
+                                uint32_t w = mk[0];
 #pragma unroll
-                    for (int q = 0; q < FR_EBL; ++q) {
-                        const float xs[8] = {x0[q].x, x0[q].y, x0[q].z, x0[q].w, x1[q].x, x1[q].y, x1[q].z, x1[q].w};
-#pragma unroll
-                        for (int i = 0; i < 8; ++i)
-                            if (((m[q] >> i) & 1u) && xs[i] <= 1.0f) {  // u reached (not the 2.0 init)
-                                const float cnd = fold(xs[i], eb[q]);
-                                if (cnd < best[i]) {
-                                    best[i] = cnd;
-                                    ib |= 1u << i;
+                                for (int r = 1; r < FR_MG / 4; ++r) w = jq / 4 == (uint32_t)r ? mk[r] : w;
+                                m[q] = (w >> (8 * (jq % 4))) & 0xffu;
+                                const uint32_t u = __builtin_amdgcn_readlane(eu, j0 + jq);
+                                eb[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(eeb), j0 + jq));
+                                if (m[q]) {
+                                    x0[q] = Pb[(uint64_t)u * 128 + 2 * lane];
+                                    x1[q] = Pb[(uint64_t)u * 128 + 2 * lane + 1];
                                 }
                             }
+                        }
+#pragma unroll
+                        for (int q = 0; q < FR_EBL; ++q) {
+                            const float xs[8] = {x0[q].x, x0[q].y, x0[q].z, x0[q].w,
+                                                 x1[q].x, x1[q].y, x1[q].z, x1[q].w};
+#pragma unroll
+                            for (int i = 0; i < 8; ++i)
+                                if (((m[q] >> i) & 1u) && xs[i] <= 1.0f) {  // u reached (not the 2.0 init)
+                                    const float cnd = fold(xs[i], eb[q]);
+                                    best[i] = cnd < best[i] ? cnd : best[i];
+                                }
+                        }
                     }
                 }
             }
@@ -534,6 +584,15 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
                     const InEdge e = in_edge[ne0 + lane];
                     neu = e.u;
                     neeb = e.eb;
+                }
+            }
+            uint32_t ib = 0;  // the lane's improved sources
+            if (own) {
+                const float ov[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    if (best[i] < ov[i]) ib |= 1u << i;
+                    else best[i] = ov[i];
                 }
             }
             if (__ballot(ib != 0)) {
