@@ -1118,8 +1118,12 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
             uint64_t nb = 64;
             if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b)
                 nb = std::min<uint64_t>(nb, std::max<uint64_t>(1, (free_b / 2) / std::max<uint64_t>(bb, 1)));
+            // launches of equal size (C4: 196 blocks as 4 x 49, not 64+64+64+4 --
+            // a small last launch pays a full run of sweeps: 0.70 -> 0.68 s)
+            const uint64_t blocks_all = std::max<uint32_t>(1, (n + 511) / 512);
+            nb = (blocks_all + (blocks_all + nb - 1) / nb - 1) / ((blocks_all + nb - 1) / nb);
             if (const char *ev = std::getenv("SRT_SSSP_FR_NB")) nb = std::max<uint64_t>(1, std::atoll(ev));
-            nb = std::min<uint64_t>(nb, std::max<uint32_t>(1, (n + 511) / 512));
+            nb = std::min<uint64_t>(nb, blocks_all);
             p->fr_nb = (uint32_t)nb;
             int cus = 256;
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device);
