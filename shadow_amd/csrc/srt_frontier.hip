@@ -442,11 +442,12 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
     const uint64_t *__restrict__ in_ptr, const InEdge *__restrict__ in_edge, uint32_t V, uint32_t NB, uint64_t E,
     const uint8_t *__restrict__ tight, float *P, const uint8_t *__restrict__ sb_cur, uint8_t *sb_next,
     uint32_t *act, uint32_t *last, uint32_t t, bool sym, const uint64_t *__restrict__ row_ptr,
-    const uint32_t *__restrict__ col) {
+    const uint32_t *__restrict__ col, unsigned long long *cnt) {
     const int lane = threadIdx.x & 63;
     const uint32_t wave = blockIdx.x * FR_WAVES + (threadIdx.x >> 6), nwaves = gridDim.x * FR_WAVES;
     const uint32_t cpb = (V + 63) / 64, nchunks = cpb * NB;
     bool any_imp = false;
+    uint32_t c_items = 0, c_work = 0, c_imp = 0, c_gath = 0;  // SRT_FR_COUNT (measurement)
     for (uint32_t c = __builtin_amdgcn_readfirstlane(wave); c < nchunks; c += nwaves) {
         const uint32_t b = c / cpb, v0 = (c % cpb) * 64;
         uint32_t *act_b = act + (uint64_t)b * V;
@@ -557,6 +558,7 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
                                 m[q] = (w >> (8 * (jq % 4))) & 0xffu;
                                 const uint32_t u = __builtin_amdgcn_readlane(eu, j0 + jq);
                                 eb[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(eeb), j0 + jq));
+                                ++c_gath;
                                 if (m[q]) {
                                     x0[q] = Pb[(uint64_t)u * 128 + 2 * lane];
                                     x1[q] = Pb[(uint64_t)u * 128 + 2 * lane + 1];
@@ -587,6 +589,8 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
                 }
             }
             uint32_t ib = 0;  // the lane's improved sources
+            ++c_items;
+            c_work += __ballot(own) != 0;
             if (own) {
                 const float ov[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
 #pragma unroll
@@ -597,6 +601,7 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
             }
             if (__ballot(ib != 0)) {
                 any_imp = true;
+                ++c_imp;
                 if (ib) {
                     pv[0] = make_float4(best[0], best[1], best[2], best[3]);
                     pv[1] = make_float4(best[4], best[5], best[6], best[7]);
@@ -611,6 +616,12 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
             eu = neu;
             eeb = neeb;
         }
+    }
+    if (cnt && lane == 0) {
+        atomicAdd(&cnt[0], (unsigned long long)c_items);
+        atomicAdd(&cnt[1], (unsigned long long)c_work);
+        atomicAdd(&cnt[2], (unsigned long long)c_imp);
+        atomicAdd(&cnt[3], (unsigned long long)c_gath);
     }
     note_improved(last, t, any_imp, lane);
 }
@@ -879,6 +890,15 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
         t0 = t_end + 2;
         hipLaunchKernelGGL(fr_seed_kernel, seed_grid, dim3(256), 0, M, nullptr, p->d_fp, p->d_fsb, chg, p->d_fact,
                            p->d_fnodes, perm, V, q0, nsrc, t0, p->d_frow_ptr, p->d_fcol);
+        // SRT_FR_COUNT=1 (measurement): per loss sweep, items processed / with
+        // work / improved / edge gathers, printed after the phase
+        static unsigned long long *dcnt_s = nullptr;
+        unsigned long long *dcnt = nullptr;
+        if (std::getenv("SRT_FR_COUNT")) {
+            if (!dcnt_s) (void)hipMalloc(&dcnt_s, 4 * 256 * 8);
+            dcnt = dcnt_s;
+            (void)hipMemsetAsync(dcnt, 0, 4 * 256 * 8, M);
+        }
         st = run_phase(p, t0, chunk_loss, [&](uint32_t t) {
             // sweep t reads the bits of sweep t - 1 (slot (t - t0 - 1) & 1; the
             // seeds are slot 0) and writes slot (t - t0) & 1, cleared first
@@ -886,10 +906,18 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
             (void)hipMemsetAsync(nxt, 0, sbytes, M);
             hipLaunchKernelGGL(fr_loss_sweep_kernel, sgrid, sblk, 0, M, p->d_in_ptr, p->d_in_edge, V, NB, E,
                                p->d_ftight, p->d_fp, cur, nxt, p->d_fact, p->d_fimp, t, p->fr_symg, p->d_frow_ptr,
-                               p->d_fcol);
+                               p->d_fcol, dcnt ? dcnt + 4 * std::min<uint32_t>(t - t0, 255) : nullptr);
         }, &t_end, &nsw, err);
         if (st != SRT_OK) return st;
         p->fr_loss_sweeps += nsw;
+        if (dcnt) {
+            unsigned long long h[4 * 256];
+            (void)hipMemcpy(h, dcnt, sizeof h, hipMemcpyDeviceToHost);
+            std::fprintf(stderr, "[srt] loss sweeps of launch %u (items/work/improved/gathers):", li);
+            for (uint32_t k = 1; k <= std::min<uint32_t>(t_end - t0, 255); ++k)
+                std::fprintf(stderr, " %llu/%llu/%llu/%llu", h[4 * k], h[4 * k + 1], h[4 * k + 2], h[4 * k + 3]);
+            std::fprintf(stderr, "\n");
+        }
         p->sssp_sweeps += nsw;
         chunk_loss = std::max<uint32_t>(nsw + 1, 4);
         p->fr_t = t_end + 2;
