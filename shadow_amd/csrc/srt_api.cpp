@@ -600,6 +600,7 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_tpk2);
     hipFree(p->d_tsort_tmp);
     hipFree(p->d_tcls);
+    hipFree(p->d_tcw);
     hipFree(p->d_ev_bad);
     hipFree(p->d_tccnt);
     hipFree(p->d_tscan_tmp);

@@ -275,6 +275,9 @@ struct srt_plan {
     // in d_tpk2, entries (1-e) bits << 32 | other endpoint; class w of vertex x
     // is [tcls[x*16 + w-1], tcls[x*16 + w]) (in-rows: offset V*16 + 1)
     bool t_level = false;            // the last run built the class CSRs (and folds by levels)
+    uint32_t t_q = 1;                // level width of the fold, units of g (1: exact levels; > 1: quantized)
+    uint32_t *d_tcw = nullptr;       // quantized fold: each class entry's exact weight (out, then in), t_cap each
+    uint64_t tcw_cap = 0;            // d_tcw entries
     uint32_t *d_tcls = nullptr;      // 2 * (V*16 + 1) class offsets
     uint32_t *d_tccnt = nullptr;     // 2 * (V*16 + 1) class counts / fill cursors
     uint64_t tcls_cap = 0;           // entries of d_tcls and d_tccnt

@@ -203,7 +203,7 @@ __global__ __launch_bounds__(256) void tight_rows_kernel(const K *__restrict__ D
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    uint64_t mw = 0, tot = 0;
+    uint64_t mw = 0, tot = 0, mnw = ~0ull;
     auto test = [&](uint32_t u, const K *Du, uint64_t k, uint64_t e) -> bool {
         if (k >= e) return false;
         const uint32_t v = col[k];
@@ -235,7 +235,10 @@ __global__ __launch_bounds__(256) void tight_rows_kernel(const K *__restrict__ D
                 const uint64_t w = KeyLat<K>::lat(d[q]);
                 const bool f = v[q] != u && !KeyLat<K>::inf(d[q]) && w * g == l[q];
                 const uint64_t m = __ballot(f);
-                if (f) mw = w > mw ? w : mw;
+                if (f) {
+                    mw = w > mw ? w : mw;
+                    mnw = w < mnw ? w : mnw;
+                }
                 if (c0 + q < TR_CH && lane == 0) bal[wv][c0 + q] = m;
                 cnt += (uint32_t)__popcll(m);
             }
@@ -261,10 +264,15 @@ __global__ __launch_bounds__(256) void tight_rows_kernel(const K *__restrict__ D
     for (int off = 32; off > 0; off >>= 1) {
         const uint64_t o = __shfl_xor(mw, off);
         mw = o > mw ? o : mw;
+        const uint64_t o2 = __shfl_xor(mnw, off);
+        mnw = o2 < mnw ? o2 : mnw;
     }
-    // tot is uniform per wave (ballot counts)
+    // tot is uniform per wave (ballot counts); total[1]: max of ~min w (zeroed by the caller)
     if (lane == 0 && mw) atomicMax(maxw, (unsigned long long)mw);
-    if (lane == 0 && tot) atomicAdd(total, (unsigned long long)tot);
+    if (lane == 0 && tot) {
+        atomicAdd(total, (unsigned long long)tot);
+        atomicMax(total + 1, (unsigned long long)~mnw);
+    }
 }
 
 // Per-row counts of a tight-edge list (v = ~0: padding): rows by target v
@@ -796,42 +804,59 @@ __global__ __launch_bounds__(LOSS_NT) void tight_loss_kernel(
 // class w of vertex x.  Applies when every tight edge has w <= WC, every
 // closure latency is < NBK units (proof bound lmax), V < 65536 (u16 member
 // lists) and the row fits LDS: lat u16 + loss f32 + members u16 (8 B/vertex).
-constexpr uint32_t WC = 15;   // exact weight classes
-constexpr uint32_t CLS = 16;  // offsets per vertex (classes 1..WC, then the end)
+constexpr uint32_t WC = 31;   // weight classes (exact weights, or quantized: floor(w / q))
+constexpr uint32_t CLS = 32;  // offsets per vertex (classes 1..WC, then the end)
+
+// class of a tight weight w: w itself (q = 1), else floor(w / q) (quantized
+// levels, q = the smallest tight weight)
+__device__ __forceinline__ uint32_t wclass(uint32_t w, uint32_t q) { return q == 1 ? w : w / q; }
 
 __global__ void tcls_count_kernel(const uint4 *__restrict__ list, uint64_t slots, uint32_t *__restrict__ cnt,
-                                  uint64_t vc1) {
+                                  uint64_t vc1, uint32_t q) {
     for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < slots; e += (uint64_t)gridDim.x * blockDim.x) {
         const uint4 r = list[e];
         if (r.x == ~0u) continue;
-        atomicAdd(&cnt[(uint64_t)r.y * CLS + r.z - 1], 1u);        // out-row of u
-        atomicAdd(&cnt[vc1 + (uint64_t)r.x * CLS + r.z - 1], 1u);  // in-row of v
+        const uint32_t c = wclass(r.z, q);
+        atomicAdd(&cnt[(uint64_t)r.y * CLS + c - 1], 1u);        // out-row of u
+        atomicAdd(&cnt[vc1 + (uint64_t)r.x * CLS + c - 1], 1u);  // in-row of v
     }
 }
 
 __global__ void tcls_fill_kernel(const uint4 *__restrict__ list, uint64_t slots, const uint32_t *__restrict__ off,
                                  uint32_t *__restrict__ cur, uint64_t *__restrict__ ce_out,
-                                 uint64_t *__restrict__ ce_in, uint64_t vc1) {
+                                 uint64_t *__restrict__ ce_in, uint64_t vc1, uint32_t q, uint32_t *__restrict__ cw,
+                                 uint64_t cw_in) {
     for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < slots; e += (uint64_t)gridDim.x * blockDim.x) {
         const uint4 r = list[e];
         if (r.x == ~0u) continue;
-        const uint64_t a = (uint64_t)r.y * CLS + r.z - 1, b = vc1 + (uint64_t)r.x * CLS + r.z - 1;
-        ce_out[off[a] + atomicAdd(&cur[a], 1u)] = ((uint64_t)r.w << 32) | r.x;
-        ce_in[off[b] + atomicAdd(&cur[b], 1u)] = ((uint64_t)r.w << 32) | r.y;
+        const uint32_t c = wclass(r.z, q);
+        const uint64_t a = (uint64_t)r.y * CLS + c - 1, b = vc1 + (uint64_t)r.x * CLS + c - 1;
+        const uint64_t ia = off[a] + atomicAdd(&cur[a], 1u), ib = off[b] + atomicAdd(&cur[b], 1u);
+        ce_out[ia] = ((uint64_t)r.w << 32) | r.x;
+        ce_in[ib] = ((uint64_t)r.w << 32) | r.y;
+        if (cw) {  // quantized classes: the exact weight beside each entry
+            cw[ia] = r.z;
+            cw[cw_in + ib] = r.z;
+        }
     }
 }
 
 // One workgroup per table row, 16 waves.  LDS: hist (level ends), lat u16
 // (0xffff: unreachable), loss f32 bits, members u16 (the vertices in level
 // order, counting sort).  Output as tight_loss_kernel.
-template <int LPT, int UNR>
+// QUANT (level width qw > 1, see level_q): lrow holds floor(L / qw); a class-c
+// edge's tail lies in level l - c or l - c - 1, and a candidate is taken only
+// when L(s,u) + w == L(s,v) exactly (the closure row's exact values, read from
+// D; the class entries' weights from cw).  The output latencies come from D.
+template <int LPT, int UNR, bool QUANT>
 __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
     const void *__restrict__ D, int key_type, uint32_t Vp, uint32_t V, const uint32_t *__restrict__ nodes, uint32_t n,
     uint32_t row0, uint32_t row1, const uint32_t *__restrict__ tcls, uint64_t vc1,
     const uint64_t *__restrict__ ce_out, const uint64_t *__restrict__ ce_in, uint64_t g,
     const uint64_t *__restrict__ sl_lat, const float *__restrict__ sl_loss, uint64_t *__restrict__ out_lat,
     float *__restrict__ out_loss, unsigned long long *stats, const uint32_t *__restrict__ row_list,
-    void *__restrict__ out32, float *__restrict__ out32_loss, bool stage16) {
+    void *__restrict__ out32, float *__restrict__ out32_loss, bool stage16, uint32_t qw,
+    const uint32_t *__restrict__ cw, uint64_t cw_in) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ uint64_t red[16];
     __shared__ unsigned long long red_min[16], red_cnt[16];
@@ -860,7 +885,7 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
         for (uint32_t v = tid; v < V; v += nt) {
             bool inf;
             const uint64_t l64 = closure_lat(D, (uint64_t)s * Vp + v, key_type, inf);
-            const uint16_t l = inf ? LINF : v == s ? (uint16_t)0 : (uint16_t)l64;
+            const uint16_t l = inf ? LINF : v == s ? (uint16_t)0 : (uint16_t)(QUANT ? l64 / qw : l64);
             lrow[v] = l;
             prow[v] = v == s ? 0u : FINF;  // petgraph's zero score (0 ns, 0.0) at s
             if (l != LINF && l > mx) mx = l;
@@ -969,7 +994,9 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
                 for (uint32_t w = 1; w <= WC; ++w) {
                     uint32_t items = 0;
                     if (w <= l) {
-                        const uint32_t j = l - w, nj = hist[j] - (j ? hist[j - 1] : 0u);
+                        // the tails' levels: l - w (and, quantized, l - w - 1)
+                        const uint32_t j = l - w, jl = QUANT && j ? j - 1 : j;
+                        const uint32_t nj = hist[j] - (jl ? hist[jl - 1] : 0u);
                         if (nj <= cnt_l) pm |= 1u << w;
                         items = nj < cnt_l ? nj : cnt_l;
                     }
@@ -985,9 +1012,9 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
             auto item = [&](uint32_t t, uint32_t &w, uint32_t &x, uint32_t &e0, uint32_t &e1) {
                 w = 1;
                 while (t >= plan_end[w]) ++w;
-                const uint32_t m = t - (w > 1 ? plan_end[w - 1] : 0u), j = l - w;
+                const uint32_t m = t - (w > 1 ? plan_end[w - 1] : 0u), j = l - w, jl = QUANT && j ? j - 1 : j;
                 const bool push = (pm >> w) & 1u;
-                x = mem[(push ? (j ? hist[j - 1] : 0u) : lo) + m];
+                x = mem[(push ? (jl ? hist[jl - 1] : 0u) : lo) + m];
                 const uint32_t *cl = push ? cls_out : cls_in;
                 e0 = cl[(uint64_t)x * CLS + w - 1];
                 e1 = cl[(uint64_t)x * CLS + w];
@@ -1003,6 +1030,9 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
                 // pull: x in N_l, its class-w in-edges u -> x, u in N_j
                 const uint16_t want = (uint16_t)(push ? l : j);
                 const float onem = push ? 1.0f - __uint_as_float(prow[x]) : 0.0f;
+                bool xinf;
+                const uint64_t Lx = QUANT ? closure_lat(D, (uint64_t)s * Vp + x, key_type, xinf) : 0;
+                const uint32_t *cwp = QUANT ? cw + (push ? 0 : cw_in) : nullptr;
                 for (uint32_t b = e0; b < e1; b += UNR * LPT) {
                     uint64_t wd[UNR];
 #pragma unroll
@@ -1017,9 +1047,25 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
                     uint16_t lo_[UNR];
 #pragma unroll
                     for (int q = 0; q < UNR; ++q) lo_[q] = lrow[o[q]];
+                    bool hit[UNR];
 #pragma unroll
                     for (int q = 0; q < UNR; ++q) {
-                        if (ok[q] && lo_[q] == want) {
+                        if (!QUANT) {
+                            hit[q] = ok[q] && lo_[q] == want;
+                        } else {
+                            // the tail's level (j or j - 1) or the head's (l), then exact
+                            hit[q] = ok[q] && (push ? lo_[q] == want : lo_[q] == want || lo_[q] + 1 == want);
+                            if (hit[q]) {
+                                bool oinf;
+                                const uint64_t Lo = closure_lat(D, (uint64_t)s * Vp + o[q], key_type, oinf);
+                                const uint64_t wq = cwp[b + sub + q * LPT];
+                                hit[q] = push ? Lx + wq == Lo : Lo + wq == Lx;
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int q = 0; q < UNR; ++q) {
+                        if (hit[q]) {
                             const float r = __uint_as_float((uint32_t)(wd[q] >> 32));
                             if (push) {
                                 const float c = 1.0f - __fmul_rn(onem, r);
@@ -1054,7 +1100,8 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
                     latv = ~0ull;
                     lossv = 1.0f;
                 } else {
-                    latv = (uint64_t)l * g;
+                    bool vinf;
+                    latv = (QUANT ? closure_lat(D, (uint64_t)s * Vp + v, key_type, vinf) : (uint64_t)l) * g;
                     lossv = __uint_as_float(prow[v]);
                 }
             }
@@ -1273,24 +1320,46 @@ static srt_status ensure_tlist(srt_plan *p, uint64_t cap, uint64_t need, srt_err
 
 // The level fold applies (see level_loss_kernel): every tight weight <= WC,
 // every closure latency < NBK units, u16 member lists, the row in LDS.
-bool level_ok(const srt_plan *p, uint64_t maxw) {
+// Returns the fold's level width q in units of g: 1 (exact levels) when every
+// tight weight is its own class (w <= WC) and every closure latency < NBK;
+// else, when the smallest tight weight minw is known (one-GPU tight pass),
+// quantized levels floor(L / q) with q = minw: a tight edge then climbs at
+// least one level, its class floor(w / q) <= WC places its tail in one of two
+// levels, and an exact test L(s,u) + w == L(s,v) on the closure row picks the
+// candidates (C3 with ns latencies: g = 1 ns, tight weights 1.0-16 ms).  0: no.
+uint32_t level_q(const srt_plan *p, uint64_t maxw, uint64_t minw) {
     if (const char *e = std::getenv("SRT_LOSS_LEVEL"))  // A/B and parity tests of the scan folds
-        if (std::atoi(e) == 0) return false;
+        if (std::atoi(e) == 0) return 0;
     const size_t lds = HIST_BYTES + (((size_t)p->V * 2 + 15) & ~(size_t)15) + (size_t)p->V * 4 + (size_t)p->V * 2;
-    return p->kp.lat32 && maxw >= 1 && maxw <= WC && p->kp.lmax < (uint64_t)NBK && p->V < 65536 &&
-           lds + 16 <= LDS_BUDGET - 4096;
+    if (!(p->kp.lat32 && p->V < 65536 && lds + 16 <= LDS_BUDGET - 4096 && maxw >= 1)) return 0;
+    if (maxw <= WC && p->kp.lmax < (uint64_t)NBK) return 1;
+    if (minw >= 2 && minw <= maxw && maxw / minw <= WC && p->kp.lmax / minw < (uint64_t)NBK - 1 &&
+        minw < (1ull << 32) && !std::getenv("SRT_LOSS_NOQ"))
+        return (uint32_t)minw;
+    return 0;
 }
 
 // Rows of the tight-edge list (slots records, v = ~0: padding, p->t_edges
 // real ones): the class CSRs when the level fold applies (no sort), else the
 // packed push (rows by source) or pull rows sorted by w.
-srt_status build_tight_rows(srt_plan *p, uint64_t slots, uint32_t ubits, uint64_t maxw, srt_err *err) {
+srt_status build_tight_rows(srt_plan *p, uint64_t slots, uint32_t ubits, uint64_t maxw, srt_err *err,
+                            uint64_t minw = 0) {
     hipStream_t M = p->stream;
     const uint32_t V = p->V;
     srt_status st;
     const uint32_t lblocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, (slots + 255) / 256));
-    p->t_level = level_ok(p, maxw);
+    p->t_q = level_q(p, maxw, minw);
+    p->t_level = p->t_q != 0;
     if (p->t_level) {
+        const uint32_t q = p->t_q;
+        if (q > 1 && p->tcw_cap < 2 * p->t_cap) {  // the exact weights beside the class entries
+            (void)hipFree(p->d_tcw);
+            p->d_tcw = nullptr;
+            p->tcw_cap = 0;
+            const hipError_t e = hipMalloc(&p->d_tcw, 2 * p->t_cap * sizeof(uint32_t));
+            if (e != hipSuccess) return fail(err, e, "hipMalloc(class weights)");
+            p->tcw_cap = 2 * p->t_cap;
+        }
         const uint64_t vc1 = (uint64_t)V * CLS + 1;
         uint64_t c1 = p->tcls_cap, c2 = p->tcls_cap;
         if ((st = grow(&p->d_tcls, &c1, 2 * vc1, err, "hipMalloc(class offsets)")) != SRT_OK ||
@@ -1298,7 +1367,7 @@ srt_status build_tight_rows(srt_plan *p, uint64_t slots, uint32_t ubits, uint64_
             return st;
         p->tcls_cap = std::min(c1, c2);
         (void)hipMemsetAsync(p->d_tccnt, 0, 2 * vc1 * 4, M);
-        hipLaunchKernelGGL(tcls_count_kernel, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tccnt, vc1);
+        hipLaunchKernelGGL(tcls_count_kernel, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tccnt, vc1, q);
         size_t need = 0;
         hipError_t e = rocprim::exclusive_scan(nullptr, need, p->d_tccnt, p->d_tcls, 0u, (size_t)vc1,
                                                rocprim::plus<uint32_t>(), M);
@@ -1316,7 +1385,7 @@ srt_status build_tight_rows(srt_plan *p, uint64_t slots, uint32_t ubits, uint64_
         }
         (void)hipMemsetAsync(p->d_tccnt, 0, 2 * vc1 * 4, M);
         hipLaunchKernelGGL(tcls_fill_kernel, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tcls,
-                           p->d_tccnt, p->d_tpk, p->d_tpk2, vc1);
+                           p->d_tccnt, p->d_tpk, p->d_tpk2, vc1, q, q > 1 ? p->d_tcw : nullptr, p->t_cap);
         p->t_push = false;
         return SRT_OK;
     }
@@ -1339,13 +1408,14 @@ srt_status launch_level(srt_plan *p, unsigned long long *d_stats, const RowJob &
     const uint32_t nt = V >= 2048 ? LOSS_NT : 256;
     const int per_cu = std::max(1, std::min(2048 / (int)nt, (int)std::max<size_t>(1, (160 * 1024) / (lds + 2048))));
     const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(rows, (uint32_t)(cu_count(p->device) * per_cu)));
-    auto kern = level_loss_kernel<LPT, 8>;  // 8 edge loads in flight a lane (C3: 7.0 -> 6.7 ms vs 4)
+    // 8 edge loads in flight a lane (C3: 7.0 -> 6.7 ms vs 4)
+    auto kern = p->t_q > 1 ? level_loss_kernel<LPT, 8, true> : level_loss_kernel<LPT, 8, false>;
     (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(LDS_BUDGET - 4096));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, p->stream, (const void *)p->d_D, p->key_type, p->Vp, V,
                        p->d_nodes, p->n, job.list ? 0u : job.range ? job.r0 : p->row0,
                        job.list ? job.count : job.range ? job.r1 : p->row1, p->d_tcls, (uint64_t)V * CLS + 1,
                        p->d_tpk, p->d_tpk2, p->kp.g, p->d_sl_lat, p->d_sl_loss, p->d_out_lat, p->d_out_loss, d_stats,
-                       job.list, job.out32, job.out32_loss, p->stage16);
+                       job.list, job.out32, job.out32_loss, p->stage16, p->t_q, p->d_tcw, p->t_cap);
     return SRT_OK;
 }
 
@@ -1376,6 +1446,7 @@ srt_status tight_csr_push_t(srt_plan *p, unsigned long long *d_stats, bool *done
                            p->d_tinfo);
         (void)hipMemcpyAsync(p->h_tcount, p->d_tinfo, sizeof(uint64_t), hipMemcpyDeviceToHost, M);
         (void)hipMemcpyAsync(p->h_tcount + 1, p->d_tmaxw, sizeof(uint64_t), hipMemcpyDeviceToHost, M);
+        (void)hipMemcpyAsync(p->h_tcount + 2, p->d_tinfo + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, M);
         return hipStreamSynchronize(M);
     };
     if (!p->d_tlist) {
@@ -1388,8 +1459,12 @@ srt_status tight_csr_push_t(srt_plan *p, unsigned long long *d_stats, bool *done
     hipError_t e = rows();
     if (e != hipSuccess) return fail(err, e, "tight-edge list");
     const uint64_t total = p->h_tcount[0], maxw = p->h_tcount[1];
+    const uint64_t minw = total ? ~p->h_tcount[2] : 0;  // the kernel kept max(~w)
     const uint32_t ubits = (uint32_t)std::max(1, bits_of(V ? V - 1 : 0));
-    if (!(p->kp.lat32 && ubits + bits_of(maxw) <= 32 && total < (1ull << 32))) return SRT_OK;
+    // the level fold's class CSRs need no packed (u, w) word: wide weights
+    // (ns units) still fold by levels when level_q allows
+    const bool packable = p->kp.lat32 && ubits + bits_of(maxw) <= 32 && total < (1ull << 32);
+    if (!packable && !(total && level_q(p, maxw, minw))) return SRT_OK;
     p->t_edges = total;
     if ((st = ensure_edge_arrays(p, err)) != SRT_OK) return st;
     const uint64_t C = std::max<uint64_t>(total, 1);
@@ -1397,8 +1472,12 @@ srt_status tight_csr_push_t(srt_plan *p, unsigned long long *d_stats, bool *done
         if ((st = ensure_tlist(p, C + C / 4 + 64, C, err)) != SRT_OK) return st;
         if ((e = rows()) != hipSuccess) return fail(err, e, "tight-edge list");
     }
-    if ((st = build_tight_rows(p, total, ubits, maxw, err)) != SRT_OK) return st;
-    p->t_packed = true;
+    if ((st = build_tight_rows(p, total, ubits, maxw, err, minw)) != SRT_OK) return st;
+    if (std::getenv("SRT_TRACE"))
+        std::fprintf(stderr, "[srt] tight edges %llu, w in [%llu, %llu] units, lmax %llu: %s fold, level width %u\n",
+                     (unsigned long long)total, (unsigned long long)minw, (unsigned long long)maxw,
+                     (unsigned long long)p->kp.lmax, p->t_level ? "level" : "scan", p->t_q);
+    p->t_packed = packable;
     *done = true;
     return SRT_OK;
 }
@@ -1416,7 +1495,7 @@ srt_status tight_csr_t(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
         (st = grow(&p->d_tmaxw, &cap_mw, 1, err, "hipMalloc(tight max)")) != SRT_OK)
         return st;
     if (!p->h_tcount) {
-        const hipError_t e = hipHostMalloc((void **)&p->h_tcount, 2 * sizeof(uint64_t), 0);
+        const hipError_t e = hipHostMalloc((void **)&p->h_tcount, 4 * sizeof(uint64_t), 0);
         if (e != hipSuccess) return fail(err, e, "hipHostMalloc");
     }
     p->t_push = false;

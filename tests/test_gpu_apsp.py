@@ -358,10 +358,11 @@ def test_level_fold_equals_scan_fold(monkeypatch, seed, directed):
         assert np.array_equal(t.packet_loss.view(np.uint32), eloss.view(np.uint32)), f"level={level}"
 
 
-@pytest.mark.parametrize("lat_hi,level", [(15, 1), (40, 0)])
+@pytest.mark.parametrize("lat_hi,level", [(31, 1), (40, 0)])
 def test_level_fold_weight_class_limit(lat_hi, level):
-    """Tight edges heavier than the 15 exact weight classes send the build to
-    the scan fold; at the limit it stays on the level fold; bits as the oracle."""
+    """Tight edges heavier than the 31 weight classes (and a smallest tight
+    weight of 1 unit: no quantized levels) send the build to the scan fold; at
+    the limit it stays on the level fold; bits as the oracle."""
     n = 140
     src, dst, lat, loss = synth.random_graph(n, 77, p_edge=0.08, directed=False, lat_range_ns=(1, lat_hi),
                                              loss_max=0.05)
@@ -440,3 +441,27 @@ def test_loss_checked_on_device_in_pieces():
     nodes = np.arange(0, n, 7, dtype=np.uint32)
     t = g.compute_shortest_paths(nodes)
     assert t.latency_ns.shape == (len(nodes), len(nodes)) and (t.latency_ns > 0).all()
+
+
+@pytest.mark.parametrize("seed", range(3))
+@pytest.mark.parametrize("directed", [False, True])
+@pytest.mark.parametrize("lat_range", [(100, 1400), (1000, 1003)])
+def test_quantized_level_fold(monkeypatch, seed, directed, lat_range):
+    """Tight weights above the 15 exact classes but within 15x of the smallest
+    one (ns-resolution latencies: C3ns): the level fold on quantized levels
+    floor(L / minw) with the exact test L(s,u) + w == L(s,v) (level_q), bit for
+    bit the oracle and the scan fold (SRT_LOSS_NOQ=1); (1000, 1003): heavy
+    ties at one quantized level."""
+    n = 120 + 31 * seed
+    src, dst, lat, loss = synth.random_graph(n, 500 + seed, p_edge=0.15, directed=directed, lat_range_ns=lat_range,
+                                             loss_max=0.05)
+    nodes = np.random.default_rng(seed).permutation(n).astype(np.uint32)
+    elat, eloss = O.compute_shortest_paths(O.Graph(directed, np.arange(n), src, dst, lat, loss), nodes)
+    for noq in ("0", "1"):
+        if noq == "1":
+            monkeypatch.setenv("SRT_LOSS_NOQ", "1")
+        g = NetworkGraph.from_edges(n, src, dst, lat, loss, directed=directed)
+        plan, t = _plan_table(g, nodes)
+        assert plan.timing()["loss_fold"] == (1 if noq == "0" else 0), noq
+        assert np.array_equal(t.latency_ns, elat)
+        assert np.array_equal(t.packet_loss.view(np.uint32), eloss.view(np.uint32)), f"noq={noq}"
