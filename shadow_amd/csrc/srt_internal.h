@@ -276,6 +276,7 @@ struct srt_plan {
     // is [tcls[x*16 + w-1], tcls[x*16 + w]) (in-rows: offset V*16 + 1)
     bool t_level = false;            // the last run built the class CSRs (and folds by levels)
     uint32_t t_q = 1;                // level width of the fold, units of g (1: exact levels; > 1: quantized)
+    uint32_t t_cls = 16;             // class offsets per vertex of the level fold's CSRs (16 or 32)
     uint32_t *d_tcw = nullptr;       // quantized fold: each class entry's exact weight (out, then in), t_cap each
     uint64_t tcw_cap = 0;            // d_tcw entries
     uint32_t *d_tcls = nullptr;      // 2 * (V*16 + 1) class offsets

@@ -800,37 +800,38 @@ __global__ __launch_bounds__(LOSS_NT) void tight_loss_kernel(
 // level), so the result is the same bits as the single-direction scans.
 //
 // Class CSRs (built from the tight-edge list, no sort): out-rows and in-rows
-// grouped by exact weight w = 1..WC; tcls[x*CLS + w-1] .. tcls[x*CLS + w] is
+// grouped by exact weight w = 1..WC; tcls[x*cls + w-1] .. tcls[x*cls + w] is
 // class w of vertex x.  Applies when every tight edge has w <= WC, every
 // closure latency is < NBK units (proof bound lmax), V < 65536 (u16 member
 // lists) and the row fits LDS: lat u16 + loss f32 + members u16 (8 B/vertex).
-constexpr uint32_t WC = 31;   // weight classes (exact weights, or quantized: floor(w / q))
-constexpr uint32_t CLS = 32;  // offsets per vertex (classes 1..WC, then the end)
+constexpr uint32_t WC = 31;   // weight classes at most (exact weights, or quantized: floor(w / q))
+// offsets per vertex (p->t_cls: classes 1..cls-1, then the end): 16 when
+// every class is <= 15 (C3: half the offset arrays of 32, 6.8 vs 7.0 ms), else 32
 
 // class of a tight weight w: w itself (q = 1), else floor(w / q) (quantized
 // levels, q = the smallest tight weight)
 __device__ __forceinline__ uint32_t wclass(uint32_t w, uint32_t q) { return q == 1 ? w : w / q; }
 
 __global__ void tcls_count_kernel(const uint4 *__restrict__ list, uint64_t slots, uint32_t *__restrict__ cnt,
-                                  uint64_t vc1, uint32_t q) {
+                                  uint64_t vc1, uint32_t q, uint32_t cls) {
     for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < slots; e += (uint64_t)gridDim.x * blockDim.x) {
         const uint4 r = list[e];
         if (r.x == ~0u) continue;
         const uint32_t c = wclass(r.z, q);
-        atomicAdd(&cnt[(uint64_t)r.y * CLS + c - 1], 1u);        // out-row of u
-        atomicAdd(&cnt[vc1 + (uint64_t)r.x * CLS + c - 1], 1u);  // in-row of v
+        atomicAdd(&cnt[(uint64_t)r.y * cls + c - 1], 1u);        // out-row of u
+        atomicAdd(&cnt[vc1 + (uint64_t)r.x * cls + c - 1], 1u);  // in-row of v
     }
 }
 
 __global__ void tcls_fill_kernel(const uint4 *__restrict__ list, uint64_t slots, const uint32_t *__restrict__ off,
                                  uint32_t *__restrict__ cur, uint64_t *__restrict__ ce_out,
                                  uint64_t *__restrict__ ce_in, uint64_t vc1, uint32_t q, uint32_t *__restrict__ cw,
-                                 uint64_t cw_in) {
+                                 uint64_t cw_in, uint32_t cls) {
     for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < slots; e += (uint64_t)gridDim.x * blockDim.x) {
         const uint4 r = list[e];
         if (r.x == ~0u) continue;
         const uint32_t c = wclass(r.z, q);
-        const uint64_t a = (uint64_t)r.y * CLS + c - 1, b = vc1 + (uint64_t)r.x * CLS + c - 1;
+        const uint64_t a = (uint64_t)r.y * cls + c - 1, b = vc1 + (uint64_t)r.x * cls + c - 1;
         const uint64_t ia = off[a] + atomicAdd(&cur[a], 1u), ib = off[b] + atomicAdd(&cur[b], 1u);
         ce_out[ia] = ((uint64_t)r.w << 32) | r.x;
         ce_in[ib] = ((uint64_t)r.w << 32) | r.y;
@@ -848,7 +849,7 @@ __global__ void tcls_fill_kernel(const uint4 *__restrict__ list, uint64_t slots,
 // edge's tail lies in level l - c or l - c - 1, and a candidate is taken only
 // when L(s,u) + w == L(s,v) exactly (the closure row's exact values, read from
 // D; the class entries' weights from cw).  The output latencies come from D.
-template <int LPT, int UNR, bool QUANT>
+template <int LPT, int UNR, bool QUANT, uint32_t CLSN>
 __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
     const void *__restrict__ D, int key_type, uint32_t Vp, uint32_t V, const uint32_t *__restrict__ nodes, uint32_t n,
     uint32_t row0, uint32_t row1, const uint32_t *__restrict__ tcls, uint64_t vc1,
@@ -860,7 +861,8 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ uint64_t red[16];
     __shared__ unsigned long long red_min[16], red_cnt[16];
-    __shared__ uint32_t plan_end[WC + 1];  // inclusive prefix of the class item counts
+    constexpr uint32_t WCN = CLSN - 1;
+    __shared__ uint32_t plan_end[WCN + 1];  // inclusive prefix of the class item counts
     __shared__ uint32_t wcnt[16][32];      // few-level sort: per-wave level counts, then bases
     __shared__ uint32_t plan_push;         // bit w: class w pushes from N_{l-w}
     uint32_t *hist = reinterpret_cast<uint32_t *>(smem);
@@ -991,7 +993,7 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
             if (!cnt_l) continue;  // uniform
             if (tid == 0) {
                 uint32_t run = 0, pm = 0;
-                for (uint32_t w = 1; w <= WC; ++w) {
+                for (uint32_t w = 1; w <= WCN; ++w) {
                     uint32_t items = 0;
                     if (w <= l) {
                         // the tails' levels: l - w (and, quantized, l - w - 1)
@@ -1006,7 +1008,7 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
                 plan_push = pm;
             }
             __syncthreads();
-            const uint32_t T = plan_end[WC], pm = plan_push;
+            const uint32_t T = plan_end[WCN], pm = plan_push;
             // item t -> (class w, member x, its edge range); the next item's
             // range is loaded while the current one is walked
             auto item = [&](uint32_t t, uint32_t &w, uint32_t &x, uint32_t &e0, uint32_t &e1) {
@@ -1016,8 +1018,8 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
                 const bool push = (pm >> w) & 1u;
                 x = mem[(push ? (jl ? hist[jl - 1] : 0u) : lo) + m];
                 const uint32_t *cl = push ? cls_out : cls_in;
-                e0 = cl[(uint64_t)x * CLS + w - 1];
-                e1 = cl[(uint64_t)x * CLS + w];
+                e0 = cl[(uint64_t)x * CLSN + w - 1];
+                e1 = cl[(uint64_t)x * CLSN + w];
             };
             uint32_t nw_ = 1, nx = 0, ne0 = 0, ne1 = 0;
             if (grp < T) item(grp, nw_, nx, ne0, ne1);
@@ -1360,14 +1362,18 @@ srt_status build_tight_rows(srt_plan *p, uint64_t slots, uint32_t ubits, uint64_
             if (e != hipSuccess) return fail(err, e, "hipMalloc(class weights)");
             p->tcw_cap = 2 * p->t_cap;
         }
-        const uint64_t vc1 = (uint64_t)V * CLS + 1;
+        const uint32_t mc = q == 1 ? (uint32_t)maxw : (uint32_t)(maxw / q);  // the largest class
+        p->t_cls = mc < 16 ? 16 : 32;
+        const uint32_t cls = p->t_cls;
+        const uint64_t vc1 = (uint64_t)V * cls + 1;
         uint64_t c1 = p->tcls_cap, c2 = p->tcls_cap;
         if ((st = grow(&p->d_tcls, &c1, 2 * vc1, err, "hipMalloc(class offsets)")) != SRT_OK ||
             (st = grow(&p->d_tccnt, &c2, 2 * vc1, err, "hipMalloc(class counts)")) != SRT_OK)
             return st;
         p->tcls_cap = std::min(c1, c2);
         (void)hipMemsetAsync(p->d_tccnt, 0, 2 * vc1 * 4, M);
-        hipLaunchKernelGGL(tcls_count_kernel, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tccnt, vc1, q);
+        hipLaunchKernelGGL(tcls_count_kernel, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tccnt, vc1, q,
+                           cls);
         size_t need = 0;
         hipError_t e = rocprim::exclusive_scan(nullptr, need, p->d_tccnt, p->d_tcls, 0u, (size_t)vc1,
                                                rocprim::plus<uint32_t>(), M);
@@ -1385,7 +1391,7 @@ srt_status build_tight_rows(srt_plan *p, uint64_t slots, uint32_t ubits, uint64_
         }
         (void)hipMemsetAsync(p->d_tccnt, 0, 2 * vc1 * 4, M);
         hipLaunchKernelGGL(tcls_fill_kernel, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tcls,
-                           p->d_tccnt, p->d_tpk, p->d_tpk2, vc1, q, q > 1 ? p->d_tcw : nullptr, p->t_cap);
+                           p->d_tccnt, p->d_tpk, p->d_tpk2, vc1, q, q > 1 ? p->d_tcw : nullptr, p->t_cap, cls);
         p->t_push = false;
         return SRT_OK;
     }
@@ -1409,11 +1415,12 @@ srt_status launch_level(srt_plan *p, unsigned long long *d_stats, const RowJob &
     const int per_cu = std::max(1, std::min(2048 / (int)nt, (int)std::max<size_t>(1, (160 * 1024) / (lds + 2048))));
     const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(rows, (uint32_t)(cu_count(p->device) * per_cu)));
     // 8 edge loads in flight a lane (C3: 7.0 -> 6.7 ms vs 4)
-    auto kern = p->t_q > 1 ? level_loss_kernel<LPT, 8, true> : level_loss_kernel<LPT, 8, false>;
+    auto kern = p->t_cls == 16 ? (p->t_q > 1 ? level_loss_kernel<LPT, 8, true, 16> : level_loss_kernel<LPT, 8, false, 16>)
+                               : (p->t_q > 1 ? level_loss_kernel<LPT, 8, true, 32> : level_loss_kernel<LPT, 8, false, 32>);
     (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(LDS_BUDGET - 4096));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, p->stream, (const void *)p->d_D, p->key_type, p->Vp, V,
                        p->d_nodes, p->n, job.list ? 0u : job.range ? job.r0 : p->row0,
-                       job.list ? job.count : job.range ? job.r1 : p->row1, p->d_tcls, (uint64_t)V * CLS + 1,
+                       job.list ? job.count : job.range ? job.r1 : p->row1, p->d_tcls, (uint64_t)V * p->t_cls + 1,
                        p->d_tpk, p->d_tpk2, p->kp.g, p->d_sl_lat, p->d_sl_loss, p->d_out_lat, p->d_out_loss, d_stats,
                        job.list, job.out32, job.out32_loss, p->stage16, p->t_q, p->d_tcw, p->t_cap);
     return SRT_OK;

@@ -3,5 +3,6 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
-SRT_TRACE=1 timeout -k 10 300 python3 bench.py --config c3ns --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --no-cold > gpurun_out/r4_c3ns.json 2> gpurun_out/r4_c3ns.err; grep "tight edges" gpurun_out/r4_c3ns.err | tail -1; python3 -c "import json; d=json.loads(open('gpurun_out/r4_c3ns.json').read().strip().splitlines()[-1]); print(d['ms_per_step'], d['config']['phases_last_build'])"
-timeout -k 10 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_apsp.py tests/test_gpu_configs.py > gpurun_out/r4_tests23.log 2>&1; echo "tests rc=$?"; tail -3 gpurun_out/r4_tests23.log
+timeout -k 10 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_apsp.py tests/test_gpu_configs.py tests/test_gpu_dist.py > gpurun_out/r4_tests25.log 2>&1; echo "tests rc=$?"; tail -2 gpurun_out/r4_tests25.log
+bash tools/ab_c3.sh "X=1" "X=2"
+timeout -k 10 300 python3 bench.py --config c3ns --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --no-cold > gpurun_out/r4_c3ns.json 2>/dev/null; python3 -c "import json; d=json.loads(open('gpurun_out/r4_c3ns.json').read().strip().splitlines()[-1]); print(d['ms_per_step'], d['config']['phases_last_build'])"
