@@ -1,8 +1,10 @@
 #!/bin/bash
-# one GPU session of round-4 work (edited per session)
+# round-4 final profiles, part B: C4 (profile), C5 (profile), C2/C2nc/C1 bench lines
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
-timeout -k 10 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_apsp.py tests/test_gpu_configs.py tests/test_gpu_dist.py > gpurun_out/r4_tests25.log 2>&1; echo "tests rc=$?"; tail -2 gpurun_out/r4_tests25.log
-bash tools/ab_c3.sh "X=1" "X=2"
-timeout -k 10 300 python3 bench.py --config c3ns --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --no-cold > gpurun_out/r4_c3ns.json 2>/dev/null; python3 -c "import json; d=json.loads(open('gpurun_out/r4_c3ns.json').read().strip().splitlines()[-1]); print(d['ms_per_step'], d['config']['phases_last_build'])"
+bash tools/profile_round.sh r04c4 --config c4 || exit 1
+bash tools/profile_round.sh r04c5 --config c5 || exit 1
+for c in c2 c2nc c1; do
+  timeout -k 10 400 python3 -u bench.py --config $c > gpurun_out/r04_$c.json 2> gpurun_out/r04_$c.err; echo "$c rc=$?"; tail -1 gpurun_out/r04_$c.json | cut -c1-200
+done
