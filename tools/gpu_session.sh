@@ -1,10 +1,11 @@
 #!/bin/bash
-# round-4 final profiles, part B: C4 (profile), C5 (profile), C2/C2nc/C1 bench lines
+# emulated 8 / 4 ranks under rest LDS padding (A/B)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
-bash tools/profile_round.sh r04c4 --config c4 || exit 1
-bash tools/profile_round.sh r04c5 --config c5 || exit 1
-for c in c2 c2nc c1; do
-  timeout -k 10 400 python3 -u bench.py --config $c > gpurun_out/r04_$c.json 2> gpurun_out/r04_$c.err; echo "$c rc=$?"; tail -1 gpurun_out/r04_$c.json | cut -c1-200
+for pad in 0 24576 40000; do
+for n in 8 4; do
+  SRT_FW_REST_PAD=$pad timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-cold --no-e2e --emulate-ranks $n > gpurun_out/emu_pad.json 2>/dev/null || exit 1
+  python3 -c "import json; d=json.loads(open('gpurun_out/emu_pad.json').read().strip().splitlines()[-1]); print('pad $pad ranks $n', round(d['ms_per_step'],2), round(d['rest_ms_per_step'],2))"
+done
 done
