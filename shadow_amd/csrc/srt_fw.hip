@@ -135,13 +135,16 @@ __device__ __forceinline__ void relax_row8<double>(double (&acc)[8], double a, c
 
 // ------------------------------------------------------------------ init
 // rows [r0, r1) of D: 0 on the diagonal, +inf elsewhere
+constexpr uint16_t F16_INF_BITS = 0x6400;  // 1024.0: f16 plans' INF (below)
+
 template <typename K>
-__global__ void fill_kernel(K *__restrict__ D, uint32_t Vp, uint32_t r0, uint32_t r1) {
+__global__ void fill_kernel(K *__restrict__ D, uint32_t Vp, uint32_t r0, uint32_t r1, bool f16) {
     const uint64_t first = (uint64_t)r0 * Vp, total = (uint64_t)(r1 - r0) * Vp;
+    const K inf = f16 ? (K)F16_INF_BITS : KeyOps<K>::inf();  // f16: 2-byte keys only
     for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < total;
          e += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t r = (uint32_t)((first + e) / Vp), c = (uint32_t)((first + e) % Vp);
-        D[first + e] = (r == c) ? KeyOps<K>::zero() : KeyOps<K>::inf();
+        D[first + e] = (r == c) ? KeyOps<K>::zero() : inf;
     }
 }
 
@@ -152,7 +155,6 @@ __global__ void fill_kernel(K *__restrict__ D, uint32_t Vp, uint32_t r0, uint32_
 // ~0.1 ms at 16k).  Values >= 1024 saturate to INF: exact, since the host
 // proved every finite distance < 1024 (every stored key is then min(real
 // walk, INF), as for u16 / u32 keys).
-constexpr uint16_t F16_INF_BITS = 0x6400;  // 1024.0
 __global__ void keys_to_f16_kernel(uint16_t *__restrict__ D, uint64_t n8) {
     for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < n8; e += (uint64_t)gridDim.x * blockDim.x) {
         uint4 v = reinterpret_cast<uint4 *>(D)[e];
@@ -204,11 +206,14 @@ __device__ __forceinline__ uint64_t edge_key(uint64_t lat, const KeyParams &kp) 
 // diagonal is the raw self-loop written by the loss pass (mod.rs:210-217).
 // UNIQUE (host-checked: no parallel edges) stores the key instead of the
 // memory-side atomic min (16k complete graph: 2.5 ms -> one plain store pass).
+// f16 (2-byte keys of an f16 plan): the keys stored as f16 integer bits
+// straight away (the conversion pass before the closure is skipped)
 template <typename K, bool UNIQUE>
 __global__ void scatter_edges_kernel(K *__restrict__ D, uint32_t Vp,
                                      const uint64_t *__restrict__ row_ptr,
                                      const uint32_t *__restrict__ col,
-                                     const uint64_t *__restrict__ lat, uint32_t u0, uint32_t u1, KeyParams kp) {
+                                     const uint64_t *__restrict__ lat, uint32_t u0, uint32_t u1, KeyParams kp,
+                                     bool f16) {
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -230,6 +235,8 @@ __global__ void scatter_edges_kernel(K *__restrict__ D, uint32_t Vp,
                 key = key < inf ? key : inf;
             }
             if constexpr (sizeof(K) == 2) {
+                if (f16)  // non-negative f16 bit patterns order like the values: the min below still holds
+                    key = key >= 1024u ? F16_INF_BITS : __builtin_bit_cast(uint16_t, (_Float16)(float)key);
                 K *dst = &D[(uint64_t)u * Vp + v];
                 if constexpr (UNIQUE) {
                     *dst = (K)key;
@@ -1886,13 +1893,17 @@ void fw_init_t(srt_plan *p) {
     const bool local = p->comm && !(sizeof(K) == 2 && (p->fw_sym || !p->fw_sym_known));
     const uint32_t r0 = local ? p->rb0 * B : 0, r1 = local ? p->rb1 * B : p->Vp;
     const uint32_t u0 = std::min(r0, p->V), u1 = std::min(r1, p->V);
-    hipLaunchKernelGGL(fill_kernel<K>, dim3(4096), dim3(256), 0, p->stream, D, p->Vp, r0, r1);
+    // f16 plans initialised in full: D in f16 keys from the start (the
+    // closure's keys_to_f16 pass is skipped: C3 -0.19 ms)
+    const bool f16 = sizeof(K) == 2 && p->fw_f16 && !local;
+    p->d_f16 = f16;
+    hipLaunchKernelGGL(fill_kernel<K>, dim3(4096), dim3(256), 0, p->stream, D, p->Vp, r0, r1, f16);
     if (p->fw_unique_edges)
         hipLaunchKernelGGL((scatter_edges_kernel<K, true>), dim3(2048), dim3(256), 0, p->stream, D, p->Vp,
-                           p->d_row_ptr, p->d_col, p->d_lat, u0, u1, p->kp);
+                           p->d_row_ptr, p->d_col, p->d_lat, u0, u1, p->kp, f16);
     else
         hipLaunchKernelGGL((scatter_edges_kernel<K, false>), dim3(2048), dim3(256), 0, p->stream, D, p->Vp,
-                           p->d_row_ptr, p->d_col, p->d_lat, u0, u1, p->kp);
+                           p->d_row_ptr, p->d_col, p->d_lat, u0, u1, p->kp, f16);
 }
 
 // Measurement only (N-rank emulation): stands in for the pivot-row broadcast
@@ -2998,9 +3009,10 @@ srt_status fw_rounds(srt_plan *p, srt_err *err) {
         // stream (every schedule's last kernel runs there, or joins it)
         const uint64_t n8 = (uint64_t)p->Vp * p->Vp / 8;
         uint16_t *D = reinterpret_cast<uint16_t *>(p->d_D);
-        if (p->fw_f16) hipLaunchKernelGGL(keys_to_f16_kernel, dim3(4096), dim3(256), 0, p->stream, D, n8);
+        if (p->fw_f16 && !p->d_f16) hipLaunchKernelGGL(keys_to_f16_kernel, dim3(4096), dim3(256), 0, p->stream, D, n8);
         const srt_status st = fw_rounds_t<uint16_t>(p, err);
         if (p->fw_f16) hipLaunchKernelGGL(keys_from_f16_kernel, dim3(4096), dim3(256), 0, p->stream, D, n8);
+        p->d_f16 = false;
         return st;
     }
     if (p->key_type == KEY_U32) return fw_rounds_t<uint32_t>(p, err);

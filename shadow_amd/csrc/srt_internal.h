@@ -101,6 +101,7 @@ struct srt_plan {
     int fw_p1 = 1;
     bool fw_small_chain = false;  // quarter-tile kernels for the look-ahead chain (sharded)
     bool fw_unique_edges = false; // no parallel edges: FW init stores instead of atomic min
+    bool d_f16 = false;           // D holds f16 keys now (the init wrote them; fw_rounds converts back)
     // rounds per row all-gather of the symmetric sharded schedule (knob
     // SRT_FW_SYM_GROUP; 1 = fw_rounds_sym_sharded's one-round chain).
     // Emulated C3, g = 1 / 2 / 4: 8 ranks 21.9 / 20.0 / 22.4 ms, 4 ranks 24.2 /
