@@ -1862,6 +1862,24 @@ __global__ void pack6_kernel(const uint64_t *__restrict__ lat, const float *__re
     }
 }
 
+// 5-byte download records (closures whose every finite latency is <= 510
+// units): the low 8 bits of the units in one array, then (16-byte aligned)
+// the loss bits with the units' 9th bit in the sign bit (a table loss is
+// never negative: folds give +0, and the diagonal, whose self-loop may be
+// -0.0, is rewritten on the host).  511 = unreachable.
+__global__ void pack5_kernel(const uint64_t *__restrict__ lat, const float *__restrict__ loss, uint8_t *__restrict__ out,
+                             uint64_t total, uint64_t g, uint64_t loss_off) {
+    uint32_t *lw = reinterpret_cast<uint32_t *>(out + loss_off);
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < total;
+         e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t l = lat[e];
+        const uint64_t u = l == ~0ull ? 511u : l / g;
+        const uint32_t u9 = u < 511u ? (uint32_t)u : 511u;
+        out[e] = (uint8_t)u9;
+        lw[e] = (__float_as_uint(loss[e]) & 0x7fffffffu) | ((u9 >> 8) << 31);
+    }
+}
+
 __global__ void widen_u32_kernel(uint64_t *__restrict__ dst, const uint32_t *__restrict__ src, uint64_t count) {
     for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < count; e += (uint64_t)gridDim.x * blockDim.x)
         dst[e] = src[e];
@@ -3040,6 +3058,11 @@ void iota_rows(uint32_t *dst, uint64_t count, uint32_t V, hipStream_t s) {
 
 void pack_paths6(srt_plan *p, uint64_t first, uint64_t count, void *dst, uint64_t loss_off, hipStream_t s) {
     hipLaunchKernelGGL(pack6_kernel, dim3(4096), dim3(256), 0, s, p->d_out_lat + first, p->d_out_loss + first,
+                       reinterpret_cast<uint8_t *>(dst), count, p->kp.g, loss_off);
+}
+
+void pack_paths5(srt_plan *p, uint64_t first, uint64_t count, void *dst, uint64_t loss_off, hipStream_t s) {
+    hipLaunchKernelGGL(pack5_kernel, dim3(4096), dim3(256), 0, s, p->d_out_lat + first, p->d_out_loss + first,
                        reinterpret_cast<uint8_t *>(dst), count, p->kp.g, loss_off);
 }
 

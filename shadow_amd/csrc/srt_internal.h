@@ -402,6 +402,8 @@ void iota_rows(uint32_t *dst, uint64_t count, uint32_t V, hipStream_t s);
 void loss_check(const float *d_loss, uint64_t count, uint64_t k0, unsigned long long *d_first, hipStream_t s);
 // u16-key plans: u16 latency units, then the f32 losses at byte offset loss_off
 void pack_paths6(srt_plan *p, uint64_t first, uint64_t count, void *dst, uint64_t loss_off, hipStream_t s);
+// 5-byte records (lmax <= 510): u8 units, then the loss bits with the 9th unit bit in the sign
+void pack_paths5(srt_plan *p, uint64_t first, uint64_t count, void *dst, uint64_t loss_off, hipStream_t s);
 // kernels (srt_sssp.hip)
 srt_status sssp_run(srt_plan *p, unsigned long long *d_stats, srt_err *err);
 // kernels (srt_frontier.hip): the latency-first frontier sweeps

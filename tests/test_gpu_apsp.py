@@ -243,11 +243,12 @@ def test_loss_pass_unpacked_form(monkeypatch, seed, directed):
 
 def test_end_to_end_compact_download_matches_device_table(monkeypatch):
     """srt_compute_shortest_paths on a dense graph downloads the table as
-    6-byte records (u16 keys: latency / g as u16, loss bits) in pieces behind
-    the chunked fold, expanded on host threads; 9,000 nodes = 2 fold chunks,
-    10 pieces.  The host table must equal, bit for bit, the device table of
-    the same build, the 8-byte records (SRT_FETCH8=1) and the 16-byte
-    download (SRT_FETCH16=1)."""
+    5-byte records (every finite latency <= 510 units: the units' low 8 bits,
+    the loss bits with the 9th unit bit in the sign) in pieces behind the
+    chunked fold, expanded on host threads; 9,000 nodes = 2 fold chunks, 10
+    pieces.  The host table must equal, bit for bit, the device table of the
+    same build, the 6-byte records (SRT_FETCH6=1), the 8-byte records
+    (SRT_FETCH8=1) and the 16-byte download (SRT_FETCH16=1)."""
     import torch
 
     from shadow_amd.dist import _CudaBuf
@@ -265,7 +266,7 @@ def test_end_to_end_compact_download_matches_device_table(monkeypatch):
     plan.close()
     assert np.array_equal(t.latency_ns.reshape(-1), L)
     assert np.array_equal(t.packet_loss.reshape(-1).view(np.uint32), P)
-    for knob in ("SRT_FETCH8", "SRT_FETCH16"):  # 8-byte records; the 16-byte srt_path download
+    for knob in ("SRT_FETCH6", "SRT_FETCH8", "SRT_FETCH16"):  # 6- and 8-byte records; the 16-byte download
         monkeypatch.setenv(knob, "1")
         t2 = g.compute_shortest_paths(nodes)
         monkeypatch.delenv(knob)
