@@ -63,6 +63,9 @@ constexpr uint32_t L16_INF = 0xffffu;
 // (<= 64 VGPRs, a few bytes of spill) beat fewer, fatter waves -- C4 1.03 s
 // at 5 waves/SIMD (92 VGPRs, 4 loss edges a batch) -> 0.79 s.
 #define FR_OCC __attribute__((amdgpu_waves_per_eu(8, 8)))
+#ifndef FR_COUNT
+#define FR_COUNT 0
+#endif
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
@@ -447,7 +450,9 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
     const uint32_t wave = blockIdx.x * FR_WAVES + (threadIdx.x >> 6), nwaves = gridDim.x * FR_WAVES;
     const uint32_t cpb = (V + 63) / 64, nchunks = cpb * NB;
     bool any_imp = false;
-    uint32_t c_items = 0, c_work = 0, c_imp = 0, c_gath = 0;  // SRT_FR_COUNT (measurement)
+#if FR_COUNT
+    uint32_t c_items = 0, c_work = 0, c_imp = 0, c_gath = 0;  // SRT_FR_COUNT (diagnostic builds)
+#endif
     for (uint32_t c = __builtin_amdgcn_readfirstlane(wave); c < nchunks; c += nwaves) {
         const uint32_t b = c / cpb, v0 = (c % cpb) * 64;
         uint32_t *act_b = act + (uint64_t)b * V;
@@ -558,7 +563,9 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
                                 m[q] = (w >> (8 * (jq % 4))) & 0xffu;
                                 const uint32_t u = __builtin_amdgcn_readlane(eu, j0 + jq);
                                 eb[q] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(eeb), j0 + jq));
+#if FR_COUNT
                                 ++c_gath;
+#endif
                                 if (m[q]) {
                                     x0[q] = Pb[(uint64_t)u * 128 + 2 * lane];
                                     x1[q] = Pb[(uint64_t)u * 128 + 2 * lane + 1];
@@ -589,8 +596,10 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
                 }
             }
             uint32_t ib = 0;  // the lane's improved sources
+#if FR_COUNT
             ++c_items;
             c_work += __ballot(own) != 0;
+#endif
             if (own) {
                 const float ov[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
 #pragma unroll
@@ -601,7 +610,9 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
             }
             if (__ballot(ib != 0)) {
                 any_imp = true;
+#if FR_COUNT
                 ++c_imp;
+#endif
                 if (ib) {
                     pv[0] = make_float4(best[0], best[1], best[2], best[3]);
                     pv[1] = make_float4(best[4], best[5], best[6], best[7]);
@@ -617,12 +628,16 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
             eeb = neeb;
         }
     }
+#if FR_COUNT
     if (cnt && lane == 0) {
         atomicAdd(&cnt[0], (unsigned long long)c_items);
         atomicAdd(&cnt[1], (unsigned long long)c_work);
         atomicAdd(&cnt[2], (unsigned long long)c_imp);
         atomicAdd(&cnt[3], (unsigned long long)c_gath);
     }
+#else
+    (void)cnt;
+#endif
     note_improved(last, t, any_imp, lane);
 }
 
@@ -890,11 +905,13 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
         t0 = t_end + 2;
         hipLaunchKernelGGL(fr_seed_kernel, seed_grid, dim3(256), 0, M, nullptr, p->d_fp, p->d_fsb, chg, p->d_fact,
                            p->d_fnodes, perm, V, q0, nsrc, t0, p->d_frow_ptr, p->d_fcol);
-        // SRT_FR_COUNT=1 (measurement): per loss sweep, items processed / with
-        // work / improved / edge gathers, printed after the phase
+        // SRT_FR_COUNT=1 in a diagnostic build (-DFR_COUNT=1): per loss sweep,
+        // items processed / with work / improved / edge gathers, printed after
+        // the phase (the counters cost the kernel registers, so they are not in
+        // the default build)
         static unsigned long long *dcnt_s = nullptr;
         unsigned long long *dcnt = nullptr;
-        if (std::getenv("SRT_FR_COUNT")) {
+        if (FR_COUNT && std::getenv("SRT_FR_COUNT")) {
             if (!dcnt_s) (void)hipMalloc(&dcnt_s, 4 * 256 * 8);
             dcnt = dcnt_s;
             (void)hipMemsetAsync(dcnt, 0, 4 * 256 * 8, M);

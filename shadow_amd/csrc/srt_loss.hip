@@ -1032,8 +1032,13 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
                 // pull: x in N_l, its class-w in-edges u -> x, u in N_j
                 const uint16_t want = (uint16_t)(push ? l : j);
                 const float onem = push ? 1.0f - __uint_as_float(prow[x]) : 0.0f;
-                bool xinf;
-                const uint64_t Lx = QUANT ? closure_lat(D, (uint64_t)s * Vp + x, key_type, xinf) : 0;
+                // exact closure values of the quantized fold (2- or 4-byte keys, level_q)
+                auto exact = [&](uint32_t y) -> uint32_t {
+                    const uint64_t idx = (uint64_t)s * Vp + y;
+                    return key_type == KEY_U16 ? (uint32_t)reinterpret_cast<const uint16_t *>(D)[idx]
+                                               : reinterpret_cast<const uint32_t *>(D)[idx];
+                };
+                const uint32_t Lx = QUANT ? exact(x) : 0u;
                 const uint32_t *cwp = QUANT ? cw + (push ? 0 : cw_in) : nullptr;
                 for (uint32_t b = e0; b < e1; b += UNR * LPT) {
                     uint64_t wd[UNR];
@@ -1058,10 +1063,8 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
                             // the tail's level (j or j - 1) or the head's (l), then exact
                             hit[q] = ok[q] && (push ? lo_[q] == want : lo_[q] == want || lo_[q] + 1 == want);
                             if (hit[q]) {
-                                bool oinf;
-                                const uint64_t Lo = closure_lat(D, (uint64_t)s * Vp + o[q], key_type, oinf);
-                                const uint64_t wq = cwp[b + sub + q * LPT];
-                                hit[q] = push ? Lx + wq == Lo : Lo + wq == Lx;
+                                const uint32_t Lo = exact(o[q]), wq = cwp[b + sub + q * LPT];
+                                hit[q] = push ? Lx + wq == Lo : Lo + wq == Lx;  // finite: no wrap below 2^31
                             }
                         }
                     }
@@ -1336,7 +1339,8 @@ uint32_t level_q(const srt_plan *p, uint64_t maxw, uint64_t minw) {
     if (!(p->kp.lat32 && p->V < 65536 && lds + 16 <= LDS_BUDGET - 4096 && maxw >= 1)) return 0;
     if (maxw <= WC && p->kp.lmax < (uint64_t)NBK) return 1;
     if (minw >= 2 && minw <= maxw && maxw / minw <= WC && p->kp.lmax / minw < (uint64_t)NBK - 1 &&
-        minw < (1ull << 32) && !std::getenv("SRT_LOSS_NOQ"))
+        minw < (1ull << 32) && (p->key_type == srt::KEY_U16 || p->key_type == srt::KEY_U32) &&
+        !std::getenv("SRT_LOSS_NOQ"))
         return (uint32_t)minw;
     return 0;
 }
@@ -1415,8 +1419,10 @@ srt_status launch_level(srt_plan *p, unsigned long long *d_stats, const RowJob &
     const int per_cu = std::max(1, std::min(2048 / (int)nt, (int)std::max<size_t>(1, (160 * 1024) / (lds + 2048))));
     const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(rows, (uint32_t)(cu_count(p->device) * per_cu)));
     // 8 edge loads in flight a lane (C3: 7.0 -> 6.7 ms vs 4)
-    auto kern = p->t_cls == 16 ? (p->t_q > 1 ? level_loss_kernel<LPT, 8, true, 16> : level_loss_kernel<LPT, 8, false, 16>)
-                               : (p->t_q > 1 ? level_loss_kernel<LPT, 8, true, 32> : level_loss_kernel<LPT, 8, false, 32>);
+    // (3 in the quantized form and 4 in the 32-class one, whose extra
+    // registers would spill at 8)
+    auto kern = p->t_cls == 16 ? (p->t_q > 1 ? level_loss_kernel<LPT, 3, true, 16> : level_loss_kernel<LPT, 8, false, 16>)
+                               : (p->t_q > 1 ? level_loss_kernel<LPT, 3, true, 32> : level_loss_kernel<LPT, 4, false, 32>);
     (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(LDS_BUDGET - 4096));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, p->stream, (const void *)p->d_D, p->key_type, p->Vp, V,
                        p->d_nodes, p->n, job.list ? 0u : job.range ? job.r0 : p->row0,
