@@ -849,7 +849,13 @@ __global__ void tcls_fill_kernel(const uint4 *__restrict__ list, uint64_t slots,
 // edge's tail lies in level l - c or l - c - 1, and a candidate is taken only
 // when L(s,u) + w == L(s,v) exactly (the closure row's exact values, read from
 // D; the class entries' weights from cw).  The output latencies come from D.
-template <int LPT, int UNR, bool QUANT, uint32_t CLSN>
+#ifndef LOSS_COUNT
+#define LOSS_COUNT 0
+#endif
+#if LOSS_COUNT
+__device__ unsigned long long loss_cnt[9];  // diagnostic builds: items, edge visits, hits, levels, phase ticks x4, push hits
+#endif
+template <int LPT, int UNR, bool QUANT, uint32_t CLSN, int VW>
 __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
     const void *__restrict__ D, int key_type, uint32_t Vp, uint32_t V, const uint32_t *__restrict__ nodes, uint32_t n,
     uint32_t row0, uint32_t row1, const uint32_t *__restrict__ tcls, uint64_t vc1,
@@ -878,19 +884,54 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
     const uint32_t *cls_out = tcls, *cls_in = tcls + vc1;
     uint64_t mn = ~0ull;
     unsigned long long unreach = 0;
+#if LOSS_COUNT
+    uint32_t c_vis = 0, c_hit = 0, c_phit = 0;
+#endif
     const uint32_t nrows = row_list ? row1 : row1 - row0;
     for (uint32_t k = blockIdx.x; k < nrows; k += gridDim.x) {
         const uint32_t i = row_list ? row_list[k] : row0 + k;
         const uint32_t s = nodes[i];
+#if LOSS_COUNT
+        unsigned long long tk0 = wall_clock64();
+#define LOSS_TICK(slot)                                                          \
+    if (tid == 0) {                                                              \
+        const unsigned long long tk1 = wall_clock64();                           \
+        atomicAdd(&loss_cnt[slot], tk1 - tk0);                                   \
+        tk0 = tk1;                                                               \
+    }
+#else
+#define LOSS_TICK(slot)
+#endif
         // 1. the row's latencies (units of g, < NBK by the host's proof bound)
         uint32_t mx = 0;
-        for (uint32_t v = tid; v < V; v += nt) {
-            bool inf;
-            const uint64_t l64 = closure_lat(D, (uint64_t)s * Vp + v, key_type, inf);
+        auto put = [&](uint32_t v, bool inf, uint64_t l64) {
             const uint16_t l = inf ? LINF : v == s ? (uint16_t)0 : (uint16_t)(QUANT ? l64 / qw : l64);
             lrow[v] = l;
             prow[v] = v == s ? 0u : FINF;  // petgraph's zero score (0 ns, 0.0) at s
             if (l != LINF && l > mx) mx = l;
+        };
+        if (key_type == KEY_U16 && (Vp & 7u) == 0) {
+            // 2-byte keys: 8 a thread in one 16-byte load (C3: 2 loads a
+            // thread instead of 16 dependent round trips; the row is padded to Vp)
+            const uint16_t *Dr = reinterpret_cast<const uint16_t *>(D) + (uint64_t)s * Vp;
+            for (uint32_t v8 = tid * 8; v8 < V; v8 += nt * 8) {
+                const uint4 raw = *reinterpret_cast<const uint4 *>(Dr + v8);
+                auto put2 = [&](uint32_t v, uint32_t wd) {
+                    const uint16_t k0 = (uint16_t)wd, k1 = (uint16_t)(wd >> 16);
+                    if (v < V) put(v, k0 >= KEY16_INF, k0);
+                    if (v + 1 < V) put(v + 1, k1 >= KEY16_INF, k1);
+                };
+                put2(v8, raw.x);
+                put2(v8 + 2, raw.y);
+                put2(v8 + 4, raw.z);
+                put2(v8 + 6, raw.w);
+            }
+        } else {
+            for (uint32_t v = tid; v < V; v += nt) {
+                bool inf;
+                const uint64_t l64 = closure_lat(D, (uint64_t)s * Vp + v, key_type, inf);
+                put(v, inf, l64);
+            }
         }
         for (uint32_t b = tid; b <= (uint32_t)NBK; b += nt) hist[b] = 0;
         for (int off = 32; off > 0; off >>= 1) {
@@ -901,6 +942,7 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
         __syncthreads();
         mx = 0;
         for (int q = 0; q < nw; ++q) mx = red[q] > mx ? (uint32_t)red[q] : mx;
+        LOSS_TICK(4)
         // 2. counting sort of the reachable vertices (s at level 0) by level.
         // Few levels (mx < 32, C3: ~6): one ballot per level and 64-vertex
         // chunk, a wave's count of level l in lane l; the per-wave counts are
@@ -987,6 +1029,7 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
         __syncthreads();
         }
         // hist[l] is now the end of level l (its start: hist[l-1], or 0)
+        LOSS_TICK(5)
         // 3. levels in increasing latency, every weight class from its smaller end
         for (uint32_t l = 1; l <= mx; ++l) {
             const uint32_t lo = hist[l - 1], cnt_l = hist[l] - lo;
@@ -1022,6 +1065,9 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
                 e1 = cl[(uint64_t)x * CLSN + w];
             };
             uint32_t nw_ = 1, nx = 0, ne0 = 0, ne1 = 0;
+#if LOSS_COUNT
+            if (tid == 0) { atomicAdd(&loss_cnt[0], (unsigned long long)T); atomicAdd(&loss_cnt[3], 1ull); }
+#endif
             if (grp < T) item(grp, nw_, nx, ne0, ne1);
             for (uint32_t t = grp; t < T; t += ngrp) {
                 const uint32_t w = nw_, x = nx, e0 = ne0, e1 = ne1, j = l - w;
@@ -1040,36 +1086,59 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
                 };
                 const uint32_t Lx = QUANT ? exact(x) : 0u;
                 const uint32_t *cwp = QUANT ? cw + (push ? 0 : cw_in) : nullptr;
-                for (uint32_t b = e0; b < e1; b += UNR * LPT) {
-                    uint64_t wd[UNR];
-#pragma unroll
-                    for (int q = 0; q < UNR; ++q) wd[q] = ce[b + sub + q * LPT];  // padded past the end
-                    uint32_t o[UNR];
-                    bool ok[UNR];
+                // VW = 2: a lane loads 2 adjacent entries (16 B) at a time from
+                // the even entry at or below e0, masking the entries outside [e0, e1)
+                constexpr int NE = UNR * VW;  // entries a lane an iteration
+                for (uint32_t b = VW == 2 ? e0 & ~1u : e0; b < e1; b += UNR * LPT * VW) {
+                    uint64_t wd[NE];
+                    uint32_t ei[NE];
 #pragma unroll
                     for (int q = 0; q < UNR; ++q) {
-                        ok[q] = b + sub + q * LPT < e1;
+                        const uint32_t at = b + (sub + q * LPT) * VW;  // padded past the end
+                        if (VW == 2) {
+                            const uint4 r2 = *reinterpret_cast<const uint4 *>(ce + at);
+                            wd[2 * q] = ((uint64_t)r2.y << 32) | r2.x;
+                            wd[2 * q + 1] = ((uint64_t)r2.w << 32) | r2.z;
+                            ei[2 * q] = at;
+                            ei[2 * q + 1] = at + 1;
+                        } else {
+                            wd[q] = ce[at];
+                            ei[q] = at;
+                        }
+                    }
+                    uint32_t o[NE];
+                    bool ok[NE];
+#pragma unroll
+                    for (int q = 0; q < NE; ++q) {
+                        ok[q] = ei[q] < e1 && (VW == 1 || ei[q] >= e0);
                         o[q] = ok[q] ? (uint32_t)wd[q] : 0u;
                     }
-                    uint16_t lo_[UNR];
+                    uint16_t lo_[NE];
 #pragma unroll
-                    for (int q = 0; q < UNR; ++q) lo_[q] = lrow[o[q]];
-                    bool hit[UNR];
+                    for (int q = 0; q < NE; ++q) lo_[q] = lrow[o[q]];
+                    bool hit[NE];
 #pragma unroll
-                    for (int q = 0; q < UNR; ++q) {
+                    for (int q = 0; q < NE; ++q) {
                         if (!QUANT) {
                             hit[q] = ok[q] && lo_[q] == want;
                         } else {
                             // the tail's level (j or j - 1) or the head's (l), then exact
                             hit[q] = ok[q] && (push ? lo_[q] == want : lo_[q] == want || lo_[q] + 1 == want);
                             if (hit[q]) {
-                                const uint32_t Lo = exact(o[q]), wq = cwp[b + sub + q * LPT];
+                                const uint32_t Lo = exact(o[q]), wq = cwp[ei[q]];
                                 hit[q] = push ? Lx + wq == Lo : Lo + wq == Lx;  // finite: no wrap below 2^31
                             }
                         }
                     }
+#if LOSS_COUNT
+                    for (int q = 0; q < NE; ++q) {
+                        c_vis += ok[q];
+                        c_hit += hit[q];
+                        c_phit += push && hit[q];
+                    }
+#endif
 #pragma unroll
-                    for (int q = 0; q < UNR; ++q) {
+                    for (int q = 0; q < NE; ++q) {
                         if (hit[q]) {
                             const float r = __uint_as_float((uint32_t)(wd[q] >> 32));
                             if (push) {
@@ -1085,43 +1154,62 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
             }
             __syncthreads();  // level l final; plan_end rewritten by the next level
         }
+        LOSS_TICK(6)
         // 4. table row i (or staging slot k)
         uint64_t *ol = out_lat + (uint64_t)i * n;
         float *op = out_loss + (uint64_t)i * n;
         uint32_t *o32 = out32 && !stage16 ? reinterpret_cast<uint32_t *>(out32) + (uint64_t)k * n : nullptr;
         uint16_t *o16 = out32 && stage16 ? reinterpret_cast<uint16_t *>(out32) + (uint64_t)k * n : nullptr;
         float *o32p = out32_loss ? out32_loss + (uint64_t)k * n : nullptr;  // staging (loss only if !out32)
-        for (uint32_t j = tid; j < n; j += nt) {
-            uint64_t latv;
-            float lossv;
-            if (j == i) {
-                latv = sl_lat[j];
-                lossv = sl_loss[j];
-            } else {
-                const uint32_t v = nodes[j];
-                const uint16_t l = lrow[v];
-                if (l == LINF) {
-                    ++unreach;
-                    latv = ~0ull;
-                    lossv = 1.0f;
+        // (4 node ids loaded ahead a thread; the staged latency is the
+        // closure's unit count, no division by g)
+        for (uint32_t j0 = tid; j0 < n; j0 += 4 * nt) {
+            uint32_t vv[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) vv[q] = j0 + q * nt < n ? nodes[j0 + q * nt] : 0u;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t j = j0 + q * nt;
+                if (j >= n) break;
+                uint64_t latv, lu;
+                float lossv;
+                if (j == i) {
+                    latv = sl_lat[j];
+                    lossv = sl_loss[j];
+                    lu = latv == ~0ull ? ~0ull : latv / g;
                 } else {
-                    bool vinf;
-                    latv = (QUANT ? closure_lat(D, (uint64_t)s * Vp + v, key_type, vinf) : (uint64_t)l) * g;
-                    lossv = __uint_as_float(prow[v]);
+                    const uint32_t v = vv[q];
+                    const uint16_t l = lrow[v];
+                    if (l == LINF) {
+                        ++unreach;
+                        latv = lu = ~0ull;
+                        lossv = 1.0f;
+                    } else {
+                        bool vinf;
+                        lu = QUANT ? closure_lat(D, (uint64_t)s * Vp + v, key_type, vinf) : (uint64_t)l;
+                        latv = lu * g;
+                        lossv = __uint_as_float(prow[v]);
+                    }
                 }
+                if (o32p) {
+                    if (o16) o16[j] = latv == ~0ull ? (uint16_t)0xffffu : (uint16_t)lu;
+                    else if (o32) o32[j] = latv == ~0ull ? ~0u : (uint32_t)lu;
+                    o32p[j] = lossv;
+                } else {
+                    ol[j] = latv;
+                    op[j] = lossv;
+                }
+                mn = latv < mn ? latv : mn;
             }
-            if (o32p) {
-                if (o16) o16[j] = latv == ~0ull ? (uint16_t)0xffffu : (uint16_t)(latv / g);
-                else if (o32) o32[j] = latv == ~0ull ? ~0u : (uint32_t)(latv / g);
-                o32p[j] = lossv;
-            } else {
-                ol[j] = latv;
-                op[j] = lossv;
-            }
-            mn = latv < mn ? latv : mn;
         }
         __syncthreads();  // the next row rewrites the LDS rows
+        LOSS_TICK(7)
     }
+#if LOSS_COUNT
+    atomicAdd(&loss_cnt[1], (unsigned long long)c_vis);
+    atomicAdd(&loss_cnt[2], (unsigned long long)c_hit);
+    atomicAdd(&loss_cnt[8], (unsigned long long)c_phit);
+#endif
     for (int off = 32; off > 0; off >>= 1) {
         const uint64_t o = __shfl_xor(mn, off);
         mn = o < mn ? o : mn;
@@ -1418,17 +1506,30 @@ srt_status launch_level(srt_plan *p, unsigned long long *d_stats, const RowJob &
     const uint32_t nt = V >= 2048 ? LOSS_NT : 256;
     const int per_cu = std::max(1, std::min(2048 / (int)nt, (int)std::max<size_t>(1, (160 * 1024) / (lds + 2048))));
     const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(rows, (uint32_t)(cu_count(p->device) * per_cu)));
-    // 8 edge loads in flight a lane (C3: 7.0 -> 6.7 ms vs 4)
-    // (3 in the quantized form and 4 in the 32-class one, whose extra
-    // registers would spill at 8)
-    auto kern = p->t_cls == 16 ? (p->t_q > 1 ? level_loss_kernel<LPT, 3, true, 16> : level_loss_kernel<LPT, 8, false, 16>)
-                               : (p->t_q > 1 ? level_loss_kernel<LPT, 3, true, 32> : level_loss_kernel<LPT, 4, false, 32>);
+    // 16-class exact form: 4 loads of 2 entries (16 B) in flight a lane (C3
+    // loss pass 6.5 -> 6.2 ms vs 8 single entries; 6 pairs 6.8, 2 lanes an
+    // item 7.2); quantized 3 (16 classes) or 2 (32) single entries, exact
+    // 32-class 4: their extra registers would spill at more
+    auto kern = p->t_cls == 16 ? (p->t_q > 1 ? level_loss_kernel<LPT, 3, true, 16, 1> : level_loss_kernel<LPT, 4, false, 16, 2>)
+                               : (p->t_q > 1 ? level_loss_kernel<LPT, 2, true, 32, 1> : level_loss_kernel<LPT, 4, false, 32, 1>);
     (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(LDS_BUDGET - 4096));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, p->stream, (const void *)p->d_D, p->key_type, p->Vp, V,
                        p->d_nodes, p->n, job.list ? 0u : job.range ? job.r0 : p->row0,
                        job.list ? job.count : job.range ? job.r1 : p->row1, p->d_tcls, (uint64_t)V * p->t_cls + 1,
                        p->d_tpk, p->d_tpk2, p->kp.g, p->d_sl_lat, p->d_sl_loss, p->d_out_lat, p->d_out_loss, d_stats,
                        job.list, job.out32, job.out32_loss, p->stage16, p->t_q, p->d_tcw, p->t_cap);
+#if LOSS_COUNT
+    {  // diagnostic builds (-DLOSS_COUNT=1): totals of every level fold so far
+        unsigned long long c[9];
+        (void)hipStreamSynchronize(p->stream);
+        (void)hipMemcpyFromSymbol(c, HIP_SYMBOL(loss_cnt), sizeof c);
+        std::fprintf(stderr,
+                     "[srt] level fold: items %llu visits %llu hits %llu (push %llu) levels %llu rows %u; us per row: "
+                     "load %.2f sort %.2f levels %.2f out %.2f\n",
+                     c[0], c[1], c[2], c[8], c[3], rows, c[4] * 0.01 / rows, c[5] * 0.01 / rows, c[6] * 0.01 / rows,
+                     c[7] * 0.01 / rows);
+    }
+#endif
     return SRT_OK;
 }
 
