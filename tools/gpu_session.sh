@@ -3,5 +3,5 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
-timeout -k 10 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu > gpurun_out/r4_tests30.log 2>&1; rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/r4_tests30.log; [ $rc -eq 0 ] || exit $rc
-bash tools/profile_round.sh r04c3 --config c3
+bash tools/ab_c3.sh "SRT_LIB=$R/shadow_amd/libsrt_a.so" "SRT_LIB=$R/shadow_amd/libsrt.so" "SRT_LIB=$R/shadow_amd/libsrt_a.so" "SRT_LIB=$R/shadow_amd/libsrt.so" || exit 1
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_apsp.py tests/test_gpu_configs.py -m gpu -k "loss or level or c3" > gpurun_out/r4_t.log 2>&1; echo "tests rc=$?"; tail -2 gpurun_out/r4_t.log
