@@ -331,7 +331,10 @@ void srt_routing_info_destroy(srt_routing_info *ri);
  * srt_init_async starts it on a library thread and returns at once, so the
  * simulator can call it first thing in main and parse its config and GML
  * graph meanwhile.  Every build (and srt_init) waits for a pending init.
- * Idempotent; errors of an async init surface in the next srt_init call. */
+ * Idempotent; errors of an async init surface in the next srt_init call.
+ * A process that may exit before its first build calls srt_init before exit
+ * (the Python package does so from its atexit): the library's own exit-time
+ * join can run after runtime statics the init thread created have gone. */
 srt_status srt_init(int device, srt_err *err);
 void srt_init_async(int device);
 

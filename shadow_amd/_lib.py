@@ -171,8 +171,27 @@ def init(device: int = -1) -> None:
     check(lib().srt_init(int(device), C.byref(err)), err)
 
 
+_exit_wait = []
+
+
 def init_async(device: int = -1) -> None:
-    """srt_init_async: the same on a library thread; the next build waits for it."""
+    """srt_init_async: the same on a library thread; the next build waits for it.
+
+    A Python exit waits for the pending init first (srt_init joins it), before
+    the interpreter's finalisation and the C-level exit: the library's own
+    atexit join runs after the destructors of runtime statics that the init
+    thread constructs lazily (registered later than that handler), and a
+    process exiting mid-init could reach them first (an intermittent SIGSEGV
+    at exit, seen once in the r04 GPU suite)."""
+    if not _exit_wait:
+        import atexit
+
+        def _wait(dev=int(device)):
+            err = SrtErr()
+            lib().srt_init(dev, C.byref(err))  # waits; a failed async init only reports
+
+        atexit.register(_wait)
+        _exit_wait.append(_wait)
     lib().srt_init_async(int(device))
 
 

@@ -1506,12 +1506,13 @@ srt_status launch_level(srt_plan *p, unsigned long long *d_stats, const RowJob &
     const uint32_t nt = V >= 2048 ? LOSS_NT : 256;
     const int per_cu = std::max(1, std::min(2048 / (int)nt, (int)std::max<size_t>(1, (160 * 1024) / (lds + 2048))));
     const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(rows, (uint32_t)(cu_count(p->device) * per_cu)));
-    // 16-class exact form: 4 loads of 2 entries (16 B) in flight a lane (C3
-    // loss pass 6.5 -> 6.2 ms vs 8 single entries; 6 pairs 6.8, 2 lanes an
-    // item 7.2); quantized 3 (16 classes) or 2 (32) single entries, exact
-    // 32-class 4: their extra registers would spill at more
+    // exact forms: loads of 2 entries (16 B), 4 in flight a lane with 16
+    // classes (C3 loss pass 6.5 -> 6.2 ms vs 8 single entries; 6 pairs 6.8,
+    // 2 lanes an item 7.2), 2 with 32 (C2 ~2% faster than 4 single entries);
+    // quantized: 3 (16 classes) or 2 (32) single entries (the exact weights
+    // beside them leave no registers for pairs)
     auto kern = p->t_cls == 16 ? (p->t_q > 1 ? level_loss_kernel<LPT, 3, true, 16, 1> : level_loss_kernel<LPT, 4, false, 16, 2>)
-                               : (p->t_q > 1 ? level_loss_kernel<LPT, 2, true, 32, 1> : level_loss_kernel<LPT, 4, false, 32, 1>);
+                               : (p->t_q > 1 ? level_loss_kernel<LPT, 2, true, 32, 1> : level_loss_kernel<LPT, 2, false, 32, 2>);
     (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(LDS_BUDGET - 4096));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, p->stream, (const void *)p->d_D, p->key_type, p->Vp, V,
                        p->d_nodes, p->n, job.list ? 0u : job.range ? job.r0 : p->row0,
