@@ -3,4 +3,8 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_routing_info.py -m gpu > gpurun_out/r4_tests34.log 2>&1; echo "ri tests rc=$?"; tail -2 gpurun_out/r4_tests34.log
+mkdir -p gpurun_out/final
+for cfg in c1 c2 c2nc; do
+  timeout -k 10 300 python3 bench.py --config $cfg > gpurun_out/final/r04${cfg}_bench.json 2> gpurun_out/final/$cfg.err || { echo "$cfg failed"; exit 1; }
+  python3 -c "import json; d=json.loads(open('gpurun_out/final/r04${cfg}_bench.json').read().strip().splitlines()[-1]); print('$cfg', round(d['ms_per_step'],3), d['value'])"
+done
