@@ -83,7 +83,13 @@ typedef struct {
     uint32_t _pad;
 } srt_path;
 
-typedef enum { SRT_ALGO_AUTO = 0, SRT_ALGO_FW = 1, SRT_ALGO_SSSP = 2 } srt_algo;
+/* FW: blocked min-plus Floyd-Warshall on the latencies + the exact-loss fold
+ * (dense graphs); SSSP: batched multi-source sweeps (sparse graphs); LEVEL:
+ * per-source bucket (Dial) Dijkstra over the edges of at most B units, B a
+ * proved bound on every shortest path (dense graphs of small diameter in units
+ * of the latency gcd); AUTO: the cheapest that applies, priced from measured
+ * rates (the plan description names the choice and the prices) */
+typedef enum { SRT_ALGO_AUTO = 0, SRT_ALGO_FW = 1, SRT_ALGO_SSSP = 2, SRT_ALGO_LEVEL = 3 } srt_algo;
 
 typedef struct {
     uint32_t algo;   /* srt_algo */
@@ -332,11 +338,13 @@ void srt_routing_info_destroy(srt_routing_info *ri);
  * simulator can call it first thing in main and parse its config and GML
  * graph meanwhile.  Every build (and srt_init) waits for a pending init.
  * Idempotent; errors of an async init surface in the next srt_init call.
- * A process that may exit before its first build calls srt_init before exit
- * (the Python package does so from its atexit): the library's own exit-time
- * join can run after runtime statics the init thread created have gone. */
+ * Exit during an async init is safe without the caller's help: the calling
+ * thread's exit (return from main, exit()) joins the init thread before any
+ * atexit handler or static destructor runs.  srt_init_wait only waits for a
+ * pending async init (no device work). */
 srt_status srt_init(int device, srt_err *err);
 void srt_init_async(int device);
+void srt_init_wait(void);
 
 /* --------------------------------------------------------------- GML ingest */
 /* Parses Shadow GML text (gml-parser grammar + NetworkGraph validation) into a

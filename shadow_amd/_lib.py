@@ -21,7 +21,7 @@ SRT_ERR_OOM = 6
 SRT_ERR_UNSUPPORTED = 7
 SRT_ERR_COMM = 8
 
-SRT_ALGO_AUTO, SRT_ALGO_FW, SRT_ALGO_SSSP = 0, 1, 2
+SRT_ALGO_AUTO, SRT_ALGO_FW, SRT_ALGO_SSSP, SRT_ALGO_LEVEL = 0, 1, 2, 3
 SRT_OPT_SAME_DEVICE = 1  # srt_opts.flags: every n_gpus rank on `device` (tests)
 PDS_NONE, PDS_INET_SENT, PDS_INET_DROPPED = 0, 1 << 8, 1 << 9
 
@@ -126,6 +126,7 @@ SIGNATURES = {
     "srt_routing_info_copy_table": (None, [_vp, C.POINTER(SrtPath)]),
     "srt_init": (C.c_int, [C.c_int, _errp]),
     "srt_init_async": (None, [C.c_int]),
+    "srt_init_wait": (None, []),
     "srt_routing_info_destroy": (None, [_vp]),
     "srt_gml_parse": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(_vp), _errp]),
     "srt_gml_csr": (C.c_int, [_vp, C.POINTER(SrtCsr)]),
@@ -177,18 +178,15 @@ _exit_wait = []
 def init_async(device: int = -1) -> None:
     """srt_init_async: the same on a library thread; the next build waits for it.
 
-    A Python exit waits for the pending init first (srt_init joins it), before
-    the interpreter's finalisation and the C-level exit: the library's own
-    atexit join runs after the destructors of runtime statics that the init
-    thread constructs lazily (registered later than that handler), and a
-    process exiting mid-init could reach them first (an intermittent SIGSEGV
-    at exit, seen once in the r04 GPU suite)."""
+    Exit mid-init is safe in the library itself (the calling thread's exit
+    joins the init thread before any static destructor runs); the package
+    also waits (srt_init_wait: no device work) before the interpreter's
+    finalisation, so the join never overlaps it."""
     if not _exit_wait:
         import atexit
 
-        def _wait(dev=int(device)):
-            err = SrtErr()
-            lib().srt_init(dev, C.byref(err))  # waits; a failed async init only reports
+        def _wait():
+            lib().srt_init_wait()
 
         atexit.register(_wait)
         _exit_wait.append(_wait)

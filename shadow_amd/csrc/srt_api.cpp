@@ -647,6 +647,13 @@ double price_fw(uint32_t Vp, uint32_t n, uint32_t V, int key_type, bool f16, boo
     const double relax = (double)Vp * Vp * Vp * (tri ? 0.5 : 1.0);
     return std::max(relax / rate, (double)(Vp / 128) * 80e-6) + (double)n * V * 2.6e-11;
 }
+// Level solve: a row walks the probe row's edge count plus ~4 passes over
+// the row's V levels (init, the level collections), at the level fold's
+// measured cost per visit (C3: 4.56 ms for 16k rows of ~160k visits), and
+// writes its 12-byte table row.
+double price_level(uint32_t n, uint32_t V, uint64_t visits) {
+    return (double)n * ((double)visits + 4.0 * V) * 1.8e-12 + (double)n * n * 12.0 / 5e12 + 3e-4;
+}
 double price_sparse(uint32_t n, uint64_t n_in, uint32_t V, bool frontier) {
     const double units = (double)n * ((double)n_in + V);
     const double per = frontier ? 1.19e-11 : 1.73e-11;  // C4: 9e10 units in 1.07 s / 1.56 s
@@ -782,6 +789,9 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
                             srt_plan **plan_out, srt_err *err, bool defer_loss) {
     clear_err(err);
     srt::init_wait();  // a pending srt_init_async finishes before any device work
+    // plans an earlier one-call build queued for teardown free their HBM
+    // before this plan sizes itself (hipMemGetInfo) or allocates anything
+    reap_drain();
     Trace tr;
     if (!g || !plan_out || (n && !nodes) || !g->row_ptr || (g->n_adj && (!g->col || !g->lat_ns || !g->loss))) {
         set_err(err, SRT_ERR_INVALID, "null argument");
@@ -954,31 +964,71 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     const bool sssp_ok = sssp_params(cs, p->V, &why_sssp);
     p->sssp_g = cs.gcd;
     const uint32_t want = opts ? opts->algo : (uint32_t)SRT_ALGO_AUTO;
+    if (want > SRT_ALGO_LEVEL) return fail(SRT_ERR_INVALID, "unknown srt_opts.algo");
+    // 3a. the level solve (srt_loss.hip level_solve_kernel): asked for, or
+    //     AUTO on a graph whose row fits LDS.  The probe proves B, a bound
+    //     on every in-use shortest path over the edges <= min(31, max edge)
+    //     units; the solve applies when one was found (B <= 31).
+    uint64_t lvl_bound = ~0ull, lvl_visits = 0;
+    std::string why_lvl = "the level solve needs V <= 18400 and every shortest path <= 31 latency units";
+    {
+        const uint64_t maxu = cs.maxlat / cs.gcd;
+        const bool fits = p->V >= 2 && p->V <= srt::LEVEL_V_MAX && n >= 1;
+        const char *kl = std::getenv("SRT_LEVEL");  // knob: 0 keeps AUTO off the level solve (A/B, tests)
+        const bool try_lvl = fits && maxu >= 1 &&
+                             (want == SRT_ALGO_LEVEL || (want == SRT_ALGO_AUTO && !(kl && std::atoi(kl) == 0)));
+        if (try_lvl) {
+            p->kp.g = cs.gcd;
+            srt_err e2{};
+            if (srt::level_probe(p, std::min<uint64_t>(31, maxu), &lvl_bound, &lvl_visits, &e2) != SRT_OK) {
+                srt_plan_destroy(p);
+                if (err) *err = e2;
+                return e2.code ? (srt_status)e2.code : SRT_ERR_HIP;
+            }
+            // the probe's lists were sized for it; the run builds its own
+            p->t_edges = 0;
+        }
+    }
+    const bool lvl_ok = lvl_bound != ~0ull;
+    tr.mark("create: level probe");
     int algo = -1;
     std::string auto_note;
     if (want == SRT_ALGO_FW) {
         if (fw_ok) algo = SRT_ALGO_FW;
     } else if (want == SRT_ALGO_SSSP) {
         if (sssp_ok) algo = SRT_ALGO_SSSP;
-    } else if (want == SRT_ALGO_AUTO) {
+    } else if (want == SRT_ALGO_LEVEL) {
+        if (lvl_ok) algo = SRT_ALGO_LEVEL;
+    } else {
         const uint64_t maxu = cs.maxlat / cs.gcd;
         const unsigned __int128 lb = ecc_units != ~0ull ? (unsigned __int128)ecc_units
                                                         : (unsigned __int128)(p->V ? p->V - 1 : 0) * maxu;
         const double t_fw = fw_ok ? price_fw(p->Vp, n, p->V, p->key_type, f16, cs.sym_a == cs.sym_b) : 1e300;
         const double t_sssp = sssp_ok ? price_sparse(n, n_in, p->V, lb < 0xffff) : 1e300;
-        char pr[96];
-        std::snprintf(pr, sizeof pr, " auto-price=fw:%.3gms,sparse:%.3gms", t_fw < 1e299 ? t_fw * 1e3 : -1.0,
-                      t_sssp < 1e299 ? t_sssp * 1e3 : -1.0);
+        const double t_lvl = lvl_ok ? price_level(n, p->V, lvl_visits) : 1e300;
+        char pr[128];
+        std::snprintf(pr, sizeof pr, " auto-price=fw:%.3gms,sparse:%.3gms,level:%.3gms", t_fw < 1e299 ? t_fw * 1e3 : -1.0,
+                      t_sssp < 1e299 ? t_sssp * 1e3 : -1.0, t_lvl < 1e299 ? t_lvl * 1e3 : -1.0);
         auto_note = pr;
-        if (fw_ok || sssp_ok) algo = t_sssp < t_fw ? SRT_ALGO_SSSP : SRT_ALGO_FW;
-    } else {
-        return fail(SRT_ERR_INVALID, "unknown srt_opts.algo");
+        if (fw_ok || sssp_ok || lvl_ok)
+            algo = t_lvl <= std::min(t_fw, t_sssp) ? SRT_ALGO_LEVEL : t_sssp < t_fw ? SRT_ALGO_SSSP : SRT_ALGO_FW;
     }
     if (algo < 0) {
-        const std::string why = want == SRT_ALGO_SSSP ? why_sssp : want == SRT_ALGO_FW ? why_fw : why_fw + "; " + why_sssp;
+        const std::string why = want == SRT_ALGO_SSSP ? why_sssp
+                                : want == SRT_ALGO_FW ? why_fw
+                                : want == SRT_ALGO_LEVEL ? why_lvl
+                                                         : why_fw + "; " + why_sssp;
         return fail(SRT_ERR_UNSUPPORTED, ("no exact path key for this graph: " + why).c_str());
     }
     p->algo = algo;
+    if (algo == SRT_ALGO_LEVEL) {
+        // levels are exact integers <= B in units of g: 2-byte download records
+        p->kp.g = cs.gcd;
+        p->kp.lmax = lvl_bound;
+        p->kp.lat32 = true;
+        p->key_type = srt::KEY_U16;
+        f16 = false;
+    }
     // SSSP plans read their in-edges (with loss) from the host-built list, never
     // d_loss: drop the deferred upload so run_tail does not copy it
     if (algo == SRT_ALGO_SSSP) {
@@ -990,7 +1040,11 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     p->row1 = n;
     p->rows_alloc = n;
     char d[200];
-    if (algo == SRT_ALGO_FW) {
+    if (algo == SRT_ALGO_LEVEL) {
+        std::snprintf(d, sizeof d, "level:u16 g=%llu lmax=%llu(probe) V=%u n=%u visits=%llu loss=in-solve",
+                      (unsigned long long)p->kp.g, (unsigned long long)p->kp.lmax, p->V, n,
+                      (unsigned long long)lvl_visits);
+    } else if (algo == SRT_ALGO_FW) {
         p->fw_f16 = f16 && p->fw_glds;
         if (const char *e = std::getenv("SRT_FW_P1")) p->fw_p1 = std::atoi(e);
         if (const char *e = std::getenv("SRT_FW_EMULATE_RANKS")) p->emulate_ranks = (uint32_t)std::atoi(e);
@@ -1269,6 +1323,7 @@ srt_status run_closure(srt_plan *p, srt_err *err) {
     const int rank = p->comm ? p->comm->rank : 0;
     unsigned long long *rstats = p->comm ? p->d_rstats + 2 * rank : p->d_stats;
     if (p->algo == SRT_ALGO_SSSP) return srt::sssp_run(p, rstats, err);
+    if (p->algo == SRT_ALGO_LEVEL) return SRT_OK;  // no closure: the rows are solved in run_tail (level_run)
     // N-rank emulation (measurement only): the first run closes D for
     // real; later runs replay rank 0's schedule on the closed D (every
     // round leaves a closed D unchanged, and the kernels' cost does not
@@ -1372,7 +1427,7 @@ srt_status srt_plan_sync(srt_plan *p, srt_err *err) {
     for (uint64_t i = 0; i < p->p3_launches; ++i) {
         if (hipEventElapsedTime(&ms, p->ev[2 * i], p->ev[2 * i + 1]) == hipSuccess) p->p3_ms += ms;
     }
-    if (p->algo == SRT_ALGO_FW && p->ev_loss0 && hipEventElapsedTime(&ms, p->ev_loss0, p->ev_loss1) == hipSuccess)
+    if (p->algo != SRT_ALGO_SSSP && p->ev_loss0 && hipEventElapsedTime(&ms, p->ev_loss0, p->ev_loss1) == hipSuccess)
         p->loss_ms = ms;
     return SRT_OK;
 }
@@ -1457,7 +1512,7 @@ srt_status srt_plan_timing(const srt_plan *p, srt_timing *o) {
     o->dominant_launches = p->p3_launches;
     o->dominant_work = p->p3_work;
     o->loss_ms = p->loss_ms;
-    o->tight_edges = p->algo == SRT_ALGO_FW ? p->t_edges : 0;
+    o->tight_edges = p->algo != SRT_ALGO_SSSP ? p->t_edges : 0;  // level solve: the pruned edges
     o->sharded_tail = p->algo == SRT_ALGO_FW && p->shard_tail ? 1u : 0u;
     o->sparse_split = 0u;  // the split sweep was removed (reserved)
     o->sparse_sweeps = p->algo == SRT_ALGO_SSSP ? p->sssp_sweeps : 0;
@@ -1583,7 +1638,7 @@ srt_status srt_plan_bind_comm(srt_plan *p, srt_comm *comm, srt_err *err) {
         char d[64];
         std::snprintf(d, sizeof d, " ranks=%d rows=[%u,%u)", comm->nranks, p->row0, p->row1);
         p->desc += d;
-        if (p->algo == SRT_ALGO_SSSP) return SRT_OK;
+        if (p->algo != SRT_ALGO_FW) return SRT_OK;  // row-sharded families: no closure block-rows
     }
     // pad the node range so every rank owns the same number of block-rows
     // (equal all-gather chunks); padded nodes are isolated and never in use
@@ -2004,7 +2059,8 @@ srt_status build_e2e(const srt_csr *g, const uint32_t *nodes, uint32_t n, srt_pa
     if (s != SRT_OK) return s;
     // one-GPU dense build with a table wanted: the fold runs in chunks of <= 64
     // Mi entries whose downloads overlap the next chunk's fold
-    const bool pipe = (out || ct) && p->n && p->algo == SRT_ALGO_FW && !p->comm && p->emulate_ranks <= 1;
+    const bool pipe = (out || ct) && p->n && (p->algo == SRT_ALGO_FW || p->algo == SRT_ALGO_LEVEL) && !p->comm &&
+                      p->emulate_ranks <= 1;
     if (pipe)
         p->fold_chunk_rows = (uint32_t)std::max<uint64_t>(
             1, std::min<uint64_t>((uint64_t)p->n * p->n, 1ull << 26) / p->n);
@@ -2082,10 +2138,20 @@ struct InitState {
 };
 InitState g_init;
 
-// The async init's thread is joined before the process's HIP runtime is torn
-// down: srt_init_async starts the runtime on the caller's thread first, then
-// registers this handler (atexit handlers run before the destructors of statics
-// constructed earlier), so a process that never builds still exits cleanly.
+// Exit while the async init runs.  glibc's exit() (also a return from main)
+// first runs the EXITING thread's thread_local destructors, and only then the
+// atexit / static-destructor list in reverse order of registration.  That
+// list is no safe place to join: the init thread registers destructors of its
+// own (the runtime's lazily built statics, code-object loaders) after any
+// handler srt_init_async could register, so those would run first, under the
+// still-running thread.  So srt_init_async plants a thread_local guard on the
+// calling thread (Shadow's main) whose destructor joins the init: it runs
+// before anything is destroyed.  On a thread that merely ends it also joins
+// (that thread waits for the init; harmless).  The atexit join stays for a
+// process that exits from another thread.
+struct InitExitGuard {
+    ~InitExitGuard() { srt::init_wait(); }
+};
 void join_init_at_exit() { srt::init_wait(); }
 
 srt_status init_device(int device, std::string *msg) {
@@ -2175,6 +2241,8 @@ srt_status srt_init(int device, srt_err *err) {
     return SRT_OK;
 }
 
+void srt_init_wait(void) { srt::init_wait(); }
+
 void srt_init_async(int device) {
     static std::once_flag reg;
     std::call_once(reg, [] {
@@ -2182,6 +2250,8 @@ void srt_init_async(int device) {
         (void)hipGetDeviceCount(&count);
         std::atexit(join_init_at_exit);
     });
+    static thread_local InitExitGuard guard;  // joins at this thread's exit / exit()
+    (void)&guard;
     std::lock_guard<std::mutex> lk(g_init.m);
     if (g_init.pending) return;
     g_init.pending = true;

@@ -302,10 +302,23 @@ srt_status srt_comm_init_local(int nranks, const int32_t *devices, srt_comm **co
         delete G;
         return SRT_ERR_HIP;
     }
+    // every comm made holds one reference; on a failed allocation the
+    // references of the comms not made are dropped first, so destroying the
+    // made ones frees G (and its events) with the last of them
+    G->refs = nranks;
     for (int r = 0; r < nranks; ++r) {
         srt_comm *c = new (std::nothrow) srt_comm();
         if (!c) {
-            for (int q = 0; q < r; ++q) srt_comm_destroy(comms[q]);
+            if (r == 0) {
+                for (hipEvent_t ev : G->ready)
+                    if (ev) (void)hipEventDestroy(ev);
+                for (hipEvent_t ev : G->done)
+                    if (ev) (void)hipEventDestroy(ev);
+                delete G;
+            } else {
+                G->refs = r;
+                for (int q = 0; q < r; ++q) srt_comm_destroy(comms[q]);
+            }
             set_err(err, SRT_ERR_OOM, "out of host memory");
             return SRT_ERR_OOM;
         }
@@ -314,7 +327,6 @@ srt_status srt_comm_init_local(int nranks, const int32_t *devices, srt_comm **co
         c->local = G;
         comms[r] = c;
     }
-    G->refs = nranks;
     if (err) std::memset(err, 0, sizeof *err);
     return SRT_OK;
 }

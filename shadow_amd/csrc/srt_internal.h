@@ -43,6 +43,9 @@ struct KeyParams {
 
 // FW tile geometry: B x B blocks, one block-row/column per round.
 constexpr int FW_B = 128;
+// level solve (SRT_ALGO_LEVEL): the row (u16 level, f32 loss, u16 member per
+// vertex) in the 160 KB LDS beside the 8 KB level table
+constexpr uint32_t LEVEL_V_MAX = 18400;
 
 // In-edge of the sparse SSSP (srt_sssp.hip): the source vertex u of an
 // adjacency entry u -> v, its latency in units of g and 1 - loss rounded to f32
@@ -389,6 +392,11 @@ srt_status fw_gather_keys(srt_plan *p, srt_err *err);
 // table rows, the raw self-loop diagonal and (min latency, unreachable) into
 // d_stats
 srt_status fw_loss(srt_plan *p, unsigned long long *d_stats, srt_err *err);
+// level solve (srt_loss.hip, SRT_ALGO_LEVEL): the create-time bound on every
+// in-use shortest path over the edges <= wmax units (~0: none; visits: edges a
+// row walks), and the build of rows [row0, row1) into the table
+srt_status level_probe(srt_plan *p, uint64_t wmax, uint64_t *bound, uint64_t *visits, srt_err *err);
+srt_status level_run(srt_plan *p, unsigned long long *d_stats, srt_err *err);
 // sharded tail: every rank's staged rows (d_slat / d_sloss, all-gathered) into the table
 void expand_shard_rows(srt_plan *p, int nranks);
 // table entries [first, first + count) -> d_pack[0, count) as srt_path

@@ -275,6 +275,86 @@ __global__ __launch_bounds__(256) void tight_rows_kernel(const K *__restrict__ D
     }
 }
 
+// Level solve (the closure-free dense path, see level_solve_kernel): the
+// adjacency entries u -> v (v != u) of latency <=
+// wmax units, straight into the list as records {v, u, w, 1f32 - e bits} (0
+// bits without losses: the create-time probe needs no loss).  Same two passes
+// and cap protocol as tight_rows_kernel; the latency is tested first and the
+// column loaded only for the lanes that pass (C3: ~3% of the entries).
+template <bool WITH_LOSS>
+__global__ __launch_bounds__(256) void prune_rows_kernel(uint32_t V, const uint64_t *__restrict__ row_ptr,
+                                                         const uint32_t *__restrict__ col,
+                                                         const uint64_t *__restrict__ lat,
+                                                         const float *__restrict__ loss, uint64_t g, uint64_t wmax_ns,
+                                                         uint4 *__restrict__ list, uint64_t cap,
+                                                         unsigned long long *cursor, unsigned long long *maxw,
+                                                         unsigned long long *total) {
+    __shared__ uint64_t bal[4][TR_CH];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    uint64_t mw = 0, tot = 0, mnw = ~0ull;
+    auto test = [&](uint32_t u, uint64_t k, uint64_t e) -> bool {
+        if (k >= e) return false;
+        const uint64_t l = lat[k];
+        return l <= wmax_ns && col[k] != u;
+    };
+    for (uint32_t u = wave; u < V; u += nwaves) {
+        const uint64_t b = row_ptr[u], e = row_ptr[u + 1];
+        const uint32_t nch = (uint32_t)((e - b + 63) / 64);
+        uint32_t cnt = 0;
+        for (uint32_t c0 = 0; c0 < nch; c0 += 4) {
+            uint64_t l[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint64_t k = b + 64ull * (c0 + q) + lane;
+                l[q] = k < e ? lat[k] : ~0ull;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint64_t k = b + 64ull * (c0 + q) + lane;
+                const bool f = l[q] <= wmax_ns && col[k] != u;  // col only where the latency passes
+                const uint64_t m = __ballot(f);
+                if (f) {
+                    const uint64_t w = l[q] / g;
+                    mw = w > mw ? w : mw;
+                    mnw = w < mnw ? w : mnw;
+                }
+                if (c0 + q < TR_CH && lane == 0) bal[wv][c0 + q] = m;
+                cnt += (uint32_t)__popcll(m);
+            }
+        }
+        if (!cnt) continue;
+        tot += cnt;
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(cursor, (unsigned long long)cnt);
+        base = __shfl(base, 0);
+        if (base + cnt > cap) continue;  // uniform: the caller grows the list and runs again
+        for (uint32_t c = 0; c < nch; ++c) {
+            const uint64_t k = b + 64ull * c + lane;
+            const uint64_t m = c < TR_CH ? bal[wv][c] : __ballot(test(u, k, e));
+            if (!m) continue;  // uniform
+            if ((m >> lane) & 1ull) {
+                const uint64_t pos = base + __popcll(m & ((1ull << lane) - 1ull));
+                const float eb = WITH_LOSS ? 1.0f - loss[k] : 0.0f;  // (1f32 - other.packet_loss), mod.rs:328
+                list[pos] = make_uint4(col[k], u, (uint32_t)(lat[k] / g), __float_as_uint(eb));
+            }
+            base += __popcll(m);
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(mw, off);
+        mw = o > mw ? o : mw;
+        const uint64_t o2 = __shfl_xor(mnw, off);
+        mnw = o2 < mnw ? o2 : mnw;
+    }
+    if (lane == 0 && mw) atomicMax(maxw, (unsigned long long)mw);
+    if (lane == 0 && tot) {
+        atomicAdd(total, (unsigned long long)tot);
+        atomicMax(total + 1, (unsigned long long)~mnw);
+    }
+}
+
 // Per-row counts of a tight-edge list (v = ~0: padding): rows by target v
 // (pull CSR) or, BY_SRC, by source u (push CSR)
 template <bool BY_SRC>
@@ -1231,6 +1311,293 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
     }
 }
 
+// ------------------------------------------------------------ level solve
+// Closure-free dense build (SRT_ALGO_LEVEL): petgraph's Dijkstra per source
+// (mod.rs:195-198) as a bucket queue with unit-wide buckets -- Dial's
+// algorithm -- over the graph's edges of latency <= B units, where B bounds
+// every shortest path (the create-time probe: out- plus in-eccentricity of one
+// in-use node, level_probe).  No edge longer than B can lie on a shortest
+// path, so the pruned graph has the same distances and the same tight edges.
+// Latencies are integers in units of g >= 1, so the bucket of level l holds
+// exactly N_l = {v : L(s,v) = l}, final once every level j < l is: its members
+// are the heads of the class-(l - j) edges out of N_j.  For each class w the
+// candidates of level l are walked from the smaller end, as in the level fold
+// above: push along class-w out-edges of N_{l-w}, or -- when the still
+// unsettled set U_l is smaller -- pull along class-w in-edges of every u in
+// U_l, testing the tail's level.  A hit sets the head's level to l (a plain
+// store: every writer stores l) and min-folds the loss candidate
+// 1 - (1 - loss[u]) (1 - e) into it by an LDS atomic on the f32 bits: the tails
+// are final, so the result is the min over tight in-edges, the same bits as the
+// reference's lexicographic (latency, loss) Dijkstra (the level fold's
+// argument).  One workgroup per table row; LDS: level u16, loss f32, and
+// the settled vertices in level order u16 (8 B a vertex, as the level fold).
+// C3 (16k complete graph, latencies 1-300 ms): B = 8, levels of ~1 / 60 /
+// 3,000 / 13,000 / few vertices, ~175k edge visits a row against 16,384^2 / 2
+// relaxations a row for the triangle Floyd-Warshall.
+// probe != nullptr: no table; probe[k] = the largest level over the in-use
+// columns of row k (0xffff if one is unreached by level lcap), probe[2] +=
+// the edges walked.
+template <int LPT, int UNR, uint32_t CLSN, int VW>
+__global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
+    uint32_t V, const uint32_t *__restrict__ nodes, uint32_t n, uint32_t row0, uint32_t row1,
+    const uint32_t *__restrict__ cls_out, const uint32_t *__restrict__ cls_in, const uint64_t *__restrict__ ce_out,
+    const uint64_t *__restrict__ ce_in, uint32_t lcap, uint64_t g, const uint64_t *__restrict__ sl_lat,
+    const float *__restrict__ sl_loss, uint64_t *__restrict__ out_lat, float *__restrict__ out_loss,
+    unsigned long long *stats, const uint32_t *__restrict__ row_list, void *__restrict__ out32,
+    float *__restrict__ out32_loss, bool stage16, uint32_t *__restrict__ probe) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ unsigned long long red_min[16], red_cnt[16];
+    __shared__ uint32_t red_max[16];
+    constexpr uint32_t WCN = CLSN - 1;
+    __shared__ uint32_t plan_end[WCN + 1];
+    __shared__ uint32_t plan_push, plan_pull;
+    __shared__ uint32_t cur[2][2];  // [level parity]: unsettled compaction, level collection
+    uint32_t *hist = reinterpret_cast<uint32_t *>(smem);  // hist[l]: end of level l in mem
+    uint16_t *lrow = reinterpret_cast<uint16_t *>(smem + HIST_BYTES);
+    const size_t lat_b = ((size_t)V * 2 + 15) & ~(size_t)15;
+    uint32_t *prow = reinterpret_cast<uint32_t *>(smem + HIST_BYTES + lat_b);
+    uint16_t *mem = reinterpret_cast<uint16_t *>(smem + HIST_BYTES + lat_b + (size_t)V * 4);
+    const uint16_t LINF = 0xffffu;
+    const uint32_t FINF = 0x7f800000u;  // +inf bits
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    const int lane = tid & 63, wv = tid >> 6, nw = nt >> 6;
+    const uint32_t grp = tid / LPT, sub = tid % LPT, ngrp = nt / LPT;
+    const uint64_t below = (1ull << lane) - 1ull;
+    uint64_t mn = ~0ull;
+    unsigned long long unreach = 0, visits = 0;
+    const uint32_t nrows = row_list ? row1 : row1 - row0;
+    for (uint32_t k = blockIdx.x; k < nrows; k += gridDim.x) {
+        const uint32_t i = row_list ? row_list[k] : row0 + k;
+        const uint32_t s = nodes[i];
+        // 1. every vertex unreached, s at level 0 (petgraph's zero score)
+        for (uint32_t v = tid; v < V; v += nt) {
+            lrow[v] = v == s ? (uint16_t)0 : LINF;
+            prow[v] = v == s ? 0u : FINF;
+        }
+        if (tid == 0) {
+            hist[0] = 1;
+            mem[0] = (uint16_t)s;
+            cur[1][0] = cur[1][1] = 0;
+        }
+        __syncthreads();
+        uint32_t settled = 1;
+        // 2. levels in increasing latency
+        for (uint32_t l = 1; l <= lcap && settled < V; ++l) {
+            const uint32_t U = V - settled, par = l & 1u;
+            if (tid == 0) {
+                uint32_t run = 0, pm = 0, pl = 0;
+                for (uint32_t w = 1; w <= WCN; ++w) {
+                    uint32_t items = 0;
+                    if (w <= l) {
+                        const uint32_t j = l - w, nj = hist[j] - (j ? hist[j - 1] : 0u);
+                        if (nj && nj <= U) {
+                            pm |= 1u << w;
+                            items = nj;
+                        } else if (nj) {
+                            pl = 1;
+                            items = U;
+                        }
+                    }
+                    run += items;
+                    plan_end[w] = run;
+                }
+                plan_push = pm;
+                plan_pull = pl;
+                cur[par][0] = cur[par][1] = 0;
+            }
+            __syncthreads();
+            const uint32_t T = plan_end[WCN], pm = plan_push;
+            // no tail level l - w (w <= WCN, every class) holds a vertex: the
+            // levels >= l are all empty (uniform)
+            if (T == 0) break;
+            if (plan_pull) {
+                // the unsettled vertices into mem[settled, V) (any order)
+                for (uint32_t base = 0; base < V; base += nt) {
+                    const uint32_t v = base + tid;
+                    const bool f = v < V && lrow[v] == LINF;
+                    const uint64_t m = __ballot(f);
+                    if (!m) continue;  // uniform
+                    uint32_t b = 0;
+                    if (lane == 0) b = atomicAdd(&cur[par][0], (uint32_t)__popcll(m));
+                    b = __shfl(b, 0);
+                    if (f) mem[settled + b + (uint32_t)__popcll(m & below)] = (uint16_t)v;
+                }
+                __syncthreads();
+            }
+            auto item = [&](uint32_t t, uint32_t &w, uint32_t &x, uint32_t &e0, uint32_t &e1) {
+                w = 1;
+                while (t >= plan_end[w]) ++w;
+                const uint32_t m = t - (w > 1 ? plan_end[w - 1] : 0u), j = l - w;
+                const bool push = (pm >> w) & 1u;
+                x = mem[push ? (j ? hist[j - 1] : 0u) + m : settled + m];
+                const uint32_t *cl = push ? cls_out : cls_in;
+                e0 = cl[(uint64_t)x * CLSN + w - 1];
+                e1 = cl[(uint64_t)x * CLSN + w];
+            };
+            uint32_t nw_ = 1, nx = 0, ne0 = 0, ne1 = 0;
+            if (grp < T) item(grp, nw_, nx, ne0, ne1);
+            for (uint32_t t = grp; t < T; t += ngrp) {
+                const uint32_t w = nw_, x = nx, e0 = ne0, e1 = ne1, j = l - w;
+                if (t + ngrp < T) item(t + ngrp, nw_, nx, ne0, ne1);
+                const bool push = (pm >> w) & 1u;
+                const uint64_t *ce = push ? ce_out : ce_in;
+                // push: x in N_j, its class-w out-edges x -> v, v unsettled or at l;
+                // pull: x unsettled, its class-w in-edges u -> x, u in N_j
+                const float onem = push ? 1.0f - __uint_as_float(prow[x]) : 0.0f;
+                constexpr int NE = UNR * VW;
+                for (uint32_t b = VW == 2 ? e0 & ~1u : e0; b < e1; b += UNR * LPT * VW) {
+                    uint64_t wd[NE];
+                    uint32_t ei[NE];
+#pragma unroll
+                    for (int q = 0; q < UNR; ++q) {
+                        const uint32_t at = b + (sub + q * LPT) * VW;  // padded past the end
+                        if (VW == 2) {
+                            const uint4 r2 = *reinterpret_cast<const uint4 *>(ce + at);
+                            wd[2 * q] = ((uint64_t)r2.y << 32) | r2.x;
+                            wd[2 * q + 1] = ((uint64_t)r2.w << 32) | r2.z;
+                            ei[2 * q] = at;
+                            ei[2 * q + 1] = at + 1;
+                        } else {
+                            wd[q] = ce[at];
+                            ei[q] = at;
+                        }
+                    }
+                    uint32_t o[NE];
+                    bool ok[NE];
+#pragma unroll
+                    for (int q = 0; q < NE; ++q) {
+                        ok[q] = ei[q] < e1 && (VW == 1 || ei[q] >= e0);
+                        o[q] = ok[q] ? (uint32_t)wd[q] : 0u;
+                    }
+                    uint16_t lo_[NE];
+#pragma unroll
+                    for (int q = 0; q < NE; ++q) lo_[q] = lrow[o[q]];
+#pragma unroll
+                    for (int q = 0; q < NE; ++q) {
+                        visits += ok[q];
+                        const bool hit = ok[q] && (push ? lo_[q] >= (uint16_t)l : lo_[q] == (uint16_t)j);
+                        if (hit) {
+                            const float r = __uint_as_float((uint32_t)(wd[q] >> 32));
+                            if (push) {
+                                lrow[o[q]] = (uint16_t)l;
+                                atomicMin(&prow[o[q]], __float_as_uint(1.0f - __fmul_rn(onem, r)));
+                            } else {
+                                lrow[x] = (uint16_t)l;
+                                const float c = 1.0f - __fmul_rn(1.0f - __uint_as_float(prow[o[q]]), r);
+                                atomicMin(&prow[x], __float_as_uint(c));
+                            }
+                        }
+                    }
+                }
+            }
+            __syncthreads();  // every head of level l found
+            // N_l (the vertices now at level l) -> mem[settled, ...)
+            for (uint32_t base = 0; base < V; base += nt) {
+                const uint32_t v = base + tid;
+                const bool f = v < V && lrow[v] == (uint16_t)l;
+                const uint64_t m = __ballot(f);
+                if (!m) continue;  // uniform
+                uint32_t b = 0;
+                if (lane == 0) b = atomicAdd(&cur[par][1], (uint32_t)__popcll(m));
+                b = __shfl(b, 0);
+                if (f) mem[settled + b + (uint32_t)__popcll(m & below)] = (uint16_t)v;
+            }
+            __syncthreads();
+            settled += cur[par][1];
+            if (tid == 0) hist[l] = settled;
+        }
+        __syncthreads();  // hist / lrow final for the output
+        // 3. table row i (or staging slot k), or the probe's row maximum
+        if (probe) {
+            uint32_t rmax = 0;
+            for (uint32_t j0 = tid; j0 < n; j0 += nt) {
+                const uint32_t l = lrow[nodes[j0]];
+                rmax = l > rmax ? l : rmax;
+            }
+            for (int off = 32; off > 0; off >>= 1) {
+                const uint32_t o = __shfl_xor(rmax, off);
+                rmax = o > rmax ? o : rmax;
+            }
+            if (lane == 0) red_max[wv] = rmax;
+            __syncthreads();
+            if (tid == 0) {
+                uint32_t m = 0;
+                for (int q = 0; q < nw; ++q) m = red_max[q] > m ? red_max[q] : m;
+                probe[k] = m;
+            }
+            __syncthreads();
+            continue;
+        }
+        uint64_t *ol = out_lat + (uint64_t)i * n;
+        float *op = out_loss + (uint64_t)i * n;
+        uint32_t *o32 = out32 && !stage16 ? reinterpret_cast<uint32_t *>(out32) + (uint64_t)k * n : nullptr;
+        uint16_t *o16 = out32 && stage16 ? reinterpret_cast<uint16_t *>(out32) + (uint64_t)k * n : nullptr;
+        float *o32p = out32_loss ? out32_loss + (uint64_t)k * n : nullptr;
+        for (uint32_t j0 = tid; j0 < n; j0 += 4 * nt) {
+            uint32_t vv[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) vv[q] = j0 + q * nt < n ? nodes[j0 + q * nt] : 0u;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t j = j0 + q * nt;
+                if (j >= n) break;
+                uint64_t latv, lu;
+                float lossv;
+                if (j == i) {
+                    latv = sl_lat[j];
+                    lossv = sl_loss[j];
+                    lu = latv == ~0ull ? ~0ull : latv / g;
+                } else {
+                    const uint16_t l = lrow[vv[q]];
+                    if (l == LINF) {
+                        ++unreach;
+                        latv = lu = ~0ull;
+                        lossv = 1.0f;
+                    } else {
+                        lu = l;
+                        latv = lu * g;
+                        lossv = __uint_as_float(prow[vv[q]]);
+                    }
+                }
+                if (o32p) {
+                    if (o16) o16[j] = latv == ~0ull ? (uint16_t)0xffffu : (uint16_t)lu;
+                    else if (o32) o32[j] = latv == ~0ull ? ~0u : (uint32_t)lu;
+                    o32p[j] = lossv;
+                } else {
+                    ol[j] = latv;
+                    op[j] = lossv;
+                }
+                mn = latv < mn ? latv : mn;
+            }
+        }
+        __syncthreads();  // the next row rewrites the LDS rows
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(mn, off);
+        mn = o < mn ? o : mn;
+        unreach += __shfl_xor(unreach, off);
+        visits += __shfl_xor(visits, off);
+    }
+    if (lane == 0) {
+        red_min[wv] = mn;
+        red_cnt[wv] = probe ? visits : unreach;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long m = red_min[0], c = red_cnt[0];
+        for (int q = 1; q < nw; ++q) {
+            m = red_min[q] < m ? red_min[q] : m;
+            c += red_cnt[q];
+        }
+        if (probe) {
+            if (c) atomicAdd(reinterpret_cast<unsigned long long *>(probe + 2), c);
+        } else {
+            atomicMin(&stats[0], m);
+            if (c) atomicAdd(&stats[1], c);
+        }
+    }
+}
+
 __global__ void loss_stats_init_kernel(unsigned long long *stats, unsigned long long *maxw) {
     stats[0] = ~0ull;
     stats[1] = 0ull;
@@ -1433,6 +1800,57 @@ uint32_t level_q(const srt_plan *p, uint64_t maxw, uint64_t minw) {
     return 0;
 }
 
+// The class CSRs of the list's slots (records {v, u, w, 1-e bits}, v = ~0:
+// padding) at level width p->t_q: out-rows in d_tpk, in-rows in d_tpk2,
+// grouped by (vertex, class floor(w / q)) -- no sort.
+srt_status build_class_csr(srt_plan *p, uint64_t slots, uint64_t maxw, srt_err *err) {
+    hipStream_t M = p->stream;
+    const uint32_t V = p->V;
+    srt_status st;
+    const uint32_t lblocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, (slots + 255) / 256));
+    const uint32_t q = p->t_q;
+    if (q > 1 && p->tcw_cap < 2 * p->t_cap) {  // the exact weights beside the class entries
+        (void)hipFree(p->d_tcw);
+        p->d_tcw = nullptr;
+        p->tcw_cap = 0;
+        const hipError_t e = hipMalloc(&p->d_tcw, 2 * p->t_cap * sizeof(uint32_t));
+        if (e != hipSuccess) return fail(err, e, "hipMalloc(class weights)");
+        p->tcw_cap = 2 * p->t_cap;
+    }
+    const uint32_t mc = q == 1 ? (uint32_t)maxw : (uint32_t)(maxw / q);  // the largest class
+    p->t_cls = mc < 16 ? 16 : 32;
+    const uint32_t cls = p->t_cls;
+    const uint64_t vc1 = (uint64_t)V * cls + 1;
+    uint64_t c1 = p->tcls_cap, c2 = p->tcls_cap;
+    if ((st = grow(&p->d_tcls, &c1, 2 * vc1, err, "hipMalloc(class offsets)")) != SRT_OK ||
+        (st = grow(&p->d_tccnt, &c2, 2 * vc1, err, "hipMalloc(class counts)")) != SRT_OK)
+        return st;
+    p->tcls_cap = std::min(c1, c2);
+    (void)hipMemsetAsync(p->d_tccnt, 0, 2 * vc1 * 4, M);
+    hipLaunchKernelGGL(tcls_count_kernel, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tccnt, vc1, q,
+                       cls);
+    size_t need = 0;
+    hipError_t e = rocprim::exclusive_scan(nullptr, need, p->d_tccnt, p->d_tcls, 0u, (size_t)vc1,
+                                           rocprim::plus<uint32_t>(), M);
+    if (e != hipSuccess) return fail(err, e, "class scan (size)");
+    uint64_t tcap = p->tscan_tmp_cap;
+    if ((st = grow(reinterpret_cast<uint8_t **>(&p->d_tscan_tmp), &tcap, need + 256, err,
+                   "hipMalloc(scan scratch)")) != SRT_OK)
+        return st;
+    p->tscan_tmp_cap = tcap;
+    for (int d = 0; d < 2; ++d) {
+        size_t have = p->tscan_tmp_cap;
+        e = rocprim::exclusive_scan(p->d_tscan_tmp, have, p->d_tccnt + d * vc1, p->d_tcls + d * vc1, 0u,
+                                    (size_t)vc1, rocprim::plus<uint32_t>(), M);
+        if (e != hipSuccess) return fail(err, e, "class scan");
+    }
+    (void)hipMemsetAsync(p->d_tccnt, 0, 2 * vc1 * 4, M);
+    hipLaunchKernelGGL(tcls_fill_kernel, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tcls,
+                       p->d_tccnt, p->d_tpk, p->d_tpk2, vc1, q, q > 1 ? p->d_tcw : nullptr, p->t_cap, cls);
+    p->t_push = false;
+    return SRT_OK;
+}
+
 // Rows of the tight-edge list (slots records, v = ~0: padding, p->t_edges
 // real ones): the class CSRs when the level fold applies (no sort), else the
 // packed push (rows by source) or pull rows sorted by w.
@@ -1440,53 +1858,10 @@ srt_status build_tight_rows(srt_plan *p, uint64_t slots, uint32_t ubits, uint64_
                             uint64_t minw = 0) {
     hipStream_t M = p->stream;
     const uint32_t V = p->V;
-    srt_status st;
     const uint32_t lblocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, (slots + 255) / 256));
     p->t_q = level_q(p, maxw, minw);
     p->t_level = p->t_q != 0;
-    if (p->t_level) {
-        const uint32_t q = p->t_q;
-        if (q > 1 && p->tcw_cap < 2 * p->t_cap) {  // the exact weights beside the class entries
-            (void)hipFree(p->d_tcw);
-            p->d_tcw = nullptr;
-            p->tcw_cap = 0;
-            const hipError_t e = hipMalloc(&p->d_tcw, 2 * p->t_cap * sizeof(uint32_t));
-            if (e != hipSuccess) return fail(err, e, "hipMalloc(class weights)");
-            p->tcw_cap = 2 * p->t_cap;
-        }
-        const uint32_t mc = q == 1 ? (uint32_t)maxw : (uint32_t)(maxw / q);  // the largest class
-        p->t_cls = mc < 16 ? 16 : 32;
-        const uint32_t cls = p->t_cls;
-        const uint64_t vc1 = (uint64_t)V * cls + 1;
-        uint64_t c1 = p->tcls_cap, c2 = p->tcls_cap;
-        if ((st = grow(&p->d_tcls, &c1, 2 * vc1, err, "hipMalloc(class offsets)")) != SRT_OK ||
-            (st = grow(&p->d_tccnt, &c2, 2 * vc1, err, "hipMalloc(class counts)")) != SRT_OK)
-            return st;
-        p->tcls_cap = std::min(c1, c2);
-        (void)hipMemsetAsync(p->d_tccnt, 0, 2 * vc1 * 4, M);
-        hipLaunchKernelGGL(tcls_count_kernel, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tccnt, vc1, q,
-                           cls);
-        size_t need = 0;
-        hipError_t e = rocprim::exclusive_scan(nullptr, need, p->d_tccnt, p->d_tcls, 0u, (size_t)vc1,
-                                               rocprim::plus<uint32_t>(), M);
-        if (e != hipSuccess) return fail(err, e, "class scan (size)");
-        uint64_t tcap = p->tscan_tmp_cap;
-        if ((st = grow(reinterpret_cast<uint8_t **>(&p->d_tscan_tmp), &tcap, need + 256, err,
-                       "hipMalloc(scan scratch)")) != SRT_OK)
-            return st;
-        p->tscan_tmp_cap = tcap;
-        for (int d = 0; d < 2; ++d) {
-            size_t have = p->tscan_tmp_cap;
-            e = rocprim::exclusive_scan(p->d_tscan_tmp, have, p->d_tccnt + d * vc1, p->d_tcls + d * vc1, 0u,
-                                        (size_t)vc1, rocprim::plus<uint32_t>(), M);
-            if (e != hipSuccess) return fail(err, e, "class scan");
-        }
-        (void)hipMemsetAsync(p->d_tccnt, 0, 2 * vc1 * 4, M);
-        hipLaunchKernelGGL(tcls_fill_kernel, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tcls,
-                           p->d_tccnt, p->d_tpk, p->d_tpk2, vc1, q, q > 1 ? p->d_tcw : nullptr, p->t_cap, cls);
-        p->t_push = false;
-        return SRT_OK;
-    }
+    if (p->t_level) return build_class_csr(p, slots, maxw, err);
     (void)hipMemsetAsync(p->d_tcnt, 0, (size_t)V * 4, M);
     // push form: CSR over tight OUT-edges (the pull form over in-edges
     // measured slower and was removed)
@@ -1925,11 +2300,170 @@ srt_status loss_emulated_t(srt_plan *p, unsigned long long *d_stats, srt_err *er
     return SRT_OK;
 }
 
+// ------------------------------------------------------------ level solve
+// The class CSRs of the graph's edges of latency <= wmax units (self-loops
+// dropped): prune_rows_kernel's list (sized by the last run; a larger count
+// grows it and runs again), then build_class_csr at level width 1.
+srt_status level_csr(srt_plan *p, uint64_t wmax, bool with_loss, srt_err *err) {
+    hipStream_t M = p->stream;
+    const uint32_t V = p->V;
+    srt_status st;
+    uint64_t cap_info = p->d_tinfo ? 2 : 0, cap_cur = p->d_tcursor ? 1 : 0, cap_mw = p->d_tmaxw ? 1 : 0;
+    if ((st = grow(&p->d_tinfo, &cap_info, 2, err, "hipMalloc(level info)")) != SRT_OK ||
+        (st = grow(&p->d_tcursor, &cap_cur, 1, err, "hipMalloc(level cursor)")) != SRT_OK ||
+        (st = grow(&p->d_tmaxw, &cap_mw, 1, err, "hipMalloc(level max)")) != SRT_OK)
+        return st;
+    if (!p->h_tcount) {
+        const hipError_t e = hipHostMalloc((void **)&p->h_tcount, 4 * sizeof(uint64_t), 0);
+        if (e != hipSuccess) return fail(err, e, "hipHostMalloc");
+    }
+    const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(8192, (V + 3) / 4));
+    auto rows = [&]() {
+        (void)hipMemsetAsync(p->d_tinfo, 0, 2 * sizeof(unsigned long long), M);
+        (void)hipMemsetAsync(p->d_tcursor, 0, sizeof(unsigned long long), M);
+        (void)hipMemsetAsync(p->d_tmaxw, 0, sizeof(unsigned long long), M);
+        const uint64_t wns = wmax * p->kp.g;
+        if (with_loss)
+            hipLaunchKernelGGL(prune_rows_kernel<true>, dim3(blocks), dim3(256), 0, M, V, p->d_row_ptr, p->d_col,
+                               p->d_lat, p->d_loss, p->kp.g, wns, p->d_tlist, p->d_tlist ? p->tlist_cap : 0ull,
+                               p->d_tcursor, (unsigned long long *)p->d_tmaxw, p->d_tinfo);
+        else
+            hipLaunchKernelGGL(prune_rows_kernel<false>, dim3(blocks), dim3(256), 0, M, V, p->d_row_ptr, p->d_col,
+                               p->d_lat, (const float *)nullptr, p->kp.g, wns, p->d_tlist,
+                               p->d_tlist ? p->tlist_cap : 0ull, p->d_tcursor, (unsigned long long *)p->d_tmaxw,
+                               p->d_tinfo);
+        (void)hipMemcpyAsync(p->h_tcount, p->d_tinfo, sizeof(uint64_t), hipMemcpyDeviceToHost, M);
+        (void)hipMemcpyAsync(p->h_tcount + 1, p->d_tmaxw, sizeof(uint64_t), hipMemcpyDeviceToHost, M);
+        return hipStreamSynchronize(M);
+    };
+    if (!p->d_tlist) {
+        const uint64_t guess = std::max<uint64_t>(1ull << 16, p->n_adj / 16);
+        if ((st = ensure_tlist(p, guess, guess, err)) != SRT_OK) return st;
+    }
+    hipError_t e = rows();
+    if (e != hipSuccess) return fail(err, e, "level edge list");
+    const uint64_t total = p->h_tcount[0], maxw = p->h_tcount[1];
+    if (total > p->tlist_cap) {
+        if ((st = ensure_tlist(p, total + total / 8 + 64, total, err)) != SRT_OK) return st;
+        if ((e = rows()) != hipSuccess) return fail(err, e, "level edge list");
+    }
+    p->t_edges = total;
+    if ((st = ensure_edge_arrays(p, err)) != SRT_OK) return st;
+    p->t_q = 1;
+    p->t_level = true;
+    return build_class_csr(p, total, std::max<uint64_t>(maxw, 1), err);
+}
+
+// level_solve_kernel over the rows of job (probe: the row list's first row,
+// no table, reverse = in- and out-CSRs swapped: distances TO the row's node)
+srt_status launch_solve(srt_plan *p, unsigned long long *d_stats, const RowJob &job, uint32_t lcap, bool reverse,
+                        uint32_t *probe) {
+    const uint32_t V = p->V, rows = job.list ? job.count : job.range ? job.r1 - job.r0 : p->row1 - p->row0;
+    if (!rows) return SRT_OK;
+    const size_t lds = HIST_BYTES + (((size_t)V * 2 + 15) & ~(size_t)15) + (size_t)V * 4 + (size_t)V * 2;
+    const uint32_t nt = V >= 2048 ? LOSS_NT : 256;
+    const int per_cu = std::max(1, std::min(2048 / (int)nt, (int)std::max<size_t>(1, (160 * 1024) / (lds + 2048))));
+    const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(rows, (uint32_t)(cu_count(p->device) * per_cu)));
+    auto kern = p->t_cls == 16 ? level_solve_kernel<4, 4, 16, 2> : level_solve_kernel<4, 2, 32, 2>;
+    (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(LDS_BUDGET - 4096));
+    const uint64_t vc1 = (uint64_t)V * p->t_cls + 1;
+    const uint32_t *co = p->d_tcls, *ci = p->d_tcls + vc1;
+    const uint64_t *eo = p->d_tpk, *ei = p->d_tpk2;
+    if (reverse) {
+        std::swap(co, ci);
+        std::swap(eo, ei);
+    }
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, p->stream, V, p->d_nodes, p->n,
+                       job.list ? 0u : job.range ? job.r0 : p->row0, job.list ? job.count : job.range ? job.r1 : p->row1,
+                       co, ci, eo, ei, lcap, p->kp.g, p->d_sl_lat, p->d_sl_loss, p->d_out_lat, p->d_out_loss, d_stats,
+                       job.list, job.out32, job.out32_loss, p->stage16, probe);
+    return SRT_OK;
+}
+
 }  // namespace
+
+// Create-time proof for the level solve: the pruned graph's (edges <= wmax
+// units) distances from and to the in-use node nodes[0] by two probe rows.
+// Every in-use u, v then has d(u, v) <= d(u, s) + d(s, v) <= in-ecc + out-ecc
+// = *bound (pruned distances bound the real ones from above); ~0 when s misses
+// an in-use node within wmax levels either way.  *visits: edges the forward
+// row walked (the AUTO price).
+srt_status level_probe(srt_plan *p, uint64_t wmax, uint64_t *bound, uint64_t *visits, srt_err *err) {
+    *bound = ~0ull;
+    *visits = 0;
+    if (!p->n) return SRT_OK;
+    srt_status st = level_csr(p, wmax, false, err);
+    if (st != SRT_OK) return st;
+    uint32_t *d_pr = nullptr;
+    hipError_t e = hipMalloc(&d_pr, 8 * sizeof(uint32_t));
+    if (e != hipSuccess) return fail(err, e, "hipMalloc(level probe)");
+    uint32_t h[8] = {};
+    (void)hipMemsetAsync(d_pr, 0, 8 * sizeof(uint32_t), p->stream);
+    RowJob job;
+    job.range = true;
+    job.r0 = 0;
+    job.r1 = 1;
+    const uint32_t cap = (uint32_t)std::min<uint64_t>(wmax, WC);
+    launch_solve(p, nullptr, job, cap, false, d_pr);
+    launch_solve(p, nullptr, job, cap, true, d_pr + 4);
+    e = hipMemcpyAsync(h, d_pr, sizeof h, hipMemcpyDeviceToHost, p->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
+    (void)hipFree(d_pr);
+    if (e != hipSuccess) return fail(err, e, "level probe");
+    uint64_t vis = 0;
+    std::memcpy(&vis, h + 2, 8);
+    *visits = vis;
+    if (h[0] <= cap && h[4] <= cap) *bound = (uint64_t)h[0] + h[4];
+    if (std::getenv("SRT_TRACE"))
+        std::fprintf(stderr, "[srt] level probe: %llu edges <= %llu units, out-ecc %u in-ecc %u, %llu visits a row\n",
+                     (unsigned long long)p->t_edges, (unsigned long long)wmax, h[0], h[4], (unsigned long long)vis);
+    return SRT_OK;
+}
+
+// The level solve's build (SRT_ALGO_LEVEL): the class CSRs of the edges <=
+// kp.lmax units (the probe's bound), then the rows -- in chunks of
+// fold_chunk_rows when the one-call build downloads behind them (ev_fold), as
+// fw_loss's fold.  A sharded plan solves its own rows [row0, row1).
+srt_status level_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
+    if (!p->ev_loss0) {
+        (void)hipEventCreate(&p->ev_loss0);
+        (void)hipEventCreate(&p->ev_loss1);
+    }
+    (void)hipEventRecord(p->ev_loss0, p->stream);
+    p->shard_tail = false;
+    p->tail_expanded = false;
+    p->stage16 = false;
+    srt_status st = level_csr(p, p->kp.lmax, true, err);
+    if (st != SRT_OK) return st;
+    hipLaunchKernelGGL(loss_stats_init_kernel, dim3(1), dim3(1), 0, p->stream, d_stats,
+                       (unsigned long long *)p->d_tmaxw);
+    const uint32_t lcap = (uint32_t)p->kp.lmax;
+    if (p->fold_chunk_rows) {
+        const uint32_t cr = p->fold_chunk_rows, nc = (p->row1 - p->row0 + cr - 1) / cr;
+        while (p->ev_fold.size() < nc) {
+            hipEvent_t e;
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(err, hipErrorUnknown, "event");
+            p->ev_fold.push_back(e);
+        }
+        for (uint32_t c = 0; c < nc; ++c) {
+            RowJob job;
+            job.range = true;
+            job.r0 = p->row0 + c * cr;
+            job.r1 = std::min(p->row1, job.r0 + cr);
+            if ((st = launch_solve(p, d_stats, job, lcap, false, nullptr)) != SRT_OK) return st;
+            (void)hipEventRecord(p->ev_fold[c], p->stream);
+        }
+    } else if ((st = launch_solve(p, d_stats, RowJob{}, lcap, false, nullptr)) != SRT_OK) {
+        return st;
+    }
+    (void)hipEventRecord(p->ev_loss1, p->stream);
+    return SRT_OK;
+}
 
 void expand_shard_rows(srt_plan *p, int nranks) { expand_slots(p, 0, (uint32_t)nranks * p->lrow_max); }
 
 srt_status fw_loss(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
+    if (p->algo == SRT_ALGO_LEVEL) return level_run(p, d_stats, err);
     if (!p->ev_loss0) {
         (void)hipEventCreate(&p->ev_loss0);
         (void)hipEventCreate(&p->ev_loss1);

@@ -156,11 +156,31 @@ def local_comms(devices) -> list:
     return [Comm(C.c_void_p(hs[r])) for r in range(n)]
 
 
-def local_build(graph, nodes, devices, algo: int = _lib.SRT_ALGO_AUTO):
+class LocalPlans:
+    """Every rank's plan of an in-process sharded build, kept on the device
+    (local_build(..., keep=True)): the caller inspects the device tables, then
+    close() destroys the plans before their communicators."""
+
+    def __init__(self, plans, comms):
+        self.plans = plans
+        self._comms = comms
+
+    def close(self):
+        for p in self.plans:
+            if p is not None:
+                p.close()
+        for c in self._comms:
+            c.close()
+        self.plans, self._comms = [], []
+
+
+def local_build(graph, nodes, devices, algo: int = _lib.SRT_ALGO_AUTO, keep: bool = False):
     """The in-process sharded build (what srt_opts.n_gpus does inside the
     library), from Python so tests can inspect every rank's plan: one plan and
     one thread per rank, collectives over srt_comm_init_local.  Returns rank
-    0's table and every rank's plan description and timing."""
+    0's table and every rank's plan description and timing -- or, keep=True,
+    a LocalPlans holding every rank's plan with its table still on the device
+    (nothing fetched)."""
     import threading
 
     from .plan import RoutingPlan
@@ -184,6 +204,7 @@ def local_build(graph, nodes, devices, algo: int = _lib.SRT_ALGO_AUTO):
         t.start()
     for t in ts:
         t.join()
+    kept = LocalPlans(plans, comms)
     try:
         for e in errors:
             if e is not None and not (isinstance(e, _lib.SrtError) and e.code == _lib.SRT_ERR_COMM):
@@ -191,11 +212,11 @@ def local_build(graph, nodes, devices, algo: int = _lib.SRT_ALGO_AUTO):
         for e in errors:
             if e is not None:
                 raise e
+        if keep:
+            kept, out = None, kept
+            return out
         table = plans[0].fetch()
         return table, [p.describe() for p in plans], [p.timing() for p in plans]
     finally:
-        for p in plans:
-            if p is not None:
-                p.close()
-        for c in comms:
-            c.close()
+        if kept is not None:
+            kept.close()

@@ -1,0 +1,183 @@
+"""GPU parity of the level solve (SRT_ALGO_LEVEL, srt_loss.hip
+level_solve_kernel): per-source bucket Dijkstra over the edges of at most B
+latency units, B the create-time probe's bound on every in-use shortest path.
+
+Bar: latency and loss bit-exact against the oracle (the petgraph-faithful
+restatement of mod.rs:183-228), diagonal = the raw self-loop, min latency
+exact; the level tables equal the Floyd-Warshall family's bit for bit; graphs
+the probe cannot bound are refused when LEVEL is forced, and AUTO then takes
+another family with the same result."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from shadow_amd import NetworkGraph, RoutingInfo, _lib, synth
+from shadow_amd import dist as sdist
+from shadow_amd.plan import RoutingPlan
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def _random(n, seed, directed, lat=(1, 9), p_edge=0.08, subset=None):
+    src, dst, l, loss = synth.random_graph(n, seed, p_edge=p_edge, directed=directed, lat_range_ns=lat, loss_max=0.05)
+    g = NetworkGraph.from_edges(n, src, dst, l, loss, directed=directed)
+    rng = np.random.default_rng(seed)
+    nodes = rng.permutation(n).astype(np.uint32)
+    if subset:
+        nodes = nodes[:subset]
+    return g, nodes, O.Graph(directed, np.arange(n), src, dst, l, loss)
+
+
+def _check(t, og, nodes):
+    elat, eloss = O.compute_shortest_paths(og, nodes)
+    assert np.array_equal(t.latency_ns, elat)
+    assert np.array_equal(_bits(t.packet_loss), _bits(eloss))
+    assert t.min_latency_ns == int(elat.min())
+
+
+@pytest.mark.parametrize("n,seed,directed,lat,p_edge,subset", [
+    (40, 1, False, (1, 9), 0.2, None), (300, 2, False, (1, 9), 0.08, None), (300, 3, True, (1, 9), 0.08, None),
+    (1000, 4, False, (1, 20), 0.05, 700), (1000, 5, True, (1, 5), 0.02, None), (2000, 6, False, (1, 31), 0.3, 1500),
+    (777, 7, True, (2, 12), 0.05, 300)])
+def test_level_matches_oracle(n, seed, directed, lat, p_edge, subset):
+    g, nodes, og = _random(n, seed, directed, lat, p_edge, subset)
+    p = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_LEVEL, device=0).run()
+    try:
+        assert p.describe().startswith("level:"), p.describe()
+        _check(p.fetch(), og, nodes)
+    finally:
+        p.close()
+
+
+def test_level_c1_complete_graph_auto():
+    """C1's 1,000-node complete graph (1-300 ms): AUTO takes the level solve
+    (B from the probe, a few ms) and matches the oracle."""
+    n = 1000
+    src, dst, lat, loss = synth.complete_graph(n, 1)
+    g = NetworkGraph.from_edges(n, src, dst, lat, loss)
+    nodes = np.random.default_rng(1).permutation(n).astype(np.uint32)
+    p = RoutingPlan(g, nodes, device=0).run()
+    try:
+        d = p.describe()
+        assert d.startswith("level:") and "auto-price=" in d, d
+        _check(p.fetch(), O.Graph(False, np.arange(n), src, dst, lat, loss), nodes)
+    finally:
+        p.close()
+
+
+@pytest.mark.parametrize("n,drop", [(4096, 0.0), (3000, 0.3)])
+def test_level_equals_fw(n, drop):
+    """C2's 4k complete graph (and a 30%-dropped dense one): the level tables
+    equal the Floyd-Warshall family's bit for bit, on the device."""
+    import torch
+
+    edges = synth.complete_graph(n, 2) if drop == 0.0 else synth.dense_graph(n, 2, drop=drop)
+    g = NetworkGraph.from_edges(n, *edges)
+    nodes = np.arange(n, dtype=np.uint32)
+    a = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_LEVEL, device=0).run()
+    b = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_FW, device=0).run()
+    try:
+        a.fetch(table=False)
+        b.fetch(table=False)
+        assert a.min_latency_ns == b.min_latency_ns
+        la, pa, _ = a.table_ptrs()
+        lb, pb, _ = b.table_ptrs()
+        dev = torch.device("cuda", 0)
+        t = lambda ptr, nb: torch.as_tensor(sdist._CudaBuf(ptr, nb), device=dev)
+        assert torch.equal(t(la, n * n * 8), t(lb, n * n * 8)), "latency"
+        assert torch.equal(t(pa, n * n * 4), t(pb, n * n * 4)), "loss bits"
+        rows = np.random.default_rng(n).choice(n, 6, replace=False)
+        order = np.concatenate([rows, np.setdiff1d(nodes, rows)]).astype(np.uint32)
+        elat, eloss = O.compute_shortest_paths(O.Graph(False, np.arange(n), *edges), order, src_count=6)
+        inv = np.empty(n, np.int64)
+        inv[order] = np.arange(n)
+        L = t(la, n * n * 8).view(torch.int64).view(n, n)
+        P = t(pa, n * n * 4).view(torch.int32).view(n, n)
+        for k, r in enumerate(rows):
+            got_l = L[r].cpu().numpy().view(np.uint64)
+            got_p = P[r].cpu().numpy().view(np.uint32)
+            exp_l, exp_p = elat[k][inv], _bits(eloss[k][inv])
+            m = np.arange(n) != r  # the diagonal: the raw self-loop (checked by the oracle tests)
+            assert np.array_equal(got_l[m], exp_l[m]) and np.array_equal(got_p[m], exp_p[m]), f"row {r}"
+    finally:
+        a.close()
+        b.close()
+
+
+def test_level_refused_when_unbounded_auto_falls_back():
+    """A ring of 100 unit edges: shortest paths up to 50 units, beyond the
+    probe's 31 levels -- forced LEVEL is refused (SRT_ERR_UNSUPPORTED), AUTO
+    builds with another family and matches the oracle."""
+    n = 100
+    src = np.concatenate([np.arange(n), np.arange(n)]).astype(np.uint32)
+    dst = np.concatenate([(np.arange(n) + 1) % n, np.arange(n)]).astype(np.uint32)
+    lat = np.ones(len(src), np.uint64) * np.uint64(synth.MS)
+    loss = np.full(len(src), 0.001, np.float32)
+    g = NetworkGraph.from_edges(n, src, dst, lat, loss)
+    nodes = np.arange(n, dtype=np.uint32)
+    with pytest.raises(_lib.SrtError) as e:
+        RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_LEVEL, device=0)
+    assert e.value.code == _lib.SRT_ERR_UNSUPPORTED
+    p = RoutingPlan(g, nodes, device=0).run()
+    try:
+        assert not p.describe().startswith("level:")
+        _check(p.fetch(), O.Graph(False, np.arange(n), src, dst, lat, loss), nodes)
+    finally:
+        p.close()
+
+
+def test_level_disconnected_in_use_node():
+    """An in-use node no edge reaches: the probe finds no bound (LEVEL is
+    refused), and AUTO's build reports the reference's assert_eq! panic."""
+    n = 50
+    g0, nodes, og = _random(n, 11, False, (1, 9), 0.3)
+    src, dst, lat, loss = og.src, og.dst, og.lat, og.loss
+    keep = (src != 7) & (dst != 7) | ((src == 7) & (dst == 7))
+    g = NetworkGraph.from_edges(n, src[keep], dst[keep], lat[keep], loss[keep])
+    with pytest.raises(_lib.SrtError) as e:
+        RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_LEVEL, device=0)
+    assert e.value.code == _lib.SRT_ERR_UNSUPPORTED
+    with pytest.raises(_lib.SrtError) as e:
+        g.compute_shortest_paths(nodes)
+    assert e.value.code == _lib.SRT_ERR_DISCONNECTED
+
+
+@pytest.mark.parametrize("n", [1000, 2500])
+def test_level_one_call_and_routing_info(n):
+    """The one-call builds (srt_compute_shortest_paths into srt_path,
+    srt_routing_info_build into download records) over the level solve."""
+    src, dst, lat, loss = synth.complete_graph(n, 21)
+    g = NetworkGraph.from_edges(n, src, dst, lat, loss)
+    nodes = np.random.default_rng(n).permutation(n).astype(np.uint32)
+    og = O.Graph(False, np.arange(n), src, dst, lat, loss)
+    t = g.compute_shortest_paths(nodes, algo=_lib.SRT_ALGO_LEVEL)
+    _check(t, og, nodes)
+    ri = RoutingInfo.build(g, nodes, algo=_lib.SRT_ALGO_LEVEL, device=0)
+    try:
+        elat, eloss = O.compute_shortest_paths(og, nodes)
+        rng = np.random.default_rng(3)
+        for _ in range(300):
+            a, b = (int(x) for x in rng.integers(0, n, 2))
+            p = ri.path(int(nodes[a]), int(nodes[b]))
+            if a == b:
+                continue
+            assert p.latency_ns == int(elat[a, b]) and np.float32(p.packet_loss).view(np.uint32) == _bits(eloss[a, b])
+        assert ri.get_smallest_latency_ns() == int(elat.min())
+    finally:
+        ri.close()
+
+
+@pytest.mark.parametrize("world,directed", [(2, False), (3, True), (8, False)])
+def test_level_sharded_rows(world, directed):
+    """Rows sharded over in-process ranks (every rank on device 0): each rank
+    solves its own rows, the rows are all-gathered, rank 0's table is the
+    oracle's."""
+    g, nodes, og = _random(900, 30 + world, directed, (1, 9), 0.05)
+    t, descs, _ = sdist.local_build(g, nodes, [0] * world, algo=_lib.SRT_ALGO_LEVEL)
+    for d in descs:
+        assert d.startswith("level:") and f"ranks={world}" in d, d
+    _check(t, og, nodes)

@@ -183,6 +183,11 @@ def test_init_async_then_exit_without_building():
     code = "import shadow_amd; shadow_amd.init_async(0)"
     r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
+    # straight through ctypes, without the package's atexit wait: the
+    # library's own exit-time join (a thread_local guard) must suffice
+    code = "from shadow_amd import _lib; _lib.lib().srt_init_async(0)"
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
     code = ("import numpy as np, shadow_amd; from shadow_amd import synth, NetworkGraph; "
             "from shadow_amd.plan import RoutingPlan; shadow_amd.init_async(0); "
             "s, d, l, p = synth.complete_graph(8, 1); "
