@@ -92,6 +92,8 @@ def parse_args():
                     help="skip the cold first-call legs (fresh processes) of the dense configs")
     ap.add_argument("--cold-child", dest="cold_child", default="", choices=["", "plain", "init"],
                     help=argparse.SUPPRESS)
+    ap.add_argument("--algo", default="auto", choices=["auto", "fw", "sssp", "level"],
+                    help="kernel family (default: AUTO, the library's priced choice -- what the drop-in runs)")
     ap.add_argument("--emulate-ranks", dest="emulate_ranks", type=int, default=0,
                     help="measurement only (dense FW, 1 GPU): time one rank of an N-rank run -- 1/N of the "
                          "block-rows plus the pivot owner's chain every round, no collectives; the table "
@@ -253,7 +255,10 @@ def timed_builds(plan, D, steps, warmup):
     return elapsed, step_ms, k_ms, k_launches, k_work, k_tiles
 
 
-def e2e_build(g, nodes, reps=3):
+ALGOS = {"auto": 0, "fw": 1, "sssp": 2, "level": 3}
+
+
+def e2e_build(g, nodes, reps=3, algo=0):
     """BASELINE.md t_build: srt_compute_shortest_paths from the host CSR to the
     srt_path table in the caller's (pre-touched, reused) host buffer -- plan
     creation and validation, the CSR upload, the build, the download -- as the
@@ -266,7 +271,7 @@ def e2e_build(g, nodes, reps=3):
     out.view(np.uint8).fill(0)
     nodes = np.ascontiguousarray(nodes, np.uint32)
     csr = g.csr()
-    opts = _lib.SrtOpts(_lib.SRT_ALGO_AUTO, -1, 0, 0)
+    opts = _lib.SrtOpts(algo, -1, 0, 0)
     best, times = None, []
     for _ in range(reps):
         err, mn = _lib.SrtErr(), C.c_uint64()
@@ -285,7 +290,7 @@ def e2e_build(g, nodes, reps=3):
                     "validation, CSR upload, build, table download and plan teardown included"}
 
 
-def routing_info_builds(g, nodes, reps=3):
+def routing_info_builds(g, nodes, reps=3, algo=0):
     """generate_routing_info as Shadow calls it (sim_config.rs:424-461):
     srt_routing_info_build from the host CSR to the RoutingInfo (the table kept
     in its downloaded record form, decoded per path()).  Best of `reps`."""
@@ -294,7 +299,7 @@ def routing_info_builds(g, nodes, reps=3):
     rb = 0
     for _ in range(reps):
         t0 = time.perf_counter()
-        ri = RoutingInfo.build(g, nodes)
+        ri = RoutingInfo.build(g, nodes, algo=algo)
         times.append((time.perf_counter() - t0) * 1e3)
         rb = ri.record_bytes()
         ri.close()
@@ -459,7 +464,7 @@ def bench_graph(args, cfg, D):
         og_args = (src, dst, lat, loss)
     if args.emulate_ranks > 1:
         os.environ["SRT_FW_EMULATE_RANKS"] = str(args.emulate_ranks)
-    plan = RoutingPlan(g, nodes, device=D.dev)
+    plan = RoutingPlan(g, nodes, algo=ALGOS[args.algo], device=D.dev)
     ranks = 1
     transport = None
     if D.world > 1:
@@ -493,8 +498,8 @@ def bench_graph(args, cfg, D):
     n = len(nodes)
     e2e = None
     if args.e2e and D.world == 1 and cfg["kind"] in ("complete", "dense"):
-        e2e = e2e_build(g, nodes)
-        e2e["routing_info"] = routing_info_builds(g, nodes)
+        e2e = e2e_build(g, nodes, algo=ALGOS[args.algo])
+        e2e["routing_info"] = routing_info_builds(g, nodes, algo=ALGOS[args.algo])
         if args.cold:
             e2e["cold"] = cold_calls(args)
     out = None
@@ -503,8 +508,33 @@ def bench_graph(args, cfg, D):
         ms_per_step = elapsed * 1e3 / args.steps
         avg_launch_s = (k_ms / 1e3) / max(k_launches, 1)
         work_per_launch = k_work / max(k_launches, 1)
-        key = desc.split(":")[1][:3] if desc.startswith("fw") else "u64"
-        if desc.startswith("fw"):
+        key = desc.split(":")[1][:3] if desc.startswith(("fw", "level")) else "u64"
+        if desc.startswith("level"):
+            # level solve: the launches write the table (12 B a pair: u64 latency
+            # + f32 loss) and walk the pruned class CSRs (L2/MALL resident)
+            achieved = work_per_launch * 12 / avg_launch_s
+            visits = int(desc.split(" visits=")[1].split()[0])
+            lmax = int(desc.split(" lmax=")[1].split("(")[0])
+            schedule = {"family": "level", "lmax": lmax, "rows_per_launch": int(work_per_launch // max(n, 1))}
+            traffic, traffic_src = measured_traffic(args, "level_solve_kernel", schedule)
+            roofline = {
+                "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK, "traffic": traffic,
+                "traffic_unit": "HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE: gfx950 16-B/lane correction)",
+                "traffic_source": (f"{traffic_src}: committed rocprofv3 PMC summary of this workload and schedule, "
+                                   f"not measured in this run" if traffic_src else
+                                   "no committed PMC summary for this workload/schedule"),
+                "schedule": schedule,
+                "kernel": "level_solve_kernel (per-source bucket Dijkstra over the class CSRs, one workgroup a row)",
+                "avg_launch_ms": avg_launch_s * 1e3, "pairs_per_launch": work_per_launch,
+                "algorithmic_bytes_per_launch": work_per_launch * 12,
+                "basis": "12 B per table pair written (u64 latency + f32 loss); the class CSRs the rows walk "
+                         "(~1e8 B) stay in L2/MALL",
+                "edge_visits_per_row": visits,
+                "edge_visits_per_s": visits * (work_per_launch / max(n, 1)) / avg_launch_s}
+            algo = (f"level solve: per-source bucket (Dial) Dijkstra over the edges <= {lmax} units (a bound proved "
+                    f"by probe rows), loss folded in the same pass")
+        elif desc.startswith("fw"):
             B_TILE = 128
             kbytes = {"f16": 2, "u16": 2, "u32": 4}.get(key, 8)
             achieved = work_per_launch / avg_launch_s

@@ -282,6 +282,7 @@ struct srt_plan {
     uint32_t t_q = 1;                // level width of the fold, units of g (1: exact levels; > 1: quantized)
     uint32_t t_cls = 16;             // class offsets per vertex of the level fold's CSRs (16 or 32)
     uint32_t *d_tcw = nullptr;       // quantized fold: each class entry's exact weight (out, then in), t_cap each
+    uint64_t lvl_cap = 0;            // level solve: class entries d_tpk / d_tpk2 hold (the probe's count)
     uint64_t tcw_cap = 0;            // d_tcw entries
     uint32_t *d_tcls = nullptr;      // 2 * (V*16 + 1) class offsets
     uint32_t *d_tccnt = nullptr;     // 2 * (V*16 + 1) class counts / fill cursors

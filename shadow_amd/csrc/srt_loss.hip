@@ -276,32 +276,37 @@ __global__ __launch_bounds__(256) void tight_rows_kernel(const K *__restrict__ D
 }
 
 // Level solve (the closure-free dense path, see level_solve_kernel): the
-// adjacency entries u -> v (v != u) of latency <=
-// wmax units, straight into the list as records {v, u, w, 1f32 - e bits} (0
-// bits without losses: the create-time probe needs no loss).  Same two passes
-// and cap protocol as tight_rows_kernel; the latency is tested first and the
-// column loaded only for the lanes that pass (C3: ~3% of the entries).
+// class CSRs of the edges u -> v (v != u) of latency <= wmax units, straight
+// from the adjacency.  Out-rows: one wave per adjacency row u (whose entries
+// ARE u's out-edges), two passes -- pass 1 tests each 64-entry chunk (the
+// latency first; the column is loaded only for the lanes that pass: C3 ~2% of
+// the entries) and keeps its ballot in LDS, counting the hits per class by
+// LDS atomics; one global atomic takes the row's range, the row's class
+// offsets are written (slot k: start of class k + 1; slot CLS - 1: the row's
+// end), and pass 2 writes every hit (1f32 - e bits << 32 | v; 0 bits without
+// losses) at its class's running position, and counts it for the in-row of
+// (v, class).  No global atomic per entry on the out side, where a row's ~50
+// entries of a class would all hit one counter.  Entries past `cap` are
+// counted, not written (the caller sizes and runs again).
 template <bool WITH_LOSS>
-__global__ __launch_bounds__(256) void prune_rows_kernel(uint32_t V, const uint64_t *__restrict__ row_ptr,
-                                                         const uint32_t *__restrict__ col,
-                                                         const uint64_t *__restrict__ lat,
-                                                         const float *__restrict__ loss, uint64_t g, uint64_t wmax_ns,
-                                                         uint4 *__restrict__ list, uint64_t cap,
-                                                         unsigned long long *cursor, unsigned long long *maxw,
-                                                         unsigned long long *total) {
+__global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t V, const uint64_t *__restrict__ row_ptr,
+                                                      const uint32_t *__restrict__ col,
+                                                      const uint64_t *__restrict__ lat, const float *__restrict__ loss,
+                                                      uint64_t g, double inv_g, uint64_t wmax_ns, uint32_t cls,
+                                                      uint32_t *__restrict__ off_out, uint32_t *__restrict__ in_cnt,
+                                                      uint64_t *__restrict__ ce_out, uint64_t cap,
+                                                      unsigned long long *cursor, unsigned long long *maxw) {
     __shared__ uint64_t bal[4][TR_CH];
+    __shared__ uint32_t ccnt[4][32];  // per wave: hits per class (pass 1), running positions (pass 2)
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    uint64_t mw = 0, tot = 0, mnw = ~0ull;
-    auto test = [&](uint32_t u, uint64_t k, uint64_t e) -> bool {
-        if (k >= e) return false;
-        const uint64_t l = lat[k];
-        return l <= wmax_ns && col[k] != u;
-    };
+    uint32_t mw = 0;
+    auto cls_of = [&](uint64_t l) -> uint32_t { return (uint32_t)((double)l * inv_g + 0.5); };  // l = c * g exactly
     for (uint32_t u = wave; u < V; u += nwaves) {
         const uint64_t b = row_ptr[u], e = row_ptr[u + 1];
         const uint32_t nch = (uint32_t)((e - b + 63) / 64);
+        if (lane < 32) ccnt[wv][lane] = 0;
         uint32_t cnt = 0;
         for (uint32_t c0 = 0; c0 < nch; c0 += 4) {
             uint64_t l[4];
@@ -316,42 +321,77 @@ __global__ __launch_bounds__(256) void prune_rows_kernel(uint32_t V, const uint6
                 const bool f = l[q] <= wmax_ns && col[k] != u;  // col only where the latency passes
                 const uint64_t m = __ballot(f);
                 if (f) {
-                    const uint64_t w = l[q] / g;
-                    mw = w > mw ? w : mw;
-                    mnw = w < mnw ? w : mnw;
+                    const uint32_t c = cls_of(l[q]);
+                    atomicAdd(&ccnt[wv][c - 1], 1u);
+                    mw = c > mw ? c : mw;
                 }
                 if (c0 + q < TR_CH && lane == 0) bal[wv][c0 + q] = m;
                 cnt += (uint32_t)__popcll(m);
             }
         }
-        if (!cnt) continue;
-        tot += cnt;
+        // cnt is uniform (ballot counts); ccnt complete for this wave's lanes
         unsigned long long base = 0;
-        if (lane == 0) base = atomicAdd(cursor, (unsigned long long)cnt);
+        if (cnt && lane == 0) base = atomicAdd(cursor, (unsigned long long)cnt);
         base = __shfl(base, 0);
-        if (base + cnt > cap) continue;  // uniform: the caller grows the list and runs again
+        const bool fits = base + cnt <= cap;
+        // class offsets of row u: exclusive prefix of the class counts (lanes < cls)
+        uint32_t x = lane < cls ? ccnt[wv][lane] : 0u, incl = x;
+        for (int o = 1; o < 32; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        const uint32_t start = (uint32_t)base + incl - x;
+        if (lane < cls) off_out[(uint64_t)u * cls + lane] = fits ? (lane == cls - 1 ? (uint32_t)(base + cnt) : start) : 0u;
+        if (lane < 32) ccnt[wv][lane] = start;  // running positions
+        if (!cnt || !fits) continue;            // uniform
         for (uint32_t c = 0; c < nch; ++c) {
             const uint64_t k = b + 64ull * c + lane;
-            const uint64_t m = c < TR_CH ? bal[wv][c] : __ballot(test(u, k, e));
+            uint64_t m;
+            if (c < TR_CH) {
+                m = bal[wv][c];
+            } else {
+                const uint64_t l = k < e ? lat[k] : ~0ull;
+                m = __ballot(l <= wmax_ns && col[k] != u);
+            }
             if (!m) continue;  // uniform
             if ((m >> lane) & 1ull) {
-                const uint64_t pos = base + __popcll(m & ((1ull << lane) - 1ull));
+                const uint32_t v = col[k], cl = cls_of(lat[k]);
+                const uint32_t pos = atomicAdd(&ccnt[wv][cl - 1], 1u);
                 const float eb = WITH_LOSS ? 1.0f - loss[k] : 0.0f;  // (1f32 - other.packet_loss), mod.rs:328
-                list[pos] = make_uint4(col[k], u, (uint32_t)(lat[k] / g), __float_as_uint(eb));
+                ce_out[pos] = ((uint64_t)__float_as_uint(eb) << 32) | v;
+                atomicAdd(&in_cnt[(uint64_t)v * cls + cl - 1], 1u);
             }
-            base += __popcll(m);
         }
     }
     for (int off = 32; off > 0; off >>= 1) {
-        const uint64_t o = __shfl_xor(mw, off);
+        const uint32_t o = __shfl_xor(mw, off);
         mw = o > mw ? o : mw;
-        const uint64_t o2 = __shfl_xor(mnw, off);
-        mnw = o2 < mnw ? o2 : mnw;
     }
     if (lane == 0 && mw) atomicMax(maxw, (unsigned long long)mw);
-    if (lane == 0 && tot) {
-        atomicAdd(total, (unsigned long long)tot);
-        atomicMax(total + 1, (unsigned long long)~mnw);
+}
+
+// In-rows of the level solve's class CSRs: every out-entry u -> v of class c
+// (walked per out-row, one wave a row) placed at its (v, c) slot's cursor
+// (in_off: the exclusive scan of lvl_out_kernel's counts) as (1-e) bits << 32 | u.
+__global__ __launch_bounds__(256) void lvl_in_kernel(uint32_t V, uint32_t cls, const uint32_t *__restrict__ off_out,
+                                                     const uint64_t *__restrict__ ce_out,
+                                                     const uint32_t *__restrict__ in_off, uint32_t *__restrict__ in_cur,
+                                                     uint64_t *__restrict__ ce_in) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t u = wave; u < V; u += nwaves) {
+        const uint32_t *ou = off_out + (uint64_t)u * cls;
+        const uint32_t e0 = ou[0], e1 = ou[cls - 1];
+        for (uint32_t k = e0 + lane; k < e1; k += 64) {
+            uint32_t c = 1;  // the class of entry k: the last class whose start is <= k
+            while (c + 1 < cls && ou[c] <= k) ++c;
+            const uint64_t w = ce_out[k];
+            const uint32_t v = (uint32_t)w;
+            const uint64_t slot = (uint64_t)v * cls + c - 1;
+            const uint32_t pos = in_off[slot] + atomicAdd(&in_cur[slot], 1u);
+            ce_in[pos] = (w & 0xffffffff00000000ull) | u;
+        }
     }
 }
 
@@ -934,6 +974,7 @@ __global__ void tcls_fill_kernel(const uint4 *__restrict__ list, uint64_t slots,
 #endif
 #if LOSS_COUNT
 __device__ unsigned long long loss_cnt[9];  // diagnostic builds: items, edge visits, hits, levels, phase ticks x4, push hits
+__device__ unsigned long long lvl_cnt[8][5];  // level solve, per level (<= 7): ticks plan+compact / walk / collect, items, rows
 #endif
 template <int LPT, int UNR, bool QUANT, uint32_t CLSN, int VW>
 __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
@@ -1312,6 +1353,7 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
 }
 
 // ------------------------------------------------------------ level solve
+constexpr size_t SOLVE_HIST = 128;  // level ends, levels <= 31
 // Closure-free dense build (SRT_ALGO_LEVEL): petgraph's Dijkstra per source
 // (mod.rs:195-198) as a bucket queue with unit-wide buckets -- Dial's
 // algorithm -- over the graph's edges of latency <= B units, where B bounds
@@ -1334,17 +1376,17 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
 // C3 (16k complete graph, latencies 1-300 ms): B = 8, levels of ~1 / 60 /
 // 3,000 / 13,000 / few vertices, ~175k edge visits a row against 16,384^2 / 2
 // relaxations a row for the triangle Floyd-Warshall.
-// probe != nullptr: no table; probe[k] = the largest level over the in-use
-// columns of row k (0xffff if one is unreached by level lcap), probe[2] +=
-// the edges walked.
-template <int LPT, int UNR, uint32_t CLSN, int VW>
+// probe != nullptr: no table; probe[2 + k] = the largest level over the
+// in-use columns of row k (0xffff if one is unreached by level lcap), the u64
+// at probe[0] += the edges walked.
+template <int LPT, int UNR, uint32_t CLSN, int VW, int K>
 __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
     uint32_t V, const uint32_t *__restrict__ nodes, uint32_t n, uint32_t row0, uint32_t row1,
     const uint32_t *__restrict__ cls_out, const uint32_t *__restrict__ cls_in, const uint64_t *__restrict__ ce_out,
     const uint64_t *__restrict__ ce_in, uint32_t lcap, uint64_t g, const uint64_t *__restrict__ sl_lat,
     const float *__restrict__ sl_loss, uint64_t *__restrict__ out_lat, float *__restrict__ out_loss,
     unsigned long long *stats, const uint32_t *__restrict__ row_list, void *__restrict__ out32,
-    float *__restrict__ out32_loss, bool stage16, uint32_t *__restrict__ probe) {
+    float *__restrict__ out32_loss, bool stage16, uint32_t *__restrict__ probe, uint32_t ib) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ unsigned long long red_min[16], red_cnt[16];
     __shared__ uint32_t red_max[16];
@@ -1352,11 +1394,14 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
     __shared__ uint32_t plan_end[WCN + 1];
     __shared__ uint32_t plan_push, plan_pull;
     __shared__ uint32_t cur[2][2];  // [level parity]: unsettled compaction, level collection
-    uint32_t *hist = reinterpret_cast<uint32_t *>(smem);  // hist[l]: end of level l in mem
-    uint16_t *lrow = reinterpret_cast<uint16_t *>(smem + HIST_BYTES);
-    const size_t lat_b = ((size_t)V * 2 + 15) & ~(size_t)15;
-    uint32_t *prow = reinterpret_cast<uint32_t *>(smem + HIST_BYTES + lat_b);
-    uint16_t *mem = reinterpret_cast<uint16_t *>(smem + HIST_BYTES + lat_b + (size_t)V * 4);
+    __shared__ uint32_t red_sc[16];
+    uint32_t *hist = reinterpret_cast<uint32_t *>(smem);  // hist[l]: end of level l in mem (l <= 31)
+    uint16_t *lrow = reinterpret_cast<uint16_t *>(smem + SOLVE_HIST);
+    const size_t lat_b = ((size_t)V * 2 + 15) & ~(size_t)15, mem_b = ((size_t)V * 2 + 15) & ~(size_t)15;
+    uint32_t *prow = reinterpret_cast<uint32_t *>(smem + SOLVE_HIST + lat_b);
+    uint16_t *mem = reinterpret_cast<uint16_t *>(smem + SOLVE_HIST + lat_b + (size_t)V * 4);
+    // flattened walk (K > 0): a batch of <= ib items {first pair (prefix), e0, e1, x | w << 16 | push << 24}
+    uint4 *tbl = reinterpret_cast<uint4 *>(smem + SOLVE_HIST + lat_b + (size_t)V * 4 + mem_b);
     const uint16_t LINF = 0xffffu;
     const uint32_t FINF = 0x7f800000u;  // +inf bits
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
@@ -1369,6 +1414,9 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
     for (uint32_t k = blockIdx.x; k < nrows; k += gridDim.x) {
         const uint32_t i = row_list ? row_list[k] : row0 + k;
         const uint32_t s = nodes[i];
+#if LOSS_COUNT
+        unsigned long long tk0 = wall_clock64();
+#endif
         // 1. every vertex unreached, s at level 0 (petgraph's zero score)
         for (uint32_t v = tid; v < V; v += nt) {
             lrow[v] = v == s ? (uint16_t)0 : LINF;
@@ -1380,6 +1428,7 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
             cur[1][0] = cur[1][1] = 0;
         }
         __syncthreads();
+        LOSS_TICK(4)
         uint32_t settled = 1;
         // 2. levels in increasing latency
         for (uint32_t l = 1; l <= lcap && settled < V; ++l) {
@@ -1410,6 +1459,21 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
             // no tail level l - w (w <= WCN, every class) holds a vertex: the
             // levels >= l are all empty (uniform)
             if (T == 0) break;
+#if LOSS_COUNT
+            unsigned long long lt0 = wall_clock64();
+#define LVL_TICK(q)                                                                    \
+    if (tid == 0 && l < 8) {                                                           \
+        const unsigned long long lt1 = wall_clock64();                                 \
+        atomicAdd(&lvl_cnt[l][q], lt1 - lt0);                                          \
+        lt0 = lt1;                                                                     \
+    }
+            if (tid == 0 && l < 8) {
+                atomicAdd(&lvl_cnt[l][3], (unsigned long long)T);
+                atomicAdd(&lvl_cnt[l][4], 1ull);
+            }
+#else
+#define LVL_TICK(q)
+#endif
             if (plan_pull) {
                 // the unsettled vertices into mem[settled, V) (any order)
                 for (uint32_t base = 0; base < V; base += nt) {
@@ -1424,6 +1488,7 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
                 }
                 __syncthreads();
             }
+            LVL_TICK(0)
             auto item = [&](uint32_t t, uint32_t &w, uint32_t &x, uint32_t &e0, uint32_t &e1) {
                 w = 1;
                 while (t >= plan_end[w]) ++w;
@@ -1434,63 +1499,160 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
                 e0 = cl[(uint64_t)x * CLSN + w - 1];
                 e1 = cl[(uint64_t)x * CLSN + w];
             };
-            uint32_t nw_ = 1, nx = 0, ne0 = 0, ne1 = 0;
-            if (grp < T) item(grp, nw_, nx, ne0, ne1);
-            for (uint32_t t = grp; t < T; t += ngrp) {
-                const uint32_t w = nw_, x = nx, e0 = ne0, e1 = ne1, j = l - w;
-                if (t + ngrp < T) item(t + ngrp, nw_, nx, ne0, ne1);
-                const bool push = (pm >> w) & 1u;
-                const uint64_t *ce = push ? ce_out : ce_in;
-                // push: x in N_j, its class-w out-edges x -> v, v unsettled or at l;
-                // pull: x unsettled, its class-w in-edges u -> x, u in N_j
-                const float onem = push ? 1.0f - __uint_as_float(prow[x]) : 0.0f;
-                constexpr int NE = UNR * VW;
-                for (uint32_t b = VW == 2 ? e0 & ~1u : e0; b < e1; b += UNR * LPT * VW) {
-                    uint64_t wd[NE];
-                    uint32_t ei[NE];
+            if constexpr (K > 0) {
+                // Flattened walk: the level's items in batches of ib, their
+                // entries as 16-byte pairs numbered across the batch (an
+                // exclusive scan of the items' pair counts); every wave walks
+                // an equal slice of the pairs, lane-consecutive (coalesced), K
+                // pair loads in flight a lane.  A group of lanes per item (K = 0)
+                // waits one round trip per 2-4 entries a lane and idles on
+                // short items.
+                for (uint32_t tb = 0; tb < T; tb += ib) {
+                    const uint32_t nb = T - tb < ib ? T - tb : ib;
+                    for (uint32_t t = tid; t < nb; t += nt) {
+                        uint32_t w, x, e0, e1;
+                        item(tb + t, w, x, e0, e1);
+                        const uint32_t p0 = e0 >> 1, p1 = e1 > e0 ? ((e1 - 1) >> 1) + 1 : p0;
+                        tbl[t] = make_uint4(p1 - p0, e0, e1, x | (w << 16) | (((pm >> w) & 1u) << 24));
+                    }
+                    __syncthreads();
+                    // exclusive scan of the pair counts (two items a thread, nb <= 2 nt)
+                    const uint32_t a0 = 2 * tid < nb ? tbl[2 * tid].x : 0u, a1 = 2 * tid + 1 < nb ? tbl[2 * tid + 1].x : 0u;
+                    const uint32_t sm = a0 + a1;
+                    uint32_t inc = sm;
+                    for (int o = 1; o < 64; o <<= 1) {
+                        const uint32_t y = __shfl_up(inc, o);
+                        if (lane >= o) inc += y;
+                    }
+                    if (lane == 63) red_sc[wv] = inc;
+                    __syncthreads();
+                    uint32_t woff = 0, P = 0;
+                    for (int q = 0; q < nw; ++q) {
+                        woff += q < wv ? red_sc[q] : 0u;
+                        P += red_sc[q];
+                    }
+                    if (2 * tid < nb) tbl[2 * tid].x = woff + inc - sm;
+                    if (2 * tid + 1 < nb) tbl[2 * tid + 1].x = woff + inc - sm + a0;
+                    __syncthreads();
+                    // this wave's slice of the pairs [pb, pe)
+                    const uint32_t pb = (uint32_t)((uint64_t)P * wv / nw), pe = (uint32_t)((uint64_t)P * (wv + 1) / nw);
+                    // the last item whose first pair is <= pb + lane
+                    uint32_t it = 0;
+                    {
+                        uint32_t lo = 0, hi = nb;  // tbl[lo].x <= p < tbl[hi].x (hi = nb: +inf)
+                        const uint32_t p = pb + lane;
+                        while (hi - lo > 1) {
+                            const uint32_t mid = (lo + hi) >> 1;
+                            if (tbl[mid].x <= p) lo = mid;
+                            else hi = mid;
+                        }
+                        it = lo;
+                    }
+                    for (uint32_t base = pb; base < pe; base += 64 * K) {
+                        uint4 d[K];
+                        uint32_t its[K], q2[K];
 #pragma unroll
-                    for (int q = 0; q < UNR; ++q) {
-                        const uint32_t at = b + (sub + q * LPT) * VW;  // padded past the end
-                        if (VW == 2) {
-                            const uint4 r2 = *reinterpret_cast<const uint4 *>(ce + at);
-                            wd[2 * q] = ((uint64_t)r2.y << 32) | r2.x;
-                            wd[2 * q + 1] = ((uint64_t)r2.w << 32) | r2.z;
-                            ei[2 * q] = at;
-                            ei[2 * q + 1] = at + 1;
-                        } else {
-                            wd[q] = ce[at];
-                            ei[q] = at;
+                        for (int st = 0; st < K; ++st) {
+                            const uint32_t pp = base + st * 64 + lane;
+                            while (it + 1 < nb && tbl[it + 1].x <= pp) ++it;
+                            its[st] = it;
+                            const uint4 tr = tbl[it];
+                            q2[st] = ((tr.y >> 1) + (pp - tr.x)) * 2;  // the pair's first entry
+                            const uint64_t *ce = (tr.w >> 24) ? ce_out : ce_in;
+                            d[st] = pp < pe ? *reinterpret_cast<const uint4 *>(ce + q2[st]) : make_uint4(0, 0, 0, 0);
+                            if (pp >= pe) q2[st] = ~1u;  // no entry
+                        }
+#pragma unroll
+                        for (int st = 0; st < K; ++st) {
+                            const uint4 tr = tbl[its[st]];
+                            const uint32_t x = tr.w & 0xffffu, w = (tr.w >> 16) & 0xffu, j = l - w;
+                            const bool push = tr.w >> 24;
+                            const uint32_t o2[2] = {d[st].x, d[st].z};
+                            const float r2[2] = {__uint_as_float(d[st].y), __uint_as_float(d[st].w)};
+                            const bool ok2[2] = {q2[st] != ~1u && q2[st] >= tr.y && q2[st] < tr.z,
+                                                 q2[st] != ~1u && q2[st] + 1 >= tr.y && q2[st] + 1 < tr.z};
+#pragma unroll
+                            for (int h = 0; h < 2; ++h) {
+                                const uint32_t o = ok2[h] ? o2[h] : 0u;
+                                const uint16_t lo_ = lrow[o];
+                                visits += ok2[h];
+                                const bool hit = ok2[h] && (push ? lo_ >= (uint16_t)l : lo_ == (uint16_t)j);
+                                if (hit) {
+                                    if (push) {
+                                        lrow[o] = (uint16_t)l;
+                                        const float onem = 1.0f - __uint_as_float(prow[x]);
+                                        atomicMin(&prow[o], __float_as_uint(1.0f - __fmul_rn(onem, r2[h])));
+                                    } else {
+                                        lrow[x] = (uint16_t)l;
+                                        const float c = 1.0f - __fmul_rn(1.0f - __uint_as_float(prow[o]), r2[h]);
+                                        atomicMin(&prow[x], __float_as_uint(c));
+                                    }
+                                }
+                            }
                         }
                     }
-                    uint32_t o[NE];
-                    bool ok[NE];
-#pragma unroll
-                    for (int q = 0; q < NE; ++q) {
-                        ok[q] = ei[q] < e1 && (VW == 1 || ei[q] >= e0);
-                        o[q] = ok[q] ? (uint32_t)wd[q] : 0u;
-                    }
-                    uint16_t lo_[NE];
-#pragma unroll
-                    for (int q = 0; q < NE; ++q) lo_[q] = lrow[o[q]];
-#pragma unroll
-                    for (int q = 0; q < NE; ++q) {
-                        visits += ok[q];
-                        const bool hit = ok[q] && (push ? lo_[q] >= (uint16_t)l : lo_[q] == (uint16_t)j);
-                        if (hit) {
-                            const float r = __uint_as_float((uint32_t)(wd[q] >> 32));
-                            if (push) {
-                                lrow[o[q]] = (uint16_t)l;
-                                atomicMin(&prow[o[q]], __float_as_uint(1.0f - __fmul_rn(onem, r)));
+                    __syncthreads();  // the next batch rewrites the table
+                }
+            } else {
+                uint32_t nw_ = 1, nx = 0, ne0 = 0, ne1 = 0;
+                if (grp < T) item(grp, nw_, nx, ne0, ne1);
+                for (uint32_t t = grp; t < T; t += ngrp) {
+                    const uint32_t w = nw_, x = nx, e0 = ne0, e1 = ne1, j = l - w;
+                    if (t + ngrp < T) item(t + ngrp, nw_, nx, ne0, ne1);
+                    const bool push = (pm >> w) & 1u;
+                    const uint64_t *ce = push ? ce_out : ce_in;
+                    // push: x in N_j, its class-w out-edges x -> v, v unsettled or at l;
+                    // pull: x unsettled, its class-w in-edges u -> x, u in N_j
+                    const float onem = push ? 1.0f - __uint_as_float(prow[x]) : 0.0f;
+                    constexpr int NE = UNR * VW;
+                    for (uint32_t b = VW == 2 ? e0 & ~1u : e0; b < e1; b += UNR * LPT * VW) {
+                        uint64_t wd[NE];
+                        uint32_t ei[NE];
+    #pragma unroll
+                        for (int q = 0; q < UNR; ++q) {
+                            const uint32_t at = b + (sub + q * LPT) * VW;  // padded past the end
+                            if (VW == 2) {
+                                const uint4 r2 = *reinterpret_cast<const uint4 *>(ce + at);
+                                wd[2 * q] = ((uint64_t)r2.y << 32) | r2.x;
+                                wd[2 * q + 1] = ((uint64_t)r2.w << 32) | r2.z;
+                                ei[2 * q] = at;
+                                ei[2 * q + 1] = at + 1;
                             } else {
-                                lrow[x] = (uint16_t)l;
-                                const float c = 1.0f - __fmul_rn(1.0f - __uint_as_float(prow[o[q]]), r);
-                                atomicMin(&prow[x], __float_as_uint(c));
+                                wd[q] = ce[at];
+                                ei[q] = at;
+                            }
+                        }
+                        uint32_t o[NE];
+                        bool ok[NE];
+    #pragma unroll
+                        for (int q = 0; q < NE; ++q) {
+                            ok[q] = ei[q] < e1 && (VW == 1 || ei[q] >= e0);
+                            o[q] = ok[q] ? (uint32_t)wd[q] : 0u;
+                        }
+                        uint16_t lo_[NE];
+    #pragma unroll
+                        for (int q = 0; q < NE; ++q) lo_[q] = lrow[o[q]];
+    #pragma unroll
+                        for (int q = 0; q < NE; ++q) {
+                            visits += ok[q];
+                            const bool hit = ok[q] && (push ? lo_[q] >= (uint16_t)l : lo_[q] == (uint16_t)j);
+                            if (hit) {
+                                const float r = __uint_as_float((uint32_t)(wd[q] >> 32));
+                                if (push) {
+                                    lrow[o[q]] = (uint16_t)l;
+                                    atomicMin(&prow[o[q]], __float_as_uint(1.0f - __fmul_rn(onem, r)));
+                                } else {
+                                    lrow[x] = (uint16_t)l;
+                                    const float c = 1.0f - __fmul_rn(1.0f - __uint_as_float(prow[o[q]]), r);
+                                    atomicMin(&prow[x], __float_as_uint(c));
+                                }
                             }
                         }
                     }
                 }
             }
             __syncthreads();  // every head of level l found
+            LVL_TICK(1)
             // N_l (the vertices now at level l) -> mem[settled, ...)
             for (uint32_t base = 0; base < V; base += nt) {
                 const uint32_t v = base + tid;
@@ -1503,10 +1665,12 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
                 if (f) mem[settled + b + (uint32_t)__popcll(m & below)] = (uint16_t)v;
             }
             __syncthreads();
+            LVL_TICK(2)
             settled += cur[par][1];
             if (tid == 0) hist[l] = settled;
         }
         __syncthreads();  // hist / lrow final for the output
+        LOSS_TICK(6)
         // 3. table row i (or staging slot k), or the probe's row maximum
         if (probe) {
             uint32_t rmax = 0;
@@ -1523,7 +1687,7 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
             if (tid == 0) {
                 uint32_t m = 0;
                 for (int q = 0; q < nw; ++q) m = red_max[q] > m ? red_max[q] : m;
-                probe[k] = m;
+                probe[2 + k] = m;
             }
             __syncthreads();
             continue;
@@ -1571,7 +1735,11 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
             }
         }
         __syncthreads();  // the next row rewrites the LDS rows
+        LOSS_TICK(7)
     }
+#if LOSS_COUNT
+    if (!probe) atomicAdd(&loss_cnt[1], visits);
+#endif
     for (int off = 32; off > 0; off >>= 1) {
         const uint64_t o = __shfl_xor(mn, off);
         mn = o < mn ? o : mn;
@@ -1590,7 +1758,7 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
             c += red_cnt[q];
         }
         if (probe) {
-            if (c) atomicAdd(reinterpret_cast<unsigned long long *>(probe + 2), c);
+            if (c) atomicAdd(reinterpret_cast<unsigned long long *>(probe), c);
         } else {
             atomicMin(&stats[0], m);
             if (c) atomicAdd(&stats[1], c);
@@ -2302,56 +2470,84 @@ srt_status loss_emulated_t(srt_plan *p, unsigned long long *d_stats, srt_err *er
 
 // ------------------------------------------------------------ level solve
 // The class CSRs of the graph's edges of latency <= wmax units (self-loops
-// dropped): prune_rows_kernel's list (sized by the last run; a larger count
-// grows it and runs again), then build_class_csr at level width 1.
+// dropped), classes = exact weights 1..wmax <= WC: out-rows straight from the
+// adjacency (lvl_out_kernel), in-rows by a scan of their counts and one walk
+// of the out-rows (lvl_in_kernel).  The entry arrays hold p->lvl_cap entries:
+// the first call (the create-time probe, wmax = min(31, max edge)) counts,
+// sizes them and runs again; every later call prunes at the probe's bound <=
+// that wmax, so its count fits and nothing waits for the host.
 srt_status level_csr(srt_plan *p, uint64_t wmax, bool with_loss, srt_err *err) {
     hipStream_t M = p->stream;
     const uint32_t V = p->V;
+    const uint32_t cls = wmax < 16 ? 16 : 32;
+    const uint64_t vc1 = (uint64_t)V * cls + 1;
     srt_status st;
-    uint64_t cap_info = p->d_tinfo ? 2 : 0, cap_cur = p->d_tcursor ? 1 : 0, cap_mw = p->d_tmaxw ? 1 : 0;
-    if ((st = grow(&p->d_tinfo, &cap_info, 2, err, "hipMalloc(level info)")) != SRT_OK ||
+    uint64_t c1 = p->tcls_cap, c2 = p->tcls_cap, cap_cur = p->d_tcursor ? 1 : 0, cap_mw = p->d_tmaxw ? 1 : 0;
+    if ((st = grow(&p->d_tcls, &c1, 2 * vc1, err, "hipMalloc(class offsets)")) != SRT_OK ||
+        (st = grow(&p->d_tccnt, &c2, 2 * vc1, err, "hipMalloc(class counts)")) != SRT_OK ||
         (st = grow(&p->d_tcursor, &cap_cur, 1, err, "hipMalloc(level cursor)")) != SRT_OK ||
         (st = grow(&p->d_tmaxw, &cap_mw, 1, err, "hipMalloc(level max)")) != SRT_OK)
         return st;
+    p->tcls_cap = std::min(c1, c2);
     if (!p->h_tcount) {
         const hipError_t e = hipHostMalloc((void **)&p->h_tcount, 4 * sizeof(uint64_t), 0);
         if (e != hipSuccess) return fail(err, e, "hipHostMalloc");
     }
     const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(8192, (V + 3) / 4));
-    auto rows = [&]() {
-        (void)hipMemsetAsync(p->d_tinfo, 0, 2 * sizeof(unsigned long long), M);
+    const uint64_t wns = wmax * p->kp.g;
+    const double inv_g = 1.0 / (double)p->kp.g;
+    auto out_pass = [&]() {
+        (void)hipMemsetAsync(p->d_tccnt, 0, 2 * vc1 * 4, M);  // in-row counts, then in-row cursors
         (void)hipMemsetAsync(p->d_tcursor, 0, sizeof(unsigned long long), M);
         (void)hipMemsetAsync(p->d_tmaxw, 0, sizeof(unsigned long long), M);
-        const uint64_t wns = wmax * p->kp.g;
         if (with_loss)
-            hipLaunchKernelGGL(prune_rows_kernel<true>, dim3(blocks), dim3(256), 0, M, V, p->d_row_ptr, p->d_col,
-                               p->d_lat, p->d_loss, p->kp.g, wns, p->d_tlist, p->d_tlist ? p->tlist_cap : 0ull,
-                               p->d_tcursor, (unsigned long long *)p->d_tmaxw, p->d_tinfo);
+            hipLaunchKernelGGL(lvl_out_kernel<true>, dim3(blocks), dim3(256), 0, M, V, p->d_row_ptr, p->d_col,
+                               p->d_lat, p->d_loss, p->kp.g, inv_g, wns, cls, p->d_tcls, p->d_tccnt, p->d_tpk,
+                               p->lvl_cap, p->d_tcursor, (unsigned long long *)p->d_tmaxw);
         else
-            hipLaunchKernelGGL(prune_rows_kernel<false>, dim3(blocks), dim3(256), 0, M, V, p->d_row_ptr, p->d_col,
-                               p->d_lat, (const float *)nullptr, p->kp.g, wns, p->d_tlist,
-                               p->d_tlist ? p->tlist_cap : 0ull, p->d_tcursor, (unsigned long long *)p->d_tmaxw,
-                               p->d_tinfo);
-        (void)hipMemcpyAsync(p->h_tcount, p->d_tinfo, sizeof(uint64_t), hipMemcpyDeviceToHost, M);
-        (void)hipMemcpyAsync(p->h_tcount + 1, p->d_tmaxw, sizeof(uint64_t), hipMemcpyDeviceToHost, M);
-        return hipStreamSynchronize(M);
+            hipLaunchKernelGGL(lvl_out_kernel<false>, dim3(blocks), dim3(256), 0, M, V, p->d_row_ptr, p->d_col,
+                               p->d_lat, (const float *)nullptr, p->kp.g, inv_g, wns, cls, p->d_tcls, p->d_tccnt,
+                               p->d_tpk, p->lvl_cap, p->d_tcursor, (unsigned long long *)p->d_tmaxw);
     };
-    if (!p->d_tlist) {
-        const uint64_t guess = std::max<uint64_t>(1ull << 16, p->n_adj / 16);
-        if ((st = ensure_tlist(p, guess, guess, err)) != SRT_OK) return st;
+    out_pass();
+    if (!p->lvl_cap) {
+        // first call: count, size the entry arrays (+1024: the solve's 2-entry
+        // loads read up to UNR * LPT * 2 entries past a class's end), run again
+        hipError_t e = hipMemcpyAsync(p->h_tcount, p->d_tcursor, sizeof(uint64_t), hipMemcpyDeviceToHost, M);
+        if (e == hipSuccess) e = hipStreamSynchronize(M);
+        if (e != hipSuccess) return fail(err, e, "level edge count");
+        const uint64_t need = std::max<uint64_t>(p->h_tcount[0], 1) + 1024;
+        uint64_t ca = 0, cb = 0;
+        (void)hipFree(p->d_tpk);
+        (void)hipFree(p->d_tpk2);
+        p->d_tpk = p->d_tpk2 = nullptr;
+        p->t_cap = 0;
+        if ((st = grow(&p->d_tpk, &ca, need, err, "hipMalloc(level out-rows)")) != SRT_OK ||
+            (st = grow(&p->d_tpk2, &cb, need, err, "hipMalloc(level in-rows)")) != SRT_OK)
+            return st;
+        p->lvl_cap = need - 1024;
+        out_pass();
     }
-    hipError_t e = rows();
-    if (e != hipSuccess) return fail(err, e, "level edge list");
-    const uint64_t total = p->h_tcount[0], maxw = p->h_tcount[1];
-    if (total > p->tlist_cap) {
-        if ((st = ensure_tlist(p, total + total / 8 + 64, total, err)) != SRT_OK) return st;
-        if ((e = rows()) != hipSuccess) return fail(err, e, "level edge list");
-    }
-    p->t_edges = total;
-    if ((st = ensure_edge_arrays(p, err)) != SRT_OK) return st;
+    size_t need = 0;
+    hipError_t e = rocprim::exclusive_scan(nullptr, need, p->d_tccnt, p->d_tcls + vc1, 0u, (size_t)vc1,
+                                           rocprim::plus<uint32_t>(), M);
+    if (e != hipSuccess) return fail(err, e, "class scan (size)");
+    uint64_t tcap = p->tscan_tmp_cap;
+    if ((st = grow(reinterpret_cast<uint8_t **>(&p->d_tscan_tmp), &tcap, need + 256, err,
+                   "hipMalloc(scan scratch)")) != SRT_OK)
+        return st;
+    p->tscan_tmp_cap = tcap;
+    size_t have = p->tscan_tmp_cap;
+    e = rocprim::exclusive_scan(p->d_tscan_tmp, have, p->d_tccnt, p->d_tcls + vc1, 0u, (size_t)vc1,
+                                rocprim::plus<uint32_t>(), M);
+    if (e != hipSuccess) return fail(err, e, "class scan");
+    hipLaunchKernelGGL(lvl_in_kernel, dim3(blocks), dim3(256), 0, M, V, cls, p->d_tcls, p->d_tpk, p->d_tcls + vc1,
+                       p->d_tccnt + vc1, p->d_tpk2);
+    p->t_cls = cls;
     p->t_q = 1;
     p->t_level = true;
-    return build_class_csr(p, total, std::max<uint64_t>(maxw, 1), err);
+    p->t_edges = p->lvl_cap;  // the probe's count (an upper bound at the run's smaller wmax)
+    return SRT_OK;
 }
 
 // level_solve_kernel over the rows of job (probe: the row list's first row,
@@ -2360,11 +2556,23 @@ srt_status launch_solve(srt_plan *p, unsigned long long *d_stats, const RowJob &
                         uint32_t *probe) {
     const uint32_t V = p->V, rows = job.list ? job.count : job.range ? job.r1 - job.r0 : p->row1 - p->row0;
     if (!rows) return SRT_OK;
-    const size_t lds = HIST_BYTES + (((size_t)V * 2 + 15) & ~(size_t)15) + (size_t)V * 4 + (size_t)V * 2;
     const uint32_t nt = V >= 2048 ? LOSS_NT : 256;
+    const size_t row_b = SOLVE_HIST + (((size_t)V * 2 + 15) & ~(size_t)15) + (size_t)V * 4 +
+                         (((size_t)V * 2 + 15) & ~(size_t)15);
+    const size_t avail = LDS_BUDGET - 4096;
+    // the flattened walk's item table takes the rest of the LDS (<= 2 nt items: its scan)
+    const uint32_t ib = (uint32_t)std::min<size_t>(2 * nt, avail > row_b + 16 ? (avail - row_b) / 16 : 1);
+    const size_t lds = row_b + (size_t)ib * 16;
     const int per_cu = std::max(1, std::min(2048 / (int)nt, (int)std::max<size_t>(1, (160 * 1024) / (lds + 2048))));
     const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(rows, (uint32_t)(cu_count(p->device) * per_cu)));
-    auto kern = p->t_cls == 16 ? level_solve_kernel<4, 4, 16, 2> : level_solve_kernel<4, 2, 32, 2>;
+    // pair loads in flight a lane of the flattened walk (knob SRT_LVL_K = 4 / 8 (16 spills); 0: the grouped walk,
+    // 4 lanes an item -- A/B measurement)
+    static const int kk = std::getenv("SRT_LVL_K") ? std::atoi(std::getenv("SRT_LVL_K")) : 8;
+    auto kern = p->t_cls == 16
+                    ? (kk == 0 ? level_solve_kernel<4, 4, 16, 2, 0> : kk == 4 ? level_solve_kernel<4, 4, 16, 2, 4>
+                                 : level_solve_kernel<4, 4, 16, 2, 8>)
+                    : (kk == 0 ? level_solve_kernel<4, 2, 32, 2, 0> : kk == 4 ? level_solve_kernel<4, 2, 32, 2, 4>
+                                 : level_solve_kernel<4, 2, 32, 2, 8>);
     (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(LDS_BUDGET - 4096));
     const uint64_t vc1 = (uint64_t)V * p->t_cls + 1;
     const uint32_t *co = p->d_tcls, *ci = p->d_tcls + vc1;
@@ -2376,47 +2584,56 @@ srt_status launch_solve(srt_plan *p, unsigned long long *d_stats, const RowJob &
     hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, p->stream, V, p->d_nodes, p->n,
                        job.list ? 0u : job.range ? job.r0 : p->row0, job.list ? job.count : job.range ? job.r1 : p->row1,
                        co, ci, eo, ei, lcap, p->kp.g, p->d_sl_lat, p->d_sl_loss, p->d_out_lat, p->d_out_loss, d_stats,
-                       job.list, job.out32, job.out32_loss, p->stage16, probe);
+                       job.list, job.out32, job.out32_loss, p->stage16, probe, ib);
     return SRT_OK;
 }
 
 }  // namespace
 
 // Create-time proof for the level solve: the pruned graph's (edges <= wmax
-// units) distances from and to the in-use node nodes[0] by two probe rows.
-// Every in-use u, v then has d(u, v) <= d(u, s) + d(s, v) <= in-ecc + out-ecc
-// = *bound (pruned distances bound the real ones from above); ~0 when s misses
-// an in-use node within wmax levels either way.  *visits: edges the forward
-// row walked (the AUTO price).
+// units) distances from and to K <= 8 in-use nodes s, spread over the node
+// list, by probe rows.  Every in-use u, v has d(u, v) <= d(u, s) + d(s, v) <=
+// in-ecc(s) + out-ecc(s) for each s (pruned distances bound the real ones from
+// above), so *bound = the smallest such sum; ~0 when every s misses an in-use
+// node within wmax levels one way or the other.  *visits: the edges a
+// forward probe row walked on average (the AUTO price).
 srt_status level_probe(srt_plan *p, uint64_t wmax, uint64_t *bound, uint64_t *visits, srt_err *err) {
     *bound = ~0ull;
     *visits = 0;
     if (!p->n) return SRT_OK;
     srt_status st = level_csr(p, wmax, false, err);
     if (st != SRT_OK) return st;
+    const uint32_t K = std::min<uint32_t>(8, p->n);
+    uint32_t rows[8];
+    for (uint32_t k = 0; k < K; ++k) rows[k] = (uint32_t)((uint64_t)k * p->n / K);
     uint32_t *d_pr = nullptr;
-    hipError_t e = hipMalloc(&d_pr, 8 * sizeof(uint32_t));
+    hipError_t e = hipMalloc(&d_pr, 48 * sizeof(uint32_t));  // fwd [0, 16), rev [16, 32), rows [32, 40)
     if (e != hipSuccess) return fail(err, e, "hipMalloc(level probe)");
-    uint32_t h[8] = {};
-    (void)hipMemsetAsync(d_pr, 0, 8 * sizeof(uint32_t), p->stream);
+    uint32_t h[32] = {};
+    (void)hipMemsetAsync(d_pr, 0, 32 * sizeof(uint32_t), p->stream);
+    e = hipMemcpyAsync(d_pr + 32, rows, K * sizeof(uint32_t), hipMemcpyHostToDevice, p->stream);
     RowJob job;
-    job.range = true;
-    job.r0 = 0;
-    job.r1 = 1;
+    job.list = d_pr + 32;
+    job.count = K;
     const uint32_t cap = (uint32_t)std::min<uint64_t>(wmax, WC);
-    launch_solve(p, nullptr, job, cap, false, d_pr);
-    launch_solve(p, nullptr, job, cap, true, d_pr + 4);
-    e = hipMemcpyAsync(h, d_pr, sizeof h, hipMemcpyDeviceToHost, p->stream);
+    if (e == hipSuccess) {
+        launch_solve(p, nullptr, job, cap, false, d_pr);
+        launch_solve(p, nullptr, job, cap, true, d_pr + 16);
+        e = hipMemcpyAsync(h, d_pr, sizeof h, hipMemcpyDeviceToHost, p->stream);
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
     (void)hipFree(d_pr);
     if (e != hipSuccess) return fail(err, e, "level probe");
     uint64_t vis = 0;
-    std::memcpy(&vis, h + 2, 8);
-    *visits = vis;
-    if (h[0] <= cap && h[4] <= cap) *bound = (uint64_t)h[0] + h[4];
+    std::memcpy(&vis, h, 8);
+    *visits = vis / K;
+    for (uint32_t k = 0; k < K; ++k)
+        if (h[2 + k] <= cap && h[18 + k] <= cap && h[2 + k] + h[18 + k] <= WC)  // classes <= WC
+            *bound = std::min<uint64_t>(*bound, (uint64_t)h[2 + k] + h[18 + k]);
     if (std::getenv("SRT_TRACE"))
-        std::fprintf(stderr, "[srt] level probe: %llu edges <= %llu units, out-ecc %u in-ecc %u, %llu visits a row\n",
-                     (unsigned long long)p->t_edges, (unsigned long long)wmax, h[0], h[4], (unsigned long long)vis);
+        std::fprintf(stderr, "[srt] level probe: %llu edges <= %llu units, %u rows, bound %lld, %llu visits a row\n",
+                     (unsigned long long)p->t_edges, (unsigned long long)wmax, K,
+                     *bound == ~0ull ? -1ll : (long long)*bound, (unsigned long long)*visits);
     return SRT_OK;
 }
 
@@ -2438,25 +2655,54 @@ srt_status level_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     hipLaunchKernelGGL(loss_stats_init_kernel, dim3(1), dim3(1), 0, p->stream, d_stats,
                        (unsigned long long *)p->d_tmaxw);
     const uint32_t lcap = (uint32_t)p->kp.lmax;
-    if (p->fold_chunk_rows) {
-        const uint32_t cr = p->fold_chunk_rows, nc = (p->row1 - p->row0 + cr - 1) / cr;
-        while (p->ev_fold.size() < nc) {
-            hipEvent_t e;
-            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(err, hipErrorUnknown, "event");
-            p->ev_fold.push_back(e);
-        }
-        for (uint32_t c = 0; c < nc; ++c) {
-            RowJob job;
-            job.range = true;
-            job.r0 = p->row0 + c * cr;
-            job.r1 = std::min(p->row1, job.r0 + cr);
-            if ((st = launch_solve(p, d_stats, job, lcap, false, nullptr)) != SRT_OK) return st;
-            (void)hipEventRecord(p->ev_fold[c], p->stream);
-        }
-    } else if ((st = launch_solve(p, d_stats, RowJob{}, lcap, false, nullptr)) != SRT_OK) {
-        return st;
+    // the solve launches are the plan's timed dominant launches (event pairs,
+    // srt_plan_kernel_stats; work = the table pairs they write)
+    const uint32_t cr = p->fold_chunk_rows ? p->fold_chunk_rows : std::max<uint32_t>(1, p->row1 - p->row0);
+    const uint32_t nc = (p->row1 - p->row0 + cr - 1) / cr;
+    while (p->ev.size() < 2 * (size_t)nc) {
+        hipEvent_t e;
+        if (hipEventCreateWithFlags(&e, (unsigned)hipEventDisableSystemFence) != hipSuccess)
+            return fail(err, hipErrorUnknown, "event");
+        p->ev.push_back(e);
+    }
+    while (p->fold_chunk_rows && p->ev_fold.size() < nc) {
+        hipEvent_t e;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(err, hipErrorUnknown, "event");
+        p->ev_fold.push_back(e);
+    }
+    p->p3_launches = 0;
+    p->p3_work = 0.0;
+    p->p3_tiles = 0;
+    for (uint32_t c = 0; c < nc; ++c) {
+        RowJob job;
+        job.range = true;
+        job.r0 = p->row0 + c * cr;
+        job.r1 = std::min(p->row1, job.r0 + cr);
+        (void)hipEventRecord(p->ev[2 * c], p->stream);
+        if ((st = launch_solve(p, d_stats, job, lcap, false, nullptr)) != SRT_OK) return st;
+        (void)hipEventRecord(p->ev[2 * c + 1], p->stream);
+        p->p3_launches++;
+        p->p3_work += (double)(job.r1 - job.r0) * p->n;
+        if (p->fold_chunk_rows) (void)hipEventRecord(p->ev_fold[c], p->stream);
     }
     (void)hipEventRecord(p->ev_loss1, p->stream);
+#if LOSS_COUNT
+    {  // diagnostic builds (-DLOSS_COUNT=1): totals of every level solve so far
+        unsigned long long c[9];
+        (void)hipStreamSynchronize(p->stream);
+        (void)hipMemcpyFromSymbol(c, HIP_SYMBOL(loss_cnt), sizeof c);
+        const double rows = (double)(p->row1 - p->row0);
+        std::fprintf(stderr, "[srt] level solve (cumulative): visits %llu, us per row per CU: init %.2f levels %.2f out %.2f\n",
+                     c[1], c[4] * 0.01 / rows, c[6] * 0.01 / rows, c[7] * 0.01 / rows);
+        unsigned long long lc[8][5];
+        (void)hipMemcpyFromSymbol(lc, HIP_SYMBOL(lvl_cnt), sizeof lc);
+        for (int l = 1; l < 8; ++l)
+            if (lc[l][4])
+                std::fprintf(stderr, "[srt]   level %d: rows %llu items/row %.0f us/row: plan %.2f walk %.2f collect %.2f\n", l,
+                             lc[l][4], (double)lc[l][3] / lc[l][4], lc[l][0] * 0.01 / lc[l][4],
+                             lc[l][1] * 0.01 / lc[l][4], lc[l][2] * 0.01 / lc[l][4]);
+    }
+#endif
     return SRT_OK;
 }
 

@@ -41,7 +41,7 @@ def _check(t, og, nodes):
 
 @pytest.mark.parametrize("n,seed,directed,lat,p_edge,subset", [
     (40, 1, False, (1, 9), 0.2, None), (300, 2, False, (1, 9), 0.08, None), (300, 3, True, (1, 9), 0.08, None),
-    (1000, 4, False, (1, 20), 0.05, 700), (1000, 5, True, (1, 5), 0.02, None), (2000, 6, False, (1, 31), 0.3, 1500),
+    (1000, 4, False, (1, 20), 0.05, 700), (1000, 5, True, (1, 5), 0.05, None), (2000, 6, False, (1, 31), 0.3, 1500),
     (777, 7, True, (2, 12), 0.05, 300)])
 def test_level_matches_oracle(n, seed, directed, lat, p_edge, subset):
     g, nodes, og = _random(n, seed, directed, lat, p_edge, subset)
