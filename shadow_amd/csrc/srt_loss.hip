@@ -1379,14 +1379,14 @@ constexpr size_t SOLVE_HIST = 128;  // level ends, levels <= 31
 // probe != nullptr: no table; probe[2 + k] = the largest level over the
 // in-use columns of row k (0xffff if one is unreached by level lcap), the u64
 // at probe[0] += the edges walked.
-template <int LPT, int UNR, uint32_t CLSN, int VW, int K>
+template <int LPT, int UNR, uint32_t CLSN, int VW, bool NT>
 __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
     uint32_t V, const uint32_t *__restrict__ nodes, uint32_t n, uint32_t row0, uint32_t row1,
     const uint32_t *__restrict__ cls_out, const uint32_t *__restrict__ cls_in, const uint64_t *__restrict__ ce_out,
     const uint64_t *__restrict__ ce_in, uint32_t lcap, uint64_t g, const uint64_t *__restrict__ sl_lat,
     const float *__restrict__ sl_loss, uint64_t *__restrict__ out_lat, float *__restrict__ out_loss,
     unsigned long long *stats, const uint32_t *__restrict__ row_list, void *__restrict__ out32,
-    float *__restrict__ out32_loss, bool stage16, uint32_t *__restrict__ probe, uint32_t ib) {
+    float *__restrict__ out32_loss, bool stage16, uint32_t *__restrict__ probe) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ unsigned long long red_min[16], red_cnt[16];
     __shared__ uint32_t red_max[16];
@@ -1394,14 +1394,12 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
     __shared__ uint32_t plan_end[WCN + 1];
     __shared__ uint32_t plan_push, plan_pull;
     __shared__ uint32_t cur[2][2];  // [level parity]: unsettled compaction, level collection
-    __shared__ uint32_t red_sc[16];
     uint32_t *hist = reinterpret_cast<uint32_t *>(smem);  // hist[l]: end of level l in mem (l <= 31)
     uint16_t *lrow = reinterpret_cast<uint16_t *>(smem + SOLVE_HIST);
     const size_t lat_b = ((size_t)V * 2 + 15) & ~(size_t)15, mem_b = ((size_t)V * 2 + 15) & ~(size_t)15;
     uint32_t *prow = reinterpret_cast<uint32_t *>(smem + SOLVE_HIST + lat_b);
     uint16_t *mem = reinterpret_cast<uint16_t *>(smem + SOLVE_HIST + lat_b + (size_t)V * 4);
-    // flattened walk (K > 0): a batch of <= ib items {first pair (prefix), e0, e1, x | w << 16 | push << 24}
-    uint4 *tbl = reinterpret_cast<uint4 *>(smem + SOLVE_HIST + lat_b + (size_t)V * 4 + mem_b);
+    (void)mem_b;
     const uint16_t LINF = 0xffffu;
     const uint32_t FINF = 0x7f800000u;  // +inf bits
     const uint32_t tid = threadIdx.x, nt = blockDim.x;
@@ -1499,153 +1497,62 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
                 e0 = cl[(uint64_t)x * CLSN + w - 1];
                 e1 = cl[(uint64_t)x * CLSN + w];
             };
-            if constexpr (K > 0) {
-                // Flattened walk: the level's items in batches of ib, their
-                // entries as 16-byte pairs numbered across the batch (an
-                // exclusive scan of the items' pair counts); every wave walks
-                // an equal slice of the pairs, lane-consecutive (coalesced), K
-                // pair loads in flight a lane.  A group of lanes per item (K = 0)
-                // waits one round trip per 2-4 entries a lane and idles on
-                // short items.
-                for (uint32_t tb = 0; tb < T; tb += ib) {
-                    const uint32_t nb = T - tb < ib ? T - tb : ib;
-                    for (uint32_t t = tid; t < nb; t += nt) {
-                        uint32_t w, x, e0, e1;
-                        item(tb + t, w, x, e0, e1);
-                        const uint32_t p0 = e0 >> 1, p1 = e1 > e0 ? ((e1 - 1) >> 1) + 1 : p0;
-                        tbl[t] = make_uint4(p1 - p0, e0, e1, x | (w << 16) | (((pm >> w) & 1u) << 24));
-                    }
-                    __syncthreads();
-                    // exclusive scan of the pair counts (two items a thread, nb <= 2 nt)
-                    const uint32_t a0 = 2 * tid < nb ? tbl[2 * tid].x : 0u, a1 = 2 * tid + 1 < nb ? tbl[2 * tid + 1].x : 0u;
-                    const uint32_t sm = a0 + a1;
-                    uint32_t inc = sm;
-                    for (int o = 1; o < 64; o <<= 1) {
-                        const uint32_t y = __shfl_up(inc, o);
-                        if (lane >= o) inc += y;
-                    }
-                    if (lane == 63) red_sc[wv] = inc;
-                    __syncthreads();
-                    uint32_t woff = 0, P = 0;
-                    for (int q = 0; q < nw; ++q) {
-                        woff += q < wv ? red_sc[q] : 0u;
-                        P += red_sc[q];
-                    }
-                    if (2 * tid < nb) tbl[2 * tid].x = woff + inc - sm;
-                    if (2 * tid + 1 < nb) tbl[2 * tid + 1].x = woff + inc - sm + a0;
-                    __syncthreads();
-                    // this wave's slice of the pairs [pb, pe)
-                    const uint32_t pb = (uint32_t)((uint64_t)P * wv / nw), pe = (uint32_t)((uint64_t)P * (wv + 1) / nw);
-                    // the last item whose first pair is <= pb + lane
-                    uint32_t it = 0;
-                    {
-                        uint32_t lo = 0, hi = nb;  // tbl[lo].x <= p < tbl[hi].x (hi = nb: +inf)
-                        const uint32_t p = pb + lane;
-                        while (hi - lo > 1) {
-                            const uint32_t mid = (lo + hi) >> 1;
-                            if (tbl[mid].x <= p) lo = mid;
-                            else hi = mid;
-                        }
-                        it = lo;
-                    }
-                    for (uint32_t base = pb; base < pe; base += 64 * K) {
-                        uint4 d[K];
-                        uint32_t its[K], q2[K];
+            uint32_t nw_ = 1, nx = 0, ne0 = 0, ne1 = 0;
+            if (grp < T) item(grp, nw_, nx, ne0, ne1);
+            for (uint32_t t = grp; t < T; t += ngrp) {
+                const uint32_t w = nw_, x = nx, e0 = ne0, e1 = ne1, j = l - w;
+                if (t + ngrp < T) item(t + ngrp, nw_, nx, ne0, ne1);
+                const bool push = (pm >> w) & 1u;
+                const uint64_t *ce = push ? ce_out : ce_in;
+                // push: x in N_j, its class-w out-edges x -> v, v unsettled or at l;
+                // pull: x unsettled, its class-w in-edges u -> x, u in N_j
+                const float onem = push ? 1.0f - __uint_as_float(prow[x]) : 0.0f;
+                constexpr int NE = UNR * VW;
+                for (uint32_t b = VW == 2 ? e0 & ~1u : e0; b < e1; b += UNR * LPT * VW) {
+                    uint64_t wd[NE];
+                    uint32_t ei[NE];
 #pragma unroll
-                        for (int st = 0; st < K; ++st) {
-                            const uint32_t pp = base + st * 64 + lane;
-                            while (it + 1 < nb && tbl[it + 1].x <= pp) ++it;
-                            its[st] = it;
-                            const uint4 tr = tbl[it];
-                            q2[st] = ((tr.y >> 1) + (pp - tr.x)) * 2;  // the pair's first entry
-                            const uint64_t *ce = (tr.w >> 24) ? ce_out : ce_in;
-                            d[st] = pp < pe ? *reinterpret_cast<const uint4 *>(ce + q2[st]) : make_uint4(0, 0, 0, 0);
-                            if (pp >= pe) q2[st] = ~1u;  // no entry
-                        }
-#pragma unroll
-                        for (int st = 0; st < K; ++st) {
-                            const uint4 tr = tbl[its[st]];
-                            const uint32_t x = tr.w & 0xffffu, w = (tr.w >> 16) & 0xffu, j = l - w;
-                            const bool push = tr.w >> 24;
-                            const uint32_t o2[2] = {d[st].x, d[st].z};
-                            const float r2[2] = {__uint_as_float(d[st].y), __uint_as_float(d[st].w)};
-                            const bool ok2[2] = {q2[st] != ~1u && q2[st] >= tr.y && q2[st] < tr.z,
-                                                 q2[st] != ~1u && q2[st] + 1 >= tr.y && q2[st] + 1 < tr.z};
-#pragma unroll
-                            for (int h = 0; h < 2; ++h) {
-                                const uint32_t o = ok2[h] ? o2[h] : 0u;
-                                const uint16_t lo_ = lrow[o];
-                                visits += ok2[h];
-                                const bool hit = ok2[h] && (push ? lo_ >= (uint16_t)l : lo_ == (uint16_t)j);
-                                if (hit) {
-                                    if (push) {
-                                        lrow[o] = (uint16_t)l;
-                                        const float onem = 1.0f - __uint_as_float(prow[x]);
-                                        atomicMin(&prow[o], __float_as_uint(1.0f - __fmul_rn(onem, r2[h])));
-                                    } else {
-                                        lrow[x] = (uint16_t)l;
-                                        const float c = 1.0f - __fmul_rn(1.0f - __uint_as_float(prow[o]), r2[h]);
-                                        atomicMin(&prow[x], __float_as_uint(c));
-                                    }
-                                }
-                            }
+                    for (int q = 0; q < UNR; ++q) {
+                        const uint32_t at = b + (sub + q * LPT) * VW;  // padded past the end
+                        if (VW == 2) {
+                            const uint4 r2 = *reinterpret_cast<const uint4 *>(ce + at);
+                            wd[2 * q] = ((uint64_t)r2.y << 32) | r2.x;
+                            wd[2 * q + 1] = ((uint64_t)r2.w << 32) | r2.z;
+                            ei[2 * q] = at;
+                            ei[2 * q + 1] = at + 1;
+                        } else {
+                            wd[q] = ce[at];
+                            ei[q] = at;
                         }
                     }
-                    __syncthreads();  // the next batch rewrites the table
-                }
-            } else {
-                uint32_t nw_ = 1, nx = 0, ne0 = 0, ne1 = 0;
-                if (grp < T) item(grp, nw_, nx, ne0, ne1);
-                for (uint32_t t = grp; t < T; t += ngrp) {
-                    const uint32_t w = nw_, x = nx, e0 = ne0, e1 = ne1, j = l - w;
-                    if (t + ngrp < T) item(t + ngrp, nw_, nx, ne0, ne1);
-                    const bool push = (pm >> w) & 1u;
-                    const uint64_t *ce = push ? ce_out : ce_in;
-                    // push: x in N_j, its class-w out-edges x -> v, v unsettled or at l;
-                    // pull: x unsettled, its class-w in-edges u -> x, u in N_j
-                    const float onem = push ? 1.0f - __uint_as_float(prow[x]) : 0.0f;
-                    constexpr int NE = UNR * VW;
-                    for (uint32_t b = VW == 2 ? e0 & ~1u : e0; b < e1; b += UNR * LPT * VW) {
-                        uint64_t wd[NE];
-                        uint32_t ei[NE];
-    #pragma unroll
-                        for (int q = 0; q < UNR; ++q) {
-                            const uint32_t at = b + (sub + q * LPT) * VW;  // padded past the end
-                            if (VW == 2) {
-                                const uint4 r2 = *reinterpret_cast<const uint4 *>(ce + at);
-                                wd[2 * q] = ((uint64_t)r2.y << 32) | r2.x;
-                                wd[2 * q + 1] = ((uint64_t)r2.w << 32) | r2.z;
-                                ei[2 * q] = at;
-                                ei[2 * q + 1] = at + 1;
+                    uint32_t o[NE];
+                    bool ok[NE];
+#pragma unroll
+                    for (int q = 0; q < NE; ++q) {
+                        ok[q] = ei[q] < e1 && (VW == 1 || ei[q] >= e0);
+                        o[q] = ok[q] ? (uint32_t)wd[q] : 0u;
+                    }
+                    uint16_t lo_[NE];
+#pragma unroll
+                    for (int q = 0; q < NE; ++q) lo_[q] = lrow[o[q]];
+#pragma unroll
+                    for (int q = 0; q < NE; ++q) {
+                        visits += ok[q];
+                        const bool hit = ok[q] && (push ? lo_[q] >= (uint16_t)l : lo_[q] == (uint16_t)j);
+                        if (hit) {
+                            // the head enters level l (every writer stores l; a
+                            // head already at l is not stored again), its loss
+                            // min-folded by an LDS atomic (reading the loss first
+                            // and skipping the atomic when it cannot lower it
+                            // measured slower: C3 walk 49 -> 56 us a row)
+                            const float r = __uint_as_float((uint32_t)(wd[q] >> 32));
+                            if (push) {
+                                if (lo_[q] != (uint16_t)l) lrow[o[q]] = (uint16_t)l;
+                                atomicMin(&prow[o[q]], __float_as_uint(1.0f - __fmul_rn(onem, r)));
                             } else {
-                                wd[q] = ce[at];
-                                ei[q] = at;
-                            }
-                        }
-                        uint32_t o[NE];
-                        bool ok[NE];
-    #pragma unroll
-                        for (int q = 0; q < NE; ++q) {
-                            ok[q] = ei[q] < e1 && (VW == 1 || ei[q] >= e0);
-                            o[q] = ok[q] ? (uint32_t)wd[q] : 0u;
-                        }
-                        uint16_t lo_[NE];
-    #pragma unroll
-                        for (int q = 0; q < NE; ++q) lo_[q] = lrow[o[q]];
-    #pragma unroll
-                        for (int q = 0; q < NE; ++q) {
-                            visits += ok[q];
-                            const bool hit = ok[q] && (push ? lo_[q] >= (uint16_t)l : lo_[q] == (uint16_t)j);
-                            if (hit) {
-                                const float r = __uint_as_float((uint32_t)(wd[q] >> 32));
-                                if (push) {
-                                    lrow[o[q]] = (uint16_t)l;
-                                    atomicMin(&prow[o[q]], __float_as_uint(1.0f - __fmul_rn(onem, r)));
-                                } else {
-                                    lrow[x] = (uint16_t)l;
-                                    const float c = 1.0f - __fmul_rn(1.0f - __uint_as_float(prow[o[q]]), r);
-                                    atomicMin(&prow[x], __float_as_uint(c));
-                                }
+                                lrow[x] = (uint16_t)l;
+                                const float c = 1.0f - __fmul_rn(1.0f - __uint_as_float(prow[o[q]]), r);
+                                atomicMin(&prow[x], __float_as_uint(c));
                             }
                         }
                     }
@@ -1723,10 +1630,15 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
                         lossv = __uint_as_float(prow[vv[q]]);
                     }
                 }
+                // streamed out without allocating in the caches (NT): the
+                // class CSRs the walks read stay resident
                 if (o32p) {
-                    if (o16) o16[j] = latv == ~0ull ? (uint16_t)0xffffu : (uint16_t)lu;
-                    else if (o32) o32[j] = latv == ~0ull ? ~0u : (uint32_t)lu;
-                    o32p[j] = lossv;
+                    if (o16) __builtin_nontemporal_store(latv == ~0ull ? (uint16_t)0xffffu : (uint16_t)lu, o16 + j);
+                    else if (o32) __builtin_nontemporal_store(latv == ~0ull ? ~0u : (uint32_t)lu, o32 + j);
+                    __builtin_nontemporal_store(lossv, o32p + j);
+                } else if (NT) {
+                    __builtin_nontemporal_store(latv, ol + j);
+                    __builtin_nontemporal_store(lossv, op + j);
                 } else {
                     ol[j] = latv;
                     op[j] = lossv;
@@ -2557,22 +2469,14 @@ srt_status launch_solve(srt_plan *p, unsigned long long *d_stats, const RowJob &
     const uint32_t V = p->V, rows = job.list ? job.count : job.range ? job.r1 - job.r0 : p->row1 - p->row0;
     if (!rows) return SRT_OK;
     const uint32_t nt = V >= 2048 ? LOSS_NT : 256;
-    const size_t row_b = SOLVE_HIST + (((size_t)V * 2 + 15) & ~(size_t)15) + (size_t)V * 4 +
-                         (((size_t)V * 2 + 15) & ~(size_t)15);
-    const size_t avail = LDS_BUDGET - 4096;
-    // the flattened walk's item table takes the rest of the LDS (<= 2 nt items: its scan)
-    const uint32_t ib = (uint32_t)std::min<size_t>(2 * nt, avail > row_b + 16 ? (avail - row_b) / 16 : 1);
-    const size_t lds = row_b + (size_t)ib * 16;
+    const size_t lds = SOLVE_HIST + (((size_t)V * 2 + 15) & ~(size_t)15) + (size_t)V * 4 +
+                       (((size_t)V * 2 + 15) & ~(size_t)15);
     const int per_cu = std::max(1, std::min(2048 / (int)nt, (int)std::max<size_t>(1, (160 * 1024) / (lds + 2048))));
     const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(rows, (uint32_t)(cu_count(p->device) * per_cu)));
-    // pair loads in flight a lane of the flattened walk (knob SRT_LVL_K = 4 / 8 (16 spills); 0: the grouped walk,
-    // 4 lanes an item -- A/B measurement)
-    static const int kk = std::getenv("SRT_LVL_K") ? std::atoi(std::getenv("SRT_LVL_K")) : 8;
-    auto kern = p->t_cls == 16
-                    ? (kk == 0 ? level_solve_kernel<4, 4, 16, 2, 0> : kk == 4 ? level_solve_kernel<4, 4, 16, 2, 4>
-                                 : level_solve_kernel<4, 4, 16, 2, 8>)
-                    : (kk == 0 ? level_solve_kernel<4, 2, 32, 2, 0> : kk == 4 ? level_solve_kernel<4, 2, 32, 2, 4>
-                                 : level_solve_kernel<4, 2, 32, 2, 8>);
+    // table rows by non-temporal stores (knob SRT_LVL_NT=0/1: A/B measurement)
+    static const bool nts = !(std::getenv("SRT_LVL_NT") && std::atoi(std::getenv("SRT_LVL_NT")) == 0);
+    auto kern = p->t_cls == 16 ? (nts ? level_solve_kernel<4, 4, 16, 2, true> : level_solve_kernel<4, 4, 16, 2, false>)
+                               : (nts ? level_solve_kernel<4, 2, 32, 2, true> : level_solve_kernel<4, 2, 32, 2, false>);
     (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(LDS_BUDGET - 4096));
     const uint64_t vc1 = (uint64_t)V * p->t_cls + 1;
     const uint32_t *co = p->d_tcls, *ci = p->d_tcls + vc1;
@@ -2584,7 +2488,7 @@ srt_status launch_solve(srt_plan *p, unsigned long long *d_stats, const RowJob &
     hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, p->stream, V, p->d_nodes, p->n,
                        job.list ? 0u : job.range ? job.r0 : p->row0, job.list ? job.count : job.range ? job.r1 : p->row1,
                        co, ci, eo, ei, lcap, p->kp.g, p->d_sl_lat, p->d_sl_loss, p->d_out_lat, p->d_out_loss, d_stats,
-                       job.list, job.out32, job.out32_loss, p->stage16, probe, ib);
+                       job.list, job.out32, job.out32_loss, p->stage16, probe);
     return SRT_OK;
 }
 

@@ -63,6 +63,10 @@ def test_c1_full_table_through_gml():
 
 
 def test_c3_16k_rows_vs_oracle_and_symmetry():
+    """C3 as the drop-in runs it (AUTO: the level solve -- B from the probe)
+    and forced onto the Floyd-Warshall family: 16 seeded oracle rows bit-exact,
+    latency symmetry on the device, and the two families' tables equal bit for
+    bit."""
     import torch
 
     n = 16384
@@ -71,8 +75,7 @@ def test_c3_16k_rows_vs_oracle_and_symmetry():
     g = NetworkGraph(n, np.arange(n, dtype=np.uint32), row_ptr, col, lat, loss, directed=False)
     nodes = np.arange(n, dtype=np.uint32)
     plan = RoutingPlan(g, nodes).run()
-    assert plan.describe().startswith("fw:f16key")  # complete graph: lmax = the longest edge (300 units < 1024)
-    assert plan.timing()["loss_fold"] == 1  # tight weights <= 15 units, latencies < 2048: the level fold
+    assert plan.describe().startswith("level:u16"), plan.describe()  # AUTO: the level solve is priced cheapest
     plan.fetch(table=False)  # every pair reachable (else DISCONNECTED), min latency
     L, P = _device_table(plan)
     assert torch.equal(L, L.t()), "undirected latency table must be symmetric"
@@ -89,7 +92,16 @@ def test_c3_16k_rows_vs_oracle_and_symmetry():
     _check_rows(L, P, rows, nodes, elat[:16][:, inv], eloss[:16][:, inv], sl_l, sl_p)
     # get_smallest_latency_ns over the whole device table == the smallest edge
     assert plan.min_latency_ns == L.min().item() == int(lat.min())
-    plan.close()
+    fw = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_FW).run()
+    try:
+        assert fw.describe().startswith("fw:f16key")  # complete graph: lmax = the longest edge (300 units < 1024)
+        assert fw.timing()["loss_fold"] == 1  # tight weights <= 15 units, latencies < 2048: the level fold
+        fw.fetch(table=False)
+        L2, P2 = _device_table(fw)
+        assert torch.equal(L, L2) and torch.equal(P, P2), "level solve != Floyd-Warshall tables"
+    finally:
+        fw.close()
+        plan.close()
 
 
 def test_c3ns_16k_u32_keys_rows_vs_oracle():
