@@ -1513,7 +1513,7 @@ srt_status srt_plan_timing(const srt_plan *p, srt_timing *o) {
     o->dominant_work = p->p3_work;
     o->loss_ms = p->loss_ms;
     o->tight_edges = p->algo != SRT_ALGO_SSSP ? p->t_edges : 0;  // level solve: the pruned edges
-    o->sharded_tail = p->algo == SRT_ALGO_FW && p->shard_tail ? 1u : 0u;
+    o->sharded_tail = p->algo != SRT_ALGO_SSSP && p->shard_tail ? 1u : 0u;  // dense: staged rows all-gathered
     o->sparse_split = 0u;  // the split sweep was removed (reserved)
     o->sparse_sweeps = p->algo == SRT_ALGO_SSSP ? p->sssp_sweeps : 0;
     o->loss_fold = p->algo == SRT_ALGO_FW && p->t_level ? 1u : 0u;
@@ -1638,7 +1638,13 @@ srt_status srt_plan_bind_comm(srt_plan *p, srt_comm *comm, srt_err *err) {
         char d[64];
         std::snprintf(d, sizeof d, " ranks=%d rows=[%u,%u)", comm->nranks, p->row0, p->row1);
         p->desc += d;
-        if (p->algo != SRT_ALGO_FW) return SRT_OK;  // row-sharded families: no closure block-rows
+        if (p->algo == SRT_ALGO_SSSP) return SRT_OK;
+        if (p->algo == SRT_ALGO_LEVEL) {
+            // rows dealt by node index ranges, solved into a 6-byte staging
+            // and all-gathered chunk by chunk (srt_loss.hip level_sharded)
+            if (srt_status st = build_loss_rows(p, comm->nranks, (p->V + W - 1) / W, err); st != SRT_OK) return st;
+            return SRT_OK;
+        }
     }
     // pad the node range so every rank owns the same number of block-rows
     // (equal all-gather chunks); padded nodes are isolated and never in use

@@ -441,9 +441,11 @@ __global__ void expand_rows_kernel(const uint32_t *__restrict__ lrows, uint32_t 
         const uint16_t *Drow = Dfull ? Dfull + (uint64_t)nodes[i] * Vp : nullptr;
         for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
             uint64_t l;
-            if (Drow) {
+            if (j == i) {
+                l = sl_lat[i];  // the raw self-loop: need not fit the staged latency field
+            } else if (Drow) {
                 const uint32_t x = Drow[nodes[j]];
-                l = j == i ? sl_lat[i] : x >= KEY16_INF ? ~0ull : (uint64_t)x * g;
+                l = x >= KEY16_INF ? ~0ull : (uint64_t)x * g;
             } else if (lat16) {
                 const uint32_t x = s16[j];
                 l = x == 0xffffu ? ~0ull : (uint64_t)x * g;
@@ -975,6 +977,7 @@ __global__ void tcls_fill_kernel(const uint4 *__restrict__ list, uint64_t slots,
 #if LOSS_COUNT
 __device__ unsigned long long loss_cnt[9];  // diagnostic builds: items, edge visits, hits, levels, phase ticks x4, push hits
 __device__ unsigned long long lvl_cnt[8][5];  // level solve, per level (<= 7): ticks plan+compact / walk / collect, items, rows
+__constant__ uint32_t lvl_diag;                // level solve ablations (SRT_LVL_DIAG)
 #endif
 template <int LPT, int UNR, bool QUANT, uint32_t CLSN, int VW>
 __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
@@ -1547,8 +1550,16 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
                             // measured slower: C3 walk 49 -> 56 us a row)
                             const float r = __uint_as_float((uint32_t)(wd[q] >> 32));
                             if (push) {
+#if LOSS_COUNT
+                                // diagnostic builds: lvl_diag bit 0 drops the loss atomics,
+                                // bit 1 the level stores (wrong tables; timing only)
+                                if (!(lvl_diag & 2) && lo_[q] != (uint16_t)l) lrow[o[q]] = (uint16_t)l;
+                                if (!(lvl_diag & 1))
+                                    atomicMin(&prow[o[q]], __float_as_uint(1.0f - __fmul_rn(onem, r)));
+#else
                                 if (lo_[q] != (uint16_t)l) lrow[o[q]] = (uint16_t)l;
                                 atomicMin(&prow[o[q]], __float_as_uint(1.0f - __fmul_rn(onem, r)));
+#endif
                             } else {
                                 lrow[x] = (uint16_t)l;
                                 const float c = 1.0f - __fmul_rn(1.0f - __uint_as_float(prow[o[q]]), r);
@@ -2545,6 +2556,66 @@ srt_status level_probe(srt_plan *p, uint64_t wmax, uint64_t *bound, uint64_t *vi
 // kp.lmax units (the probe's bound), then the rows -- in chunks of
 // fold_chunk_rows when the one-call build downloads behind them (ev_fold), as
 // fw_loss's fold.  A sharded plan solves its own rows [row0, row1).
+namespace {
+// Sharded level solve (comm bound): this rank's rows (d_lrows, by
+// build_loss_rows) solved in tail_q chunks into the staging as u16 latency
+// units + f32 loss (6 B a pair, half the table's 12), chunk c's rows
+// all-gathered on the comm stream behind chunk c + 1's solve and expanded into
+// every rank's table behind its all-gather -- the sharded FW tail's pipeline
+// with the solve in place of the fold.
+srt_status level_sharded(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
+    const uint32_t W = (uint32_t)p->comm->nranks, r = (uint32_t)p->comm->rank;
+    const size_t chunk = (size_t)p->lrow_max * p->n;
+    p->stage16 = true;
+    p->stage_loss_only = false;
+    if (!p->d_slat) {
+        void *a = nullptr, *b = nullptr;
+        hipError_t e = hipMalloc(&a, std::max<size_t>(chunk * W, 1) * 4);
+        if (e == hipSuccess) e = hipMalloc(&b, std::max<size_t>(chunk * W, 1) * 4);
+        if (e != hipSuccess) {
+            (void)hipFree(a);
+            return fail(err, e, "hipMalloc(row staging)");
+        }
+        p->d_slat = (uint32_t *)a;
+        p->d_sloss = (float *)b;
+    }
+    const uint32_t q = p->tail_q, cr = p->tail_cr, lcap = (uint32_t)p->kp.lmax;
+    const size_t cbytes = (size_t)cr * p->n * 4, lbytes = (size_t)cr * p->n * 2;
+    hipStream_t M = p->stream, C = p->comm_stream;
+    while (p->ev.size() < 2 * (size_t)q) {
+        hipEvent_t e;
+        if (hipEventCreateWithFlags(&e, (unsigned)hipEventDisableSystemFence) != hipSuccess)
+            return fail(err, hipErrorUnknown, "event");
+        p->ev.push_back(e);
+    }
+    srt_status st;
+    for (uint32_t c = 0; c < q; ++c) {
+        const size_t slot = ((size_t)c * W + r) * cr;
+        RowJob job;
+        job.list = p->d_lrows + slot;
+        job.count = p->lrow_cnt[r] > c * cr ? std::min(cr, p->lrow_cnt[r] - c * cr) : 0u;
+        job.out32 = reinterpret_cast<uint8_t *>(p->d_slat) + slot * p->n * 2;
+        job.out32_loss = p->d_sloss + slot * p->n;
+        (void)hipEventRecord(p->ev[2 * c], M);
+        if ((st = launch_solve(p, d_stats, job, lcap, false, nullptr)) != SRT_OK) return st;
+        (void)hipEventRecord(p->ev[2 * c + 1], M);
+        p->p3_launches++;
+        p->p3_work += (double)job.count * p->n;
+        (void)hipEventRecord(p->ev_tail[c], M);
+        (void)hipStreamWaitEvent(C, p->ev_tail[c], 0);
+        const size_t base = (size_t)c * W * cr * p->n;
+        if ((st = comm_allgather_inplace(p->comm, reinterpret_cast<uint8_t *>(p->d_slat) + base * 2, lbytes, C,
+                                         err)) != SRT_OK ||
+            (st = comm_allgather_inplace(p->comm, p->d_sloss + base, cbytes, C, err)) != SRT_OK)
+            return st;
+        (void)hipEventRecord(p->ev_tail[q + c], C);
+    }
+    expand_chunks_behind(p, W);
+    p->shard_tail = true;
+    return SRT_OK;
+}
+}  // namespace
+
 srt_status level_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     if (!p->ev_loss0) {
         (void)hipEventCreate(&p->ev_loss0);
@@ -2558,6 +2629,20 @@ srt_status level_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     if (st != SRT_OK) return st;
     hipLaunchKernelGGL(loss_stats_init_kernel, dim3(1), dim3(1), 0, p->stream, d_stats,
                        (unsigned long long *)p->d_tmaxw);
+#if LOSS_COUNT
+    {
+        const uint32_t dg = std::getenv("SRT_LVL_DIAG") ? (uint32_t)std::atoi(std::getenv("SRT_LVL_DIAG")) : 0u;
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(lvl_diag), &dg, sizeof dg);
+    }
+#endif
+    if (p->comm) {
+        p->p3_launches = 0;
+        p->p3_work = 0.0;
+        p->p3_tiles = 0;
+        st = level_sharded(p, d_stats, err);
+        (void)hipEventRecord(p->ev_loss1, p->stream);
+        return st;
+    }
     const uint32_t lcap = (uint32_t)p->kp.lmax;
     // the solve launches are the plan's timed dominant launches (event pairs,
     // srt_plan_kernel_stats; work = the table pairs they write)

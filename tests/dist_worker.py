@@ -39,7 +39,8 @@ def main():
         lat = (np.asarray(lat, dtype=np.uint64) << np.uint64(34)) + np.uint64(1)  # gcd 1: no unit rescale
     g = NetworkGraph.from_edges(n, src, dst, lat, loss, directed=not undirected)
     nodes = np.random.default_rng(seed).permutation(n).astype(np.uint32)
-    algo = {"auto": _lib.SRT_ALGO_AUTO, "fw": _lib.SRT_ALGO_FW, "sssp": _lib.SRT_ALGO_SSSP}[algo_name]
+    algo = {"auto": _lib.SRT_ALGO_AUTO, "fw": _lib.SRT_ALGO_FW, "sssp": _lib.SRT_ALGO_SSSP,
+            "level": _lib.SRT_ALGO_LEVEL}[algo_name]
     plan = RoutingPlan(g, nodes, algo=algo, device=0)
     sdist.bind(plan, rank, world, 0, transport=transport)
     plan.run()
@@ -61,6 +62,8 @@ def main():
         ok = ok and np.array_equal(t.packet_loss.view(np.uint32), eloss.view(np.uint32))
         # dense builds: the loss pass ran on the rank's own closure rows
         ok = ok and (algo_name != "fw" or tail == (0 if wide else 1))
+        # level solve: rows staged as 6-byte records and all-gathered chunk by chunk
+        ok = ok and (algo_name != "level" or (plan.describe().startswith("level:") and tail == 1))
         ok = ok and (want_rests is None or tm["dominant_launches"] == int(want_rests))
         # a symmetric dense graph runs the triangle schedule, a directed one never
         ok = ok and (algo_name != "fw" or ("sym=triangle" in plan.describe()) == undirected)

@@ -38,7 +38,10 @@ def _port():
     # ... in groups of g rounds, one row all-gather per group ("s<g>:<rest launches>"; a sharded
     # plan pads to whole block-rows a rank: 8 ranks 16 block-rows, the last group of 3 ragged)
     (2, 1000, 16, "fw", "undirected", "s2:4"), (3, 1300, 17, "fw", "undirected", "s4:3"),
-    (8, 1100, 18, "fw", "undirected", "s2:8"), (8, 1500, 19, "fw", "undirected", "s3:6")])
+    (8, 1100, 18, "fw", "undirected", "s2:8"), (8, 1500, 19, "fw", "undirected", "s3:6"),
+    # the level solve: rows by node-index ranges, 6-byte staged rows all-gathered
+    (2, 600, 22, "level", "undirected", None), (3, 500, 23, "level", False, None),
+    (8, 1100, 24, "level", "undirected", None)])
 def test_sharded_build_matches_oracle(world, n, seed, algo, wide, group):
     """Dense builds assert the sharded tail ran (or, "wide", the replicated
     fallback) and, for undirected graphs, the symmetric schedule; every rank's
