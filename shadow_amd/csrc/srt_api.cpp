@@ -1336,20 +1336,14 @@ srt_status run_closure(srt_plan *p, srt_err *err) {
     return srt::fw_rounds(p, err);
 }
 
-srt_status run_tail(srt_plan *p, srt_err *err) {
-    srt_status st;
-    // table rows [row0, row1) of this rank; every rank then holds the whole
-    // table after the row exchange, and the stats of all ranks
-    const int rank = p->comm ? p->comm->rank : 0, nranks = p->comm ? p->comm->nranks : 1;
-    unsigned long long *rstats = p->comm ? p->d_rstats + 2 * rank : p->d_stats;
+// End-to-end build: the edge losses, uploaded while the closure runs and
+// range-checked on the device (LossUpload).  The copies run on the host
+// thread once their stream reaches them, so they go on the comm stream (idle
+// on one GPU; the closure is all on the main and side streams) and the main
+// stream waits for them before the loss pass -- on the main stream they would
+// queue behind the closure (measured: C3 +19 ms, serial).
+srt_status upload_deferred_loss(srt_plan *p, srt_err *err) {
     if (p->h_loss_defer) {
-        // end-to-end build: the edge losses, uploaded while the closure runs
-        // and range-checked on the device (LossUpload).  The copies run on
-        // the host thread once their stream reaches them, so they go on the
-        // comm stream (idle on one GPU; the closure is all on the main and
-        // side streams) and the main stream waits for them before the loss
-        // pass -- on the main stream they would queue behind the closure
-        // (measured: C3 +19 ms, serial).
         hipStream_t up = p->comm ? p->stream : p->comm_stream;
         if (!p->d_lossbad) {
             HIP_TRY(hipMalloc(&p->d_lossbad, 8), "hipMalloc(loss check)");
@@ -1370,6 +1364,16 @@ srt_status run_tail(srt_plan *p, srt_err *err) {
         }
         p->h_loss_defer = nullptr;
     }
+    return SRT_OK;
+}
+
+srt_status run_tail(srt_plan *p, srt_err *err) {
+    srt_status st;
+    // table rows [row0, row1) of this rank; every rank then holds the whole
+    // table after the row exchange, and the stats of all ranks
+    const int rank = p->comm ? p->comm->rank : 0, nranks = p->comm ? p->comm->nranks : 1;
+    unsigned long long *rstats = p->comm ? p->d_rstats + 2 * rank : p->d_stats;
+    if ((st = upload_deferred_loss(p, err)) != SRT_OK) return st;
     if (p->algo != SRT_ALGO_SSSP) {
         // exact loss over the tight DAG (sharded: over this rank's own
         // closure rows, see fw_loss)
@@ -1976,6 +1980,180 @@ srt_status fetch_pipelined(srt_plan *p, srt_path *out, srt::CompactTable *ct, ui
     return s;
 }
 
+// The in-process multi-GPU build of a level plan (srt_opts.n_gpus > 1, the
+// family AUTO picks for C1-C3): rank 0's plan did the one CSR scan and
+// upload; its class CSRs (the whole input of a solve: ~0.1 GB at C3) go to
+// every other device over xGMI (hipMemcpyPeerAsync; ranks on the same device
+// share them), every rank solves its contiguous rows into a 6-byte staging
+// (u16 latency units + f32 loss) and downloads them over its own PCIe link
+// straight into the caller's records (RoutingInfo) or, expanded by its
+// thread, into the caller's srt_path rows.  No table exchange between the
+// GPUs: Shadow's one consumer is the host (sim_config.rs:136-140, 424-461).
+// SRT_MULTI_EMULATE=1 (measurement only): rank 0's share alone -- its rows,
+// the others skipped (their rows are left unwritten).
+srt_status build_multi_level(srt_plan *p0, const std::vector<int32_t> &devs, srt_path *out, srt::CompactTable *ct,
+                             uint64_t *min_latency_ns, srt_err *err) {
+    Trace tr;
+    const int N = (int)devs.size();
+    const uint32_t n = p0->n;
+    const bool emulate = std::getenv("SRT_MULTI_EMULATE") && std::atoi(std::getenv("SRT_MULTI_EMULATE")) != 0;
+    HIP_TRY(hipSetDevice(p0->device), "hipSetDevice");
+    if (srt_status s = upload_deferred_loss(p0, err); s != SRT_OK) return s;
+    if (srt_status s = srt::level_prepare(p0, err); s != SRT_OK) return s;
+    hipEvent_t ready = nullptr;
+    HIP_TRY(hipEventCreateWithFlags(&ready, hipEventDisableTiming), "event");
+    HIP_TRY(hipEventRecord(ready, p0->stream), "event record");
+    tr.mark("multi: class CSRs on rank 0");
+    if (ct) {
+        const int T = host_threads((uint64_t)n * n);
+        if (!ct_alloc(ct, n, p0->kp.g, true, T)) {
+            (void)hipEventDestroy(ready);
+            set_err(err, SRT_ERR_OOM, "out of host memory (routing table)");
+            return SRT_ERR_OOM;
+        }
+    }
+    const srt::LevelCtx c0 = srt::level_ctx(p0);
+    const uint64_t vc1 = (uint64_t)p0->V * p0->t_cls + 1, ents = p0->lvl_cap + 1024;
+    std::vector<srt_status> sts(N, SRT_OK);
+    std::vector<srt_err> errs(N);
+    std::vector<unsigned long long> mins(N, ~0ull), unre(N, 0);
+    auto rank_fn = [&](int r) {
+        srt_err *e2 = &errs[r];
+        std::memset(e2, 0, sizeof *e2);
+        const uint32_t r0 = (uint32_t)((uint64_t)n * r / N), r1 = (uint32_t)((uint64_t)n * (r + 1) / N);
+        const uint64_t rows = r1 - r0;
+        std::vector<void *> owned;
+        hipStream_t st = nullptr;
+        auto fail = [&](hipError_t e, const char *what) {
+            sts[r] = hip_fail(e2, e, what);
+        };
+        auto dev_alloc = [&](size_t bytes) -> void * {
+            void *q = nullptr;
+            if (hipMalloc(&q, std::max<size_t>(bytes, 1)) != hipSuccess) return nullptr;
+            owned.push_back(q);
+            return q;
+        };
+        hipError_t e = hipSetDevice(devs[r]);
+        srt::LevelCtx c = c0;
+        c.device = devs[r];
+        if (e == hipSuccess) e = r == 0 ? hipSuccess : hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+        if (r == 0) st = p0->stream;
+        c.stream = st;
+        if (e == hipSuccess) e = hipStreamWaitEvent(st, ready, 0);
+        if (e == hipSuccess && devs[r] != devs[0]) {
+            // the solve's inputs from rank 0's device
+            uint32_t *tcls = (uint32_t *)dev_alloc(2 * vc1 * 4);
+            uint64_t *eo = (uint64_t *)dev_alloc(ents * 8), *ei = (uint64_t *)dev_alloc(ents * 8);
+            uint32_t *nd = (uint32_t *)dev_alloc((size_t)n * 4);
+            uint64_t *sl = (uint64_t *)dev_alloc((size_t)n * 8);
+            float *sp = (float *)dev_alloc((size_t)n * 4);
+            if (!tcls || !eo || !ei || !nd || !sl || !sp) e = hipErrorOutOfMemory;
+            if (e == hipSuccess) e = hipMemcpyPeerAsync(tcls, devs[r], c0.tcls, devs[0], 2 * vc1 * 4, st);
+            if (e == hipSuccess) e = hipMemcpyPeerAsync(eo, devs[r], c0.ce_out, devs[0], ents * 8, st);
+            if (e == hipSuccess) e = hipMemcpyPeerAsync(ei, devs[r], c0.ce_in, devs[0], ents * 8, st);
+            if (e == hipSuccess) e = hipMemcpyPeerAsync(nd, devs[r], c0.nodes, devs[0], (size_t)n * 4, st);
+            if (e == hipSuccess) e = hipMemcpyPeerAsync(sl, devs[r], c0.sl_lat, devs[0], (size_t)n * 8, st);
+            if (e == hipSuccess) e = hipMemcpyPeerAsync(sp, devs[r], c0.sl_loss, devs[0], (size_t)n * 4, st);
+            c.tcls = tcls;
+            c.ce_out = eo;
+            c.ce_in = ei;
+            c.nodes = nd;
+            c.sl_lat = sl;
+            c.sl_loss = sp;
+        }
+        uint16_t *s16 = nullptr;
+        float *sloss = nullptr;
+        unsigned long long *dst = nullptr;
+        if (e == hipSuccess) {
+            s16 = (uint16_t *)dev_alloc(rows * n * 2 + 256);
+            sloss = (float *)dev_alloc(rows * n * 4);
+            dst = (unsigned long long *)dev_alloc(4 * 8);
+            if (!s16 || !sloss || !dst) e = hipErrorOutOfMemory;
+        }
+        if (e == hipSuccess && rows) {
+            srt::level_stats_init(dst, st);
+            srt::level_solve_stage(c, r0, r1, (uint32_t)p0->kp.lmax, s16, sloss, dst);
+        }
+        unsigned long long hs[2] = {~0ull, 0};
+        std::vector<uint16_t> h16;
+        std::vector<float> hl;
+        if (e == hipSuccess && rows) {
+            if (ct) {
+                // straight into the RoutingInfo's 6-byte records
+                e = hipMemcpyAsync(ct->lat16 + (uint64_t)r0 * n, s16, rows * n * 2, hipMemcpyDeviceToHost, st);
+                if (e == hipSuccess)
+                    e = hipMemcpyAsync(ct->loss + (uint64_t)r0 * n, sloss, rows * n * 4, hipMemcpyDeviceToHost, st);
+            } else {
+                h16.resize(rows * n);
+                hl.resize(rows * n);
+                e = hipMemcpyAsync(h16.data(), s16, rows * n * 2, hipMemcpyDeviceToHost, st);
+                if (e == hipSuccess) e = hipMemcpyAsync(hl.data(), sloss, rows * n * 4, hipMemcpyDeviceToHost, st);
+            }
+            if (e == hipSuccess) e = hipMemcpyAsync(hs, dst, sizeof hs, hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+        }
+        if (e == hipSuccess && out && rows) {
+            // expanded into the caller's srt_path rows by this rank's share of the host threads
+            const uint64_t g = p0->kp.g, cnt = rows * n;
+            const int T = std::max(1, host_threads(cnt) / (emulate ? 1 : N));
+            auto part = [&](int w) {
+                for (uint64_t k = cnt * w / T; k < cnt * (w + 1) / T; ++k) {
+                    srt_path q;
+                    q.latency_ns = h16[k] == 0xffffu ? ~0ull : (uint64_t)h16[k] * g;
+                    q.packet_loss = hl[k];
+                    q._pad = 0;
+                    out[(uint64_t)r0 * n + k] = q;
+                }
+            };
+            std::vector<std::thread> pool;
+            for (int w = 1; w < T; ++w) pool.emplace_back(part, w);
+            part(0);
+            for (auto &t : pool) t.join();
+        }
+        if (st && r != 0) (void)hipStreamSynchronize(st);
+        for (void *q : owned) (void)hipFree(q);
+        if (st && r != 0) (void)hipStreamDestroy(st);
+        if (e != hipSuccess) fail(e, "multi-GPU level solve");
+        mins[r] = hs[0];
+        unre[r] = hs[1];
+    };
+    std::vector<std::thread> th;
+    for (int r = 0; r < N; ++r) {
+        if (emulate && r > 0) continue;
+        th.emplace_back(rank_fn, r);
+    }
+    for (auto &t : th) t.join();
+    (void)hipSetDevice(p0->device);
+    (void)hipEventDestroy(ready);
+    tr.mark("multi: ranks solved + downloaded");
+    for (int r = 0; r < N; ++r)
+        if (sts[r] != SRT_OK) {
+            if (err) *err = errs[r];
+            return sts[r];
+        }
+    unsigned long long mn = ~0ull, un = 0;
+    for (int r = 0; r < N; ++r) {
+        mn = std::min(mn, mins[r]);
+        un += unre[r];
+    }
+    if (un != 0 && !emulate) {
+        char buf[200];
+        const unsigned long long nn = (unsigned long long)n * n;
+        std::snprintf(buf, sizeof buf, "assertion `left == right` failed\n  left: %llu\n right: %llu", nn - un, nn);
+        set_err(err, SRT_ERR_DISCONNECTED, buf);
+        return SRT_ERR_DISCONNECTED;
+    }
+    if (min_latency_ns) *min_latency_ns = mn;
+    // the diagonal: the raw self-loops (mod.rs:210-217), from the host
+    if (ct) {
+        ct->diag.resize(n);
+        for (uint32_t i = 0; i < n; ++i) ct->diag[i] = srt_path{p0->h_sl_lat[i], p0->h_sl_loss[i], 0u};
+    } else {
+        for (uint32_t i = 0; i < n; ++i) out[(uint64_t)i * n + i] = srt_path{p0->h_sl_lat[i], p0->h_sl_loss[i], 0u};
+    }
+    return SRT_OK;
+}
+
 // The multi-GPU build inside the caller's process (srt_opts.n_gpus > 1): one
 // host thread and one plan per device, bound to an in-process communicator
 // (srt_comm_init_local), every sharded schedule unchanged; rank 0's plan holds
@@ -1999,6 +2177,31 @@ srt_status build_multi(const srt_csr *g, const uint32_t *nodes, uint32_t n, srt_
     }
     std::vector<int32_t> devs(N);
     for (int r = 0; r < N; ++r) devs[r] = same ? first : first + r;
+    {
+        // rank 0's plan: the one CSR scan + upload and the family choice; a
+        // level plan needs no other plan (build_multi_level)
+        srt_opts o0 = *opts;
+        o0.device = devs[0];
+        o0.n_gpus = 1;
+        o0.flags &= ~(uint32_t)SRT_OPT_SAME_DEVICE;
+        srt_plan *p0 = nullptr;
+        if (srt_status s = plan_create_impl(g, nodes, n, &o0, &p0, err, true); s != SRT_OK) return s;
+        if (p0->algo == SRT_ALGO_LEVEL) {
+            srt_status s = build_multi_level(p0, devs, out, ct, min_latency_ns, err);
+            // the device's loss range check: a parse-time error, so it wins
+            if (p0->h_lossbad && s != SRT_ERR_HIP) {
+                (void)hipSetDevice(p0->device);
+                (void)hipStreamSynchronize(p0->comm_stream);
+                if (*p0->h_lossbad != ~0ull) {
+                    s = SRT_ERR_INVALID;
+                    set_err(err, SRT_ERR_INVALID, "Edge 'packet_loss' is not in the range [0,1]");
+                }
+            }
+            reap_async(p0);
+            return s;
+        }
+        srt_plan_destroy(p0);
+    }
     std::vector<srt_comm *> comms(N, nullptr);
     if (srt_status s = srt_comm_init_local(N, devs.data(), comms.data(), err); s != SRT_OK) return s;
     std::vector<srt_plan *> plans(N, nullptr);

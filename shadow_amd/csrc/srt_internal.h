@@ -398,6 +398,30 @@ srt_status fw_loss(srt_plan *p, unsigned long long *d_stats, srt_err *err);
 // row walks), and the build of rows [row0, row1) into the table
 srt_status level_probe(srt_plan *p, uint64_t wmax, uint64_t *bound, uint64_t *visits, srt_err *err);
 srt_status level_run(srt_plan *p, unsigned long long *d_stats, srt_err *err);
+// what a level solve launch reads and writes: a plan's buffers (level_ctx),
+// or a peer device's copies of its class CSRs (the in-process multi-GPU build)
+struct LevelCtx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t V = 0, n = 0, t_cls = 16;
+    uint64_t g = 1;
+    const uint32_t *tcls = nullptr;  // 2 * (V * t_cls + 1) class offsets (out, then in)
+    const uint64_t *ce_out = nullptr, *ce_in = nullptr;
+    const uint32_t *nodes = nullptr;
+    const uint64_t *sl_lat = nullptr;
+    const float *sl_loss = nullptr;
+    uint64_t *out_lat = nullptr;
+    float *out_loss = nullptr;
+};
+LevelCtx level_ctx(srt_plan *p);
+// the class CSRs of a level plan at its bound (the run's first step)
+srt_status level_prepare(srt_plan *p, srt_err *err);
+// rows [r0, r1) staged as u16 latency units + f32 loss (row r0 + k at k * n),
+// (min latency, unreachable) min/added into d_stats, on c.stream
+void level_solve_stage(const LevelCtx &c, uint32_t r0, uint32_t r1, uint32_t lmax, uint16_t *stage_lat,
+                       float *stage_loss, unsigned long long *d_stats);
+// d_stats = (~0, 0) on stream s
+void level_stats_init(unsigned long long *d_stats, hipStream_t s);
 // sharded tail: every rank's staged rows (d_slat / d_sloss, all-gathered) into the table
 void expand_shard_rows(srt_plan *p, int nranks);
 // table entries [first, first + count) -> d_pack[0, count) as srt_path

@@ -2391,6 +2391,28 @@ srt_status loss_emulated_t(srt_plan *p, unsigned long long *d_stats, srt_err *er
     return SRT_OK;
 }
 
+}  // namespace
+
+LevelCtx level_ctx(srt_plan *p) {
+    LevelCtx c;
+    c.device = p->device;
+    c.stream = p->stream;
+    c.V = p->V;
+    c.n = p->n;
+    c.g = p->kp.g;
+    c.t_cls = p->t_cls;
+    c.tcls = p->d_tcls;
+    c.ce_out = p->d_tpk;
+    c.ce_in = p->d_tpk2;
+    c.nodes = p->d_nodes;
+    c.sl_lat = p->d_sl_lat;
+    c.sl_loss = p->d_sl_loss;
+    c.out_lat = p->d_out_lat;
+    c.out_loss = p->d_out_loss;
+    return c;
+}
+
+namespace {
 // ------------------------------------------------------------ level solve
 // The class CSRs of the graph's edges of latency <= wmax units (self-loops
 // dropped), classes = exact weights 1..wmax <= WC: out-rows straight from the
@@ -2473,33 +2495,41 @@ srt_status level_csr(srt_plan *p, uint64_t wmax, bool with_loss, srt_err *err) {
     return SRT_OK;
 }
 
-// level_solve_kernel over the rows of job (probe: the row list's first row,
-// no table, reverse = in- and out-CSRs swapped: distances TO the row's node)
-srt_status launch_solve(srt_plan *p, unsigned long long *d_stats, const RowJob &job, uint32_t lcap, bool reverse,
-                        uint32_t *probe) {
-    const uint32_t V = p->V, rows = job.list ? job.count : job.range ? job.r1 - job.r0 : p->row1 - p->row0;
-    if (!rows) return SRT_OK;
+// level_solve_kernel over rows [r0, r1) (or the row list) of the context c
+// (probe: no table, reverse = in- and out-CSRs swapped: distances TO the
+// row's node); staging: u16 latency units + f32 loss, row k of the job at k * n
+void launch_solve_ctx(const LevelCtx &c, unsigned long long *d_stats, const uint32_t *list, uint32_t r0, uint32_t r1,
+                      uint32_t lcap, bool reverse, uint32_t *probe, void *out16, float *out_loss_stage) {
+    const uint32_t V = c.V, rows = list ? r1 : r1 - r0;
+    if (!rows) return;
     const uint32_t nt = V >= 2048 ? LOSS_NT : 256;
     const size_t lds = SOLVE_HIST + (((size_t)V * 2 + 15) & ~(size_t)15) + (size_t)V * 4 +
                        (((size_t)V * 2 + 15) & ~(size_t)15);
     const int per_cu = std::max(1, std::min(2048 / (int)nt, (int)std::max<size_t>(1, (160 * 1024) / (lds + 2048))));
-    const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(rows, (uint32_t)(cu_count(p->device) * per_cu)));
+    const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(rows, (uint32_t)(cu_count(c.device) * per_cu)));
     // table rows by non-temporal stores (knob SRT_LVL_NT=0/1: A/B measurement)
     static const bool nts = !(std::getenv("SRT_LVL_NT") && std::atoi(std::getenv("SRT_LVL_NT")) == 0);
-    auto kern = p->t_cls == 16 ? (nts ? level_solve_kernel<4, 4, 16, 2, true> : level_solve_kernel<4, 4, 16, 2, false>)
-                               : (nts ? level_solve_kernel<4, 2, 32, 2, true> : level_solve_kernel<4, 2, 32, 2, false>);
+    auto kern = c.t_cls == 16 ? (nts ? level_solve_kernel<4, 4, 16, 2, true> : level_solve_kernel<4, 4, 16, 2, false>)
+                              : (nts ? level_solve_kernel<4, 2, 32, 2, true> : level_solve_kernel<4, 2, 32, 2, false>);
     (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(LDS_BUDGET - 4096));
-    const uint64_t vc1 = (uint64_t)V * p->t_cls + 1;
-    const uint32_t *co = p->d_tcls, *ci = p->d_tcls + vc1;
-    const uint64_t *eo = p->d_tpk, *ei = p->d_tpk2;
+    const uint64_t vc1 = (uint64_t)V * c.t_cls + 1;
+    const uint32_t *co = c.tcls, *ci = c.tcls + vc1;
+    const uint64_t *eo = c.ce_out, *ei = c.ce_in;
     if (reverse) {
         std::swap(co, ci);
         std::swap(eo, ei);
     }
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, p->stream, V, p->d_nodes, p->n,
-                       job.list ? 0u : job.range ? job.r0 : p->row0, job.list ? job.count : job.range ? job.r1 : p->row1,
-                       co, ci, eo, ei, lcap, p->kp.g, p->d_sl_lat, p->d_sl_loss, p->d_out_lat, p->d_out_loss, d_stats,
-                       job.list, job.out32, job.out32_loss, p->stage16, probe);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, c.stream, V, c.nodes, c.n, list ? 0u : r0, list ? r1 : r1, co,
+                       ci, eo, ei, lcap, c.g, c.sl_lat, c.sl_loss, c.out_lat, c.out_loss, d_stats, list, out16,
+                       out_loss_stage, out16 != nullptr, probe);
+}
+
+srt_status launch_solve(srt_plan *p, unsigned long long *d_stats, const RowJob &job, uint32_t lcap, bool reverse,
+                        uint32_t *probe) {
+    const uint32_t r0 = job.list ? 0u : job.range ? job.r0 : p->row0;
+    const uint32_t r1 = job.list ? job.count : job.range ? job.r1 : p->row1;
+    launch_solve_ctx(level_ctx(p), d_stats, job.list, r0, r1, lcap, reverse, probe,
+                     job.out32_loss && p->stage16 ? job.out32 : nullptr, job.out32_loss);
     return SRT_OK;
 }
 
@@ -2615,6 +2645,17 @@ srt_status level_sharded(srt_plan *p, unsigned long long *d_stats, srt_err *err)
     return SRT_OK;
 }
 }  // namespace
+
+srt_status level_prepare(srt_plan *p, srt_err *err) { return level_csr(p, p->kp.lmax, true, err); }
+
+void level_solve_stage(const LevelCtx &c, uint32_t r0, uint32_t r1, uint32_t lmax, uint16_t *stage_lat,
+                       float *stage_loss, unsigned long long *d_stats) {
+    launch_solve_ctx(c, d_stats, nullptr, r0, r1, lmax, false, nullptr, stage_lat, stage_loss);
+}
+
+void level_stats_init(unsigned long long *d_stats, hipStream_t s) {
+    hipLaunchKernelGGL(loss_stats_init_kernel, dim3(1), dim3(1), 0, s, d_stats, d_stats + 2);
+}
 
 srt_status level_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     if (!p->ev_loss0) {

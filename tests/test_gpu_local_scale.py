@@ -134,3 +134,31 @@ def test_c4_100k_sparse_two_ranks():
             kept.close()
     finally:
         one.close()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_c3_16k_routing_info_in_process_ranks(c3, world):
+    """generate_routing_info over `world` in-process ranks (the drop-in's
+    srt_opts.n_gpus; here every rank on device 0): rank 0's plan scans the CSR
+    once, every rank solves its rows and downloads them into the RoutingInfo
+    records -- the table equals the one-GPU RoutingInfo's bit for bit, and the
+    16 oracle rows."""
+    from shadow_amd import RoutingInfo
+
+    g, nodes, one, rows, elat, eloss, sl_l, sl_p = c3
+    multi = RoutingInfo.build(g, nodes, device=0, n_gpus=world, same_device=True)
+    single = RoutingInfo.build(g, nodes, device=0)
+    try:
+        assert multi.record_bytes() == single.record_bytes() == 6
+        assert multi.get_smallest_latency_ns() == single.get_smallest_latency_ns() == one.min_latency_ns
+        ml, mp = multi.table()
+        sl, sp = single.table()
+        assert np.array_equal(ml, sl) and np.array_equal(mp.view(np.uint32), sp.view(np.uint32))
+        del sl, sp
+        for k, r in enumerate(rows):
+            exp_l, exp_p = elat[k].copy(), eloss[k].copy()
+            exp_l[r], exp_p[r] = sl_l[r], sl_p[r]
+            assert np.array_equal(ml[r], exp_l) and np.array_equal(mp[r].view(np.uint32), exp_p.view(np.uint32)), r
+    finally:
+        multi.close()
+        single.close()
