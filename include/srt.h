@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define SRT_ABI_VERSION 1
+#define SRT_ABI_VERSION 2
 
 typedef enum {
     SRT_OK = 0,
@@ -170,6 +170,7 @@ typedef struct {
     uint32_t loss_fold;         /* dense: 1 = the level fold (tight edges walked by weight class
                                    from the smaller latency level), 0 = the single-direction scan */
     uint32_t reserved0;
+    uint64_t edge_visits;       /* level solve: class-CSR entries the last run's rows walked (ABI 2) */
 } srt_timing;
 srt_status srt_plan_timing(const srt_plan *plan, srt_timing *out);
 /* C tiles (128 x 128 keys) the last FW run's dominant launches loaded and

@@ -55,7 +55,8 @@ class SrtTiming(C.Structure):
     _fields_ = [("total_ms", C.c_double), ("dominant_ms", C.c_double), ("dominant_launches", C.c_uint64),
                 ("dominant_work", C.c_double), ("loss_ms", C.c_double), ("tight_edges", C.c_uint64),
                 ("sharded_tail", C.c_uint32), ("sparse_split", C.c_uint32),
-                ("sparse_sweeps", C.c_uint64), ("loss_fold", C.c_uint32), ("reserved0", C.c_uint32)]
+                ("sparse_sweeps", C.c_uint64), ("loss_fold", C.c_uint32), ("reserved0", C.c_uint32),
+                ("edge_visits", C.c_uint64)]
 
 
 class SrtRound(C.Structure):
@@ -154,7 +155,7 @@ def lib():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
-        if L.srt_abi_version() != 1:
+        if L.srt_abi_version() != 2:
             raise SrtError(SRT_ERR_UNSUPPORTED, "libsrt ABI version mismatch")
         _lib = L
     return _lib

@@ -589,6 +589,7 @@ void free_plan_buffers(srt_plan *p) {
     if (p->d_lossbad) hipFree(p->d_lossbad);
     if (p->h_lossbad) hipHostFree(p->h_lossbad);
     hipFree(p->d_rstats);
+    hipFree(p->d_lvisit);
     hipFree(p->d_ev_scratch);
     hipFree(p->d_tflag);
     hipFree(p->d_tcnt);
@@ -1433,6 +1434,10 @@ srt_status srt_plan_sync(srt_plan *p, srt_err *err) {
     }
     if (p->algo != SRT_ALGO_SSSP && p->ev_loss0 && hipEventElapsedTime(&ms, p->ev_loss0, p->ev_loss1) == hipSuccess)
         p->loss_ms = ms;
+    if (p->algo == SRT_ALGO_LEVEL && p->d_lvisit) {
+        unsigned long long v = 0;
+        if (hipMemcpy(&v, p->d_lvisit, sizeof v, hipMemcpyDeviceToHost) == hipSuccess) p->lvl_visits = v;
+    }
     return SRT_OK;
 }
 
@@ -1522,6 +1527,7 @@ srt_status srt_plan_timing(const srt_plan *p, srt_timing *o) {
     o->sparse_sweeps = p->algo == SRT_ALGO_SSSP ? p->sssp_sweeps : 0;
     o->loss_fold = p->algo == SRT_ALGO_FW && p->t_level ? 1u : 0u;
     o->reserved0 = 0;
+    o->edge_visits = p->algo == SRT_ALGO_LEVEL ? p->lvl_visits : 0;
     return SRT_OK;
 }
 
@@ -2036,6 +2042,7 @@ srt_status build_multi_level(srt_plan *p0, const std::vector<int32_t> &devs, srt
         hipError_t e = hipSetDevice(devs[r]);
         srt::LevelCtx c = c0;
         c.device = devs[r];
+        c.visits = nullptr;
         if (e == hipSuccess) e = r == 0 ? hipSuccess : hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
         if (r == 0) st = p0->stream;
         c.stream = st;

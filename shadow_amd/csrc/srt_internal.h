@@ -283,6 +283,8 @@ struct srt_plan {
     uint32_t t_cls = 16;             // class offsets per vertex of the level fold's CSRs (16 or 32)
     uint32_t *d_tcw = nullptr;       // quantized fold: each class entry's exact weight (out, then in), t_cap each
     uint64_t lvl_cap = 0;            // level solve: class entries d_tpk / d_tpk2 hold (the probe's count)
+    unsigned long long *d_lvisit = nullptr;  // level solve: class entries the last run walked
+    uint64_t lvl_visits = 0;                 // its host copy (srt_plan_sync)
     uint64_t tcw_cap = 0;            // d_tcw entries
     uint32_t *d_tcls = nullptr;      // 2 * (V*16 + 1) class offsets
     uint32_t *d_tccnt = nullptr;     // 2 * (V*16 + 1) class counts / fill cursors
@@ -412,6 +414,7 @@ struct LevelCtx {
     const float *sl_loss = nullptr;
     uint64_t *out_lat = nullptr;
     float *out_loss = nullptr;
+    unsigned long long *visits = nullptr;  // class entries walked (nullable)
 };
 LevelCtx level_ctx(srt_plan *p);
 // the class CSRs of a level plan at its bound (the run's first step)

@@ -1389,9 +1389,10 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
     const uint64_t *__restrict__ ce_in, uint32_t lcap, uint64_t g, const uint64_t *__restrict__ sl_lat,
     const float *__restrict__ sl_loss, uint64_t *__restrict__ out_lat, float *__restrict__ out_loss,
     unsigned long long *stats, const uint32_t *__restrict__ row_list, void *__restrict__ out32,
-    float *__restrict__ out32_loss, bool stage16, uint32_t *__restrict__ probe) {
+    float *__restrict__ out32_loss, bool stage16, uint32_t *__restrict__ probe,
+    unsigned long long *__restrict__ visit_cnt) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    __shared__ unsigned long long red_min[16], red_cnt[16];
+    __shared__ unsigned long long red_min[16], red_cnt[16], red_vis[16];
     __shared__ uint32_t red_max[16];
     constexpr uint32_t WCN = CLSN - 1;
     __shared__ uint32_t plan_end[WCN + 1];
@@ -1671,20 +1672,23 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
     }
     if (lane == 0) {
         red_min[wv] = mn;
-        red_cnt[wv] = probe ? visits : unreach;
+        red_cnt[wv] = unreach;
+        red_vis[wv] = visits;
     }
     __syncthreads();
     if (tid == 0) {
-        unsigned long long m = red_min[0], c = red_cnt[0];
+        unsigned long long m = red_min[0], c = red_cnt[0], vz = red_vis[0];
         for (int q = 1; q < nw; ++q) {
             m = red_min[q] < m ? red_min[q] : m;
             c += red_cnt[q];
+            vz += red_vis[q];
         }
         if (probe) {
-            if (c) atomicAdd(reinterpret_cast<unsigned long long *>(probe), c);
+            if (vz) atomicAdd(reinterpret_cast<unsigned long long *>(probe), vz);
         } else {
             atomicMin(&stats[0], m);
             if (c) atomicAdd(&stats[1], c);
+            if (visit_cnt && vz) atomicAdd(visit_cnt, vz);
         }
     }
 }
@@ -2409,6 +2413,7 @@ LevelCtx level_ctx(srt_plan *p) {
     c.sl_loss = p->d_sl_loss;
     c.out_lat = p->d_out_lat;
     c.out_loss = p->d_out_loss;
+    c.visits = p->d_lvisit;
     return c;
 }
 
@@ -2521,7 +2526,7 @@ void launch_solve_ctx(const LevelCtx &c, unsigned long long *d_stats, const uint
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, c.stream, V, c.nodes, c.n, list ? 0u : r0, list ? r1 : r1, co,
                        ci, eo, ei, lcap, c.g, c.sl_lat, c.sl_loss, c.out_lat, c.out_loss, d_stats, list, out16,
-                       out_loss_stage, out16 != nullptr, probe);
+                       out_loss_stage, out16 != nullptr, probe, c.visits);
 }
 
 srt_status launch_solve(srt_plan *p, unsigned long long *d_stats, const RowJob &job, uint32_t lcap, bool reverse,
@@ -2670,6 +2675,11 @@ srt_status level_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     if (st != SRT_OK) return st;
     hipLaunchKernelGGL(loss_stats_init_kernel, dim3(1), dim3(1), 0, p->stream, d_stats,
                        (unsigned long long *)p->d_tmaxw);
+    if (!p->d_lvisit) {
+        const hipError_t e = hipMalloc(&p->d_lvisit, sizeof(unsigned long long));
+        if (e != hipSuccess) return fail(err, e, "hipMalloc(visit counter)");
+    }
+    (void)hipMemsetAsync(p->d_lvisit, 0, sizeof(unsigned long long), p->stream);
 #if LOSS_COUNT
     {
         const uint32_t dg = std::getenv("SRT_LVL_DIAG") ? (uint32_t)std::atoi(std::getenv("SRT_LVL_DIAG")) : 0u;
