@@ -180,9 +180,12 @@ def measured_traffic(args, kernel_tag, schedule):
             continue
         if d.get("schedule") != schedule:
             continue
-        for k, v in d.get("kernels", {}).items():
-            if kernel_tag in k:
-                return v["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
+        # several instantiations may carry the tag (the level family's probe
+        # launches use a smaller variant): the dominant one moved the most bytes
+        hits = [v for k, v in d.get("kernels", {}).items() if kernel_tag in k]
+        if hits:
+            v = max(hits, key=lambda v: v["hbm_bytes_per_launch"] * v.get("dispatches", 1))
+            return v["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
     return None, None
 
 
