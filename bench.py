@@ -524,8 +524,12 @@ def bench_graph(args, cfg, D):
             achieved = alg_bytes / avg_launch_s
             visits = visits_run // max(n, 1)
             lmax = int(desc.split(" lmax=")[1].split("(")[0])
+            sh = int(desc.split(" q=")[1].split()[0]) if " q=" in desc else 0  # quantized: bucket width
             schedule = {"family": "level", "lmax": lmax, "rows_per_launch": int(work_per_launch // max(n, 1))}
-            traffic, traffic_src = measured_traffic(args, "level_solve_kernel", schedule)
+            if sh:
+                schedule["q"] = sh
+            kname = "level_q_kernel" if sh else "level_solve_kernel"
+            traffic, traffic_src = measured_traffic(args, kname, schedule)
             roofline = {
                 "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK, "traffic": traffic,
@@ -534,7 +538,8 @@ def bench_graph(args, cfg, D):
                                    f"not measured in this run" if traffic_src else
                                    "no committed PMC summary for this workload/schedule"),
                 "schedule": schedule,
-                "kernel": "level_solve_kernel (per-source bucket Dijkstra over the class CSRs, one workgroup a row)",
+                "kernel": (f"{kname} (per-source bucket Dijkstra over the class CSRs, one workgroup a row"
+                           + (f"; buckets of {sh} units, u64 (latency, loss) keys)" if sh else ")")),
                 "avg_launch_ms": avg_launch_s * 1e3, "pairs_per_launch": work_per_launch,
                 "algorithmic_bytes_per_launch": alg_bytes,
                 "basis": "12 B per table pair written (u64 latency + f32 loss) + 8 B per class-CSR entry the rows "
@@ -542,7 +547,8 @@ def bench_graph(args, cfg, D):
                 "edge_visits_per_row": visits,
                 "edge_visits_per_s": visits_launch / avg_launch_s}
             algo = (f"level solve: per-source bucket (Dial) Dijkstra over the edges <= {lmax} units (a bound proved "
-                    f"by probe rows), loss folded in the same pass")
+                    f"by probe rows), loss folded in the same pass"
+                    + (f"; quantized buckets of {sh} units (the shortest edge)" if sh else ""))
         elif desc.startswith("fw"):
             B_TILE = 128
             kbytes = {"f16": 2, "u16": 2, "u32": 4}.get(key, 8)

@@ -590,6 +590,7 @@ void free_plan_buffers(srt_plan *p) {
     if (p->h_lossbad) hipHostFree(p->h_lossbad);
     hipFree(p->d_rstats);
     hipFree(p->d_lvisit);
+    hipFree(p->d_lmem);
     hipFree(p->d_ev_scratch);
     hipFree(p->d_tflag);
     hipFree(p->d_tcnt);
@@ -971,7 +972,9 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     //     on every in-use shortest path over the edges <= min(31, max edge)
     //     units; the solve applies when one was found (B <= 31).
     uint64_t lvl_bound = ~0ull, lvl_visits = 0;
-    std::string why_lvl = "the level solve needs V <= 18400 and every shortest path <= 31 latency units";
+    std::string why_lvl =
+        "the level solve needs V <= 18400 and every shortest path <= 31 latency units (or 31 buckets as wide "
+        "as the shortest edge)";
     {
         const uint64_t maxu = cs.maxlat / cs.gcd;
         const bool fits = p->V >= 2 && p->V <= srt::LEVEL_V_MAX && n >= 1;
@@ -980,11 +983,38 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
                              (want == SRT_ALGO_LEVEL || (want == SRT_ALGO_AUTO && !(kl && std::atoi(kl) == 0)));
         if (try_lvl) {
             p->kp.g = cs.gcd;
+            p->lvl_q = 0;
             srt_err e2{};
-            if (srt::level_probe(p, std::min<uint64_t>(31, maxu), &lvl_bound, &lvl_visits, &e2) != SRT_OK) {
+            auto probe_fail = [&]() {
                 srt_plan_destroy(p);
                 if (err) *err = e2;
                 return e2.code ? (srt_status)e2.code : SRT_ERR_HIP;
+            };
+            if (srt::level_probe(p, std::min<uint64_t>(31, maxu), &lvl_bound, &lvl_visits, &e2) != SRT_OK)
+                return probe_fail();
+            // no bound within 31 units: the quantized solve, buckets of q <= the
+            // shortest edge (C3ns: g = 1 ns, edges >= 1 ms), when the shortest
+            // paths stay under 32 such buckets
+            const char *kq = std::getenv("SRT_LEVEL_Q");  // knob: 0 = integer levels only (A/B, tests)
+            if (lvl_bound == ~0ull && !(kq && std::atoi(kq) == 0)) {
+                uint64_t mn_ns = ~0ull;
+                if (srt::level_min_edge(p, &mn_ns, &e2) != SRT_OK) return probe_fail();
+                const uint64_t mu = mn_ns == ~0ull ? 0 : mn_ns / cs.gcd;
+                const uint32_t vb = srt::level_vbits(p->V);
+                // an entry keeps the remainder w - c q (< q) in 34 - vb bits;
+                // latencies up to 32 q stay below 2^31
+                const uint64_t q = std::min<uint64_t>(std::min<uint64_t>(mu, 1ull << (34 - vb)), 1ull << 26);
+                if (q >= 2) {
+                    uint32_t rb = 0;
+                    while ((1ull << rb) < q) ++rb;
+                    p->lvl_q = (uint32_t)q;
+                    p->lvl_rb = rb;
+                    p->lvl_vb = vb;
+                    if (srt::level_probe(p, std::min<uint64_t>(maxu, 32 * q - 1), &lvl_bound, &lvl_visits, &e2) !=
+                        SRT_OK)
+                        return probe_fail();
+                    if (lvl_bound == ~0ull) p->lvl_q = 0;
+                }
             }
             // the probe's lists were sized for it; the run builds its own
             p->t_edges = 0;
@@ -1024,11 +1054,14 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     p->algo = algo;
     if (algo == SRT_ALGO_LEVEL) {
         // levels are exact integers <= B in units of g: 2-byte download records
+        // (quantized: B < 32 << sh < 2^31, 4-byte ones)
         p->kp.g = cs.gcd;
         p->kp.lmax = lvl_bound;
         p->kp.lat32 = true;
-        p->key_type = srt::KEY_U16;
+        p->key_type = p->lvl_q ? srt::KEY_U32 : srt::KEY_U16;
         f16 = false;
+    } else {
+        p->lvl_q = 0;
     }
     // SSSP plans read their in-edges (with loss) from the host-built list, never
     // d_loss: drop the deferred upload so run_tail does not copy it
@@ -1042,9 +1075,14 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     p->rows_alloc = n;
     char d[200];
     if (algo == SRT_ALGO_LEVEL) {
-        std::snprintf(d, sizeof d, "level:u16 g=%llu lmax=%llu(probe) V=%u n=%u visits=%llu loss=in-solve",
-                      (unsigned long long)p->kp.g, (unsigned long long)p->kp.lmax, p->V, n,
-                      (unsigned long long)lvl_visits);
+        if (p->lvl_q)
+            std::snprintf(d, sizeof d, "level:u32 g=%llu q=%u lmax=%llu(probe) V=%u n=%u visits=%llu loss=in-solve",
+                          (unsigned long long)p->kp.g, p->lvl_q, (unsigned long long)p->kp.lmax, p->V, n,
+                          (unsigned long long)lvl_visits);
+        else
+            std::snprintf(d, sizeof d, "level:u16 g=%llu lmax=%llu(probe) V=%u n=%u visits=%llu loss=in-solve",
+                          (unsigned long long)p->kp.g, (unsigned long long)p->kp.lmax, p->V, n,
+                          (unsigned long long)lvl_visits);
     } else if (algo == SRT_ALGO_FW) {
         p->fw_f16 = f16 && p->fw_glds;
         if (const char *e = std::getenv("SRT_FW_P1")) p->fw_p1 = std::atoi(e);
@@ -2010,9 +2048,11 @@ srt_status build_multi_level(srt_plan *p0, const std::vector<int32_t> &devs, srt
     HIP_TRY(hipEventCreateWithFlags(&ready, hipEventDisableTiming), "event");
     HIP_TRY(hipEventRecord(ready, p0->stream), "event record");
     tr.mark("multi: class CSRs on rank 0");
+    // quantized plans (latency units past u16): u32 staging, 8-byte records
+    const bool quant = p0->lvl_q != 0;
     if (ct) {
         const int T = host_threads((uint64_t)n * n);
-        if (!ct_alloc(ct, n, p0->kp.g, true, T)) {
+        if (!ct_alloc(ct, n, p0->kp.g, !quant, T)) {
             (void)hipEventDestroy(ready);
             set_err(err, SRT_ERR_OOM, "out of host memory (routing table)");
             return SRT_ERR_OOM;
@@ -2068,32 +2108,42 @@ srt_status build_multi_level(srt_plan *p0, const std::vector<int32_t> &devs, srt
             c.sl_lat = sl;
             c.sl_loss = sp;
         }
-        uint16_t *s16 = nullptr;
+        // staging: u16 (u32 when quantized) latency units + f32 loss, or --
+        // quantized into a RoutingInfo -- its 8-byte records as they are
+        const size_t lw = quant ? 4 : 2;
+        const uint32_t mode = quant ? (ct ? 3u : 2u) : 1u;
+        void *s16 = nullptr;
         float *sloss = nullptr;
         unsigned long long *dst = nullptr;
         if (e == hipSuccess) {
-            s16 = (uint16_t *)dev_alloc(rows * n * 2 + 256);
-            sloss = (float *)dev_alloc(rows * n * 4);
+            s16 = dev_alloc(mode == 3 ? rows * n * 8 : rows * n * lw + 256);
+            sloss = mode == 3 ? nullptr : (float *)dev_alloc(rows * n * 4);
             dst = (unsigned long long *)dev_alloc(4 * 8);
-            if (!s16 || !sloss || !dst) e = hipErrorOutOfMemory;
+            // the quantized solve's per-workgroup scratch: every rank its own
+            // (ranks sharing a device run concurrently)
+            if (quant) c.lmem = (uint16_t *)dev_alloc(srt::level_scratch_bytes(devs[r], p0->V, true));
+            if (!s16 || (mode != 3 && !sloss) || !dst || (quant && !c.lmem)) e = hipErrorOutOfMemory;
         }
         if (e == hipSuccess && rows) {
             srt::level_stats_init(dst, st);
-            srt::level_solve_stage(c, r0, r1, (uint32_t)p0->kp.lmax, s16, sloss, dst);
+            srt::level_solve_stage(c, r0, r1, (uint32_t)p0->kp.lmax, s16, sloss, mode, dst);
         }
         unsigned long long hs[2] = {~0ull, 0};
-        std::vector<uint16_t> h16;
+        std::vector<uint8_t> h16;
         std::vector<float> hl;
         if (e == hipSuccess && rows) {
-            if (ct) {
+            if (ct && mode == 3) {
+                // straight into the RoutingInfo's 8-byte records
+                e = hipMemcpyAsync(ct->rec8 + (uint64_t)r0 * n, s16, rows * n * 8, hipMemcpyDeviceToHost, st);
+            } else if (ct) {
                 // straight into the RoutingInfo's 6-byte records
                 e = hipMemcpyAsync(ct->lat16 + (uint64_t)r0 * n, s16, rows * n * 2, hipMemcpyDeviceToHost, st);
                 if (e == hipSuccess)
                     e = hipMemcpyAsync(ct->loss + (uint64_t)r0 * n, sloss, rows * n * 4, hipMemcpyDeviceToHost, st);
             } else {
-                h16.resize(rows * n);
+                h16.resize(rows * n * lw);
                 hl.resize(rows * n);
-                e = hipMemcpyAsync(h16.data(), s16, rows * n * 2, hipMemcpyDeviceToHost, st);
+                e = hipMemcpyAsync(h16.data(), s16, rows * n * lw, hipMemcpyDeviceToHost, st);
                 if (e == hipSuccess) e = hipMemcpyAsync(hl.data(), sloss, rows * n * 4, hipMemcpyDeviceToHost, st);
             }
             if (e == hipSuccess) e = hipMemcpyAsync(hs, dst, sizeof hs, hipMemcpyDeviceToHost, st);
@@ -2103,10 +2153,15 @@ srt_status build_multi_level(srt_plan *p0, const std::vector<int32_t> &devs, srt
             // expanded into the caller's srt_path rows by this rank's share of the host threads
             const uint64_t g = p0->kp.g, cnt = rows * n;
             const int T = std::max(1, host_threads(cnt) / (emulate ? 1 : N));
+            const uint16_t *l16 = reinterpret_cast<const uint16_t *>(h16.data());
+            const uint32_t *l32 = reinterpret_cast<const uint32_t *>(h16.data());
             auto part = [&](int w) {
                 for (uint64_t k = cnt * w / T; k < cnt * (w + 1) / T; ++k) {
                     srt_path q;
-                    q.latency_ns = h16[k] == 0xffffu ? ~0ull : (uint64_t)h16[k] * g;
+                    if (quant)
+                        q.latency_ns = l32[k] == ~0u ? ~0ull : (uint64_t)l32[k] * g;
+                    else
+                        q.latency_ns = l16[k] == 0xffffu ? ~0ull : (uint64_t)l16[k] * g;
                     q.packet_loss = hl[k];
                     q._pad = 0;
                     out[(uint64_t)r0 * n + k] = q;

@@ -284,6 +284,9 @@ struct srt_plan {
     uint32_t *d_tcw = nullptr;       // quantized fold: each class entry's exact weight (out, then in), t_cap each
     uint64_t lvl_cap = 0;            // level solve: class entries d_tpk / d_tpk2 hold (the probe's count)
     unsigned long long *d_lvisit = nullptr;  // level solve: class entries the last run walked
+    uint32_t lvl_q = 0, lvl_rb = 0, lvl_vb = 0;  // quantized level solve: bucket width (units), entry field bits
+    uint16_t *d_lmem = nullptr;              // its per-workgroup scratch (lmem_cap u16)
+    uint64_t lmem_cap = 0;
     uint64_t lvl_visits = 0;                 // its host copy (srt_plan_sync)
     uint64_t tcw_cap = 0;            // d_tcw entries
     uint32_t *d_tcls = nullptr;      // 2 * (V*16 + 1) class offsets
@@ -415,14 +418,24 @@ struct LevelCtx {
     uint64_t *out_lat = nullptr;
     float *out_loss = nullptr;
     unsigned long long *visits = nullptr;  // class entries walked (nullable)
+    uint32_t q = 0, rb = 0, vb = 0;        // quantized solve: bucket width (units), remainder / vertex bits of an entry
+    uint16_t *lmem = nullptr;              // quantized solve: level_scratch_bytes of per-workgroup scratch
 };
 LevelCtx level_ctx(srt_plan *p);
 // the class CSRs of a level plan at its bound (the run's first step)
 srt_status level_prepare(srt_plan *p, srt_err *err);
-// rows [r0, r1) staged as u16 latency units + f32 loss (row r0 + k at k * n),
-// (min latency, unreachable) min/added into d_stats, on c.stream
-void level_solve_stage(const LevelCtx &c, uint32_t r0, uint32_t r1, uint32_t lmax, uint16_t *stage_lat,
-                       float *stage_loss, unsigned long long *d_stats);
+// rows [r0, r1) staged (row r0 + k at k * n) as u16 (stage_mode 1) or u32 (2)
+// latency units + f32 loss, or as 8-byte records {u32 units, loss bits} (3,
+// quantized plans only); (min latency, unreachable) min/added into d_stats, on
+// c.stream
+void level_solve_stage(const LevelCtx &c, uint32_t r0, uint32_t r1, uint32_t lmax, void *stage_lat,
+                       float *stage_loss, uint32_t stage_mode, unsigned long long *d_stats);
+// bytes of the quantized solve's scratch on `device` for V vertices (0 unless quant)
+size_t level_scratch_bytes(int device, uint32_t V, bool quant);
+// bits of a vertex index < V in a quantized class entry
+uint32_t level_vbits(uint32_t V);
+// the shortest non-self-loop edge latency of the plan's uploaded graph, ns
+srt_status level_min_edge(srt_plan *p, uint64_t *min_ns, srt_err *err);
 // d_stats = (~0, 0) on stream s
 void level_stats_init(unsigned long long *d_stats, hipStream_t s);
 // sharded tail: every rank's staged rows (d_slat / d_sloss, all-gathered) into the table

@@ -293,6 +293,7 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t V, const uint64_t
                                                       const uint32_t *__restrict__ col,
                                                       const uint64_t *__restrict__ lat, const float *__restrict__ loss,
                                                       uint64_t g, double inv_g, uint64_t wmax_ns, uint32_t cls,
+                                                      uint32_t q, uint32_t vb,
                                                       uint32_t *__restrict__ off_out, uint32_t *__restrict__ in_cnt,
                                                       uint64_t *__restrict__ ce_out, uint64_t cap,
                                                       unsigned long long *cursor, unsigned long long *maxw) {
@@ -302,7 +303,9 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t V, const uint64_t
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     uint32_t mw = 0;
-    auto cls_of = [&](uint64_t l) -> uint32_t { return (uint32_t)((double)l * inv_g + 0.5); };  // l = c * g exactly
+    // l = w * g exactly; the class: w / q (q = 0: the exact weight)
+    auto units_of = [&](uint64_t l) -> uint64_t { return (uint64_t)((double)l * inv_g + 0.5); };
+    auto cls_of = [&](uint64_t l) -> uint32_t { return (uint32_t)(q ? units_of(l) / q : units_of(l)); };
     for (uint32_t u = wave; u < V; u += nwaves) {
         const uint64_t b = row_ptr[u], e = row_ptr[u + 1];
         const uint32_t nch = (uint32_t)((e - b + 63) / 64);
@@ -355,10 +358,15 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t V, const uint64_t
             }
             if (!m) continue;  // uniform
             if ((m >> lane) & 1ull) {
-                const uint32_t v = col[k], cl = cls_of(lat[k]);
+                const uint32_t v = col[k];
+                const uint64_t wu = units_of(lat[k]);
+                const uint32_t cl = (uint32_t)(q ? wu / q : wu);
                 const uint32_t pos = atomicAdd(&ccnt[wv][cl - 1], 1u);
                 const float eb = WITH_LOSS ? 1.0f - loss[k] : 0.0f;  // (1f32 - other.packet_loss), mod.rs:328
-                ce_out[pos] = ((uint64_t)__float_as_uint(eb) << 32) | v;
+                // q > 0 (quantized classes): the weight's remainder w - c q rides
+                // along, (1 - e) in bits 34.. (a loss in [0, 1]: its bits are < 2^30)
+                ce_out[pos] = q ? ((uint64_t)__float_as_uint(eb) << 34) | ((wu - (uint64_t)cl * q) << vb) | v
+                                : ((uint64_t)__float_as_uint(eb) << 32) | v;
                 atomicAdd(&in_cnt[(uint64_t)v * cls + cl - 1], 1u);
             }
         }
@@ -372,8 +380,10 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t V, const uint64_t
 
 // In-rows of the level solve's class CSRs: every out-entry u -> v of class c
 // (walked per out-row, one wave a row) placed at its (v, c) slot's cursor
-// (in_off: the exclusive scan of lvl_out_kernel's counts) as (1-e) bits << 32 | u.
-__global__ __launch_bounds__(256) void lvl_in_kernel(uint32_t V, uint32_t cls, const uint32_t *__restrict__ off_out,
+// (in_off: the exclusive scan of lvl_out_kernel's counts), its head v (the
+// bits of vmask) replaced by the tail u.
+__global__ __launch_bounds__(256) void lvl_in_kernel(uint32_t V, uint32_t cls, uint64_t vmask,
+                                                     const uint32_t *__restrict__ off_out,
                                                      const uint64_t *__restrict__ ce_out,
                                                      const uint32_t *__restrict__ in_off, uint32_t *__restrict__ in_cur,
                                                      uint64_t *__restrict__ ce_in) {
@@ -387,10 +397,10 @@ __global__ __launch_bounds__(256) void lvl_in_kernel(uint32_t V, uint32_t cls, c
             uint32_t c = 1;  // the class of entry k: the last class whose start is <= k
             while (c + 1 < cls && ou[c] <= k) ++c;
             const uint64_t w = ce_out[k];
-            const uint32_t v = (uint32_t)w;
+            const uint32_t v = (uint32_t)(w & vmask);
             const uint64_t slot = (uint64_t)v * cls + c - 1;
             const uint32_t pos = in_off[slot] + atomicAdd(&in_cur[slot], 1u);
-            ce_in[pos] = (w & 0xffffffff00000000ull) | u;
+            ce_in[pos] = (w & ~vmask) | u;
         }
     }
 }
@@ -1693,6 +1703,333 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
     }
 }
 
+// ------------------------------------------------- quantized level solve
+// The level solve for latencies that are not small integers of g (Shadow
+// reads any unit down to ns, units.rs:377-388: C3ns has g = 1 ns and edges of
+// 1-301 ms).  Buckets of width q <= the shortest edge (units): bucket k holds
+// the vertices of L(s, v) in [k q, (k + 1) q), classes c = floor(w / q) >= 1.
+// A tight predecessor u of v has L(s, u) <= L(s, v) - q, so it lies in an
+// earlier bucket, and an edge of class c out of bucket j reaches bucket j + c
+// or j + c + 1.  Processing the pairs (j, c) with j + c = k at step k (push
+// along class-c out-edges of N_j, or pull into the unsettled set along class-c
+// in-edges from tails in bucket j, the smaller end as in level_solve_kernel)
+// therefore leaves every vertex whose key lands in bucket k final once step k
+// is done: its candidates come from steps k - 1 and k only.  A vertex's key is
+// one u64, L units << 32 | loss bits, min-ed by an LDS atomic: the
+// lexicographic (latency, loss) order of the reference's Dijkstra (mod.rs:
+// 305-340), over tails that are final when read.  Candidates past dcap (the
+// probe's bound B) are dropped, so every key stored is settled by the last
+// bucket, B / q.  Class entries: v in bits [0, vb), the weight's remainder
+// w - c q in [vb, vb + rb), (1f32 - e) bits in [34, 64).  LDS: 8 B a vertex;
+// the settled vertices in bucket order live in a per-workgroup global scratch
+// (mem_all + blockIdx.x * V, L2-resident).  stage_mode: 0 the table, 2 u32
+// units + f32 loss staging (row k at k * n), 3 8-byte records {units, loss
+// bits}.  probe != nullptr: probe[2 + k] = the largest L units over the in-use
+// columns of row k (~0 if one is unreached), the u64 at probe[0] += visits.
+template <int LPT, int UNR, uint32_t CLSN, int VW, bool NT>
+__global__ __launch_bounds__(LOSS_NT) void level_q_kernel(
+    uint32_t V, const uint32_t *__restrict__ nodes, uint32_t n, uint32_t row0, uint32_t row1,
+    const uint32_t *__restrict__ cls_out, const uint32_t *__restrict__ cls_in, const uint64_t *__restrict__ ce_out,
+    const uint64_t *__restrict__ ce_in, uint32_t kcap, uint32_t dcap, uint32_t qw, uint32_t rb, uint32_t vb, uint64_t g,
+    const uint64_t *__restrict__ sl_lat, const float *__restrict__ sl_loss, uint64_t *__restrict__ out_lat,
+    float *__restrict__ out_loss, unsigned long long *stats, const uint32_t *__restrict__ row_list,
+    void *__restrict__ stage, float *__restrict__ stage_loss, uint32_t stage_mode, uint32_t *__restrict__ probe,
+    unsigned long long *__restrict__ visit_cnt, uint16_t *__restrict__ mem_all) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ unsigned long long red_min[16], red_cnt[16], red_vis[16];
+    __shared__ uint32_t red_max[16];
+    constexpr uint32_t WCN = CLSN - 1;
+    __shared__ uint32_t plan_end[WCN + 1];
+    __shared__ uint32_t plan_push, plan_pull;
+    __shared__ uint32_t cur[2][2];
+    uint32_t *hist = reinterpret_cast<uint32_t *>(smem);  // hist[k]: end of bucket k in mem (k <= 31)
+    unsigned long long *key = reinterpret_cast<unsigned long long *>(smem + SOLVE_HIST);
+    uint16_t *mem = mem_all + (uint64_t)blockIdx.x * V;
+    const unsigned long long KINF = ~0ull;
+    const uint64_t vmask = (1ull << vb) - 1ull, rmask = (1ull << rb) - 1ull;
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    const int lane = tid & 63, wv = tid >> 6, nw = nt >> 6;
+    const uint32_t grp = tid / LPT, sub = tid % LPT, ngrp = nt / LPT;
+    const uint64_t below = (1ull << lane) - 1ull;
+    uint64_t mn = ~0ull;
+    unsigned long long unreach = 0, visits = 0;
+    const uint32_t nrows = row_list ? row1 : row1 - row0;
+    for (uint32_t k = blockIdx.x; k < nrows; k += gridDim.x) {
+        const uint32_t i = row_list ? row_list[k] : row0 + k;
+        const uint32_t s = nodes[i];
+        for (uint32_t v = tid; v < V; v += nt) key[v] = v == s ? 0ull : KINF;
+        if (tid == 0) {
+            hist[0] = 1;
+            mem[0] = (uint16_t)s;
+            cur[1][0] = cur[1][1] = 0;
+        }
+        __syncthreads();
+        uint32_t settled = 1;
+        for (uint32_t b = 1; b <= kcap && settled < V; ++b) {
+            const uint32_t U = V - settled, par = b & 1u;
+            if (tid == 0) {
+                uint32_t run = 0, pm = 0, pl = 0;
+                for (uint32_t c = 1; c <= WCN; ++c) {
+                    uint32_t items = 0;
+                    if (c <= b) {
+                        const uint32_t j = b - c, nj = hist[j] - (j ? hist[j - 1] : 0u);
+                        if (nj && nj <= U) {
+                            pm |= 1u << c;
+                            items = nj;
+                        } else if (nj) {
+                            pl = 1;
+                            items = U;
+                        }
+                    }
+                    run += items;
+                    plan_end[c] = run;
+                }
+                plan_push = pm;
+                plan_pull = pl;
+                cur[par][0] = cur[par][1] = 0;
+            }
+            __syncthreads();
+            const uint32_t T = plan_end[WCN], pm = plan_push;
+            const uint32_t lo = b * qw, hi = lo + qw;  // bucket b: latencies [lo, hi)
+            if (T && plan_pull) {
+                // the unsettled vertices (key at bucket >= b, or none) into mem[settled, V)
+                for (uint32_t base = 0; base < V; base += nt) {
+                    const uint32_t v = base + tid;
+                    const bool f = v < V && (uint32_t)(key[v] >> 32) >= lo;
+                    const uint64_t m = __ballot(f);
+                    if (!m) continue;  // uniform
+                    uint32_t o = 0;
+                    if (lane == 0) o = atomicAdd(&cur[par][0], (uint32_t)__popcll(m));
+                    o = __shfl(o, 0);
+                    if (f) mem[settled + o + (uint32_t)__popcll(m & below)] = (uint16_t)v;
+                }
+                __syncthreads();
+            }
+            auto item = [&](uint32_t t, uint32_t &c, uint32_t &x, uint32_t &e0, uint32_t &e1) {
+                c = 1;
+                while (t >= plan_end[c]) ++c;
+                const uint32_t m = t - (c > 1 ? plan_end[c - 1] : 0u), j = b - c;
+                const bool push = (pm >> c) & 1u;
+                x = mem[push ? (j ? hist[j - 1] : 0u) + m : settled + m];
+                const uint32_t *cl = push ? cls_out : cls_in;
+                e0 = cl[(uint64_t)x * CLSN + c - 1];
+                e1 = cl[(uint64_t)x * CLSN + c];
+            };
+            uint32_t nc_ = 1, nx = 0, ne0 = 0, ne1 = 0;
+            if (grp < T) item(grp, nc_, nx, ne0, ne1);
+            for (uint32_t t = grp; t < T; t += ngrp) {
+                const uint32_t c = nc_, x = nx, e0 = ne0, e1 = ne1, j = b - c;
+                if (t + ngrp < T) item(t + ngrp, nc_, nx, ne0, ne1);
+                const bool push = (pm >> c) & 1u;
+                const uint64_t *ce = push ? ce_out : ce_in;
+                const uint32_t cbase = c * qw, jlo = j * qw, jhi = jlo + qw;
+                // push: x in bucket j (final), its class-c out-edges x -> v;
+                // pull: x unsettled, its class-c in-edges u -> x from u in bucket j
+                const unsigned long long kx = push ? key[x] : 0ull;
+                const uint32_t dx = (uint32_t)(kx >> 32);
+                const float onem = 1.0f - __uint_as_float((uint32_t)kx);
+                unsigned long long best = KINF;
+                constexpr int NE = UNR * VW;
+                for (uint32_t e = VW == 2 ? e0 & ~1u : e0; e < e1; e += UNR * LPT * VW) {
+                    uint64_t wd[NE];
+                    uint32_t ei[NE];
+#pragma unroll
+                    for (int q = 0; q < UNR; ++q) {
+                        const uint32_t at = e + (sub + q * LPT) * VW;  // padded past the end
+                        if (VW == 2) {
+                            const uint4 r2 = *reinterpret_cast<const uint4 *>(ce + at);
+                            wd[2 * q] = ((uint64_t)r2.y << 32) | r2.x;
+                            wd[2 * q + 1] = ((uint64_t)r2.w << 32) | r2.z;
+                            ei[2 * q] = at;
+                            ei[2 * q + 1] = at + 1;
+                        } else {
+                            wd[q] = ce[at];
+                            ei[q] = at;
+                        }
+                    }
+                    uint32_t o[NE];
+                    bool ok[NE];
+#pragma unroll
+                    for (int q = 0; q < NE; ++q) {
+                        ok[q] = ei[q] < e1 && (VW == 1 || ei[q] >= e0);
+                        o[q] = ok[q] ? (uint32_t)(wd[q] & vmask) : 0u;
+                    }
+                    unsigned long long ko[NE];
+#pragma unroll
+                    for (int q = 0; q < NE; ++q) ko[q] = key[o[q]];
+#pragma unroll
+                    for (int q = 0; q < NE; ++q) {
+                        visits += ok[q];
+                        const uint32_t w = cbase + (uint32_t)((wd[q] >> vb) & rmask);
+                        const float r = __uint_as_float((uint32_t)(wd[q] >> 34));
+                        if (push) {
+                            const uint32_t d = dx + w;
+                            const unsigned long long ck =
+                                ((unsigned long long)d << 32) | __float_as_uint(1.0f - __fmul_rn(onem, r));
+                            if (ok[q] && d <= dcap && ck < ko[q]) atomicMin(&key[o[q]], ck);
+                        } else {
+                            const uint32_t du = (uint32_t)(ko[q] >> 32), d = du + w;
+                            // tail in bucket j (an unreached tail's ~0 is past every bucket)
+                            if (ok[q] && du >= jlo && du < jhi && d <= dcap) {
+                                const float lu = __uint_as_float((uint32_t)ko[q]);
+                                const unsigned long long ck =
+                                    ((unsigned long long)d << 32) | __float_as_uint(1.0f - __fmul_rn(1.0f - lu, r));
+                                best = ck < best ? ck : best;
+                            }
+                        }
+                    }
+                }
+                if (!push && best != KINF) atomicMin(&key[x], best);
+            }
+            __syncthreads();  // every key of bucket b final
+            // N_b (the keys now in bucket b) -> mem[settled, ...)
+            for (uint32_t base = 0; base < V; base += nt) {
+                const uint32_t v = base + tid;
+                const unsigned long long kv = v < V ? key[v] : KINF;
+                const uint32_t dv = (uint32_t)(kv >> 32);
+                const bool f = kv != KINF && dv >= lo && dv < hi;
+                const uint64_t m = __ballot(f);
+                if (!m) continue;  // uniform
+                uint32_t o = 0;
+                if (lane == 0) o = atomicAdd(&cur[par][1], (uint32_t)__popcll(m));
+                o = __shfl(o, 0);
+                if (f) mem[settled + o + (uint32_t)__popcll(m & below)] = (uint16_t)v;
+            }
+            __syncthreads();
+            const uint32_t got = cur[par][1];
+            // no tail in buckets b - WCN .. b and bucket b empty: every later
+            // bucket is empty (uniform)
+            if (!T && !got) break;
+            settled += got;
+            if (tid == 0) hist[b] = settled;
+        }
+        __syncthreads();  // keys final for the output
+        if (probe) {
+            uint32_t rmax = 0;
+            for (uint32_t j0 = tid; j0 < n; j0 += nt) {
+                const unsigned long long kv = key[nodes[j0]];
+                const uint32_t l = kv == KINF ? ~0u : (uint32_t)(kv >> 32);
+                rmax = l > rmax ? l : rmax;
+            }
+            for (int off = 32; off > 0; off >>= 1) {
+                const uint32_t o = __shfl_xor(rmax, off);
+                rmax = o > rmax ? o : rmax;
+            }
+            if (lane == 0) red_max[wv] = rmax;
+            __syncthreads();
+            if (tid == 0) {
+                uint32_t m = 0;
+                for (int q = 0; q < nw; ++q) m = red_max[q] > m ? red_max[q] : m;
+                probe[2 + k] = m;
+            }
+            __syncthreads();
+            continue;
+        }
+        uint64_t *ol = out_lat + (uint64_t)i * n;
+        float *op = out_loss + (uint64_t)i * n;
+        uint32_t *o32 = stage_mode == 2 ? reinterpret_cast<uint32_t *>(stage) + (uint64_t)k * n : nullptr;
+        float *o32p = stage_mode == 2 ? stage_loss + (uint64_t)k * n : nullptr;
+        uint2 *orec = stage_mode == 3 ? reinterpret_cast<uint2 *>(stage) + (uint64_t)k * n : nullptr;
+        for (uint32_t j0 = tid; j0 < n; j0 += 4 * nt) {
+            uint32_t vv[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) vv[q] = j0 + q * nt < n ? nodes[j0 + q * nt] : 0u;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t j = j0 + q * nt;
+                if (j >= n) break;
+                uint64_t latv, lu;
+                float lossv;
+                if (j == i) {
+                    latv = sl_lat[j];
+                    lossv = sl_loss[j];
+                    lu = latv == ~0ull ? ~0ull : latv / g;
+                } else {
+                    const unsigned long long kv = key[vv[q]];
+                    if (kv == KINF) {
+                        ++unreach;
+                        latv = lu = ~0ull;
+                        lossv = 1.0f;
+                    } else {
+                        lu = kv >> 32;
+                        latv = lu * g;
+                        lossv = __uint_as_float((uint32_t)kv);
+                    }
+                }
+                // a staged self-loop past the u32 field saturates; the
+                // consumers rewrite the diagonal from the host's self-loops
+                const uint32_t l32 = lu >= 0xffffffffull ? ~0u : (uint32_t)lu;
+                if (orec) {
+                    __builtin_nontemporal_store(((uint64_t)__float_as_uint(lossv) << 32) | l32,
+                                                reinterpret_cast<uint64_t *>(orec) + j);
+                } else if (o32) {
+                    __builtin_nontemporal_store(l32, o32 + j);
+                    __builtin_nontemporal_store(lossv, o32p + j);
+                } else if (NT) {
+                    __builtin_nontemporal_store(latv, ol + j);
+                    __builtin_nontemporal_store(lossv, op + j);
+                } else {
+                    ol[j] = latv;
+                    op[j] = lossv;
+                }
+                mn = latv < mn ? latv : mn;
+            }
+        }
+        __syncthreads();  // the next row rewrites the LDS keys and the scratch
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(mn, off);
+        mn = o < mn ? o : mn;
+        unreach += __shfl_xor(unreach, off);
+        visits += __shfl_xor(visits, off);
+    }
+    if (lane == 0) {
+        red_min[wv] = mn;
+        red_cnt[wv] = unreach;
+        red_vis[wv] = visits;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long m = red_min[0], c = red_cnt[0], vz = red_vis[0];
+        for (int q = 1; q < nw; ++q) {
+            m = red_min[q] < m ? red_min[q] : m;
+            c += red_cnt[q];
+            vz += red_vis[q];
+        }
+        if (probe) {
+            if (vz) atomicAdd(reinterpret_cast<unsigned long long *>(probe), vz);
+        } else {
+            atomicMin(&stats[0], m);
+            if (c) atomicAdd(&stats[1], c);
+            if (visit_cnt && vz) atomicAdd(visit_cnt, vz);
+        }
+    }
+}
+
+// The shortest non-self-loop edge latency (ns) min-ed into *out: one wave per
+// adjacency row; the column is read only where the latency would lower the
+// lane's minimum (the quantized level solve's bucket width)
+__global__ __launch_bounds__(256) void edge_min_kernel(uint32_t V, const uint64_t *__restrict__ row_ptr,
+                                                       const uint32_t *__restrict__ col,
+                                                       const uint64_t *__restrict__ lat, unsigned long long *out) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    uint64_t m = ~0ull;
+    for (uint32_t u = wave; u < V; u += nwaves) {
+        const uint64_t b = row_ptr[u], e = row_ptr[u + 1];
+        for (uint64_t k = b + lane; k < e; k += 64) {
+            const uint64_t l = lat[k];
+            if (l < m && col[k] != u) m = l;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(m, off);
+        m = o < m ? o : m;
+    }
+    if (lane == 0 && m != ~0ull) atomicMin(out, (unsigned long long)m);
+}
+
 __global__ void loss_stats_init_kernel(unsigned long long *stats, unsigned long long *maxw) {
     stats[0] = ~0ull;
     stats[1] = 0ull;
@@ -2414,7 +2751,17 @@ LevelCtx level_ctx(srt_plan *p) {
     c.out_lat = p->d_out_lat;
     c.out_loss = p->d_out_loss;
     c.visits = p->d_lvisit;
+    c.q = p->lvl_q;
+    c.rb = p->lvl_rb;
+    c.vb = p->lvl_vb;
+    c.lmem = p->d_lmem;
     return c;
+}
+
+uint32_t level_vbits(uint32_t V) {
+    uint32_t vb = 1;
+    while ((1u << vb) < V) ++vb;
+    return vb;
 }
 
 namespace {
@@ -2429,7 +2776,8 @@ namespace {
 srt_status level_csr(srt_plan *p, uint64_t wmax, bool with_loss, srt_err *err) {
     hipStream_t M = p->stream;
     const uint32_t V = p->V;
-    const uint32_t cls = wmax < 16 ? 16 : 32;
+    const uint32_t q = p->lvl_q, vb = q ? p->lvl_vb : 32u;
+    const uint32_t cls = (q ? wmax / q : wmax) < 16 ? 16 : 32;
     const uint64_t vc1 = (uint64_t)V * cls + 1;
     srt_status st;
     uint64_t c1 = p->tcls_cap, c2 = p->tcls_cap, cap_cur = p->d_tcursor ? 1 : 0, cap_mw = p->d_tmaxw ? 1 : 0;
@@ -2452,12 +2800,12 @@ srt_status level_csr(srt_plan *p, uint64_t wmax, bool with_loss, srt_err *err) {
         (void)hipMemsetAsync(p->d_tmaxw, 0, sizeof(unsigned long long), M);
         if (with_loss)
             hipLaunchKernelGGL(lvl_out_kernel<true>, dim3(blocks), dim3(256), 0, M, V, p->d_row_ptr, p->d_col,
-                               p->d_lat, p->d_loss, p->kp.g, inv_g, wns, cls, p->d_tcls, p->d_tccnt, p->d_tpk,
-                               p->lvl_cap, p->d_tcursor, (unsigned long long *)p->d_tmaxw);
+                               p->d_lat, p->d_loss, p->kp.g, inv_g, wns, cls, q, vb, p->d_tcls, p->d_tccnt,
+                               p->d_tpk, p->lvl_cap, p->d_tcursor, (unsigned long long *)p->d_tmaxw);
         else
             hipLaunchKernelGGL(lvl_out_kernel<false>, dim3(blocks), dim3(256), 0, M, V, p->d_row_ptr, p->d_col,
-                               p->d_lat, (const float *)nullptr, p->kp.g, inv_g, wns, cls, p->d_tcls, p->d_tccnt,
-                               p->d_tpk, p->lvl_cap, p->d_tcursor, (unsigned long long *)p->d_tmaxw);
+                               p->d_lat, (const float *)nullptr, p->kp.g, inv_g, wns, cls, q, vb, p->d_tcls,
+                               p->d_tccnt, p->d_tpk, p->lvl_cap, p->d_tcursor, (unsigned long long *)p->d_tmaxw);
     };
     out_pass();
     if (!p->lvl_cap) {
@@ -2491,8 +2839,9 @@ srt_status level_csr(srt_plan *p, uint64_t wmax, bool with_loss, srt_err *err) {
     e = rocprim::exclusive_scan(p->d_tscan_tmp, have, p->d_tccnt, p->d_tcls + vc1, 0u, (size_t)vc1,
                                 rocprim::plus<uint32_t>(), M);
     if (e != hipSuccess) return fail(err, e, "class scan");
-    hipLaunchKernelGGL(lvl_in_kernel, dim3(blocks), dim3(256), 0, M, V, cls, p->d_tcls, p->d_tpk, p->d_tcls + vc1,
-                       p->d_tccnt + vc1, p->d_tpk2);
+    const uint64_t vmask = q ? (1ull << vb) - 1ull : 0xffffffffull;
+    hipLaunchKernelGGL(lvl_in_kernel, dim3(blocks), dim3(256), 0, M, V, cls, vmask, p->d_tcls, p->d_tpk,
+                       p->d_tcls + vc1, p->d_tccnt + vc1, p->d_tpk2);
     p->t_cls = cls;
     p->t_q = 1;
     p->t_level = true;
@@ -2500,23 +2849,36 @@ srt_status level_csr(srt_plan *p, uint64_t wmax, bool with_loss, srt_err *err) {
     return SRT_OK;
 }
 
-// level_solve_kernel over rows [r0, r1) (or the row list) of the context c
-// (probe: no table, reverse = in- and out-CSRs swapped: distances TO the
-// row's node); staging: u16 latency units + f32 loss, row k of the job at k * n
+// Workgroups of a level solve launch over `rows` rows (one row per
+// workgroup at a time; the LDS row decides how many fit a CU)
+uint32_t level_grid(int device, uint32_t V, bool quant, uint32_t rows, uint32_t *nt_out) {
+    const uint32_t nt = V >= 2048 ? LOSS_NT : 256;
+    const size_t lds = quant ? SOLVE_HIST + (size_t)V * 8
+                             : SOLVE_HIST + (((size_t)V * 2 + 15) & ~(size_t)15) + (size_t)V * 4 +
+                                   (((size_t)V * 2 + 15) & ~(size_t)15);
+    const int per_cu = std::max(1, std::min(2048 / (int)nt, (int)std::max<size_t>(1, (160 * 1024) / (lds + 2048))));
+    if (nt_out) *nt_out = nt;
+    return std::max<uint32_t>(1, std::min<uint32_t>(rows, (uint32_t)(cu_count(device) * per_cu)));
+}
+
+// level_solve_kernel (or level_q_kernel, c.q > 0) over rows [r0, r1) (or the
+// row list) of the context c (probe: no table, reverse = in- and out-CSRs
+// swapped: distances TO the row's node); lcap = the bound B in units.
+// stage_mode 0: the table; 1: u16 latency units + f32 loss staging, row k of
+// the job at k * n; 2: u32 units + loss; 3: 8-byte records (quantized only)
 void launch_solve_ctx(const LevelCtx &c, unsigned long long *d_stats, const uint32_t *list, uint32_t r0, uint32_t r1,
-                      uint32_t lcap, bool reverse, uint32_t *probe, void *out16, float *out_loss_stage) {
+                      uint32_t lcap, bool reverse, uint32_t *probe, void *stage, float *stage_loss,
+                      uint32_t stage_mode) {
     const uint32_t V = c.V, rows = list ? r1 : r1 - r0;
     if (!rows) return;
-    const uint32_t nt = V >= 2048 ? LOSS_NT : 256;
-    const size_t lds = SOLVE_HIST + (((size_t)V * 2 + 15) & ~(size_t)15) + (size_t)V * 4 +
-                       (((size_t)V * 2 + 15) & ~(size_t)15);
-    const int per_cu = std::max(1, std::min(2048 / (int)nt, (int)std::max<size_t>(1, (160 * 1024) / (lds + 2048))));
-    const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>(rows, (uint32_t)(cu_count(c.device) * per_cu)));
+    const bool quant = c.q != 0;
+    uint32_t nt = 0;
+    const uint32_t grid = level_grid(c.device, V, quant, rows, &nt);
+    const size_t lds = quant ? SOLVE_HIST + (size_t)V * 8
+                             : SOLVE_HIST + (((size_t)V * 2 + 15) & ~(size_t)15) + (size_t)V * 4 +
+                                   (((size_t)V * 2 + 15) & ~(size_t)15);
     // table rows by non-temporal stores (knob SRT_LVL_NT=0/1: A/B measurement)
     static const bool nts = !(std::getenv("SRT_LVL_NT") && std::atoi(std::getenv("SRT_LVL_NT")) == 0);
-    auto kern = c.t_cls == 16 ? (nts ? level_solve_kernel<4, 4, 16, 2, true> : level_solve_kernel<4, 4, 16, 2, false>)
-                              : (nts ? level_solve_kernel<4, 2, 32, 2, true> : level_solve_kernel<4, 2, 32, 2, false>);
-    (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(LDS_BUDGET - 4096));
     const uint64_t vc1 = (uint64_t)V * c.t_cls + 1;
     const uint32_t *co = c.tcls, *ci = c.tcls + vc1;
     const uint64_t *eo = c.ce_out, *ei = c.ce_in;
@@ -2524,17 +2886,42 @@ void launch_solve_ctx(const LevelCtx &c, unsigned long long *d_stats, const uint
         std::swap(co, ci);
         std::swap(eo, ei);
     }
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, c.stream, V, c.nodes, c.n, list ? 0u : r0, list ? r1 : r1, co,
-                       ci, eo, ei, lcap, c.g, c.sl_lat, c.sl_loss, c.out_lat, c.out_loss, d_stats, list, out16,
-                       out_loss_stage, out16 != nullptr, probe, c.visits);
+    if (quant) {
+        auto kern = c.t_cls == 16 ? (nts ? level_q_kernel<4, 4, 16, 2, true> : level_q_kernel<4, 4, 16, 2, false>)
+                                  : (nts ? level_q_kernel<4, 2, 32, 2, true> : level_q_kernel<4, 2, 32, 2, false>);
+        (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)(LDS_BUDGET - 4096));
+        const uint32_t kcap = std::min<uint32_t>(lcap / c.q, WC);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, c.stream, V, c.nodes, c.n, list ? 0u : r0, r1, co, ci,
+                           eo, ei, kcap, lcap, c.q, c.rb, c.vb, c.g, c.sl_lat, c.sl_loss, c.out_lat, c.out_loss, d_stats,
+                           list, stage, stage_loss, stage_mode, probe, c.visits, c.lmem);
+        return;
+    }
+    auto kern = c.t_cls == 16 ? (nts ? level_solve_kernel<4, 4, 16, 2, true> : level_solve_kernel<4, 4, 16, 2, false>)
+                              : (nts ? level_solve_kernel<4, 2, 32, 2, true> : level_solve_kernel<4, 2, 32, 2, false>);
+    (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(LDS_BUDGET - 4096));
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, c.stream, V, c.nodes, c.n, list ? 0u : r0, r1, co, ci, eo, ei,
+                       lcap, c.g, c.sl_lat, c.sl_loss, c.out_lat, c.out_loss, d_stats, list,
+                       stage_mode ? stage : nullptr, stage_mode ? stage_loss : nullptr, stage_mode == 1, probe,
+                       c.visits);
+}
+
+// the per-workgroup scratch of the quantized solve (p->d_lmem): every
+// workgroup a launch may have, V u16 each
+srt_status level_scratch(srt_plan *p, srt_err *err) {
+    if (!p->lvl_q) return SRT_OK;
+    const uint64_t need = (uint64_t)level_grid(p->device, p->V, true, ~0u, nullptr) * p->V;
+    return grow(&p->d_lmem, &p->lmem_cap, need, err, "hipMalloc(level scratch)");
 }
 
 srt_status launch_solve(srt_plan *p, unsigned long long *d_stats, const RowJob &job, uint32_t lcap, bool reverse,
-                        uint32_t *probe) {
+                        uint32_t *probe, srt_err *err) {
+    srt_status st = level_scratch(p, err);
+    if (st != SRT_OK) return st;
     const uint32_t r0 = job.list ? 0u : job.range ? job.r0 : p->row0;
     const uint32_t r1 = job.list ? job.count : job.range ? job.r1 : p->row1;
-    launch_solve_ctx(level_ctx(p), d_stats, job.list, r0, r1, lcap, reverse, probe,
-                     job.out32_loss && p->stage16 ? job.out32 : nullptr, job.out32_loss);
+    launch_solve_ctx(level_ctx(p), d_stats, job.list, r0, r1, lcap, reverse, probe, job.out32_loss ? job.out32 : nullptr,
+                     job.out32_loss, job.out32_loss ? (p->stage16 ? 1u : 2u) : 0u);
     return SRT_OK;
 }
 
@@ -2546,11 +2933,14 @@ srt_status launch_solve(srt_plan *p, unsigned long long *d_stats, const RowJob &
 // in-ecc(s) + out-ecc(s) for each s (pruned distances bound the real ones from
 // above), so *bound = the smallest such sum; ~0 when every s misses an in-use
 // node within wmax levels one way or the other.  *visits: the edges a
-// forward probe row walked on average (the AUTO price).
+// forward probe row walked on average (the AUTO price).  p->lvl_q > 0: the
+// quantized solve's buckets of q units; the bound must keep every class and
+// bucket <= 31 (B < 32 q).
 srt_status level_probe(srt_plan *p, uint64_t wmax, uint64_t *bound, uint64_t *visits, srt_err *err) {
     *bound = ~0ull;
     *visits = 0;
     if (!p->n) return SRT_OK;
+    p->lvl_cap = 0;  // a new bound: count and size the entry arrays again
     srt_status st = level_csr(p, wmax, false, err);
     if (st != SRT_OK) return st;
     const uint32_t K = std::min<uint32_t>(8, p->n);
@@ -2565,10 +2955,17 @@ srt_status level_probe(srt_plan *p, uint64_t wmax, uint64_t *bound, uint64_t *vi
     RowJob job;
     job.list = d_pr + 32;
     job.count = K;
-    const uint32_t cap = (uint32_t)std::min<uint64_t>(wmax, WC);
+    const uint64_t LQ = (uint64_t)(WC + 1) * (p->lvl_q ? p->lvl_q : 1) - 1;  // the largest bound the solve takes
+    // distances up to LQ (not only up to wmax: a path of short edges may be
+    // longer than the longest edge)
+    const uint32_t cap = (uint32_t)LQ;
     if (e == hipSuccess) {
-        launch_solve(p, nullptr, job, cap, false, d_pr);
-        launch_solve(p, nullptr, job, cap, true, d_pr + 16);
+        if ((st = launch_solve(p, nullptr, job, cap, false, d_pr, err)) != SRT_OK ||
+            (st = launch_solve(p, nullptr, job, cap, true, d_pr + 16, err)) != SRT_OK) {
+            (void)hipStreamSynchronize(p->stream);
+            (void)hipFree(d_pr);
+            return st;
+        }
         e = hipMemcpyAsync(h, d_pr, sizeof h, hipMemcpyDeviceToHost, p->stream);
     }
     if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
@@ -2578,11 +2975,12 @@ srt_status level_probe(srt_plan *p, uint64_t wmax, uint64_t *bound, uint64_t *vi
     std::memcpy(&vis, h, 8);
     *visits = vis / K;
     for (uint32_t k = 0; k < K; ++k)
-        if (h[2 + k] <= cap && h[18 + k] <= cap && h[2 + k] + h[18 + k] <= WC)  // classes <= WC
+        if (h[2 + k] <= cap && h[18 + k] <= cap && (uint64_t)h[2 + k] + h[18 + k] <= LQ)  // classes <= WC
             *bound = std::min<uint64_t>(*bound, (uint64_t)h[2 + k] + h[18 + k]);
     if (std::getenv("SRT_TRACE"))
-        std::fprintf(stderr, "[srt] level probe: %llu edges <= %llu units, %u rows, bound %lld, %llu visits a row\n",
-                     (unsigned long long)p->t_edges, (unsigned long long)wmax, K,
+        std::fprintf(stderr,
+                     "[srt] level probe: %llu edges <= %llu units, q %u, %u rows, bound %lld, %llu visits a row\n",
+                     (unsigned long long)p->t_edges, (unsigned long long)wmax, p->lvl_q, K,
                      *bound == ~0ull ? -1ll : (long long)*bound, (unsigned long long)*visits);
     return SRT_OK;
 }
@@ -2601,7 +2999,7 @@ namespace {
 srt_status level_sharded(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     const uint32_t W = (uint32_t)p->comm->nranks, r = (uint32_t)p->comm->rank;
     const size_t chunk = (size_t)p->lrow_max * p->n;
-    p->stage16 = true;
+    p->stage16 = p->lvl_q == 0;  // quantized: u32 units
     p->stage_loss_only = false;
     if (!p->d_slat) {
         void *a = nullptr, *b = nullptr;
@@ -2615,7 +3013,7 @@ srt_status level_sharded(srt_plan *p, unsigned long long *d_stats, srt_err *err)
         p->d_sloss = (float *)b;
     }
     const uint32_t q = p->tail_q, cr = p->tail_cr, lcap = (uint32_t)p->kp.lmax;
-    const size_t cbytes = (size_t)cr * p->n * 4, lbytes = (size_t)cr * p->n * 2;
+    const size_t cbytes = (size_t)cr * p->n * 4, lbytes = (size_t)cr * p->n * (p->stage16 ? 2 : 4);
     hipStream_t M = p->stream, C = p->comm_stream;
     while (p->ev.size() < 2 * (size_t)q) {
         hipEvent_t e;
@@ -2629,17 +3027,18 @@ srt_status level_sharded(srt_plan *p, unsigned long long *d_stats, srt_err *err)
         RowJob job;
         job.list = p->d_lrows + slot;
         job.count = p->lrow_cnt[r] > c * cr ? std::min(cr, p->lrow_cnt[r] - c * cr) : 0u;
-        job.out32 = reinterpret_cast<uint8_t *>(p->d_slat) + slot * p->n * 2;
+        job.out32 = reinterpret_cast<uint8_t *>(p->d_slat) + slot * p->n * (p->stage16 ? 2 : 4);
         job.out32_loss = p->d_sloss + slot * p->n;
         (void)hipEventRecord(p->ev[2 * c], M);
-        if ((st = launch_solve(p, d_stats, job, lcap, false, nullptr)) != SRT_OK) return st;
+        if ((st = launch_solve(p, d_stats, job, lcap, false, nullptr, err)) != SRT_OK) return st;
         (void)hipEventRecord(p->ev[2 * c + 1], M);
         p->p3_launches++;
         p->p3_work += (double)job.count * p->n;
         (void)hipEventRecord(p->ev_tail[c], M);
         (void)hipStreamWaitEvent(C, p->ev_tail[c], 0);
         const size_t base = (size_t)c * W * cr * p->n;
-        if ((st = comm_allgather_inplace(p->comm, reinterpret_cast<uint8_t *>(p->d_slat) + base * 2, lbytes, C,
+        if ((st = comm_allgather_inplace(p->comm,
+                                         reinterpret_cast<uint8_t *>(p->d_slat) + base * (p->stage16 ? 2 : 4), lbytes, C,
                                          err)) != SRT_OK ||
             (st = comm_allgather_inplace(p->comm, p->d_sloss + base, cbytes, C, err)) != SRT_OK)
             return st;
@@ -2653,9 +3052,29 @@ srt_status level_sharded(srt_plan *p, unsigned long long *d_stats, srt_err *err)
 
 srt_status level_prepare(srt_plan *p, srt_err *err) { return level_csr(p, p->kp.lmax, true, err); }
 
-void level_solve_stage(const LevelCtx &c, uint32_t r0, uint32_t r1, uint32_t lmax, uint16_t *stage_lat,
-                       float *stage_loss, unsigned long long *d_stats) {
-    launch_solve_ctx(c, d_stats, nullptr, r0, r1, lmax, false, nullptr, stage_lat, stage_loss);
+void level_solve_stage(const LevelCtx &c, uint32_t r0, uint32_t r1, uint32_t lmax, void *stage_lat,
+                       float *stage_loss, uint32_t stage_mode, unsigned long long *d_stats) {
+    launch_solve_ctx(c, d_stats, nullptr, r0, r1, lmax, false, nullptr, stage_lat, stage_loss, stage_mode);
+}
+
+size_t level_scratch_bytes(int device, uint32_t V, bool quant) {
+    return quant ? (size_t)level_grid(device, V, true, ~0u, nullptr) * V * 2 : 0;
+}
+
+// The shortest non-self-loop edge of the plan's graph, ns (~0: none)
+srt_status level_min_edge(srt_plan *p, uint64_t *min_ns, srt_err *err) {
+    *min_ns = ~0ull;
+    unsigned long long *d = nullptr;
+    hipError_t e = hipMalloc(&d, sizeof *d);
+    if (e != hipSuccess) return fail(err, e, "hipMalloc(edge min)");
+    (void)hipMemsetAsync(d, 0xff, sizeof *d, p->stream);
+    const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(8192, (p->V + 3) / 4));
+    hipLaunchKernelGGL(edge_min_kernel, dim3(blocks), dim3(256), 0, p->stream, p->V, p->d_row_ptr, p->d_col, p->d_lat,
+                       d);
+    e = hipMemcpyAsync(min_ns, d, sizeof *d, hipMemcpyDeviceToHost, p->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
+    (void)hipFree(d);
+    return e == hipSuccess ? SRT_OK : fail(err, e, "edge min");
 }
 
 void level_stats_init(unsigned long long *d_stats, hipStream_t s) {
@@ -2719,7 +3138,7 @@ srt_status level_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
         job.r0 = p->row0 + c * cr;
         job.r1 = std::min(p->row1, job.r0 + cr);
         (void)hipEventRecord(p->ev[2 * c], p->stream);
-        if ((st = launch_solve(p, d_stats, job, lcap, false, nullptr)) != SRT_OK) return st;
+        if ((st = launch_solve(p, d_stats, job, lcap, false, nullptr, err)) != SRT_OK) return st;
         (void)hipEventRecord(p->ev[2 * c + 1], p->stream);
         p->p3_launches++;
         p->p3_work += (double)(job.r1 - job.r0) * p->n;

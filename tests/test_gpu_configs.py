@@ -105,8 +105,10 @@ def test_c3_16k_rows_vs_oracle_and_symmetry():
 
 
 def test_c3ns_16k_u32_keys_rows_vs_oracle():
-    """C3 with ns latencies (bench --config c3ns): g = 1 ns, so the closure
-    runs u32 keys and the loss pass the quantized level fold; 16 seeded rows bit-exact
+    """C3 with ns latencies (bench --config c3ns): g = 1 ns, so no bound fits
+    31 units and AUTO takes the quantized level solve (buckets as wide as the
+    shortest edge, ~1 ms); its device table equals the Floyd-Warshall family's
+    (u32 keys, quantized level fold) bit for bit, 16 seeded rows bit-exact
     against the oracle, symmetry over the device table."""
     import torch
 
@@ -117,12 +119,20 @@ def test_c3ns_16k_u32_keys_rows_vs_oracle():
     nodes = np.arange(n, dtype=np.uint32)
     plan = RoutingPlan(g, nodes).run()
     d = plan.describe()
-    assert d.startswith("fw:u32key ") and " g=1 " in d, d
-    # tight weights in ns units (1.0-4.6 ms): the level fold on quantized levels
-    assert plan.timing()["loss_fold"] == 1
+    assert d.startswith("level:u32 ") and " g=1 " in d and " q=" in d, d
     plan.fetch(table=False)
     L, P = _device_table(plan)
     assert torch.equal(L, L.t())
+    fw = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_FW).run()
+    try:
+        assert fw.describe().startswith("fw:u32key ") and fw.timing()["loss_fold"] == 1
+        fw.fetch(table=False)
+        assert fw.min_latency_ns == plan.min_latency_ns
+        L2, P2 = _device_table(fw)
+        assert torch.equal(L, L2) and torch.equal(P, P2), "quantized level solve != Floyd-Warshall tables"
+        del L2, P2
+    finally:
+        fw.close()
     rows = np.random.default_rng(33).choice(n, 16, replace=False)
     order = np.concatenate([rows, np.setdiff1d(nodes, rows)]).astype(np.uint32)
     og = O.Graph(False, nodes, *edges)

@@ -181,3 +181,119 @@ def test_level_sharded_rows(world, directed):
     for d in descs:
         assert d.startswith("level:") and f"ranks={world}" in d, d
     _check(t, og, nodes)
+
+
+def _random_ns(n, seed, directed, p_edge=0.08, lat_ms=(1, 9), subset=None):
+    """A random graph in ns: integer-ms latencies plus a seeded sub-ms offset
+    (g = 1 ns, like bench --config c3ns), so no bound fits 31 units and the
+    quantized solve (buckets of 2^19 ns) takes it."""
+    src, dst, l, loss = synth.random_graph(n, seed, p_edge=p_edge, directed=directed, lat_range_ns=lat_ms,
+                                           loss_max=0.05)
+    off = np.random.default_rng(seed + 7).integers(0, synth.MS, size=len(l), dtype=np.uint64)
+    l = np.asarray(l, np.uint64) * np.uint64(synth.MS) + off
+    g = NetworkGraph.from_edges(n, src, dst, l, loss, directed=directed)
+    nodes = np.random.default_rng(seed).permutation(n).astype(np.uint32)
+    if subset:
+        nodes = nodes[:subset]
+    return g, nodes, O.Graph(directed, np.arange(n), src, dst, l, loss)
+
+
+@pytest.mark.parametrize("n,seed,directed,p_edge,lat_ms,subset", [
+    (60, 1, False, 0.3, (1, 9), None), (400, 2, False, 0.08, (1, 9), None), (400, 3, True, 0.08, (1, 9), 250),
+    (1200, 4, False, 0.3, (1, 40), None), (900, 5, True, 0.05, (2, 6), None)])
+def test_level_quantized_matches_oracle(n, seed, directed, p_edge, lat_ms, subset):
+    """ns latencies: the quantized level solve (level:u32, buckets as wide as the
+    shortest edge) is bit-exact against the oracle."""
+    g, nodes, og = _random_ns(n, seed, directed, p_edge, lat_ms, subset)
+    p = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_LEVEL, device=0).run()
+    try:
+        d = p.describe()
+        assert d.startswith("level:u32 ") and " g=1 " in d and " q=" in d, d
+        _check(p.fetch(), og, nodes)
+    finally:
+        p.close()
+
+
+def test_level_quantized_integer_units():
+    """Integer-ms latencies 2-9 ms over a ring-heavy graph whose paths exceed
+    31 units: the integer probe fails, the quantized one (buckets of 2 ms, the
+    shortest edge) bounds it; AUTO == FW == oracle."""
+    n = 300
+    src, dst, lat, loss = synth.random_graph(n, 8, p_edge=0.01, directed=False, lat_range_ns=(2, 9), loss_max=0.05)
+    lat = np.asarray(lat, np.uint64) * np.uint64(synth.MS)
+    g = NetworkGraph.from_edges(n, src, dst, lat, loss)
+    nodes = np.arange(n, dtype=np.uint32)
+    og = O.Graph(False, np.arange(n), src, dst, lat, loss)
+    elat, _ = O.compute_shortest_paths(og, nodes)
+    assert elat.max() // synth.MS > 31, "the graph must defeat the integer probe"
+    p = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_LEVEL, device=0).run()
+    try:
+        d = p.describe()
+        assert d.startswith("level:u32 ") and " q=2 " in d, d
+        _check(p.fetch(), og, nodes)
+    finally:
+        p.close()
+
+
+def test_level_quantized_equals_fw_dense():
+    """A 3,000-node complete ns graph (C3ns's shape at 3k): the quantized
+    level tables equal the Floyd-Warshall family's (u32 keys) bit for bit on
+    the device, and AUTO takes the level solve."""
+    import torch
+
+    n = 3000
+    edges = synth.complete_graph_ns(n, 5)
+    g = NetworkGraph.from_edges(n, *edges)
+    nodes = np.arange(n, dtype=np.uint32)
+    a = RoutingPlan(g, nodes, device=0).run()
+    b = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_FW, device=0).run()
+    try:
+        assert a.describe().startswith("level:u32 "), a.describe()
+        assert b.describe().startswith("fw:u32key "), b.describe()
+        a.fetch(table=False)
+        b.fetch(table=False)
+        assert a.min_latency_ns == b.min_latency_ns
+        la, pa, _ = a.table_ptrs()
+        lb, pb, _ = b.table_ptrs()
+        dev = torch.device("cuda", 0)
+        t = lambda ptr, nb: torch.as_tensor(sdist._CudaBuf(ptr, nb), device=dev)
+        assert torch.equal(t(la, n * n * 8), t(lb, n * n * 8)), "latency"
+        assert torch.equal(t(pa, n * n * 4), t(pb, n * n * 4)), "loss bits"
+    finally:
+        a.close()
+        b.close()
+
+
+@pytest.mark.parametrize("n_gpus", [1, 3])
+def test_level_quantized_routing_info(n_gpus):
+    """RoutingInfo over a quantized plan: 8-byte records (u32 units), one GPU
+    and 3 in-process ranks (every rank's records downloaded straight into the
+    caller's array); paths and the min latency against the oracle."""
+    n = 1500
+    src, dst, lat, loss = synth.complete_graph_ns(n, 9)
+    g = NetworkGraph.from_edges(n, src, dst, lat, loss)
+    nodes = np.random.default_rng(n).permutation(n).astype(np.uint32)
+    og = O.Graph(False, np.arange(n), src, dst, lat, loss)
+    ri = RoutingInfo.build(g, nodes, device=0, n_gpus=n_gpus, same_device=n_gpus > 1)
+    try:
+        assert ri.record_bytes() == 8
+        elat, eloss = O.compute_shortest_paths(og, nodes)
+        ml, mp = ri.table()
+        off = ~np.eye(n, dtype=bool)
+        assert np.array_equal(ml[off], elat[off]) and np.array_equal(_bits(mp[off]), _bits(eloss[off]))
+        assert ri.get_smallest_latency_ns() == int(elat.min())
+    finally:
+        ri.close()
+    t = g.compute_shortest_paths(nodes, n_gpus=n_gpus, same_device=n_gpus > 1)
+    _check(t, og, nodes)
+
+
+@pytest.mark.parametrize("world,directed", [(2, False), (3, True)])
+def test_level_quantized_sharded_rows(world, directed):
+    """Quantized rows sharded over in-process communicator ranks: u32 staging
+    all-gathered chunk by chunk; rank 0's table is the oracle's."""
+    g, nodes, og = _random_ns(700, 40 + world, directed, 0.05)
+    t, descs, _ = sdist.local_build(g, nodes, [0] * world, algo=_lib.SRT_ALGO_LEVEL)
+    for d in descs:
+        assert d.startswith("level:u32 ") and f"ranks={world}" in d, d
+    _check(t, og, nodes)

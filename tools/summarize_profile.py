@@ -49,6 +49,8 @@ LABELS = {
     "fr_emit_kernel": "frontier emit",
     "decide_kernel": "packet decide",
     "level_solve_kernel": "level solve",
+    "level_q_kernel": "quantized level solve",
+    "edge_min_kernel": "shortest edge (quantized level probe)",
     "lvl_out_kernel": "level class CSR, out-rows",
     "lvl_in_kernel": "level class CSR, in-rows",
     "draw_kernel": "packet draw",
@@ -63,7 +65,7 @@ FETCH_CORR = {"minplus_u32_kernel": 2.0, "minplus_u16_kernel": 2.0,
               # frontier sweeps: 128-B rows gathered 16 B a lane (8 lanes a line)
               "fr_lat_sweep_kernel": 2.0, "fr_tight_kernel": 2.0, "fr_loss_sweep_kernel": 2.0, "fr_emit_kernel": 2.0,
               # level solve: class entries gathered 16 B a lane (4 lanes a 64-B run)
-              "level_solve_kernel": 2.0}
+              "level_solve_kernel": 2.0, "level_q_kernel": 2.0}
 
 
 def short(name):
