@@ -92,6 +92,10 @@ def parse_args():
                     help="skip the cold first-call legs (fresh processes) of the dense configs")
     ap.add_argument("--cold-child", dest="cold_child", default="", choices=["", "plain", "init"],
                     help=argparse.SUPPRESS)
+    ap.add_argument("--exchange", default="none", choices=["none", "allgather"],
+                    help="N > 1, LEVEL / SSSP plans: 'none' = rows sharded with no collective (each rank's rows stay "
+                         "in its HBM); 'allgather' = the communicator-bound build (rows all-gathered over RCCL so "
+                         "every rank holds the whole table)")
     ap.add_argument("--algo", default="auto", choices=["auto", "fw", "sssp", "level"],
                     help="kernel family (default: AUTO, the library's priced choice -- what the drop-in runs)")
     ap.add_argument("--emulate-ranks", dest="emulate_ranks", type=int, default=0,
@@ -215,10 +219,16 @@ class Dist:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        # rehearsal of the N-rank schedule on a one-GPU box (SRT_BENCH_ONE_DEVICE=1:
+        # every rank on cuda:0, barrier / max over gloo); never the measured setup
+        self.one_device = os.environ.get("SRT_BENCH_ONE_DEVICE") == "1"
+        self.dev = 0 if self.one_device else self.local_rank
         if self.world > 1:
-            torch.cuda.set_device(self.local_rank)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local_rank))
-        self.dev = self.local_rank
+            torch.cuda.set_device(self.dev)
+            if self.one_device:
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local_rank))
 
     def barrier(self):
         if self.world > 1:
@@ -228,7 +238,7 @@ class Dist:
     def max_over_ranks(self, x):
         if self.world == 1:
             return x
-        t = self.torch.tensor([x], dtype=self.torch.float64, device=f"cuda:{self.dev}")
+        t = self.torch.tensor([x], dtype=self.torch.float64, device="cpu" if self.one_device else f"cuda:{self.dev}")
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -470,7 +480,12 @@ def bench_graph(args, cfg, D):
     plan = RoutingPlan(g, nodes, algo=ALGOS[args.algo], device=D.dev)
     ranks = 1
     transport = None
-    if D.world > 1:
+    if D.world > 1 and args.exchange == "none" and plan.describe().startswith(("level", "sssp")):
+        # independent source rows (mod.rs:190-208): each rank builds its share
+        # of the rows into its own HBM, no collective in the data path -- the
+        # table stays distributed by rows, as the in-process build downloads it
+        plan.shard_rows(D.world, D.rank)
+    elif D.world > 1:
         from shadow_amd import dist as sdist
         # the collectives' transport is part of the measurement: native RCCL on
         # the plan's streams unless SRT_COMM names another; a failure to set it
@@ -480,6 +495,8 @@ def bench_graph(args, cfg, D):
     desc = plan.describe()
     if " ranks=" in desc:
         ranks = int(desc.split(" ranks=")[1].split()[0])
+    elif " shard=" in desc:
+        ranks = int(desc.split(" shard=")[1].split("/")[1].split()[0])
     if ranks != D.world:
         raise SystemExit(f"plan bound to {ranks} ranks but WORLD_SIZE={D.world}")
     elapsed, step_ms, k_ms, k_launches, k_work, k_tiles = timed_builds(plan, D, args.steps, args.warmup)
@@ -635,7 +652,10 @@ def bench_graph(args, cfg, D):
             "vs_baseline": None, "dtype": key,
             "data": data,
             "config": {"workload": f"{label}, use_shortest_path=true, {algo}", "nodes": n_nodes, "in_use": n,
-                       "pairs": pairs, "parallelism": f"rows{ranks}" if ranks > 1 else "single",
+                       "pairs": pairs,
+                       "parallelism": ("single" if ranks == 1 else
+                                       f"rows{ranks} (no exchange: each rank's rows stay in its HBM)"
+                                       if " shard=" in desc else f"rows{ranks} (all-gathered over {transport})"),
                        "transport": transport, "nranks": ranks,
                        "plan": desc, "step_ms": [round(x, 3) for x in step_ms], "build_wallclock_ms": ms_per_step,
                        "phases_last_build": {"device_total_ms": timing["total_ms"],

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define SRT_ABI_VERSION 2
+#define SRT_ABI_VERSION 3
 
 typedef enum {
     SRT_OK = 0,
@@ -213,6 +213,16 @@ void srt_comm_abort(srt_comm *comm);
  * block-row from its owner and all-gathers the path keys at the end, so every
  * rank holds the full table.  The communicator must outlive the plan. */
 srt_status srt_plan_bind_comm(srt_plan *plan, srt_comm *comm, srt_err *err);
+/* Row sharding without an exchange, for plans whose source rows are
+ * independent (LEVEL and SSSP: one Dijkstra per source, the rayon fan-out of
+ * mod.rs:190-208): from now on srt_plan_run computes only table rows
+ * [rank*n/nranks, (rank+1)*n/nranks) (other rows are not written) and the
+ * connectivity check / min latency of srt_plan_fetch cover those rows;
+ * srt_plan_fetch refuses `out` (read the rows through srt_plan_table).  The
+ * multi-process form of srt_opts.n_gpus: each rank's rows stay in its HBM or go
+ * to the host over its own link, no collective.  FW plans (the closure needs
+ * every pivot row): SRT_ERR_UNSUPPORTED -- bind a communicator instead. */
+srt_status srt_plan_shard_rows(srt_plan *plan, int nranks, int rank, srt_err *err);
 
 /* ------------------------------------------------------- packet delivery */
 /* One outgoing inter-host packet, in the source host's send order. */

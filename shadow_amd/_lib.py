@@ -107,6 +107,7 @@ SIGNATURES = {
     "srt_comm_init_local": (C.c_int, [C.c_int, C.POINTER(C.c_int32), C.POINTER(_vp), _errp]),
     "srt_comm_abort": (None, [_vp]),
     "srt_plan_bind_comm": (C.c_int, [_vp, _vp, _errp]),
+    "srt_plan_shard_rows": (C.c_int, [_vp, C.c_int, C.c_int, _errp]),
     "srt_packet_batch": (C.c_int, [_vp, _vp, _vp, C.c_uint32, C.c_uint64, _vp, C.POINTER(SrtRound), _vp, _vp, _vp,
                                    _vp, _errp]),
     "srt_packet_events_status": (C.c_int, [_vp, _errp]),
@@ -155,7 +156,7 @@ def lib():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
-        if L.srt_abi_version() != 2:
+        if L.srt_abi_version() != 3:
             raise SrtError(SRT_ERR_UNSUPPORTED, "libsrt ABI version mismatch")
         _lib = L
     return _lib

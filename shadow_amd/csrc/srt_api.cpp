@@ -1507,6 +1507,10 @@ srt_status srt_plan_fetch(srt_plan *p, srt_path *out, uint64_t *min_latency_ns, 
         return SRT_ERR_DISCONNECTED;
     }
     if (min_latency_ns) *min_latency_ns = stats[0];
+    if (out && p->row_shard) {
+        set_err(err, SRT_ERR_INVALID, "row-sharded plan: only its own rows were built (read them via srt_plan_table)");
+        return SRT_ERR_INVALID;
+    }
     if (out && p->n) {
         // AoS staging in chunks of at most 64 Mi entries (1 GiB): the 100k-node
         // table is 1e10 entries and must not be duplicated whole in HBM
@@ -1712,6 +1716,31 @@ srt_status srt_plan_bind_comm(srt_plan *p, srt_comm *comm, srt_err *err) {
     if (srt_status st = build_loss_rows(p, comm->nranks, per * srt::FW_B, err); st != SRT_OK) return st;
     char d[64];
     std::snprintf(d, sizeof d, " closure-rows=[%u,%u)", p->rb0 * srt::FW_B, p->rb1 * srt::FW_B);
+    p->desc += d;
+    return SRT_OK;
+}
+
+srt_status srt_plan_shard_rows(srt_plan *p, int nranks, int rank, srt_err *err) {
+    clear_err(err);
+    if (!p || nranks < 1 || rank < 0 || rank >= nranks) {
+        set_err(err, SRT_ERR_INVALID, "null plan or rank outside [0, nranks)");
+        return SRT_ERR_INVALID;
+    }
+    if (p->comm || p->row_shard) {
+        set_err(err, SRT_ERR_INVALID, "plan already sharded");
+        return SRT_ERR_INVALID;
+    }
+    if (p->algo != SRT_ALGO_LEVEL && p->algo != SRT_ALGO_SSSP) {
+        set_err(err, SRT_ERR_UNSUPPORTED,
+                "row sharding without an exchange needs independent source rows (LEVEL or SSSP plans); "
+                "bind a communicator for Floyd-Warshall");
+        return SRT_ERR_UNSUPPORTED;
+    }
+    p->row0 = (uint32_t)((uint64_t)p->n * rank / nranks);
+    p->row1 = (uint32_t)((uint64_t)p->n * (rank + 1) / nranks);
+    p->row_shard = true;
+    char d[80];
+    std::snprintf(d, sizeof d, " shard=%d/%d rows=[%u,%u)", rank, nranks, p->row0, p->row1);
     p->desc += d;
     return SRT_OK;
 }

@@ -306,6 +306,7 @@ struct srt_plan {
     // table rows travel as u32 latency units + f32 loss and are expanded into
     // the table on every rank
     bool shard_tail = false;               // this run used the sharded tail
+    bool row_shard = false;                // srt_plan_shard_rows: rows [row0, row1) only, no exchange
     bool tail_expanded = false;            // ... and expanded its chunks behind their all-gathers
     std::vector<uint32_t> lrow_cnt;        // per rank: loss-pass rows
     uint32_t lrow_max = 0;                 // staging rows per rank (tail_q chunks of tail_cr rows)

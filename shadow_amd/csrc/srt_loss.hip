@@ -311,24 +311,32 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t V, const uint64_t
         const uint32_t nch = (uint32_t)((e - b + 63) / 64);
         if (lane < 32) ccnt[wv][lane] = 0;
         uint32_t cnt = 0;
-        for (uint32_t c0 = 0; c0 < nch; c0 += 4) {
-            uint64_t l[4];
+        // 8 chunks in flight: their latencies, then -- all issued before any
+        // is tested -- the columns of the lanes whose latency passes
+        constexpr int PU = 8;
+        for (uint32_t c0 = 0; c0 < nch; c0 += PU) {
+            uint64_t l[PU];
+            uint32_t cc[PU];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < PU; ++q) {
                 const uint64_t k = b + 64ull * (c0 + q) + lane;
                 l[q] = k < e ? lat[k] : ~0ull;
             }
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < PU; ++q) {
                 const uint64_t k = b + 64ull * (c0 + q) + lane;
-                const bool f = l[q] <= wmax_ns && col[k] != u;  // col only where the latency passes
+                cc[q] = l[q] <= wmax_ns ? col[k] : u;
+            }
+#pragma unroll
+            for (int q = 0; q < PU; ++q) {
+                const bool f = l[q] <= wmax_ns && cc[q] != u;
                 const uint64_t m = __ballot(f);
                 if (f) {
                     const uint32_t c = cls_of(l[q]);
                     atomicAdd(&ccnt[wv][c - 1], 1u);
                     mw = c > mw ? c : mw;
                 }
-                if (c0 + q < TR_CH && lane == 0) bal[wv][c0 + q] = m;
+                if (c0 + q < TR_CH && c0 + q < nch && lane == 0) bal[wv][c0 + q] = m;
                 cnt += (uint32_t)__popcll(m);
             }
         }
@@ -347,28 +355,49 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t V, const uint64_t
         if (lane < cls) off_out[(uint64_t)u * cls + lane] = fits ? (lane == cls - 1 ? (uint32_t)(base + cnt) : start) : 0u;
         if (lane < 32) ccnt[wv][lane] = start;  // running positions
         if (!cnt || !fits) continue;            // uniform
-        for (uint32_t c = 0; c < nch; ++c) {
+        auto place = [&](uint32_t v, uint64_t l, float ls) {
+            const uint64_t wu = units_of(l);
+            const uint32_t cl = (uint32_t)(q ? wu / q : wu);
+            const uint32_t pos = atomicAdd(&ccnt[wv][cl - 1], 1u);
+            const float eb = WITH_LOSS ? 1.0f - ls : 0.0f;  // (1f32 - other.packet_loss), mod.rs:328
+            // q > 0 (quantized classes): the weight's remainder w - c q rides
+            // along, (1 - e) in bits 34.. (a loss in [0, 1]: its bits are < 2^30)
+            ce_out[pos] = q ? ((uint64_t)__float_as_uint(eb) << 34) | ((wu - (uint64_t)cl * q) << vb) | v
+                            : ((uint64_t)__float_as_uint(eb) << 32) | v;
+            atomicAdd(&in_cnt[(uint64_t)v * cls + cl - 1], 1u);
+        };
+        // the kept chunks PU at a time: every hit's column, latency and loss
+        // loaded before the first is placed (one memory round trip a group,
+        // not one a chunk)
+        const uint32_t nc1 = nch < TR_CH ? nch : TR_CH;
+        for (uint32_t c0 = 0; c0 < nc1; c0 += PU) {
+            uint64_t mm[PU], any = 0;
+#pragma unroll
+            for (int z = 0; z < PU; ++z) {
+                mm[z] = c0 + z < nc1 ? bal[wv][c0 + z] : 0ull;
+                any |= mm[z];
+            }
+            if (!any) continue;  // uniform
+            uint32_t vv[PU];
+            uint64_t ll[PU];
+            float ls[PU];
+#pragma unroll
+            for (int z = 0; z < PU; ++z) {
+                const bool h = (mm[z] >> lane) & 1ull;
+                const uint64_t k = b + 64ull * (c0 + z) + lane;
+                vv[z] = h ? col[k] : 0u;
+                ll[z] = h ? lat[k] : 0ull;
+                ls[z] = WITH_LOSS && h ? loss[k] : 0.0f;
+            }
+#pragma unroll
+            for (int z = 0; z < PU; ++z)
+                if ((mm[z] >> lane) & 1ull) place(vv[z], ll[z], ls[z]);
+        }
+        for (uint32_t c = TR_CH; c < nch; ++c) {  // rows past TR_CH chunks: tested again
             const uint64_t k = b + 64ull * c + lane;
-            uint64_t m;
-            if (c < TR_CH) {
-                m = bal[wv][c];
-            } else {
-                const uint64_t l = k < e ? lat[k] : ~0ull;
-                m = __ballot(l <= wmax_ns && col[k] != u);
-            }
-            if (!m) continue;  // uniform
-            if ((m >> lane) & 1ull) {
-                const uint32_t v = col[k];
-                const uint64_t wu = units_of(lat[k]);
-                const uint32_t cl = (uint32_t)(q ? wu / q : wu);
-                const uint32_t pos = atomicAdd(&ccnt[wv][cl - 1], 1u);
-                const float eb = WITH_LOSS ? 1.0f - loss[k] : 0.0f;  // (1f32 - other.packet_loss), mod.rs:328
-                // q > 0 (quantized classes): the weight's remainder w - c q rides
-                // along, (1 - e) in bits 34.. (a loss in [0, 1]: its bits are < 2^30)
-                ce_out[pos] = q ? ((uint64_t)__float_as_uint(eb) << 34) | ((wu - (uint64_t)cl * q) << vb) | v
-                                : ((uint64_t)__float_as_uint(eb) << 32) | v;
-                atomicAdd(&in_cnt[(uint64_t)v * cls + cl - 1], 1u);
-            }
+            const uint64_t l = k < e ? lat[k] : ~0ull;
+            const bool f = l <= wmax_ns && col[k] != u;
+            if (f) place(col[k], l, WITH_LOSS ? loss[k] : 0.0f);
         }
     }
     for (int off = 32; off > 0; off >>= 1) {
@@ -390,17 +419,36 @@ __global__ __launch_bounds__(256) void lvl_in_kernel(uint32_t V, uint32_t cls, u
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    constexpr int IU = 4;  // chunks of 64 entries in flight
     for (uint32_t u = wave; u < V; u += nwaves) {
-        const uint32_t *ou = off_out + (uint64_t)u * cls;
-        const uint32_t e0 = ou[0], e1 = ou[cls - 1];
-        for (uint32_t k = e0 + lane; k < e1; k += 64) {
-            uint32_t c = 1;  // the class of entry k: the last class whose start is <= k
-            while (c + 1 < cls && ou[c] <= k) ++c;
-            const uint64_t w = ce_out[k];
-            const uint32_t v = (uint32_t)(w & vmask);
-            const uint64_t slot = (uint64_t)v * cls + c - 1;
-            const uint32_t pos = in_off[slot] + atomicAdd(&in_cur[slot], 1u);
-            ce_in[pos] = (w & ~vmask) | u;
+        // the row's class offsets, one a lane (slot c: start of class c + 1;
+        // slot cls - 1: the row's end): an entry's class by lane broadcasts
+        const uint32_t myo = lane < cls ? off_out[(uint64_t)u * cls + lane] : ~0u;
+        const uint32_t e0 = __shfl(myo, 0), e1 = __shfl(myo, (int)cls - 1);
+        for (uint32_t base = e0; base < e1; base += 64 * IU) {
+            uint32_t kk[IU], cc[IU];
+            uint64_t w[IU];
+#pragma unroll
+            for (int z = 0; z < IU; ++z) {
+                kk[z] = base + 64 * z + lane;
+                cc[z] = 1;  // the class of entry k: 1 + the class starts <= k past the first
+            }
+            for (uint32_t j = 1; j + 1 < cls; ++j) {
+                const uint32_t oj = __shfl(myo, (int)j);
+#pragma unroll
+                for (int z = 0; z < IU; ++z) cc[z] += oj <= kk[z];
+            }
+#pragma unroll
+            for (int z = 0; z < IU; ++z) w[z] = kk[z] < e1 ? ce_out[kk[z]] : 0ull;
+            uint32_t pos[IU];
+#pragma unroll
+            for (int z = 0; z < IU; ++z) {
+                const uint64_t slot = (uint64_t)(uint32_t)(w[z] & vmask) * cls + cc[z] - 1;
+                pos[z] = kk[z] < e1 ? in_off[slot] + atomicAdd(&in_cur[slot], 1u) : 0u;
+            }
+#pragma unroll
+            for (int z = 0; z < IU; ++z)
+                if (kk[z] < e1) ce_in[pos[z]] = (w[z] & ~vmask) | u;
         }
     }
 }

@@ -89,6 +89,13 @@ class RoutingPlan:
         _lib.lib().srt_plan_table(self._h, C.byref(lat), C.byref(loss), C.byref(n))
         return lat.value, loss.value, n.value
 
+    def shard_rows(self, nranks: int, rank: int):
+        """srt_plan_shard_rows: this plan builds only table rows
+        [rank*n/nranks, (rank+1)*n/nranks), no exchange (LEVEL / SSSP plans)."""
+        err = _lib.SrtErr()
+        _lib.check(_lib.lib().srt_plan_shard_rows(self._h, int(nranks), int(rank), C.byref(err)), err)
+        return self
+
     def bind_comm(self, comm):
         err = _lib.SrtErr()
         _lib.check(_lib.lib().srt_plan_bind_comm(self._h, comm, C.byref(err)), err)

@@ -297,3 +297,47 @@ def test_level_quantized_sharded_rows(world, directed):
     for d in descs:
         assert d.startswith("level:u32 ") and f"ranks={world}" in d, d
     _check(t, og, nodes)
+
+
+@pytest.mark.parametrize("quant", [False, True])
+def test_level_shard_rows_no_exchange(quant):
+    """srt_plan_shard_rows (the multi-process form, no collective): 3 plans,
+    each building only its third of the rows into its own table; together the
+    rows are the oracle's table.  fetch(out) is refused on a sharded plan, and
+    Floyd-Warshall plans refuse the sharding."""
+    import torch
+
+    if quant:
+        g, nodes, og = _random_ns(500, 61, False, 0.08)
+    else:
+        g, nodes, og = _random(500, 61, False, (1, 9), 0.08)
+    n = len(nodes)
+    elat, eloss = O.compute_shortest_paths(og, nodes)
+    dev = torch.device("cuda", 0)
+    mins = []
+    for r in range(3):
+        p = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_LEVEL, device=0).shard_rows(3, r)
+        try:
+            assert f"shard={r}/3" in p.describe()
+            p.run()
+            p.fetch(table=False)
+            mins.append(p.min_latency_ns)
+            with pytest.raises(_lib.SrtError) as e:
+                p.fetch()
+            assert e.value.code == _lib.SRT_ERR_INVALID
+            la, pa, _ = p.table_ptrs()
+            L = torch.as_tensor(sdist._CudaBuf(la, n * n * 8), device=dev).view(torch.int64).view(n, n)
+            P = torch.as_tensor(sdist._CudaBuf(pa, n * n * 4), device=dev).view(torch.int32).view(n, n)
+            r0, r1 = n * r // 3, n * (r + 1) // 3
+            assert np.array_equal(L[r0:r1].cpu().numpy().view(np.uint64), elat[r0:r1])
+            assert np.array_equal(P[r0:r1].cpu().numpy().view(np.uint32), _bits(eloss[r0:r1]))
+        finally:
+            p.close()
+    assert min(mins) == int(elat.min())
+    fw = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_FW, device=0)
+    try:
+        with pytest.raises(_lib.SrtError) as e:
+            fw.shard_rows(2, 0)
+        assert e.value.code == _lib.SRT_ERR_UNSUPPORTED
+    finally:
+        fw.close()
