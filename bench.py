@@ -98,6 +98,10 @@ def parse_args():
                          "every rank holds the whole table)")
     ap.add_argument("--algo", default="auto", choices=["auto", "fw", "sssp", "level"],
                     help="kernel family (default: AUTO, the library's priced choice -- what the drop-in runs)")
+    ap.add_argument("--rank-share", dest="rank_share", type=int, default=0,
+                    help="measurement only: one GPU builds rank 0's rows of an N-rank row-sharded build "
+                         "(srt_plan_shard_rows(N, 0): exactly that rank's work, no exchange exists) and prints "
+                         "its time; not a bench line")
     ap.add_argument("--emulate-ranks", dest="emulate_ranks", type=int, default=0,
                     help="measurement only (dense FW, 1 GPU): time one rank of an N-rank run -- 1/N of the "
                          "block-rows plus the pivot owner's chain every round, no collectives; the table "
@@ -480,6 +484,22 @@ def bench_graph(args, cfg, D):
     plan = RoutingPlan(g, nodes, algo=ALGOS[args.algo], device=D.dev)
     ranks = 1
     transport = None
+    if args.rank_share > 1 and D.world == 1:
+        plan.shard_rows(args.rank_share, 0)
+        elapsed, step_ms, k_ms, k_launches, k_work, _ = timed_builds(plan, D, args.steps, args.warmup)
+        t = plan.timing()
+        ms = elapsed * 1e3 / args.steps
+        print(json.dumps({"rank_share": {"ranks": args.rank_share, "rank": 0, "config": args.config,
+                                         "plan": plan.describe(), "ms_per_step": ms,
+                                         "solve_ms_per_step": k_ms / args.steps,
+                                         "device_total_ms_last": t["total_ms"],
+                                         "implied_value_pairs_per_s": len(nodes) ** 2 / (ms / 1e3),
+                                         "note": "rank 0's rows of an N-rank row-sharded build, measured alone on one "
+                                                 "GPU: the whole of that rank's work (row sharding has no exchange); "
+                                                 "the implied value assumes the N ranks run concurrently on N GPUs"}}),
+              flush=True)
+        plan.close()
+        return None
     if D.world > 1 and args.exchange == "none" and plan.describe().startswith(("level", "sssp")):
         # independent source rows (mod.rs:190-208): each rank builds its share
         # of the rows into its own HBM, no collective in the data path -- the

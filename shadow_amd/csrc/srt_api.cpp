@@ -544,6 +544,8 @@ srt_status dmalloc(T **p, size_t count, srt_err *err) {
 }
 
 void free_plan_buffers(srt_plan *p) {
+    if (p->loss_checker.joinable()) p->loss_checker.join();  // it writes h_lossbad
+    hipFree(p->d_lidx);
     hipFree(p->d_row_ptr);
     hipFree(p->d_col);
     hipFree(p->d_lat);
@@ -984,6 +986,7 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         if (try_lvl) {
             p->kp.g = cs.gcd;
             p->lvl_q = 0;
+            p->lvl_maxu = maxu;
             srt_err e2{};
             auto probe_fail = [&]() {
                 srt_plan_destroy(p);
@@ -1381,7 +1384,104 @@ srt_status run_closure(srt_plan *p, srt_err *err) {
 // on one GPU; the closure is all on the main and side streams) and the main
 // stream waits for them before the loss pass -- on the main stream they would
 // queue behind the closure (measured: C3 +19 ms, serial).
+// Level plans (n_adj < 2^32): only the losses the class CSRs read cross PCIe
+// -- their adjacency indices listed on the device (latency <= B units, not a
+// self-loop: C3 5.4M of 268M entries), downloaded into the pinned staging,
+// gathered on host threads and scattered into d_loss -- while the range check
+// of every loss (the reference's parse-time error) runs on host threads
+// behind the build (p->loss_checker, joined before h_lossbad is read).
+// C3: the 1 GB loss upload (~25 ms on the critical path) becomes ~22 MB each
+// way.  false: not applicable (the caller uploads everything).
+bool upload_level_losses(srt_plan *p, srt_err *err, srt_status *st) {
+    *st = SRT_OK;
+    if (p->algo != SRT_ALGO_LEVEL || p->n_adj >= (1ull << 32) || !p->lvl_cap || std::getenv("SRT_LOSS_FULL"))
+        return false;
+    std::unique_lock<std::mutex> lk(g_pinned.m, std::try_to_lock);
+    const uint64_t cap = p->lvl_cap;  // the probe's count: >= the run's (its bound is >= B)
+    if (!lk.owns_lock() || g_pinned.bytes < 64) return false;
+    hipStream_t M = p->stream;
+    auto fail = [&](hipError_t e, const char *what) {
+        *st = hip_fail(err, e, what);
+        return true;
+    };
+    hipError_t e = hipSuccess;
+    if (!p->d_lidx || p->lidx_cap < cap) {
+        (void)hipFree(p->d_lidx);
+        p->d_lidx = nullptr;
+        e = hipMalloc(&p->d_lidx, cap * 8 + 16);
+        if (e != hipSuccess) return fail(e, "hipMalloc(loss indices)");
+        p->lidx_cap = cap;
+    }
+    uint32_t *d_idx = reinterpret_cast<uint32_t *>(p->d_lidx);
+    float *d_val = reinterpret_cast<float *>(d_idx + cap);
+    unsigned long long *d_cnt = reinterpret_cast<unsigned long long *>(d_val + cap + (cap & 1));
+    srt::level_loss_index(p, d_idx, cap, d_cnt, M);
+    uint64_t *h = reinterpret_cast<uint64_t *>(g_pinned.buf);
+    e = hipMemcpyAsync(h, d_cnt, 8, hipMemcpyDeviceToHost, M);
+    if (e == hipSuccess) e = hipStreamSynchronize(M);
+    if (e != hipSuccess) return fail(e, "loss indices (count)");
+    const uint64_t cnt = h[0];
+    // (cnt > cap cannot happen: the probe's bound is >= the run's)
+    if (cnt > cap || g_pinned.bytes < cnt * 8) return false;  // the full upload
+    // the range check of every loss, behind the build (8 host threads)
+    const float *src = p->h_loss_defer;
+    const uint64_t m = p->n_adj;
+    unsigned long long *hb = p->h_lossbad;
+    *hb = ~0ull;
+    p->loss_checker = std::thread([src, m, hb] {
+        const int T = std::max(1, std::min(8, host_threads(m)));
+        std::vector<uint64_t> first(T, ~0ull);
+        std::vector<std::thread> pool;
+        const uint32_t *q = reinterpret_cast<const uint32_t *>(src);
+        for (int t = 0; t < T; ++t)
+            pool.emplace_back([&, t] {
+                for (uint64_t k = m * t / T; k < m * (t + 1) / T; ++k)
+                    if (srt::loss_bits_bad(q[k])) {
+                        first[t] = k;
+                        break;
+                    }
+            });
+        for (auto &th : pool) th.join();
+        *hb = *std::min_element(first.begin(), first.end());
+    });
+    uint32_t *hidx = reinterpret_cast<uint32_t *>(g_pinned.buf);
+    float *hval = reinterpret_cast<float *>(hidx + cnt);
+    e = hipMemcpyAsync(hidx, d_idx, cnt * 4, hipMemcpyDeviceToHost, M);
+    if (e == hipSuccess) e = hipStreamSynchronize(M);
+    if (e != hipSuccess) return fail(e, "loss indices");
+    {
+        const int T = host_threads(cnt * 16);
+        std::vector<std::thread> pool;
+        auto part = [&](int t) {
+            for (uint64_t i = cnt * t / T; i < cnt * (t + 1) / T; ++i) hval[i] = src[hidx[i]];
+        };
+        for (int t = 1; t < T; ++t) pool.emplace_back(part, t);
+        part(0);
+        for (auto &th : pool) th.join();
+    }
+    e = hipMemcpyAsync(d_val, hval, cnt * 4, hipMemcpyHostToDevice, M);
+    if (e != hipSuccess) return fail(e, "upload (needed losses)");
+    srt::loss_scatter(d_idx, d_val, cnt, p->d_loss, M);
+    // the staging is reused by the download: the upload must be done first
+    e = hipStreamSynchronize(M);
+    if (e != hipSuccess) return fail(e, "upload (needed losses)");
+    p->h_loss_defer = nullptr;
+    return true;
+}
+
+void join_loss_check(srt_plan *p) {
+    if (p->loss_checker.joinable()) p->loss_checker.join();
+}
+
 srt_status upload_deferred_loss(srt_plan *p, srt_err *err) {
+    if (p->h_loss_defer && !p->d_lossbad) {
+        HIP_TRY(hipMalloc(&p->d_lossbad, 8), "hipMalloc(loss check)");
+        HIP_TRY(hipHostMalloc((void **)&p->h_lossbad, 8, 0), "hipHostMalloc(loss check)");
+    }
+    if (p->h_loss_defer) {
+        srt_status st;
+        if (upload_level_losses(p, err, &st)) return st;
+    }
     if (p->h_loss_defer) {
         hipStream_t up = p->comm ? p->stream : p->comm_stream;
         if (!p->d_lossbad) {
@@ -2280,6 +2380,7 @@ srt_status build_multi(const srt_csr *g, const uint32_t *nodes, uint32_t n, srt_
         if (p0->algo == SRT_ALGO_LEVEL) {
             srt_status s = build_multi_level(p0, devs, out, ct, min_latency_ns, err);
             // the device's loss range check: a parse-time error, so it wins
+            join_loss_check(p0);
             if (p0->h_lossbad && s != SRT_ERR_HIP) {
                 (void)hipSetDevice(p0->device);
                 (void)hipStreamSynchronize(p0->comm_stream);
@@ -2413,6 +2514,7 @@ srt_status build_e2e(const srt_csr *g, const uint32_t *nodes, uint32_t n, srt_pa
     tr.mark("e2e: build + fetch");
     // the device's loss range check (the host scan skipped it): a parse-time
     // error, so it wins over any error of the build itself
+    join_loss_check(p);
     if (p->h_lossbad && s != SRT_ERR_HIP) {
         (void)hipStreamSynchronize(p->comm_stream);
         if (*p->h_lossbad != ~0ull) {

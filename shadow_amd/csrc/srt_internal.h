@@ -7,6 +7,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/srt.h"
@@ -140,6 +141,9 @@ struct srt_plan {
     // end-to-end builds: the losses are range-checked on the device as they
     // are uploaded; the first bad entry (~0 if none) lands in h_lossbad
     unsigned long long *d_lossbad = nullptr, *h_lossbad = nullptr;
+    std::thread loss_checker;  // level plans: the range check of every loss on host threads (h_lossbad)
+    void *d_lidx = nullptr;    // level plans' loss upload: needed entries' indices (u32), then their losses
+    uint64_t lidx_cap = 0;
     uint32_t fold_chunk_rows = 0;
     std::vector<hipEvent_t> ev_fold;      // emulation: D holds the closure (first run done)
     uint64_t emu_tight = 0, emu_maxw = 0;  // emulation: tight edges / max latency of the closure
@@ -283,6 +287,8 @@ struct srt_plan {
     uint32_t t_cls = 16;             // class offsets per vertex of the level fold's CSRs (16 or 32)
     uint32_t *d_tcw = nullptr;       // quantized fold: each class entry's exact weight (out, then in), t_cap each
     uint64_t lvl_cap = 0;            // level solve: class entries d_tpk / d_tpk2 hold (the probe's count)
+    uint64_t lvl_est = 0;            // the probe's entry-count estimate (sizes the arrays before its one pass)
+    uint64_t lvl_maxu = 0;           // the longest edge, units of g (the estimate's scale)
     unsigned long long *d_lvisit = nullptr;  // level solve: class entries the last run walked
     uint32_t lvl_q = 0, lvl_rb = 0, lvl_vb = 0;  // quantized level solve: bucket width (units), entry field bits
     uint16_t *d_lmem = nullptr;              // its per-workgroup scratch (lmem_cap u16)
@@ -437,6 +443,11 @@ size_t level_scratch_bytes(int device, uint32_t V, bool quant);
 uint32_t level_vbits(uint32_t V);
 // the shortest non-self-loop edge latency of the plan's uploaded graph, ns
 srt_status level_min_edge(srt_plan *p, uint64_t *min_ns, srt_err *err);
+// the adjacency indices (u32) of the entries a level plan's class CSRs read
+// (latency <= kp.lmax units, not a self-loop) into d_idx (cap entries), their
+// count into *d_cnt; and the scatter of gathered losses into d_loss
+void level_loss_index(srt_plan *p, uint32_t *d_idx, uint64_t cap, unsigned long long *d_cnt, hipStream_t s);
+void loss_scatter(const uint32_t *d_idx, const float *d_val, uint64_t count, float *d_loss, hipStream_t s);
 // d_stats = (~0, 0) on stream s
 void level_stats_init(unsigned long long *d_stats, hipStream_t s);
 // sharded tail: every rank's staged rows (d_slat / d_sloss, all-gathered) into the table

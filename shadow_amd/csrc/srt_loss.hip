@@ -311,32 +311,24 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t V, const uint64_t
         const uint32_t nch = (uint32_t)((e - b + 63) / 64);
         if (lane < 32) ccnt[wv][lane] = 0;
         uint32_t cnt = 0;
-        // 8 chunks in flight: their latencies, then -- all issued before any
-        // is tested -- the columns of the lanes whose latency passes
-        constexpr int PU = 8;
-        for (uint32_t c0 = 0; c0 < nch; c0 += PU) {
-            uint64_t l[PU];
-            uint32_t cc[PU];
+        for (uint32_t c0 = 0; c0 < nch; c0 += 4) {
+            uint64_t l[4];
 #pragma unroll
-            for (int q = 0; q < PU; ++q) {
+            for (int q = 0; q < 4; ++q) {
                 const uint64_t k = b + 64ull * (c0 + q) + lane;
                 l[q] = k < e ? lat[k] : ~0ull;
             }
 #pragma unroll
-            for (int q = 0; q < PU; ++q) {
+            for (int q = 0; q < 4; ++q) {
                 const uint64_t k = b + 64ull * (c0 + q) + lane;
-                cc[q] = l[q] <= wmax_ns ? col[k] : u;
-            }
-#pragma unroll
-            for (int q = 0; q < PU; ++q) {
-                const bool f = l[q] <= wmax_ns && cc[q] != u;
+                const bool f = l[q] <= wmax_ns && col[k] != u;  // col only where the latency passes
                 const uint64_t m = __ballot(f);
                 if (f) {
                     const uint32_t c = cls_of(l[q]);
                     atomicAdd(&ccnt[wv][c - 1], 1u);
                     mw = c > mw ? c : mw;
                 }
-                if (c0 + q < TR_CH && c0 + q < nch && lane == 0) bal[wv][c0 + q] = m;
+                if (c0 + q < TR_CH && lane == 0) bal[wv][c0 + q] = m;
                 cnt += (uint32_t)__popcll(m);
             }
         }
@@ -355,49 +347,28 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t V, const uint64_t
         if (lane < cls) off_out[(uint64_t)u * cls + lane] = fits ? (lane == cls - 1 ? (uint32_t)(base + cnt) : start) : 0u;
         if (lane < 32) ccnt[wv][lane] = start;  // running positions
         if (!cnt || !fits) continue;            // uniform
-        auto place = [&](uint32_t v, uint64_t l, float ls) {
-            const uint64_t wu = units_of(l);
-            const uint32_t cl = (uint32_t)(q ? wu / q : wu);
-            const uint32_t pos = atomicAdd(&ccnt[wv][cl - 1], 1u);
-            const float eb = WITH_LOSS ? 1.0f - ls : 0.0f;  // (1f32 - other.packet_loss), mod.rs:328
-            // q > 0 (quantized classes): the weight's remainder w - c q rides
-            // along, (1 - e) in bits 34.. (a loss in [0, 1]: its bits are < 2^30)
-            ce_out[pos] = q ? ((uint64_t)__float_as_uint(eb) << 34) | ((wu - (uint64_t)cl * q) << vb) | v
-                            : ((uint64_t)__float_as_uint(eb) << 32) | v;
-            atomicAdd(&in_cnt[(uint64_t)v * cls + cl - 1], 1u);
-        };
-        // the kept chunks PU at a time: every hit's column, latency and loss
-        // loaded before the first is placed (one memory round trip a group,
-        // not one a chunk)
-        const uint32_t nc1 = nch < TR_CH ? nch : TR_CH;
-        for (uint32_t c0 = 0; c0 < nc1; c0 += PU) {
-            uint64_t mm[PU], any = 0;
-#pragma unroll
-            for (int z = 0; z < PU; ++z) {
-                mm[z] = c0 + z < nc1 ? bal[wv][c0 + z] : 0ull;
-                any |= mm[z];
-            }
-            if (!any) continue;  // uniform
-            uint32_t vv[PU];
-            uint64_t ll[PU];
-            float ls[PU];
-#pragma unroll
-            for (int z = 0; z < PU; ++z) {
-                const bool h = (mm[z] >> lane) & 1ull;
-                const uint64_t k = b + 64ull * (c0 + z) + lane;
-                vv[z] = h ? col[k] : 0u;
-                ll[z] = h ? lat[k] : 0ull;
-                ls[z] = WITH_LOSS && h ? loss[k] : 0.0f;
-            }
-#pragma unroll
-            for (int z = 0; z < PU; ++z)
-                if ((mm[z] >> lane) & 1ull) place(vv[z], ll[z], ls[z]);
-        }
-        for (uint32_t c = TR_CH; c < nch; ++c) {  // rows past TR_CH chunks: tested again
+        for (uint32_t c = 0; c < nch; ++c) {
             const uint64_t k = b + 64ull * c + lane;
-            const uint64_t l = k < e ? lat[k] : ~0ull;
-            const bool f = l <= wmax_ns && col[k] != u;
-            if (f) place(col[k], l, WITH_LOSS ? loss[k] : 0.0f);
+            uint64_t m;
+            if (c < TR_CH) {
+                m = bal[wv][c];
+            } else {
+                const uint64_t l = k < e ? lat[k] : ~0ull;
+                m = __ballot(l <= wmax_ns && col[k] != u);
+            }
+            if (!m) continue;  // uniform
+            if ((m >> lane) & 1ull) {
+                const uint32_t v = col[k];
+                const uint64_t wu = units_of(lat[k]);
+                const uint32_t cl = (uint32_t)(q ? wu / q : wu);
+                const uint32_t pos = atomicAdd(&ccnt[wv][cl - 1], 1u);
+                const float eb = WITH_LOSS ? 1.0f - loss[k] : 0.0f;  // (1f32 - other.packet_loss), mod.rs:328
+                // q > 0 (quantized classes): the weight's remainder w - c q rides
+                // along, (1 - e) in bits 34.. (a loss in [0, 1]: its bits are < 2^30)
+                ce_out[pos] = q ? ((uint64_t)__float_as_uint(eb) << 34) | ((wu - (uint64_t)cl * q) << vb) | v
+                                : ((uint64_t)__float_as_uint(eb) << 32) | v;
+                atomicAdd(&in_cnt[(uint64_t)v * cls + cl - 1], 1u);
+            }
         }
     }
     for (int off = 32; off > 0; off >>= 1) {
@@ -419,38 +390,73 @@ __global__ __launch_bounds__(256) void lvl_in_kernel(uint32_t V, uint32_t cls, u
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    constexpr int IU = 4;  // chunks of 64 entries in flight
     for (uint32_t u = wave; u < V; u += nwaves) {
-        // the row's class offsets, one a lane (slot c: start of class c + 1;
-        // slot cls - 1: the row's end): an entry's class by lane broadcasts
-        const uint32_t myo = lane < cls ? off_out[(uint64_t)u * cls + lane] : ~0u;
-        const uint32_t e0 = __shfl(myo, 0), e1 = __shfl(myo, (int)cls - 1);
-        for (uint32_t base = e0; base < e1; base += 64 * IU) {
-            uint32_t kk[IU], cc[IU];
-            uint64_t w[IU];
-#pragma unroll
-            for (int z = 0; z < IU; ++z) {
-                kk[z] = base + 64 * z + lane;
-                cc[z] = 1;  // the class of entry k: 1 + the class starts <= k past the first
-            }
-            for (uint32_t j = 1; j + 1 < cls; ++j) {
-                const uint32_t oj = __shfl(myo, (int)j);
-#pragma unroll
-                for (int z = 0; z < IU; ++z) cc[z] += oj <= kk[z];
-            }
-#pragma unroll
-            for (int z = 0; z < IU; ++z) w[z] = kk[z] < e1 ? ce_out[kk[z]] : 0ull;
-            uint32_t pos[IU];
-#pragma unroll
-            for (int z = 0; z < IU; ++z) {
-                const uint64_t slot = (uint64_t)(uint32_t)(w[z] & vmask) * cls + cc[z] - 1;
-                pos[z] = kk[z] < e1 ? in_off[slot] + atomicAdd(&in_cur[slot], 1u) : 0u;
-            }
-#pragma unroll
-            for (int z = 0; z < IU; ++z)
-                if (kk[z] < e1) ce_in[pos[z]] = (w[z] & ~vmask) | u;
+        const uint32_t *ou = off_out + (uint64_t)u * cls;
+        const uint32_t e0 = ou[0], e1 = ou[cls - 1];
+        for (uint32_t k = e0 + lane; k < e1; k += 64) {
+            uint32_t c = 1;  // the class of entry k: the last class whose start is <= k
+            while (c + 1 < cls && ou[c] <= k) ++c;
+            const uint64_t w = ce_out[k];
+            const uint32_t v = (uint32_t)(w & vmask);
+            const uint64_t slot = (uint64_t)v * cls + c - 1;
+            const uint32_t pos = in_off[slot] + atomicAdd(&in_cur[slot], 1u);
+            ce_in[pos] = (w & ~vmask) | u;
         }
     }
+}
+
+// The adjacency indices of the entries a level plan's class CSRs read
+// (latency <= wmax_ns, not a self-loop), for the one-call build's loss upload
+// (only those losses cross PCIe).  One wave per row: pass 1 keeps the chunks'
+// ballots in LDS, one atomic reserves the row's range, pass 2 writes the
+// indices in row order.  Past `cap` entries are counted, not written.
+__global__ __launch_bounds__(256) void lvl_index_kernel(uint32_t V, const uint64_t *__restrict__ row_ptr,
+                                                        const uint32_t *__restrict__ col,
+                                                        const uint64_t *__restrict__ lat, uint64_t wmax_ns,
+                                                        uint32_t *__restrict__ idx, uint64_t cap,
+                                                        unsigned long long *cursor) {
+    __shared__ uint64_t bal[4][TR_CH];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (uint32_t u = wave; u < V; u += nwaves) {
+        const uint64_t b = row_ptr[u], e = row_ptr[u + 1];
+        const uint32_t nch = (uint32_t)((e - b + 63) / 64);
+        auto test = [&](uint32_t c) -> uint64_t {
+            const uint64_t k = b + 64ull * c + lane;
+            const uint64_t l = k < e ? lat[k] : ~0ull;
+            return __ballot(l <= wmax_ns && col[k] != u);
+        };
+        uint32_t cnt = 0;
+        for (uint32_t c0 = 0; c0 < nch; c0 += 4) {
+            uint64_t m[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) m[q] = c0 + q < nch ? test(c0 + q) : 0ull;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (c0 + q < TR_CH && lane == 0) bal[wv][c0 + q] = m[q];
+                cnt += (uint32_t)__popcll(m[q]);
+            }
+        }
+        unsigned long long base = 0;
+        if (cnt && lane == 0) base = atomicAdd(cursor, (unsigned long long)cnt);
+        base = __shfl(base, 0);
+        if (!cnt || base + cnt > cap) continue;  // uniform
+        for (uint32_t c = 0; c < nch; ++c) {
+            const uint64_t m = c < TR_CH ? bal[wv][c] : test(c);
+            if (!m) continue;  // uniform
+            if ((m >> lane) & 1ull) idx[base + (uint64_t)__popcll(m & below)] = (uint32_t)(b + 64ull * c + lane);
+            base += (uint64_t)__popcll(m);
+        }
+    }
+}
+
+__global__ void loss_scatter_kernel(const uint32_t *__restrict__ idx, const float *__restrict__ val, uint64_t count,
+                                    float *__restrict__ loss) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < count;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        loss[idx[i]] = val[i];
 }
 
 // Per-row counts of a tight-edge list (v = ~0: padding): rows by target v
@@ -2855,24 +2861,37 @@ srt_status level_csr(srt_plan *p, uint64_t wmax, bool with_loss, srt_err *err) {
                                p->d_lat, (const float *)nullptr, p->kp.g, inv_g, wns, cls, q, vb, p->d_tcls,
                                p->d_tccnt, p->d_tpk, p->lvl_cap, p->d_tcursor, (unsigned long long *)p->d_tmaxw);
     };
-    out_pass();
-    if (!p->lvl_cap) {
-        // first call: count, size the entry arrays (+1024: the solve's 2-entry
-        // loads read up to UNR * LPT * 2 entries past a class's end), run again
-        hipError_t e = hipMemcpyAsync(p->h_tcount, p->d_tcursor, sizeof(uint64_t), hipMemcpyDeviceToHost, M);
-        if (e == hipSuccess) e = hipStreamSynchronize(M);
-        if (e != hipSuccess) return fail(err, e, "level edge count");
-        const uint64_t need = std::max<uint64_t>(p->h_tcount[0], 1) + 1024;
+    // first call (the create-time probe): entry arrays of the caller's
+    // estimate (p->lvl_est; +1024: the solve's 2-entry loads read up to UNR *
+    // LPT * 2 entries past a class's end), one pass, the count read back; an
+    // estimate too small (or none) sizes them by the count and runs again.
+    // lvl_cap = the count: every later call prunes at a bound <= this wmax
+    auto size_arrays = [&](uint64_t entries) -> srt_status {
         uint64_t ca = 0, cb = 0;
         (void)hipFree(p->d_tpk);
         (void)hipFree(p->d_tpk2);
         p->d_tpk = p->d_tpk2 = nullptr;
         p->t_cap = 0;
-        if ((st = grow(&p->d_tpk, &ca, need, err, "hipMalloc(level out-rows)")) != SRT_OK ||
-            (st = grow(&p->d_tpk2, &cb, need, err, "hipMalloc(level in-rows)")) != SRT_OK)
-            return st;
-        p->lvl_cap = need - 1024;
-        out_pass();
+        srt_status s2;
+        if ((s2 = grow(&p->d_tpk, &ca, entries + 1024, err, "hipMalloc(level out-rows)")) != SRT_OK ||
+            (s2 = grow(&p->d_tpk2, &cb, entries + 1024, err, "hipMalloc(level in-rows)")) != SRT_OK)
+            return s2;
+        p->lvl_cap = entries;
+        return SRT_OK;
+    };
+    const bool first = !p->lvl_cap;
+    if (first && p->lvl_est && (st = size_arrays(p->lvl_est)) != SRT_OK) return st;
+    out_pass();
+    if (first) {
+        hipError_t e = hipMemcpyAsync(p->h_tcount, p->d_tcursor, sizeof(uint64_t), hipMemcpyDeviceToHost, M);
+        if (e == hipSuccess) e = hipStreamSynchronize(M);
+        if (e != hipSuccess) return fail(err, e, "level edge count");
+        const uint64_t count = std::max<uint64_t>(p->h_tcount[0], 1);
+        if (count > p->lvl_cap) {
+            if ((st = size_arrays(count)) != SRT_OK) return st;
+            out_pass();
+        }
+        p->lvl_cap = count;
     }
     size_t need = 0;
     hipError_t e = rocprim::exclusive_scan(nullptr, need, p->d_tccnt, p->d_tcls + vc1, 0u, (size_t)vc1,
@@ -2989,6 +3008,12 @@ srt_status level_probe(srt_plan *p, uint64_t wmax, uint64_t *bound, uint64_t *vi
     *visits = 0;
     if (!p->n) return SRT_OK;
     p->lvl_cap = 0;  // a new bound: count and size the entry arrays again
+    // the estimate: latencies spread evenly up to the longest edge, twice over
+    {
+        const uint64_t maxu = p->lvl_maxu ? p->lvl_maxu : wmax;
+        const double f = std::min(1.0, 2.0 * (double)wmax / (double)std::max<uint64_t>(maxu, 1));
+        p->lvl_est = (uint64_t)((double)p->n_adj * f) + 65536;
+    }
     srt_status st = level_csr(p, wmax, false, err);
     if (st != SRT_OK) return st;
     const uint32_t K = std::min<uint32_t>(8, p->n);
@@ -3107,6 +3132,19 @@ void level_solve_stage(const LevelCtx &c, uint32_t r0, uint32_t r1, uint32_t lma
 
 size_t level_scratch_bytes(int device, uint32_t V, bool quant) {
     return quant ? (size_t)level_grid(device, V, true, ~0u, nullptr) * V * 2 : 0;
+}
+
+void level_loss_index(srt_plan *p, uint32_t *d_idx, uint64_t cap, unsigned long long *d_cnt, hipStream_t s) {
+    const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(8192, (p->V + 3) / 4));
+    (void)hipMemsetAsync(d_cnt, 0, sizeof *d_cnt, s);
+    hipLaunchKernelGGL(lvl_index_kernel, dim3(blocks), dim3(256), 0, s, p->V, p->d_row_ptr, p->d_col, p->d_lat,
+                       p->kp.lmax * p->kp.g, d_idx, cap, d_cnt);
+}
+
+void loss_scatter(const uint32_t *d_idx, const float *d_val, uint64_t count, float *d_loss, hipStream_t s) {
+    if (count)
+        hipLaunchKernelGGL(loss_scatter_kernel, dim3((uint32_t)std::min<uint64_t>(4096, (count + 255) / 256)),
+                           dim3(256), 0, s, d_idx, d_val, count, d_loss);
 }
 
 // The shortest non-self-loop edge of the plan's graph, ns (~0: none)

@@ -341,3 +341,46 @@ def test_level_shard_rows_no_exchange(quant):
         assert e.value.code == _lib.SRT_ERR_UNSUPPORTED
     finally:
         fw.close()
+
+
+def test_level_one_call_uploads_needed_losses(monkeypatch):
+    """One-call builds of a level plan upload only the losses the class CSRs
+    read (indices listed on the device, gathered on the host) and range-check
+    every loss on host threads: a bad loss on an edge the solve never reads is
+    still the reference's parse-time error; the tables equal the full-upload
+    path's (SRT_LOSS_FULL=1) and the oracle's rows."""
+    err = _lib.SrtErr()
+    assert _lib.lib().srt_init(0, err) == 0  # pins the staging the upload uses
+    n = 4200
+    row_ptr, col, lat, loss = synth.complete_csr(n, 31)
+    loss = loss.copy()
+    far = int(np.argmax(lat[: n]))  # row 0's longest edge: never on a shortest path
+    assert lat[far] > 100 * synth.MS
+    keep = loss[far]
+    loss[far] = np.float32(1.5)
+    g = NetworkGraph(n, np.arange(n, dtype=np.uint32), row_ptr, col, lat, loss, directed=False)
+    with pytest.raises(_lib.SrtError) as e:
+        RoutingInfo.build(g, np.arange(n, dtype=np.uint32))
+    assert str(e.value) == "Edge 'packet_loss' is not in the range [0,1]"
+    loss[far] = keep
+    g = NetworkGraph(n, np.arange(n, dtype=np.uint32), row_ptr, col, lat, loss, directed=False)
+    nodes = np.random.default_rng(31).permutation(n).astype(np.uint32)
+    a = RoutingInfo.build(g, nodes, device=0)
+    monkeypatch.setenv("SRT_LOSS_FULL", "1")
+    b = RoutingInfo.build(g, nodes, device=0)
+    try:
+        la, pa = a.table()
+        lb, pb = b.table()
+        assert np.array_equal(la, lb) and np.array_equal(_bits(pa), _bits(pb))
+        src, dst, l2, p2 = synth.complete_graph(n, 31)
+        rows = np.arange(5)
+        order = np.concatenate([nodes[rows], np.setdiff1d(nodes, nodes[rows])]).astype(np.uint32)
+        elat, eloss = O.compute_shortest_paths(O.Graph(False, np.arange(n), src, dst, l2, p2), order, src_count=5)
+        pos = {int(v): i for i, v in enumerate(order)}
+        inv = np.array([pos[int(v)] for v in nodes])
+        for r in rows:
+            m = np.arange(n) != r
+            assert np.array_equal(la[r][m], elat[r][inv][m]) and np.array_equal(_bits(pa[r][m]), _bits(eloss[r][inv][m]))
+    finally:
+        a.close()
+        b.close()

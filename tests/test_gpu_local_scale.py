@@ -162,3 +162,28 @@ def test_c3_16k_routing_info_in_process_ranks(c3, world):
     finally:
         multi.close()
         single.close()
+
+
+def test_level_two_distinct_devices():
+    """The in-process level build across two physical devices (peer copies of
+    the class CSRs over xGMI, one solve and one PCIe download per device):
+    equal to the one-GPU RoutingInfo.  Skipped on a one-GPU box -- the
+    cross-device path is unverified until a multi-GPU lease runs it."""
+    from shadow_amd import RoutingInfo
+
+    if _lib.lib().srt_device_count() < 2:
+        pytest.skip("needs two visible devices")
+    n = 3000
+    src, dst, lat, loss = synth.complete_graph(n, 12)
+    g = NetworkGraph.from_edges(n, src, dst, lat, loss)
+    nodes = np.random.default_rng(12).permutation(n).astype(np.uint32)
+    multi = RoutingInfo.build(g, nodes, device=0, n_gpus=2)
+    single = RoutingInfo.build(g, nodes, device=0)
+    try:
+        ml, mp = multi.table()
+        sl, sp = single.table()
+        assert np.array_equal(ml, sl) and np.array_equal(mp.view(np.uint32), sp.view(np.uint32))
+        assert multi.get_smallest_latency_ns() == single.get_smallest_latency_ns()
+    finally:
+        multi.close()
+        single.close()
