@@ -197,6 +197,21 @@ def measured_traffic(args, kernel_tag, schedule):
     return None, None
 
 
+def packet_traffic():
+    """HBM bytes of one C5 round's draw + decide kernels from the newest
+    committed C5 PMC summary (one dispatch of each a round), or None."""
+    import glob
+    for f in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))):
+        d = json.load(open(f))
+        if not d.get("config", "").startswith("C5 "):
+            continue
+        tot = sum(v["hbm_bytes_per_launch"] for k, v in d.get("kernels", {}).items()
+                  if k.startswith(("draw_kernel", "decide_kernel")))
+        if tot:
+            return tot, os.path.relpath(f, ROOT)
+    return None, None
+
+
 def frontier_traffic(args, schedule, launches):
     """HBM bytes per launch of the frontier path: every fr_* kernel's bytes per
     dispatch x its dispatches, over the run's launches, from the newest committed
@@ -765,6 +780,7 @@ def bench_packets(args, cfg, D):
     if D.rank == 0:
         per_round = elapsed / args.steps
         bytes_per_round = n_pkts * 52 + hosts * 64
+        traffic, traffic_src = packet_traffic()
         cpu = None
         if args.cpu_baseline and D.world == 1:
             table = plan.fetch()
@@ -790,7 +806,11 @@ def bench_packets(args, cfg, D):
                        "packets": n_pkts, "hosts": hosts, "parallelism": "replicas"},
             "roofline": {"bound": "hbm", "achieved": bytes_per_round / (dev_ms / 1e3) / 1e9,
                          "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                         "frac": bytes_per_round / (dev_ms / 1e3) / HBM_PEAK, "traffic": None,
+                         "frac": bytes_per_round / (dev_ms / 1e3) / HBM_PEAK, "traffic": traffic,
+                         "traffic_unit": "HBM bytes per round (FETCH_SIZE + WRITE_SIZE of draw_kernel + decide_kernel)",
+                         "traffic_source": (f"{traffic_src}: committed rocprofv3 PMC summary of this workload, not "
+                                            f"measured in this run" if traffic_src else
+                                            "no committed PMC summary for this workload"),
                          "kernel": "draw_kernel + decide_kernel (one round)", "device_ms_per_round": dev_ms,
                          "basis": "52 B/packet + 64 B/host (SURVEY.md 8(d))"},
             "cpu_baseline": cpu,
