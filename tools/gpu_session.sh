@@ -1,9 +1,7 @@
 #!/bin/bash
-# one GPU session of round-5 work (edited per session): bench lines with the committed PMC traffic
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out/r05lines
-for c in c3 c2 c2nc c3ns c5 c4; do
-  timeout -k 10 400 python3 -u bench.py --config $c --steps 10 --warmup 2 > gpurun_out/r05lines/$c.json 2> gpurun_out/r05lines/$c.err || { echo "bench $c failed"; tail -5 gpurun_out/r05lines/$c.err; exit 1; }
-  python3 -c "import json; d=json.loads(open('gpurun_out/r05lines/$c.json').read().strip().splitlines()[-1]); r=d.get('roofline') or {}; print('$c', d['value'], d['ms_per_step'], r.get('frac'), r.get('traffic'))"
-done
+mkdir -p gpurun_out/s25
+SRT_TRACE=1 timeout -k 10 300 python3 -u tools/multi_emulate.py 1 2 4 8 > gpurun_out/s25/emu.json 2> gpurun_out/s25/emu.err || { echo "emulate failed"; tail -5 gpurun_out/s25/emu.err; exit 1; }
+cat gpurun_out/s25/emu.json | cut -c1-200
+grep "multi:" gpurun_out/s25/emu.err | tail -6
