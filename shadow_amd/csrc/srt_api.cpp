@@ -1063,6 +1063,20 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         p->kp.lat32 = true;
         p->key_type = p->lvl_q ? srt::KEY_U32 : srt::KEY_U16;
         f16 = false;
+        // complete graphs in identity rows whose pairs <= B mirror exactly
+        // (latency here; the losses too when they are on the device, else the
+        // one-call build checks the losses it gathers): no class in-rows
+        const char *ks = std::getenv("SRT_LVL_SYM");  // knob: 0 = always build the in-rows (A/B, tests)
+        if (cs.complete && !(ks && std::atoi(ks) == 0)) {
+            srt_err e2{};
+            bool sym = false;
+            if (srt::level_sym_check(p, lvl_bound, p->h_loss_defer == nullptr, &sym, &e2) != SRT_OK) {
+                srt_plan_destroy(p);
+                if (err) *err = e2;
+                return SRT_ERR_HIP;
+            }
+            p->lvl_sym = sym;
+        }
     } else {
         p->lvl_q = 0;
     }
@@ -1079,13 +1093,13 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     char d[200];
     if (algo == SRT_ALGO_LEVEL) {
         if (p->lvl_q)
-            std::snprintf(d, sizeof d, "level:u32 g=%llu q=%u lmax=%llu(probe) V=%u n=%u visits=%llu loss=in-solve",
+            std::snprintf(d, sizeof d, "level:u32 g=%llu q=%u lmax=%llu(probe) V=%u n=%u visits=%llu loss=in-solve%s",
                           (unsigned long long)p->kp.g, p->lvl_q, (unsigned long long)p->kp.lmax, p->V, n,
-                          (unsigned long long)lvl_visits);
+                          (unsigned long long)lvl_visits, p->lvl_sym ? " rows=sym" : "");
         else
-            std::snprintf(d, sizeof d, "level:u16 g=%llu lmax=%llu(probe) V=%u n=%u visits=%llu loss=in-solve",
+            std::snprintf(d, sizeof d, "level:u16 g=%llu lmax=%llu(probe) V=%u n=%u visits=%llu loss=in-solve%s",
                           (unsigned long long)p->kp.g, (unsigned long long)p->kp.lmax, p->V, n,
-                          (unsigned long long)lvl_visits);
+                          (unsigned long long)lvl_visits, p->lvl_sym ? " rows=sym" : "");
     } else if (algo == SRT_ALGO_FW) {
         p->fw_f16 = f16 && p->fw_glds;
         if (const char *e = std::getenv("SRT_FW_P1")) p->fw_p1 = std::atoi(e);
@@ -1450,14 +1464,29 @@ bool upload_level_losses(srt_plan *p, srt_err *err, srt_status *st) {
     if (e == hipSuccess) e = hipStreamSynchronize(M);
     if (e != hipSuccess) return fail(e, "loss indices");
     {
+        // symmetric plans (identity rows, latencies checked at create): every
+        // needed entry's mirror must carry the same loss bits, else the run
+        // builds its in-rows after all
         const int T = host_threads(cnt * 16);
+        const bool chk = p->lvl_sym;
+        const uint64_t V = p->V;
+        const uint32_t *sb = reinterpret_cast<const uint32_t *>(src);
+        std::vector<uint8_t> asym(T, 0);
         std::vector<std::thread> pool;
         auto part = [&](int t) {
-            for (uint64_t i = cnt * t / T; i < cnt * (t + 1) / T; ++i) hval[i] = src[hidx[i]];
+            uint8_t a = 0;
+            for (uint64_t i = cnt * t / T; i < cnt * (t + 1) / T; ++i) {
+                const uint64_t k = hidx[i];
+                hval[i] = src[k];
+                if (chk) a |= sb[k] != sb[(k % V) * V + k / V];
+            }
+            asym[t] = a;
         };
         for (int t = 1; t < T; ++t) pool.emplace_back(part, t);
         part(0);
         for (auto &th : pool) th.join();
+        for (uint8_t a : asym)
+            if (a) p->lvl_sym = false;
     }
     e = hipMemcpyAsync(d_val, hval, cnt * 4, hipMemcpyHostToDevice, M);
     if (e != hipSuccess) return fail(e, "upload (needed losses)");
@@ -1481,6 +1510,7 @@ srt_status upload_deferred_loss(srt_plan *p, srt_err *err) {
     if (p->h_loss_defer) {
         srt_status st;
         if (upload_level_losses(p, err, &st)) return st;
+        p->lvl_sym = false;  // the losses' mirrors were not checked: build the in-rows
     }
     if (p->h_loss_defer) {
         hipStream_t up = p->comm ? p->stream : p->comm_stream;
@@ -2219,14 +2249,15 @@ srt_status build_multi_level(srt_plan *p0, const std::vector<int32_t> &devs, srt
         if (e == hipSuccess && devs[r] != devs[0]) {
             // the solve's inputs from rank 0's device
             uint32_t *tcls = (uint32_t *)dev_alloc(2 * vc1 * 4);
-            uint64_t *eo = (uint64_t *)dev_alloc(ents * 8), *ei = (uint64_t *)dev_alloc(ents * 8);
+            const bool alias = c0.ce_in == c0.ce_out;  // symmetric plan: one entry array
+            uint64_t *eo = (uint64_t *)dev_alloc(ents * 8), *ei = alias ? eo : (uint64_t *)dev_alloc(ents * 8);
             uint32_t *nd = (uint32_t *)dev_alloc((size_t)n * 4);
             uint64_t *sl = (uint64_t *)dev_alloc((size_t)n * 8);
             float *sp = (float *)dev_alloc((size_t)n * 4);
             if (!tcls || !eo || !ei || !nd || !sl || !sp) e = hipErrorOutOfMemory;
             if (e == hipSuccess) e = hipMemcpyPeerAsync(tcls, devs[r], c0.tcls, devs[0], 2 * vc1 * 4, st);
             if (e == hipSuccess) e = hipMemcpyPeerAsync(eo, devs[r], c0.ce_out, devs[0], ents * 8, st);
-            if (e == hipSuccess) e = hipMemcpyPeerAsync(ei, devs[r], c0.ce_in, devs[0], ents * 8, st);
+            if (e == hipSuccess && !alias) e = hipMemcpyPeerAsync(ei, devs[r], c0.ce_in, devs[0], ents * 8, st);
             if (e == hipSuccess) e = hipMemcpyPeerAsync(nd, devs[r], c0.nodes, devs[0], (size_t)n * 4, st);
             if (e == hipSuccess) e = hipMemcpyPeerAsync(sl, devs[r], c0.sl_lat, devs[0], (size_t)n * 8, st);
             if (e == hipSuccess) e = hipMemcpyPeerAsync(sp, devs[r], c0.sl_loss, devs[0], (size_t)n * 4, st);

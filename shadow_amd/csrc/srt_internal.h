@@ -287,6 +287,7 @@ struct srt_plan {
     uint32_t t_cls = 16;             // class offsets per vertex of the level fold's CSRs (16 or 32)
     uint32_t *d_tcw = nullptr;       // quantized fold: each class entry's exact weight (out, then in), t_cap each
     uint64_t lvl_cap = 0;            // level solve: class entries d_tpk / d_tpk2 hold (the probe's count)
+    bool lvl_sym = false;            // level solve: the class in-rows are the out-rows (lvl_sym_tile_kernel)
     uint64_t lvl_est = 0;            // the probe's entry-count estimate (sizes the arrays before its one pass)
     uint64_t lvl_maxu = 0;           // the longest edge, units of g (the estimate's scale)
     unsigned long long *d_lvisit = nullptr;  // level solve: class entries the last run walked
@@ -443,6 +444,10 @@ size_t level_scratch_bytes(int device, uint32_t V, bool quant);
 uint32_t level_vbits(uint32_t V);
 // the shortest non-self-loop edge latency of the plan's uploaded graph, ns
 srt_status level_min_edge(srt_plan *p, uint64_t *min_ns, srt_err *err);
+// *sym = the adjacency is V x V identity rows whose pairs of latency <= wmax
+// units mirror each other exactly (and their losses when with_loss: d_loss
+// uploaded) -- a level plan then builds no in-rows
+srt_status level_sym_check(srt_plan *p, uint64_t wmax_units, bool with_loss, bool *sym, srt_err *err);
 // the adjacency indices (u32) of the entries a level plan's class CSRs read
 // (latency <= kp.lmax units, not a self-loop) into d_idx (cap entries), their
 // count into *d_cnt; and the scatter of gathered losses into d_loss

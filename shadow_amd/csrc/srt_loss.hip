@@ -288,7 +288,7 @@ __global__ __launch_bounds__(256) void tight_rows_kernel(const K *__restrict__ D
 // (v, class).  No global atomic per entry on the out side, where a row's ~50
 // entries of a class would all hit one counter.  Entries past `cap` are
 // counted, not written (the caller sizes and runs again).
-template <bool WITH_LOSS>
+template <bool WITH_LOSS, bool IN = true>
 __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t V, const uint64_t *__restrict__ row_ptr,
                                                       const uint32_t *__restrict__ col,
                                                       const uint64_t *__restrict__ lat, const float *__restrict__ loss,
@@ -367,7 +367,7 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t V, const uint64_t
                 // along, (1 - e) in bits 34.. (a loss in [0, 1]: its bits are < 2^30)
                 ce_out[pos] = q ? ((uint64_t)__float_as_uint(eb) << 34) | ((wu - (uint64_t)cl * q) << vb) | v
                                 : ((uint64_t)__float_as_uint(eb) << 32) | v;
-                atomicAdd(&in_cnt[(uint64_t)v * cls + cl - 1], 1u);
+                if (IN) atomicAdd(&in_cnt[(uint64_t)v * cls + cl - 1], 1u);  // symmetric plans: no in-rows
             }
         }
     }
@@ -403,6 +403,52 @@ __global__ __launch_bounds__(256) void lvl_in_kernel(uint32_t V, uint32_t cls, u
             ce_in[pos] = (w & ~vmask) | u;
         }
     }
+}
+
+// Exact check that a level plan's class in-rows equal its out-rows, so the
+// run builds only the out-rows (lvl_sym): every adjacency row u is exactly the
+// columns 0 .. V-1 in order (complete graphs as Shadow writes them, self-loop
+// included), and every pair of latency <= wmax_ns has its mirror with the same
+// latency (and, loss != nullptr, the same loss bits) -- then the class-c
+// in-entries of x are the class-c out-entries of x, entry for entry.  64 x 64
+// tiles (i <= j) and their mirrors through LDS; any difference clears *ok.
+__global__ __launch_bounds__(256) void lvl_sym_tile_kernel(uint32_t V, const uint64_t *__restrict__ row_ptr,
+                                                           const uint32_t *__restrict__ col,
+                                                           const uint64_t *__restrict__ lat,
+                                                           const float *__restrict__ loss, uint64_t wmax_ns,
+                                                           uint32_t *ok) {
+    __shared__ uint64_t tl[64][65];
+    __shared__ uint32_t tp[64][65];
+    const uint32_t nb = (V + 63) / 64, tid = threadIdx.x;
+    bool bad = false;
+    for (uint64_t t = blockIdx.x; t < (uint64_t)nb * nb; t += gridDim.x) {
+        const uint32_t bi = (uint32_t)(t / nb), bj = (uint32_t)(t % nb);
+        if (bi > bj) continue;  // uniform
+        // tile (bj, bi) staged, then compared with tile (bi, bj) transposed
+        for (uint32_t e = tid; e < 64 * 64; e += 256) {
+            const uint32_t r = e / 64, c = e % 64, u = bj * 64 + r, v = bi * 64 + c;
+            if (u < V && v < V) {
+                const uint64_t k = (uint64_t)u * V + v;
+                tl[r][c] = lat[k];
+                tp[r][c] = loss ? __float_as_uint(loss[k]) : 0u;
+                bad |= row_ptr[u] != (uint64_t)u * V || col[k] != v;
+            }
+        }
+        __syncthreads();
+        for (uint32_t e = tid; e < 64 * 64; e += 256) {
+            const uint32_t r = e / 64, c = e % 64, u = bi * 64 + r, v = bj * 64 + c;
+            if (u < V && v < V) {
+                const uint64_t k = (uint64_t)u * V + v;
+                const uint64_t l = lat[k];
+                bad |= row_ptr[u] != (uint64_t)u * V || col[k] != v;
+                const uint64_t lm = tl[c][r];
+                if (u != v && (l <= wmax_ns || lm <= wmax_ns))
+                    bad |= l != lm || (loss && __float_as_uint(loss[k]) != tp[c][r]);
+            }
+        }
+        __syncthreads();
+    }
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicAnd(ok, 0u);
 }
 
 // The adjacency indices of the entries a level plan's class CSRs read
@@ -2798,7 +2844,7 @@ LevelCtx level_ctx(srt_plan *p) {
     c.t_cls = p->t_cls;
     c.tcls = p->d_tcls;
     c.ce_out = p->d_tpk;
-    c.ce_in = p->d_tpk2;
+    c.ce_in = p->lvl_sym ? p->d_tpk : p->d_tpk2;
     c.nodes = p->d_nodes;
     c.sl_lat = p->d_sl_lat;
     c.sl_loss = p->d_sl_loss;
@@ -2852,7 +2898,11 @@ srt_status level_csr(srt_plan *p, uint64_t wmax, bool with_loss, srt_err *err) {
         (void)hipMemsetAsync(p->d_tccnt, 0, 2 * vc1 * 4, M);  // in-row counts, then in-row cursors
         (void)hipMemsetAsync(p->d_tcursor, 0, sizeof(unsigned long long), M);
         (void)hipMemsetAsync(p->d_tmaxw, 0, sizeof(unsigned long long), M);
-        if (with_loss)
+        if (with_loss && p->lvl_sym)
+            hipLaunchKernelGGL((lvl_out_kernel<true, false>), dim3(blocks), dim3(256), 0, M, V, p->d_row_ptr, p->d_col,
+                               p->d_lat, p->d_loss, p->kp.g, inv_g, wns, cls, q, vb, p->d_tcls, p->d_tccnt,
+                               p->d_tpk, p->lvl_cap, p->d_tcursor, (unsigned long long *)p->d_tmaxw);
+        else if (with_loss)
             hipLaunchKernelGGL(lvl_out_kernel<true>, dim3(blocks), dim3(256), 0, M, V, p->d_row_ptr, p->d_col,
                                p->d_lat, p->d_loss, p->kp.g, inv_g, wns, cls, q, vb, p->d_tcls, p->d_tccnt,
                                p->d_tpk, p->lvl_cap, p->d_tcursor, (unsigned long long *)p->d_tmaxw);
@@ -2892,6 +2942,18 @@ srt_status level_csr(srt_plan *p, uint64_t wmax, bool with_loss, srt_err *err) {
             out_pass();
         }
         p->lvl_cap = count;
+    }
+    if (with_loss && p->lvl_sym) {
+        // symmetric plan (lvl_sym_tile_kernel): the in-rows are the out-rows;
+        // their offsets copied, the entries read through the same array
+        // (level_ctx)
+        const hipError_t e = hipMemcpyAsync(p->d_tcls + vc1, p->d_tcls, vc1 * 4, hipMemcpyDeviceToDevice, M);
+        if (e != hipSuccess) return fail(err, e, "class offsets (symmetric)");
+        p->t_cls = cls;
+        p->t_q = 1;
+        p->t_level = true;
+        p->t_edges = p->lvl_cap;
+        return SRT_OK;
     }
     size_t need = 0;
     hipError_t e = rocprim::exclusive_scan(nullptr, need, p->d_tccnt, p->d_tcls + vc1, 0u, (size_t)vc1,
@@ -3145,6 +3207,28 @@ void loss_scatter(const uint32_t *d_idx, const float *d_val, uint64_t count, flo
     if (count)
         hipLaunchKernelGGL(loss_scatter_kernel, dim3((uint32_t)std::min<uint64_t>(4096, (count + 255) / 256)),
                            dim3(256), 0, s, d_idx, d_val, count, d_loss);
+}
+
+srt_status level_sym_check(srt_plan *p, uint64_t wmax_units, bool with_loss, bool *sym, srt_err *err) {
+    *sym = false;
+    if (!p->V || p->n_adj != (uint64_t)p->V * p->V) return SRT_OK;
+    uint32_t *d_ok = nullptr;
+    hipError_t e = hipMalloc(&d_ok, 4);
+    if (e != hipSuccess) return fail(err, e, "hipMalloc(symmetry flag)");
+    uint32_t one = 1;
+    e = hipMemcpyAsync(d_ok, &one, 4, hipMemcpyHostToDevice, p->stream);
+    const uint64_t nb = (p->V + 63) / 64;
+    if (e == hipSuccess)
+        hipLaunchKernelGGL(lvl_sym_tile_kernel, dim3((uint32_t)std::min<uint64_t>(nb * nb, 8192)), dim3(256), 0,
+                           p->stream, p->V, p->d_row_ptr, p->d_col, p->d_lat, with_loss ? p->d_loss : nullptr,
+                           wmax_units * p->kp.g, d_ok);
+    uint32_t ok = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&ok, d_ok, 4, hipMemcpyDeviceToHost, p->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
+    (void)hipFree(d_ok);
+    if (e != hipSuccess) return fail(err, e, "symmetry check");
+    *sym = ok != 0;
+    return SRT_OK;
 }
 
 // The shortest non-self-loop edge of the plan's graph, ns (~0: none)

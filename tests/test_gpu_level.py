@@ -384,3 +384,48 @@ def test_level_one_call_uploads_needed_losses(monkeypatch):
     finally:
         a.close()
         b.close()
+
+
+@pytest.mark.parametrize("ns", [False, True])
+def test_level_symmetric_rows(monkeypatch, ns):
+    """Complete graphs in identity rows whose pairs mirror exactly build only
+    the class out-rows (the in-rows are the same entries: 'rows=sym'); the
+    tables equal the two-CSR build's (SRT_LVL_SYM=0) bit for bit, and a
+    directed complete graph (different latency each way) keeps both CSRs."""
+    import torch
+
+    n = 2000
+    edges = synth.complete_graph_ns(n, 41) if ns else synth.complete_graph(n, 41)
+    row_ptr, col, lat, loss = synth.complete_csr(n, 41, edges=edges)
+    g = NetworkGraph(n, np.arange(n, dtype=np.uint32), row_ptr, col, lat, loss, directed=False)
+    nodes = np.random.default_rng(41).permutation(n).astype(np.uint32)
+    a = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_LEVEL, device=0).run()
+    monkeypatch.setenv("SRT_LVL_SYM", "0")
+    b = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_LEVEL, device=0).run()
+    monkeypatch.delenv("SRT_LVL_SYM")
+    try:
+        assert "rows=sym" in a.describe() and "rows=sym" not in b.describe(), (a.describe(), b.describe())
+        dev = torch.device("cuda", 0)
+        t = lambda ptr, nb: torch.as_tensor(sdist._CudaBuf(ptr, nb), device=dev)
+        la, pa, _ = a.table_ptrs()
+        lb, pb, _ = b.table_ptrs()
+        assert torch.equal(t(la, n * n * 8), t(lb, n * n * 8)) and torch.equal(t(pa, n * n * 4), t(pb, n * n * 4))
+        _check(a.fetch(), O.Graph(False, np.arange(n), *edges), nodes)
+    finally:
+        a.close()
+        b.close()
+    # directed complete graph: row u's latencies differ from column u's
+    rng = np.random.default_rng(42)
+    lat2 = lat.copy().reshape(n, n)
+    lat2 += (rng.integers(0, 3, size=(n, n)).astype(np.uint64) * np.uint64(synth.MS))
+    np.fill_diagonal(lat2, lat.reshape(n, n).diagonal())
+    lat2 = lat2.reshape(-1)
+    g2 = NetworkGraph(n, np.arange(n, dtype=np.uint32), row_ptr, col, lat2, loss, directed=True)
+    c = RoutingPlan(g2, nodes, device=0).run()
+    try:
+        assert c.describe().startswith("level:") and "rows=sym" not in c.describe(), c.describe()
+        src = np.repeat(np.arange(n, dtype=np.uint32), n)
+        dst = np.tile(np.arange(n, dtype=np.uint32), n)
+        _check(c.fetch(), O.Graph(True, np.arange(n), src, dst, lat2, loss), nodes)
+    finally:
+        c.close()
