@@ -993,6 +993,16 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
                 if (err) *err = e2;
                 return e2.code ? (srt_status)e2.code : SRT_ERR_HIP;
             };
+            // complete graphs in identity rows whose pairs mirror exactly (the
+            // latencies here, over every pair; the losses too when they are on
+            // the device, else the one-call build checks the losses it
+            // gathers): one class CSR, the in-rows being the out-rows
+            const char *ks = std::getenv("SRT_LVL_SYM");  // knob: 0 = always build the in-rows (A/B, tests)
+            if (cs.complete && !(ks && std::atoi(ks) == 0)) {
+                bool sym = false;
+                if (srt::level_sym_check(p, maxu, !defer_loss, &sym, &e2) != SRT_OK) return probe_fail();
+                p->lvl_sym_lat = p->lvl_sym = sym;
+            }
             if (srt::level_probe(p, std::min<uint64_t>(31, maxu), &lvl_bound, &lvl_visits, &e2) != SRT_OK)
                 return probe_fail();
             // no bound within 31 units: the quantized solve, buckets of q <= the
@@ -1063,22 +1073,10 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         p->kp.lat32 = true;
         p->key_type = p->lvl_q ? srt::KEY_U32 : srt::KEY_U16;
         f16 = false;
-        // complete graphs in identity rows whose pairs <= B mirror exactly
-        // (latency here; the losses too when they are on the device, else the
-        // one-call build checks the losses it gathers): no class in-rows
-        const char *ks = std::getenv("SRT_LVL_SYM");  // knob: 0 = always build the in-rows (A/B, tests)
-        if (cs.complete && !(ks && std::atoi(ks) == 0)) {
-            srt_err e2{};
-            bool sym = false;
-            if (srt::level_sym_check(p, lvl_bound, p->h_loss_defer == nullptr, &sym, &e2) != SRT_OK) {
-                srt_plan_destroy(p);
-                if (err) *err = e2;
-                return SRT_ERR_HIP;
-            }
-            p->lvl_sym = sym;
-        }
+
     } else {
         p->lvl_q = 0;
+        p->lvl_sym = p->lvl_sym_lat = false;
     }
     // SSSP plans read their in-edges (with loss) from the host-built list, never
     // d_loss: drop the deferred upload so run_tail does not copy it
@@ -1422,7 +1420,7 @@ bool upload_level_losses(srt_plan *p, srt_err *err, srt_status *st) {
     if (!p->d_lidx || p->lidx_cap < cap) {
         (void)hipFree(p->d_lidx);
         p->d_lidx = nullptr;
-        e = hipMalloc(&p->d_lidx, cap * 8 + 16);
+        e = hipMalloc(&p->d_lidx, cap * 8 + 32);
         if (e != hipSuccess) return fail(e, "hipMalloc(loss indices)");
         p->lidx_cap = cap;
     }
@@ -1464,36 +1462,31 @@ bool upload_level_losses(srt_plan *p, srt_err *err, srt_status *st) {
     if (e == hipSuccess) e = hipStreamSynchronize(M);
     if (e != hipSuccess) return fail(e, "loss indices");
     {
-        // symmetric plans (identity rows, latencies checked at create): every
-        // needed entry's mirror must carry the same loss bits, else the run
-        // builds its in-rows after all
         const int T = host_threads(cnt * 16);
-        const bool chk = p->lvl_sym;
-        const uint64_t V = p->V;
-        const uint32_t *sb = reinterpret_cast<const uint32_t *>(src);
-        std::vector<uint8_t> asym(T, 0);
         std::vector<std::thread> pool;
         auto part = [&](int t) {
-            uint8_t a = 0;
-            for (uint64_t i = cnt * t / T; i < cnt * (t + 1) / T; ++i) {
-                const uint64_t k = hidx[i];
-                hval[i] = src[k];
-                if (chk) a |= sb[k] != sb[(k % V) * V + k / V];
-            }
-            asym[t] = a;
+            for (uint64_t i = cnt * t / T; i < cnt * (t + 1) / T; ++i) hval[i] = src[hidx[i]];
         };
         for (int t = 1; t < T; ++t) pool.emplace_back(part, t);
         part(0);
         for (auto &th : pool) th.join();
-        for (uint8_t a : asym)
-            if (a) p->lvl_sym = false;
     }
     e = hipMemcpyAsync(d_val, hval, cnt * 4, hipMemcpyHostToDevice, M);
     if (e != hipSuccess) return fail(e, "upload (needed losses)");
     srt::loss_scatter(d_idx, d_val, cnt, p->d_loss, M);
+    // symmetric plans (identity rows, latencies checked at create): every
+    // uploaded loss must equal its mirror's, else the run builds its in-rows
+    uint32_t *d_ok = reinterpret_cast<uint32_t *>(d_cnt + 1);
+    if (p->lvl_sym) {
+        h[0] = 1;
+        e = hipMemcpyAsync(d_ok, h, 4, hipMemcpyHostToDevice, M);
+        if (e == hipSuccess) srt::loss_mirror_check(d_idx, cnt, p->V, p->d_loss, d_ok, M);
+        if (e == hipSuccess) e = hipMemcpyAsync(h, d_ok, 4, hipMemcpyDeviceToHost, M);
+    }
     // the staging is reused by the download: the upload must be done first
-    e = hipStreamSynchronize(M);
+    if (e == hipSuccess) e = hipStreamSynchronize(M);
     if (e != hipSuccess) return fail(e, "upload (needed losses)");
+    if (p->lvl_sym && reinterpret_cast<uint32_t *>(h)[0] == 0) p->lvl_sym = false;
     p->h_loss_defer = nullptr;
     return true;
 }

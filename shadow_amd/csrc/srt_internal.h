@@ -287,7 +287,9 @@ struct srt_plan {
     uint32_t t_cls = 16;             // class offsets per vertex of the level fold's CSRs (16 or 32)
     uint32_t *d_tcw = nullptr;       // quantized fold: each class entry's exact weight (out, then in), t_cap each
     uint64_t lvl_cap = 0;            // level solve: class entries d_tpk / d_tpk2 hold (the probe's count)
-    bool lvl_sym = false;            // level solve: the class in-rows are the out-rows (lvl_sym_tile_kernel)
+    bool lvl_sym_lat = false;        // level solve: identity rows, mirrored latencies (lvl_sym_tile_kernel)
+    bool lvl_sym = false;            // ... and mirrored losses: the class in-rows are the out-rows
+    bool lvl_single = false;         // the last class-CSR build made out-rows only (in-rows = out-rows)
     uint64_t lvl_est = 0;            // the probe's entry-count estimate (sizes the arrays before its one pass)
     uint64_t lvl_maxu = 0;           // the longest edge, units of g (the estimate's scale)
     unsigned long long *d_lvisit = nullptr;  // level solve: class entries the last run walked
@@ -453,6 +455,9 @@ srt_status level_sym_check(srt_plan *p, uint64_t wmax_units, bool with_loss, boo
 // count into *d_cnt; and the scatter of gathered losses into d_loss
 void level_loss_index(srt_plan *p, uint32_t *d_idx, uint64_t cap, unsigned long long *d_cnt, hipStream_t s);
 void loss_scatter(const uint32_t *d_idx, const float *d_val, uint64_t count, float *d_loss, hipStream_t s);
+// *d_ok cleared when an uploaded loss (identity rows) differs from its mirror's
+void loss_mirror_check(const uint32_t *d_idx, uint64_t count, uint64_t V, const float *d_loss, uint32_t *d_ok,
+                       hipStream_t s);
 // d_stats = (~0, 0) on stream s
 void level_stats_init(unsigned long long *d_stats, hipStream_t s);
 // sharded tail: every rank's staged rows (d_slat / d_sloss, all-gathered) into the table

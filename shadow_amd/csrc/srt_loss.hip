@@ -288,7 +288,7 @@ __global__ __launch_bounds__(256) void tight_rows_kernel(const K *__restrict__ D
 // (v, class).  No global atomic per entry on the out side, where a row's ~50
 // entries of a class would all hit one counter.  Entries past `cap` are
 // counted, not written (the caller sizes and runs again).
-template <bool WITH_LOSS, bool IN = true>
+template <bool WITH_LOSS, bool IN = true, bool IDENT = false>
 __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t V, const uint64_t *__restrict__ row_ptr,
                                                       const uint32_t *__restrict__ col,
                                                       const uint64_t *__restrict__ lat, const float *__restrict__ loss,
@@ -298,6 +298,7 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t V, const uint64_t
                                                       uint64_t *__restrict__ ce_out, uint64_t cap,
                                                       unsigned long long *cursor, unsigned long long *maxw) {
     __shared__ uint64_t bal[4][TR_CH];
+    __shared__ uint16_t pre[4][TR_CH];  // per wave: the row's hits before chunk c
     __shared__ uint32_t ccnt[4][32];  // per wave: hits per class (pass 1), running positions (pass 2)
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -321,14 +322,19 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t V, const uint64_t
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const uint64_t k = b + 64ull * (c0 + q) + lane;
-                const bool f = l[q] <= wmax_ns && col[k] != u;  // col only where the latency passes
+                // col only where the latency passes; identity rows (IDENT): the
+                // column is the entry's place in its row
+                const bool f = l[q] <= wmax_ns && (IDENT ? (uint32_t)(k - b) != u : col[k] != u);
                 const uint64_t m = __ballot(f);
                 if (f) {
                     const uint32_t c = cls_of(l[q]);
                     atomicAdd(&ccnt[wv][c - 1], 1u);
                     mw = c > mw ? c : mw;
                 }
-                if (c0 + q < TR_CH && lane == 0) bal[wv][c0 + q] = m;
+                if (c0 + q < TR_CH && lane == 0) {
+                    bal[wv][c0 + q] = m;
+                    pre[wv][c0 + q] = (uint16_t)cnt;
+                }
                 cnt += (uint32_t)__popcll(m);
             }
         }
@@ -347,28 +353,52 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t V, const uint64_t
         if (lane < cls) off_out[(uint64_t)u * cls + lane] = fits ? (lane == cls - 1 ? (uint32_t)(base + cnt) : start) : 0u;
         if (lane < 32) ccnt[wv][lane] = start;  // running positions
         if (!cnt || !fits) continue;            // uniform
-        for (uint32_t c = 0; c < nch; ++c) {
+        auto place = [&](uint64_t k) {
+            const uint32_t v = IDENT ? (uint32_t)(k - b) : col[k];
+            const uint64_t wu = units_of(lat[k]);
+            const float ls = WITH_LOSS ? loss[k] : 0.0f;
+            const uint32_t cl = (uint32_t)(q ? wu / q : wu);
+            const uint32_t pos = atomicAdd(&ccnt[wv][cl - 1], 1u);
+            const float eb = WITH_LOSS ? 1.0f - ls : 0.0f;  // (1f32 - other.packet_loss), mod.rs:328
+            // q > 0 (quantized classes): the weight's remainder w - c q rides
+            // along, (1 - e) in bits 34.. (a loss in [0, 1]: its bits are < 2^30)
+            ce_out[pos] = q ? ((uint64_t)__float_as_uint(eb) << 34) | ((wu - (uint64_t)cl * q) << vb) | v
+                            : ((uint64_t)__float_as_uint(eb) << 32) | v;
+            if (IN) atomicAdd(&in_cnt[(uint64_t)v * cls + cl - 1], 1u);  // symmetric plans: no in-rows
+        };
+        // the hits of the kept chunks dealt one a lane (the j-th hit: the chunk
+        // whose prefix count covers j, the (j - prefix)-th set bit of its
+        // ballot): ~330 hits a row (C3) in 6 rounds of independent loads, not
+        // one dependent round a chunk with a hit
+        const uint32_t nc1 = nch < TR_CH ? nch : TR_CH;
+        const uint32_t cntk = nc1 == nch ? cnt : (uint32_t)pre[wv][nc1 - 1] + (uint32_t)__popcll(bal[wv][nc1 - 1]);
+        for (uint32_t j0 = 0; j0 < cntk; j0 += 64) {  // uniform
+            const uint32_t j = j0 + lane;
+            if (j >= cntk) continue;
+            uint32_t lo = 0, hi = nc1 - 1;  // the last chunk whose prefix is <= j
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) >> 1;
+                if (pre[wv][mid] <= j) lo = mid;
+                else hi = mid - 1;
+            }
+            uint64_t m = bal[wv][lo];
+            uint32_t r = j - pre[wv][lo], bit = 0;
+            for (uint32_t w = 32; w > 0; w >>= 1) {  // the r-th set bit of m
+                const uint32_t lowc = (uint32_t)__popcll(m & ((1ull << w) - 1ull));
+                if (r >= lowc) {
+                    r -= lowc;
+                    m >>= w;
+                    bit += w;
+                } else {
+                    m &= (1ull << w) - 1ull;
+                }
+            }
+            place(b + 64ull * lo + bit);
+        }
+        for (uint32_t c = TR_CH; c < nch; ++c) {  // rows past TR_CH chunks: tested again
             const uint64_t k = b + 64ull * c + lane;
-            uint64_t m;
-            if (c < TR_CH) {
-                m = bal[wv][c];
-            } else {
-                const uint64_t l = k < e ? lat[k] : ~0ull;
-                m = __ballot(l <= wmax_ns && col[k] != u);
-            }
-            if (!m) continue;  // uniform
-            if ((m >> lane) & 1ull) {
-                const uint32_t v = col[k];
-                const uint64_t wu = units_of(lat[k]);
-                const uint32_t cl = (uint32_t)(q ? wu / q : wu);
-                const uint32_t pos = atomicAdd(&ccnt[wv][cl - 1], 1u);
-                const float eb = WITH_LOSS ? 1.0f - loss[k] : 0.0f;  // (1f32 - other.packet_loss), mod.rs:328
-                // q > 0 (quantized classes): the weight's remainder w - c q rides
-                // along, (1 - e) in bits 34.. (a loss in [0, 1]: its bits are < 2^30)
-                ce_out[pos] = q ? ((uint64_t)__float_as_uint(eb) << 34) | ((wu - (uint64_t)cl * q) << vb) | v
-                                : ((uint64_t)__float_as_uint(eb) << 32) | v;
-                if (IN) atomicAdd(&in_cnt[(uint64_t)v * cls + cl - 1], 1u);  // symmetric plans: no in-rows
-            }
+            const uint64_t l = k < e ? lat[k] : ~0ull;
+            if (l <= wmax_ns && (IDENT ? (uint32_t)(k - b) != u : col[k] != u)) place(k);
         }
     }
     for (int off = 32; off > 0; off >>= 1) {
@@ -496,6 +526,20 @@ __global__ __launch_bounds__(256) void lvl_index_kernel(uint32_t V, const uint64
             base += (uint64_t)__popcll(m);
         }
     }
+}
+
+// symmetric plans' one-call build: every uploaded loss equals its mirror's
+// (identity rows: entry u * V + v <-> v * V + u; the mirror is uploaded too,
+// having the same latency); any difference clears *ok
+__global__ void loss_mirror_check_kernel(const uint32_t *__restrict__ idx, uint64_t count, uint64_t V,
+                                         const float *__restrict__ loss, uint32_t *ok) {
+    bool bad = false;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < count;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = idx[i];
+        bad |= __float_as_uint(loss[k]) != __float_as_uint(loss[(k % V) * V + k / V]);
+    }
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicAnd(ok, 0u);
 }
 
 __global__ void loss_scatter_kernel(const uint32_t *__restrict__ idx, const float *__restrict__ val, uint64_t count,
@@ -2844,7 +2888,7 @@ LevelCtx level_ctx(srt_plan *p) {
     c.t_cls = p->t_cls;
     c.tcls = p->d_tcls;
     c.ce_out = p->d_tpk;
-    c.ce_in = p->lvl_sym ? p->d_tpk : p->d_tpk2;
+    c.ce_in = p->lvl_single ? p->d_tpk : p->d_tpk2;
     c.nodes = p->d_nodes;
     c.sl_lat = p->d_sl_lat;
     c.sl_loss = p->d_sl_loss;
@@ -2894,14 +2938,22 @@ srt_status level_csr(srt_plan *p, uint64_t wmax, bool with_loss, srt_err *err) {
     const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(8192, (V + 3) / 4));
     const uint64_t wns = wmax * p->kp.g;
     const double inv_g = 1.0 / (double)p->kp.g;
+    // symmetric plans (lvl_sym_tile_kernel: identity rows, mirrored pairs --
+    // their losses too when the entries carry them): out-rows only
+    const bool single = with_loss ? p->lvl_sym : p->lvl_sym_lat;
+    p->lvl_single = single;
     auto out_pass = [&]() {
         (void)hipMemsetAsync(p->d_tccnt, 0, 2 * vc1 * 4, M);  // in-row counts, then in-row cursors
         (void)hipMemsetAsync(p->d_tcursor, 0, sizeof(unsigned long long), M);
         (void)hipMemsetAsync(p->d_tmaxw, 0, sizeof(unsigned long long), M);
-        if (with_loss && p->lvl_sym)
-            hipLaunchKernelGGL((lvl_out_kernel<true, false>), dim3(blocks), dim3(256), 0, M, V, p->d_row_ptr, p->d_col,
-                               p->d_lat, p->d_loss, p->kp.g, inv_g, wns, cls, q, vb, p->d_tcls, p->d_tccnt,
+        if (single && with_loss)  // symmetric plans have identity rows (lvl_sym_tile_kernel)
+            hipLaunchKernelGGL((lvl_out_kernel<true, false, true>), dim3(blocks), dim3(256), 0, M, V, p->d_row_ptr,
+                               p->d_col, p->d_lat, p->d_loss, p->kp.g, inv_g, wns, cls, q, vb, p->d_tcls, p->d_tccnt,
                                p->d_tpk, p->lvl_cap, p->d_tcursor, (unsigned long long *)p->d_tmaxw);
+        else if (single)
+            hipLaunchKernelGGL((lvl_out_kernel<false, false, true>), dim3(blocks), dim3(256), 0, M, V, p->d_row_ptr,
+                               p->d_col, p->d_lat, (const float *)nullptr, p->kp.g, inv_g, wns, cls, q, vb, p->d_tcls,
+                               p->d_tccnt, p->d_tpk, p->lvl_cap, p->d_tcursor, (unsigned long long *)p->d_tmaxw);
         else if (with_loss)
             hipLaunchKernelGGL(lvl_out_kernel<true>, dim3(blocks), dim3(256), 0, M, V, p->d_row_ptr, p->d_col,
                                p->d_lat, p->d_loss, p->kp.g, inv_g, wns, cls, q, vb, p->d_tcls, p->d_tccnt,
@@ -2943,7 +2995,7 @@ srt_status level_csr(srt_plan *p, uint64_t wmax, bool with_loss, srt_err *err) {
         }
         p->lvl_cap = count;
     }
-    if (with_loss && p->lvl_sym) {
+    if (single) {
         // symmetric plan (lvl_sym_tile_kernel): the in-rows are the out-rows;
         // their offsets copied, the entries read through the same array
         // (level_ctx)
@@ -3207,6 +3259,13 @@ void loss_scatter(const uint32_t *d_idx, const float *d_val, uint64_t count, flo
     if (count)
         hipLaunchKernelGGL(loss_scatter_kernel, dim3((uint32_t)std::min<uint64_t>(4096, (count + 255) / 256)),
                            dim3(256), 0, s, d_idx, d_val, count, d_loss);
+}
+
+void loss_mirror_check(const uint32_t *d_idx, uint64_t count, uint64_t V, const float *d_loss, uint32_t *d_ok,
+                       hipStream_t s) {
+    if (count)
+        hipLaunchKernelGGL(loss_mirror_check_kernel, dim3((uint32_t)std::min<uint64_t>(4096, (count + 255) / 256)),
+                           dim3(256), 0, s, d_idx, count, V, d_loss, d_ok);
 }
 
 srt_status level_sym_check(srt_plan *p, uint64_t wmax_units, bool with_loss, bool *sym, srt_err *err) {
