@@ -466,3 +466,24 @@ def test_quantized_level_fold(monkeypatch, seed, directed, lat_range):
         assert plan.timing()["loss_fold"] == (1 if noq == "0" else 0), noq
         assert np.array_equal(t.latency_ns, elat)
         assert np.array_equal(t.packet_loss.view(np.uint32), eloss.view(np.uint32)), f"noq={noq}"
+
+
+@pytest.mark.parametrize("mixed", [False, True])
+def test_piece_upload_whole_ms(small_upload_pieces, mixed):
+    """The piece upload on whole-millisecond latencies (u32 ns pieces), and
+    with one latency off the millisecond grid (g = 1 ns); both families,
+    oracle bits (the one-call build takes the piece upload once the staging is
+    pinned: srt_init first).  (A u16-millisecond upload copy halved the PCIe
+    bytes but slowed the host scan that feeds it 1.8x: not kept.)"""
+    err = _lib.SrtErr()
+    assert _lib.lib().srt_init(0, err) == 0
+    n = 150
+    src, dst, lat, loss = synth.random_graph(n, 77 + mixed, p_edge=0.1, lat_range_ns=(1, 50), loss_max=0.05)
+    lat = np.asarray(lat, np.uint64) * np.uint64(synth.MS)
+    if mixed:
+        lat[len(lat) // 2] += np.uint64(1)  # one latency off the millisecond grid
+    edges = (src, dst, lat, loss)
+    _check(edges, np.arange(n, dtype=np.uint32), False, n, algo=_lib.SRT_ALGO_FW)
+    if not mixed:  # (g = 1 ns: the packed sparse key has no room for V x 50 ms)
+        _check(edges, np.arange(0, n, 3, dtype=np.uint32), False, n, algo=_lib.SRT_ALGO_SSSP)
+    _check(edges, np.arange(n, dtype=np.uint32), False, n)
