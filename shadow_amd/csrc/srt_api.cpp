@@ -975,7 +975,7 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     //     units; the solve applies when one was found (B <= 31).
     uint64_t lvl_bound = ~0ull, lvl_visits = 0;
     std::string why_lvl =
-        "the level solve needs V <= 18400 and every shortest path <= 31 latency units (or 31 buckets as wide "
+        "the level solve needs V <= 18400 and every shortest path <= 63 latency units (or 63 buckets as wide "
         "as the shortest edge)";
     {
         const uint64_t maxu = cs.maxlat / cs.gcd;
@@ -1003,11 +1003,15 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
                 if (srt::level_sym_check(p, maxu, !defer_loss, &sym, &e2) != SRT_OK) return probe_fail();
                 p->lvl_sym_lat = p->lvl_sym = sym;
             }
-            if (srt::level_probe(p, std::min<uint64_t>(31, maxu), &lvl_bound, &lvl_visits, &e2) != SRT_OK)
+            // levels of one unit: 31 classes first (C1-C3: B <= 14), then 63
+            if (srt::level_probe(p, std::min<uint64_t>(31, maxu), 31, &lvl_bound, &lvl_visits, &e2) != SRT_OK)
                 return probe_fail();
-            // no bound within 31 units: the quantized solve, buckets of q <= the
+            if (lvl_bound == ~0ull &&
+                srt::level_probe(p, std::min<uint64_t>(63, maxu), 63, &lvl_bound, &lvl_visits, &e2) != SRT_OK)
+                return probe_fail();
+            // no bound within 63 units: the quantized solve, buckets of q <= the
             // shortest edge (C3ns: g = 1 ns, edges >= 1 ms), when the shortest
-            // paths stay under 32 such buckets
+            // paths stay under 64 such buckets
             const char *kq = std::getenv("SRT_LEVEL_Q");  // knob: 0 = integer levels only (A/B, tests)
             if (lvl_bound == ~0ull && !(kq && std::atoi(kq) == 0)) {
                 uint64_t mn_ns = ~0ull;
@@ -1015,16 +1019,20 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
                 const uint64_t mu = mn_ns == ~0ull ? 0 : mn_ns / cs.gcd;
                 const uint32_t vb = srt::level_vbits(p->V);
                 // an entry keeps the remainder w - c q (< q) in 34 - vb bits;
-                // latencies up to 32 q stay below 2^31
-                const uint64_t q = std::min<uint64_t>(std::min<uint64_t>(mu, 1ull << (34 - vb)), 1ull << 26);
+                // latencies up to 64 q stay below 2^31
+                const uint64_t q = std::min<uint64_t>(std::min<uint64_t>(mu, 1ull << (34 - vb)), 1ull << 25);
                 if (q >= 2) {
                     uint32_t rb = 0;
                     while ((1ull << rb) < q) ++rb;
                     p->lvl_q = (uint32_t)q;
                     p->lvl_rb = rb;
                     p->lvl_vb = vb;
-                    if (srt::level_probe(p, std::min<uint64_t>(maxu, 32 * q - 1), &lvl_bound, &lvl_visits, &e2) !=
+                    if (srt::level_probe(p, std::min<uint64_t>(maxu, 32 * q - 1), 31, &lvl_bound, &lvl_visits, &e2) !=
                         SRT_OK)
+                        return probe_fail();
+                    if (lvl_bound == ~0ull &&
+                        srt::level_probe(p, std::min<uint64_t>(maxu, 64 * q - 1), 63, &lvl_bound, &lvl_visits, &e2) !=
+                            SRT_OK)
                         return probe_fail();
                     if (lvl_bound == ~0ull) p->lvl_q = 0;
                 }

@@ -411,7 +411,7 @@ srt_status fw_loss(srt_plan *p, unsigned long long *d_stats, srt_err *err);
 // level solve (srt_loss.hip, SRT_ALGO_LEVEL): the create-time bound on every
 // in-use shortest path over the edges <= wmax units (~0: none; visits: edges a
 // row walks), and the build of rows [row0, row1) into the table
-srt_status level_probe(srt_plan *p, uint64_t wmax, uint64_t *bound, uint64_t *visits, srt_err *err);
+srt_status level_probe(srt_plan *p, uint64_t wmax, uint32_t wc, uint64_t *bound, uint64_t *visits, srt_err *err);
 srt_status level_run(srt_plan *p, unsigned long long *d_stats, srt_err *err);
 // what a level solve launch reads and writes: a plan's buffers (level_ctx),
 // or a peer device's copies of its class CSRs (the in-process multi-GPU build)

@@ -299,7 +299,7 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t V, const uint64_t
                                                       unsigned long long *cursor, unsigned long long *maxw) {
     __shared__ uint64_t bal[4][TR_CH];
     __shared__ uint16_t pre[4][TR_CH];  // per wave: the row's hits before chunk c
-    __shared__ uint32_t ccnt[4][32];  // per wave: hits per class (pass 1), running positions (pass 2)
+    __shared__ uint32_t ccnt[4][64];  // per wave: hits per class (pass 1), running positions (pass 2)
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -310,7 +310,7 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t V, const uint64_t
     for (uint32_t u = wave; u < V; u += nwaves) {
         const uint64_t b = row_ptr[u], e = row_ptr[u + 1];
         const uint32_t nch = (uint32_t)((e - b + 63) / 64);
-        if (lane < 32) ccnt[wv][lane] = 0;
+        ccnt[wv][lane] = 0;
         uint32_t cnt = 0;
         for (uint32_t c0 = 0; c0 < nch; c0 += 4) {
             uint64_t l[4];
@@ -345,13 +345,13 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t V, const uint64_t
         const bool fits = base + cnt <= cap;
         // class offsets of row u: exclusive prefix of the class counts (lanes < cls)
         uint32_t x = lane < cls ? ccnt[wv][lane] : 0u, incl = x;
-        for (int o = 1; o < 32; o <<= 1) {
+        for (int o = 1; o < 64; o <<= 1) {
             const uint32_t y = __shfl_up(incl, o);
             if (lane >= o) incl += y;
         }
         const uint32_t start = (uint32_t)base + incl - x;
         if (lane < cls) off_out[(uint64_t)u * cls + lane] = fits ? (lane == cls - 1 ? (uint32_t)(base + cnt) : start) : 0u;
-        if (lane < 32) ccnt[wv][lane] = start;  // running positions
+        ccnt[wv][lane] = start;  // running positions
         if (!cnt || !fits) continue;            // uniform
         auto place = [&](uint64_t k) {
             const uint32_t v = IDENT ? (uint32_t)(k - b) : col[k];
@@ -1510,7 +1510,8 @@ __global__ __launch_bounds__(LOSS_NT) void level_loss_kernel(
 }
 
 // ------------------------------------------------------------ level solve
-constexpr size_t SOLVE_HIST = 128;  // level ends, levels <= 31
+constexpr size_t SOLVE_HIST = 256;  // level ends, levels <= LWC
+constexpr uint32_t LWC = 63;        // the level solve's classes / levels at most (CLSN 64)
 // Closure-free dense build (SRT_ALGO_LEVEL): petgraph's Dijkstra per source
 // (mod.rs:195-198) as a bucket queue with unit-wide buckets -- Dial's
 // algorithm -- over the graph's edges of latency <= B units, where B bounds
@@ -1550,7 +1551,8 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
     __shared__ uint32_t red_max[16];
     constexpr uint32_t WCN = CLSN - 1;
     __shared__ uint32_t plan_end[WCN + 1];
-    __shared__ uint32_t plan_push, plan_pull;
+    __shared__ uint64_t plan_push;
+    __shared__ uint32_t plan_pull;
     __shared__ uint32_t cur[2][2];  // [level parity]: unsettled compaction, level collection
     uint32_t *hist = reinterpret_cast<uint32_t *>(smem);  // hist[l]: end of level l in mem (l <= 31)
     uint16_t *lrow = reinterpret_cast<uint16_t *>(smem + SOLVE_HIST);
@@ -1590,13 +1592,14 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
         for (uint32_t l = 1; l <= lcap && settled < V; ++l) {
             const uint32_t U = V - settled, par = l & 1u;
             if (tid == 0) {
-                uint32_t run = 0, pm = 0, pl = 0;
+                uint32_t run = 0, pl = 0;
+                uint64_t pm = 0;
                 for (uint32_t w = 1; w <= WCN; ++w) {
                     uint32_t items = 0;
                     if (w <= l) {
                         const uint32_t j = l - w, nj = hist[j] - (j ? hist[j - 1] : 0u);
                         if (nj && nj <= U) {
-                            pm |= 1u << w;
+                            pm |= 1ull << w;
                             items = nj;
                         } else if (nj) {
                             pl = 1;
@@ -1611,7 +1614,8 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
                 cur[par][0] = cur[par][1] = 0;
             }
             __syncthreads();
-            const uint32_t T = plan_end[WCN], pm = plan_push;
+            const uint32_t T = plan_end[WCN];
+            const uint64_t pm = plan_push;
             // no tail level l - w (w <= WCN, every class) holds a vertex: the
             // levels >= l are all empty (uniform)
             if (T == 0) break;
@@ -1649,7 +1653,7 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
                 w = 1;
                 while (t >= plan_end[w]) ++w;
                 const uint32_t m = t - (w > 1 ? plan_end[w - 1] : 0u), j = l - w;
-                const bool push = (pm >> w) & 1u;
+                const bool push = (pm >> w) & 1ull;
                 x = mem[push ? (j ? hist[j - 1] : 0u) + m : settled + m];
                 const uint32_t *cl = push ? cls_out : cls_in;
                 e0 = cl[(uint64_t)x * CLSN + w - 1];
@@ -1660,7 +1664,7 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
             for (uint32_t t = grp; t < T; t += ngrp) {
                 const uint32_t w = nw_, x = nx, e0 = ne0, e1 = ne1, j = l - w;
                 if (t + ngrp < T) item(t + ngrp, nw_, nx, ne0, ne1);
-                const bool push = (pm >> w) & 1u;
+                const bool push = (pm >> w) & 1ull;
                 const uint64_t *ce = push ? ce_out : ce_in;
                 // push: x in N_j, its class-w out-edges x -> v, v unsettled or at l;
                 // pull: x unsettled, its class-w in-edges u -> x, u in N_j
@@ -1884,7 +1888,8 @@ __global__ __launch_bounds__(LOSS_NT) void level_q_kernel(
     __shared__ uint32_t red_max[16];
     constexpr uint32_t WCN = CLSN - 1;
     __shared__ uint32_t plan_end[WCN + 1];
-    __shared__ uint32_t plan_push, plan_pull;
+    __shared__ uint64_t plan_push;
+    __shared__ uint32_t plan_pull;
     __shared__ uint32_t cur[2][2];
     uint32_t *hist = reinterpret_cast<uint32_t *>(smem);  // hist[k]: end of bucket k in mem (k <= 31)
     unsigned long long *key = reinterpret_cast<unsigned long long *>(smem + SOLVE_HIST);
@@ -1912,13 +1917,14 @@ __global__ __launch_bounds__(LOSS_NT) void level_q_kernel(
         for (uint32_t b = 1; b <= kcap && settled < V; ++b) {
             const uint32_t U = V - settled, par = b & 1u;
             if (tid == 0) {
-                uint32_t run = 0, pm = 0, pl = 0;
+                uint32_t run = 0, pl = 0;
+                uint64_t pm = 0;
                 for (uint32_t c = 1; c <= WCN; ++c) {
                     uint32_t items = 0;
                     if (c <= b) {
                         const uint32_t j = b - c, nj = hist[j] - (j ? hist[j - 1] : 0u);
                         if (nj && nj <= U) {
-                            pm |= 1u << c;
+                            pm |= 1ull << c;
                             items = nj;
                         } else if (nj) {
                             pl = 1;
@@ -1933,7 +1939,8 @@ __global__ __launch_bounds__(LOSS_NT) void level_q_kernel(
                 cur[par][0] = cur[par][1] = 0;
             }
             __syncthreads();
-            const uint32_t T = plan_end[WCN], pm = plan_push;
+            const uint32_t T = plan_end[WCN];
+            const uint64_t pm = plan_push;
             const uint32_t lo = b * qw, hi = lo + qw;  // bucket b: latencies [lo, hi)
             if (T && plan_pull) {
                 // the unsettled vertices (key at bucket >= b, or none) into mem[settled, V)
@@ -1953,7 +1960,7 @@ __global__ __launch_bounds__(LOSS_NT) void level_q_kernel(
                 c = 1;
                 while (t >= plan_end[c]) ++c;
                 const uint32_t m = t - (c > 1 ? plan_end[c - 1] : 0u), j = b - c;
-                const bool push = (pm >> c) & 1u;
+                const bool push = (pm >> c) & 1ull;
                 x = mem[push ? (j ? hist[j - 1] : 0u) + m : settled + m];
                 const uint32_t *cl = push ? cls_out : cls_in;
                 e0 = cl[(uint64_t)x * CLSN + c - 1];
@@ -1964,7 +1971,7 @@ __global__ __launch_bounds__(LOSS_NT) void level_q_kernel(
             for (uint32_t t = grp; t < T; t += ngrp) {
                 const uint32_t c = nc_, x = nx, e0 = ne0, e1 = ne1, j = b - c;
                 if (t + ngrp < T) item(t + ngrp, nc_, nx, ne0, ne1);
-                const bool push = (pm >> c) & 1u;
+                const bool push = (pm >> c) & 1ull;
                 const uint64_t *ce = push ? ce_out : ce_in;
                 const uint32_t cbase = c * qw, jlo = j * qw, jhi = jlo + qw;
                 // push: x in bucket j (final), its class-c out-edges x -> v;
@@ -2921,7 +2928,8 @@ srt_status level_csr(srt_plan *p, uint64_t wmax, bool with_loss, srt_err *err) {
     hipStream_t M = p->stream;
     const uint32_t V = p->V;
     const uint32_t q = p->lvl_q, vb = q ? p->lvl_vb : 32u;
-    const uint32_t cls = (q ? wmax / q : wmax) < 16 ? 16 : 32;
+    const uint64_t ncls = q ? wmax / q : wmax;
+    const uint32_t cls = ncls < 16 ? 16 : ncls < 32 ? 32 : 64;
     const uint64_t vc1 = (uint64_t)V * cls + 1;
     srt_status st;
     uint64_t c1 = p->tcls_cap, c2 = p->tcls_cap, cap_cur = p->d_tcursor ? 1 : 0, cap_mw = p->d_tmaxw ? 1 : 0;
@@ -3068,18 +3076,20 @@ void launch_solve_ctx(const LevelCtx &c, unsigned long long *d_stats, const uint
         std::swap(eo, ei);
     }
     if (quant) {
-        auto kern = c.t_cls == 16 ? (nts ? level_q_kernel<4, 4, 16, 2, true> : level_q_kernel<4, 4, 16, 2, false>)
-                                  : (nts ? level_q_kernel<4, 2, 32, 2, true> : level_q_kernel<4, 2, 32, 2, false>);
+        auto kern = c.t_cls == 16   ? (nts ? level_q_kernel<4, 4, 16, 2, true> : level_q_kernel<4, 4, 16, 2, false>)
+                    : c.t_cls == 32 ? (nts ? level_q_kernel<4, 2, 32, 2, true> : level_q_kernel<4, 2, 32, 2, false>)
+                                    : (nts ? level_q_kernel<4, 2, 64, 2, true> : level_q_kernel<4, 2, 64, 2, false>);
         (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)(LDS_BUDGET - 4096));
-        const uint32_t kcap = std::min<uint32_t>(lcap / c.q, WC);
+        const uint32_t kcap = std::min<uint32_t>(lcap / c.q, LWC);
         hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, c.stream, V, c.nodes, c.n, list ? 0u : r0, r1, co, ci,
                            eo, ei, kcap, lcap, c.q, c.rb, c.vb, c.g, c.sl_lat, c.sl_loss, c.out_lat, c.out_loss, d_stats,
                            list, stage, stage_loss, stage_mode, probe, c.visits, c.lmem);
         return;
     }
-    auto kern = c.t_cls == 16 ? (nts ? level_solve_kernel<4, 4, 16, 2, true> : level_solve_kernel<4, 4, 16, 2, false>)
-                              : (nts ? level_solve_kernel<4, 2, 32, 2, true> : level_solve_kernel<4, 2, 32, 2, false>);
+    auto kern = c.t_cls == 16   ? (nts ? level_solve_kernel<4, 4, 16, 2, true> : level_solve_kernel<4, 4, 16, 2, false>)
+                : c.t_cls == 32 ? (nts ? level_solve_kernel<4, 2, 32, 2, true> : level_solve_kernel<4, 2, 32, 2, false>)
+                                : (nts ? level_solve_kernel<4, 2, 64, 2, true> : level_solve_kernel<4, 2, 64, 2, false>);
     (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(LDS_BUDGET - 4096));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, c.stream, V, c.nodes, c.n, list ? 0u : r0, r1, co, ci, eo, ei,
                        lcap, c.g, c.sl_lat, c.sl_loss, c.out_lat, c.out_loss, d_stats, list,
@@ -3117,7 +3127,7 @@ srt_status launch_solve(srt_plan *p, unsigned long long *d_stats, const RowJob &
 // forward probe row walked on average (the AUTO price).  p->lvl_q > 0: the
 // quantized solve's buckets of q units; the bound must keep every class and
 // bucket <= 31 (B < 32 q).
-srt_status level_probe(srt_plan *p, uint64_t wmax, uint64_t *bound, uint64_t *visits, srt_err *err) {
+srt_status level_probe(srt_plan *p, uint64_t wmax, uint32_t wc, uint64_t *bound, uint64_t *visits, srt_err *err) {
     *bound = ~0ull;
     *visits = 0;
     if (!p->n) return SRT_OK;
@@ -3142,7 +3152,7 @@ srt_status level_probe(srt_plan *p, uint64_t wmax, uint64_t *bound, uint64_t *vi
     RowJob job;
     job.list = d_pr + 32;
     job.count = K;
-    const uint64_t LQ = (uint64_t)(WC + 1) * (p->lvl_q ? p->lvl_q : 1) - 1;  // the largest bound the solve takes
+    const uint64_t LQ = (uint64_t)(wc + 1) * (p->lvl_q ? p->lvl_q : 1) - 1;  // the largest bound the solve takes
     // distances up to LQ (not only up to wmax: a path of short edges may be
     // longer than the longest edge)
     const uint32_t cap = (uint32_t)LQ;
@@ -3162,7 +3172,7 @@ srt_status level_probe(srt_plan *p, uint64_t wmax, uint64_t *bound, uint64_t *vi
     std::memcpy(&vis, h, 8);
     *visits = vis / K;
     for (uint32_t k = 0; k < K; ++k)
-        if (h[2 + k] <= cap && h[18 + k] <= cap && (uint64_t)h[2 + k] + h[18 + k] <= LQ)  // classes <= WC
+        if (h[2 + k] <= cap && h[18 + k] <= cap && (uint64_t)h[2 + k] + h[18 + k] <= LQ)  // classes <= wc
             *bound = std::min<uint64_t>(*bound, (uint64_t)h[2 + k] + h[18 + k]);
     if (std::getenv("SRT_TRACE"))
         std::fprintf(stderr,

@@ -215,21 +215,39 @@ def test_level_quantized_matches_oracle(n, seed, directed, p_edge, lat_ms, subse
 
 
 def test_level_quantized_integer_units():
-    """Integer-ms latencies 2-9 ms over a ring-heavy graph whose paths exceed
-    31 units: the integer probe fails, the quantized one (buckets of 2 ms, the
-    shortest edge) bounds it; AUTO == FW == oracle."""
+    """Integer-ms latencies 2-9 ms over a sparse ring-heavy graph whose probe
+    bound (72 units) exceeds the 63 unit levels: the integer probes fail, the
+    quantized one (64 buckets of 2 ms, the shortest edge) bounds it; AUTO ==
+    oracle."""
     n = 300
-    src, dst, lat, loss = synth.random_graph(n, 8, p_edge=0.01, directed=False, lat_range_ns=(2, 9), loss_max=0.05)
+    src, dst, lat, loss = synth.random_graph(n, 8, p_edge=0.006, directed=False, lat_range_ns=(2, 9), loss_max=0.05)
     lat = np.asarray(lat, np.uint64) * np.uint64(synth.MS)
     g = NetworkGraph.from_edges(n, src, dst, lat, loss)
     nodes = np.arange(n, dtype=np.uint32)
     og = O.Graph(False, np.arange(n), src, dst, lat, loss)
-    elat, _ = O.compute_shortest_paths(og, nodes)
-    assert elat.max() // synth.MS > 31, "the graph must defeat the integer probe"
     p = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_LEVEL, device=0).run()
     try:
         d = p.describe()
         assert d.startswith("level:u32 ") and " q=2 " in d, d
+        _check(p.fetch(), og, nodes)
+    finally:
+        p.close()
+
+
+def test_level_63_unit_levels():
+    """Shortest paths past 31 units (probe bound 38): the 31-class probe fails,
+    the 63-class one bounds it (64 class offsets a vertex); level == oracle."""
+    n = 300
+    src, dst, lat, loss = synth.random_graph(n, 8, p_edge=0.012, directed=False, lat_range_ns=(1, 9), loss_max=0.05)
+    lat = np.asarray(lat, np.uint64) * np.uint64(synth.MS)
+    g = NetworkGraph.from_edges(n, src, dst, lat, loss)
+    nodes = np.arange(n, dtype=np.uint32)
+    og = O.Graph(False, np.arange(n), src, dst, lat, loss)
+    p = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_LEVEL, device=0).run()
+    try:
+        d = p.describe()
+        lmax = int(d.split(" lmax=")[1].split("(")[0])
+        assert d.startswith("level:u16 ") and 31 < lmax <= 63, d
         _check(p.fetch(), og, nodes)
     finally:
         p.close()
