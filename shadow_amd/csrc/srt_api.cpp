@@ -578,6 +578,8 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_fl);
     hipFree(p->d_fp);
     hipFree(p->d_ftight);
+    hipFree(p->d_fce);
+    hipFree(p->d_fcnt);
     hipFree(p->d_fchg);
     hipFree(p->d_fact);
     hipFree(p->d_fdone);
@@ -1260,6 +1262,8 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
             PLAN_TRY(dmalloc(&p->d_fl, (size_t)p->fr_lblocks * p->V * 512, err));
             PLAN_TRY(dmalloc(&p->d_fp, (size_t)nb * p->V * 512, err));
             PLAN_TRY(dmalloc(&p->d_ftight, (size_t)nb * std::max<uint64_t>(n_in, 1) * 64, err));
+            PLAN_TRY(dmalloc(&p->d_fce, (size_t)nb * std::max<uint64_t>(n_in, 1), err));
+            PLAN_TRY(dmalloc(&p->d_fcnt, (size_t)nb * p->V, err));
             PLAN_TRY(dmalloc(reinterpret_cast<uint8_t **>(&p->d_fchg), (size_t)nb * p->V * srt::frontier_chg_bytes(), err));
             PLAN_TRY(dmalloc(&p->d_fact, (size_t)nb * p->V, err));
             PLAN_TRY(dmalloc(&p->d_fsb, (size_t)2 * nb * p->V * 64, err));

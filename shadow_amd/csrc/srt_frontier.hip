@@ -113,22 +113,28 @@ struct Chg {
 // The marks of v's out-neighbours for sweep t + 1, plain stores (stamps only
 // grow, and final items are flagged apart, so a mark never lowers anything and
 // needs no read first).  Latency-symmetric graphs: the out-neighbours are the
-// in-edge sources, already in the lanes' registers (eu_last: the last in-edge
-// chunk, the only one at <= 64 in-edges); else the CSR row.
-__device__ __forceinline__ void mark(uint32_t *act_b, uint32_t v, uint32_t t, bool sym, const InEdge *in_edge,
-                                     uint32_t eu_last, uint64_t e0, uint64_t e1, const uint64_t *__restrict__ row_ptr,
-                                     const uint32_t *__restrict__ col, int lane) {
+// in-edge sources [e0, e1); else the CSR row.
+__device__ __forceinline__ void mark_rows(uint32_t *act_b, uint32_t v, uint32_t t, bool sym, const InEdge *in_edge,
+                                          uint64_t e0, uint64_t e1, const uint64_t *__restrict__ row_ptr,
+                                          const uint32_t *__restrict__ col, int lane) {
     if (sym) {
-        if (e1 - e0 <= 64) {
-            if (e0 + lane < e1) act_b[eu_last] = t + 1;
-        } else {
-            for (uint64_t k = e0 + lane; k < e1; k += 64) act_b[in_edge[k].u] = t + 1;
-        }
+        for (uint64_t k = e0 + lane; k < e1; k += 64) act_b[in_edge[k].u] = t + 1;
     } else {
         for (uint64_t k = row_ptr[v] + lane; k < row_ptr[v + 1]; k += 64) {
             const uint32_t x = col[k];
             if (x != v) act_b[x] = t + 1;
         }
+    }
+}
+// the same with the in-edge sources already in the lanes' registers (eu_last:
+// the last in-edge chunk, the only one at <= 64 in-edges)
+__device__ __forceinline__ void mark(uint32_t *act_b, uint32_t v, uint32_t t, bool sym, const InEdge *in_edge,
+                                     uint32_t eu_last, uint64_t e0, uint64_t e1, const uint64_t *__restrict__ row_ptr,
+                                     const uint32_t *__restrict__ col, int lane) {
+    if (sym && e1 - e0 <= 64) {
+        if (e0 + lane < e1) act_b[eu_last] = t + 1;
+    } else {
+        mark_rows(act_b, v, t, sym, in_edge, e0, e1, row_ptr, col, lane);
     }
 }
 
@@ -379,18 +385,23 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_lat_sweep_kernel(
 }
 
 // ---------------------------------------------------------- tight pass
-// Every item (b, v), every in-edge k = (u -> v) of v:
-// tight[(b * E + k) * 64 + lane] = the lane's 8-bit mask of sources s with
-// L(s,u) + w == L(s,v) -- the only edges the loss sweeps read along.  A wave
-// takes 64-vertex chunks, as the sweeps do: every chunk holds one hub (slot
-// 0, srt_api.cpp's vertex order), so the waves stay balanced -- striding
-// single items by the wave count (a multiple of 64) put every hub on the same
-// few waves (C4: 33 -> 90 ms).
+// Every item (b, v): the in-edges k = (u -> v) of v that end a shortest path
+// for at least one of the block's 512 sources (C4: about a third of them),
+// compacted in in-edge order to positions e0 = in_ptr[v], e0 + 1, ...:
+// ce[b * E + e0 + j] = (u, 1 - e) and tight[(b * E + e0 + j) * 64 + lane] =
+// the lane's 8-bit mask of sources s with L(s,u) + w == L(s,v);
+// cnt[b * V + v] = how many.  The loss sweeps walk only these, so an item's
+// scan costs its tight edges, not its degree.  A wave takes 64-vertex chunks,
+// as the sweeps do: every chunk holds one hub (slot 0, srt_api.cpp's vertex
+// order), so the waves stay balanced -- striding single items by the wave
+// count (a multiple of 64) put every hub on the same few waves (C4: 33 -> 90
+// ms).
 __global__ __launch_bounds__(FR_WAVES * 64) void fr_tight_kernel(const uint64_t *__restrict__ in_ptr,
                                                                  const InEdge *__restrict__ in_edge, uint32_t V,
                                                                  uint32_t NB, uint64_t E,
                                                                  const uint16_t *__restrict__ L,
-                                                                 uint8_t *__restrict__ tight) {
+                                                                 uint8_t *__restrict__ tight, uint2 *__restrict__ ce,
+                                                                 uint32_t *__restrict__ cnt) {
     const int lane = threadIdx.x & 63;
     const uint32_t wave = blockIdx.x * FR_WAVES + (threadIdx.x >> 6), nwaves = gridDim.x * FR_WAVES;
     const uint32_t cpb = (V + 63) / 64, nchunks = cpb * NB;
@@ -400,16 +411,21 @@ __global__ __launch_bounds__(FR_WAVES * 64) void fr_tight_kernel(const uint64_t 
         const uint4 *Lb = reinterpret_cast<const uint4 *>(L + (uint64_t)b * V * FR_SRC);
         const uint4 own = Lb[(uint64_t)v * 64 + lane];
         uint8_t *tb = tight + (uint64_t)b * E * 64 + lane;
+        uint2 *cb = ce + (uint64_t)b * E;
         const uint64_t e0 = in_ptr[v], e1 = in_ptr[v + 1];
+        uint64_t j = e0;  // next compacted position (wave-uniform)
         for (uint64_t c0 = e0; c0 < e1; c0 += 64) {
             const uint64_t k = c0 + lane;
-            uint32_t eu = 0, ew = 0;
+            uint32_t eu = 0, ew = 0, eb = 0;
             if (k < e1) {
                 const InEdge e = in_edge[k];
                 eu = e.u;
                 ew = e.w;
+                eb = __float_as_uint(e.eb);
             }
             const uint32_t n = e1 - c0 < 64 ? (uint32_t)(e1 - c0) : 64u;
+            const uint64_t jc = j;
+            uint64_t keep = 0;  // the chunk's edges kept
             for (uint32_t j0 = 0; j0 < n; j0 += FR_EB) {
                 uint4 x[FR_EB];
                 uint32_t w[FR_EB];
@@ -425,14 +441,25 @@ __global__ __launch_bounds__(FR_WAVES * 64) void fr_tight_kernel(const uint64_t 
                 }
 #pragma unroll
                 for (int q = 0; q < FR_EB; ++q)
-                    if (j0 + q < n) tb[(c0 + j0 + q) * 64] = (uint8_t)tight8(x[q], own, w[q]);
+                    if (j0 + q < n) {
+                        const uint32_t m = tight8(x[q], own, w[q]);
+                        if (__ballot(m != 0)) {
+                            tb[j * 64] = (uint8_t)m;
+                            keep |= 1ull << (j0 + q);
+                            ++j;
+                        }
+                    }
             }
+            if ((keep >> lane) & 1ull)
+                cb[jc + __builtin_popcountll(keep & ((1ull << lane) - 1ull))] = make_uint2(eu, eb);
         }
+        if (lane == 0) cnt[(uint64_t)b * V + v] = (uint32_t)(j - e0);
     }
 }
 
 // ---------------------------------------------------------- loss sweep
-// Pull over tight in-edges with per-source change bits, double-buffered:
+// Pull over the item's compacted tight in-edges (the tight pass) with
+// per-source change bits, double-buffered:
 // sb_cur[b][u][lane] = the lane's sources of u whose loss changed in sweep
 // t - 1, sb_next = those of sweep t (cleared before it; read as well, so a
 // change made earlier in the same sweep is picked up at once, Gauss-Seidel).
@@ -443,7 +470,7 @@ __global__ __launch_bounds__(FR_WAVES * 64) void fr_tight_kernel(const uint64_t 
 // gather, the own losses loaded beside the in-edges; marks from registers.
 __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
     const uint64_t *__restrict__ in_ptr, const InEdge *__restrict__ in_edge, uint32_t V, uint32_t NB, uint64_t E,
-    const uint8_t *__restrict__ tight, float *P, const uint8_t *__restrict__ sb_cur, uint8_t *sb_next,
+    const uint8_t *__restrict__ tight, const uint2 *__restrict__ ce, const uint32_t *__restrict__ tcnt, float *P, const uint8_t *__restrict__ sb_cur, uint8_t *sb_next,
     uint32_t *act, uint32_t *last, uint32_t t, bool sym, const uint64_t *__restrict__ row_ptr,
     const uint32_t *__restrict__ col, unsigned long long *cnt) {
     const int lane = threadIdx.x & 63;
@@ -460,6 +487,8 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
         uint64_t items = __ballot(a >= t);
         float4 *Pb = reinterpret_cast<float4 *>(P + (uint64_t)b * V * FR_SRC);
         const uint8_t *tb = tight + (uint64_t)b * E * 64 + lane;
+        const uint2 *cb = ce + (uint64_t)b * E;
+        const uint32_t *cnb = tcnt + (uint64_t)b * V;
         const uint8_t *sbc = sb_cur + (uint64_t)b * V * 64 + lane;
         uint8_t *sbn = sb_next + (uint64_t)b * V * 64 + lane;
         if (!items) continue;
@@ -468,13 +497,14 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
         // change bytes are in flight
         uint32_t v = v0 + __builtin_ctzll(items);
         items &= items - 1;
-        uint64_t e0 = in_ptr[v], e1 = in_ptr[v + 1];
+        uint64_t e0 = in_ptr[v], f1 = in_ptr[v + 1];  // [e0, e1): tight, [e0, f1): all in-edges
+        uint64_t e1 = e0 + cnb[v];
         uint32_t eu = 0;
         float eeb = 0.f;
         if (e0 + lane < e1) {
-            const InEdge e = in_edge[e0 + lane];
-            eu = e.u;
-            eeb = e.eb;
+            const uint2 e = cb[e0 + lane];
+            eu = e.x;
+            eeb = __uint_as_float(e.y);
         }
         for (;;) {
             const bool more = items != 0;
@@ -487,7 +517,7 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
             float best[8] = {2.f, 2.f, 2.f, 2.f, 2.f, 2.f, 2.f, 2.f};
             float4 o0 = make_float4(2.f, 2.f, 2.f, 2.f), o1 = o0;
             bool own = false;
-            uint64_t ne0 = 0, ne1 = 0;
+            uint64_t ne0 = 0, ne1 = 0, nf1 = 0;
             uint32_t neu = 0;
             float neeb = 0.f;
             bool pre = !more;
@@ -497,9 +527,9 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
                     eu = 0;
                     eeb = 0.f;
                     if (k < e1) {
-                        const InEdge e = in_edge[k];
-                        eu = e.u;
-                        eeb = e.eb;
+                        const uint2 e = cb[k];
+                        eu = e.x;
+                        eeb = __uint_as_float(e.y);
                     }
                 }
                 const uint32_t n = e1 - c0 < 64 ? (uint32_t)(e1 - c0) : 64u;
@@ -538,11 +568,12 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
                     if (!pre) {  // the next item's head, behind this group's loads
                         pre = true;
                         ne0 = in_ptr[vn];
-                        ne1 = in_ptr[vn + 1];
+                        nf1 = in_ptr[vn + 1];
+                        ne1 = ne0 + cnb[vn];
                         if (ne0 + lane < ne1) {
-                            const InEdge e = in_edge[ne0 + lane];
-                            neu = e.u;
-                            neeb = e.eb;
+                            const uint2 e = cb[ne0 + lane];
+                            neu = e.x;
+                            neeb = __uint_as_float(e.y);
                         }
                     }
                     while (amask) {
@@ -586,13 +617,14 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
                     }
                 }
             }
-            if (!pre) {  // v has no in-edge
+            if (!pre) {  // v has no tight in-edge
                 ne0 = in_ptr[vn];
-                ne1 = in_ptr[vn + 1];
+                nf1 = in_ptr[vn + 1];
+                ne1 = ne0 + cnb[vn];
                 if (ne0 + lane < ne1) {
-                    const InEdge e = in_edge[ne0 + lane];
-                    neu = e.u;
-                    neeb = e.eb;
+                    const uint2 e = cb[ne0 + lane];
+                    neu = e.x;
+                    neeb = __uint_as_float(e.y);
                 }
             }
             uint32_t ib = 0;  // the lane's improved sources
@@ -618,12 +650,13 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
                     pv[1] = make_float4(best[4], best[5], best[6], best[7]);
                     sbn[(uint64_t)v * 64] = (uint8_t)ib;  // only this wave writes v's byte this sweep
                 }
-                mark(act_b, v, t, sym, in_edge, eu, e0, e1, row_ptr, col, lane);
+                mark_rows(act_b, v, t, sym, in_edge, e0, f1, row_ptr, col, lane);
             }
             if (!more) break;
             v = vn;
             e0 = ne0;
             e1 = ne1;
+            f1 = nf1;
             eu = neu;
             eeb = neeb;
         }
@@ -894,7 +927,8 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
         p->sssp_sweeps += nsw;
         chunk_lat = std::max<uint32_t>(nsw + 1, 4);
         // 2. tight masks
-        hipLaunchKernelGGL(fr_tight_kernel, sgrid, sblk, 0, M, p->d_in_ptr, p->d_in_edge, V, NB, E, L, p->d_ftight);
+        hipLaunchKernelGGL(fr_tight_kernel, sgrid, sblk, 0, M, p->d_in_ptr, p->d_in_edge, V, NB, E, L, p->d_ftight,
+                           p->d_fce, p->d_fcnt);
         // 3. loss (activity cleared of the final marks; change bits double-buffered)
         const size_t sbytes = (size_t)NB * V * 64;
         if ((e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p->d_fp), 0x40000000u, (size_t)NB * V * FR_SRC,
@@ -922,7 +956,7 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
             uint8_t *cur = p->d_fsb + ((t - t0 - 1) & 1) * sbytes, *nxt = p->d_fsb + ((t - t0) & 1) * sbytes;
             (void)hipMemsetAsync(nxt, 0, sbytes, M);
             hipLaunchKernelGGL(fr_loss_sweep_kernel, sgrid, sblk, 0, M, p->d_in_ptr, p->d_in_edge, V, NB, E,
-                               p->d_ftight, p->d_fp, cur, nxt, p->d_fact, p->d_fimp, t, p->fr_symg, p->d_frow_ptr,
+                               p->d_ftight, p->d_fce, p->d_fcnt, p->d_fp, cur, nxt, p->d_fact, p->d_fimp, t, p->fr_symg, p->d_frow_ptr,
                                p->d_fcol, dcnt ? dcnt + 4 * std::min<uint32_t>(t - t0, 255) : nullptr);
         }, &t_end, &nsw, err);
         if (st != SRT_OK) return st;
@@ -950,9 +984,10 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
 }
 
 // device bytes of one 512-source block in flight: L (1 KB) + P (2 KB) + change
-// record (16 B) + 2 x per-source change bits (128 B) + activity (4 B) per
-// vertex, the tight masks (64 B) per in-edge
-uint64_t frontier_block_bytes(uint32_t V, uint64_t E) { return (uint64_t)V * (1024 + 2048 + 148) + E * 64; }
+// record (16 B) + 2 x per-source change bits (128 B) + activity (4 B) + tight
+// count (4 B) per vertex, the tight masks (64 B) and compacted edge (8 B) per
+// in-edge
+uint64_t frontier_block_bytes(uint32_t V, uint64_t E) { return (uint64_t)V * (1024 + 2048 + 152) + E * 72; }
 size_t frontier_chg_bytes() { return sizeof(Chg); }
 
 }  // namespace srt

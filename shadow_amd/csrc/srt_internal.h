@@ -236,6 +236,8 @@ struct srt_plan {
     uint16_t *d_fl = nullptr;            // fr_lblocks * V * 512 u16 latencies (units of g)
     float *d_fp = nullptr;               // fr_nb * V * 512 f32 losses
     uint8_t *d_ftight = nullptr;         // fr_nb * n_in_edges * 64 tight-source bytes
+    uint2 *d_fce = nullptr;              // fr_nb * n_in_edges compacted tight in-edges (u, 1 - e)
+    uint32_t *d_fcnt = nullptr;          // fr_nb * V tight in-edge counts
     void *d_fchg = nullptr;              // fr_nb * V change records (srt_frontier.hip Chg, 16 B)
     uint32_t *d_fact = nullptr;          // fr_nb * V activation stamps
     uint8_t *d_ffin = nullptr;           // fr_nb * V: item exact from the start (symmetric seeding)
