@@ -639,6 +639,7 @@ def bench_graph(args, cfg, D):
             frontier = desc.startswith("sssp:frontier")
             if frontier:
                 schedule = {"state": "frontier-u16", "blocks": int(desc.split(" blocks=")[1].split()[0]),
+                            "first": int(desc.split(" first=")[1].split()[0]) if " first=" in desc else 0,
                             "seed": desc.split(" seed=")[1].split()[0],
                             "source_order": "bfs" if "order=bfs" in desc else "table"}
                 traffic, traffic_src = frontier_traffic(args, schedule, launches_per_step)

@@ -580,6 +580,7 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_ftight);
     hipFree(p->d_fce);
     hipFree(p->d_fcnt);
+    hipFree(p->d_fctl);
     hipFree(p->d_fchg);
     hipFree(p->d_fact);
     hipFree(p->d_fdone);
@@ -1258,12 +1259,31 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
             p->fr_symg = latency_symmetric(g, in_ptr, in_edge, cs.gcd);
             p->fr_sym = !(ks && std::atoi(ks) == 0) && all_blocks > nb &&
                         all_blocks * p->V * 1024ull <= (uint64_t)free_b / 4 && p->fr_symg;
+            // a smaller first launch: the only one whose latency phase starts
+            // from the sources alone (C4, 4 launches: 49+49+49+49 blocks 0.488 s,
+            // 12+61+61+62 0.463, 20+... 0.465, 28+... 0.463); ~1/12 of the
+            // blocks, the rest keep the launch count, so their buffers grow to
+            // hold them.  Knob SRT_FR_FIRST = blocks (0: equal launches; A/B).
+            p->fr_first = 0;
+            if (p->fr_sym) {
+                const char *ev = std::getenv("SRT_FR_FIRST");
+                const uint64_t f = ev ? std::atoll(ev) : all_blocks / 12, k = (all_blocks + nb - 1) / nb;
+                if (f > 0 && f < nb && k >= 2) {
+                    const uint64_t rest = (all_blocks - f + k - 2) / (k - 1);
+                    if (rest <= 64 && rest * bb <= free_b / 2) {
+                        nb = std::max(nb, rest);
+                        p->fr_first = (uint32_t)f;
+                        p->fr_nb = (uint32_t)nb;
+                    }
+                }
+            }
             p->fr_lblocks = p->fr_sym ? (uint32_t)all_blocks : (uint32_t)nb;
             PLAN_TRY(dmalloc(&p->d_fl, (size_t)p->fr_lblocks * p->V * 512, err));
             PLAN_TRY(dmalloc(&p->d_fp, (size_t)nb * p->V * 512, err));
             PLAN_TRY(dmalloc(&p->d_ftight, (size_t)nb * std::max<uint64_t>(n_in, 1) * 64, err));
             PLAN_TRY(dmalloc(&p->d_fce, (size_t)nb * std::max<uint64_t>(n_in, 1), err));
             PLAN_TRY(dmalloc(&p->d_fcnt, (size_t)nb * p->V, err));
+            PLAN_TRY(dmalloc(&p->d_fctl, 8, err));
             PLAN_TRY(dmalloc(reinterpret_cast<uint8_t **>(&p->d_fchg), (size_t)nb * p->V * srt::frontier_chg_bytes(), err));
             PLAN_TRY(dmalloc(&p->d_fact, (size_t)nb * p->V, err));
             PLAN_TRY(dmalloc(&p->d_fsb, (size_t)2 * nb * p->V * 64, err));
@@ -1279,10 +1299,10 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
             p->fr_t = 1;
             char df[160];
             std::snprintf(df, sizeof df,
-                          "sssp:frontier u16|f32 g=%llu lmax=%llu%s V=%u n=%u E_in=%llu blocks=%u order=%s seed=%s",
+                          "sssp:frontier u16|f32 g=%llu lmax=%llu%s V=%u n=%u E_in=%llu blocks=%u first=%u order=%s seed=%s",
                           (unsigned long long)p->sssp_g, (unsigned long long)(ecc_units != ~0ull ? ecc_units : 0),
                           ecc_units != ~0ull ? "(ecc)" : "(V-1)", p->V, p->n, (unsigned long long)p->n_in_edges,
-                          p->fr_nb, p->h_bfs_rank.empty() ? "table" : "bfs", p->fr_sym ? "sym" : "none");
+                          p->fr_nb, p->fr_first, p->h_bfs_rank.empty() ? "table" : "bfs", p->fr_sym ? "sym" : "none");
             p->desc = df;
         }
         if (p->sssp_act_on && !p->sssp_frontier)

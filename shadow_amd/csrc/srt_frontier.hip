@@ -138,6 +138,34 @@ __device__ __forceinline__ void mark(uint32_t *act_b, uint32_t v, uint32_t t, bo
     }
 }
 
+// Dense sweeps.  In the heavy sweeps of a phase nearly every item of the
+// launch is marked and improves (C4: 4.7M of 4.9M items in each of ~10 loss
+// sweeps), so the activity flags and the marks cost stores and scans for
+// nothing.  ctl[t & 3] counts the items sweep t improved, ctl[4 + (t & 3)] says
+// that sweep t stored no marks.  Sweep t runs dense (every item, no activity
+// read) if sweep t - 1 improved more than dense_min items or stored no marks,
+// and stores no marks if sweep t - 1 improved more than nomark_min
+// (> dense_min): a sweep after one that stored none is dense, so no mark is
+// ever missing.  The host zeroes ctl before a phase (sweep t0 -- the seeds --
+// counts 0: sweep t0 + 1 runs on the seeds' marks).
+struct SweepMode {
+    bool dense, mark;
+};
+__device__ __forceinline__ SweepMode sweep_mode(uint32_t *ctl, uint32_t t, uint32_t dense_min, uint32_t nomark_min) {
+    const uint32_t pc = ctl[(t - 1) & 3], pn = ctl[4 + ((t - 1) & 3)];
+    SweepMode m;
+    m.dense = pn != 0 || pc > dense_min;
+    m.mark = pc <= nomark_min;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // sweep t + 1 counts from 0; this sweep's mark flag
+        ctl[(t + 1) & 3] = 0;
+        ctl[4 + (t & 3)] = m.mark ? 0u : 1u;
+    }
+    return m;
+}
+__device__ __forceinline__ void count_improved(uint32_t *ctl, uint32_t t, uint32_t n, int lane) {
+    if (lane == 0 && n) atomicAdd(&ctl[t & 3], n);
+}
+
 // the phase's last-improvement stamp, once per wave at the end of a sweep
 // (every improving wave stores the same value: read first, a hot word)
 __device__ __forceinline__ void note_improved(uint32_t *last, uint32_t t, bool any, int lane) {
@@ -246,18 +274,21 @@ __global__ void fr_sym_act_kernel(uint32_t *act, uint8_t *fin, Chg *chg, const u
 __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_lat_sweep_kernel(
     const uint64_t *__restrict__ in_ptr, const InEdge *__restrict__ in_edge, uint32_t V, uint32_t NB,
     uint16_t *L, Chg *chg, uint32_t *act, const uint8_t *__restrict__ fin, uint32_t *last, uint32_t t, bool sym,
-    const uint64_t *__restrict__ row_ptr, const uint32_t *__restrict__ col) {
+    const uint64_t *__restrict__ row_ptr, const uint32_t *__restrict__ col, uint32_t *ctl, uint32_t dense_min,
+    uint32_t nomark_min) {
     const int lane = threadIdx.x & 63;
     const uint32_t wave = blockIdx.x * FR_WAVES + (threadIdx.x >> 6), nwaves = gridDim.x * FR_WAVES;
     const uint32_t cpb = (V + 63) / 64, nchunks = cpb * NB;
     bool any_imp = false;
+    uint32_t n_imp = 0;
+    const SweepMode md = sweep_mode(ctl, t, dense_min, nomark_min);
     for (uint32_t c = __builtin_amdgcn_readfirstlane(wave); c < nchunks; c += nwaves) {
         const uint32_t b = c / cpb, v0 = (c % cpb) * 64;
         uint32_t *act_b = act + (uint64_t)b * V;
         const bool in = v0 + lane < V;
-        const uint32_t a = in ? act_b[v0 + lane] : 0u;
+        const uint32_t a = in && !md.dense ? act_b[v0 + lane] : 0u;
         const bool f = in && fin[(uint64_t)b * V + v0 + lane];
-        uint64_t items = __ballot(a >= t && !f);
+        uint64_t items = __ballot((md.dense ? in : a >= t) && !f);
         uint4 *Lb = reinterpret_cast<uint4 *>(L + (uint64_t)b * V * FR_SRC);
         Chg *chg_b = chg + (uint64_t)b * V;
         if (!items) continue;
@@ -362,6 +393,7 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_lat_sweep_kernel(
             const uint64_t im = __ballot(imp);
             if (im) {
                 any_imp = true;
+                ++n_imp;
                 if (imp) Lb[(uint64_t)v * 64 + lane] = best;
                 if (lane == 0) {  // this sweep's lanes, and those of sweep t - 1 that readers may still need
                     Chg cnew;
@@ -370,7 +402,7 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_lat_sweep_kernel(
                     cnew.lanes = im | (old.stamp + 1 == t ? old.lanes : 0ull);
                     chg_b[v] = cnew;
                 }
-                mark(act_b, v, t, sym, in_edge, eu, e0, e1, row_ptr, col, lane);
+                if (md.mark) mark(act_b, v, t, sym, in_edge, eu, e0, e1, row_ptr, col, lane);
             }
             if (!more) break;
             v = vn;
@@ -382,6 +414,7 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_lat_sweep_kernel(
         }
     }
     note_improved(last, t, any_imp, lane);
+    count_improved(ctl, t, n_imp, lane);
 }
 
 // ---------------------------------------------------------- tight pass
@@ -472,19 +505,21 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
     const uint64_t *__restrict__ in_ptr, const InEdge *__restrict__ in_edge, uint32_t V, uint32_t NB, uint64_t E,
     const uint8_t *__restrict__ tight, const uint2 *__restrict__ ce, const uint32_t *__restrict__ tcnt, float *P, const uint8_t *__restrict__ sb_cur, uint8_t *sb_next,
     uint32_t *act, uint32_t *last, uint32_t t, bool sym, const uint64_t *__restrict__ row_ptr,
-    const uint32_t *__restrict__ col, unsigned long long *cnt) {
+    const uint32_t *__restrict__ col, uint32_t *ctl, uint32_t dense_min, uint32_t nomark_min, unsigned long long *cnt) {
     const int lane = threadIdx.x & 63;
     const uint32_t wave = blockIdx.x * FR_WAVES + (threadIdx.x >> 6), nwaves = gridDim.x * FR_WAVES;
     const uint32_t cpb = (V + 63) / 64, nchunks = cpb * NB;
     bool any_imp = false;
+    uint32_t n_imp = 0;
+    const SweepMode md = sweep_mode(ctl, t, dense_min, nomark_min);
 #if FR_COUNT
     uint32_t c_items = 0, c_work = 0, c_imp = 0, c_gath = 0;  // SRT_FR_COUNT (diagnostic builds)
 #endif
     for (uint32_t c = __builtin_amdgcn_readfirstlane(wave); c < nchunks; c += nwaves) {
         const uint32_t b = c / cpb, v0 = (c % cpb) * 64;
         uint32_t *act_b = act + (uint64_t)b * V;
-        const uint32_t a = v0 + lane < V ? act_b[v0 + lane] : 0u;
-        uint64_t items = __ballot(a >= t);
+        const uint32_t a = v0 + lane < V && !md.dense ? act_b[v0 + lane] : 0u;
+        uint64_t items = __ballot(md.dense ? v0 + lane < V : a >= t);
         float4 *Pb = reinterpret_cast<float4 *>(P + (uint64_t)b * V * FR_SRC);
         const uint8_t *tb = tight + (uint64_t)b * E * 64 + lane;
         const uint2 *cb = ce + (uint64_t)b * E;
@@ -642,6 +677,7 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
             }
             if (__ballot(ib != 0)) {
                 any_imp = true;
+                ++n_imp;
 #if FR_COUNT
                 ++c_imp;
 #endif
@@ -650,7 +686,7 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
                     pv[1] = make_float4(best[4], best[5], best[6], best[7]);
                     sbn[(uint64_t)v * 64] = (uint8_t)ib;  // only this wave writes v's byte this sweep
                 }
-                mark_rows(act_b, v, t, sym, in_edge, e0, f1, row_ptr, col, lane);
+                if (md.mark) mark_rows(act_b, v, t, sym, in_edge, e0, f1, row_ptr, col, lane);
             }
             if (!more) break;
             v = vn;
@@ -672,6 +708,7 @@ __global__ __launch_bounds__(FR_WAVES * 64) FR_OCC void fr_loss_sweep_kernel(
     (void)cnt;
 #endif
     note_improved(last, t, any_imp, lane);
+    count_improved(ctl, t, n_imp, lane);
 }
 
 // ---------------------------------------------------------------- emit
@@ -840,7 +877,7 @@ srt_status run_phase(srt_plan *p, uint32_t t0, uint32_t chunk, F sweep, uint32_t
 // sources a launch.  Returns with the stream drained up to the last emit.
 srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     hipStream_t M = p->stream;
-    const uint32_t V = p->V, per_launch = p->fr_nb * FR_SRC;
+    const uint32_t V = p->V;
     const uint64_t E = p->n_in_edges;
     Chg *chg = reinterpret_cast<Chg *>(p->d_fchg);
     p->p3_launches = 0;
@@ -886,7 +923,22 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
         p->fr_t = 1;
     }
     hipLaunchKernelGGL(fr_stats_init_kernel, dim3(1), dim3(1), 0, M, d_stats);
-    const uint32_t launches = (rows + per_launch - 1) / per_launch;
+    // launches: blocks of 512 rows in equal shares of at most fr_nb blocks;
+    // with symmetric seeding optionally a smaller first launch (fr_first
+    // blocks: the only launch whose latency phase starts from the sources
+    // alone)
+    std::vector<uint32_t> lblk;
+    {
+        const uint32_t blocks = (rows + FR_SRC - 1) / FR_SRC;
+        uint32_t rest = blocks;
+        if (sym && p->fr_first && p->fr_first < blocks) {
+            lblk.push_back(p->fr_first);
+            rest -= p->fr_first;
+        }
+        const uint32_t k = (rest + p->fr_nb - 1) / p->fr_nb;
+        for (uint32_t i = 0; i < k; ++i) lblk.push_back(rest / k + (i < rest % k));
+    }
+    const uint32_t launches = (uint32_t)lblk.size();
     while (p->ev.size() < 2 * (size_t)launches) {
         hipEvent_t ev;
         (void)hipEventCreateWithFlags(&ev, 0);
@@ -894,10 +946,14 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
     }
     const dim3 sgrid(p->fr_grid), sblk(FR_WAVES * 64);
     uint32_t chunk_lat = 12, chunk_loss = 12;
-    for (uint32_t li = 0; li < launches; ++li) {
-        const uint32_t q0 = p->row0 + li * per_launch;
-        const uint32_t nsrc = std::min<uint32_t>(per_launch, p->row1 - q0);
-        const uint32_t NB = (nsrc + FR_SRC - 1) / FR_SRC, B0 = li * p->fr_nb;
+    // dense sweeps past half the launch's items improved, no marks past three
+    // quarters (knob SRT_FR_DENSE=0: A/B)
+    const char *kd = std::getenv("SRT_FR_DENSE");
+    const bool dense_on = !(kd && std::atoi(kd) == 0);
+    for (uint32_t li = 0, B0 = 0; li < launches; B0 += lblk[li++]) {
+        const uint32_t q0 = p->row0 + B0 * FR_SRC;
+        const uint32_t nsrc = std::min<uint32_t>(lblk[li] * FR_SRC, p->row1 - q0);
+        const uint32_t NB = (nsrc + FR_SRC - 1) / FR_SRC;
         uint16_t *L = p->d_fl + (sym ? (uint64_t)B0 * V * FR_SRC : 0);
         const dim3 seed_grid((nsrc + 255) / 256);
         (void)hipEventRecord(p->ev[2 * li], M);
@@ -905,6 +961,10 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
         //    graphs), the sources
         if ((e = hipMemsetAsync(L, 0xff, (size_t)NB * V * FR_SRC * 2, M)) != hipSuccess)
             return hip_err(err, e, "sssp init");
+        const uint64_t items = (uint64_t)NB * V;
+        const uint32_t dmin = dense_on ? (uint32_t)std::min<uint64_t>(items / 2, ~0u) : ~0u;
+        const uint32_t nmin = dense_on ? (uint32_t)std::min<uint64_t>(items * 3 / 4, ~0u) : ~0u;
+        if ((e = hipMemsetAsync(p->d_fctl, 0, 8 * 4, M)) != hipSuccess) return hip_err(err, e, "sssp init");
         uint32_t t0 = ++p->fr_t;
         if (sym && B0 > 0) {
             hipLaunchKernelGGL(fr_sym_copy_kernel, dim3(NB * 8, B0 * 8), dim3(256), 0, M, p->d_fl, p->d_fnodes, perm, V,
@@ -920,7 +980,7 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
         uint32_t t_end = 0, nsw = 0;
         srt_status st = run_phase(p, t0, chunk_lat, [&](uint32_t t) {
             hipLaunchKernelGGL(fr_lat_sweep_kernel, sgrid, sblk, 0, M, p->d_in_ptr, p->d_in_edge, V, NB, L, chg,
-                               p->d_fact, p->d_ffin, p->d_fimp, t, p->fr_symg, p->d_frow_ptr, p->d_fcol);
+                               p->d_fact, p->d_ffin, p->d_fimp, t, p->fr_symg, p->d_frow_ptr, p->d_fcol, p->d_fctl, dmin, nmin);
         }, &t_end, &nsw, err);
         if (st != SRT_OK) return st;
         p->fr_lat_sweeps += nsw;
@@ -934,7 +994,8 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
         if ((e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p->d_fp), 0x40000000u, (size_t)NB * V * FR_SRC,
                                    M)) != hipSuccess ||
             (e = hipMemsetAsync(p->d_fact, 0, (size_t)NB * V * 4, M)) != hipSuccess ||
-            (e = hipMemsetAsync(p->d_fsb, 0, sbytes, M)) != hipSuccess)
+            (e = hipMemsetAsync(p->d_fsb, 0, sbytes, M)) != hipSuccess ||
+            (e = hipMemsetAsync(p->d_fctl, 0, 8 * 4, M)) != hipSuccess)
             return hip_err(err, e, "sssp loss init");
         t0 = t_end + 2;
         hipLaunchKernelGGL(fr_seed_kernel, seed_grid, dim3(256), 0, M, nullptr, p->d_fp, p->d_fsb, chg, p->d_fact,
@@ -957,7 +1018,8 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
             (void)hipMemsetAsync(nxt, 0, sbytes, M);
             hipLaunchKernelGGL(fr_loss_sweep_kernel, sgrid, sblk, 0, M, p->d_in_ptr, p->d_in_edge, V, NB, E,
                                p->d_ftight, p->d_fce, p->d_fcnt, p->d_fp, cur, nxt, p->d_fact, p->d_fimp, t, p->fr_symg, p->d_frow_ptr,
-                               p->d_fcol, dcnt ? dcnt + 4 * std::min<uint32_t>(t - t0, 255) : nullptr);
+                               p->d_fcol, p->d_fctl, dmin, nmin,
+                               dcnt ? dcnt + 4 * std::min<uint32_t>(t - t0, 255) : nullptr);
         }, &t_end, &nsw, err);
         if (st != SRT_OK) return st;
         p->fr_loss_sweeps += nsw;

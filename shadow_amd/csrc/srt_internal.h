@@ -238,6 +238,8 @@ struct srt_plan {
     uint8_t *d_ftight = nullptr;         // fr_nb * n_in_edges * 64 tight-source bytes
     uint2 *d_fce = nullptr;              // fr_nb * n_in_edges compacted tight in-edges (u, 1 - e)
     uint32_t *d_fcnt = nullptr;          // fr_nb * V tight in-edge counts
+    uint32_t fr_first = 0;               // blocks of a smaller first launch (0: equal launches)
+    uint32_t *d_fctl = nullptr;          // 8 sweep-mode words (srt_frontier.hip sweep_mode)
     void *d_fchg = nullptr;              // fr_nb * V change records (srt_frontier.hip Chg, 16 B)
     uint32_t *d_fact = nullptr;          // fr_nb * V activation stamps
     uint8_t *d_ffin = nullptr;           // fr_nb * V: item exact from the start (symmetric seeding)

@@ -17,24 +17,31 @@ pytestmark = pytest.mark.gpu
 SSSP = _lib.SRT_ALGO_SSSP
 
 
-@pytest.fixture(autouse=True, params=["frontier", "frontier-small", "frontier-nosym", "packed", "packed-delta", "packed-fine"])
+@pytest.fixture(autouse=True, params=["frontier", "frontier-small", "frontier-first", "frontier-nosym", "packed",
+                                      "packed-delta", "packed-fine"])
 def sweep_mode(request, monkeypatch):
     """Every test runs the sparse build five ways, all of which must give the
     same bits: the latency-first frontier sweeps (srt_frontier.hip, the default
     when every distance fits u16 units), the same with one 512-source block a
     launch, a 3-workgroup sweep grid and sources in table order (several
     launches share the sweep stamps; waves loop over many chunks; undirected
-    graphs seed each launch from the earlier rows' columns), the same without
-    that symmetric seeding, and the
+    graphs seed each launch from the earlier rows' columns), launches of two
+    blocks after a first launch of one, with the dense sweeps off (unequal
+    launches, buffers larger than a launch; every sweep on its marks), the
+    same without that symmetric seeding, and the
     packed-key sweep (srt_sssp.hip, SRT_SSSP_KEY=64) ungated, with
     delta-stepping at a quarter of the mean in-edge latency and with very narrow
     buckets (factor 0.01: most keys wait in the pending masks)."""
     for k in ("SRT_SSSP_DELTA", "SRT_SSSP_ORDER", "SRT_SSSP_KEY", "SRT_SSSP_FR_NB", "SRT_SSSP_FR_GRID",
-              "SRT_SSSP_SYM"):
+              "SRT_SSSP_SYM", "SRT_FR_FIRST", "SRT_FR_DENSE"):
         monkeypatch.delenv(k, raising=False)
     if request.param == "frontier-nosym":
         monkeypatch.setenv("SRT_SSSP_FR_NB", "1")
         monkeypatch.setenv("SRT_SSSP_SYM", "0")
+    if request.param == "frontier-first":
+        monkeypatch.setenv("SRT_SSSP_FR_NB", "2")
+        monkeypatch.setenv("SRT_FR_FIRST", "1")
+        monkeypatch.setenv("SRT_FR_DENSE", "0")
     if request.param == "frontier-small":
         monkeypatch.setenv("SRT_SSSP_FR_NB", "1")
         monkeypatch.setenv("SRT_SSSP_FR_GRID", "3")
@@ -256,6 +263,8 @@ def test_repeated_runs_same_bits(sweep_mode):
     plan = RoutingPlan(g, nodes, algo=SSSP)
     if sweep_mode == "frontier-small":
         assert "seed=sym" in plan.describe(), plan.describe()
+    if sweep_mode == "frontier-first":
+        assert "seed=sym" in plan.describe() and " first=1 " in plan.describe(), plan.describe()
     ref = None
     for _ in range(3):
         plan.run()
