@@ -434,7 +434,7 @@ __global__ __launch_bounds__(FR_WAVES * 64) void fr_tight_kernel(const uint64_t 
                                                                  uint32_t NB, uint64_t E,
                                                                  const uint16_t *__restrict__ L,
                                                                  uint8_t *__restrict__ tight, uint2 *__restrict__ ce,
-                                                                 uint32_t *__restrict__ cnt) {
+                                                                 uint32_t *__restrict__ cnt, float *__restrict__ P) {
     const int lane = threadIdx.x & 63;
     const uint32_t wave = blockIdx.x * FR_WAVES + (threadIdx.x >> 6), nwaves = gridDim.x * FR_WAVES;
     const uint32_t cpb = (V + 63) / 64, nchunks = cpb * NB;
@@ -445,6 +445,12 @@ __global__ __launch_bounds__(FR_WAVES * 64) void fr_tight_kernel(const uint64_t 
         const uint4 own = Lb[(uint64_t)v * 64 + lane];
         uint8_t *tb = tight + (uint64_t)b * E * 64 + lane;
         uint2 *cb = ce + (uint64_t)b * E;
+        {  // the loss phase starts from P = 2.0 ("not reached"), stored here beside the reads
+            float4 *pv = reinterpret_cast<float4 *>(P + (uint64_t)b * V * FR_SRC) + (uint64_t)v * 128 + 2 * lane;
+            const float4 two = make_float4(2.f, 2.f, 2.f, 2.f);
+            pv[0] = two;
+            pv[1] = two;
+        }
         const uint64_t e0 = in_ptr[v], e1 = in_ptr[v + 1];
         uint64_t j = e0;  // next compacted position (wave-uniform)
         for (uint64_t c0 = e0; c0 < e1; c0 += 64) {
@@ -947,7 +953,8 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
     const dim3 sgrid(p->fr_grid), sblk(FR_WAVES * 64);
     uint32_t chunk_lat = 12, chunk_loss = 12;
     // dense sweeps past half the launch's items improved, no marks past three
-    // quarters (knob SRT_FR_DENSE=0: A/B)
+    // quarters (C4: 0.511 s without, 0.490 with; thresholds 30/60, 25/50 and
+    // 60/85 % measured within 0.5%).  Knob SRT_FR_DENSE=0 (A/B, tests).
     const char *kd = std::getenv("SRT_FR_DENSE");
     const bool dense_on = !(kd && std::atoi(kd) == 0);
     for (uint32_t li = 0, B0 = 0; li < launches; B0 += lblk[li++]) {
@@ -988,12 +995,11 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
         chunk_lat = std::max<uint32_t>(nsw + 1, 4);
         // 2. tight masks
         hipLaunchKernelGGL(fr_tight_kernel, sgrid, sblk, 0, M, p->d_in_ptr, p->d_in_edge, V, NB, E, L, p->d_ftight,
-                           p->d_fce, p->d_fcnt);
-        // 3. loss (activity cleared of the final marks; change bits double-buffered)
+                           p->d_fce, p->d_fcnt, p->d_fp);
+        // 3. loss (P = 2.0 stored by the tight pass; activity cleared of the
+        //    final marks; change bits double-buffered)
         const size_t sbytes = (size_t)NB * V * 64;
-        if ((e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p->d_fp), 0x40000000u, (size_t)NB * V * FR_SRC,
-                                   M)) != hipSuccess ||
-            (e = hipMemsetAsync(p->d_fact, 0, (size_t)NB * V * 4, M)) != hipSuccess ||
+        if ((e = hipMemsetAsync(p->d_fact, 0, (size_t)NB * V * 4, M)) != hipSuccess ||
             (e = hipMemsetAsync(p->d_fsb, 0, sbytes, M)) != hipSuccess ||
             (e = hipMemsetAsync(p->d_fctl, 0, 8 * 4, M)) != hipSuccess)
             return hip_err(err, e, "sssp loss init");
