@@ -27,6 +27,7 @@
 #include <new>
 #include <numeric>
 #include <string>
+#include <queue>
 #include <thread>
 #include <vector>
 
@@ -732,12 +733,23 @@ bool latency_symmetric(const srt_csr *g, const std::vector<uint64_t> &in_ptr, co
     return true;
 }
 
-// Breadth-first discovery rank of every vertex over the adjacency, from the
-// highest-degree vertex (then from the lowest-numbered unvisited one): the
-// sparse sweep puts table rows in this order into its 64-source words, so a
-// word's sources are graph neighbours / siblings whose labels change at the
-// same vertices in the same sweeps (fewer 128-B lines gathered per change).
-std::vector<uint32_t> bfs_rank(const srt_csr *g) {
+// Source order of the sparse sweeps: the level order of a shortest-latency
+// tree from the highest-degree vertex (then from the lowest-numbered vertex
+// not yet reached): the root, its tree children, theirs, ... each parent's
+// children together.  The sweeps put table rows in this order into their
+// words, lanes (8 sources) and 128-B lines (32 sources); sources at the same
+// tree depth under nearby parents reach most targets along paths of the same
+// hop count, so a word's labels change at the same vertices in the same
+// sweeps.  C4's graph (tools measurement on the host, hop counts of the
+// shortest-path trees of 32-source lines over all targets): 3.1 distinct hop
+// counts a line in this order, 9.7 in plain breadth-first order from the same
+// root, 7.5 in tree depth-first order.  Measured on C4: loss sweeps 266 -> 214
+// ms a build; but as the order of the launches (which sources come first) it
+// costs the symmetric seeding (latency sweeps 94 -> 142 ms), so the frontier
+// composes launches in breadth-first order (hop_rank) and orders rows within a
+// launch by this rank.
+// plain breadth-first discovery order from the same root (knob SRT_SSSP_ORDER=2, A/B)
+std::vector<uint32_t> hop_rank(const srt_csr *g) {
     const uint32_t V = g->n_nodes;
     std::vector<uint32_t> rank(V, ~0u), q;
     q.reserve(V);
@@ -750,18 +762,75 @@ std::vector<uint32_t> bfs_rank(const srt_csr *g) {
         if (rank[root] == ~0u) {
             rank[root] = next++;
             q.push_back(root);
-            for (size_t h = q.size() - 1; h < q.size(); ++h) {
-                const uint32_t u = q[h];
-                for (uint64_t k = g->row_ptr[u]; k < g->row_ptr[u + 1]; ++k) {
+            for (size_t h = q.size() - 1; h < q.size(); ++h)
+                for (uint64_t k = g->row_ptr[q[h]]; k < g->row_ptr[q[h] + 1]; ++k) {
                     const uint32_t v = g->col[k];
                     if (v < V && rank[v] == ~0u) {
                         rank[v] = next++;
                         q.push_back(v);
                     }
                 }
-            }
         }
         while (scan < V && rank[scan] != ~0u) ++scan;
+        root = scan;
+    }
+    return rank;
+}
+
+std::vector<uint32_t> spt_rank(const srt_csr *g) {
+    const uint32_t V = g->n_nodes, NONE = ~0u;
+    std::vector<uint32_t> rank(V, NONE), first(V, NONE), last(V, NONE), sib(V, NONE), q;
+    std::vector<uint64_t> dist(V, ~0ull);
+    std::vector<uint32_t> pred(V, NONE);
+    std::vector<uint8_t> done(V, 0);
+    q.reserve(V);
+    uint32_t start = 0;
+    uint64_t best = 0;
+    for (uint32_t u = 0; u < V; ++u)
+        if (g->row_ptr[u + 1] - g->row_ptr[u] > best) best = g->row_ptr[u + 1] - g->row_ptr[u], start = u;
+    typedef std::pair<uint64_t, uint32_t> Item;
+    std::priority_queue<Item, std::vector<Item>, std::greater<Item>> heap;
+    uint32_t next = 0;
+    for (uint32_t root = start, scan = 0; next < V;) {
+        if (rank[root] == NONE) {
+            // Dijkstra over the adjacency's latencies; a vertex joins its
+            // parent's child list when settled (children in settle order)
+            dist[root] = 0;
+            heap.push({0, root});
+            while (!heap.empty()) {
+                const Item it = heap.top();
+                heap.pop();
+                const uint32_t u = it.second;
+                if (done[u] || it.first != dist[u]) continue;
+                done[u] = 1;
+                if (u != root) {
+                    const uint32_t pu = pred[u];
+                    if (last[pu] == NONE) first[pu] = u;
+                    else sib[last[pu]] = u;
+                    last[pu] = u;
+                }
+                for (uint64_t k = g->row_ptr[u]; k < g->row_ptr[u + 1]; ++k) {
+                    const uint32_t v = g->col[k];
+                    if (v >= V || done[v]) continue;
+                    const uint64_t d = it.first + g->lat_ns[k];
+                    if (d < dist[v]) {
+                        dist[v] = d;
+                        pred[v] = u;
+                        heap.push({d, v});
+                    }
+                }
+            }
+            // the tree's level order
+            q.clear();
+            q.push_back(root);
+            rank[root] = next++;
+            for (size_t h = 0; h < q.size(); ++h)
+                for (uint32_t c = first[q[h]]; c != NONE; c = sib[c]) {
+                    rank[c] = next++;
+                    q.push_back(c);
+                }
+        }
+        while (scan < V && rank[scan] != NONE) ++scan;
         root = scan;
     }
     return rank;
@@ -1180,8 +1249,16 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         std::vector<srt::InEdge> in_edge;
         build_in_edges(g, p->sssp_g, n_in, &in_ptr, &in_edge);
         // source order of the sweep's words (knob SRT_SSSP_ORDER=0: table order)
-        if (!(std::getenv("SRT_SSSP_ORDER") && std::atoi(std::getenv("SRT_SSSP_ORDER")) == 0))
-            p->h_bfs_rank = bfs_rank(g);
+        {
+            const char *ko = std::getenv("SRT_SSSP_ORDER");
+            const int om = ko ? std::atoi(ko) : 1;
+            // 1: launches in breadth-first order, rows within a launch in
+            // shortest-latency-tree level order (frontier sweeps); 2: breadth-first
+            // only; 3: tree level order only (A/B)
+            if (om == 1 || om == 2) p->h_bfs_rank = hop_rank(g);
+            if (om == 3) p->h_bfs_rank = spt_rank(g);
+            if (om == 1) p->h_spt_rank = spt_rank(g);
+        }
         PLAN_TRY(dmalloc(&p->d_in_ptr, in_ptr.size(), err));
         PLAN_TRY(dmalloc(&p->d_in_edge, in_edge.size(), err));
         // latency-first frontier sweeps (srt_frontier.hip) when every finite

@@ -897,6 +897,21 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
     // the BFS source order of this rank's rows and, per vertex, the block in
     // which it is a source (built once per row range), uploaded on the plan's
     // stream from host copies the plan keeps
+    // launches: blocks of 512 rows in equal shares of at most fr_nb blocks;
+    // with symmetric seeding optionally a smaller first launch (fr_first
+    // blocks: the only launch whose latency phase starts from the sources
+    // alone)
+    std::vector<uint32_t> lblk;
+    {
+        const uint32_t blocks = (rows + FR_SRC - 1) / FR_SRC;
+        uint32_t rest = blocks;
+        if (sym && p->fr_first && p->fr_first < blocks) {
+            lblk.push_back(p->fr_first);
+            rest -= p->fr_first;
+        }
+        const uint32_t k = (rest + p->fr_nb - 1) / p->fr_nb;
+        for (uint32_t i = 0; i < k; ++i) lblk.push_back(rest / k + (i < rest % k));
+    }
     const uint32_t *perm = nullptr;
     if (p->row1 > p->row0 && (!p->d_fdone || p->sperm_r0 != p->row0 || p->sperm_r1 != p->row1)) {
         const bool bfs = !p->h_bfs_rank.empty();
@@ -906,6 +921,16 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
             std::stable_sort(p->h_sperm.begin() + p->row0, p->h_sperm.begin() + p->row1, [&](uint32_t a, uint32_t b) {
                 return p->h_bfs_rank[p->nodes[a]] < p->h_bfs_rank[p->nodes[b]];
             });
+            // within each launch: shortest-latency-tree level order (srt_api.cpp
+            // spt_rank), so a lane's and a line's sources change together
+            if (!p->h_spt_rank.empty())
+                for (uint32_t li = 0, q = 0; li < lblk.size(); q += lblk[li++] * FR_SRC) {
+                    auto b0 = p->h_sperm.begin() + p->row0 + q;
+                    auto b1 = p->h_sperm.begin() + p->row0 + std::min<uint32_t>(rows, q + lblk[li] * FR_SRC);
+                    std::stable_sort(b0, b1, [&](uint32_t a, uint32_t b) {
+                        return p->h_spt_rank[p->nodes[a]] < p->h_spt_rank[p->nodes[b]];
+                    });
+                }
         }
         p->h_fdone.assign(V, ~0u);
         for (uint32_t q = 0; q < rows; ++q)
@@ -929,21 +954,6 @@ srt_status frontier_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) 
         p->fr_t = 1;
     }
     hipLaunchKernelGGL(fr_stats_init_kernel, dim3(1), dim3(1), 0, M, d_stats);
-    // launches: blocks of 512 rows in equal shares of at most fr_nb blocks;
-    // with symmetric seeding optionally a smaller first launch (fr_first
-    // blocks: the only launch whose latency phase starts from the sources
-    // alone)
-    std::vector<uint32_t> lblk;
-    {
-        const uint32_t blocks = (rows + FR_SRC - 1) / FR_SRC;
-        uint32_t rest = blocks;
-        if (sym && p->fr_first && p->fr_first < blocks) {
-            lblk.push_back(p->fr_first);
-            rest -= p->fr_first;
-        }
-        const uint32_t k = (rest + p->fr_nb - 1) / p->fr_nb;
-        for (uint32_t i = 0; i < k; ++i) lblk.push_back(rest / k + (i < rest % k));
-    }
     const uint32_t launches = (uint32_t)lblk.size();
     while (p->ev.size() < 2 * (size_t)launches) {
         hipEvent_t ev;

@@ -206,6 +206,7 @@ struct srt_plan {
     // sparse SSSP (algo == SRT_ALGO_SSSP, srt_sssp.hip)
     uint64_t *d_in_ptr = nullptr;        // V + 1
     std::vector<uint32_t> h_bfs_rank;    // BFS discovery rank per vertex (empty: table order)
+    std::vector<uint32_t> h_spt_rank;    // shortest-latency-tree level rank (frontier: order within a launch)
     uint32_t *d_sperm = nullptr;         // n: sweep slot q -> table row (rows [sperm_r0, sperm_r1) permuted)
     uint32_t sperm_r0 = 0, sperm_r1 = 0;
     srt::InEdge *d_in_edge = nullptr;    // n_in_edges (self-loops dropped)
