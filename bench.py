@@ -641,7 +641,7 @@ def bench_graph(args, cfg, D):
                 schedule = {"state": "frontier-u16", "blocks": int(desc.split(" blocks=")[1].split()[0]),
                             "first": int(desc.split(" first=")[1].split()[0]) if " first=" in desc else 0,
                             "seed": desc.split(" seed=")[1].split()[0],
-                            "source_order": "bfs" if "order=bfs" in desc else "table"}
+                            "source_order": desc.split(" order=")[1].split()[0]}
                 traffic, traffic_src = frontier_traffic(args, schedule, launches_per_step)
                 kernel = ("fr_lat_sweep_kernel + fr_tight_kernel + fr_loss_sweep_kernel: every sweep of one launch "
                           "(its blocks of 512 sources)")
@@ -650,7 +650,7 @@ def bench_graph(args, cfg, D):
                 state = desc.split("state=")[1].split()[0] if "state=" in desc else "keys"
                 schedule = {"state": state,
                             "words_per_lane": int(desc.split(" R=")[1].split()[0]) if " R=" in desc else 0,
-                            "source_order": "bfs" if "order=bfs" in desc else "table"}
+                            "source_order": desc.split(" order=")[1].split()[0]}
                 per_sweep, traffic_src = measured_traffic(args, "(sssp_sweep)", schedule)
                 traffic = per_sweep * sweeps_per_launch if per_sweep else None
                 kernel = "sssp_sweep_kernel (all sweeps of one launch)"

@@ -1379,7 +1379,9 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
                           "sssp:frontier u16|f32 g=%llu lmax=%llu%s V=%u n=%u E_in=%llu blocks=%u first=%u order=%s seed=%s",
                           (unsigned long long)p->sssp_g, (unsigned long long)(ecc_units != ~0ull ? ecc_units : 0),
                           ecc_units != ~0ull ? "(ecc)" : "(V-1)", p->V, p->n, (unsigned long long)p->n_in_edges,
-                          p->fr_nb, p->fr_first, p->h_bfs_rank.empty() ? "table" : "bfs", p->fr_sym ? "sym" : "none");
+                          p->fr_nb, p->fr_first,
+                          p->h_bfs_rank.empty() ? "table" : p->h_spt_rank.empty() ? "bfs" : "bfs+tree",
+                          p->fr_sym ? "sym" : "none");
             p->desc = df;
         }
         if (p->sssp_act_on && !p->sssp_frontier)
