@@ -1,12 +1,9 @@
 #!/bin/bash
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out/s50
-timeout -k 10 1000 python3 -u -m pytest -q --timeout 300 --timeout-method thread tests -m gpu > gpurun_out/s50/gpu_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/s50/gpu_tests.log; exit 1; }
-tail -2 gpurun_out/s50/gpu_tests.log
-timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/s50/smoke.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/s50/smoke.log; exit 1; }
-tail -1 gpurun_out/s50/smoke.log
-timeout -k 10 300 python3 -u bench.py --config c4 --steps 5 --warmup 1 > gpurun_out/s50/c4.json 2> gpurun_out/s50/c4.err || { echo "bench failed"; tail -5 gpurun_out/s50/c4.err; exit 1; }
-tail -1 gpurun_out/s50/c4.json | cut -c1-200
-timeout -k 10 300 python3 -u bench.py > gpurun_out/s50/c3.json 2> gpurun_out/s50/c3.err || { echo "bench c3 failed"; tail -5 gpurun_out/s50/c3.err; exit 1; }
-tail -1 gpurun_out/s50/c3.json | cut -c1-200
+mkdir -p gpurun_out/s52
+for v in new head new head; do
+lib=$GRAFT_REPO_ROOT/shadow_amd/libsrt.so; [ $v = head ] && lib=$GRAFT_REPO_ROOT/tools/diag/libsrt_head.so
+SRT_LIB=$lib timeout -k 10 300 python3 -u bench.py --config c4 --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --no-cold > gpurun_out/s52/$v.json 2> gpurun_out/s52/$v.err || { echo "bench $v failed"; tail -5 gpurun_out/s52/$v.err; exit 1; }
+python3 -c "import json; d=json.loads(open('gpurun_out/s52/$v.json').read().strip().splitlines()[-1]); print('$v', d['ms_per_step'], d['roofline'].get('sweeps_per_launch'))"
+done
