@@ -3041,11 +3041,18 @@ srt_status level_csr(srt_plan *p, uint64_t wmax, bool with_loss, srt_err *err) {
 // Workgroups of a level solve launch over `rows` rows (one row per
 // workgroup at a time; the LDS row decides how many fit a CU)
 uint32_t level_grid(int device, uint32_t V, bool quant, uint32_t rows, uint32_t *nt_out) {
-    const uint32_t nt = V >= 2048 ? LOSS_NT : 256;
     const size_t lds = quant ? SOLVE_HIST + (size_t)V * 8
                              : SOLVE_HIST + (((size_t)V * 2 + 15) & ~(size_t)15) + (size_t)V * 4 +
                                    (((size_t)V * 2 + 15) & ~(size_t)15);
-    const int per_cu = std::max(1, std::min(2048 / (int)nt, (int)std::max<size_t>(1, (160 * 1024) / (lds + 2048))));
+    // workgroups a CU's LDS holds, then the fewest threads a workgroup (256,
+    // 512 or 1024) that still fill the CU's 2,048 thread slots: more rows in
+    // flight a CU for small graphs (C2, 4k: 4 x 512 threads 0.39 ms a solve
+    // against 2 x 1024 0.50 ms; 4 x 256 0.39), one 1,024-thread workgroup for
+    // C3's 128 KB rows
+    const int lds_cu = (int)std::max<size_t>(1, (160 * 1024) / (lds + 2048));
+    uint32_t nt = 256;
+    while (nt < LOSS_NT && (int)(2048 / nt) > lds_cu) nt *= 2;
+    const int per_cu = std::max(1, std::min(2048 / (int)nt, lds_cu));
     if (nt_out) *nt_out = nt;
     return std::max<uint32_t>(1, std::min<uint32_t>(rows, (uint32_t)(cu_count(device) * per_cu)));
 }
