@@ -232,6 +232,9 @@ def test_sweep_family_is_reported(sweep_mode):
     d = plan.describe()
     if sweep_mode.startswith("frontier"):
         assert d.startswith("sssp:frontier u16") and "(ecc)" in d, d
+        # source order: launches breadth-first, rows within them in
+        # shortest-latency-tree level order (table order when forced)
+        assert (" order=table " in d) if sweep_mode == "frontier-small" else (" order=bfs+tree " in d), d
     else:
         delta = int(d.split(" delta=")[1].split()[0])
         assert (delta == 0) == (sweep_mode == "packed"), d
