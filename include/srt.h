@@ -15,6 +15,14 @@
  *                                  src/main/core/worker.rs:326-410 (+ :539-553)
  *   srt_gml_parse               <- NetworkGraph::parse / gml_parser::parse
  *                                  src/main/network/graph/mod.rs:134-181
+ *   srt_gml_parse_file          <- load_network_graph + read_xz
+ *                                  src/main/network/graph/mod.rs:479-509
+ *   srt_ip_assignment_* / srt_ip_resolver_* / srt_packet_batch_ip
+ *                               <- IpAssignment (mod.rs:352-420) and the
+ *                                  send path's lookups (worker.rs:539-553)
+ *   srt_xoshiro_* / srt_host_node_seed
+ *                               <- Host::random (host.rs:122, 233) seeding
+ *                                  (sim_config.rs:47-53, 222-244)
  *   srt_routing_info_*          <- generate_routing_info + RoutingInfo
  *                                  src/main/core/sim_config.rs:424-461,
  *                                  src/main/network/graph/mod.rs:428-477
@@ -41,7 +49,7 @@
 extern "C" {
 #endif
 
-#define SRT_ABI_VERSION 3
+#define SRT_ABI_VERSION 4
 
 typedef enum {
     SRT_OK = 0,
@@ -286,6 +294,77 @@ srt_status srt_packet_events(srt_plan *plan, const uint32_t *d_host_pkt_ptr, uin
  * returns SRT_OK; else SRT_OK. */
 srt_status srt_packet_events_status(srt_plan *plan, srt_err *err);
 
+/* ---------------------------------------------------- IP assignment (a10) */
+/* IpAssignment<u32> (src/main/network/graph/mod.rs:352-420): IPv4 address ->
+ * GML node id.  Addresses cross the ABI in network byte order, as Shadow's C
+ * exports pass them (in_addr_t, worker.rs:669-700).  Single-threaded use
+ * (sim_config.rs:399-420 fills it once, on the main thread). */
+typedef struct srt_ip_assignment srt_ip_assignment;
+srt_status srt_ip_assignment_create(srt_ip_assignment **out);
+void srt_ip_assignment_destroy(srt_ip_assignment *ia);
+/* assign_ip (mod.rs:383-394): SRT_ERR_INVALID "IP address has already been
+ * assigned" (IpPreviouslyAssignedError) when the address is taken */
+srt_status srt_ip_assignment_assign_ip(srt_ip_assignment *ia, uint32_t node_id, uint32_t ipv4_be, srt_err *err);
+/* assign (mod.rs:371-381): the next free address after the last one assign
+ * handed out, from 11.0.0.1 upward, skipping *.0 and *.255 (:406-420);
+ * returns it (network byte order) */
+uint32_t srt_ip_assignment_assign(srt_ip_assignment *ia, uint32_t node_id);
+/* get_node (mod.rs:397-399): 1 and *node_id, or 0 (None) */
+int srt_ip_assignment_get_node(const srt_ip_assignment *ia, uint32_t ipv4_be, uint32_t *node_id);
+/* get_nodes (mod.rs:402-404): the distinct assigned node ids, ascending, up to
+ * cap of them into out (may be NULL); returns how many there are */
+uint32_t srt_ip_assignment_get_nodes(const srt_ip_assignment *ia, uint32_t *out, uint32_t cap);
+uint32_t srt_ip_assignment_size(const srt_ip_assignment *ia);
+
+/* The assignment frozen against a routing table for the send path: IPv4 ->
+ * table row (the row of the address's node; row_ids[i] = GML id of table row
+ * i, e.g. the in-use nodes in srt_routing_info / srt_plan order).  Replaces the
+ * two get_node lookups + the path() hash of every WorkerShared::latency /
+ * reliability call (worker.rs:539-553).  Immutable: thread-safe. */
+typedef struct srt_ip_resolver srt_ip_resolver;
+srt_status srt_ip_resolver_create(const srt_ip_assignment *ia, const uint32_t *row_ids, uint32_t n_rows,
+                                  srt_ip_resolver **out, srt_err *err);
+void srt_ip_resolver_destroy(srt_ip_resolver *r);
+/* host batch: rows[i] = table row of ips_be[i], -1 when the address is not
+ * assigned or its node has no row (the reference's None) */
+srt_status srt_ip_resolve_rows(const srt_ip_resolver *r, const uint32_t *ips_be, uint64_t n, int32_t *rows);
+
+/* A packet by address: srt_pkt with the table row / column replaced by the
+ * source / destination IPv4 (network byte order, packet_getSourceIP /
+ * packet_getDestinationIP, worker.rs:341-345).  Same 24-byte layout. */
+typedef struct {
+    uint32_t src_host;
+    uint32_t src_ip;
+    uint32_t dst_ip;
+    uint32_t payload_size;
+    uint64_t t_ns;
+} srt_pkt_ip;
+/* srt_packet_batch with each packet's addresses resolved on the device
+ * through `res` (its table is uploaded to the plan's device on first use).
+ * Asynchronous like srt_packet_batch: a packet that is not completed and has
+ * an address without a row (the reference's reliability(..).unwrap() panic,
+ * worker.rs:359) is reported by the next srt_packet_status. */
+srt_status srt_packet_batch_ip(srt_plan *plan, srt_ip_resolver *res, const srt_pkt_ip *d_pkts,
+                               const uint32_t *d_host_pkt_ptr, uint32_t n_hosts, uint64_t n_pkts, uint64_t *d_rng,
+                               const srt_round *round, uint32_t *d_flags, uint64_t *d_deliver, uint64_t *d_counters,
+                               uint64_t *d_stats, srt_err *err);
+/* Synchronises the plan's stream; SRT_ERR_INVALID if an srt_packet_batch_ip
+ * since the last check met an unresolvable address, else SRT_OK. */
+srt_status srt_packet_status(srt_plan *plan, srt_err *err);
+
+/* ------------------------------------------------------ host RNG (a12) */
+/* The host's Xoshiro256PlusPlus (host.rs:122, 233; rand_xoshiro 0.6.0) as the
+ * 4 x u64 state srt_packet_batch advances.  Host-side helpers so the caller
+ * can seed states, continue a stream on the host (the syscalls' draws,
+ * host.rs:1373-1385) and check the hand-off; see INTEGRATION.md section 4. */
+/* seed_from_u64 (SplitMix64 outputs as the four words) */
+void srt_xoshiro_seed_from_u64(uint64_t seed, uint64_t state[4]);
+/* count next_u64 draws (out may be NULL), state advanced in place */
+void srt_xoshiro_next_u64(uint64_t state[4], uint64_t count, uint64_t *out);
+/* a host's node_seed (sim_config.rs:47-53, 222-244): the first next_u64 of
+ * seed_from_u64(general_seed) ^ DefaultHasher(hostname) (SipHash-1-3) */
+uint64_t srt_host_node_seed(uint32_t general_seed, const char *hostname, size_t len);
+
 /* ------------------------------------------------------------- RoutingInfo */
 /* Dense RoutingInfo keyed by GML node ids: replaces the
  * HashMap<(u32,u32), PathProperties> and the RwLock<HashMap> packet counters of
@@ -364,6 +443,18 @@ typedef struct srt_gml srt_gml;
 srt_status srt_gml_parse(const char *text, size_t len, srt_gml **out, srt_err *err);
 srt_status srt_gml_csr(const srt_gml *g, srt_csr *csr);
 void srt_gml_free(srt_gml *g);
+
+/* load_network_graph's file sources (mod.rs:494-509) + NetworkGraph::parse:
+ * reads `path`, decompresses it when xz != 0 (read_xz, mod.rs:479-492: the
+ * .xz container with LZMA2 blocks and CRC32 / CRC64 / SHA-256 / no checks,
+ * what lzma-rs 0.3.0 decodes), checks UTF-8 (String::from_utf8) and parses.
+ * Errors carry the reference's contexts: "Failed to open file: \"{path}\""
+ * / "Failed to read file: {path}" / "Failed to decompress file: ...". */
+srt_status srt_gml_parse_file(const char *path, int xz, srt_gml **out, srt_err *err);
+/* read_xz's decompression alone: *out (library-allocated, free with srt_free,
+ * NUL-terminated for convenience) holds *out_len decompressed bytes */
+srt_status srt_xz_decompress(const uint8_t *in, size_t len, uint8_t **out, size_t *out_len, srt_err *err);
+void srt_free(void *p);
 
 #ifdef __cplusplus
 }

@@ -115,6 +115,42 @@ class OracleError(Exception):
         self.code, self.a_id, self.b_id = code, a_id, b_id
 
 
+# ------------------------------------------------------------ IpAssignment
+class IpAssignment:
+    """Restatement of IpAssignment<u32> (src/main/network/graph/mod.rs:352-420),
+    addresses as host-order u32: a dict map, last_assigned_addr from 11.0.0.0
+    (:366), assign loops increment_address (:406-420, skip *.0 / *.255) until a
+    vacant entry (:371-381), assign_ip refuses an occupied one (:383-394)."""
+
+    def __init__(self):
+        self.map = {}
+        self.last = 11 << 24
+
+    def assign(self, node_id: int) -> int:
+        while True:
+            x = self.last
+            while True:
+                x += 1
+                if x & 0xFF not in (0, 255):
+                    break
+            self.last = x
+            if x not in self.map:
+                self.map[x] = node_id
+                return x
+
+    def assign_ip(self, node_id: int, ip: int) -> bool:
+        if ip in self.map:
+            return False  # IpPreviouslyAssignedError
+        self.map[ip] = node_id
+        return True
+
+    def get_node(self, ip: int):
+        return self.map.get(ip)
+
+    def get_nodes(self) -> set:
+        return set(self.map.values())
+
+
 # ---------------------------------------------------------------- RNG / units
 def xoshiro_seed(seed: int) -> np.ndarray:
     s = np.zeros(4, np.uint64)

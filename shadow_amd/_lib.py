@@ -133,6 +133,26 @@ SIGNATURES = {
     "srt_gml_parse": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(_vp), _errp]),
     "srt_gml_csr": (C.c_int, [_vp, C.POINTER(SrtCsr)]),
     "srt_gml_free": (None, [_vp]),
+    "srt_gml_parse_file": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(_vp), _errp]),
+    "srt_xz_decompress": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(C.c_size_t),
+                                    _errp]),
+    "srt_free": (None, [_vp]),
+    "srt_ip_assignment_create": (C.c_int, [C.POINTER(_vp)]),
+    "srt_ip_assignment_destroy": (None, [_vp]),
+    "srt_ip_assignment_assign_ip": (C.c_int, [_vp, C.c_uint32, C.c_uint32, _errp]),
+    "srt_ip_assignment_assign": (C.c_uint32, [_vp, C.c_uint32]),
+    "srt_ip_assignment_get_node": (C.c_int, [_vp, C.c_uint32, _u32p]),
+    "srt_ip_assignment_get_nodes": (C.c_uint32, [_vp, _u32p, C.c_uint32]),
+    "srt_ip_assignment_size": (C.c_uint32, [_vp]),
+    "srt_ip_resolver_create": (C.c_int, [_vp, _u32p, C.c_uint32, C.POINTER(_vp), _errp]),
+    "srt_ip_resolver_destroy": (None, [_vp]),
+    "srt_ip_resolve_rows": (C.c_int, [_vp, _u32p, C.c_uint64, C.POINTER(C.c_int32)]),
+    "srt_packet_batch_ip": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, C.c_uint64, _vp, C.POINTER(SrtRound), _vp,
+                                      _vp, _vp, _vp, _errp]),
+    "srt_packet_status": (C.c_int, [_vp, _errp]),
+    "srt_xoshiro_seed_from_u64": (None, [C.c_uint64, _u64p]),
+    "srt_xoshiro_next_u64": (None, [_u64p, C.c_uint64, _u64p]),
+    "srt_host_node_seed": (C.c_uint64, [C.c_uint32, C.c_char_p, C.c_size_t]),
 }
 
 
@@ -156,7 +176,7 @@ def lib():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
-        if L.srt_abi_version() != 3:
+        if L.srt_abi_version() != 4:
             raise SrtError(SRT_ERR_UNSUPPORTED, "libsrt ABI version mismatch")
         _lib = L
     return _lib

@@ -568,6 +568,8 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_rowslots);
     hipFree(p->d_fbuf);
     hipFree(p->d_draws);
+    hipFree(p->d_pkt_tab);
+    hipFree(p->d_pkt_bad);
     hipFree(p->d_in_ptr);
     hipFree(p->d_sperm);
     hipFree(p->d_in_edge);
@@ -1684,6 +1686,7 @@ srt_status srt_plan_run_async(srt_plan *p, srt_err *err) {
         set_err(err, SRT_ERR_INVALID, "null plan");
         return SRT_ERR_INVALID;
     }
+    ++p->run_no;  // the packet stage's packed table is stale from here
     srt_status st = run_closure(p, err);
     if (st == SRT_OK) st = run_tail(p, err);
     return st;

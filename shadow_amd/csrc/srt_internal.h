@@ -59,9 +59,37 @@ struct InEdge {
     uint32_t pad;
 };
 
+// IPv4 (host order) -> table row of the packet stage (srt_ip.cpp): a direct
+// array over [base, base + span) (mode 1) or open addressing over 1 << bits
+// slots {ip << 32 | row + 1} (mode 2, 0 = empty); -1 = no row
+constexpr int MAX_DEVICES = 64;
+struct IpTable {
+    uint32_t mode, base, span, bits;
+    const int32_t *direct;
+    const uint64_t *hash;
+};
+__host__ __device__ inline uint64_t ip_hash(uint32_t ip, uint32_t bits) {
+    return (uint64_t)((ip * 0x9E3779B1u) >> (32 - bits));
+}
+__host__ __device__ inline int32_t ip_lookup(const IpTable &t, uint32_t ip) {
+    if (t.mode == 1) {
+        const uint32_t k = ip - t.base;
+        return k < t.span ? t.direct[k] : -1;
+    }
+    const uint64_t mask = (1ull << t.bits) - 1;
+    for (uint64_t s = ip_hash(ip, t.bits);; s = (s + 1) & mask) {
+        const uint64_t v = t.hash[s];
+        if (!v) return -1;
+        if ((uint32_t)(v >> 32) == ip) return (int32_t)(uint32_t)v - 1;
+    }
+}
+
 }  // namespace srt
 
+struct srt_ip_resolver;
 namespace srt {
+// the resolver's table on `device` (uploaded on first use)
+srt_status ip_table_device(srt_ip_resolver *r, int device, IpTable *out, srt_err *err);
 struct LocalGroup;  // srt_comm.cpp: the ranks of one process (srt_comm_init_local)
 constexpr int MAX_LOCAL_RANKS = 16;
 // source buffers of one in-process collective, by rank (a kernel argument)
@@ -167,8 +195,12 @@ struct srt_plan {
     srt_path *d_pack = nullptr;             // AoS staging for fetch
     void *d_pack8 = nullptr;                // 8-byte staging of the compact end-to-end download
     uint32_t *d_up32 = nullptr;             // u32 latency slots of the piece-pipelined upload
-    uint64_t *d_draws = nullptr;            // packet stage: one RNG draw per packet
-    uint64_t draws_cap = 0;
+    uint64_t *d_draws = nullptr;            // packet stage: one RNG draw per packet (a host block's
+    uint64_t draws_cap = 0;                 // draws overflowing its LDS) + per-block minima
+    uint4 *d_pkt_tab = nullptr;             // packet stage: the table as 16-B {latency, loss} records
+    uint64_t pkt_tab_run = 0;               // ... packed from the build numbered run_no (0: none)
+    uint64_t run_no = 0;                    // builds of this plan (srt_plan_run_async)
+    uint32_t *d_pkt_bad = nullptr;          // packet stage: bit 0 = a packet's address had no row
     void *d_ev_scratch = nullptr;           // packet events: per-destination counts + cursors
     uint32_t *d_ev_bad = nullptr;    // srt_packet_events: bit 0 a destination out of range, bit 2 a group over EV_CAP
     struct EvCall {                  // the last srt_packet_events call (exact fallback)

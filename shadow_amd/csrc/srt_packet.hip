@@ -10,9 +10,21 @@
 //   drop iff !(t < bootstrap_end) && chance >= reliability && payload > 0
 //   else: delay = latency; counter++; SENT; deliver = max(t + delay, round_end)
 //
-// Two kernels: (A) one lane per host walks its packets and advances its
-// xoshiro256++ state -- the only sequential part, ~20 integer ops per draw;
-// (B) one lane per packet does the table gather and the decision, HBM-bound.
+// One kernel a round (round_kernel): a workgroup takes HB consecutive source
+// hosts.  Phase 1: one lane per host walks its packets in send order and
+// advances its xoshiro256++ state -- the only sequential part, a dependent
+// chain of ~20 integer ops a draw -- leaving the draws in LDS.  Phase 2: the
+// workgroup's 256 lanes decide the block's packets from those draws: one 16-B
+// gather of the packed {latency, loss} table record (packed once per build),
+// the drop rule, the deliver-time clamp, the per-path counter, block minima.
+// The draws never travel through HBM (a block whose packets overflow its LDS
+// keeps them in a global scratch instead).  The host walks of the other
+// resident workgroups overlap each block's chain.
+//
+// The packet's table row and column come either from srt_pkt (resolved by the
+// caller) or, in srt_packet_batch_ip, from its IPv4 addresses through the
+// frozen IpAssignment (srt_ip.cpp): the reference's per-packet
+// ip_assignment.get_node + routing_info.path lookups (worker.rs:539-553).
 #include <cstdlib>
 #include <cstring>
 
@@ -20,11 +32,10 @@
 
 namespace {
 
-__device__ __forceinline__ uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+__host__ __device__ __forceinline__ uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
 
 // rand_xoshiro 0.6.0 Xoshiro256PlusPlus::next_u64
-__device__ __forceinline__ uint64_t xoshiro_next(uint64_t &s0, uint64_t &s1, uint64_t &s2,
-                                                 uint64_t &s3) {
+__host__ __device__ __forceinline__ uint64_t xoshiro_next(uint64_t &s0, uint64_t &s1, uint64_t &s2, uint64_t &s3) {
     const uint64_t r = rotl(s0 + s3, 23) + s0;
     const uint64_t t = s1 << 17;
     s2 ^= s0;
@@ -36,99 +47,153 @@ __device__ __forceinline__ uint64_t xoshiro_next(uint64_t &s0, uint64_t &s1, uin
     return r;
 }
 
-// One lane per host; the walk is a dependent chain per lane, so the grid is
-// spread thin (DT threads per block: 10k hosts -> 157 CUs at DT = 64, not 40)
-// and the send times are fetched PF at a time (independent loads in flight)
-// so the walk is not one memory latency per packet.
-template <int DT, int PF>
-__global__ __launch_bounds__(DT) void draw_kernel(const srt_pkt *__restrict__ pkts,
-                                                  const uint32_t *__restrict__ host_ptr, uint32_t n_hosts,
-                                                  uint64_t *__restrict__ rng, uint64_t sim_end,
-                                                  uint64_t *__restrict__ draws) {
-    const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
-    if (h >= n_hosts) return;
-    uint64_t s0 = rng[4 * (uint64_t)h], s1 = rng[4 * (uint64_t)h + 1];
-    uint64_t s2 = rng[4 * (uint64_t)h + 2], s3 = rng[4 * (uint64_t)h + 3];
-    const uint32_t b = host_ptr[h], e = host_ptr[h + 1];
-    for (uint32_t p0 = b; p0 < e; p0 += PF) {
-        uint64_t tt[PF];
-#pragma unroll
-        for (int q = 0; q < PF; ++q) tt[q] = p0 + q < e ? pkts[p0 + q].t_ns : 0;
-#pragma unroll
-        for (int q = 0; q < PF; ++q) {
-            if (p0 + q >= e || tt[q] >= sim_end) continue;  // completed: no draw
-            draws[p0 + q] = xoshiro_next(s0, s1, s2, s3);
-        }
+constexpr int RT = 256;          // threads a round workgroup
+constexpr int HB = 8;            // source hosts a workgroup (C5: 1,250 workgroups, ~800 packets each)
+constexpr uint32_t DCAP = 3072;  // draws a workgroup keeps in LDS (24 KB)
+constexpr int PF = 16;           // send times in flight a host walk
+
+// the packet's (row, column) of the table: resolved by the caller, or from its
+// addresses (network byte order); -1 when an address has no row
+template <bool IP>
+__device__ __forceinline__ void pkt_rows(const srt_pkt &k, const srt::IpTable &ipt, int32_t &i, int32_t &j) {
+    if (IP) {
+        i = srt::ip_lookup(ipt, __builtin_bswap32(k.src_row));
+        j = srt::ip_lookup(ipt, __builtin_bswap32(k.dst_row));
+    } else {
+        i = (int32_t)k.src_row;
+        j = (int32_t)k.dst_row;
     }
-    rng[4 * (uint64_t)h] = s0;
-    rng[4 * (uint64_t)h + 1] = s1;
-    rng[4 * (uint64_t)h + 2] = s2;
-    rng[4 * (uint64_t)h + 3] = s3;
 }
 
-constexpr int DECIDE_THREADS = 256;
-
-__global__ __launch_bounds__(DECIDE_THREADS) void decide_kernel(const srt_pkt *__restrict__ pkts, uint64_t n_pkts,
-                              const uint64_t *__restrict__ draws,
-                              const uint64_t *__restrict__ lat, const float *__restrict__ loss,
-                              uint32_t n, srt_round r, uint32_t *__restrict__ flags,
-                              uint64_t *__restrict__ deliver, unsigned long long *counters,
-                              unsigned long long *__restrict__ partial) {
+template <bool IP, bool TAB16>
+__global__ __launch_bounds__(RT) void round_kernel(const srt_pkt *__restrict__ pkts,
+                                                   const uint32_t *__restrict__ host_ptr, uint32_t n_hosts,
+                                                   uint64_t *__restrict__ rng, srt_round r,
+                                                   const uint4 *__restrict__ tab, const uint64_t *__restrict__ lat,
+                                                   const float *__restrict__ loss, uint32_t n, srt::IpTable ipt,
+                                                   uint32_t *__restrict__ flags, uint64_t *__restrict__ deliver,
+                                                   unsigned long long *counters,
+                                                   unsigned long long *__restrict__ partial,
+                                                   uint64_t *__restrict__ gdraws, uint32_t *__restrict__ bad) {
+    __shared__ uint64_t sdraw[DCAP];
+    __shared__ uint32_t sptr[HB + 1];
+    __shared__ unsigned long long red[2][RT / 64];
+    const uint32_t t = threadIdx.x;
+    const uint32_t h0 = blockIdx.x * HB;
+    const uint32_t nh = min((uint32_t)HB, n_hosts - h0);
+    if (t <= nh) sptr[t] = host_ptr[h0 + t];
+    __syncthreads();
+    const uint32_t pb = sptr[0], pe = sptr[nh];
+    const bool in_lds = pe - pb <= DCAP;
+    // phase 1: host i walked by lane i / 4 of wave i % 4 (the chains spread over the SIMDs)
+    {
+        const uint32_t i = (t & 63) * 4 + (t >> 6);
+        if ((t & 63) < (HB + 3) / 4 && i < nh) {
+            const uint64_t h = h0 + i;
+            uint64_t s0 = rng[4 * h], s1 = rng[4 * h + 1], s2 = rng[4 * h + 2], s3 = rng[4 * h + 3];
+            const uint32_t b = sptr[i], e = sptr[i + 1];
+            for (uint32_t p0 = b; p0 < e; p0 += PF) {
+                uint64_t tt[PF];
+#pragma unroll
+                for (int q = 0; q < PF; ++q) tt[q] = p0 + q < e ? pkts[p0 + q].t_ns : ~0ull;
+#pragma unroll
+                for (int q = 0; q < PF; ++q) {
+                    if (p0 + q >= e || tt[q] >= r.sim_end_ns) continue;  // completed: no draw
+                    const uint64_t d = xoshiro_next(s0, s1, s2, s3);
+                    if (in_lds) sdraw[p0 + q - pb] = d;
+                    else gdraws[p0 + q] = d;
+                }
+            }
+            rng[4 * h] = s0;
+            rng[4 * h + 1] = s1;
+            rng[4 * h + 2] = s2;
+            rng[4 * h + 3] = s3;
+        }
+    }
+    __syncthreads();
+    // phase 2: the block's packets, one a lane
     unsigned long long min_lat = ~0ull, min_deliver = ~0ull;
-    for (uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; p < n_pkts;
-         p += (uint64_t)gridDim.x * blockDim.x) {
+    bool unresolved = false;
+    for (uint32_t p = pb + t; p < pe; p += RT) {
         const srt_pkt k = pkts[p];
         uint32_t f = SRT_PDS_NONE;
         uint64_t d = 0;
         if (k.t_ns < r.sim_end_ns) {
-            const uint64_t o = (uint64_t)k.src_row * n + k.dst_row;
-            const float rel32 = 1.0f - loss[o];
-            const double reliability = (double)rel32;
-            const double chance = (double)(draws[p] >> 11) * 0x1.0p-53;
-            const bool bootstrapping = k.t_ns < r.bootstrap_end_ns;
-            if (!bootstrapping && chance >= reliability && k.payload_size > 0) {
-                f = SRT_PDS_INET_DROPPED;
+            int32_t i, j;
+            pkt_rows<IP>(k, ipt, i, j);
+            if (i < 0 || j < 0) {
+                unresolved = true;  // the reference's reliability(..).unwrap() panics (worker.rs:359)
             } else {
-                const uint64_t delay = lat[o];
-                f = SRT_PDS_INET_SENT;
-                d = k.t_ns + delay;
-                if (d < r.round_end_ns) d = r.round_end_ns;
-                if (counters) atomicAdd(&counters[o], 1ull);
-                min_lat = delay < min_lat ? delay : min_lat;
-                min_deliver = d < min_deliver ? d : min_deliver;
+                const uint64_t o = (uint64_t)(uint32_t)i * n + (uint32_t)j;
+                uint64_t delay;
+                float ls;
+                if (TAB16) {
+                    const uint4 rec = tab[o];
+                    delay = (uint64_t)rec.x | (uint64_t)rec.y << 32;
+                    ls = __uint_as_float(rec.z);
+                } else {
+                    delay = lat[o];
+                    ls = loss[o];
+                }
+                const float rel32 = 1.0f - ls;
+                const double reliability = (double)rel32;
+                const uint64_t draw = in_lds ? sdraw[p - pb] : gdraws[p];
+                const double chance = (double)(draw >> 11) * 0x1.0p-53;
+                const bool bootstrapping = k.t_ns < r.bootstrap_end_ns;
+                if (!bootstrapping && chance >= reliability && k.payload_size > 0) {
+                    f = SRT_PDS_INET_DROPPED;
+                } else {
+                    f = SRT_PDS_INET_SENT;
+                    d = k.t_ns + delay;
+                    if (d < r.round_end_ns) d = r.round_end_ns;
+                    if (counters) atomicAdd(&counters[o], 1ull);
+                    min_lat = delay < min_lat ? delay : min_lat;
+                    min_deliver = d < min_deliver ? d : min_deliver;
+                }
             }
         }
         flags[p] = f;
         deliver[p] = d;
     }
-    // wave, then block reduction: one pair of atomics per block (same-address
+    if (IP && __any(unresolved) && (t & 63) == 0) atomicOr(bad, 1u);
+    // wave, then block reduction: one pair of partials per block (same-address
     // atomics from every wave serialise at the memory-side atomic unit)
     for (int off = 32; off > 0; off >>= 1) {
         const unsigned long long a = __shfl_xor(min_lat, off), b = __shfl_xor(min_deliver, off);
         min_lat = a < min_lat ? a : min_lat;
         min_deliver = b < min_deliver ? b : min_deliver;
     }
-    __shared__ unsigned long long red[2][DECIDE_THREADS / 64];
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
+    const int w = t >> 6;
+    if ((t & 63) == 0) {
         red[0][w] = min_lat;
         red[1][w] = min_deliver;
     }
     __syncthreads();
-    if (threadIdx.x == 0 && partial) {
-        for (int k = 1; k < DECIDE_THREADS / 64; ++k) {
-            min_lat = red[0][k] < min_lat ? red[0][k] : min_lat;
-            min_deliver = red[1][k] < min_deliver ? red[1][k] : min_deliver;
+    if (t == 0 && partial) {
+        for (int q = 1; q < RT / 64; ++q) {
+            min_lat = red[0][q] < min_lat ? red[0][q] : min_lat;
+            min_deliver = red[1][q] < min_deliver ? red[1][q] : min_deliver;
         }
         partial[2 * blockIdx.x] = min_lat;
         partial[2 * blockIdx.x + 1] = min_deliver;
     }
 }
 
+// the built table as 16-B records {latency lo, latency hi, loss bits, 0}: one
+// gather a packet instead of two (the table is static through a simulation)
+__global__ __launch_bounds__(256) void pack_tab16_kernel(const uint64_t *__restrict__ lat,
+                                                         const float *__restrict__ loss, uint64_t count,
+                                                         uint4 *__restrict__ out) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < count;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t l = lat[i];
+        out[i] = make_uint4((uint32_t)l, (uint32_t)(l >> 32), __float_as_uint(loss[i]), 0u);
+    }
+}
+
 // Block partials -> the caller's stats (min-combined).  Same-address atomics
-// from every block of decide_kernel serialise at the memory-side atomic unit
-// (2048 blocks x 2 = ~60 us measured, more than the whole decision pass), so
-// they are combined here by one workgroup: two atomics per round.
+// from every block serialise at the memory-side atomic unit, so they are
+// combined here by one workgroup: two atomics per round.
 __global__ __launch_bounds__(1024) void stats_kernel(const unsigned long long *__restrict__ partial, uint32_t nblocks,
                                                      unsigned long long *stats) {
     unsigned long long a = ~0ull, b = ~0ull;
@@ -158,79 +223,219 @@ __global__ __launch_bounds__(1024) void stats_kernel(const unsigned long long *_
     }
 }
 
+void perr(srt_err *err, int code, const char *msg) {
+    if (!err) return;
+    err->code = code;
+    std::snprintf(err->msg, sizeof err->msg, "%s", msg);
+}
+
+// tables up to this size are packed into 16-B records for the round's gathers
+constexpr uint64_t TAB16_MAX_BYTES = 1ull << 30;
+
+srt_status packet_round(srt_plan *plan, const srt_pkt *d_pkts, const uint32_t *d_host_pkt_ptr, uint32_t n_hosts,
+                        uint64_t n_pkts, uint64_t *d_rng, const srt_round *round, uint32_t *d_flags,
+                        uint64_t *d_deliver, uint64_t *d_counters, uint64_t *d_stats, const srt::IpTable *ipt,
+                        srt_err *err) {
+    srt::init_wait();  // a pending srt_init_async finishes first
+    if (err) std::memset(err, 0, sizeof *err);
+    if (!plan || !round || (n_pkts && (!d_pkts || !d_flags || !d_deliver)) || !d_host_pkt_ptr ||
+        (n_hosts && !d_rng)) {
+        perr(err, SRT_ERR_INVALID, "null argument");
+        return SRT_ERR_INVALID;
+    }
+    if (!plan->ran) {
+        perr(err, SRT_ERR_INVALID, "routing table not built (run the plan first)");
+        return SRT_ERR_INVALID;
+    }
+    if (plan->row_shard || plan->row0 != 0 || plan->row1 != plan->n) {
+        perr(err, SRT_ERR_INVALID, "the packet stage needs the whole table on the plan's device");
+        return SRT_ERR_INVALID;
+    }
+    if (hipSetDevice(plan->device) != hipSuccess) return SRT_ERR_HIP;
+    hipStream_t s = plan->stream;
+    const uint32_t blocks = (n_hosts + HB - 1) / HB;
+    // scratch: the draws of blocks whose packets overflow their LDS, then
+    // {min latency, min deliver} per block
+    const uint64_t need = n_pkts + 2 * (uint64_t)std::max<uint32_t>(blocks, 1);
+    if (need > plan->draws_cap) {
+        if (plan->d_draws) (void)hipFree(plan->d_draws);
+        plan->d_draws = nullptr;
+        plan->draws_cap = 0;
+        if (hipMalloc(&plan->d_draws, need * sizeof(uint64_t)) != hipSuccess) {
+            perr(err, SRT_ERR_OOM, "hipMalloc(draws) failed");
+            return SRT_ERR_OOM;
+        }
+        plan->draws_cap = need;
+    }
+    const uint64_t nn = (uint64_t)plan->n * plan->n;
+    // knob SRT_PKT_TAB16=0: the two-gather form tables over 1 GiB use (tests)
+    static const bool tab16_off = [] {
+        const char *e = std::getenv("SRT_PKT_TAB16");
+        return e && std::atoi(e) == 0;
+    }();
+    const bool tab16 = nn * 16 <= TAB16_MAX_BYTES && nn > 0 && !tab16_off;
+    if (tab16 && plan->pkt_tab_run != plan->run_no) {
+        if (!plan->d_pkt_tab && hipMalloc(&plan->d_pkt_tab, nn * 16) != hipSuccess) {
+            plan->d_pkt_tab = nullptr;
+            perr(err, SRT_ERR_OOM, "hipMalloc(packed table) failed");
+            return SRT_ERR_OOM;
+        }
+        hipLaunchKernelGGL(pack_tab16_kernel, dim3((uint32_t)std::min<uint64_t>((nn + 255) / 256, 8192)), dim3(256),
+                           0, s, plan->d_out_lat, plan->d_out_loss, nn, plan->d_pkt_tab);
+        plan->pkt_tab_run = plan->run_no;
+    }
+    if (ipt && !plan->d_pkt_bad) {
+        if (hipMalloc(&plan->d_pkt_bad, 4) != hipSuccess) {
+            plan->d_pkt_bad = nullptr;
+            perr(err, SRT_ERR_OOM, "hipMalloc(status) failed");
+            return SRT_ERR_OOM;
+        }
+        (void)hipMemsetAsync(plan->d_pkt_bad, 0, 4, s);
+    }
+    unsigned long long *partial = (unsigned long long *)(plan->d_draws + n_pkts);
+    const srt::IpTable none{};
+    if (blocks) {
+        auto *k = ipt ? (tab16 ? round_kernel<true, true> : round_kernel<true, false>)
+                      : (tab16 ? round_kernel<false, true> : round_kernel<false, false>);
+        hipLaunchKernelGGL(k, dim3(blocks), dim3(RT), 0, s, d_pkts, d_host_pkt_ptr, n_hosts, d_rng, *round,
+                           plan->d_pkt_tab, plan->d_out_lat, plan->d_out_loss, plan->n, ipt ? *ipt : none, d_flags,
+                           d_deliver, (unsigned long long *)d_counters, d_stats ? partial : nullptr, plan->d_draws,
+                           plan->d_pkt_bad);
+        if (d_stats)
+            hipLaunchKernelGGL(stats_kernel, dim3(1), dim3(1024), 0, s, partial, blocks,
+                               (unsigned long long *)d_stats);
+    }
+    if (hipGetLastError() != hipSuccess) {
+        perr(err, SRT_ERR_HIP, "packet kernel launch failed");
+        return SRT_ERR_HIP;
+    }
+    return SRT_OK;
+}
+
 }  // namespace
 
 namespace srt {
 // srt_init: loads this unit's code object (srt::preload_kernels)
 hipError_t preload_packet() {
     hipFuncAttributes a;
-    return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&decide_kernel));
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&round_kernel<false, true>));
 }
 }  // namespace srt
 
-extern "C" srt_status srt_packet_batch(srt_plan *plan, const srt_pkt *d_pkts,
-                                       const uint32_t *d_host_pkt_ptr, uint32_t n_hosts,
-                                       uint64_t n_pkts, uint64_t *d_rng, const srt_round *round,
-                                       uint32_t *d_flags, uint64_t *d_deliver,
-                                       uint64_t *d_counters, uint64_t *d_stats, srt_err *err) {
-    srt::init_wait();  // a pending srt_init_async finishes first
+extern "C" srt_status srt_packet_batch(srt_plan *plan, const srt_pkt *d_pkts, const uint32_t *d_host_pkt_ptr,
+                                       uint32_t n_hosts, uint64_t n_pkts, uint64_t *d_rng, const srt_round *round,
+                                       uint32_t *d_flags, uint64_t *d_deliver, uint64_t *d_counters,
+                                       uint64_t *d_stats, srt_err *err) {
+    return packet_round(plan, d_pkts, d_host_pkt_ptr, n_hosts, n_pkts, d_rng, round, d_flags, d_deliver, d_counters,
+                        d_stats, nullptr, err);
+}
+
+extern "C" srt_status srt_packet_batch_ip(srt_plan *plan, srt_ip_resolver *res, const srt_pkt_ip *d_pkts,
+                                          const uint32_t *d_host_pkt_ptr, uint32_t n_hosts, uint64_t n_pkts,
+                                          uint64_t *d_rng, const srt_round *round, uint32_t *d_flags,
+                                          uint64_t *d_deliver, uint64_t *d_counters, uint64_t *d_stats,
+                                          srt_err *err) {
     if (err) std::memset(err, 0, sizeof *err);
-    if (!plan || !round || (n_pkts && (!d_pkts || !d_flags || !d_deliver)) || !d_host_pkt_ptr ||
-        (n_hosts && !d_rng)) {
-        if (err) {
-            err->code = SRT_ERR_INVALID;
-            std::snprintf(err->msg, sizeof err->msg, "null argument");
-        }
+    if (!plan || !res) {
+        perr(err, SRT_ERR_INVALID, "null argument");
         return SRT_ERR_INVALID;
     }
-    if (!plan->ran) {
-        if (err) {
-            err->code = SRT_ERR_INVALID;
-            std::snprintf(err->msg, sizeof err->msg, "routing table not built (run the plan first)");
-        }
-        return SRT_ERR_INVALID;
-    }
-    if (hipSetDevice(plan->device) != hipSuccess) return SRT_ERR_HIP;
-    // scratch: one draw per packet, then {min latency, min deliver} per decide block
-    constexpr uint64_t MAX_DECIDE_BLOCKS = 2048;  // grid-stride: 8 blocks per CU
-    const uint64_t need = n_pkts + 2 * MAX_DECIDE_BLOCKS;
-    if (need > plan->draws_cap) {
-        if (plan->d_draws) (void)hipFree(plan->d_draws);
-        plan->d_draws = nullptr;
-        plan->draws_cap = 0;
-        if (hipMalloc(&plan->d_draws, need * sizeof(uint64_t)) != hipSuccess) {
-            if (err) {
-                err->code = SRT_ERR_OOM;
-                std::snprintf(err->msg, sizeof err->msg, "hipMalloc(draws) failed");
-            }
-            return SRT_ERR_OOM;
-        }
-        plan->draws_cap = need;
-    }
-    unsigned long long *partial = (unsigned long long *)(plan->d_draws + n_pkts);
-    hipStream_t s = plan->stream;
-    if (n_hosts) {
-        // 64 threads x 16 packets in flight a host (C5: 103 us/round vs 137
-        // at 256 threads; 32 in flight no faster)
-        hipLaunchKernelGGL((draw_kernel<64, 16>), dim3((n_hosts + 63) / 64), dim3(64), 0, s, d_pkts,
-                           d_host_pkt_ptr, n_hosts, d_rng, round->sim_end_ns, plan->d_draws);
-    }
-    if (n_pkts) {
-        uint64_t blocks = (n_pkts + DECIDE_THREADS - 1) / DECIDE_THREADS;
-        if (blocks > MAX_DECIDE_BLOCKS) blocks = MAX_DECIDE_BLOCKS;
-        hipLaunchKernelGGL(decide_kernel, dim3((uint32_t)blocks), dim3(DECIDE_THREADS), 0, s, d_pkts, n_pkts,
-                           plan->d_draws, plan->d_out_lat, plan->d_out_loss, plan->n, *round,
-                           d_flags, d_deliver, (unsigned long long *)d_counters, d_stats ? partial : nullptr);
-        if (d_stats)
-            hipLaunchKernelGGL(stats_kernel, dim3(1), dim3(1024), 0, s, partial, (uint32_t)blocks,
-                               (unsigned long long *)d_stats);
-    }
-    if (hipGetLastError() != hipSuccess) {
-        if (err) {
-            err->code = SRT_ERR_HIP;
-            std::snprintf(err->msg, sizeof err->msg, "packet kernel launch failed");
-        }
+    static_assert(sizeof(srt_pkt_ip) == sizeof(srt_pkt), "srt_pkt_ip mirrors srt_pkt's layout");
+    srt::IpTable t{};
+    if (srt_status st = srt::ip_table_device(res, plan->device, &t, err); st != SRT_OK) return st;
+    return packet_round(plan, reinterpret_cast<const srt_pkt *>(d_pkts), d_host_pkt_ptr, n_hosts, n_pkts, d_rng,
+                        round, d_flags, d_deliver, d_counters, d_stats, &t, err);
+}
+
+extern "C" srt_status srt_packet_status(srt_plan *plan, srt_err *err) {
+    if (err) std::memset(err, 0, sizeof *err);
+    if (!plan) return SRT_ERR_INVALID;
+    if (hipSetDevice(plan->device) != hipSuccess || hipStreamSynchronize(plan->stream) != hipSuccess) {
+        perr(err, SRT_ERR_HIP, "hipStreamSynchronize failed");
         return SRT_ERR_HIP;
     }
+    if (!plan->d_pkt_bad) return SRT_OK;
+    uint32_t bad = 0;
+    if (hipMemcpy(&bad, plan->d_pkt_bad, 4, hipMemcpyDeviceToHost) != hipSuccess) return SRT_ERR_HIP;
+    if (bad) {
+        (void)hipMemset(plan->d_pkt_bad, 0, 4);
+        // WorkerShared::reliability(src, dst).unwrap() (worker.rs:359-361)
+        perr(err, SRT_ERR_INVALID, "a packet's source or destination address has no node in the routing table");
+        return SRT_ERR_INVALID;
+    }
     return SRT_OK;
+}
+
+// ------------------------------------------------------------------ host RNG
+// The per-host stream lives in Shadow's Host (host.rs:122, 233); these are the
+// library's host-side copies of its three steps, so a caller can seed, advance
+// and check the 4 x u64 states it hands to srt_packet_batch.
+extern "C" void srt_xoshiro_seed_from_u64(uint64_t seed, uint64_t state[4]) {
+    // rand_core 0.6 SeedableRng::seed_from_u64 for Xoshiro256PlusPlus
+    // (rand_xoshiro 0.6.0): SplitMix64 outputs as the four state words
+    uint64_t x = seed;
+    for (int i = 0; i < 4; ++i) {
+        x += 0x9E3779B97F4A7C15ull;
+        uint64_t z = x;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        state[i] = z ^ (z >> 31);
+    }
+}
+
+extern "C" void srt_xoshiro_next_u64(uint64_t state[4], uint64_t count, uint64_t *out) {
+    uint64_t s0 = state[0], s1 = state[1], s2 = state[2], s3 = state[3];
+    for (uint64_t i = 0; i < count; ++i) {
+        const uint64_t v = xoshiro_next(s0, s1, s2, s3);
+        if (out) out[i] = v;
+    }
+    state[0] = s0;
+    state[1] = s1;
+    state[2] = s2;
+    state[3] = s3;
+}
+
+namespace {
+// std::hash::DefaultHasher (SipHash-1-3, keys 0, 0; Rust 1.76) of a &str:
+// the bytes, then 0xFF (str's Hash impl)
+uint64_t siphash13_str(const char *s, size_t len) {
+    uint64_t v0 = 0x736F6D6570736575ull, v1 = 0x646F72616E646F6Dull, v2 = 0x6C7967656E657261ull,
+             v3 = 0x7465646279746573ull;
+    auto round = [&] {
+        v0 += v1; v1 = rotl(v1, 13); v1 ^= v0; v0 = rotl(v0, 32);
+        v2 += v3; v3 = rotl(v3, 16); v3 ^= v2;
+        v0 += v3; v3 = rotl(v3, 21); v3 ^= v0;
+        v2 += v1; v1 = rotl(v1, 17); v1 ^= v2; v2 = rotl(v2, 32);
+    };
+    const size_t n = len + 1;
+    auto byte = [&](size_t i) -> uint64_t { return i < len ? (uint8_t)s[i] : 0xffu; };
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w = 0;
+        for (int k = 0; k < 8; ++k) w |= byte(i + k) << (8 * k);
+        v3 ^= w;
+        round();
+        v0 ^= w;
+    }
+    uint64_t b = (uint64_t)(n & 0xff) << 56;
+    for (size_t k = 0; i + k < n; ++k) b |= byte(i + k) << (8 * k);
+    v3 ^= b;
+    round();
+    v0 ^= b;
+    v2 ^= 0xff;
+    round();
+    round();
+    round();
+    return v0 ^ v1 ^ v2 ^ v3;
+}
+}  // namespace
+
+extern "C" uint64_t srt_host_node_seed(uint32_t general_seed, const char *hostname, size_t len) {
+    // sim_config.rs:47-53: randomness_for_seed_calc = the first u64 of
+    // Xoshiro256PlusPlus::seed_from_u64(general.seed); :222-227, :244: the
+    // host's seed = that ^ DefaultHasher(hostname)
+    uint64_t st[4], r = 0;
+    srt_xoshiro_seed_from_u64(general_seed, st);
+    srt_xoshiro_next_u64(st, 1, &r);
+    return r ^ siphash13_str(hostname ? hostname : "", hostname ? len : 0);
 }

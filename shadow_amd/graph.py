@@ -143,6 +143,23 @@ class NetworkGraph:
         h = C.c_void_p()
         err = _lib.SrtErr()
         _lib.check(L.srt_gml_parse(b, len(b), C.byref(h), C.byref(err)), err)
+        return cls._from_gml(h)
+
+    @classmethod
+    def parse_file(cls, path: str, xz: bool = False) -> "NetworkGraph":
+        """load_network_graph's file source (mod.rs:494-509; read_xz :479-492 when
+        xz) + parse, all in libsrt (srt_gml_parse_file: the library's xz decoder)."""
+        import os
+        L = _lib.lib()
+        h = C.c_void_p()
+        err = _lib.SrtErr()
+        _lib.check(L.srt_gml_parse_file(os.path.expanduser(path).encode(), int(bool(xz)), C.byref(h),
+                                        C.byref(err)), err)
+        return cls._from_gml(h)
+
+    @classmethod
+    def _from_gml(cls, h) -> "NetworkGraph":
+        L = _lib.lib()
         try:
             csr = _lib.SrtCsr()
             L.srt_gml_csr(h, C.byref(csr))
@@ -208,41 +225,97 @@ class NetworkGraph:
         return self._run("srt_get_direct_paths", nodes, _lib.SRT_ALGO_AUTO, device)
 
 
+def _ip_be(ip) -> int:
+    """IPv4 (str / int / IPv4Address) -> u32 in network byte order."""
+    return int.from_bytes(ipaddress.IPv4Address(ip).packed, "little")
+
+
+def _ip_from_be(x: int) -> ipaddress.IPv4Address:
+    return ipaddress.IPv4Address(int(x).to_bytes(4, "little"))
+
+
 class IpAssignment:
-    """mod.rs:352-420: IP <-> node id; auto-assignment from 11.0.0.1 upward,
-    skipping addresses ending in .0 or .255."""
+    """IpAssignment<u32> (mod.rs:352-420) in libsrt (srt_ip_assignment_*):
+    IP <-> node id; auto-assignment from 11.0.0.1 upward, skipping addresses
+    ending in .0 or .255; assign_ip refuses a taken address."""
 
     def __init__(self):
-        self._map: Dict[ipaddress.IPv4Address, int] = {}
-        self._last = ipaddress.IPv4Address("11.0.0.0")
-
-    @staticmethod
-    def _increment(addr: ipaddress.IPv4Address) -> ipaddress.IPv4Address:
-        x = int(addr)
-        while True:
-            x += 1
-            if x & 0xFF not in (0, 255):
-                return ipaddress.IPv4Address(x)
+        self._h = C.c_void_p()
+        _lib.check(_lib.lib().srt_ip_assignment_create(C.byref(self._h)), _lib.SrtErr())
 
     def assign(self, node_id: int) -> ipaddress.IPv4Address:
-        while True:
-            ip = self._increment(self._last)
-            self._last = ip
-            if ip not in self._map:
-                self._map[ip] = node_id
-                return ip
+        return _ip_from_be(_lib.lib().srt_ip_assignment_assign(self._h, int(node_id)))
 
     def assign_ip(self, node_id: int, ip) -> None:
-        ip = ipaddress.IPv4Address(ip)
-        if ip in self._map:
-            raise ValueError("IP address has already been assigned")
-        self._map[ip] = node_id
+        err = _lib.SrtErr()
+        rc = _lib.lib().srt_ip_assignment_assign_ip(self._h, int(node_id), _ip_be(ip), C.byref(err))
+        if rc != _lib.SRT_OK:
+            raise ValueError(err.msg.decode())  # IpPreviouslyAssignedError (mod.rs:343-350)
 
     def get_node(self, ip) -> Optional[int]:
-        return self._map.get(ipaddress.IPv4Address(ip))
+        v = C.c_uint32()
+        return int(v.value) if _lib.lib().srt_ip_assignment_get_node(self._h, _ip_be(ip), C.byref(v)) else None
 
     def get_nodes(self) -> set:
-        return set(self._map.values())
+        L = _lib.lib()
+        k = L.srt_ip_assignment_get_nodes(self._h, None, 0)
+        out = np.zeros(max(k, 1), np.uint32)
+        L.srt_ip_assignment_get_nodes(self._h, out.ctypes.data_as(C.POINTER(C.c_uint32)), k)
+        return set(out[:k].tolist())
+
+    def __len__(self) -> int:
+        return int(_lib.lib().srt_ip_assignment_size(self._h))
+
+    def resolver(self, row_ids) -> "IpResolver":
+        """The assignment frozen against a table whose row i is GML node row_ids[i]."""
+        return IpResolver(self, row_ids)
+
+    def close(self):
+        if self._h:
+            _lib.lib().srt_ip_assignment_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class IpResolver:
+    """srt_ip_resolver: IPv4 -> table row for the send path (the two get_node
+    lookups + path() of WorkerShared::latency / reliability, worker.rs:539-553),
+    on host threads (rows) or inside the device round (RoutingPlan.packet_batch_ip)."""
+
+    def __init__(self, assignment: IpAssignment, row_ids):
+        ids = np.ascontiguousarray(row_ids, np.uint32)
+        self._h = C.c_void_p()
+        err = _lib.SrtErr()
+        _lib.check(_lib.lib().srt_ip_resolver_create(assignment._h, ids.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                                     len(ids), C.byref(self._h), C.byref(err)), err)
+
+    def rows(self, ips_be: np.ndarray) -> np.ndarray:
+        """int32 table rows of u32 network-byte-order addresses (-1: no row)."""
+        ips = np.ascontiguousarray(ips_be, np.uint32)
+        out = np.empty(len(ips), np.int32)
+        _lib.check(_lib.lib().srt_ip_resolve_rows(self._h, ips.ctypes.data_as(C.POINTER(C.c_uint32)), len(ips),
+                                                  out.ctypes.data_as(C.POINTER(C.c_int32))), _lib.SrtErr())
+        return out
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            _lib.lib().srt_ip_resolver_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class RoutingInfo:
@@ -359,9 +432,8 @@ def load_network_graph(options) -> str:
       {"type": "gml", "file": {"path": p, "compression": None | "xz"}}
       {"type": "gml", "inline": text}
       {"type": "1_gbit_switch"}
-    Paths get tilde expansion; xz files are decompressed on the host (the
-    reference uses lzma-rs here too) and must be UTF-8."""
-    import lzma
+    Paths get tilde expansion; xz files are decompressed by libsrt's own
+    .xz / LZMA2 decoder (the reference's lzma-rs step) and must be UTF-8."""
     import os
 
     kind = options.get("type")
@@ -387,14 +459,29 @@ def load_network_graph(options) -> str:
     except OSError as e:
         raise GraphLoadError(f"Failed to open file: {path!r}") from e
     with f:
-        try:
-            data = lzma.decompress(f.read(), format=lzma.FORMAT_XZ)
-        except lzma.LZMAError as e:
-            raise GraphLoadError("Failed to decompress file") from e
+        raw = f.read()
+    try:
+        data = xz_decompress(raw)
+    except _lib.SrtError as e:
+        raise GraphLoadError("Failed to decompress file") from e
     try:
         return data.decode("utf-8")
     except UnicodeDecodeError as e:
         raise GraphLoadError(f"invalid utf-8 in {path!r}") from e
+
+
+def xz_decompress(raw: bytes) -> bytes:
+    """read_xz's decompression (mod.rs:479-492) by libsrt's .xz / LZMA2 decoder
+    (srt_xz_decompress); raises SrtError("Failed to decompress file: ...")."""
+    L = _lib.lib()
+    out = C.POINTER(C.c_uint8)()
+    n = C.c_size_t()
+    err = _lib.SrtErr()
+    _lib.check(L.srt_xz_decompress(raw, len(raw), C.byref(out), C.byref(n), C.byref(err)), err)
+    try:
+        return C.string_at(out, n.value)
+    finally:
+        L.srt_free(out)
 
 
 def generate_routing_info(graph: NetworkGraph, node_ids: set, use_shortest_paths: bool = True) -> RoutingInfo:

@@ -168,3 +168,31 @@ class RoutingPlan:
             stats.data_ptr() if stats is not None else None, C.byref(err)), err)
         if sync:
             self.sync()
+
+    def packet_batch_ip(self, resolver, pkts, host_ptr, rng, round_end_ns: int, bootstrap_end_ns: int,
+                        sim_end_ns: int, flags, deliver, counters=None, stats=None, sync: bool = True):
+        """srt_packet_batch_ip: as packet_batch, with pkts a uint8 view of
+        srt_pkt_ip records (source / destination IPv4 in network byte order,
+        resolved on the device through `resolver`, an IpResolver over this
+        plan's table rows).  sync=True also checks srt_packet_status (an
+        address without a row raises, as the reference's unwrap panics)."""
+        import torch
+
+        n_hosts = host_ptr.numel() - 1
+        n_pkts = flags.numel()
+        torch.cuda.ExternalStream(self.stream_ptr(), device=flags.device).wait_stream(
+            torch.cuda.current_stream(flags.device))
+        r = _lib.SrtRound(round_end_ns, bootstrap_end_ns, sim_end_ns)
+        err = _lib.SrtErr()
+        _lib.check(_lib.lib().srt_packet_batch_ip(
+            self._h, resolver.handle, pkts.data_ptr(), host_ptr.data_ptr(), n_hosts, n_pkts, rng.data_ptr(),
+            C.byref(r), flags.data_ptr(), deliver.data_ptr(),
+            counters.data_ptr() if counters is not None else None,
+            stats.data_ptr() if stats is not None else None, C.byref(err)), err)
+        if sync:
+            self.packet_status()
+
+    def packet_status(self):
+        """srt_packet_status: synchronises; raises if a batch met an address without a row."""
+        err = _lib.SrtErr()
+        _lib.check(_lib.lib().srt_packet_status(self._h, C.byref(err)), err)

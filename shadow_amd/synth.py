@@ -153,6 +153,9 @@ def barabasi_albert(n: int, m: int, seed: int, lat_ms=(1, 300), loss_max=0.01):
 
 PKT_DTYPE = np.dtype([("src_host", "<u4"), ("src_row", "<u4"), ("dst_row", "<u4"), ("payload_size", "<u4"),
                       ("t_ns", "<u8")])
+# srt_pkt_ip: the packet by address (IPv4 in network byte order)
+PKT_IP_DTYPE = np.dtype([("src_host", "<u4"), ("src_ip", "<u4"), ("dst_ip", "<u4"), ("payload_size", "<u4"),
+                         ("t_ns", "<u8")])
 
 
 def packet_round(n_hosts: int, n_rows: int, n_pkts: int, seed: int, round_start: int, round_end: int):

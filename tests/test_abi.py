@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_struct_layout():
     L = _lib.lib()
-    assert L.srt_abi_version() == 3
+    assert L.srt_abi_version() == 4
     assert C.sizeof(_lib.SrtPath) == 16  # #[repr(C)] PathProperties mirror
     assert C.sizeof(_lib.SrtTiming) == 80  # ABI 2: + edge_visits (ABI 3: + srt_plan_shard_rows)
     assert C.sizeof(_lib.SrtCsr) == 56
