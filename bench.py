@@ -92,10 +92,12 @@ def parse_args():
                     help="skip the cold first-call legs (fresh processes) of the dense configs")
     ap.add_argument("--cold-child", dest="cold_child", default="", choices=["", "plain", "init"],
                     help=argparse.SUPPRESS)
-    ap.add_argument("--exchange", default="none", choices=["none", "allgather"],
-                    help="N > 1, LEVEL / SSSP plans: 'none' = rows sharded with no collective (each rank's rows stay "
-                         "in its HBM); 'allgather' = the communicator-bound build (rows all-gathered over RCCL so "
-                         "every rank holds the whole table)")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "none", "allgather"],
+                    help="N > 1: 'allgather' (the default, 'auto') = the communicator-bound build the north_star "
+                         "names: rows all-gathered over RCCL so every rank holds the whole table (the line's value; "
+                         "the no-exchange share is measured after it and carried as config.no_exchange); 'none' = "
+                         "LEVEL / SSSP rows sharded with no collective as the value (each rank's rows stay in its HBM)")
+    ap.add_argument("--tbuild-child", dest="tbuild_child", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--algo", default="auto", choices=["auto", "fw", "sssp", "level"],
                     help="kernel family (default: AUTO, the library's priced choice -- what the drop-in runs)")
     ap.add_argument("--rank-share", dest="rank_share", type=int, default=0,
@@ -198,15 +200,16 @@ def measured_traffic(args, kernel_tag, schedule):
 
 
 def packet_traffic():
-    """HBM bytes of one C5 round's draw + decide kernels from the newest
-    committed C5 PMC summary (one dispatch of each a round), or None."""
+    """HBM bytes of one C5 round's kernels (round_kernel + pack/stats; r05 and
+    before: draw_kernel + decide_kernel) from the newest committed C5 PMC
+    summary of the current kernel, or None."""
     import glob
     for f in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))):
         d = json.load(open(f))
         if not d.get("config", "").startswith("C5 "):
             continue
         tot = sum(v["hbm_bytes_per_launch"] for k, v in d.get("kernels", {}).items()
-                  if k.startswith(("draw_kernel", "decide_kernel")))
+                  if k.startswith(("round_kernel", "stats_kernel")))
         if tot:
             return tot, os.path.relpath(f, ROOT)
     return None, None
@@ -389,6 +392,63 @@ def cold_calls(args):
                     "at process start, overlapped with building the graph (Shadow: config + GML parsing)"}
 
 
+def synth_graph(args, cfg):
+    """The config's dense graph as a NetworkGraph (complete / dense kinds)."""
+    from shadow_amd import NetworkGraph, synth
+    n = args.nodes or cfg["nodes"]
+    seed = cfg["seed"] if args.seed < 0 else args.seed
+    if cfg["kind"] == "dense":
+        row_ptr, col, lat, loss = synth.dense_csr(n, synth.dense_graph(n, seed, drop=cfg["drop"]))
+    else:
+        row_ptr, col, lat, loss = synth.complete_csr(n, seed, edges=synth.complete_graph_ns(n, seed)
+                                                     if cfg.get("ns") else None)
+    return NetworkGraph(n, np.arange(n, dtype=np.uint32), row_ptr, col, lat, loss, directed=False)
+
+
+def tbuild_child(args):
+    """BASELINE.md's t_build at N GPUs as Shadow calls it: ONE process
+    (generate_routing_info runs once, in Shadow's main thread,
+    sim_config.rs:136-140) building with srt_opts.n_gpus = N -- one library
+    thread and one plan per device, each device solving its share of the rows
+    and downloading them over its own link.  Run by rank 0 of an N-rank bench
+    as a child process after every rank released its plans."""
+    from shadow_amd import RoutingInfo
+    cfg = CONFIGS[args.config]
+    g = synth_graph(args, cfg)
+    n = g.n_nodes
+    nodes = np.arange(n, dtype=np.uint32)
+    same = os.environ.get("SRT_BENCH_ONE_DEVICE") == "1"
+    N = args.tbuild_child
+    out = {"n_gpus": N, "same_device": same}
+    times = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        ri = RoutingInfo.build(g, nodes, n_gpus=N, same_device=same, device=0)
+        times.append((time.perf_counter() - t0) * 1e3)
+        ri.close()
+    out["routing_info_ms"] = min(times)
+    out["routing_info_call_ms"] = [round(x, 2) for x in times]
+    out["routing_info_pairs_per_s"] = n * n / (min(times) / 1e3)
+    out["span"] = ("srt_routing_info_build with srt_opts.n_gpus = N from one process: host CSR -> RoutingInfo "
+                   "(validation, upload, class CSRs, every device's rows solved and downloaded over its own link)")
+    print(json.dumps(out), flush=True)
+
+
+def tbuild_leg(args, N):
+    """Rank 0: tbuild_child in a fresh process; its JSON, or the failure."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--tbuild-child", str(N), "--config", args.config]
+    if args.nodes:
+        cmd += ["--nodes", str(args.nodes)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    except subprocess.TimeoutExpired:
+        return {"error": "t_build child timed out (600 s)"}
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    if r.returncode != 0 or not line:
+        return {"error": f"t_build child failed (rc {r.returncode}): {(r.stderr or r.stdout)[-600:]}"}
+    return json.loads(line[-1])
+
+
 def gml_graph(n_nodes, seed):
     from shadow_amd import synth
     src, dst, lat, loss = synth.complete_graph(n_nodes, seed)
@@ -515,7 +575,8 @@ def bench_graph(args, cfg, D):
               flush=True)
         plan.close()
         return None
-    if D.world > 1 and args.exchange == "none" and plan.describe().startswith(("level", "sssp")):
+    exchange = args.exchange if args.exchange != "auto" else ("allgather" if D.world > 1 else "none")
+    if D.world > 1 and exchange == "none" and plan.describe().startswith(("level", "sssp")):
         # independent source rows (mod.rs:190-208): each rank builds its share
         # of the rows into its own HBM, no collective in the data path -- the
         # table stays distributed by rows, as the in-process build downloads it
@@ -525,8 +586,8 @@ def bench_graph(args, cfg, D):
         # the collectives' transport is part of the measurement: native RCCL on
         # the plan's streams unless SRT_COMM names another; a failure to set it
         # up ends the run (no silent fallback to a different transport)
-        transport = os.environ.get("SRT_COMM", "rccl")
-        sdist.bind(plan, D.rank, D.world, D.local_rank, transport=transport)
+        transport = os.environ.get("SRT_COMM", "torch" if D.one_device else "rccl")
+        sdist.bind(plan, D.rank, D.world, D.dev, transport=transport)
     desc = plan.describe()
     if " ranks=" in desc:
         ranks = int(desc.split(" ranks=")[1].split()[0])
@@ -551,6 +612,24 @@ def bench_graph(args, cfg, D):
     plan.fetch(table=False)  # connectivity check + min latency (not timed)
     plan.close()
     n = len(nodes)
+    no_exchange = None
+    if D.world > 1 and transport is not None and desc.startswith(("level", "sssp")):
+        # the same build with rows sharded and no collective (each rank's rows
+        # stay in its HBM): what the exchange costs, carried beside the value
+        p2 = RoutingPlan(g, nodes, algo=ALGOS[args.algo], device=D.dev)
+        p2.shard_rows(D.world, D.rank)
+        e2, st2, _, _, _, _ = timed_builds(p2, D, args.steps, args.warmup)
+        p2.close()
+        no_exchange = {"ms_per_step": e2 * 1e3 / args.steps, "value": n * n / (e2 / args.steps),
+                       "step_ms": [round(x, 3) for x in st2],
+                       "what": "rows sharded with no collective (srt_plan_shard_rows): each rank's rows stay in its "
+                               "HBM, no rank holds the table -- the exchange-free share of the build, not the value"}
+    t_build = None
+    if D.world > 1 and args.e2e and cfg["kind"] in ("complete", "dense"):
+        D.barrier()  # every rank's plans are released: the devices are free for one process
+        if D.rank == 0:
+            t_build = tbuild_leg(args, D.world)
+        D.barrier()
     e2e = None
     if args.e2e and D.world == 1 and cfg["kind"] in ("complete", "dense"):
         e2e = e2e_build(g, nodes, algo=ALGOS[args.algo])
@@ -694,6 +773,13 @@ def bench_graph(args, cfg, D):
                                        if " shard=" in desc else f"rows{ranks} (all-gathered over {transport})"),
                        "transport": transport, "nranks": ranks,
                        "plan": desc, "step_ms": [round(x, 3) for x in step_ms], "build_wallclock_ms": ms_per_step,
+                       "create_device_ms": timing["create_device_ms"],
+                       "fresh_graph": {"ms": ms_per_step + timing["create_device_ms"],
+                                       "value": pairs / ((ms_per_step + timing["create_device_ms"]) / 1e3),
+                                       "what": "a build of a graph seen for the first time: the step plus the device "
+                                               "work of plan creation (bound proofs, level probes, symmetry check) -- "
+                                               "Shadow builds once per process (sim_config.rs:136-140)"},
+                       "no_exchange": no_exchange, "t_build": t_build,
                        "phases_last_build": {"device_total_ms": timing["total_ms"],
                                              "dominant_ms": timing["dominant_ms"],
                                              "exact_loss_pass_ms": timing["loss_ms"],
@@ -808,11 +894,12 @@ def bench_packets(args, cfg, D):
             "roofline": {"bound": "hbm", "achieved": bytes_per_round / (dev_ms / 1e3) / 1e9,
                          "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": bytes_per_round / (dev_ms / 1e3) / HBM_PEAK, "traffic": traffic,
-                         "traffic_unit": "HBM bytes per round (FETCH_SIZE + WRITE_SIZE of draw_kernel + decide_kernel)",
+                         "traffic_unit": "HBM bytes per round (FETCH_SIZE + WRITE_SIZE of round_kernel + stats_kernel)",
                          "traffic_source": (f"{traffic_src}: committed rocprofv3 PMC summary of this workload, not "
                                             f"measured in this run" if traffic_src else
                                             "no committed PMC summary for this workload"),
-                         "kernel": "draw_kernel + decide_kernel (one round)", "device_ms_per_round": dev_ms,
+                         "kernel": "round_kernel + stats_kernel (one round: per-host draws in LDS, decisions)",
+                         "device_ms_per_round": dev_ms,
                          "basis": "52 B/packet + 64 B/host (SURVEY.md 8(d))"},
             "cpu_baseline": cpu,
             "events": {"ms_per_round": events_ms, "device_ms_per_round": events_dev_ms,
@@ -843,6 +930,9 @@ def main():
     args = parse_args()
     if args.cold_child:
         cold_child(args)
+        return
+    if args.tbuild_child:
+        tbuild_child(args)
         return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 and world == 1:

@@ -179,6 +179,8 @@ typedef struct {
                                    from the smaller latency level), 0 = the single-direction scan */
     uint32_t reserved0;
     uint64_t edge_visits;       /* level solve: class-CSR entries the last run's rows walked (ABI 2) */
+    double create_device_ms;    /* device work of srt_plan_create, once per graph: bound proofs, the
+                                   level probes, the symmetry check (ABI 4) */
 } srt_timing;
 srt_status srt_plan_timing(const srt_plan *plan, srt_timing *out);
 /* C tiles (128 x 128 keys) the last FW run's dominant launches loaded and

@@ -56,7 +56,7 @@ class SrtTiming(C.Structure):
                 ("dominant_work", C.c_double), ("loss_ms", C.c_double), ("tight_edges", C.c_uint64),
                 ("sharded_tail", C.c_uint32), ("sparse_split", C.c_uint32),
                 ("sparse_sweeps", C.c_uint64), ("loss_fold", C.c_uint32), ("reserved0", C.c_uint32),
-                ("edge_visits", C.c_uint64)]
+                ("edge_visits", C.c_uint64), ("create_device_ms", C.c_double)]
 
 
 class SrtRound(C.Structure):

@@ -967,6 +967,7 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     tr.mark(piped ? "create: device setup+piece upload" : "create: device setup+upload");
     if (piped) pu.finish(&cs);
     else scanner.join();
+    p->ident_rows = cs.ident;
     tr.mark("create: CSR scan (joined)");
 
     // 2. the reference's errors, in its order: edge attributes (parse time),
@@ -999,6 +1000,11 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         return dst;
     }
 
+    // the kernels of creation (bound proofs, probes, symmetry check) are
+    // timed from here on (srt::cspan_*): srt_timing.create_device_ms
+    p->in_create = true;
+    auto dev_timed = [&](auto &&fn) -> srt_status { return fn(); };
+
     // 2b. the key-width proof from the real diameter, where the family is
     //     likely dense, the graph is not complete (complete graphs have the
     //     longest-edge bound) and (V-1) * max edge would not allow f16 keys
@@ -1020,7 +1026,7 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
             (unsigned __int128)(p->V ? p->V - 1 : 0) * maxu >= 1024 && !std::getenv("SRT_FW_NO_ECC")) {
             uint64_t b = ~0ull;
             srt_err e2{};
-            if (srt::fw_ecc_bound(p, 512, &b, &ecc_sweeps, &e2) != SRT_OK) {
+            if (dev_timed([&] { return srt::fw_ecc_bound(p, 512, &b, &ecc_sweeps, &e2); }) != SRT_OK) {
                 srt_plan_destroy(p);
                 if (err) *err = e2;
                 return SRT_ERR_HIP;
@@ -1074,22 +1080,23 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
             const char *ks = std::getenv("SRT_LVL_SYM");  // knob: 0 = always build the in-rows (A/B, tests)
             if (cs.complete && !(ks && std::atoi(ks) == 0)) {
                 bool sym = false;
-                if (srt::level_sym_check(p, maxu, !defer_loss, &sym, &e2) != SRT_OK) return probe_fail();
+                if (dev_timed([&] { return srt::level_sym_check(p, maxu, !defer_loss, &sym, &e2); }) != SRT_OK)
+                    return probe_fail();
                 p->lvl_sym_lat = p->lvl_sym = sym;
             }
             // levels of one unit: 31 classes first (C1-C3: B <= 14), then 63
-            if (srt::level_probe(p, std::min<uint64_t>(31, maxu), 31, &lvl_bound, &lvl_visits, &e2) != SRT_OK)
-                return probe_fail();
-            if (lvl_bound == ~0ull &&
-                srt::level_probe(p, std::min<uint64_t>(63, maxu), 63, &lvl_bound, &lvl_visits, &e2) != SRT_OK)
-                return probe_fail();
+            auto probe = [&](uint64_t wmax, uint32_t wc) {
+                return dev_timed([&] { return srt::level_probe(p, wmax, wc, &lvl_bound, &lvl_visits, &e2); });
+            };
+            if (probe(std::min<uint64_t>(31, maxu), 31) != SRT_OK) return probe_fail();
+            if (lvl_bound == ~0ull && probe(std::min<uint64_t>(63, maxu), 63) != SRT_OK) return probe_fail();
             // no bound within 63 units: the quantized solve, buckets of q <= the
             // shortest edge (C3ns: g = 1 ns, edges >= 1 ms), when the shortest
             // paths stay under 64 such buckets
             const char *kq = std::getenv("SRT_LEVEL_Q");  // knob: 0 = integer levels only (A/B, tests)
             if (lvl_bound == ~0ull && !(kq && std::atoi(kq) == 0)) {
                 uint64_t mn_ns = ~0ull;
-                if (srt::level_min_edge(p, &mn_ns, &e2) != SRT_OK) return probe_fail();
+                if (dev_timed([&] { return srt::level_min_edge(p, &mn_ns, &e2); }) != SRT_OK) return probe_fail();
                 const uint64_t mu = mn_ns == ~0ull ? 0 : mn_ns / cs.gcd;
                 const uint32_t vb = srt::level_vbits(p->V);
                 // an entry keeps the remainder w - c q (< q) in 34 - vb bits;
@@ -1101,12 +1108,8 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
                     p->lvl_q = (uint32_t)q;
                     p->lvl_rb = rb;
                     p->lvl_vb = vb;
-                    if (srt::level_probe(p, std::min<uint64_t>(maxu, 32 * q - 1), 31, &lvl_bound, &lvl_visits, &e2) !=
-                        SRT_OK)
-                        return probe_fail();
-                    if (lvl_bound == ~0ull &&
-                        srt::level_probe(p, std::min<uint64_t>(maxu, 64 * q - 1), 63, &lvl_bound, &lvl_visits, &e2) !=
-                            SRT_OK)
+                    if (probe(std::min<uint64_t>(maxu, 32 * q - 1), 31) != SRT_OK) return probe_fail();
+                    if (lvl_bound == ~0ull && probe(std::min<uint64_t>(maxu, 64 * q - 1), 63) != SRT_OK)
                         return probe_fail();
                     if (lvl_bound == ~0ull) p->lvl_q = 0;
                 }
@@ -1476,6 +1479,14 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     }
     tr.mark("create: upload");
     p->desc += auto_note;
+    p->in_create = false;
+    p->create_device_ms = 0.0;
+    for (size_t i = 0; i + 1 < p->cspan.size(); i += 2) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, p->cspan[i], p->cspan[i + 1]) == hipSuccess) p->create_device_ms += ms;
+    }
+    for (hipEvent_t e : p->cspan) (void)hipEventDestroy(e);
+    p->cspan.clear();
     *plan_out = p;
     return SRT_OK;
 }
@@ -1807,6 +1818,7 @@ srt_status srt_plan_timing(const srt_plan *p, srt_timing *o) {
     o->loss_fold = p->algo == SRT_ALGO_FW && p->t_level ? 1u : 0u;
     o->reserved0 = 0;
     o->edge_visits = p->algo == SRT_ALGO_LEVEL ? p->lvl_visits : 0;
+    o->create_device_ms = p->create_device_ms;
     return SRT_OK;
 }
 
@@ -1826,6 +1838,7 @@ void srt_plan_destroy(srt_plan *p) {
     (void)give_stream_set(p);  // synchronised above: reusable by the next plan
     for (hipEvent_t e : p->ev) hipEventDestroy(e);
     for (hipEvent_t e : p->ev_tail) hipEventDestroy(e);
+    for (hipEvent_t e : p->cspan) hipEventDestroy(e);
     for (hipEvent_t e : {p->ev_begin, p->ev_end, p->ev_cross, p->ev_pivot, p->ev_row, p->ev_bcast, p->ev_loss0,
                          p->ev_loss1, p->ev_upload})
         if (e) hipEventDestroy(e);
@@ -2733,6 +2746,24 @@ srt_status init_device(int device, std::string *msg) {
 }  // extern "C"
 
 namespace srt {
+void cspan_begin(srt_plan *p) {
+    if (!p->in_create) return;
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return;
+    (void)hipEventRecord(e, p->stream);
+    p->cspan.push_back(e);
+}
+void cspan_end(srt_plan *p) {
+    if (!p->in_create || p->cspan.size() % 2 == 0) return;
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) {
+        (void)hipEventDestroy(p->cspan.back());
+        p->cspan.pop_back();
+        return;
+    }
+    (void)hipEventRecord(e, p->stream);
+    p->cspan.push_back(e);
+}
 void init_wait() {
     std::thread t;
     {

@@ -2978,8 +2978,10 @@ srt_status fw_ecc_bound(srt_plan *p, uint32_t max_sweeps, uint64_t *bound_ns, ui
         uint32_t h = 0;
         e = hipMemsetAsync(flag, 0, 4, p->stream);
         if (e != hipSuccess) break;
+        cspan_begin(p);
         hipLaunchKernelGGL(ecc_sweep_kernel, dim3(blocks), dim3(256), 0, p->stream, p->d_row_ptr, p->d_col, p->d_lat,
                            V, dout, din, flag);
+        cspan_end(p);
         e = hipMemcpyAsync(&h, flag, 4, hipMemcpyDeviceToHost, p->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
         *sweeps = it + 1;
@@ -2990,8 +2992,10 @@ srt_status fw_ecc_bound(srt_plan *p, uint32_t max_sweeps, uint64_t *bound_ns, ui
     }
     unsigned long long m[2] = {~0ull, ~0ull};
     if (e == hipSuccess && settled) {
+        cspan_begin(p);
         hipLaunchKernelGGL(ecc_max_kernel, dim3(std::min<uint32_t>(1024, (V + 255) / 256)), dim3(256), 0, p->stream,
                            dout, din, V, out);
+        cspan_end(p);
         e = hipMemcpyAsync(m, out, 16, hipMemcpyDeviceToHost, p->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
     }

@@ -177,6 +177,10 @@ struct srt_plan {
     uint64_t emu_tight = 0, emu_maxw = 0;  // emulation: tight edges / max latency of the closure
     std::string desc;
     bool identity_nodes = false;
+    bool ident_rows = false;  // the adjacency is V identity rows (host scan, CsrStats::ident)
+    double create_device_ms = 0.0;  // device work of srt_plan_create (probes, symmetry / bound checks)
+    bool in_create = false;         // srt_plan_create is running: its kernels are timed (srt::cspan_*)
+    std::vector<hipEvent_t> cspan;  // event pairs around those kernels
 
     // device buffers
     uint64_t *d_row_ptr = nullptr;
@@ -376,6 +380,11 @@ struct srt_plan {
 };
 
 namespace srt {
+// plan creation's kernels, timed by event pairs on the plan's stream while
+// p->in_create (srt_timing.create_device_ms sums them; host work between the
+// pairs -- allocation, count read-backs -- is not device time)
+void cspan_begin(srt_plan *p);
+void cspan_end(srt_plan *p);
 // A host routing table in the record form of its download (srt_routing.cpp
 // decodes it per path() call): SRT_RI_REC6 = lat16[n*n] (latency / g, 0xFFFF
 // unreachable) + loss[n*n]; SRT_RI_REC8 = rec8[n*n] {latency / g (~0:

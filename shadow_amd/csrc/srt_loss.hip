@@ -436,44 +436,65 @@ __global__ __launch_bounds__(256) void lvl_in_kernel(uint32_t V, uint32_t cls, u
 }
 
 // Exact check that a level plan's class in-rows equal its out-rows, so the
-// run builds only the out-rows (lvl_sym): every adjacency row u is exactly the
-// columns 0 .. V-1 in order (complete graphs as Shadow writes them, self-loop
-// included), and every pair of latency <= wmax_ns has its mirror with the same
-// latency (and, loss != nullptr, the same loss bits) -- then the class-c
-// in-entries of x are the class-c out-entries of x, entry for entry.  64 x 64
-// tiles (i <= j) and their mirrors through LDS; any difference clears *ok.
-__global__ __launch_bounds__(256) void lvl_sym_tile_kernel(uint32_t V, const uint64_t *__restrict__ row_ptr,
-                                                           const uint32_t *__restrict__ col,
-                                                           const uint64_t *__restrict__ lat,
+// run builds only the out-rows (lvl_sym): the adjacency is V identity rows
+// (proved by the host scan, CsrStats::ident: entry (u, v) at u * V + v) and
+// every pair of latency <= wmax_ns has its mirror with the same latency (and,
+// loss != nullptr, the same loss bits) -- then the class-c in-entries of x are
+// the class-c out-entries of x, entry for entry.  Triangle tile pairs (bi <=
+// bj) of 64 x 64: tile (bj, bi) staged in LDS, tile (bi, bj) compared with it
+// transposed; a wave reads 64 consecutive latencies of a row a step (512 B),
+// losses only where a latency is short enough to matter.  Any difference
+// clears *ok.
+__global__ __launch_bounds__(256) void lvl_sym_tile_kernel(uint32_t V, const uint64_t *__restrict__ lat,
                                                            const float *__restrict__ loss, uint64_t wmax_ns,
                                                            uint32_t *ok) {
     __shared__ uint64_t tl[64][65];
     __shared__ uint32_t tp[64][65];
-    const uint32_t nb = (V + 63) / 64, tid = threadIdx.x;
+    const uint32_t nb = (V + 63) / 64, tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const uint64_t ntri = (uint64_t)nb * (nb + 1) / 2;
     bool bad = false;
-    for (uint64_t t = blockIdx.x; t < (uint64_t)nb * nb; t += gridDim.x) {
-        const uint32_t bi = (uint32_t)(t / nb), bj = (uint32_t)(t % nb);
-        if (bi > bj) continue;  // uniform
-        // tile (bj, bi) staged, then compared with tile (bi, bj) transposed
-        for (uint32_t e = tid; e < 64 * 64; e += 256) {
-            const uint32_t r = e / 64, c = e % 64, u = bj * 64 + r, v = bi * 64 + c;
-            if (u < V && v < V) {
-                const uint64_t k = (uint64_t)u * V + v;
-                tl[r][c] = lat[k];
-                tp[r][c] = loss ? __float_as_uint(loss[k]) : 0u;
-                bad |= row_ptr[u] != (uint64_t)u * V || col[k] != v;
-            }
+    for (uint64_t t = blockIdx.x; t < ntri; t += gridDim.x) {
+        // triangle index -> (bi, bj), bi <= bj: row bi starts at bi * nb - bi (bi - 1) / 2
+        const double nn = 2.0 * nb + 1.0;
+        uint32_t bi = (uint32_t)((nn - sqrt(nn * nn - 8.0 * (double)t)) * 0.5);
+        auto row0 = [&](uint64_t r) { return r * nb - r * (r - 1) / 2; };
+        while (bi > 0 && row0(bi) > t) --bi;
+        while (row0(bi + 1) <= t) ++bi;
+        const uint32_t bj = bi + (uint32_t)(t - row0(bi));
+        // a wave's 16 rows of a tile in flight at once (latency and loss
+        // together: 12 B a lane a row), then through LDS
+        const uint32_t v_a = bi * 64 + tx;  // staged tile (bj, bi): column bi * 64 + tx
+        uint64_t la[16];
+        uint32_t pa[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t u = bj * 64 + ty + 4 * i;
+            const bool in = u < V && v_a < V;
+            const uint64_t k = (uint64_t)u * V + v_a;
+            la[i] = in ? lat[k] : 0ull;
+            pa[i] = in && loss ? __float_as_uint(loss[k]) : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            tl[ty + 4 * i][tx] = la[i];
+            tp[ty + 4 * i][tx] = pa[i];
         }
         __syncthreads();
-        for (uint32_t e = tid; e < 64 * 64; e += 256) {
-            const uint32_t r = e / 64, c = e % 64, u = bi * 64 + r, v = bj * 64 + c;
-            if (u < V && v < V) {
-                const uint64_t k = (uint64_t)u * V + v;
-                const uint64_t l = lat[k];
-                bad |= row_ptr[u] != (uint64_t)u * V || col[k] != v;
-                const uint64_t lm = tl[c][r];
-                if (u != v && (l <= wmax_ns || lm <= wmax_ns))
-                    bad |= l != lm || (loss && __float_as_uint(loss[k]) != tp[c][r]);
+        const uint32_t v_b = bj * 64 + tx;  // compared tile (bi, bj)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t u = bi * 64 + ty + 4 * i;
+            const bool in = u < V && v_b < V;
+            const uint64_t k = (uint64_t)u * V + v_b;
+            la[i] = in ? lat[k] : 0ull;
+            pa[i] = in && loss ? __float_as_uint(loss[k]) : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t r = ty + 4 * i, u = bi * 64 + r;
+            if (u < V && v_b < V && u != v_b) {
+                const uint64_t l = la[i], lm = tl[tx][r];
+                if (l <= wmax_ns || lm <= wmax_ns) bad |= l != lm || pa[i] != tp[tx][r];
             }
         }
         __syncthreads();
@@ -2983,15 +3004,19 @@ srt_status level_csr(srt_plan *p, uint64_t wmax, bool with_loss, srt_err *err) {
         p->d_tpk = p->d_tpk2 = nullptr;
         p->t_cap = 0;
         srt_status s2;
+        // symmetric plans read the in-rows through the out-rows: no second array
+        // (allocated below when a later run needs in-rows after all)
         if ((s2 = grow(&p->d_tpk, &ca, entries + 1024, err, "hipMalloc(level out-rows)")) != SRT_OK ||
-            (s2 = grow(&p->d_tpk2, &cb, entries + 1024, err, "hipMalloc(level in-rows)")) != SRT_OK)
+            (!single && (s2 = grow(&p->d_tpk2, &cb, entries + 1024, err, "hipMalloc(level in-rows)")) != SRT_OK))
             return s2;
         p->lvl_cap = entries;
         return SRT_OK;
     };
     const bool first = !p->lvl_cap;
     if (first && p->lvl_est && (st = size_arrays(p->lvl_est)) != SRT_OK) return st;
+    cspan_begin(p);
     out_pass();
+    cspan_end(p);
     if (first) {
         hipError_t e = hipMemcpyAsync(p->h_tcount, p->d_tcursor, sizeof(uint64_t), hipMemcpyDeviceToHost, M);
         if (e == hipSuccess) e = hipStreamSynchronize(M);
@@ -2999,7 +3024,9 @@ srt_status level_csr(srt_plan *p, uint64_t wmax, bool with_loss, srt_err *err) {
         const uint64_t count = std::max<uint64_t>(p->h_tcount[0], 1);
         if (count > p->lvl_cap) {
             if ((st = size_arrays(count)) != SRT_OK) return st;
+            cspan_begin(p);
             out_pass();
+            cspan_end(p);
         }
         p->lvl_cap = count;
     }
@@ -3007,13 +3034,19 @@ srt_status level_csr(srt_plan *p, uint64_t wmax, bool with_loss, srt_err *err) {
         // symmetric plan (lvl_sym_tile_kernel): the in-rows are the out-rows;
         // their offsets copied, the entries read through the same array
         // (level_ctx)
+        cspan_begin(p);
         const hipError_t e = hipMemcpyAsync(p->d_tcls + vc1, p->d_tcls, vc1 * 4, hipMemcpyDeviceToDevice, M);
+        cspan_end(p);
         if (e != hipSuccess) return fail(err, e, "class offsets (symmetric)");
         p->t_cls = cls;
         p->t_q = 1;
         p->t_level = true;
         p->t_edges = p->lvl_cap;
         return SRT_OK;
+    }
+    if (!p->d_tpk2) {  // a symmetric plan whose run needs in-rows (its losses did not mirror)
+        uint64_t cb = 0;
+        if ((st = grow(&p->d_tpk2, &cb, p->lvl_cap + 1024, err, "hipMalloc(level in-rows)")) != SRT_OK) return st;
     }
     size_t need = 0;
     hipError_t e = rocprim::exclusive_scan(nullptr, need, p->d_tccnt, p->d_tcls + vc1, 0u, (size_t)vc1,
@@ -3025,12 +3058,14 @@ srt_status level_csr(srt_plan *p, uint64_t wmax, bool with_loss, srt_err *err) {
         return st;
     p->tscan_tmp_cap = tcap;
     size_t have = p->tscan_tmp_cap;
+    cspan_begin(p);
     e = rocprim::exclusive_scan(p->d_tscan_tmp, have, p->d_tccnt, p->d_tcls + vc1, 0u, (size_t)vc1,
                                 rocprim::plus<uint32_t>(), M);
     if (e != hipSuccess) return fail(err, e, "class scan");
     const uint64_t vmask = q ? (1ull << vb) - 1ull : 0xffffffffull;
     hipLaunchKernelGGL(lvl_in_kernel, dim3(blocks), dim3(256), 0, M, V, cls, vmask, p->d_tcls, p->d_tpk,
                        p->d_tcls + vc1, p->d_tccnt + vc1, p->d_tpk2);
+    cspan_end(p);
     p->t_cls = cls;
     p->t_q = 1;
     p->t_level = true;
@@ -3164,8 +3199,11 @@ srt_status level_probe(srt_plan *p, uint64_t wmax, uint32_t wc, uint64_t *bound,
     // longer than the longest edge)
     const uint32_t cap = (uint32_t)LQ;
     if (e == hipSuccess) {
-        if ((st = launch_solve(p, nullptr, job, cap, false, d_pr, err)) != SRT_OK ||
-            (st = launch_solve(p, nullptr, job, cap, true, d_pr + 16, err)) != SRT_OK) {
+        cspan_begin(p);
+        st = launch_solve(p, nullptr, job, cap, false, d_pr, err);
+        if (st == SRT_OK) st = launch_solve(p, nullptr, job, cap, true, d_pr + 16, err);
+        cspan_end(p);
+        if (st != SRT_OK) {
             (void)hipStreamSynchronize(p->stream);
             (void)hipFree(d_pr);
             return st;
@@ -3287,17 +3325,18 @@ void loss_mirror_check(const uint32_t *d_idx, uint64_t count, uint64_t V, const 
 
 srt_status level_sym_check(srt_plan *p, uint64_t wmax_units, bool with_loss, bool *sym, srt_err *err) {
     *sym = false;
-    if (!p->V || p->n_adj != (uint64_t)p->V * p->V) return SRT_OK;
+    if (!p->V || p->n_adj != (uint64_t)p->V * p->V || !p->ident_rows) return SRT_OK;
     uint32_t *d_ok = nullptr;
     hipError_t e = hipMalloc(&d_ok, 4);
     if (e != hipSuccess) return fail(err, e, "hipMalloc(symmetry flag)");
     uint32_t one = 1;
     e = hipMemcpyAsync(d_ok, &one, 4, hipMemcpyHostToDevice, p->stream);
     const uint64_t nb = (p->V + 63) / 64;
+    cspan_begin(p);
     if (e == hipSuccess)
-        hipLaunchKernelGGL(lvl_sym_tile_kernel, dim3((uint32_t)std::min<uint64_t>(nb * nb, 8192)), dim3(256), 0,
-                           p->stream, p->V, p->d_row_ptr, p->d_col, p->d_lat, with_loss ? p->d_loss : nullptr,
-                           wmax_units * p->kp.g, d_ok);
+        hipLaunchKernelGGL(lvl_sym_tile_kernel, dim3((uint32_t)std::min<uint64_t>(nb * (nb + 1) / 2, 8192)), dim3(256),
+                           0, p->stream, p->V, p->d_lat, with_loss ? p->d_loss : nullptr, wmax_units * p->kp.g, d_ok);
+    cspan_end(p);
     uint32_t ok = 0;
     if (e == hipSuccess) e = hipMemcpyAsync(&ok, d_ok, 4, hipMemcpyDeviceToHost, p->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
@@ -3315,8 +3354,10 @@ srt_status level_min_edge(srt_plan *p, uint64_t *min_ns, srt_err *err) {
     if (e != hipSuccess) return fail(err, e, "hipMalloc(edge min)");
     (void)hipMemsetAsync(d, 0xff, sizeof *d, p->stream);
     const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(8192, (p->V + 3) / 4));
+    cspan_begin(p);
     hipLaunchKernelGGL(edge_min_kernel, dim3(blocks), dim3(256), 0, p->stream, p->V, p->d_row_ptr, p->d_col, p->d_lat,
                        d);
+    cspan_end(p);
     e = hipMemcpyAsync(min_ns, d, sizeof *d, hipMemcpyDeviceToHost, p->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
     (void)hipFree(d);

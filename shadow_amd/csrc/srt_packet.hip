@@ -11,15 +11,14 @@
 //   else: delay = latency; counter++; SENT; deliver = max(t + delay, round_end)
 //
 // One kernel a round (round_kernel): a workgroup takes HB consecutive source
-// hosts.  Phase 1: one lane per host walks its packets in send order and
-// advances its xoshiro256++ state -- the only sequential part, a dependent
-// chain of ~20 integer ops a draw -- leaving the draws in LDS.  Phase 2: the
-// workgroup's 256 lanes decide the block's packets from those draws: one 16-B
-// gather of the packed {latency, loss} table record (packed once per build),
+// hosts.  One lane per host walks its packets in send order and advances its
+// xoshiro256++ state -- the only sequential part, a dependent chain of ~20
+// integer ops a draw -- leaving the draws in LDS, while every lane loads its
+// packets (the record, then one 16-B gather of the packed {latency, loss}
+// table record, packed once per build); then every lane decides its packets:
 // the drop rule, the deliver-time clamp, the per-path counter, block minima.
 // The draws never travel through HBM (a block whose packets overflow its LDS
-// keeps them in a global scratch instead).  The host walks of the other
-// resident workgroups overlap each block's chain.
+// keeps them in a global scratch instead).
 //
 // The packet's table row and column come either from srt_pkt (resolved by the
 // caller) or, in srt_packet_batch_ip, from its IPv4 addresses through the
@@ -50,7 +49,8 @@ __host__ __device__ __forceinline__ uint64_t xoshiro_next(uint64_t &s0, uint64_t
 constexpr int RT = 256;          // threads a round workgroup
 constexpr int HB = 8;            // source hosts a workgroup (C5: 1,250 workgroups, ~800 packets each)
 constexpr uint32_t DCAP = 3072;  // draws a workgroup keeps in LDS (24 KB)
-constexpr int PF = 16;           // send times in flight a host walk
+constexpr int KP = 4;            // packets a lane holds across the host walks (RT * KP = 1,024 a workgroup)
+constexpr int PF = 16;           // send times in flight a host walk (the exact walk)
 
 // the packet's (row, column) of the table: resolved by the caller, or from its
 // addresses (network byte order); -1 when an address has no row
@@ -65,6 +65,50 @@ __device__ __forceinline__ void pkt_rows(const srt_pkt &k, const srt::IpTable &i
     }
 }
 
+// a packet's inputs once its record and table entry are loaded
+struct PktIn {
+    uint64_t t, delay;
+    uint64_t o;          // table index (~0: completed or unresolved)
+    uint32_t payload;
+    float ls;
+    bool live, unresolved;
+};
+
+template <bool IP, bool TAB16>
+__device__ __forceinline__ PktIn load_pkt(const srt_pkt *__restrict__ pkts, uint32_t p, const srt_round &r,
+                                          const uint4 *__restrict__ tab, const uint64_t *__restrict__ lat,
+                                          const float *__restrict__ loss, uint32_t n, const srt::IpTable &ipt) {
+    const srt_pkt k = pkts[p];
+    PktIn x{k.t_ns, 0, ~0ull, k.payload_size, 0.0f, false, false};
+    if (k.t_ns < r.sim_end_ns) {
+        int32_t i, j;
+        pkt_rows<IP>(k, ipt, i, j);
+        if (i < 0 || j < 0) {
+            x.unresolved = true;  // the reference's reliability(..).unwrap() panics (worker.rs:359)
+        } else {
+            x.live = true;
+            x.o = (uint64_t)(uint32_t)i * n + (uint32_t)j;
+            if (TAB16) {
+                const uint4 rec = tab[x.o];
+                x.delay = (uint64_t)rec.x | (uint64_t)rec.y << 32;
+                x.ls = __uint_as_float(rec.z);
+            } else {
+                x.delay = lat[x.o];
+                x.ls = loss[x.o];
+            }
+        }
+    }
+    return x;
+}
+
+// The round of HB source hosts.  The walks are dependent chains (one draw a
+// packet, host.rs:233 stream order) and the loads are independent, so they
+// overlap: every lane issues the loads of its packets (record, then the 16-B
+// table record) while one lane per host runs its chain speculatively -- a draw
+// for every packet, which is exact unless a packet is completed (t >= sim_end:
+// no draw, worker.rs:336-339).  The block then knows which hosts had one;
+// those (rare: the last round of a simulation) redo their walk exactly from
+// the saved state.  Then every lane decides its packets from the draws in LDS.
 template <bool IP, bool TAB16>
 __global__ __launch_bounds__(RT) void round_kernel(const srt_pkt *__restrict__ pkts,
                                                    const uint32_t *__restrict__ host_ptr, uint32_t n_hosts,
@@ -77,21 +121,64 @@ __global__ __launch_bounds__(RT) void round_kernel(const srt_pkt *__restrict__ p
                                                    uint64_t *__restrict__ gdraws, uint32_t *__restrict__ bad) {
     __shared__ uint64_t sdraw[DCAP];
     __shared__ uint32_t sptr[HB + 1];
+    __shared__ uint32_t scomp;  // bit i: host i of the block has a completed packet
     __shared__ unsigned long long red[2][RT / 64];
     const uint32_t t = threadIdx.x;
     const uint32_t h0 = blockIdx.x * HB;
     const uint32_t nh = min((uint32_t)HB, n_hosts - h0);
     if (t <= nh) sptr[t] = host_ptr[h0 + t];
+    if (t == 0) scomp = 0;
     __syncthreads();
     const uint32_t pb = sptr[0], pe = sptr[nh];
     const bool in_lds = pe - pb <= DCAP;
-    // phase 1: host i walked by lane i / 4 of wave i % 4 (the chains spread over the SIMDs)
-    {
-        const uint32_t i = (t & 63) * 4 + (t >> 6);
-        if ((t & 63) < (HB + 3) / 4 && i < nh) {
-            const uint64_t h = h0 + i;
-            uint64_t s0 = rng[4 * h], s1 = rng[4 * h + 1], s2 = rng[4 * h + 2], s3 = rng[4 * h + 3];
-            const uint32_t b = sptr[i], e = sptr[i + 1];
+    auto put = [&](uint32_t p, uint64_t d) {
+        if (in_lds) sdraw[p - pb] = d;
+        else gdraws[p] = d;
+    };
+    // (1) the lane's packets: loads issued first (they do not depend on the draws)
+    PktIn mine[KP];
+#pragma unroll
+    for (int q = 0; q < KP; ++q) {
+        const uint32_t p = pb + t + q * RT;
+        if (p < pe) mine[q] = load_pkt<IP, TAB16>(pkts, p, r, tab, lat, loss, n, ipt);
+    }
+    // (2) one lane a host: the speculative walk (no send-time loads), host i
+    // on lane i / 4 of wave i % 4 so the chains spread over the SIMDs
+    const uint32_t wi = (t & 63) * 4 + (t >> 6);
+    const bool walker = (t & 63) < (HB + 3) / 4 && wi < nh;
+    uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    if (walker) {
+        const uint64_t h = h0 + wi;
+        a0 = s0 = rng[4 * h];
+        a1 = s1 = rng[4 * h + 1];
+        a2 = s2 = rng[4 * h + 2];
+        a3 = s3 = rng[4 * h + 3];
+        for (uint32_t p = sptr[wi], e = sptr[wi + 1]; p < e; ++p) put(p, xoshiro_next(s0, s1, s2, s3));
+    }
+    // hosts with a completed packet (their walks skip its draw)
+#pragma unroll
+    for (int q = 0; q < KP; ++q) {
+        const uint32_t p = pb + t + q * RT;
+        if (p < pe && mine[q].t >= r.sim_end_ns) {
+            uint32_t i = 0;
+            while (i + 1 < nh && sptr[i + 1] <= p) ++i;
+            atomicOr(&scomp, 1u << i);
+        }
+    }
+    for (uint32_t p = pb + t + KP * RT; p < pe; p += RT)  // past KP a lane: the send time only
+        if (pkts[p].t_ns >= r.sim_end_ns) {
+            uint32_t i = 0;
+            while (i + 1 < nh && sptr[i + 1] <= p) ++i;
+            atomicOr(&scomp, 1u << i);
+        }
+    __syncthreads();
+    if (walker) {
+        if ((scomp >> wi) & 1u) {  // the exact walk, from the saved state
+            s0 = a0;
+            s1 = a1;
+            s2 = a2;
+            s3 = a3;
+            const uint32_t b = sptr[wi], e = sptr[wi + 1];
             for (uint32_t p0 = b; p0 < e; p0 += PF) {
                 uint64_t tt[PF];
 #pragma unroll
@@ -99,62 +186,50 @@ __global__ __launch_bounds__(RT) void round_kernel(const srt_pkt *__restrict__ p
 #pragma unroll
                 for (int q = 0; q < PF; ++q) {
                     if (p0 + q >= e || tt[q] >= r.sim_end_ns) continue;  // completed: no draw
-                    const uint64_t d = xoshiro_next(s0, s1, s2, s3);
-                    if (in_lds) sdraw[p0 + q - pb] = d;
-                    else gdraws[p0 + q] = d;
+                    put(p0 + q, xoshiro_next(s0, s1, s2, s3));
                 }
             }
-            rng[4 * h] = s0;
-            rng[4 * h + 1] = s1;
-            rng[4 * h + 2] = s2;
-            rng[4 * h + 3] = s3;
         }
+        const uint64_t h = h0 + wi;
+        rng[4 * h] = s0;
+        rng[4 * h + 1] = s1;
+        rng[4 * h + 2] = s2;
+        rng[4 * h + 3] = s3;
     }
     __syncthreads();
-    // phase 2: the block's packets, one a lane
+    // (3) the decisions
     unsigned long long min_lat = ~0ull, min_deliver = ~0ull;
     bool unresolved = false;
-    for (uint32_t p = pb + t; p < pe; p += RT) {
-        const srt_pkt k = pkts[p];
+    auto decide = [&](uint32_t p, const PktIn &x) {
         uint32_t f = SRT_PDS_NONE;
         uint64_t d = 0;
-        if (k.t_ns < r.sim_end_ns) {
-            int32_t i, j;
-            pkt_rows<IP>(k, ipt, i, j);
-            if (i < 0 || j < 0) {
-                unresolved = true;  // the reference's reliability(..).unwrap() panics (worker.rs:359)
+        unresolved |= x.unresolved;
+        if (x.live) {
+            const float rel32 = 1.0f - x.ls;
+            const double reliability = (double)rel32;
+            const uint64_t draw = in_lds ? sdraw[p - pb] : gdraws[p];
+            const double chance = (double)(draw >> 11) * 0x1.0p-53;
+            const bool bootstrapping = x.t < r.bootstrap_end_ns;
+            if (!bootstrapping && chance >= reliability && x.payload > 0) {
+                f = SRT_PDS_INET_DROPPED;
             } else {
-                const uint64_t o = (uint64_t)(uint32_t)i * n + (uint32_t)j;
-                uint64_t delay;
-                float ls;
-                if (TAB16) {
-                    const uint4 rec = tab[o];
-                    delay = (uint64_t)rec.x | (uint64_t)rec.y << 32;
-                    ls = __uint_as_float(rec.z);
-                } else {
-                    delay = lat[o];
-                    ls = loss[o];
-                }
-                const float rel32 = 1.0f - ls;
-                const double reliability = (double)rel32;
-                const uint64_t draw = in_lds ? sdraw[p - pb] : gdraws[p];
-                const double chance = (double)(draw >> 11) * 0x1.0p-53;
-                const bool bootstrapping = k.t_ns < r.bootstrap_end_ns;
-                if (!bootstrapping && chance >= reliability && k.payload_size > 0) {
-                    f = SRT_PDS_INET_DROPPED;
-                } else {
-                    f = SRT_PDS_INET_SENT;
-                    d = k.t_ns + delay;
-                    if (d < r.round_end_ns) d = r.round_end_ns;
-                    if (counters) atomicAdd(&counters[o], 1ull);
-                    min_lat = delay < min_lat ? delay : min_lat;
-                    min_deliver = d < min_deliver ? d : min_deliver;
-                }
+                f = SRT_PDS_INET_SENT;
+                d = x.t + x.delay;
+                if (d < r.round_end_ns) d = r.round_end_ns;
+                if (counters) atomicAdd(&counters[x.o], 1ull);
+                min_lat = x.delay < min_lat ? x.delay : min_lat;
+                min_deliver = d < min_deliver ? d : min_deliver;
             }
         }
         flags[p] = f;
         deliver[p] = d;
+    };
+#pragma unroll
+    for (int q = 0; q < KP; ++q) {
+        const uint32_t p = pb + t + q * RT;
+        if (p < pe) decide(p, mine[q]);
     }
+    for (uint32_t p = pb + t + KP * RT; p < pe; p += RT) decide(p, load_pkt<IP, TAB16>(pkts, p, r, tab, lat, loss, n, ipt));
     if (IP && __any(unresolved) && (t & 63) == 0) atomicOr(bad, 1u);
     // wave, then block reduction: one pair of partials per block (same-address
     // atomics from every wave serialise at the memory-side atomic unit)

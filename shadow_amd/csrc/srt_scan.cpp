@@ -176,7 +176,7 @@ void scan_rows(const srt_csr *g, uint32_t r0, uint32_t r1, CsrStats &st, CsrStat
         }
         maxlat = a.mx > maxlat ? a.mx : maxlat;
         over |= a.hi != 0;
-        if (identity) ident &= n == V && a.idx == 0;
+        ident &= n == V && a.idx == 0;
         uint64_t first = ~0ull;
         if (a.self) first = (uint64_t)(std::find(g->col + b, g->col + e, u) - g->col);
         out->sl_cnt[u] = a.self;
@@ -208,10 +208,12 @@ void scan_rows(const srt_csr *g, uint32_t r0, uint32_t r1, CsrStats &st, CsrStat
     st.sym_b = sb;
     if (lat_over && over) *lat_over = true;
     if (identity && !ident) *identity = false;
+    st.ident &= ident;
 }
 
 void merge_stats(const std::vector<CsrStats> &part, uint32_t V, CsrStats *out) {
     out->complete = V > 0;
+    out->ident = V > 0;
     uint32_t sa = 0, sb = 0;
     for (const CsrStats &st : part) {
         out->gcd = std::gcd(out->gcd, st.gcd);
@@ -224,6 +226,7 @@ void merge_stats(const std::vector<CsrStats> &part, uint32_t V, CsrStats *out) {
         out->badcol_k = std::min(out->badcol_k, st.badcol_k);
         out->unique &= st.unique;
         out->complete &= st.complete;
+        out->ident &= st.ident;
     }
     out->sym_a = sa;
     out->sym_b = sb;

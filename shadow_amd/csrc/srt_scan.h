@@ -14,6 +14,9 @@ struct CsrStats {
     uint64_t gcd = 0, maxlat = 0, selfloops = 0;
     uint64_t zero_k = ~0ull, badloss_k = ~0ull, badcol_k = ~0ull;
     bool unique = true, complete = true;
+    // every row is exactly the entries 0 .. V-1 in order (complete graphs as
+    // Shadow writes them): entry (u, v) sits at u * V + v
+    bool ident = true;
     // symmetry fingerprint for the family price: sums over entries (u, v, l)
     // of u*(v*v + l) and of v*(u*u + l) (mod 2^32) -- equal for every graph
     // whose entry multiset is closed under (u, v, l) -> (v, u, l)

@@ -37,7 +37,7 @@ def test_abi_version_and_struct_layout():
     L = _lib.lib()
     assert L.srt_abi_version() == 4
     assert C.sizeof(_lib.SrtPath) == 16  # #[repr(C)] PathProperties mirror
-    assert C.sizeof(_lib.SrtTiming) == 80  # ABI 2: + edge_visits (ABI 3: + srt_plan_shard_rows)
+    assert C.sizeof(_lib.SrtTiming) == 88  # ABI 2: + edge_visits; ABI 4: + create_device_ms
     assert C.sizeof(_lib.SrtCsr) == 56
     assert C.sizeof(_lib.SrtErr) == 268
 
