@@ -996,6 +996,10 @@ static void *sp_worker(void *arg) {
 
 static int n_threads(int threads) {
     if (threads > 0) return threads;
+    /* the job's CPU share when the box declares one (the GPU box: 16 of its
+       many CPUs), else every online CPU (rayon's default pool) */
+    const char *e = getenv("OMP_NUM_THREADS");
+    if (e && atoi(e) > 0) return atoi(e);
     long c = sysconf(_SC_NPROCESSORS_ONLN);
     return c > 0 ? (int)c : 1;
 }

@@ -1001,7 +1001,18 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     }
 
     // the kernels of creation (bound proofs, probes, symmetry check) are
-    // timed from here on (srt::cspan_*): srt_timing.create_device_ms
+    // timed from here on (srt::cspan_*): srt_timing.create_device_ms.  The
+    // code objects are loaded first (once per device and process; srt_init
+    // does it ahead of time), so a span holds no lazy load of a kernel.
+    {
+        static std::mutex mu;
+        static std::vector<int> loaded;
+        std::lock_guard<std::mutex> lk(mu);
+        if (std::find(loaded.begin(), loaded.end(), p->device) == loaded.end()) {
+            (void)hipSetDevice(p->device);
+            if (srt::preload_kernels() == hipSuccess) loaded.push_back(p->device);
+        }
+    }
     p->in_create = true;
     auto dev_timed = [&](auto &&fn) -> srt_status { return fn(); };
 

@@ -47,9 +47,9 @@ __host__ __device__ __forceinline__ uint64_t xoshiro_next(uint64_t &s0, uint64_t
 }
 
 constexpr int RT = 256;          // threads a round workgroup
-constexpr int HB = 8;            // source hosts a workgroup (C5: 1,250 workgroups, ~800 packets each)
+constexpr int HB = 16;           // source hosts a workgroup (C5: 625 workgroups, ~1,600 packets each)
 constexpr uint32_t DCAP = 3072;  // draws a workgroup keeps in LDS (24 KB)
-constexpr int KP = 4;            // packets a lane holds across the host walks (RT * KP = 1,024 a workgroup)
+constexpr int KP = 8;            // packets a lane holds across the host walks (RT * KP = 2,048 a workgroup)
 constexpr int PF = 16;           // send times in flight a host walk (the exact walk)
 
 // the packet's (row, column) of the table: resolved by the caller, or from its
@@ -142,10 +142,13 @@ __global__ __launch_bounds__(RT) void round_kernel(const srt_pkt *__restrict__ p
         const uint32_t p = pb + t + q * RT;
         if (p < pe) mine[q] = load_pkt<IP, TAB16>(pkts, p, r, tab, lat, loss, n, ipt);
     }
-    // (2) one lane a host: the speculative walk (no send-time loads), host i
-    // on lane i / 4 of wave i % 4 so the chains spread over the SIMDs
-    const uint32_t wi = (t & 63) * 4 + (t >> 6);
-    const bool walker = (t & 63) < (HB + 3) / 4 && wi < nh;
+    // (2) one lane a host, all in wave 0: the speculative walk (no send-time
+    // loads).  A chain instruction costs its wave a full issue slot however
+    // few lanes are active, so the walkers share one wave: the other three
+    // waves' SIMDs stay free for other workgroups' walks and loads (walkers
+    // spread one or two a wave measured 54-72 us a C5 round, VALU issue-bound)
+    const uint32_t wi = t;
+    const bool walker = t < nh;
     uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, a0 = 0, a1 = 0, a2 = 0, a3 = 0;
     if (walker) {
         const uint64_t h = h0 + wi;

@@ -571,7 +571,7 @@ srt_status srt_xz_decompress(const uint8_t *in, size_t len, uint8_t **out, size_
             set(err, SRT_ERR_OOM, "out of host memory");
             return SRT_ERR_OOM;
         }
-        std::memcpy(r, buf.data(), buf.size());
+        if (!buf.empty()) std::memcpy(r, buf.data(), buf.size());
         r[buf.size()] = 0;
         *out = r;
         *out_len = buf.size();

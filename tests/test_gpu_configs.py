@@ -7,9 +7,11 @@ it checks seeded sample rows, and size-independent properties cover the rest
 on the device (latency symmetry of undirected graphs, every pair reachable).
 
   C1  1,000-node complete graph through its GML text: the full table
-  C3  16,384-node complete graph: 16 seeded oracle rows + symmetry
+  C1  also against tests/golden/c1_table.json: the SHA-256 of the oracle's table
+  C3  16,384-node complete graph: 128 oracle rows (every 8-rank shard's first
+      and last) + symmetry
   C4  100,000-node Barabasi-Albert graph, ALL nodes in use (the sparse sweep's
-      256 groups in flight): 8 seeded oracle rows, symmetric blocks, no
+      256 groups in flight): 32 seeded oracle rows, symmetric blocks, no
       unreachable pair; the 120 GB table never leaves the device
   C5  1M packets / 10k hosts on the C1 nodes (loss U[0,0.25]), decided on the
       GPU's table and by the oracle on ITS OWN table
@@ -62,11 +64,34 @@ def test_c1_full_table_through_gml():
     assert t.min_latency_ns == int(elat.min())
 
 
+def test_c1_table_matches_pinned_fixture():
+    """C1 pinned without a live oracle run: the GPU table (GML text ->
+    srt_compute_shortest_paths, nodes in GML order) hashes to the SHA-256 of
+    the oracle's table committed in tests/golden/c1_table.json
+    (tools/make_c1_fixture.py), and the 1,000 sampled pairs match."""
+    import hashlib
+    import json
+    import os
+    fx = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c1_table.json")))
+    n = fx["nodes"]
+    src, dst, lat, loss = synth.complete_graph(n, fx["seed"])
+    text = synth.gml_text(n, src, dst, lat, loss)
+    assert hashlib.sha256(text.encode()).hexdigest() == fx["gml_sha256"]
+    t = NetworkGraph.parse(text).compute_shortest_paths(np.arange(n, dtype=np.uint32))
+    h = hashlib.sha256(np.ascontiguousarray(t.latency_ns, np.uint64).tobytes() +
+                       np.ascontiguousarray(t.packet_loss, np.float32).tobytes()).hexdigest()
+    assert h == fx["table_sha256"]
+    for i, j, l, p in fx["samples"]:
+        assert int(t.latency_ns[i, j]) == l and int(t.packet_loss[i, j:j + 1].view(np.uint32)[0]) == p
+    assert t.min_latency_ns == fx["min_latency_ns"]
+
+
 def test_c3_16k_rows_vs_oracle_and_symmetry():
     """C3 as the drop-in runs it (AUTO: the level solve -- B from the probe)
-    and forced onto the Floyd-Warshall family: 16 seeded oracle rows bit-exact,
-    latency symmetry on the device, and the two families' tables equal bit for
-    bit."""
+    and forced onto the Floyd-Warshall family: 128 oracle rows bit-exact (the
+    first and last row of every shard of an 8-rank build plus 112 seeded
+    ones), latency symmetry on the device, and the two families' tables equal
+    bit for bit."""
     import torch
 
     n = 16384
@@ -79,17 +104,20 @@ def test_c3_16k_rows_vs_oracle_and_symmetry():
     plan.fetch(table=False)  # every pair reachable (else DISCONNECTED), min latency
     L, P = _device_table(plan)
     assert torch.equal(L, L.t()), "undirected latency table must be symmetric"
-    rows = np.random.default_rng(3).choice(n, 16, replace=False)
+    edges8 = np.array([b for r in range(8) for b in (r * n // 8, (r + 1) * n // 8 - 1)])
+    rest = np.setdiff1d(np.arange(n), edges8)
+    rows = np.concatenate([edges8, np.random.default_rng(3).choice(rest, 112, replace=False)])
+    k = len(rows)
     order = np.concatenate([rows, np.setdiff1d(nodes, rows)]).astype(np.uint32)
     og = O.Graph(False, nodes, *edges)
     del row_ptr, col
-    elat, eloss = O.compute_shortest_paths(og, order, src_count=16, mode=1)
+    elat, eloss = O.compute_shortest_paths(og, order, src_count=k, mode=1)
     # oracle columns are in `order`; put them back in node order
     inv = np.empty(n, np.int64)
     inv[order] = np.arange(n)
     sl_l = lat.reshape(n, n).diagonal().copy()
     sl_p = loss.reshape(n, n).diagonal().copy()
-    _check_rows(L, P, rows, nodes, elat[:16][:, inv], eloss[:16][:, inv], sl_l, sl_p)
+    _check_rows(L, P, rows, nodes, elat[:k][:, inv], eloss[:k][:, inv], sl_l, sl_p)
     # get_smallest_latency_ns over the whole device table == the smallest edge
     assert plan.min_latency_ns == L.min().item() == int(lat.min())
     fw = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_FW).run()
@@ -161,10 +189,10 @@ def test_c4_100k_all_in_use():
     for _ in range(16):  # symmetric 2048 x 2048 blocks
         a, b = rng.integers(0, n - 2048, size=2)
         assert torch.equal(L[a:a + 2048, b:b + 2048], L[b:b + 2048, a:a + 2048].t())
-    rows = np.sort(rng.choice(n, 8, replace=False))
+    rows = np.sort(rng.choice(n, 32, replace=False))
     order = np.concatenate([rows, np.setdiff1d(nodes, rows)]).astype(np.uint32)
     og = O.Graph(False, nodes, src, dst, lat, loss)
-    elat, eloss = O.compute_shortest_paths(og, order, src_count=8, mode=1)
+    elat, eloss = O.compute_shortest_paths(og, order, src_count=32, mode=1)
     inv = np.empty(n, np.int64)
     inv[order] = np.arange(n)
     sl = src == dst
@@ -172,7 +200,7 @@ def test_c4_100k_all_in_use():
     sl_p = np.empty(n, np.float32)
     sl_l[src[sl]] = lat[sl]
     sl_p[src[sl]] = loss[sl]
-    _check_rows(L, P, rows, nodes, elat[:8][:, inv], eloss[:8][:, inv], sl_l, sl_p)
+    _check_rows(L, P, rows, nodes, elat[:32][:, inv], eloss[:32][:, inv], sl_l, sl_p)
     plan.close()
 
 
