@@ -560,6 +560,10 @@ def bench_graph(args, cfg, D):
     ranks = 1
     transport = None
     if args.rank_share > 1 and D.world == 1:
+        # rank 0's share of an N-rank build whose class CSR is sharded too: its
+        # slice built, the all-gather of the slices modelled as a wait (25 us +
+        # received bytes / 300 GB/s; SRT_LVL_SHARD_EMU=0 builds the whole CSR)
+        os.environ.setdefault("SRT_LVL_SHARD_EMU", "1")
         plan.shard_rows(args.rank_share, 0)
         elapsed, step_ms, k_ms, k_launches, k_work, _ = timed_builds(plan, D, args.steps, args.warmup)
         t = plan.timing()
@@ -569,9 +573,12 @@ def bench_graph(args, cfg, D):
                                          "solve_ms_per_step": k_ms / args.steps,
                                          "device_total_ms_last": t["total_ms"],
                                          "implied_value_pairs_per_s": len(nodes) ** 2 / (ms / 1e3),
+                                         "csr_shard_emulated": os.environ.get("SRT_LVL_SHARD_EMU") == "1",
                                          "note": "rank 0's rows of an N-rank row-sharded build, measured alone on one "
-                                                 "GPU: the whole of that rank's work (row sharding has no exchange); "
-                                                 "the implied value assumes the N ranks run concurrently on N GPUs"}}),
+                                                 "GPU: its slice of the class CSR, the slices' all-gather modelled as a "
+                                                 "wait (25 us + received bytes / 300 GB/s), its rows solved (the table "
+                                                 "rows are not exchanged); the implied value assumes the N ranks run "
+                                                 "concurrently on N GPUs"}}),
               flush=True)
         plan.close()
         return None

@@ -569,6 +569,8 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_fbuf);
     hipFree(p->d_draws);
     hipFree(p->d_pkt_tab);
+    hipFree(p->d_lvl_offstage);
+    hipFree(p->d_lvl_counts);
     hipFree(p->d_pkt_bad);
     hipFree(p->d_in_ptr);
     hipFree(p->d_sperm);
@@ -2000,6 +2002,10 @@ srt_status srt_plan_shard_rows(srt_plan *p, int nranks, int rank, srt_err *err) 
     p->row0 = (uint32_t)((uint64_t)p->n * rank / nranks);
     p->row1 = (uint32_t)((uint64_t)p->n * (rank + 1) / nranks);
     p->row_shard = true;
+    // measurement only (bench.py --rank-share): this rank's share of a build
+    // whose class CSR is sharded too, the all-gather modelled (level_csr_sharded)
+    if (const char *e = std::getenv("SRT_LVL_SHARD_EMU"); e && std::atoi(e) == 1 && nranks > 1)
+        p->lvl_emu_ranks = (uint32_t)nranks;
     char d[80];
     std::snprintf(d, sizeof d, " shard=%d/%d rows=[%u,%u)", rank, nranks, p->row0, p->row1);
     p->desc += d;

@@ -333,6 +333,16 @@ struct srt_plan {
     bool lvl_single = false;         // the last class-CSR build made out-rows only (in-rows = out-rows)
     uint64_t lvl_est = 0;            // the probe's entry-count estimate (sizes the arrays before its one pass)
     uint64_t lvl_maxu = 0;           // the longest edge, units of g (the estimate's scale)
+    // sharded class CSR (symmetric level plans over W ranks): rank r builds the
+    // out-rows of vertices [r * vr, (r + 1) * vr) into entry slot r (lvl_seg_cap
+    // entries a slot, so the offsets are absolute) and the slots are
+    // all-gathered (level_csr_sharded)
+    uint64_t lvl_seg_cap = 0;
+    uint32_t *d_lvl_offstage = nullptr;  // W * vr * cls class offsets, slot r = rank r's vertices
+    uint64_t lvl_offstage_cap = 0;
+    unsigned long long *d_lvl_counts = nullptr;  // W per-rank entry counts (sizing)
+    uint32_t lvl_emu_ranks = 0;      // measurement (srt_plan_shard_rows + SRT_LVL_SHARD_EMU=1): rank row0's slice
+    bool lvl_emu_built = false;      // ... every slice built once (the first run); later runs rebuild the own one
     unsigned long long *d_lvisit = nullptr;  // level solve: class entries the last run walked
     uint32_t lvl_q = 0, lvl_rb = 0, lvl_vb = 0;  // quantized level solve: bucket width (units), entry field bits
     uint16_t *d_lmem = nullptr;              // its per-workgroup scratch (lmem_cap u16)

@@ -289,7 +289,7 @@ __global__ __launch_bounds__(256) void tight_rows_kernel(const K *__restrict__ D
 // entries of a class would all hit one counter.  Entries past `cap` are
 // counted, not written (the caller sizes and runs again).
 template <bool WITH_LOSS, bool IN = true, bool IDENT = false>
-__global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t V, const uint64_t *__restrict__ row_ptr,
+__global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t u0, uint32_t V, const uint64_t *__restrict__ row_ptr,
                                                       const uint32_t *__restrict__ col,
                                                       const uint64_t *__restrict__ lat, const float *__restrict__ loss,
                                                       uint64_t g, double inv_g, uint64_t wmax_ns, uint32_t cls,
@@ -307,7 +307,7 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t V, const uint64_t
     // l = w * g exactly; the class: w / q (q = 0: the exact weight)
     auto units_of = [&](uint64_t l) -> uint64_t { return (uint64_t)((double)l * inv_g + 0.5); };
     auto cls_of = [&](uint64_t l) -> uint32_t { return (uint32_t)(q ? units_of(l) / q : units_of(l)); };
-    for (uint32_t u = wave; u < V; u += nwaves) {
+    for (uint32_t u = u0 + wave; u < V; u += nwaves) {  // rows [u0, V)
         const uint64_t b = row_ptr[u], e = row_ptr[u + 1];
         const uint32_t nch = (uint32_t)((e - b + 63) / 64);
         ccnt[wv][lane] = 0;
@@ -2976,19 +2976,19 @@ srt_status level_csr(srt_plan *p, uint64_t wmax, bool with_loss, srt_err *err) {
         (void)hipMemsetAsync(p->d_tcursor, 0, sizeof(unsigned long long), M);
         (void)hipMemsetAsync(p->d_tmaxw, 0, sizeof(unsigned long long), M);
         if (single && with_loss)  // symmetric plans have identity rows (lvl_sym_tile_kernel)
-            hipLaunchKernelGGL((lvl_out_kernel<true, false, true>), dim3(blocks), dim3(256), 0, M, V, p->d_row_ptr,
+            hipLaunchKernelGGL((lvl_out_kernel<true, false, true>), dim3(blocks), dim3(256), 0, M, 0u, V, p->d_row_ptr,
                                p->d_col, p->d_lat, p->d_loss, p->kp.g, inv_g, wns, cls, q, vb, p->d_tcls, p->d_tccnt,
                                p->d_tpk, p->lvl_cap, p->d_tcursor, (unsigned long long *)p->d_tmaxw);
         else if (single)
-            hipLaunchKernelGGL((lvl_out_kernel<false, false, true>), dim3(blocks), dim3(256), 0, M, V, p->d_row_ptr,
+            hipLaunchKernelGGL((lvl_out_kernel<false, false, true>), dim3(blocks), dim3(256), 0, M, 0u, V, p->d_row_ptr,
                                p->d_col, p->d_lat, (const float *)nullptr, p->kp.g, inv_g, wns, cls, q, vb, p->d_tcls,
                                p->d_tccnt, p->d_tpk, p->lvl_cap, p->d_tcursor, (unsigned long long *)p->d_tmaxw);
         else if (with_loss)
-            hipLaunchKernelGGL(lvl_out_kernel<true>, dim3(blocks), dim3(256), 0, M, V, p->d_row_ptr, p->d_col,
+            hipLaunchKernelGGL(lvl_out_kernel<true>, dim3(blocks), dim3(256), 0, M, 0u, V, p->d_row_ptr, p->d_col,
                                p->d_lat, p->d_loss, p->kp.g, inv_g, wns, cls, q, vb, p->d_tcls, p->d_tccnt,
                                p->d_tpk, p->lvl_cap, p->d_tcursor, (unsigned long long *)p->d_tmaxw);
         else
-            hipLaunchKernelGGL(lvl_out_kernel<false>, dim3(blocks), dim3(256), 0, M, V, p->d_row_ptr, p->d_col,
+            hipLaunchKernelGGL(lvl_out_kernel<false>, dim3(blocks), dim3(256), 0, M, 0u, V, p->d_row_ptr, p->d_col,
                                p->d_lat, (const float *)nullptr, p->kp.g, inv_g, wns, cls, q, vb, p->d_tcls,
                                p->d_tccnt, p->d_tpk, p->lvl_cap, p->d_tcursor, (unsigned long long *)p->d_tmaxw);
     };
@@ -3070,6 +3070,116 @@ srt_status level_csr(srt_plan *p, uint64_t wmax, bool with_loss, srt_err *err) {
     p->t_q = 1;
     p->t_level = true;
     p->t_edges = p->lvl_cap;  // the probe's count (an upper bound at the run's smaller wmax)
+    return SRT_OK;
+}
+
+__global__ void set_u64_kernel(unsigned long long *p, unsigned long long v) { *p = v; }
+
+// The class CSR of a symmetric level plan (identity rows, mirrored pairs:
+// out-rows only) built sharded over W ranks: the fixed per-graph work of a
+// row-sharded build, which every rank paid whole before (C3: 0.63 ms of an
+// 8-rank share of ~1.4 ms).  Rank r builds the out-rows of vertices [r vr,
+// (r + 1) vr) into entry slot r (entries [r C, (r + 1) C), its cursor starting
+// at r C, so the class offsets it writes are absolute) and its offsets into
+// offset slot r; one all-gather of each (in place, C entries and vr * cls
+// offsets a rank -- C3, 8 ranks: ~5 MB + 128 KB a rank) and every rank holds
+// the whole class CSR.  C = the largest slice's entry count, measured once (a
+// counting pass per slice and an all-gather of the counts) at the first run.
+// comm == nullptr: the measurement form (srt_plan_shard_rows with
+// SRT_LVL_SHARD_EMU=1, one GPU): the first run builds every slice, later runs
+// rebuild the own slice only and wait out a modelled all-gather
+// (SRT_FW_EMU_AG_US + received bytes / SRT_FW_EMU_AG_GBPS, as the FW emulation).
+srt_status level_csr_sharded(srt_plan *p, uint64_t wmax, bool with_loss, uint32_t W, uint32_t r, srt_comm *comm,
+                             srt_err *err) {
+    hipStream_t M = p->stream;
+    const uint32_t V = p->V, vr = (V + W - 1) / W;
+    const uint32_t cls = wmax < 16 ? 16 : wmax < 32 ? 32 : 64;
+    const uint64_t vc1 = (uint64_t)V * cls + 1;
+    srt_status st;
+    uint64_t c1 = p->tcls_cap, c2 = p->tcls_cap, cap_cur = p->d_tcursor ? 1 : 0, cap_mw = p->d_tmaxw ? 1 : 0,
+             cap_cnt = p->d_lvl_counts ? W : 0;
+    if ((st = grow(&p->d_tcls, &c1, 2 * vc1, err, "hipMalloc(class offsets)")) != SRT_OK ||
+        (st = grow(&p->d_tccnt, &c2, 2 * vc1, err, "hipMalloc(class counts)")) != SRT_OK ||
+        (st = grow(&p->d_tcursor, &cap_cur, 1, err, "hipMalloc(level cursor)")) != SRT_OK ||
+        (st = grow(&p->d_tmaxw, &cap_mw, 1, err, "hipMalloc(level max)")) != SRT_OK ||
+        (st = grow(&p->d_lvl_offstage, &p->lvl_offstage_cap, (uint64_t)W * vr * cls, err,
+                   "hipMalloc(class offset slots)")) != SRT_OK ||
+        (st = grow(&p->d_lvl_counts, &cap_cnt, W, err, "hipMalloc(slice counts)")) != SRT_OK)
+        return st;
+    p->tcls_cap = std::min(c1, c2);
+    const double inv_g = 1.0 / (double)p->kp.g;
+    const uint64_t wns = wmax * p->kp.g;
+    auto slice = [&](uint32_t s, uint64_t base, uint64_t cap, uint64_t *entries) {
+        const uint32_t u0 = std::min(V, s * vr), u1 = std::min(V, (s + 1) * vr);
+        const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(8192, (u1 - u0 + 3) / 4));
+        hipLaunchKernelGGL(set_u64_kernel, dim3(1), dim3(1), 0, M, p->d_tcursor, (unsigned long long)base);
+        if (with_loss)
+            hipLaunchKernelGGL((lvl_out_kernel<true, false, true>), dim3(blocks), dim3(256), 0, M, u0, u1, p->d_row_ptr,
+                               p->d_col, p->d_lat, p->d_loss, p->kp.g, inv_g, wns, cls, 0u, 32u, p->d_lvl_offstage,
+                               p->d_tccnt, entries, cap, p->d_tcursor, (unsigned long long *)p->d_tmaxw);
+        else
+            hipLaunchKernelGGL((lvl_out_kernel<false, false, true>), dim3(blocks), dim3(256), 0, M, u0, u1,
+                               p->d_row_ptr, p->d_col, p->d_lat, (const float *)nullptr, p->kp.g, inv_g, wns, cls, 0u,
+                               32u, p->d_lvl_offstage, p->d_tccnt, entries, cap, p->d_tcursor,
+                               (unsigned long long *)p->d_tmaxw);
+    };
+    const bool emu = comm == nullptr;
+    if (!p->lvl_seg_cap) {
+        // sizing: every slice counted (cap 0: nothing written); the measured
+        // form counts all W here, a rank its own and all-gathers the counts
+        std::vector<unsigned long long> cnt(W, 0);
+        for (uint32_t s = 0; s < W; ++s) {
+            if (!emu && s != r) continue;
+            slice(s, 0, 0, p->d_tpk);
+            const hipError_t e = hipMemcpyAsync(p->d_lvl_counts + s, p->d_tcursor, 8, hipMemcpyDeviceToDevice, M);
+            if (e != hipSuccess) return fail(err, e, "slice count");
+        }
+        if (!emu && (st = comm_allgather_inplace(comm, p->d_lvl_counts, 8, M, err)) != SRT_OK) return st;
+        hipError_t e = hipMemcpyAsync(cnt.data(), p->d_lvl_counts, 8ull * W, hipMemcpyDeviceToHost, M);
+        if (e == hipSuccess) e = hipStreamSynchronize(M);
+        if (e != hipSuccess) return fail(err, e, "slice counts");
+        uint64_t C = 1;
+        for (uint32_t s = 0; s < W; ++s) C = std::max<uint64_t>(C, cnt[s]);
+        (void)hipFree(p->d_tpk);
+        (void)hipFree(p->d_tpk2);
+        p->d_tpk = p->d_tpk2 = nullptr;
+        uint64_t ca = 0;
+        if ((st = grow(&p->d_tpk, &ca, C * W + 1024, err, "hipMalloc(level out-rows)")) != SRT_OK) return st;
+        p->lvl_seg_cap = C;
+        p->lvl_cap = C * W;
+        p->lvl_emu_built = false;
+    }
+    const uint64_t C = p->lvl_seg_cap;
+    cspan_begin(p);
+    if (emu && !p->lvl_emu_built) {  // the measured form's first run: every rank's slice
+        for (uint32_t s = 0; s < W; ++s) slice(s, s * C, (s + 1) * C, p->d_tpk);
+        p->lvl_emu_built = true;
+    } else {
+        slice(r, (uint64_t)r * C, (uint64_t)(r + 1) * C, p->d_tpk);
+        if (emu) {
+            int khz = 100000;
+            (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, p->device);
+            const double lat_us = std::getenv("SRT_FW_EMU_AG_US") ? std::atof(std::getenv("SRT_FW_EMU_AG_US")) : 25.0;
+            const double gbps = std::getenv("SRT_FW_EMU_AG_GBPS") ? std::atof(std::getenv("SRT_FW_EMU_AG_GBPS")) : 300.0;
+            const double bytes = (double)C * 8 + (double)vr * cls * 4;
+            const double us = lat_us + bytes * (W - 1) / (gbps * 1e3);
+            hipLaunchKernelGGL(emu_wait_kernel, dim3(1), dim3(64), 0, M, (long long)(us * khz / 1000.0));
+        } else if ((st = comm_allgather_inplace(comm, p->d_tpk, C * 8, M, err)) != SRT_OK ||
+                   (st = comm_allgather_inplace(comm, p->d_lvl_offstage, (uint64_t)vr * cls * 4, M, err)) != SRT_OK) {
+            return st;
+        }
+    }
+    // the offsets, out-rows and (symmetric) in-rows alike
+    hipError_t e = hipMemcpyAsync(p->d_tcls, p->d_lvl_offstage, (uint64_t)V * cls * 4, hipMemcpyDeviceToDevice, M);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(p->d_tcls + vc1, p->d_lvl_offstage, (uint64_t)V * cls * 4, hipMemcpyDeviceToDevice, M);
+    cspan_end(p);
+    if (e != hipSuccess) return fail(err, e, "class offsets (sharded)");
+    p->lvl_single = true;
+    p->t_cls = cls;
+    p->t_q = 1;
+    p->t_level = true;
+    p->t_edges = C * W;
     return SRT_OK;
 }
 
@@ -3377,7 +3487,18 @@ srt_status level_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     p->shard_tail = false;
     p->tail_expanded = false;
     p->stage16 = false;
-    srt_status st = level_csr(p, p->kp.lmax, true, err);
+    // symmetric integer-level plans sharded over ranks build the class CSR
+    // sharded too (level_csr_sharded); the others build it whole
+    const bool sym_int = p->lvl_sym && !p->lvl_q && p->ident_rows;
+    srt_status st;
+    if (sym_int && p->comm && p->comm->nranks > 1)
+        st = level_csr_sharded(p, p->kp.lmax, true, (uint32_t)p->comm->nranks, (uint32_t)p->comm->rank, p->comm, err);
+    else if (sym_int && p->row_shard && p->lvl_emu_ranks > 1)
+        st = level_csr_sharded(p, p->kp.lmax, true, p->lvl_emu_ranks,
+                               (uint32_t)((uint64_t)p->row0 * p->lvl_emu_ranks / std::max<uint32_t>(p->n, 1)), nullptr,
+                               err);
+    else
+        st = level_csr(p, p->kp.lmax, true, err);
     if (st != SRT_OK) return st;
     hipLaunchKernelGGL(loss_stats_init_kernel, dim3(1), dim3(1), 0, p->stream, d_stats,
                        (unsigned long long *)p->d_tmaxw);

@@ -447,3 +447,53 @@ def test_level_symmetric_rows(monkeypatch, ns):
         _check(c.fetch(), O.Graph(True, np.arange(n), src, dst, lat2, loss), nodes)
     finally:
         c.close()
+
+
+def _complete_identity(n, seed):
+    """A complete undirected graph in identity rows (row u = columns 0 .. n-1,
+    as bench.py's C3 CSR): the symmetric level plans' shape (rows=sym)."""
+    edges = synth.complete_graph(n, seed, lat_ms=(1, 40))
+    row_ptr, col, lat, loss = synth.complete_csr(n, seed, edges=edges)
+    g = NetworkGraph(n, np.arange(n, dtype=np.uint32), row_ptr, col, lat, loss, directed=False)
+    return g, np.arange(n, dtype=np.uint32), O.Graph(False, np.arange(n), *edges)
+
+
+@pytest.mark.parametrize("world", [3, 8])
+def test_level_sharded_class_csr(world):
+    """Communicator-bound symmetric level plans build the class CSR sharded
+    (each rank its vertex slice into its own slot, the slots all-gathered) and
+    then their rows: rank 0's whole table is the oracle's, at 3 ranks (slices
+    of unequal fill) and 8."""
+    g, nodes, og = _complete_identity(1200, 70 + world)
+    t, descs, _ = sdist.local_build(g, nodes, [0] * world, algo=_lib.SRT_ALGO_LEVEL)
+    for d in descs:
+        assert d.startswith("level:u16 ") and " rows=sym" in d and f"ranks={world}" in d, d
+    _check(t, og, nodes)
+
+
+def test_level_rank_share_emulated(monkeypatch):
+    """bench.py --rank-share's measured form (SRT_LVL_SHARD_EMU=1): a
+    row-sharded plan's class CSR built as N slices (all at the first run, the
+    own slice after it); the rank's rows stay the oracle's over three runs."""
+    import torch
+
+    monkeypatch.setenv("SRT_LVL_SHARD_EMU", "1")
+    g, nodes, og = _complete_identity(1000, 91)
+    n = len(nodes)
+    elat, eloss = O.compute_shortest_paths(og, nodes)
+    dev = torch.device("cuda", 0)
+    for r in (0, 5):
+        p = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_LEVEL, device=0).shard_rows(8, r)
+        try:
+            assert " rows=sym" in p.describe(), p.describe()
+            for _ in range(3):
+                p.run()
+                la, pa, _ = p.table_ptrs()
+                L = torch.as_tensor(sdist._CudaBuf(la, n * n * 8), device=dev).view(torch.int64).view(n, n)
+                P = torch.as_tensor(sdist._CudaBuf(pa, n * n * 4), device=dev).view(torch.int32).view(n, n)
+                r0, r1 = n * r // 8, n * (r + 1) // 8
+                exp_l, exp_p = elat[r0:r1].copy(), _bits(eloss[r0:r1]).copy()
+                got_l, got_p = L[r0:r1].cpu().numpy().view(np.uint64), P[r0:r1].cpu().numpy().view(np.uint32)
+                assert np.array_equal(got_l, exp_l) and np.array_equal(got_p, exp_p)
+        finally:
+            p.close()
