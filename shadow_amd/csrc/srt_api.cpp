@@ -1737,6 +1737,13 @@ srt_status srt_plan_sync(srt_plan *p, srt_err *err) {
         unsigned long long v = 0;
         if (hipMemcpy(&v, p->d_lvisit, sizeof v, hipMemcpyDeviceToHost) == hipSuccess) p->lvl_visits = v;
     }
+    // in-process transport: what this rank received matched its senders'
+    // checksums (srt_comm.cpp local_collective)
+    if (p->comm && srt::local_corrupt(p->comm)) {
+        set_err(err, SRT_ERR_COMM,
+                "in-process collective: data received from a peer device differs from the sender's (checksum)");
+        return SRT_ERR_COMM;
+    }
     return SRT_OK;
 }
 
@@ -2356,6 +2363,35 @@ srt_status build_multi_level(srt_plan *p0, const std::vector<int32_t> &devs, srt
     }
     const srt::LevelCtx c0 = srt::level_ctx(p0);
     const uint64_t vc1 = (uint64_t)p0->V * p0->t_cls + 1, ents = p0->lvl_cap + 1024;
+    // the copies of the solve's inputs on the other devices are checked against
+    // rank 0's originals (srt::checksum; SRT_ERR_COMM on a mismatch).  Knobs
+    // (tests on one GPU): SRT_MULTI_FORCE_COPY=1 copies to ranks that share
+    // rank 0's device too; SRT_TEST_CORRUPT_PEER=r flips a byte of rank r's copy
+    const bool force_copy = std::getenv("SRT_MULTI_FORCE_COPY") && std::atoi(std::getenv("SRT_MULTI_FORCE_COPY")) == 1;
+    const int corrupt_rank = std::getenv("SRT_TEST_CORRUPT_PEER") ? std::atoi(std::getenv("SRT_TEST_CORRUPT_PEER")) : -1;
+    struct CopySrc {
+        const void *p;
+        uint64_t bytes;
+    };
+    const bool alias0 = c0.ce_in == c0.ce_out;
+    const CopySrc srcs[6] = {{c0.tcls, 2 * vc1 * 4}, {c0.ce_out, ents * 8}, {alias0 ? nullptr : c0.ce_in, ents * 8},
+                             {c0.nodes, (uint64_t)n * 4}, {c0.sl_lat, (uint64_t)n * 8}, {c0.sl_loss, (uint64_t)n * 4}};
+    unsigned long long h_ck0[6] = {};
+    bool any_copy = false;
+    for (int r = 1; r < N; ++r) any_copy |= devs[r] != devs[0] || force_copy;
+    if (any_copy && !emulate) {
+        unsigned long long *d_ck = nullptr;
+        hipError_t e = hipMalloc(&d_ck, sizeof h_ck0);
+        for (int k = 0; k < 6 && e == hipSuccess; ++k)
+            if (srcs[k].p) srt::checksum(srcs[k].p, srcs[k].bytes, d_ck + k, p0->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(h_ck0, d_ck, sizeof h_ck0, hipMemcpyDeviceToHost, p0->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(p0->stream);
+        (void)hipFree(d_ck);
+        if (e != hipSuccess) {
+            (void)hipEventDestroy(ready);
+            return hip_fail(err, e, "class CSR checksums");
+        }
+    }
     std::vector<srt_status> sts(N, SRT_OK);
     std::vector<srt_err> errs(N);
     std::vector<unsigned long long> mins(N, ~0ull), unre(N, 0);
@@ -2383,7 +2419,8 @@ srt_status build_multi_level(srt_plan *p0, const std::vector<int32_t> &devs, srt
         if (r == 0) st = p0->stream;
         c.stream = st;
         if (e == hipSuccess) e = hipStreamWaitEvent(st, ready, 0);
-        if (e == hipSuccess && devs[r] != devs[0]) {
+        bool corrupt = false;
+        if (e == hipSuccess && (devs[r] != devs[0] || (force_copy && r != 0))) {
             // the solve's inputs from rank 0's device
             uint32_t *tcls = (uint32_t *)dev_alloc(2 * vc1 * 4);
             const bool alias = c0.ce_in == c0.ce_out;  // symmetric plan: one entry array
@@ -2404,6 +2441,26 @@ srt_status build_multi_level(srt_plan *p0, const std::vector<int32_t> &devs, srt
             c.nodes = nd;
             c.sl_lat = sl;
             c.sl_loss = sp;
+            // every copy against rank 0's checksum before anything reads it
+            unsigned long long *d_ck = (unsigned long long *)dev_alloc(6 * 8);
+            if (!d_ck) e = hipErrorOutOfMemory;
+            if (e == hipSuccess && r == corrupt_rank) srt::corrupt_byte(eo, st);
+            const void *dsts[6] = {tcls, eo, alias ? nullptr : ei, nd, sl, sp};
+            unsigned long long h_ck[6] = {};
+            for (int k = 0; k < 6 && e == hipSuccess; ++k)
+                if (srcs[k].p) srt::checksum(dsts[k], srcs[k].bytes, d_ck + k, st);
+            if (e == hipSuccess) e = hipMemcpyAsync(h_ck, d_ck, sizeof h_ck, hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            for (int k = 0; k < 6 && e == hipSuccess; ++k) corrupt |= srcs[k].p && h_ck[k] != h_ck0[k];
+        }
+        if (corrupt) {
+            if (st && r != 0) (void)hipStreamSynchronize(st);
+            for (void *q : owned) (void)hipFree(q);
+            if (st && r != 0) (void)hipStreamDestroy(st);
+            set_err(e2, SRT_ERR_COMM, "multi-GPU level build: a device's copy of the class CSRs differs from rank 0's "
+                                      "(checksum)");
+            sts[r] = SRT_ERR_COMM;
+            return;
         }
         // staging: u16 (u32 when quantized) latency units + f32 loss, or --
         // quantized into a RoutingInfo -- its 8-byte records as they are

@@ -12,6 +12,7 @@
 
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -47,6 +48,14 @@ struct LocalGroup {
     int n = 0;
     std::vector<int> dev;
     std::vector<hipEvent_t> ready, done;
+    // integrity: every collective's contributions are checksummed by their
+    // senders (sums[r], on rank r's device) before `ready`, and every receiver
+    // checksums what it received (tmp[r][q]) and compares with the sender's
+    // word over xGMI; a mismatch sets bad[r] (on rank r's device), which
+    // srt_plan_sync / the in-process builds report as SRT_ERR_COMM
+    std::vector<unsigned long long *> sums, tmp;
+    std::vector<uint32_t *> bad;
+    int corrupt_rank = -1;  // test knob SRT_TEST_CORRUPT_PEER = rank: flips a received byte
     std::vector<const uint8_t *> ptr;
     std::mutex m;
     std::condition_variable cv;
@@ -80,6 +89,7 @@ namespace {
 srt_status local_collective(srt_comm *c, uint8_t *buf, uint64_t bytes, int root, hipStream_t s, srt_err *err) {
     LocalGroup *G = c->local;
     const int r = c->rank, N = G->n;
+    if (root < 0 || root == r) checksum(root < 0 ? buf + (uint64_t)r * bytes : buf, bytes, G->sums[r], s);
     hipError_t e = hipEventRecord(G->ready[r], s);
     if (e != hipSuccess) {
         G->abort();
@@ -99,6 +109,13 @@ srt_status local_collective(srt_comm *c, uint8_t *buf, uint64_t bytes, int root,
             if (q != r && (root < 0 || q == root)) (void)hipStreamWaitEvent(s, G->ready[q], 0);
         }
         peer_gather(buf, src, bytes, N, r, root, s);
+        for (int q = 0; q < N; ++q) {
+            if (q == r || (root >= 0 && q != root)) continue;
+            uint8_t *slot = root < 0 ? buf + (uint64_t)q * bytes : buf;
+            if (r == G->corrupt_rank && bytes) corrupt_byte(slot, s);
+            checksum(slot, bytes, G->tmp[r] + q, s);
+            checksum_cmp(G->tmp[r] + q, G->sums[q], G->bad[r], s);
+        }
     }
     e = hipEventRecord(G->done[r], s);
     if (e != hipSuccess) {
@@ -123,6 +140,17 @@ srt_status local_collective(srt_comm *c, uint8_t *buf, uint64_t bytes, int root,
     return SRT_OK;
 }
 }  // namespace
+
+bool local_corrupt(srt_comm *c) {
+    if (!c || !c->local) return false;
+    uint32_t b = 0;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(c->local->dev[c->rank]);
+    const bool bad = hipMemcpy(&b, c->local->bad[c->rank], 4, hipMemcpyDeviceToHost) != hipSuccess || b != 0;
+    (void)hipSetDevice(cur);
+    return bad;
+}
 
 srt_status comm_bcast(srt_comm *c, void *buf, size_t bytes, int root, hipStream_t s, srt_err *err) {
     if (c->local) return local_collective(c, (uint8_t *)buf, bytes, root, s, err);
@@ -273,7 +301,16 @@ srt_status srt_comm_init_local(int nranks, const int32_t *devices, srt_comm **co
         e = hipSetDevice(d);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&G->ready[r], hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&G->done[r], hipEventDisableTiming);
+        void *sm = nullptr, *tm = nullptr, *bd = nullptr;
+        if (e == hipSuccess) e = hipMalloc(&sm, 8);
+        if (e == hipSuccess) e = hipMalloc(&tm, 8ull * nranks);
+        if (e == hipSuccess) e = hipMalloc(&bd, 4);
+        if (e == hipSuccess) e = hipMemset(bd, 0, 4);
+        G->sums.push_back((unsigned long long *)sm);
+        G->tmp.push_back((unsigned long long *)tm);
+        G->bad.push_back((uint32_t *)bd);
     }
+    if (const char *k = std::getenv("SRT_TEST_CORRUPT_PEER")) G->corrupt_rank = std::atoi(k);
     // peer access between every pair of distinct devices (xGMI reads)
     for (int a = 0; a < nranks && e == hipSuccess; ++a)
         for (int b = 0; b < nranks && e == hipSuccess; ++b) {
@@ -296,6 +333,9 @@ srt_status srt_comm_init_local(int nranks, const int32_t *devices, srt_comm **co
             if (ev) (void)hipEventDestroy(ev);
         for (hipEvent_t ev : G->done)
             if (ev) (void)hipEventDestroy(ev);
+        for (auto *q : G->sums) (void)hipFree(q);
+        for (auto *q : G->tmp) (void)hipFree(q);
+        for (auto *q : G->bad) (void)hipFree(q);
         char m[200];
         std::snprintf(m, sizeof m, "srt_comm_init_local: %s", hipGetErrorString(e));
         set_err(err, SRT_ERR_HIP, m);
@@ -349,6 +389,9 @@ void srt_comm_destroy(srt_comm *comm) {
                 if (ev) (void)hipEventDestroy(ev);
             for (hipEvent_t ev : G->done)
                 if (ev) (void)hipEventDestroy(ev);
+            for (auto *q : G->sums) (void)hipFree(q);
+            for (auto *q : G->tmp) (void)hipFree(q);
+            for (auto *q : G->bad) (void)hipFree(q);
             delete G;
         }
     }

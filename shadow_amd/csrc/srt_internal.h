@@ -100,6 +100,16 @@ struct PeerSrcs {
 // broadcast (only = root): dst[0, bytes) <- src.p[root][0, bytes); on stream s
 // (srt_peer.hip)
 void peer_gather(uint8_t *dst, const PeerSrcs &src, uint64_t bytes, int nranks, int skip, int only, hipStream_t s);
+// the in-process transports' integrity check (srt_peer.hip): *out = a
+// position-weighted checksum of d[0, bytes) (out zeroed first); *bad |= 1 when
+// *a != *b (b may live on a peer device); corrupt_byte flips a bit of d[0]
+// (test knob SRT_TEST_CORRUPT_PEER)
+void checksum(const void *d, uint64_t bytes, unsigned long long *out, hipStream_t s);
+void checksum_cmp(const unsigned long long *a, const unsigned long long *b, uint32_t *bad, hipStream_t s);
+void corrupt_byte(void *d, hipStream_t s);
+// rank r of an in-process group: 1 when a collective it received did not match
+// its senders' checksums (read after the rank's stream is synchronised)
+bool local_corrupt(srt_comm *c);
 }  // namespace srt
 
 struct srt_comm {

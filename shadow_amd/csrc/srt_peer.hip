@@ -29,7 +29,48 @@ __global__ __launch_bounds__(256) void peer_gather_kernel(uint8_t *dst, PeerSrcs
     }
 }
 
+// Position-weighted checksum of a buffer: the sum over its u32 words w_i of
+// (w_i + 1) (2 i + 1) mod 2^64 (bytes, weighted by byte position, when the
+// buffer is not word-aligned).  One flipped bit changes it (the weights are
+// odd), and so does a word moved to another place.
+__global__ __launch_bounds__(256) void cksum_kernel(const uint8_t *__restrict__ p, uint64_t bytes, int words,
+                                                    unsigned long long *out) {
+    unsigned long long acc = 0;
+    const uint64_t n = words ? bytes / 4 : bytes;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t w = words ? reinterpret_cast<const uint32_t *>(p)[i] : p[i];
+        acc += (w + 1ull) * (2ull * i + 1ull);
+    }
+    if (words && blockIdx.x == 0 && threadIdx.x == 0)
+        for (uint64_t b = n * 4; b < bytes; ++b) acc += ((uint64_t)p[b] + 1ull) * (2ull * (n + b) + 1ull);
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+    if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
+}
+
+__global__ void cksum_cmp_kernel(const unsigned long long *a, const unsigned long long *b, uint32_t *bad) {
+    if (*a != *b) atomicOr(bad, 1u);
+}
+
+__global__ void flip_byte_kernel(uint8_t *p) { p[0] ^= 0x40u; }
+
 }  // namespace
+
+void checksum(const void *d, uint64_t bytes, unsigned long long *out, hipStream_t s) {
+    (void)hipMemsetAsync(out, 0, sizeof *out, s);
+    if (!bytes) return;
+    const int words = ((uintptr_t)d % 4) == 0;
+    const uint64_t n = words ? bytes / 4 : bytes;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(1024, std::max<uint64_t>(1, n / 2048));
+    hipLaunchKernelGGL(cksum_kernel, dim3(blocks), dim3(256), 0, s, (const uint8_t *)d, bytes, words, out);
+}
+
+void checksum_cmp(const unsigned long long *a, const unsigned long long *b, uint32_t *bad, hipStream_t s) {
+    hipLaunchKernelGGL(cksum_cmp_kernel, dim3(1), dim3(1), 0, s, a, b, bad);
+}
+
+void corrupt_byte(void *d, hipStream_t s) {
+    hipLaunchKernelGGL(flip_byte_kernel, dim3(1), dim3(1), 0, s, (uint8_t *)d);
+}
 
 // dst's slots <- src[q]'s slots (q != skip; only >= 0: that slot alone), on s
 void peer_gather(uint8_t *dst, const PeerSrcs &src, uint64_t bytes, int nranks, int skip, int only, hipStream_t s) {

@@ -95,3 +95,41 @@ def test_n_gpus_errors():
     with pytest.raises(_lib.SrtError) as e:
         g.compute_shortest_paths([0, 1], device=0, n_gpus=n_dev + 1)
     assert e.value.code == _lib.SRT_ERR_INVALID
+
+
+def test_level_peer_copies_checked(monkeypatch):
+    """The in-process level build copies the class CSRs to every other device
+    and checks each copy against rank 0's checksum before a row is solved
+    (SRT_MULTI_FORCE_COPY=1 makes ranks sharing the one GPU take that copy
+    path): a clean copy gives the oracle's table, a corrupted one
+    (SRT_TEST_CORRUPT_PEER=2) is refused with SRT_ERR_COMM."""
+    n = 700
+    src, dst, lat, loss = synth.complete_graph(n, 17, lat_ms=(1, 30))
+    g = NetworkGraph.from_edges(n, src, dst, lat, loss)
+    nodes = np.random.default_rng(17).permutation(n).astype(np.uint32)
+    og = O.Graph(False, np.arange(n), src, dst, lat, loss)
+    monkeypatch.setenv("SRT_MULTI_FORCE_COPY", "1")
+    t = g.compute_shortest_paths(nodes, n_gpus=3, same_device=True)
+    elat, eloss = O.compute_shortest_paths(og, nodes)
+    assert np.array_equal(t.latency_ns, elat)
+    assert np.array_equal(t.packet_loss.view(np.uint32), eloss.view(np.uint32))
+    monkeypatch.setenv("SRT_TEST_CORRUPT_PEER", "2")
+    with pytest.raises(_lib.SrtError) as e:
+        g.compute_shortest_paths(nodes, n_gpus=3, same_device=True)
+    assert e.value.code == _lib.SRT_ERR_COMM and "checksum" in str(e.value)
+
+
+@pytest.mark.parametrize("algo", [_lib.SRT_ALGO_FW, _lib.SRT_ALGO_LEVEL])
+def test_local_collective_corruption_detected(monkeypatch, algo):
+    """Every in-process collective is checked: senders checksum their slots,
+    receivers what arrived; a flipped byte on rank 1 (SRT_TEST_CORRUPT_PEER=1)
+    surfaces as SRT_ERR_COMM instead of a wrong table."""
+    n = 500
+    src, dst, lat, loss = synth.random_graph(n, 23, p_edge=0.08, directed=False, lat_range_ns=(1, 9))
+    lat = np.asarray(lat, np.uint64) * np.uint64(synth.MS)
+    g = NetworkGraph.from_edges(n, src, dst, lat, loss)
+    nodes = np.arange(n, dtype=np.uint32)
+    monkeypatch.setenv("SRT_TEST_CORRUPT_PEER", "1")
+    with pytest.raises(_lib.SrtError) as e:
+        sdist.local_build(g, nodes, [0, 0, 0], algo=algo)
+    assert e.value.code == _lib.SRT_ERR_COMM, str(e.value)
