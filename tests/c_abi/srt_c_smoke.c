@@ -136,6 +136,37 @@ int main(void) {
             srt_routing_info_destroy(ri);
         }
     }
+    /* the packet stage's host side from plain C (ABI 4): IpAssignment
+     * (mod.rs:352-420) and its resolver, the host RNG helpers */
+    {
+        srt_ip_assignment *ia = NULL;
+        CHECK(srt_ip_assignment_create(&ia) == SRT_OK && ia, "ip assignment");
+        const uint32_t a0 = srt_ip_assignment_assign(ia, 30), a1 = srt_ip_assignment_assign(ia, 10);
+        /* 11.0.0.1 and 11.0.0.2 in network byte order */
+        CHECK(a0 == 0x0100000Bu && a1 == 0x0200000Bu, "assign %08x %08x", a0, a1);
+        srt_err e;
+        CHECK(srt_ip_assignment_assign_ip(ia, 20, 0x0300000Bu, &e) == SRT_OK, "assign_ip");
+        CHECK(srt_ip_assignment_assign_ip(ia, 20, 0x0300000Bu, &e) == SRT_ERR_INVALID &&
+                  strcmp(e.msg, "IP address has already been assigned") == 0,
+              "assign_ip twice: %s", e.msg);
+        uint32_t node = 0;
+        CHECK(srt_ip_assignment_get_node(ia, a1, &node) == 1 && node == 10, "get_node");
+        const uint32_t row_ids[3] = {30, 10, 20};
+        srt_ip_resolver *res = NULL;
+        CHECK(srt_ip_resolver_create(ia, row_ids, 3, &res, &e) == SRT_OK, "resolver");
+        const uint32_t q[4] = {a0, a1, 0x0300000Bu, 0x0400000Bu};
+        int32_t rows[4];
+        CHECK(srt_ip_resolve_rows(res, q, 4, rows) == SRT_OK && rows[0] == 0 && rows[1] == 1 && rows[2] == 2 &&
+                  rows[3] == -1,
+              "resolve rows %d %d %d %d", rows[0], rows[1], rows[2], rows[3]);
+        srt_ip_resolver_destroy(res);
+        srt_ip_assignment_destroy(ia);
+        uint64_t st4[4] = {1, 2, 3, 4}, d[2];
+        srt_xoshiro_next_u64(st4, 2, d);
+        CHECK(d[0] == 41943041ull && d[1] == 58720359ull, "xoshiro256++ vector");
+        srt_xoshiro_seed_from_u64(0, st4);
+        CHECK(st4[0] == 0xe220a8397b1dcdafull, "SplitMix64(0)");
+    }
     if (fails) {
         fprintf(stderr, "%d check(s) failed\n", fails);
         return 1;
