@@ -2444,7 +2444,7 @@ srt_status build_multi_level(srt_plan *p0, const std::vector<int32_t> &devs, srt
             // every copy against rank 0's checksum before anything reads it
             unsigned long long *d_ck = (unsigned long long *)dev_alloc(6 * 8);
             if (!d_ck) e = hipErrorOutOfMemory;
-            if (e == hipSuccess && r == corrupt_rank) srt::corrupt_byte(eo, st);
+            if (e == hipSuccess && r == corrupt_rank) srt::corrupt_byte(sp, (uint64_t)n * 4, st);  // a loss value
             const void *dsts[6] = {tcls, eo, alias ? nullptr : ei, nd, sl, sp};
             unsigned long long h_ck[6] = {};
             for (int k = 0; k < 6 && e == hipSuccess; ++k)

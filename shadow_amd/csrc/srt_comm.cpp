@@ -112,7 +112,7 @@ srt_status local_collective(srt_comm *c, uint8_t *buf, uint64_t bytes, int root,
         for (int q = 0; q < N; ++q) {
             if (q == r || (root >= 0 && q != root)) continue;
             uint8_t *slot = root < 0 ? buf + (uint64_t)q * bytes : buf;
-            if (r == G->corrupt_rank && bytes) corrupt_byte(slot, s);
+            if (r == G->corrupt_rank) corrupt_byte(slot, bytes, s);
             checksum(slot, bytes, G->tmp[r] + q, s);
             checksum_cmp(G->tmp[r] + q, G->sums[q], G->bad[r], s);
         }

@@ -102,11 +102,12 @@ struct PeerSrcs {
 void peer_gather(uint8_t *dst, const PeerSrcs &src, uint64_t bytes, int nranks, int skip, int only, hipStream_t s);
 // the in-process transports' integrity check (srt_peer.hip): *out = a
 // position-weighted checksum of d[0, bytes) (out zeroed first); *bad |= 1 when
-// *a != *b (b may live on a peer device); corrupt_byte flips a bit of d[0]
-// (test knob SRT_TEST_CORRUPT_PEER)
+// *a != *b (b may live on a peer device); corrupt_byte flips a bit of the last
+// byte of d[0, bytes) -- a value bit of the payloads' last record, never an
+// index (test knob SRT_TEST_CORRUPT_PEER)
 void checksum(const void *d, uint64_t bytes, unsigned long long *out, hipStream_t s);
 void checksum_cmp(const unsigned long long *a, const unsigned long long *b, uint32_t *bad, hipStream_t s);
-void corrupt_byte(void *d, hipStream_t s);
+void corrupt_byte(void *d, uint64_t bytes, hipStream_t s);
 // rank r of an in-process group: 1 when a collective it received did not match
 // its senders' checksums (read after the rank's stream is synchronised)
 bool local_corrupt(srt_comm *c);

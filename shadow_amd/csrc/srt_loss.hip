@@ -573,10 +573,11 @@ __global__ void loss_scatter_kernel(const uint32_t *__restrict__ idx, const floa
 // Per-row counts of a tight-edge list (v = ~0: padding): rows by target v
 // (pull CSR) or, BY_SRC, by source u (push CSR)
 template <bool BY_SRC>
-__global__ void tight_list_count_kernel(const uint4 *__restrict__ list, uint64_t slots, uint32_t *__restrict__ cnt) {
+__global__ void tight_list_count_kernel(const uint4 *__restrict__ list, uint64_t slots, uint32_t *__restrict__ cnt,
+                                        uint32_t nv) {
     for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < slots; e += (uint64_t)gridDim.x * blockDim.x) {
         const uint4 r = list[e];
-        if (r.x != ~0u) atomicAdd(&cnt[BY_SRC ? r.y : r.x], 1u);
+        if (r.x != ~0u && r.x < nv && r.y < nv) atomicAdd(&cnt[BY_SRC ? r.y : r.x], 1u);
     }
 }
 
@@ -585,10 +586,10 @@ __global__ void tight_list_count_kernel(const uint4 *__restrict__ list, uint64_t
 template <bool BY_SRC>
 __global__ void tight_list_fill_kernel(const uint4 *__restrict__ list, uint64_t slots,
                                        const uint64_t *__restrict__ ptr, uint32_t *__restrict__ cur,
-                                       uint64_t *__restrict__ tpk, uint32_t ubits) {
+                                       uint64_t *__restrict__ tpk, uint32_t ubits, uint32_t nv) {
     for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < slots; e += (uint64_t)gridDim.x * blockDim.x) {
         const uint4 r = list[e];
-        if (r.x == ~0u) continue;
+        if (r.x == ~0u || r.x >= nv || r.y >= nv) continue;  // padding (or a record the transport damaged)
         const uint32_t row = BY_SRC ? r.y : r.x, other = BY_SRC ? r.x : r.y;
         const uint64_t pos = ptr[row] + atomicAdd(&cur[row], 1u);
         tpk[pos] = ((uint64_t)r.w << 32) | ((r.z << ubits) | other);
@@ -1111,10 +1112,12 @@ __device__ __forceinline__ uint32_t wclass(uint32_t w, uint32_t q) { return q ==
 
 __global__ void tcls_count_kernel(const uint4 *__restrict__ list, uint64_t slots, uint32_t *__restrict__ cnt,
                                   uint64_t vc1, uint32_t q, uint32_t cls) {
+    const uint64_t nv = (vc1 - 1) / cls;
     for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < slots; e += (uint64_t)gridDim.x * blockDim.x) {
         const uint4 r = list[e];
         if (r.x == ~0u) continue;
         const uint32_t c = wclass(r.z, q);
+        if (r.x >= nv || r.y >= nv || c == 0 || c >= cls) continue;  // a record the transport damaged
         atomicAdd(&cnt[(uint64_t)r.y * cls + c - 1], 1u);        // out-row of u
         atomicAdd(&cnt[vc1 + (uint64_t)r.x * cls + c - 1], 1u);  // in-row of v
     }
@@ -1124,10 +1127,12 @@ __global__ void tcls_fill_kernel(const uint4 *__restrict__ list, uint64_t slots,
                                  uint32_t *__restrict__ cur, uint64_t *__restrict__ ce_out,
                                  uint64_t *__restrict__ ce_in, uint64_t vc1, uint32_t q, uint32_t *__restrict__ cw,
                                  uint64_t cw_in, uint32_t cls) {
+    const uint64_t nv = (vc1 - 1) / cls;
     for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < slots; e += (uint64_t)gridDim.x * blockDim.x) {
         const uint4 r = list[e];
         if (r.x == ~0u) continue;
         const uint32_t c = wclass(r.z, q);
+        if (r.x >= nv || r.y >= nv || c == 0 || c >= cls) continue;
         const uint64_t a = (uint64_t)r.y * cls + c - 1, b = vc1 + (uint64_t)r.x * cls + c - 1;
         const uint64_t ia = off[a] + atomicAdd(&cur[a], 1u), ib = off[b] + atomicAdd(&cur[b], 1u);
         ce_out[ia] = ((uint64_t)r.w << 32) | r.x;
@@ -2469,10 +2474,10 @@ srt_status build_tight_rows(srt_plan *p, uint64_t slots, uint32_t ubits, uint64_
     (void)hipMemsetAsync(p->d_tcnt, 0, (size_t)V * 4, M);
     // push form: CSR over tight OUT-edges (the pull form over in-edges
     // measured slower and was removed)
-    hipLaunchKernelGGL(tight_list_count_kernel<true>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tcnt);
+    hipLaunchKernelGGL(tight_list_count_kernel<true>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tcnt, V);
     hipLaunchKernelGGL(tight_scan_kernel, dim3(1), dim3(1024), 0, M, p->d_tcnt, p->d_tptr, V);
     hipLaunchKernelGGL(tight_list_fill_kernel<true>, dim3(lblocks), dim3(256), 0, M, p->d_tlist, slots, p->d_tptr,
-                       p->d_tcnt, p->d_tpk2, ubits);
+                       p->d_tcnt, p->d_tpk2, ubits, V);
     p->t_push = true;
     return sort_packed(p, ubits, maxw, err);
 }

@@ -51,7 +51,7 @@ __global__ void cksum_cmp_kernel(const unsigned long long *a, const unsigned lon
     if (*a != *b) atomicOr(bad, 1u);
 }
 
-__global__ void flip_byte_kernel(uint8_t *p) { p[0] ^= 0x40u; }
+__global__ void flip_byte_kernel(uint8_t *p) { p[0] ^= 0x40u; }  // a value bit of the slot's last word
 
 }  // namespace
 
@@ -68,8 +68,8 @@ void checksum_cmp(const unsigned long long *a, const unsigned long long *b, uint
     hipLaunchKernelGGL(cksum_cmp_kernel, dim3(1), dim3(1), 0, s, a, b, bad);
 }
 
-void corrupt_byte(void *d, hipStream_t s) {
-    hipLaunchKernelGGL(flip_byte_kernel, dim3(1), dim3(1), 0, s, (uint8_t *)d);
+void corrupt_byte(void *d, uint64_t bytes, hipStream_t s) {
+    if (bytes) hipLaunchKernelGGL(flip_byte_kernel, dim3(1), dim3(1), 0, s, (uint8_t *)d + bytes - 1);
 }
 
 // dst's slots <- src[q]'s slots (q != skip; only >= 0: that slot alone), on s

@@ -5,6 +5,7 @@ cd $GRAFT_REPO_ROOT
 O=gpurun_out/s7
 mkdir -p $O
 export TMPDIR=/tmp
+timeout -k 10 200 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_local.py -m gpu -k "corruption or peer_copies" > $O/t0.log 2>&1 || { echo "corruption tests failed"; tail -30 $O/t0.log; exit 1; }
 timeout -k 10 1100 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread tests -m gpu > $O/tests.log 2>&1 || { echo "tests failed"; grep -E "FAILED|Error" $O/tests.log | head -20; tail -30 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 for N in 2 4 8; do
