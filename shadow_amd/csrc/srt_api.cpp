@@ -1175,6 +1175,13 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     } else {
         p->lvl_q = 0;
         p->lvl_sym = p->lvl_sym_lat = false;
+        // the level probe's class CSRs (sized for it): freed before the
+        // closure families size anything by the free HBM; their own runs grow
+        // these arrays again from zero
+        for (void *q : {(void *)p->d_tpk, (void *)p->d_tpk2, (void *)p->d_tcls, (void *)p->d_tccnt}) (void)hipFree(q);
+        p->d_tpk = p->d_tpk2 = nullptr;
+        p->d_tcls = p->d_tccnt = nullptr;
+        p->t_cap = p->tcls_cap = p->lvl_cap = 0;
     }
     // SSSP plans read their in-edges (with loss) from the host-built list, never
     // d_loss: drop the deferred upload so run_tail does not copy it
@@ -1266,19 +1273,6 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         std::vector<uint64_t> in_ptr;
         std::vector<srt::InEdge> in_edge;
         build_in_edges(g, p->sssp_g, n_in, &in_ptr, &in_edge);
-        // source order of the sweep's words (knob SRT_SSSP_ORDER=0: table order)
-        {
-            const char *ko = std::getenv("SRT_SSSP_ORDER");
-            const int om = ko ? std::atoi(ko) : 1;
-            // 1: launches in breadth-first order, rows within a launch in
-            // shortest-latency-tree level order (frontier sweeps); 2: breadth-first
-            // only; 3: tree level order only (A/B)
-            if (om == 1 || om == 2) p->h_bfs_rank = hop_rank(g);
-            if (om == 3) p->h_bfs_rank = spt_rank(g);
-            if (om == 1) p->h_spt_rank = spt_rank(g);
-        }
-        PLAN_TRY(dmalloc(&p->d_in_ptr, in_ptr.size(), err));
-        PLAN_TRY(dmalloc(&p->d_in_edge, in_edge.size(), err));
         // latency-first frontier sweeps (srt_frontier.hip) when every finite
         // distance fits u16 units: the proved bound (eccentricity, or (V-1) *
         // max edge) below 0xFFFF.  Knob SRT_SSSP_KEY=64 keeps the packed-key
@@ -1289,6 +1283,19 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
                                                             : (unsigned __int128)(p->V ? p->V - 1 : 0) * maxu;
             const char *kk = std::getenv("SRT_SSSP_KEY");
             p->sssp_frontier = lb < 0xffff && !(kk && std::atoi(kk) == 64);
+        }
+        PLAN_TRY(dmalloc(&p->d_in_ptr, in_ptr.size(), err));
+        PLAN_TRY(dmalloc(&p->d_in_edge, in_edge.size(), err));
+        // source order of the sweep's words (knob SRT_SSSP_ORDER=0: table order)
+        {
+            const char *ko = std::getenv("SRT_SSSP_ORDER");
+            const int om = ko ? std::atoi(ko) : 1;
+            // 1: launches in breadth-first order, rows within a launch in
+            // shortest-latency-tree level order (frontier sweeps); 2: breadth-first
+            // only; 3: tree level order only (A/B)
+            if (om == 1 || om == 2) p->h_bfs_rank = hop_rank(g);
+            if (om == 3) p->h_bfs_rank = spt_rank(g);
+            if (om == 1 && p->sssp_frontier) p->h_spt_rank = spt_rank(g);  // read by frontier sweeps only
         }
         if (!p->sssp_frontier) {
             PLAN_TRY(dmalloc(&p->d_sD, (size_t)p->sssp_nb * p->V * 64, err));
@@ -2593,14 +2600,15 @@ srt_status build_multi(const srt_csr *g, const uint32_t *nodes, uint32_t n, srt_
     }
     std::vector<int32_t> devs(N);
     for (int r = 0; r < N; ++r) devs[r] = same ? first : first + r;
+    srt_plan *p0 = nullptr;
     {
         // rank 0's plan: the one CSR scan + upload and the family choice; a
-        // level plan needs no other plan (build_multi_level)
+        // level plan needs no other plan (build_multi_level), a closure plan
+        // is rank 0's plan of the sharded run below
         srt_opts o0 = *opts;
         o0.device = devs[0];
         o0.n_gpus = 1;
         o0.flags &= ~(uint32_t)SRT_OPT_SAME_DEVICE;
-        srt_plan *p0 = nullptr;
         if (srt_status s = plan_create_impl(g, nodes, n, &o0, &p0, err, true); s != SRT_OK) return s;
         if (p0->algo == SRT_ALGO_LEVEL) {
             srt_status s = build_multi_level(p0, devs, out, ct, min_latency_ns, err);
@@ -2617,11 +2625,15 @@ srt_status build_multi(const srt_csr *g, const uint32_t *nodes, uint32_t n, srt_
             reap_async(p0);
             return s;
         }
-        srt_plan_destroy(p0);
     }
     std::vector<srt_comm *> comms(N, nullptr);
-    if (srt_status s = srt_comm_init_local(N, devs.data(), comms.data(), err); s != SRT_OK) return s;
+    if (srt_status s = srt_comm_init_local(N, devs.data(), comms.data(), err); s != SRT_OK) {
+        join_loss_check(p0);
+        srt_plan_destroy(p0);
+        return s;
+    }
     std::vector<srt_plan *> plans(N, nullptr);
+    plans[0] = p0;  // its losses upload in its run (run_tail), g stays valid until then
     std::vector<srt_status> sts(N, SRT_OK);
     std::vector<srt_err> errs(N);
     std::vector<std::thread> th;
@@ -2632,7 +2644,7 @@ srt_status build_multi(const srt_csr *g, const uint32_t *nodes, uint32_t n, srt_
             o.n_gpus = 1;
             o.flags &= ~(uint32_t)SRT_OPT_SAME_DEVICE;
             std::memset(&errs[r], 0, sizeof errs[r]);
-            srt_status s = plan_create_impl(g, nodes, n, &o, &plans[r], &errs[r], false);
+            srt_status s = r == 0 ? SRT_OK : plan_create_impl(g, nodes, n, &o, &plans[r], &errs[r], false);
             if (s == SRT_OK) s = srt_plan_bind_comm(plans[r], comms[r], &errs[r]);
             if (s == SRT_OK) s = srt_plan_run(plans[r], &errs[r]);
             if (s != SRT_OK) srt_comm_abort(comms[r]);  // releases the others' collectives
@@ -2667,6 +2679,18 @@ srt_status build_multi(const srt_csr *g, const uint32_t *nodes, uint32_t n, srt_
     if (s == SRT_OK && ct) {
         ct->diag.resize(n);
         for (uint32_t i = 0; i < n; ++i) ct->diag[i] = out[(uint64_t)i * n + i];
+    }
+    // rank 0's device loss range check (its deferred upload): a parse-time
+    // error, so it wins over any error of the build itself
+    join_loss_check(p0);
+    if (p0->h_lossbad && s != SRT_ERR_HIP) {
+        (void)hipSetDevice(p0->device);
+        (void)hipStreamSynchronize(p0->stream);
+        (void)hipStreamSynchronize(p0->comm_stream);
+        if (*p0->h_lossbad != ~0ull) {
+            s = SRT_ERR_INVALID;
+            set_err(err, SRT_ERR_INVALID, "Edge 'packet_loss' is not in the range [0,1]");
+        }
     }
     for (int r = 0; r < N; ++r) srt_plan_destroy(plans[r]);
     for (int r = 0; r < N; ++r) srt_comm_destroy(comms[r]);

@@ -1,0 +1,17 @@
+#!/bin/bash
+# round-6 session 9: packed 4-byte class entries -- parity, then C3 A/B (8-byte, packed UNR 4, packed UNR 2), rank share 8
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r6pk
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 600 python3 -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_level.py tests/test_gpu_local.py tests/test_gpu_configs.py -m gpu > $O/t0.log 2>&1 || { echo "tests failed"; grep -E "FAILED|Error" $O/t0.log | head -20; tail -30 $O/t0.log; exit 1; }
+tail -2 $O/t0.log
+for V in pk4 ce8 pk2; do
+  case $V in ce8) export SRT_LVL_CE4=0;; pk2) unset SRT_LVL_CE4; export SRT_LVL_CE4_UNR=2;; *) ;; esac
+  timeout -k 10 300 python3 -u bench.py --steps 10 --warmup 3 --no-cold --no-cpu-baseline --no-e2e > $O/c3_$V.json 2> $O/c3_$V.err || { echo "bench $V failed"; tail -20 $O/c3_$V.err; exit 1; }
+  python3 -c "import json; d=json.loads(open('$O/c3_$V.json').read().strip().splitlines()[-1]); print('$V', d['ms_per_step'], d['config']['phases_last_build'])"
+done
+unset SRT_LVL_CE4_UNR
+timeout -k 10 300 python3 -u bench.py --rank-share 8 --steps 20 --warmup 3 > $O/rank_share_8.json 2> $O/rank_share_8.err || { echo "rank share failed"; tail -20 $O/rank_share_8.err; exit 1; }
+tail -1 $O/rank_share_8.json | cut -c1-400
