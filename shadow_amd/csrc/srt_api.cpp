@@ -1556,6 +1556,7 @@ bool upload_level_losses(srt_plan *p, srt_err *err, srt_status *st) {
     const uint64_t cap = p->lvl_cap;  // the probe's count: >= the run's (its bound is >= B)
     if (!lk.owns_lock() || g_pinned.bytes < 64) return false;
     hipStream_t M = p->stream;
+    Trace tr;
     auto fail = [&](hipError_t e, const char *what) {
         *st = hip_fail(err, e, what);
         return true;
@@ -1577,44 +1578,61 @@ bool upload_level_losses(srt_plan *p, srt_err *err, srt_status *st) {
     if (e == hipSuccess) e = hipStreamSynchronize(M);
     if (e != hipSuccess) return fail(e, "loss indices (count)");
     const uint64_t cnt = h[0];
+    tr.mark("losses: needed entries listed");
     // (cnt > cap cannot happen: the probe's bound is >= the run's)
     if (cnt > cap || g_pinned.bytes < cnt * 8) return false;  // the full upload
-    // the range check of every loss, behind the build (8 host threads)
+    // the range check of every loss, behind the build (8 host threads),
+    // started once the needed losses are gathered (knob SRT_LOSSCHK_EARLY=1:
+    // before the gather, A/B) -- it streams the whole loss array, and the
+    // gather's cache misses wait behind it
     const float *src = p->h_loss_defer;
     const uint64_t m = p->n_adj;
     unsigned long long *hb = p->h_lossbad;
     *hb = ~0ull;
-    p->loss_checker = std::thread([src, m, hb] {
-        const int T = std::max(1, std::min(8, host_threads(m)));
-        std::vector<uint64_t> first(T, ~0ull);
-        std::vector<std::thread> pool;
-        const uint32_t *q = reinterpret_cast<const uint32_t *>(src);
-        for (int t = 0; t < T; ++t)
-            pool.emplace_back([&, t] {
-                for (uint64_t k = m * t / T; k < m * (t + 1) / T; ++k)
-                    if (srt::loss_bits_bad(q[k])) {
-                        first[t] = k;
-                        break;
-                    }
-            });
-        for (auto &th : pool) th.join();
-        *hb = *std::min_element(first.begin(), first.end());
-    });
+    auto start_checker = [&]() {
+        p->loss_checker = std::thread([src, m, hb] {
+            const int T = std::max(1, std::min(8, host_threads(m)));
+            std::vector<uint64_t> first(T, ~0ull);
+            std::vector<std::thread> pool;
+            const uint32_t *q = reinterpret_cast<const uint32_t *>(src);
+            for (int t = 0; t < T; ++t)
+                pool.emplace_back([&, t] {
+                    for (uint64_t k = m * t / T; k < m * (t + 1) / T; ++k)
+                        if (srt::loss_bits_bad(q[k])) {
+                            first[t] = k;
+                            break;
+                        }
+                });
+            for (auto &th : pool) th.join();
+            *hb = *std::min_element(first.begin(), first.end());
+        });
+    };
+    const bool early = std::getenv("SRT_LOSSCHK_EARLY") && std::atoi(std::getenv("SRT_LOSSCHK_EARLY")) == 1;
+    if (early) start_checker();
     uint32_t *hidx = reinterpret_cast<uint32_t *>(g_pinned.buf);
     float *hval = reinterpret_cast<float *>(hidx + cnt);
     e = hipMemcpyAsync(hidx, d_idx, cnt * 4, hipMemcpyDeviceToHost, M);
     if (e == hipSuccess) e = hipStreamSynchronize(M);
     if (e != hipSuccess) return fail(e, "loss indices");
+    tr.mark("losses: indices on the host");
     {
         const int T = host_threads(cnt * 16);
         std::vector<std::thread> pool;
+        // one cache miss a loss (~330 scattered columns a row): 32 gathers
+        // ahead in flight by prefetch
         auto part = [&](int t) {
-            for (uint64_t i = cnt * t / T; i < cnt * (t + 1) / T; ++i) hval[i] = src[hidx[i]];
+            const uint64_t a = cnt * t / T, b = cnt * (t + 1) / T;
+            for (uint64_t i = a; i < b; ++i) {
+                if (i + 32 < b) __builtin_prefetch(src + hidx[i + 32], 0, 0);
+                hval[i] = src[hidx[i]];
+            }
         };
         for (int t = 1; t < T; ++t) pool.emplace_back(part, t);
         part(0);
         for (auto &th : pool) th.join();
     }
+    tr.mark("losses: gathered");
+    if (!early) start_checker();
     e = hipMemcpyAsync(d_val, hval, cnt * 4, hipMemcpyHostToDevice, M);
     if (e != hipSuccess) return fail(e, "upload (needed losses)");
     srt::loss_scatter(d_idx, d_val, cnt, p->d_loss, M);
@@ -1631,6 +1649,7 @@ bool upload_level_losses(srt_plan *p, srt_err *err, srt_status *st) {
     if (e == hipSuccess) e = hipStreamSynchronize(M);
     if (e != hipSuccess) return fail(e, "upload (needed losses)");
     if (p->lvl_sym && reinterpret_cast<uint32_t *>(h)[0] == 0) p->lvl_sym = false;
+    tr.mark("losses: uploaded, scattered, mirror-checked");
     p->h_loss_defer = nullptr;
     return true;
 }
