@@ -1563,7 +1563,9 @@ constexpr uint32_t LWC = 63;        // the level solve's classes / levels at mos
 // probe != nullptr: no table; probe[2 + k] = the largest level over the
 // in-use columns of row k (0xffff if one is unreached by level lcap), the u64
 // at probe[0] += the edges walked.
-template <int LPT, int UNR, uint32_t CLSN, int VW, bool NT>
+// SP (VW = 2): the class lists walked as one stream of chunks a lane group,
+// software-pipelined (see the walk below).
+template <int LPT, int UNR, uint32_t CLSN, int VW, bool NT, bool SP = false>
 __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
     uint32_t V, const uint32_t *__restrict__ nodes, uint32_t n, uint32_t row0, uint32_t row1,
     const uint32_t *__restrict__ cls_out, const uint32_t *__restrict__ cls_in, const uint64_t *__restrict__ ce_out,
@@ -1675,8 +1677,10 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
                 __syncthreads();
             }
             LVL_TICK(0)
+            // item t: its class w (searched up from the w passed in -- a lane
+            // group's items come in increasing t, so from its last item's:
+            // one LDS read, not up to WCN dependent ones), vertex and list
             auto item = [&](uint32_t t, uint32_t &w, uint32_t &x, uint32_t &e0, uint32_t &e1) {
-                w = 1;
                 while (t >= plan_end[w]) ++w;
                 const uint32_t m = t - (w > 1 ? plan_end[w - 1] : 0u), j = l - w;
                 const bool push = (pm >> w) & 1ull;
@@ -1685,70 +1689,170 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
                 e0 = cl[(uint64_t)x * CLSN + w - 1];
                 e1 = cl[(uint64_t)x * CLSN + w];
             };
-            uint32_t nw_ = 1, nx = 0, ne0 = 0, ne1 = 0;
-            if (grp < T) item(grp, nw_, nx, ne0, ne1);
-            for (uint32_t t = grp; t < T; t += ngrp) {
-                const uint32_t w = nw_, x = nx, e0 = ne0, e1 = ne1, j = l - w;
-                if (t + ngrp < T) item(t + ngrp, nw_, nx, ne0, ne1);
-                const bool push = (pm >> w) & 1ull;
-                const uint64_t *ce = push ? ce_out : ce_in;
-                // push: x in N_j, its class-w out-edges x -> v, v unsettled or at l;
-                // pull: x unsettled, its class-w in-edges u -> x, u in N_j
-                const float onem = push ? 1.0f - __uint_as_float(prow[x]) : 0.0f;
-                constexpr int NE = UNR * VW;
-                for (uint32_t b = VW == 2 ? e0 & ~1u : e0; b < e1; b += UNR * LPT * VW) {
-                    uint64_t wd[NE];
-                    uint32_t ei[NE];
+            if constexpr (SP) {
+                // The level's items as one stream of chunks a lane group (CH
+                // entries of one item's class list, UNR pairs a lane): the next
+                // chunk's entry loads go out before this chunk's level probes
+                // and folds, so their latency hides behind the LDS work, and an
+                // item's offsets are read one item ahead.  Push and pull chunks
+                // run apart (push is uniform in an item and, but at a class
+                // boundary, in a wave), without a per-entry direction test.
+                static_assert(VW == 2, "the pipelined walk loads entry pairs");
+                constexpr uint32_t CH = UNR * LPT * 2;
+                constexpr int NE = UNR * 2;
+                auto load = [&](uint4 *d, uint32_t w, uint32_t b) {
+                    const uint64_t *ce = ((pm >> w) & 1ull) ? ce_out : ce_in;
 #pragma unroll
-                    for (int q = 0; q < UNR; ++q) {
-                        const uint32_t at = b + (sub + q * LPT) * VW;  // padded past the end
-                        if (VW == 2) {
-                            const uint4 r2 = *reinterpret_cast<const uint4 *>(ce + at);
-                            wd[2 * q] = ((uint64_t)r2.y << 32) | r2.x;
-                            wd[2 * q + 1] = ((uint64_t)r2.w << 32) | r2.z;
-                            ei[2 * q] = at;
-                            ei[2 * q + 1] = at + 1;
+                    for (int q = 0; q < UNR; ++q) d[q] = *reinterpret_cast<const uint4 *>(ce + b + (sub + q * LPT) * 2);
+                };
+                uint32_t ct = grp, cw = 1, cx = 0, ce0 = 0, ce1 = 0;  // the chunk's item
+                uint32_t pw = 1, px = 0, pe0 = 0, pe1 = 0;            // the group's next item
+                if (ct < T) item(ct, cw, cx, ce0, ce1);
+                pw = cw;
+                if (ct + ngrp < T) item(ct + ngrp, pw, px, pe0, pe1);
+                uint32_t cb = ce0 & ~1u;
+                uint4 cur[UNR];
+                if (ct < T) load(cur, cw, cb);
+                while (ct < T) {
+                    // the next chunk: this item's next one, or the next item's first
+                    uint32_t nt2 = ct, nw2 = cw, nx2 = cx, ne02 = ce0, ne12 = ce1, nb = cb + CH;
+                    const bool adv = nb >= ce1;
+                    if (adv) {
+                        nt2 = ct + ngrp;
+                        nw2 = pw;
+                        nx2 = px;
+                        ne02 = pe0;
+                        ne12 = pe1;
+                        nb = pe0 & ~1u;
+                    }
+                    uint4 nxt[UNR];
+                    if (nt2 < T) load(nxt, nw2, nb);
+                    if (adv && nt2 + ngrp < T) item(nt2 + ngrp, pw, px, pe0, pe1);
+                    if (cb < ce1) {
+                        uint64_t wd[NE];
+                        uint32_t o[NE];
+                        bool ok[NE];
+#pragma unroll
+                        for (int q = 0; q < UNR; ++q) {
+                            wd[2 * q] = ((uint64_t)cur[q].y << 32) | cur[q].x;
+                            wd[2 * q + 1] = ((uint64_t)cur[q].w << 32) | cur[q].z;
+                            const uint32_t at = cb + (sub + q * LPT) * 2;
+                            ok[2 * q] = at < ce1 && at >= ce0;
+                            ok[2 * q + 1] = at + 1 < ce1;  // at + 1 >= ce0: at >= ce0 & ~1
+                        }
+#pragma unroll
+                        for (int q = 0; q < NE; ++q) o[q] = ok[q] ? (uint32_t)wd[q] : 0u;
+                        uint16_t lo_[NE];
+#pragma unroll
+                        for (int q = 0; q < NE; ++q) lo_[q] = lrow[o[q]];
+#pragma unroll
+                        for (int q = 0; q < NE; ++q) visits += ok[q];
+                        if ((pm >> cw) & 1ull) {
+                            // push: x in N_j, its class-w out-edges x -> v, v
+                            // unsettled or at l: v enters level l (stored once),
+                            // its loss min-folded by an LDS atomic
+                            const float onem = 1.0f - __uint_as_float(prow[cx]);
+#pragma unroll
+                            for (int q = 0; q < NE; ++q)
+                                if (ok[q] && lo_[q] >= (uint16_t)l) {
+                                    const float r = __uint_as_float((uint32_t)(wd[q] >> 32));
+#if LOSS_COUNT
+                                    if (!(lvl_diag & 2) && lo_[q] > (uint16_t)l) lrow[o[q]] = (uint16_t)l;
+                                    if (!(lvl_diag & 1))
+                                        atomicMin(&prow[o[q]], __float_as_uint(1.0f - __fmul_rn(onem, r)));
+#else
+                                    if (lo_[q] > (uint16_t)l) lrow[o[q]] = (uint16_t)l;
+                                    atomicMin(&prow[o[q]], __float_as_uint(1.0f - __fmul_rn(onem, r)));
+#endif
+                                }
                         } else {
-                            wd[q] = ce[at];
-                            ei[q] = at;
+                            // pull: x unsettled, its class-w in-edges u -> x, u in N_j
+                            const uint32_t j = l - cw;
+#pragma unroll
+                            for (int q = 0; q < NE; ++q)
+                                if (ok[q] && lo_[q] == (uint16_t)j) {
+                                    const float r = __uint_as_float((uint32_t)(wd[q] >> 32));
+                                    lrow[cx] = (uint16_t)l;
+                                    const float c = 1.0f - __fmul_rn(1.0f - __uint_as_float(prow[o[q]]), r);
+                                    atomicMin(&prow[cx], __float_as_uint(c));
+                                }
                         }
                     }
-                    uint32_t o[NE];
-                    bool ok[NE];
+                    ct = nt2;
+                    cw = nw2;
+                    cx = nx2;
+                    ce0 = ne02;
+                    ce1 = ne12;
+                    cb = nb;
 #pragma unroll
-                    for (int q = 0; q < NE; ++q) {
-                        ok[q] = ei[q] < e1 && (VW == 1 || ei[q] >= e0);
-                        o[q] = ok[q] ? (uint32_t)wd[q] : 0u;
-                    }
-                    uint16_t lo_[NE];
+                    for (int q = 0; q < UNR; ++q) cur[q] = nxt[q];
+                }
+            } else {
+                uint32_t nw_ = 1, nx = 0, ne0 = 0, ne1 = 0;
+                if (grp < T) item(grp, nw_, nx, ne0, ne1);
+                for (uint32_t t = grp; t < T; t += ngrp) {
+                    const uint32_t w = nw_, x = nx, e0 = ne0, e1 = ne1, j = l - w;
+                    if (t + ngrp < T) item(t + ngrp, nw_, nx, ne0, ne1);
+                    const bool push = (pm >> w) & 1ull;
+                    const uint64_t *ce = push ? ce_out : ce_in;
+                    // push: x in N_j, its class-w out-edges x -> v, v unsettled or at l;
+                    // pull: x unsettled, its class-w in-edges u -> x, u in N_j
+                    const float onem = push ? 1.0f - __uint_as_float(prow[x]) : 0.0f;
+                    constexpr int NE = UNR * VW;
+                    for (uint32_t b = VW == 2 ? e0 & ~1u : e0; b < e1; b += UNR * LPT * VW) {
+                        uint64_t wd[NE];
+                        uint32_t ei[NE];
 #pragma unroll
-                    for (int q = 0; q < NE; ++q) lo_[q] = lrow[o[q]];
-#pragma unroll
-                    for (int q = 0; q < NE; ++q) {
-                        visits += ok[q];
-                        const bool hit = ok[q] && (push ? lo_[q] >= (uint16_t)l : lo_[q] == (uint16_t)j);
-                        if (hit) {
-                            // the head enters level l (every writer stores l; a
-                            // head already at l is not stored again), its loss
-                            // min-folded by an LDS atomic (reading the loss first
-                            // and skipping the atomic when it cannot lower it
-                            // measured slower: C3 walk 49 -> 56 us a row)
-                            const float r = __uint_as_float((uint32_t)(wd[q] >> 32));
-                            if (push) {
-#if LOSS_COUNT
-                                // diagnostic builds: lvl_diag bit 0 drops the loss atomics,
-                                // bit 1 the level stores (wrong tables; timing only)
-                                if (!(lvl_diag & 2) && lo_[q] != (uint16_t)l) lrow[o[q]] = (uint16_t)l;
-                                if (!(lvl_diag & 1))
-                                    atomicMin(&prow[o[q]], __float_as_uint(1.0f - __fmul_rn(onem, r)));
-#else
-                                if (lo_[q] != (uint16_t)l) lrow[o[q]] = (uint16_t)l;
-                                atomicMin(&prow[o[q]], __float_as_uint(1.0f - __fmul_rn(onem, r)));
-#endif
+                        for (int q = 0; q < UNR; ++q) {
+                            const uint32_t at = b + (sub + q * LPT) * VW;  // padded past the end
+                            if (VW == 2) {
+                                const uint4 r2 = *reinterpret_cast<const uint4 *>(ce + at);
+                                wd[2 * q] = ((uint64_t)r2.y << 32) | r2.x;
+                                wd[2 * q + 1] = ((uint64_t)r2.w << 32) | r2.z;
+                                ei[2 * q] = at;
+                                ei[2 * q + 1] = at + 1;
                             } else {
-                                lrow[x] = (uint16_t)l;
-                                const float c = 1.0f - __fmul_rn(1.0f - __uint_as_float(prow[o[q]]), r);
-                                atomicMin(&prow[x], __float_as_uint(c));
+                                wd[q] = ce[at];
+                                ei[q] = at;
+                            }
+                        }
+                        uint32_t o[NE];
+                        bool ok[NE];
+#pragma unroll
+                        for (int q = 0; q < NE; ++q) {
+                            ok[q] = ei[q] < e1 && (VW == 1 || ei[q] >= e0);
+                            o[q] = ok[q] ? (uint32_t)wd[q] : 0u;
+                        }
+                        uint16_t lo_[NE];
+#pragma unroll
+                        for (int q = 0; q < NE; ++q) lo_[q] = lrow[o[q]];
+#pragma unroll
+                        for (int q = 0; q < NE; ++q) {
+                            visits += ok[q];
+                            const bool hit = ok[q] && (push ? lo_[q] >= (uint16_t)l : lo_[q] == (uint16_t)j);
+                            if (hit) {
+                                // the head enters level l (every writer stores l; a
+                                // head already at l is not stored again), its loss
+                                // min-folded by an LDS atomic (reading the loss first
+                                // and skipping the atomic when it cannot lower it
+                                // measured slower: C3 walk 49 -> 56 us a row)
+                                const float r = __uint_as_float((uint32_t)(wd[q] >> 32));
+                                if (push) {
+#if LOSS_COUNT
+                                    // diagnostic builds: lvl_diag bit 0 drops the loss atomics,
+                                    // bit 1 the level stores (wrong tables; timing only)
+                                    if (!(lvl_diag & 2) && lo_[q] != (uint16_t)l) lrow[o[q]] = (uint16_t)l;
+                                    if (!(lvl_diag & 1))
+                                        atomicMin(&prow[o[q]], __float_as_uint(1.0f - __fmul_rn(onem, r)));
+#else
+                                    if (lo_[q] != (uint16_t)l) lrow[o[q]] = (uint16_t)l;
+                                    atomicMin(&prow[o[q]], __float_as_uint(1.0f - __fmul_rn(onem, r)));
+#endif
+                                } else {
+                                    lrow[x] = (uint16_t)l;
+                                    const float c = 1.0f - __fmul_rn(1.0f - __uint_as_float(prow[o[q]]), r);
+                                    atomicMin(&prow[x], __float_as_uint(c));
+                                }
                             }
                         }
                     }
@@ -3244,7 +3348,11 @@ void launch_solve_ctx(const LevelCtx &c, unsigned long long *d_stats, const uint
                            list, stage, stage_loss, stage_mode, probe, c.visits, c.lmem);
         return;
     }
-    auto kern = c.t_cls == 16   ? (nts ? level_solve_kernel<4, 4, 16, 2, true> : level_solve_kernel<4, 4, 16, 2, false>)
+    // knob SRT_LVL_SP=0: the per-item walk (A/B)
+    static const bool sp = !(std::getenv("SRT_LVL_SP") && std::atoi(std::getenv("SRT_LVL_SP")) == 0);
+    auto kern = c.t_cls == 16 && sp
+                    ? (nts ? level_solve_kernel<4, 4, 16, 2, true, true> : level_solve_kernel<4, 4, 16, 2, false, true>)
+                : c.t_cls == 16 ? (nts ? level_solve_kernel<4, 4, 16, 2, true> : level_solve_kernel<4, 4, 16, 2, false>)
                 : c.t_cls == 32 ? (nts ? level_solve_kernel<4, 2, 32, 2, true> : level_solve_kernel<4, 2, 32, 2, false>)
                                 : (nts ? level_solve_kernel<4, 2, 64, 2, true> : level_solve_kernel<4, 2, 64, 2, false>);
     (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(LDS_BUDGET - 4096));
