@@ -3348,13 +3348,21 @@ void launch_solve_ctx(const LevelCtx &c, unsigned long long *d_stats, const uint
                            list, stage, stage_loss, stage_mode, probe, c.visits, c.lmem);
         return;
     }
-    // knob SRT_LVL_SP=0: the per-item walk (A/B)
+    // knob SRT_LVL_SP=0: the per-item walk (A/B).  Measured at C3 (same box):
+    // branch-free hits through a per-lane dummy word 4.83 ms, the same as the
+    // pipelined walk; lane groups x pairs in flight 4x4 (kept) 4.79, 2x4 5.22,
+    // 8x2 5.50, 4x2 5.57, 2x2 6.09 ms
     static const bool sp = !(std::getenv("SRT_LVL_SP") && std::atoi(std::getenv("SRT_LVL_SP")) == 0);
-    auto kern = c.t_cls == 16 && sp
-                    ? (nts ? level_solve_kernel<4, 4, 16, 2, true, true> : level_solve_kernel<4, 4, 16, 2, false, true>)
-                : c.t_cls == 16 ? (nts ? level_solve_kernel<4, 4, 16, 2, true> : level_solve_kernel<4, 4, 16, 2, false>)
-                : c.t_cls == 32 ? (nts ? level_solve_kernel<4, 2, 32, 2, true> : level_solve_kernel<4, 2, 32, 2, false>)
-                                : (nts ? level_solve_kernel<4, 2, 64, 2, true> : level_solve_kernel<4, 2, 64, 2, false>);
+    auto kern =
+        sp ? (c.t_cls == 16   ? (nts ? level_solve_kernel<4, 4, 16, 2, true, true>
+                                     : level_solve_kernel<4, 4, 16, 2, false, true>)
+              : c.t_cls == 32 ? (nts ? level_solve_kernel<4, 2, 32, 2, true, true>
+                                     : level_solve_kernel<4, 2, 32, 2, false, true>)
+                              : (nts ? level_solve_kernel<4, 2, 64, 2, true, true>
+                                     : level_solve_kernel<4, 2, 64, 2, false, true>))
+           : (c.t_cls == 16   ? (nts ? level_solve_kernel<4, 4, 16, 2, true> : level_solve_kernel<4, 4, 16, 2, false>)
+              : c.t_cls == 32 ? (nts ? level_solve_kernel<4, 2, 32, 2, true> : level_solve_kernel<4, 2, 32, 2, false>)
+                              : (nts ? level_solve_kernel<4, 2, 64, 2, true> : level_solve_kernel<4, 2, 64, 2, false>));
     (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(LDS_BUDGET - 4096));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, c.stream, V, c.nodes, c.n, list ? 0u : r0, r1, co, ci, eo, ei,
                        lcap, c.g, c.sl_lat, c.sl_loss, c.out_lat, c.out_loss, d_stats, list,
