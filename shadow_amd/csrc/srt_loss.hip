@@ -507,6 +507,7 @@ __global__ __launch_bounds__(256) void lvl_sym_tile_kernel(uint32_t V, const uin
 // (only those losses cross PCIe).  One wave per row: pass 1 keeps the chunks'
 // ballots in LDS, one atomic reserves the row's range, pass 2 writes the
 // indices in row order.  Past `cap` entries are counted, not written.
+template <bool IDENT>
 __global__ __launch_bounds__(256) void lvl_index_kernel(uint32_t V, const uint64_t *__restrict__ row_ptr,
                                                         const uint32_t *__restrict__ col,
                                                         const uint64_t *__restrict__ lat, uint64_t wmax_ns,
@@ -523,7 +524,7 @@ __global__ __launch_bounds__(256) void lvl_index_kernel(uint32_t V, const uint64
         auto test = [&](uint32_t c) -> uint64_t {
             const uint64_t k = b + 64ull * c + lane;
             const uint64_t l = k < e ? lat[k] : ~0ull;
-            return __ballot(l <= wmax_ns && col[k] != u);
+            return __ballot(l <= wmax_ns && (IDENT ? (uint32_t)(k - b) != u : col[k] != u));
         };
         uint32_t cnt = 0;
         for (uint32_t c0 = 0; c0 < nch; c0 += 4) {
@@ -3537,8 +3538,13 @@ size_t level_scratch_bytes(int device, uint32_t V, bool quant) {
 void level_loss_index(srt_plan *p, uint32_t *d_idx, uint64_t cap, unsigned long long *d_cnt, hipStream_t s) {
     const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(8192, (p->V + 3) / 4));
     (void)hipMemsetAsync(d_cnt, 0, sizeof *d_cnt, s);
-    hipLaunchKernelGGL(lvl_index_kernel, dim3(blocks), dim3(256), 0, s, p->V, p->d_row_ptr, p->d_col, p->d_lat,
-                       p->kp.lmax * p->kp.g, d_idx, cap, d_cnt);
+    // identity rows: the column is the entry's place in its row (no column loads)
+    if (p->ident_rows)
+        hipLaunchKernelGGL(lvl_index_kernel<true>, dim3(blocks), dim3(256), 0, s, p->V, p->d_row_ptr, p->d_col,
+                           p->d_lat, p->kp.lmax * p->kp.g, d_idx, cap, d_cnt);
+    else
+        hipLaunchKernelGGL(lvl_index_kernel<false>, dim3(blocks), dim3(256), 0, s, p->V, p->d_row_ptr, p->d_col,
+                           p->d_lat, p->kp.lmax * p->kp.g, d_idx, cap, d_cnt);
 }
 
 void loss_scatter(const uint32_t *d_idx, const float *d_val, uint64_t count, float *d_loss, hipStream_t s) {
