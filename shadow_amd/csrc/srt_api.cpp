@@ -970,6 +970,11 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     if (piped) pu.finish(&cs);
     else scanner.join();
     p->ident_rows = cs.ident;
+    {
+        bool idn = n == g->n_nodes;
+        for (uint32_t j = 0; idn && j < n; ++j) idn = nodes[j] == j;
+        p->ident_nodes = idn;
+    }
     tr.mark("create: CSR scan (joined)");
 
     // 2. the reference's errors, in its order: edge attributes (parse time),

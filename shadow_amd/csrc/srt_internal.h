@@ -189,6 +189,7 @@ struct srt_plan {
     std::string desc;
     bool identity_nodes = false;
     bool ident_rows = false;  // the adjacency is V identity rows (host scan, CsrStats::ident)
+    bool ident_nodes = false;  // the in-use nodes are 0 .. V-1 in order (nodes[j] = j, n = V)
     double create_device_ms = 0.0;  // device work of srt_plan_create (probes, symmetry / bound checks)
     bool in_create = false;         // srt_plan_create is running: its kernels are timed (srt::cspan_*)
     std::vector<hipEvent_t> cspan;  // event pairs around those kernels
@@ -497,6 +498,7 @@ struct LevelCtx {
     unsigned long long *visits = nullptr;  // class entries walked (nullable)
     uint32_t q = 0, rb = 0, vb = 0;        // quantized solve: bucket width (units), remainder / vertex bits of an entry
     uint16_t *lmem = nullptr;              // quantized solve: level_scratch_bytes of per-workgroup scratch
+    bool idn = false;                      // nodes[j] = j, n = V, n % 4 == 0: the vectorised row output
 };
 LevelCtx level_ctx(srt_plan *p);
 // the class CSRs of a level plan at its bound (the run's first step)

@@ -1574,7 +1574,7 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
     const float *__restrict__ sl_loss, uint64_t *__restrict__ out_lat, float *__restrict__ out_loss,
     unsigned long long *stats, const uint32_t *__restrict__ row_list, void *__restrict__ out32,
     float *__restrict__ out32_loss, bool stage16, uint32_t *__restrict__ probe,
-    unsigned long long *__restrict__ visit_cnt) {
+    unsigned long long *__restrict__ visit_cnt, bool idn) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ unsigned long long red_min[16], red_cnt[16], red_vis[16];
     __shared__ uint32_t red_max[16];
@@ -1604,10 +1604,25 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
 #if LOSS_COUNT
         unsigned long long tk0 = wall_clock64();
 #endif
-        // 1. every vertex unreached, s at level 0 (petgraph's zero score)
-        for (uint32_t v = tid; v < V; v += nt) {
-            lrow[v] = v == s ? (uint16_t)0 : LINF;
-            prow[v] = v == s ? 0u : FINF;
+        // 1. every vertex unreached, s at level 0 (petgraph's zero score);
+        // four vertices a thread a step (8-B level and 16-B loss stores)
+        for (uint32_t v4 = 4 * tid; v4 < V; v4 += 4 * nt) {
+            if (v4 + 3 < V) {
+                uint2 lw = make_uint2(0xffffffffu, 0xffffffffu);
+                uint4 pw = make_uint4(FINF, FINF, FINF, FINF);
+                if (s - v4 < 4u) {
+                    const uint32_t q = s - v4;
+                    (q < 2 ? lw.x : lw.y) &= q & 1 ? 0x0000ffffu : 0xffff0000u;
+                    (q == 0 ? pw.x : q == 1 ? pw.y : q == 2 ? pw.z : pw.w) = 0u;
+                }
+                *reinterpret_cast<uint2 *>(lrow + v4) = lw;
+                *reinterpret_cast<uint4 *>(prow + v4) = pw;
+            } else {
+                for (uint32_t v = v4; v < V; ++v) {
+                    lrow[v] = v == s ? (uint16_t)0 : LINF;
+                    prow[v] = v == s ? 0u : FINF;
+                }
+            }
         }
         if (tid == 0) {
             hist[0] = 1;
@@ -1617,6 +1632,37 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
         __syncthreads();
         LOSS_TICK(4)
         uint32_t settled = 1;
+        // the vertices v with lrow[v] == want appended to mem[at + cur[par][ci]
+        // ...) in any order: four a thread a step (one 8-B level read), one
+        // LDS atomic a wave a step
+        auto compact = [&](uint16_t want, uint32_t at, uint32_t par, int ci) {
+            for (uint32_t v4 = 4 * tid; v4 < V; v4 += 4 * nt) {
+                uint32_t fm = 0;
+                if (v4 + 3 < V) {
+                    const uint2 w = *reinterpret_cast<const uint2 *>(lrow + v4);
+                    fm = (uint32_t)((w.x & 0xffffu) == want) | (uint32_t)((w.x >> 16) == want) << 1 |
+                         (uint32_t)((w.y & 0xffffu) == want) << 2 | (uint32_t)((w.y >> 16) == want) << 3;
+                } else {
+                    for (uint32_t q = 0; q < 4; ++q)
+                        if (v4 + q < V && lrow[v4 + q] == want) fm |= 1u << q;
+                }
+                uint32_t tot = 0, bel = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint64_t m = __ballot((fm >> q) & 1u);
+                    tot += (uint32_t)__popcll(m);
+                    bel += (uint32_t)__popcll(m & below);
+                }
+                if (!tot) continue;  // uniform
+                uint32_t b = 0;
+                if (lane == 0) b = atomicAdd(&cur[par][ci], tot);
+                b = __shfl(b, 0);
+                uint32_t pos = at + b + bel;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if ((fm >> q) & 1u) mem[pos++] = (uint16_t)(v4 + q);
+            }
+        };
         // 2. levels in increasing latency
         for (uint32_t l = 1; l <= lcap && settled < V; ++l) {
             const uint32_t U = V - settled, par = l & 1u;
@@ -1665,16 +1711,7 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
 #endif
             if (plan_pull) {
                 // the unsettled vertices into mem[settled, V) (any order)
-                for (uint32_t base = 0; base < V; base += nt) {
-                    const uint32_t v = base + tid;
-                    const bool f = v < V && lrow[v] == LINF;
-                    const uint64_t m = __ballot(f);
-                    if (!m) continue;  // uniform
-                    uint32_t b = 0;
-                    if (lane == 0) b = atomicAdd(&cur[par][0], (uint32_t)__popcll(m));
-                    b = __shfl(b, 0);
-                    if (f) mem[settled + b + (uint32_t)__popcll(m & below)] = (uint16_t)v;
-                }
+                compact(LINF, settled, par, 0);
                 __syncthreads();
             }
             LVL_TICK(0)
@@ -1862,16 +1899,7 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
             __syncthreads();  // every head of level l found
             LVL_TICK(1)
             // N_l (the vertices now at level l) -> mem[settled, ...)
-            for (uint32_t base = 0; base < V; base += nt) {
-                const uint32_t v = base + tid;
-                const bool f = v < V && lrow[v] == (uint16_t)l;
-                const uint64_t m = __ballot(f);
-                if (!m) continue;  // uniform
-                uint32_t b = 0;
-                if (lane == 0) b = atomicAdd(&cur[par][1], (uint32_t)__popcll(m));
-                b = __shfl(b, 0);
-                if (f) mem[settled + b + (uint32_t)__popcll(m & below)] = (uint16_t)v;
-            }
+            compact((uint16_t)l, settled, par, 1);
             __syncthreads();
             LVL_TICK(2)
             settled += cur[par][1];
@@ -1905,6 +1933,66 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
         uint32_t *o32 = out32 && !stage16 ? reinterpret_cast<uint32_t *>(out32) + (uint64_t)k * n : nullptr;
         uint16_t *o16 = out32 && stage16 ? reinterpret_cast<uint16_t *>(out32) + (uint64_t)k * n : nullptr;
         float *o32p = out32_loss ? out32_loss + (uint64_t)k * n : nullptr;
+        if (idn) {
+            // every node in use, in node order (nodes[j] = j, n = V, n % 4 == 0):
+            // four columns a thread a step -- one 8-B level and one 16-B loss
+            // read from LDS, 16-B non-temporal stores
+            typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+            typedef float f32x4 __attribute__((ext_vector_type(4)));
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+            for (uint32_t j4 = 4 * tid; j4 < n; j4 += 4 * nt) {
+                const uint2 lw = *reinterpret_cast<const uint2 *>(lrow + j4);
+                const uint4 pw = *reinterpret_cast<const uint4 *>(prow + j4);
+                const uint32_t lv[4] = {lw.x & 0xffffu, lw.x >> 16, lw.y & 0xffffu, lw.y >> 16};
+                const uint32_t pv[4] = {pw.x, pw.y, pw.z, pw.w};
+                uint64_t lu[4], latv[4];
+                float lossv[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (j4 + q == i) {
+                        latv[q] = sl_lat[i];
+                        lossv[q] = sl_loss[i];
+                        lu[q] = latv[q] == ~0ull ? ~0ull : latv[q] / g;
+                    } else if (lv[q] == LINF) {
+                        ++unreach;
+                        latv[q] = lu[q] = ~0ull;
+                        lossv[q] = 1.0f;
+                    } else {
+                        lu[q] = lv[q];
+                        latv[q] = lu[q] * g;
+                        lossv[q] = __uint_as_float(pv[q]);
+                    }
+                    mn = latv[q] < mn ? latv[q] : mn;
+                }
+                const f32x4 lp = {lossv[0], lossv[1], lossv[2], lossv[3]};
+                if (o32p) {
+                    if (o16) {
+                        const u16x4 lq = {(unsigned short)(latv[0] == ~0ull ? 0xffffu : lu[0]),
+                                          (unsigned short)(latv[1] == ~0ull ? 0xffffu : lu[1]),
+                                          (unsigned short)(latv[2] == ~0ull ? 0xffffu : lu[2]),
+                                          (unsigned short)(latv[3] == ~0ull ? 0xffffu : lu[3])};
+                        __builtin_nontemporal_store(lq, reinterpret_cast<u16x4 *>(o16 + j4));
+                    } else if (o32) {
+                        const u32x4 lq = {latv[0] == ~0ull ? ~0u : (unsigned)lu[0],
+                                          latv[1] == ~0ull ? ~0u : (unsigned)lu[1],
+                                          latv[2] == ~0ull ? ~0u : (unsigned)lu[2],
+                                          latv[3] == ~0ull ? ~0u : (unsigned)lu[3]};
+                        __builtin_nontemporal_store(lq, reinterpret_cast<u32x4 *>(o32 + j4));
+                    }
+                    __builtin_nontemporal_store(lp, reinterpret_cast<f32x4 *>(o32p + j4));
+                } else if (NT) {
+                    const u64x2 a = {latv[0], latv[1]}, c = {latv[2], latv[3]};
+                    __builtin_nontemporal_store(a, reinterpret_cast<u64x2 *>(ol + j4));
+                    __builtin_nontemporal_store(c, reinterpret_cast<u64x2 *>(ol + j4 + 2));
+                    __builtin_nontemporal_store(lp, reinterpret_cast<f32x4 *>(op + j4));
+                } else {
+                    *reinterpret_cast<u64x2 *>(ol + j4) = u64x2{latv[0], latv[1]};
+                    *reinterpret_cast<u64x2 *>(ol + j4 + 2) = u64x2{latv[2], latv[3]};
+                    *reinterpret_cast<f32x4 *>(op + j4) = lp;
+                }
+            }
+        } else
         for (uint32_t j0 = tid; j0 < n; j0 += 4 * nt) {
             uint32_t vv[4];
 #pragma unroll
@@ -3037,6 +3125,7 @@ LevelCtx level_ctx(srt_plan *p) {
     c.rb = p->lvl_rb;
     c.vb = p->lvl_vb;
     c.lmem = p->d_lmem;
+    c.idn = p->ident_nodes && p->n == p->V && p->n % 4 == 0;
     return c;
 }
 
@@ -3368,7 +3457,7 @@ void launch_solve_ctx(const LevelCtx &c, unsigned long long *d_stats, const uint
     hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, c.stream, V, c.nodes, c.n, list ? 0u : r0, r1, co, ci, eo, ei,
                        lcap, c.g, c.sl_lat, c.sl_loss, c.out_lat, c.out_loss, d_stats, list,
                        stage_mode ? stage : nullptr, stage_mode ? stage_loss : nullptr, stage_mode == 1, probe,
-                       c.visits);
+                       c.visits, c.idn);
 }
 
 // the per-workgroup scratch of the quantized solve (p->d_lmem): every
