@@ -1610,10 +1610,14 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
             if (v4 + 3 < V) {
                 uint2 lw = make_uint2(0xffffffffu, 0xffffffffu);
                 uint4 pw = make_uint4(FINF, FINF, FINF, FINF);
-                if (s - v4 < 4u) {
+                if (s - v4 < 4u) {  // s among them: level 0, loss 0 (selects, no indexed lvalue)
                     const uint32_t q = s - v4;
-                    (q < 2 ? lw.x : lw.y) &= q & 1 ? 0x0000ffffu : 0xffff0000u;
-                    (q == 0 ? pw.x : q == 1 ? pw.y : q == 2 ? pw.z : pw.w) = 0u;
+                    lw.x &= q == 0 ? 0xffff0000u : q == 1 ? 0x0000ffffu : 0xffffffffu;
+                    lw.y &= q == 2 ? 0xffff0000u : q == 3 ? 0x0000ffffu : 0xffffffffu;
+                    pw.x = q == 0 ? 0u : pw.x;
+                    pw.y = q == 1 ? 0u : pw.y;
+                    pw.z = q == 2 ? 0u : pw.z;
+                    pw.w = q == 3 ? 0u : pw.w;
                 }
                 *reinterpret_cast<uint2 *>(lrow + v4) = lw;
                 *reinterpret_cast<uint4 *>(prow + v4) = pw;
