@@ -1747,17 +1747,25 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
 #pragma unroll
                     for (int q = 0; q < UNR; ++q) d[q] = *reinterpret_cast<const uint4 *>(ce + b + (sub + q * LPT) * 2);
                 };
-                uint32_t ct = grp, cw = 1, cx = 0, ce0 = 0, ce1 = 0;  // the chunk's item
-                uint32_t pw = 1, px = 0, pe0 = 0, pe1 = 0;            // the group's next item
+                // a small level (2 T <= lane groups) in a workgroup alone on its
+                // CU (1,024 threads: nothing else hides its latency): K groups an
+                // item, group g taking item g mod T's chunks g div T, + K, + 2K,
+                // ... (one item a group), so its few lists are walked in one or
+                // two steps instead of one chunk a step by one group (C3 4.40 ->
+                // 4.26 ms; C2's 4 workgroups a CU: 0.334 -> 0.351 ms, so not there)
+                const uint32_t K = nt == LOSS_NT && 2 * T <= ngrp ? ngrp / T : 1u;
+                const uint32_t CHS = K * CH;  // a group's chunk stride in an item
+                uint32_t ct = K > 1 ? (grp < T * K ? grp % T : T) : grp, cw = 1, cx = 0, ce0 = 0, ce1 = 0;
+                uint32_t pw = 1, px = 0, pe0 = 0, pe1 = 0;  // the group's next item
                 if (ct < T) item(ct, cw, cx, ce0, ce1);
                 pw = cw;
                 if (ct + ngrp < T) item(ct + ngrp, pw, px, pe0, pe1);
-                uint32_t cb = ce0 & ~1u;
+                uint32_t cb = (ce0 & ~1u) + (K > 1 ? grp / T : 0u) * CH;
                 uint4 cur[UNR];
-                if (ct < T) load(cur, cw, cb);
+                if (ct < T && cb < ce1) load(cur, cw, cb);  // (a chunk past a short list: nothing to load)
                 while (ct < T) {
                     // the next chunk: this item's next one, or the next item's first
-                    uint32_t nt2 = ct, nw2 = cw, nx2 = cx, ne02 = ce0, ne12 = ce1, nb = cb + CH;
+                    uint32_t nt2 = ct, nw2 = cw, nx2 = cx, ne02 = ce0, ne12 = ce1, nb = cb + CHS;
                     const bool adv = nb >= ce1;
                     if (adv) {
                         nt2 = ct + ngrp;
