@@ -1557,11 +1557,22 @@ bool upload_level_losses(srt_plan *p, srt_err *err, srt_status *st) {
     *st = SRT_OK;
     if (p->algo != SRT_ALGO_LEVEL || p->n_adj >= (1ull << 32) || !p->lvl_cap || std::getenv("SRT_LOSS_FULL"))
         return false;
-    std::unique_lock<std::mutex> lk(g_pinned.m, std::try_to_lock);
-    const uint64_t cap = p->lvl_cap;  // the probe's count: >= the run's (its bound is >= B)
-    if (!lk.owns_lock() || g_pinned.bytes < 64) return false;
-    hipStream_t M = p->stream;
+    // the pinned staging: waited for when busy -- the first one-call build of
+    // a process without srt_init pins it on a thread behind its closure
+    // (build_e2e), and the needed-loss path (~5 ms at C3) beats the full
+    // pageable upload it would otherwise fall back to (~25-48 ms)
     Trace tr;
+    std::unique_lock<std::mutex> lk(g_pinned.m, std::try_to_lock);
+    if (!lk.owns_lock()) {
+        lk.lock();
+        tr.mark("losses: waited for the pinned staging");
+    }
+    const uint64_t cap = p->lvl_cap;  // the probe's count: >= the run's (its bound is >= B)
+    if (g_pinned.bytes < 64) {
+        tr.mark("losses: no pinned staging, full upload");
+        return false;
+    }
+    hipStream_t M = p->stream;
     auto fail = [&](hipError_t e, const char *what) {
         *st = hip_fail(err, e, what);
         return true;
@@ -1585,7 +1596,10 @@ bool upload_level_losses(srt_plan *p, srt_err *err, srt_status *st) {
     const uint64_t cnt = h[0];
     tr.mark("losses: needed entries listed");
     // (cnt > cap cannot happen: the probe's bound is >= the run's)
-    if (cnt > cap || g_pinned.bytes < cnt * 8) return false;  // the full upload
+    if (cnt > cap || g_pinned.bytes < cnt * 8) {  // the full upload
+        tr.mark("losses: staging too small, full upload");
+        return false;
+    }
     // the range check of every loss, behind the build (8 host threads),
     // started once the needed losses are gathered (knob SRT_LOSSCHK_EARLY=1:
     // before the gather, A/B) -- it streams the whole loss array, and the
