@@ -1102,11 +1102,15 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
                     return probe_fail();
                 p->lvl_sym_lat = p->lvl_sym = sym;
             }
-            // levels of one unit: 31 classes first (C1-C3: B <= 14), then 63
+            // levels of one unit
             auto probe = [&](uint64_t wmax, uint32_t wc) {
                 return dev_timed([&] { return srt::level_probe(p, wmax, wc, &lvl_bound, &lvl_visits, &e2); });
             };
-            if (probe(std::min<uint64_t>(31, maxu), 31) != SRT_OK) return probe_fail();
+            // 15 classes first (r06: C1-C3 prove B <= 14 there, and the probe CSR
+            // of the edges <= 15 units is half the one at 31), then 31, then 63
+            // (each also admits longer paths of short edges: bounds up to wc)
+            if (probe(std::min<uint64_t>(15, maxu), 15) != SRT_OK) return probe_fail();
+            if (lvl_bound == ~0ull && probe(std::min<uint64_t>(31, maxu), 31) != SRT_OK) return probe_fail();
             if (lvl_bound == ~0ull && probe(std::min<uint64_t>(63, maxu), 63) != SRT_OK) return probe_fail();
             // no bound within 63 units: the quantized solve, buckets of q <= the
             // shortest edge (C3ns: g = 1 ns, edges >= 1 ms), when the shortest
