@@ -76,8 +76,8 @@ PATH_DTYPE = np.dtype([("lat", "<u8"), ("loss", "<f4"), ("pad", "<u4")])
 def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--nodes", type=int, default=0, help="override the config's node count")
     ap.add_argument("--in-use", dest="in_use", type=int, default=0,
