@@ -47,7 +47,10 @@ __host__ __device__ __forceinline__ uint64_t xoshiro_next(uint64_t &s0, uint64_t
 }
 
 constexpr int RT = 256;          // threads a round workgroup
-constexpr int HB = 16;           // source hosts a workgroup (C5: 625 workgroups, ~1,600 packets each)
+#ifndef SRT_PKT_HB
+#define SRT_PKT_HB 16
+#endif
+constexpr int HB = SRT_PKT_HB;   // source hosts a workgroup (C5: 625 workgroups, ~1,600 packets each)
 constexpr uint32_t DCAP = 3072;  // draws a workgroup keeps in LDS (24 KB)
 constexpr int KP = 8;            // packets a lane holds across the host walks (RT * KP = 2,048 a workgroup)
 constexpr int PF = 16;           // send times in flight a host walk (the exact walk)
