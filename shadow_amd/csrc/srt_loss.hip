@@ -280,14 +280,19 @@ __global__ __launch_bounds__(256) void tight_rows_kernel(const K *__restrict__ D
 // from the adjacency.  Out-rows: one wave per adjacency row u (whose entries
 // ARE u's out-edges), two passes -- pass 1 tests each 64-entry chunk (the
 // latency first; the column is loaded only for the lanes that pass: C3 ~2% of
-// the entries) and keeps its ballot in LDS, counting the hits per class by
-// LDS atomics; one global atomic takes the row's range, the row's class
-// offsets are written (slot k: start of class k + 1; slot CLS - 1: the row's
-// end), and pass 2 writes every hit (1f32 - e bits << 32 | v; 0 bits without
-// losses) at its class's running position, and counts it for the in-row of
-// (v, class).  No global atomic per entry on the out side, where a row's ~50
-// entries of a class would all hit one counter.  Entries past `cap` are
-// counted, not written (the caller sizes and runs again).
+// the entries), counts the hits per class by LDS atomics and stages each hit
+// (its place in the row, its weight in units) in LDS at its ballot rank; one
+// global atomic takes the row's range, the row's class offsets are written
+// (slot k: start of class k + 1; slot CLS - 1: the row's end), and pass 2
+// deals the staged hits one a lane, OUT_PL a lane at once (their loss / column
+// gathers in flight together), writing each (1f32 - e bits << 32 | v; 0 bits
+// without losses) at its class's running position and counting it for the
+// in-row of (v, class).  A row with more than OUT_SCAP hits is tested again
+// chunk by chunk in pass 2.  No global atomic per entry on the out side, where
+// a row's ~50 entries of a class would all hit one counter.  Entries past
+// `cap` are counted, not written (the caller sizes and runs again).
+constexpr uint32_t OUT_SCAP = 512;  // hits a wave stages in LDS (C3: ~330 a row)
+constexpr int OUT_PL = 4;           // staged hits a lane places at once (pass 2)
 template <bool WITH_LOSS, bool IN = true, bool IDENT = false>
 __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t u0, uint32_t V, const uint64_t *__restrict__ row_ptr,
                                                       const uint32_t *__restrict__ col,
@@ -297,43 +302,44 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t u0, uint32_t V, c
                                                       uint32_t *__restrict__ off_out, uint32_t *__restrict__ in_cnt,
                                                       uint64_t *__restrict__ ce_out, uint64_t cap,
                                                       unsigned long long *cursor, unsigned long long *maxw) {
-    __shared__ uint64_t bal[4][TR_CH];
-    __shared__ uint16_t pre[4][TR_CH];  // per wave: the row's hits before chunk c
-    __shared__ uint32_t ccnt[4][64];  // per wave: hits per class (pass 1), running positions (pass 2)
+    __shared__ uint2 stage[4][OUT_SCAP];  // per wave: {place in the row, weight in units} of hit j
+    __shared__ uint32_t ccnt[4][64];      // per wave: hits per class (pass 1), running positions (pass 2)
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const uint64_t below = (1ull << lane) - 1ull;
     uint32_t mw = 0;
     // l = w * g exactly; the class: w / q (q = 0: the exact weight)
     auto units_of = [&](uint64_t l) -> uint64_t { return (uint64_t)((double)l * inv_g + 0.5); };
-    auto cls_of = [&](uint64_t l) -> uint32_t { return (uint32_t)(q ? units_of(l) / q : units_of(l)); };
+    auto cls_of_units = [&](uint64_t wu) -> uint32_t { return (uint32_t)(q ? wu / q : wu); };
     for (uint32_t u = u0 + wave; u < V; u += nwaves) {  // rows [u0, V)
         const uint64_t b = row_ptr[u], e = row_ptr[u + 1];
         const uint32_t nch = (uint32_t)((e - b + 63) / 64);
         ccnt[wv][lane] = 0;
         uint32_t cnt = 0;
+        bool wide = false;  // a weight of 2^32 units or more: not staged (the row is tested again)
         for (uint32_t c0 = 0; c0 < nch; c0 += 4) {
             uint64_t l[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint64_t k = b + 64ull * (c0 + q) + lane;
-                l[q] = k < e ? lat[k] : ~0ull;
+            for (int r = 0; r < 4; ++r) {
+                const uint64_t k = b + 64ull * (c0 + r) + lane;
+                l[r] = k < e ? lat[k] : ~0ull;
             }
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint64_t k = b + 64ull * (c0 + q) + lane;
+            for (int r = 0; r < 4; ++r) {
+                const uint64_t k = b + 64ull * (c0 + r) + lane;
                 // col only where the latency passes; identity rows (IDENT): the
                 // column is the entry's place in its row
-                const bool f = l[q] <= wmax_ns && (IDENT ? (uint32_t)(k - b) != u : col[k] != u);
+                const bool f = l[r] <= wmax_ns && (IDENT ? (uint32_t)(k - b) != u : col[k] != u);
                 const uint64_t m = __ballot(f);
                 if (f) {
-                    const uint32_t c = cls_of(l[q]);
+                    const uint64_t wu = units_of(l[r]);
+                    const uint32_t c = cls_of_units(wu);
                     atomicAdd(&ccnt[wv][c - 1], 1u);
                     mw = c > mw ? c : mw;
-                }
-                if (c0 + q < TR_CH && lane == 0) {
-                    bal[wv][c0 + q] = m;
-                    pre[wv][c0 + q] = (uint16_t)cnt;
+                    const uint32_t j = cnt + (uint32_t)__popcll(m & below);
+                    wide |= (wu >> 32) != 0;
+                    if (j < OUT_SCAP) stage[wv][j] = make_uint2((uint32_t)(k - b), (uint32_t)wu);
                 }
                 cnt += (uint32_t)__popcll(m);
             }
@@ -352,12 +358,10 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t u0, uint32_t V, c
         const uint32_t start = (uint32_t)base + incl - x;
         if (lane < cls) off_out[(uint64_t)u * cls + lane] = fits ? (lane == cls - 1 ? (uint32_t)(base + cnt) : start) : 0u;
         ccnt[wv][lane] = start;  // running positions
-        if (!cnt || !fits) continue;            // uniform
-        auto place = [&](uint64_t k) {
-            const uint32_t v = IDENT ? (uint32_t)(k - b) : col[k];
-            const uint64_t wu = units_of(lat[k]);
-            const float ls = WITH_LOSS ? loss[k] : 0.0f;
-            const uint32_t cl = (uint32_t)(q ? wu / q : wu);
+        if (!cnt || !fits) continue;  // uniform
+        const bool staged = cnt <= OUT_SCAP && !__any(wide);
+        auto put = [&](uint32_t v, uint64_t wu, float ls) {
+            const uint32_t cl = cls_of_units(wu);
             const uint32_t pos = atomicAdd(&ccnt[wv][cl - 1], 1u);
             const float eb = WITH_LOSS ? 1.0f - ls : 0.0f;  // (1f32 - other.packet_loss), mod.rs:328
             // q > 0 (quantized classes): the weight's remainder w - c q rides
@@ -366,39 +370,33 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t u0, uint32_t V, c
                             : ((uint64_t)__float_as_uint(eb) << 32) | v;
             if (IN) atomicAdd(&in_cnt[(uint64_t)v * cls + cl - 1], 1u);  // symmetric plans: no in-rows
         };
-        // the hits of the kept chunks dealt one a lane (the j-th hit: the chunk
-        // whose prefix count covers j, the (j - prefix)-th set bit of its
-        // ballot): ~330 hits a row (C3) in 6 rounds of independent loads, not
-        // one dependent round a chunk with a hit
-        const uint32_t nc1 = nch < TR_CH ? nch : TR_CH;
-        const uint32_t cntk = nc1 == nch ? cnt : (uint32_t)pre[wv][nc1 - 1] + (uint32_t)__popcll(bal[wv][nc1 - 1]);
-        for (uint32_t j0 = 0; j0 < cntk; j0 += 64) {  // uniform
-            const uint32_t j = j0 + lane;
-            if (j >= cntk) continue;
-            uint32_t lo = 0, hi = nc1 - 1;  // the last chunk whose prefix is <= j
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi + 1) >> 1;
-                if (pre[wv][mid] <= j) lo = mid;
-                else hi = mid - 1;
-            }
-            uint64_t m = bal[wv][lo];
-            uint32_t r = j - pre[wv][lo], bit = 0;
-            for (uint32_t w = 32; w > 0; w >>= 1) {  // the r-th set bit of m
-                const uint32_t lowc = (uint32_t)__popcll(m & ((1ull << w) - 1ull));
-                if (r >= lowc) {
-                    r -= lowc;
-                    m >>= w;
-                    bit += w;
-                } else {
-                    m &= (1ull << w) - 1ull;
+        if (staged) {  // uniform: the staged hits, OUT_PL a lane at once
+            for (uint32_t j0 = 0; j0 < cnt; j0 += 64 * OUT_PL) {
+                uint2 h[OUT_PL];
+                uint32_t v[OUT_PL];
+                float ls[OUT_PL];
+#pragma unroll
+                for (int r = 0; r < OUT_PL; ++r) {
+                    const uint32_t j = j0 + 64 * r + lane;
+                    h[r] = j < cnt ? stage[wv][j] : make_uint2(0u, 0u);
                 }
+#pragma unroll
+                for (int r = 0; r < OUT_PL; ++r) {
+                    const bool ok = j0 + 64 * r + lane < cnt;
+                    v[r] = IDENT ? h[r].x : ok ? col[b + h[r].x] : 0u;
+                    ls[r] = WITH_LOSS && ok ? loss[b + h[r].x] : 0.0f;
+                }
+#pragma unroll
+                for (int r = 0; r < OUT_PL; ++r)
+                    if (j0 + 64 * r + lane < cnt) put(v[r], h[r].y, ls[r]);
             }
-            place(b + 64ull * lo + bit);
-        }
-        for (uint32_t c = TR_CH; c < nch; ++c) {  // rows past TR_CH chunks: tested again
-            const uint64_t k = b + 64ull * c + lane;
-            const uint64_t l = k < e ? lat[k] : ~0ull;
-            if (l <= wmax_ns && (IDENT ? (uint32_t)(k - b) != u : col[k] != u)) place(k);
+        } else {  // rows of more hits: tested again, chunk by chunk
+            for (uint32_t c = 0; c < nch; ++c) {
+                const uint64_t k = b + 64ull * c + lane;
+                const uint64_t l = k < e ? lat[k] : ~0ull;
+                if (l <= wmax_ns && (IDENT ? (uint32_t)(k - b) != u : col[k] != u))
+                    put(IDENT ? (uint32_t)(k - b) : col[k], units_of(l), WITH_LOSS ? loss[k] : 0.0f);
+            }
         }
     }
     for (int off = 32; off > 0; off >>= 1) {
