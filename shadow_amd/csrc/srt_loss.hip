@@ -281,18 +281,23 @@ __global__ __launch_bounds__(256) void tight_rows_kernel(const K *__restrict__ D
 // ARE u's out-edges), two passes -- pass 1 tests each 64-entry chunk (the
 // latency first; the column is loaded only for the lanes that pass: C3 ~2% of
 // the entries), counts the hits per class by LDS atomics and stages each hit
-// (its place in the row, its weight in units) in LDS at its ballot rank; one
+// (its place in the row, 16 bits, and its weight in units, 16 bits, or a mark
+// that pass 2 reads the latency again) in LDS at its ballot rank; one
 // global atomic takes the row's range, the row's class offsets are written
 // (slot k: start of class k + 1; slot CLS - 1: the row's end), and pass 2
-// deals the staged hits one a lane, OUT_PL a lane at once (their loss / column
-// gathers in flight together), writing each (1f32 - e bits << 32 | v; 0 bits
+// deals the staged hits, OUT_PL a lane at once (their loss / column gathers in
+// flight together), writing each (1f32 - e bits << 32 | v; 0 bits
 // without losses) at its class's running position and counting it for the
-// in-row of (v, class).  A row with more than OUT_SCAP hits is tested again
-// chunk by chunk in pass 2.  No global atomic per entry on the out side, where
+// in-row of (v, class).  A row with more than OUT_SCAP hits, or of more than
+// 65,536 entries, is tested again chunk by chunk in pass 2.  No global atomic per entry on the out side, where
 // a row's ~50 entries of a class would all hit one counter.  Entries past
 // `cap` are counted, not written (the caller sizes and runs again).
-constexpr uint32_t OUT_SCAP = 512;  // hits a wave stages in LDS (C3: ~330 a row)
+constexpr uint32_t OUT_SCAP = 1024;  // hits a wave stages in LDS (C3: ~330 a row at the bound, more in the probes)
 constexpr int OUT_PL = 4;           // staged hits a lane places at once (pass 2)
+#ifndef SRT_OUT_UNR
+#define SRT_OUT_UNR 8
+#endif
+constexpr int OUT_UNR = SRT_OUT_UNR;  // chunks of a row in flight a lane (pass 1)
 template <bool WITH_LOSS, bool IN = true, bool IDENT = false>
 __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t u0, uint32_t V, const uint64_t *__restrict__ row_ptr,
                                                       const uint32_t *__restrict__ col,
@@ -302,7 +307,7 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t u0, uint32_t V, c
                                                       uint32_t *__restrict__ off_out, uint32_t *__restrict__ in_cnt,
                                                       uint64_t *__restrict__ ce_out, uint64_t cap,
                                                       unsigned long long *cursor, unsigned long long *maxw) {
-    __shared__ uint2 stage[4][OUT_SCAP];  // per wave: {place in the row, weight in units} of hit j
+    __shared__ uint32_t stage[4][OUT_SCAP];  // per wave: place in the row | units << 16 (0xffff: read again) of hit j
     __shared__ uint32_t ccnt[4][64];      // per wave: hits per class (pass 1), running positions (pass 2)
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -317,16 +322,15 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t u0, uint32_t V, c
         const uint32_t nch = (uint32_t)((e - b + 63) / 64);
         ccnt[wv][lane] = 0;
         uint32_t cnt = 0;
-        bool wide = false;  // a weight of 2^32 units or more: not staged (the row is tested again)
-        for (uint32_t c0 = 0; c0 < nch; c0 += 4) {
-            uint64_t l[4];
+        for (uint32_t c0 = 0; c0 < nch; c0 += OUT_UNR) {
+            uint64_t l[OUT_UNR];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
+            for (int r = 0; r < OUT_UNR; ++r) {
                 const uint64_t k = b + 64ull * (c0 + r) + lane;
                 l[r] = k < e ? lat[k] : ~0ull;
             }
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
+            for (int r = 0; r < OUT_UNR; ++r) {
                 const uint64_t k = b + 64ull * (c0 + r) + lane;
                 // col only where the latency passes; identity rows (IDENT): the
                 // column is the entry's place in its row
@@ -338,8 +342,7 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t u0, uint32_t V, c
                     atomicAdd(&ccnt[wv][c - 1], 1u);
                     mw = c > mw ? c : mw;
                     const uint32_t j = cnt + (uint32_t)__popcll(m & below);
-                    wide |= (wu >> 32) != 0;
-                    if (j < OUT_SCAP) stage[wv][j] = make_uint2((uint32_t)(k - b), (uint32_t)wu);
+                    if (j < OUT_SCAP) stage[wv][j] = (uint32_t)(k - b) | (wu < 0xffffu ? (uint32_t)wu : 0xffffu) << 16;
                 }
                 cnt += (uint32_t)__popcll(m);
             }
@@ -359,7 +362,7 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t u0, uint32_t V, c
         if (lane < cls) off_out[(uint64_t)u * cls + lane] = fits ? (lane == cls - 1 ? (uint32_t)(base + cnt) : start) : 0u;
         ccnt[wv][lane] = start;  // running positions
         if (!cnt || !fits) continue;  // uniform
-        const bool staged = cnt <= OUT_SCAP && !__any(wide);
+        const bool staged = cnt <= OUT_SCAP && e - b <= 65536;
         auto put = [&](uint32_t v, uint64_t wu, float ls) {
             const uint32_t cl = cls_of_units(wu);
             const uint32_t pos = atomicAdd(&ccnt[wv][cl - 1], 1u);
@@ -372,23 +375,26 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t u0, uint32_t V, c
         };
         if (staged) {  // uniform: the staged hits, OUT_PL a lane at once
             for (uint32_t j0 = 0; j0 < cnt; j0 += 64 * OUT_PL) {
-                uint2 h[OUT_PL];
-                uint32_t v[OUT_PL];
+                uint32_t o[OUT_PL], v[OUT_PL];
+                uint64_t wu[OUT_PL];
                 float ls[OUT_PL];
 #pragma unroll
                 for (int r = 0; r < OUT_PL; ++r) {
                     const uint32_t j = j0 + 64 * r + lane;
-                    h[r] = j < cnt ? stage[wv][j] : make_uint2(0u, 0u);
+                    const uint32_t h = j < cnt ? stage[wv][j] : 0u;
+                    o[r] = h & 0xffffu;
+                    wu[r] = h >> 16;
                 }
 #pragma unroll
                 for (int r = 0; r < OUT_PL; ++r) {
                     const bool ok = j0 + 64 * r + lane < cnt;
-                    v[r] = IDENT ? h[r].x : ok ? col[b + h[r].x] : 0u;
-                    ls[r] = WITH_LOSS && ok ? loss[b + h[r].x] : 0.0f;
+                    v[r] = IDENT ? o[r] : ok ? col[b + o[r]] : 0u;
+                    ls[r] = WITH_LOSS && ok ? loss[b + o[r]] : 0.0f;
+                    if (ok && wu[r] == 0xffffu) wu[r] = units_of(lat[b + o[r]]);  // wide weights
                 }
 #pragma unroll
                 for (int r = 0; r < OUT_PL; ++r)
-                    if (j0 + 64 * r + lane < cnt) put(v[r], h[r].y, ls[r]);
+                    if (j0 + 64 * r + lane < cnt) put(v[r], wu[r], ls[r]);
             }
         } else {  // rows of more hits: tested again, chunk by chunk
             for (uint32_t c = 0; c < nch; ++c) {
