@@ -447,6 +447,23 @@ def test_level_symmetric_rows(monkeypatch, ns):
         _check(c.fetch(), O.Graph(True, np.arange(n), src, dst, lat2, loss), nodes)
     finally:
         c.close()
+    # mirrored latencies, one short edge's loss differing from its mirror's:
+    # the symmetry check compares the losses beside short latencies too
+    loss3 = loss.copy().reshape(n, n)
+    row = lat.reshape(n, n)[7].copy()
+    row[7] = np.iinfo(np.uint64).max
+    v = int(np.argmin(row))
+    loss3[7, v] = np.float32(0.5) if loss3[7, v] != np.float32(0.5) else np.float32(0.25)
+    loss3 = loss3.reshape(-1)
+    g3 = NetworkGraph(n, np.arange(n, dtype=np.uint32), row_ptr, col, lat, loss3, directed=True)
+    d = RoutingPlan(g3, nodes, algo=_lib.SRT_ALGO_LEVEL, device=0).run()
+    try:
+        assert "rows=sym" not in d.describe(), d.describe()
+        src = np.repeat(np.arange(n, dtype=np.uint32), n)
+        dst = np.tile(np.arange(n, dtype=np.uint32), n)
+        _check(d.fetch(), O.Graph(True, np.arange(n), src, dst, lat, loss3), nodes)
+    finally:
+        d.close()
 
 
 def _complete_identity(n, seed):
