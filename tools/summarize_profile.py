@@ -76,16 +76,24 @@ def short(name):
 
 
 def pmc(path, counter):
+    """Counter KB summed per kernel and launch grid: one instantiation may run
+    at several grids (the level family's create-time probes launch the build's
+    solve kernel over a few sources), and the build's launches are the ones a
+    bench line quotes.  The largest grid keeps the kernel's name; the others
+    are keyed '<name> [grid N]'."""
     per = collections.defaultdict(float)
     disp = collections.defaultdict(set)
     for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
-            k = short(r["Kernel_Name"])
+            k = (short(r["Kernel_Name"]), int(r.get("Grid_Size") or 0))
             per[k] += float(r["Counter_Value"])
             disp[k].add(r["Dispatch_Id"])
-    return {k: (v, len(disp[k])) for k, v in per.items()}
+    top = collections.defaultdict(int)
+    for (k, g) in per:
+        top[k] = max(top[k], g)
+    return {(k if g == top[k] else f"{k} [grid {g}]"): (v, len(disp[(k, g)])) for (k, g), v in per.items()}
 
 
 def main():
@@ -114,7 +122,8 @@ def main():
     doc = {"round": tag, "config": config, "launches": launches,
            "schedule": json.loads(sys.argv[4]) if len(sys.argv) > 4 else None,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (MI355X_MICROARCH.md "
-                     "HBM section), KB per dispatch averaged over the dispatches of each kernel. "
+                     "HBM section), KB per dispatch averaged over the dispatches of each kernel and launch grid (the "
+                     "largest grid under the kernel's name, others as '[grid N]'). "
                      "hbm_bytes_per_launch = fetch_correction x FETCH_SIZE + WRITE_SIZE: x2 for the u32 tile "
                      "kernel (16-B/lane C-tile and LDS-DMA panel reads, the guide's gfx950 correction); 1 "
                      "elsewhere (raw counter: the f64 tile kernels' 8-B/lane C loads calibrated 1:1 in r01, "
