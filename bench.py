@@ -208,8 +208,10 @@ def packet_traffic():
         d = json.load(open(f))
         if not d.get("config", "").startswith("C5 "):
             continue
-        tot = sum(v["hbm_bytes_per_launch"] for k, v in d.get("kernels", {}).items()
-                  if k.startswith(("round_kernel", "stats_kernel")))
+        ks = d.get("kernels", {})
+        if not any(k.startswith("round_kernel") for k in ks):  # an older kernel shape (draw + decide)
+            continue
+        tot = sum(v["hbm_bytes_per_launch"] for k, v in ks.items() if k.startswith(("round_kernel", "stats_kernel")))
         if tot:
             return tot, os.path.relpath(f, ROOT)
     return None, None
