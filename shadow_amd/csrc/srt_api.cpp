@@ -550,6 +550,7 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_row_ptr);
     hipFree(p->d_col);
     hipFree(p->d_lat);
+    hipFree(p->d_lat16);
     hipFree(p->d_loss);
     hipFree(p->d_nodes);
     hipFree(p->d_D);
@@ -1184,6 +1185,8 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
     } else {
         p->lvl_q = 0;
         p->lvl_sym = p->lvl_sym_lat = false;
+        (void)hipFree(p->d_lat16);
+        p->d_lat16 = nullptr;
         // the level probe's class CSRs (sized for it): freed before the
         // closure families size anything by the free HBM; their own runs grow
         // these arrays again from zero
@@ -1207,11 +1210,11 @@ srt_status plan_create_impl(const srt_csr *g, const uint32_t *nodes, uint32_t n,
         if (p->lvl_q)
             std::snprintf(d, sizeof d, "level:u32 g=%llu q=%u lmax=%llu(probe) V=%u n=%u visits=%llu loss=in-solve%s",
                           (unsigned long long)p->kp.g, p->lvl_q, (unsigned long long)p->kp.lmax, p->V, n,
-                          (unsigned long long)lvl_visits, p->lvl_sym ? " rows=sym" : "");
+                          (unsigned long long)lvl_visits, p->lvl_sym ? (p->d_lat16 ? " rows=sym lat16" : " rows=sym") : "");
         else
             std::snprintf(d, sizeof d, "level:u16 g=%llu lmax=%llu(probe) V=%u n=%u visits=%llu loss=in-solve%s",
                           (unsigned long long)p->kp.g, (unsigned long long)p->kp.lmax, p->V, n,
-                          (unsigned long long)lvl_visits, p->lvl_sym ? " rows=sym" : "");
+                          (unsigned long long)lvl_visits, p->lvl_sym ? (p->d_lat16 ? " rows=sym lat16" : " rows=sym") : "");
     } else if (algo == SRT_ALGO_FW) {
         p->fw_f16 = f16 && p->fw_glds;
         if (const char *e = std::getenv("SRT_FW_P1")) p->fw_p1 = std::atoi(e);

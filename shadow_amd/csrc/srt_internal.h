@@ -342,6 +342,7 @@ struct srt_plan {
     uint64_t lvl_cap = 0;            // level solve: class entries d_tpk / d_tpk2 hold (the probe's count)
     bool lvl_sym_lat = false;        // level solve: identity rows, mirrored latencies (lvl_sym_tile_kernel)
     bool lvl_sym = false;            // ... and mirrored losses: the class in-rows are the out-rows
+    uint16_t *d_lat16 = nullptr;     // symmetric level plans: the adjacency's latencies in units of g (< 0xffff), written by the symmetry check
     bool lvl_single = false;         // the last class-CSR build made out-rows only (in-rows = out-rows)
     uint64_t lvl_est = 0;            // the probe's entry-count estimate (sizes the arrays before its one pass)
     uint64_t lvl_maxu = 0;           // the longest edge, units of g (the estimate's scale)

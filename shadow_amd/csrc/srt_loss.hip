@@ -298,7 +298,8 @@ constexpr int OUT_PL = 4;           // staged hits a lane places at once (pass 2
 #define SRT_OUT_UNR 8
 #endif
 constexpr int OUT_UNR = SRT_OUT_UNR;  // chunks of a row in flight a lane (pass 1)
-template <bool WITH_LOSS, bool IN = true, bool IDENT = false>
+constexpr int OUT_UNR16 = 8;          // ... of the u16 copy: 256-entry chunks (8 B a lane)
+template <bool WITH_LOSS, bool IN = true, bool IDENT = false, bool L16 = false>
 __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t u0, uint32_t V, const uint64_t *__restrict__ row_ptr,
                                                       const uint32_t *__restrict__ col,
                                                       const uint64_t *__restrict__ lat, const float *__restrict__ loss,
@@ -306,7 +307,9 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t u0, uint32_t V, c
                                                       uint32_t q, uint32_t vb,
                                                       uint32_t *__restrict__ off_out, uint32_t *__restrict__ in_cnt,
                                                       uint64_t *__restrict__ ce_out, uint64_t cap,
-                                                      unsigned long long *cursor, unsigned long long *maxw) {
+                                                      unsigned long long *cursor, unsigned long long *maxw,
+                                                      const uint16_t *__restrict__ lat16 = nullptr) {
+    static_assert(!L16 || (IDENT && !IN), "the u16 copy: identity rows of symmetric plans");
     __shared__ uint32_t stage[4][OUT_SCAP];  // per wave: place in the row | units << 16 (0xffff: read again) of hit j
     __shared__ uint32_t ccnt[4][64];      // per wave: hits per class (pass 1), running positions (pass 2)
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -322,7 +325,38 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t u0, uint32_t V, c
         const uint32_t nch = (uint32_t)((e - b + 63) / 64);
         ccnt[wv][lane] = 0;
         uint32_t cnt = 0;
-        for (uint32_t c0 = 0; c0 < nch; c0 += OUT_UNR) {
+        const uint32_t wmax_u = (uint32_t)(wmax_ns / g);  // L16: the bound in units (wmax_ns = wmax_u g, < 0xffff)
+        if (L16) {  // u16 units, 4 a lane a 256-entry chunk (identity rows of V % 4 == 0 entries)
+            const uint2 *row = reinterpret_cast<const uint2 *>(lat16 + b);
+            const uint32_t len = (uint32_t)(e - b), nq = (len + 255) / 256;
+            for (uint32_t c0 = 0; c0 < nq; c0 += OUT_UNR16) {
+                uint2 x[OUT_UNR16];
+#pragma unroll
+                for (int r = 0; r < OUT_UNR16; ++r) {
+                    const uint32_t o = 256 * (c0 + r) + 4 * lane;
+                    x[r] = o < len ? row[64 * (c0 + r) + lane] : make_uint2(~0u, ~0u);
+                }
+#pragma unroll
+                for (int r = 0; r < OUT_UNR16; ++r) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const uint32_t w = ((i < 2 ? x[r].x : x[r].y) >> (16 * (i & 1))) & 0xffffu;
+                        const uint32_t o = 256 * (c0 + r) + 4 * lane + i;
+                        const bool f = w <= wmax_u && o != u;
+                        const uint64_t m = __ballot(f);
+                        if (f) {
+                            const uint32_t c = cls_of_units(w);
+                            atomicAdd(&ccnt[wv][c - 1], 1u);
+                            mw = c > mw ? c : mw;
+                            const uint32_t j = cnt + (uint32_t)__popcll(m & below);
+                            if (j < OUT_SCAP) stage[wv][j] = o | w << 16;
+                        }
+                        cnt += (uint32_t)__popcll(m);
+                    }
+                }
+            }
+        }
+        for (uint32_t c0 = 0; c0 < (L16 ? 0u : nch); c0 += OUT_UNR) {
             uint64_t l[OUT_UNR];
 #pragma unroll
             for (int r = 0; r < OUT_UNR; ++r) {
@@ -396,6 +430,11 @@ __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t u0, uint32_t V, c
                 for (int r = 0; r < OUT_PL; ++r)
                     if (j0 + 64 * r + lane < cnt) put(v[r], wu[r], ls[r]);
             }
+        } else if (L16) {  // rows of more hits: tested again
+            for (uint64_t k = b + lane; k < e; k += 64) {
+                const uint32_t w = lat16[k];
+                if (w <= wmax_u && (uint32_t)(k - b) != u) put((uint32_t)(k - b), w, WITH_LOSS ? loss[k] : 0.0f);
+            }
         } else {  // rows of more hits: tested again, chunk by chunk
             for (uint32_t c = 0; c < nch; ++c) {
                 const uint64_t k = b + 64ull * c + lane;
@@ -439,6 +478,13 @@ __global__ __launch_bounds__(256) void lvl_in_kernel(uint32_t V, uint32_t cls, u
     }
 }
 
+// a latency in units of g for the u16 adjacency copy (exact: g divides every
+// edge latency; 0xffff: longer than any class bound)
+__device__ __forceinline__ uint16_t units16(uint64_t l, double inv_g) {
+    const uint64_t u = (uint64_t)((double)l * inv_g + 0.5);
+    return (uint16_t)(u < 0xffffu ? u : 0xffffu);
+}
+
 // Exact check that a level plan's class in-rows equal its out-rows, so the
 // run builds only the out-rows (lvl_sym): the adjacency is V identity rows
 // (proved by the host scan, CsrStats::ident: entry (u, v) at u * V + v) and
@@ -451,7 +497,7 @@ __global__ __launch_bounds__(256) void lvl_in_kernel(uint32_t V, uint32_t cls, u
 // clears *ok.
 __global__ __launch_bounds__(256) void lvl_sym_tile_kernel(uint32_t V, const uint64_t *__restrict__ lat,
                                                            const float *__restrict__ loss, uint64_t wmax_ns,
-                                                           uint32_t *ok) {
+                                                           uint32_t *ok, uint16_t *__restrict__ lat16, double inv_g) {
     __shared__ uint64_t tl[64][65];
     __shared__ uint32_t tp[64][65];
     const uint32_t nb = (V + 63) / 64, tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
@@ -483,6 +529,13 @@ __global__ __launch_bounds__(256) void lvl_sym_tile_kernel(uint32_t V, const uin
             tl[ty + 4 * i][tx] = la[i];
             tp[ty + 4 * i][tx] = pa[i];
         }
+        if (lat16) {  // the u16-unit copy of the adjacency (every tile: the triangle's and its mirror's)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const uint32_t u = bj * 64 + ty + 4 * i;
+                if (u < V && v_a < V) lat16[(uint64_t)u * V + v_a] = units16(la[i], inv_g);
+            }
+        }
         __syncthreads();
         const uint32_t v_b = bj * 64 + tx;  // compared tile (bi, bj)
 #pragma unroll
@@ -492,6 +545,13 @@ __global__ __launch_bounds__(256) void lvl_sym_tile_kernel(uint32_t V, const uin
             const uint64_t k = (uint64_t)u * V + v_b;
             la[i] = in ? lat[k] : 0ull;
             pa[i] = in && loss ? __float_as_uint(loss[k]) : 0u;
+        }
+        if (lat16 && bi != bj) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const uint32_t u = bi * 64 + ty + 4 * i;
+                if (u < V && v_b < V) lat16[(uint64_t)u * V + v_b] = units16(la[i], inv_g);
+            }
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -3190,7 +3250,17 @@ srt_status level_csr(srt_plan *p, uint64_t wmax, bool with_loss, srt_err *err) {
         (void)hipMemsetAsync(p->d_tccnt, 0, 2 * vc1 * 4, M);  // in-row counts, then in-row cursors
         (void)hipMemsetAsync(p->d_tcursor, 0, sizeof(unsigned long long), M);
         (void)hipMemsetAsync(p->d_tmaxw, 0, sizeof(unsigned long long), M);
-        if (single && with_loss)  // symmetric plans have identity rows (lvl_sym_tile_kernel)
+        if (single && p->d_lat16 && with_loss)  // the u16-unit copy (symmetry check; wmax < 0xffff units)
+            hipLaunchKernelGGL((lvl_out_kernel<true, false, true, true>), dim3(blocks), dim3(256), 0, M, 0u, V,
+                               p->d_row_ptr, p->d_col, p->d_lat, p->d_loss, p->kp.g, inv_g, wns, cls, q, vb, p->d_tcls,
+                               p->d_tccnt, p->d_tpk, p->lvl_cap, p->d_tcursor, (unsigned long long *)p->d_tmaxw,
+                               p->d_lat16);
+        else if (single && p->d_lat16)
+            hipLaunchKernelGGL((lvl_out_kernel<false, false, true, true>), dim3(blocks), dim3(256), 0, M, 0u, V,
+                               p->d_row_ptr, p->d_col, p->d_lat, (const float *)nullptr, p->kp.g, inv_g, wns, cls, q, vb,
+                               p->d_tcls, p->d_tccnt, p->d_tpk, p->lvl_cap, p->d_tcursor,
+                               (unsigned long long *)p->d_tmaxw, p->d_lat16);
+        else if (single && with_loss)  // symmetric plans have identity rows (lvl_sym_tile_kernel)
             hipLaunchKernelGGL((lvl_out_kernel<true, false, true>), dim3(blocks), dim3(256), 0, M, 0u, V, p->d_row_ptr,
                                p->d_col, p->d_lat, p->d_loss, p->kp.g, inv_g, wns, cls, q, vb, p->d_tcls, p->d_tccnt,
                                p->d_tpk, p->lvl_cap, p->d_tcursor, (unsigned long long *)p->d_tmaxw);
@@ -3674,10 +3744,25 @@ srt_status level_sym_check(srt_plan *p, uint64_t wmax_units, bool with_loss, boo
     uint32_t one = 1;
     e = hipMemcpyAsync(d_ok, &one, 4, hipMemcpyHostToDevice, p->stream);
     const uint64_t nb = (p->V + 63) / 64;
+    // every latency below 0xffff units and rows of a multiple of 4 entries: the
+    // check also writes the adjacency's u16-unit copy, which the class-CSR
+    // passes stream instead of the u64 latencies (a quarter of the bytes; C3
+    // 16k: out-rows 538 -> 309 us a build, the check 542 -> 854 us once).  From
+    // 8,192 vertices: at C2's 4k it measured 0.01-0.02 ms slower a build
+    const char *k16 = std::getenv("SRT_LAT16");  // knob: 0 = never, 1 = at any size (A/B, tests)
+    const int kv16 = k16 ? std::atoi(k16) : -1;
+    const bool want16 = wmax_units < 0xffff && p->V % 4 == 0 && kv16 != 0 && (kv16 == 1 || p->V >= 8192);
+    (void)hipFree(p->d_lat16);
+    p->d_lat16 = nullptr;
+    if (e == hipSuccess && want16 && hipMalloc(&p->d_lat16, p->n_adj * 2) != hipSuccess) {
+        (void)hipGetLastError();
+        p->d_lat16 = nullptr;  // no room: the u64 latencies are streamed
+    }
     cspan_begin(p);
     if (e == hipSuccess)
         hipLaunchKernelGGL(lvl_sym_tile_kernel, dim3((uint32_t)std::min<uint64_t>(nb * (nb + 1) / 2, 8192)), dim3(256),
-                           0, p->stream, p->V, p->d_lat, with_loss ? p->d_loss : nullptr, wmax_units * p->kp.g, d_ok);
+                           0, p->stream, p->V, p->d_lat, with_loss ? p->d_loss : nullptr, wmax_units * p->kp.g, d_ok,
+                           p->d_lat16, 1.0 / (double)p->kp.g);
     cspan_end(p);
     uint32_t ok = 0;
     if (e == hipSuccess) e = hipMemcpyAsync(&ok, d_ok, 4, hipMemcpyDeviceToHost, p->stream);
@@ -3685,6 +3770,10 @@ srt_status level_sym_check(srt_plan *p, uint64_t wmax_units, bool with_loss, boo
     (void)hipFree(d_ok);
     if (e != hipSuccess) return fail(err, e, "symmetry check");
     *sym = ok != 0;
+    if (!*sym) {  // only symmetric plans' out-rows read it
+        (void)hipFree(p->d_lat16);
+        p->d_lat16 = nullptr;
+    }
     return SRT_OK;
 }
 

@@ -101,6 +101,7 @@ def test_c3_16k_rows_vs_oracle_and_symmetry():
     nodes = np.arange(n, dtype=np.uint32)
     plan = RoutingPlan(g, nodes).run()
     assert plan.describe().startswith("level:u16"), plan.describe()  # AUTO: the level solve is priced cheapest
+    assert "rows=sym lat16" in plan.describe(), plan.describe()  # the class out-rows from the u16-unit copy
     plan.fetch(table=False)  # every pair reachable (else DISCONNECTED), min latency
     L, P = _device_table(plan)
     assert torch.equal(L, L.t()), "undirected latency table must be symmetric"

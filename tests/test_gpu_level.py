@@ -429,6 +429,17 @@ def test_level_symmetric_rows(monkeypatch, ns):
         lb, pb, _ = b.table_ptrs()
         assert torch.equal(t(la, n * n * 8), t(lb, n * n * 8)) and torch.equal(t(pa, n * n * 4), t(pb, n * n * 4))
         _check(a.fetch(), O.Graph(False, np.arange(n), *edges), nodes)
+        # the class out-rows streamed from the u16-unit adjacency copy (on by
+        # default from 8,192 vertices; forced here): the same tables bit for bit
+        monkeypatch.setenv("SRT_LAT16", "1")
+        c16 = RoutingPlan(g, nodes, algo=_lib.SRT_ALGO_LEVEL, device=0).run()
+        monkeypatch.delenv("SRT_LAT16")
+        try:
+            assert ("lat16" in c16.describe()) == (not ns) and "lat16" not in a.describe(), (c16.describe(), a.describe())
+            lc, pc, _ = c16.table_ptrs()
+            assert torch.equal(t(la, n * n * 8), t(lc, n * n * 8)) and torch.equal(t(pa, n * n * 4), t(pc, n * n * 4))
+        finally:
+            c16.close()
     finally:
         a.close()
         b.close()
