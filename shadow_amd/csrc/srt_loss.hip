@@ -529,14 +529,20 @@ __global__ __launch_bounds__(256) void lvl_sym_tile_kernel(uint32_t V, const uin
             tl[ty + 4 * i][tx] = la[i];
             tp[ty + 4 * i][tx] = pa[i];
         }
-        if (lat16) {  // the u16-unit copy of the adjacency (every tile: the triangle's and its mirror's)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const uint32_t u = bj * 64 + ty + 4 * i;
-                if (u < V && v_a < V) lat16[(uint64_t)u * V + v_a] = units16(la[i], inv_g);
-            }
-        }
         __syncthreads();
+        // the u16-unit copy of the adjacency (V % 4 == 0): every tile, the
+        // triangle's and its mirror's, out of the LDS tile 4 entries (8 B) a store
+        auto put16 = [&](uint32_t r0, uint32_t c0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t gi = threadIdx.x + 256 * i, r = gi >> 4, c = (gi & 15) * 4;
+                if (r0 + r < V && c0 + c < V) {
+                    const uint32_t lo = units16(tl[r][c], inv_g) | (uint32_t)units16(tl[r][c + 1], inv_g) << 16;
+                    const uint32_t hi = units16(tl[r][c + 2], inv_g) | (uint32_t)units16(tl[r][c + 3], inv_g) << 16;
+                    *reinterpret_cast<uint2 *>(lat16 + (uint64_t)(r0 + r) * V + c0 + c) = make_uint2(lo, hi);
+                }
+            }
+        };
         const uint32_t v_b = bj * 64 + tx;  // compared tile (bi, bj)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -546,13 +552,7 @@ __global__ __launch_bounds__(256) void lvl_sym_tile_kernel(uint32_t V, const uin
             la[i] = in ? lat[k] : 0ull;
             pa[i] = in && loss ? __float_as_uint(loss[k]) : 0u;
         }
-        if (lat16 && bi != bj) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const uint32_t u = bi * 64 + ty + 4 * i;
-                if (u < V && v_b < V) lat16[(uint64_t)u * V + v_b] = units16(la[i], inv_g);
-            }
-        }
+        if (lat16) put16(bj * 64, bi * 64);  // the staged tile's, behind the compared tile's loads
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             const uint32_t r = ty + 4 * i, u = bi * 64 + r;
@@ -562,6 +562,13 @@ __global__ __launch_bounds__(256) void lvl_sym_tile_kernel(uint32_t V, const uin
             }
         }
         __syncthreads();
+        if (lat16 && bi != bj) {  // the compared tile through the same LDS tile
+#pragma unroll
+            for (int i = 0; i < 16; ++i) tl[ty + 4 * i][tx] = la[i];
+            __syncthreads();
+            put16(bi * 64, bj * 64);
+            __syncthreads();
+        }
     }
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicAnd(ok, 0u);
 }
