@@ -181,6 +181,25 @@ def test_c4_graph_row_sample():
         assert np.array_equal(_bits(t.packet_loss[r]), _bits(ep))
 
 
+@pytest.mark.parametrize("seed", [31, 32])
+def test_loss_sweeps_over_reused_rows(monkeypatch, sweep_mode, seed):
+    """The frontier loss sweeps' same-sweep reads: a reader can see a parent's
+    change bit before that parent's P store lands (or a stale line in its own
+    L1).  Correct because every P value a reader can see for (s, v) within a
+    launch is >= the final one -- the tight pass stores 2.0 ("not reached"),
+    then only improvements follow -- so a stale read delays a fold to the next
+    sweep and never corrupts it.  Here one 512-source block a launch, so every
+    launch reuses the P rows the previous launch left (without the 2.0 start a
+    stale read returns another source's loss: the r05 failure that
+    test_c4_graph_row_sample caught at C4 scale), over tie-heavy latencies
+    (many tight in-edges, many loss sweeps); every row against the oracle."""
+    if sweep_mode.startswith("frontier"):
+        monkeypatch.setenv("SRT_SSSP_FR_NB", "1")
+    n = 2500
+    e = synth.barabasi_albert(n, 4, seed, lat_ms=(1, 6), loss_max=0.05)
+    _check(e, np.arange(n, dtype=np.uint32), False, n)
+
+
 def test_fw_and_sssp_agree_on_latency():
     # the dense closure + exact-loss pass and the sparse sweep on one graph: same bits
     n = 300
