@@ -55,6 +55,7 @@ RELAX_BASIS = {"f16": "2 v_pk_add_f16 + 1 v_pk_minimum3_f16 per 4 relaxations (2
                "u32": "2 v_add_u32 (issued at twice the rate) + 1 v_min3_u32 per 2 relaxations = 1 VALU slot",
                "f64": "v_add_f64 + v_min_f64 = 2 VALU slots", "u64": "v_lshl_add_u64 + v_cmp + 2 v_cndmask = 4 slots"}
 HBM_PEAK = 8.0e12  # B/s
+MALL_GATHER_PEAK = 8.6e12  # B/s: random rows of a 38 MB table, Infinity Cache (MI355X_MICROARCH.md)
 
 CONFIGS = {
     "c1": dict(kind="gml", nodes=1000, seed=1),
@@ -685,7 +686,16 @@ def bench_graph(args, cfg, D):
                 "basis": "12 B per table pair written (u64 latency + f32 loss) + 8 B per class-CSR entry the rows "
                          "walk (counted by the kernel; the class CSRs exceed the 4 MB L2 of an XCD)",
                 "edge_visits_per_row": visits,
-                "edge_visits_per_s": visits_launch / avg_launch_s}
+                "edge_visits_per_s": visits_launch / avg_launch_s,
+                # the class entries are gathered from beyond L2 (Infinity Cache): the guide's measured
+                # random-row rate from a table of that size is the second ceiling; the table write alone
+                # is the floor every build pays
+                "second_peak": {"what": "Infinity Cache random-row gather (MI355X_MICROARCH.md 'Indexed rows: "
+                                        "gather into LDS', 38 MB table: 8.6 TB/s chip-wide; C3's class CSR is 43 MB)",
+                                "peak": MALL_GATHER_PEAK / 1e9, "unit": "GB/s", "frac": achieved / MALL_GATHER_PEAK},
+                "write_floor": {"bytes_per_launch": work_per_launch * 12,
+                                "frac_of_hbm": work_per_launch * 12 / avg_launch_s / HBM_PEAK,
+                                "what": "the 12-B table pairs alone over the launch time"}}
             algo = (f"level solve: per-source bucket (Dial) Dijkstra over the edges <= {lmax} units (a bound proved "
                     f"by probe rows), loss folded in the same pass"
                     + (f"; quantized buckets of {sh} units (the shortest edge)" if sh else ""))

@@ -137,9 +137,14 @@ def main():
         disp = collections.defaultdict(set)
         for f in glob.glob(os.path.join(sq_dir, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
-                k = short(r["Kernel_Name"])
+                k = (short(r["Kernel_Name"]), int(r.get("Grid_Size") or 0))
                 per[k][r["Counter_Name"]] += float(r["Counter_Value"])
                 disp[k].add(r["Dispatch_Id"])
+        top = collections.defaultdict(int)
+        for (k, g) in per:
+            top[k] = max(top[k], g)
+        per = {(k if g == top[k] else f"{k} [grid {g}]"): v for (k, g), v in per.items()}
+        disp = {(k if g == top[k] else f"{k} [grid {g}]"): v for (k, g), v in disp.items()}
         sq = {}
         for k, c in per.items():
             n = max(len(disp[k]), 1)
