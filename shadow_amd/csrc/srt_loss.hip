@@ -3254,7 +3254,8 @@ srt_status level_csr(srt_plan *p, uint64_t wmax, bool with_loss, srt_err *err) {
     const bool single = with_loss ? p->lvl_sym : p->lvl_sym_lat;
     p->lvl_single = single;
     auto out_pass = [&]() {
-        (void)hipMemsetAsync(p->d_tccnt, 0, 2 * vc1 * 4, M);  // in-row counts, then in-row cursors
+        if (!single)  // in-row counts, then in-row cursors (out-rows-only plans count none)
+            (void)hipMemsetAsync(p->d_tccnt, 0, 2 * vc1 * 4, M);
         (void)hipMemsetAsync(p->d_tcursor, 0, sizeof(unsigned long long), M);
         (void)hipMemsetAsync(p->d_tmaxw, 0, sizeof(unsigned long long), M);
         if (single && p->d_lat16 && with_loss)  // the u16-unit copy (symmetry check; wmax < 0xffff units)
