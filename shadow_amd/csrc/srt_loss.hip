@@ -293,12 +293,18 @@ __global__ __launch_bounds__(256) void tight_rows_kernel(const K *__restrict__ D
 // a row's ~50 entries of a class would all hit one counter.  Entries past
 // `cap` are counted, not written (the caller sizes and runs again).
 constexpr uint32_t OUT_SCAP = 1024;  // hits a wave stages in LDS (C3: ~330 a row at the bound, more in the probes)
-constexpr int OUT_PL = 4;           // staged hits a lane places at once (pass 2)
+#ifndef SRT_OUT_PL
+#define SRT_OUT_PL 4
+#endif
+constexpr int OUT_PL = SRT_OUT_PL;  // staged hits a lane places at once (pass 2)
 #ifndef SRT_OUT_UNR
 #define SRT_OUT_UNR 8
 #endif
 constexpr int OUT_UNR = SRT_OUT_UNR;  // chunks of a row in flight a lane (pass 1)
-constexpr int OUT_UNR16 = 8;          // ... of the u16 copy: 256-entry chunks (8 B a lane)
+#ifndef SRT_OUT_UNR16
+#define SRT_OUT_UNR16 8
+#endif
+constexpr int OUT_UNR16 = SRT_OUT_UNR16;  // ... of the u16 copy: 256-entry chunks (8 B a lane)
 template <bool WITH_LOSS, bool IN = true, bool IDENT = false, bool L16 = false>
 __global__ __launch_bounds__(256) void lvl_out_kernel(uint32_t u0, uint32_t V, const uint64_t *__restrict__ row_ptr,
                                                       const uint32_t *__restrict__ col,
