@@ -2495,6 +2495,18 @@ __global__ void loss_stats_init_kernel(unsigned long long *stats, unsigned long 
     *maxw = 0ull;
 }
 
+// the level build's per-run counters in one launch (small memsets are a
+// ~4.6 us fill kernel each on the device timeline): stats, the class max,
+// the visit count; or (stats == nullptr) the class-CSR pass's cursor and max
+__global__ void level_zero_kernel(unsigned long long *stats, unsigned long long *a, unsigned long long *b) {
+    if (stats) {
+        stats[0] = ~0ull;
+        stats[1] = 0ull;
+    }
+    if (a) *a = 0ull;
+    if (b) *b = 0ull;
+}
+
 srt_status fail(srt_err *err, hipError_t e, const char *what) {
     const srt_status st = e == hipErrorOutOfMemory ? SRT_ERR_OOM : SRT_ERR_HIP;
     if (err) {
@@ -3262,8 +3274,8 @@ srt_status level_csr(srt_plan *p, uint64_t wmax, bool with_loss, srt_err *err) {
     auto out_pass = [&]() {
         if (!single)  // in-row counts, then in-row cursors (out-rows-only plans count none)
             (void)hipMemsetAsync(p->d_tccnt, 0, 2 * vc1 * 4, M);
-        (void)hipMemsetAsync(p->d_tcursor, 0, sizeof(unsigned long long), M);
-        (void)hipMemsetAsync(p->d_tmaxw, 0, sizeof(unsigned long long), M);
+        hipLaunchKernelGGL(level_zero_kernel, dim3(1), dim3(1), 0, M, (unsigned long long *)nullptr,
+                           (unsigned long long *)p->d_tcursor, (unsigned long long *)p->d_tmaxw);
         if (single && p->d_lat16 && with_loss)  // the u16-unit copy (symmetry check; wmax < 0xffff units)
             hipLaunchKernelGGL((lvl_out_kernel<true, false, true, true>), dim3(blocks), dim3(256), 0, M, 0u, V,
                                p->d_row_ptr, p->d_col, p->d_lat, p->d_loss, p->kp.g, inv_g, wns, cls, q, vb, p->d_tcls,
@@ -3835,13 +3847,12 @@ srt_status level_run(srt_plan *p, unsigned long long *d_stats, srt_err *err) {
     else
         st = level_csr(p, p->kp.lmax, true, err);
     if (st != SRT_OK) return st;
-    hipLaunchKernelGGL(loss_stats_init_kernel, dim3(1), dim3(1), 0, p->stream, d_stats,
-                       (unsigned long long *)p->d_tmaxw);
     if (!p->d_lvisit) {
         const hipError_t e = hipMalloc(&p->d_lvisit, sizeof(unsigned long long));
         if (e != hipSuccess) return fail(err, e, "hipMalloc(visit counter)");
     }
-    (void)hipMemsetAsync(p->d_lvisit, 0, sizeof(unsigned long long), p->stream);
+    hipLaunchKernelGGL(level_zero_kernel, dim3(1), dim3(1), 0, p->stream, d_stats, (unsigned long long *)p->d_tmaxw,
+                       p->d_lvisit);
 #if LOSS_COUNT
     {
         const uint32_t dg = std::getenv("SRT_LVL_DIAG") ? (uint32_t)std::atoi(std::getenv("SRT_LVL_DIAG")) : 0u;
