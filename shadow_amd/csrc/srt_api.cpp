@@ -551,6 +551,7 @@ void free_plan_buffers(srt_plan *p) {
     hipFree(p->d_col);
     hipFree(p->d_lat);
     hipFree(p->d_lat16);
+    hipFree(p->d_rowctr);
     hipFree(p->d_loss);
     hipFree(p->d_nodes);
     hipFree(p->d_D);
@@ -2467,6 +2468,7 @@ srt_status build_multi_level(srt_plan *p0, const std::vector<int32_t> &devs, srt
         srt::LevelCtx c = c0;
         c.device = devs[r];
         c.visits = nullptr;
+        c.row_ctr = nullptr;  // ranks solve concurrently: rows dealt statically
         if (e == hipSuccess) e = r == 0 ? hipSuccess : hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
         if (r == 0) st = p0->stream;
         c.stream = st;

@@ -356,6 +356,7 @@ struct srt_plan {
     unsigned long long *d_lvl_counts = nullptr;  // W per-rank entry counts (sizing)
     uint32_t lvl_emu_ranks = 0;      // measurement (srt_plan_shard_rows + SRT_LVL_SHARD_EMU=1): rank row0's slice
     bool lvl_emu_built = false;      // ... every slice built once (the first run); later runs rebuild the own one
+    unsigned long long *d_rowctr = nullptr;  // level solve: the rows dealt by a counter (LevelCtx::row_ctr)
     unsigned long long *d_lvisit = nullptr;  // level solve: class entries the last run walked
     uint32_t lvl_q = 0, lvl_rb = 0, lvl_vb = 0;  // quantized level solve: bucket width (units), entry field bits
     uint16_t *d_lmem = nullptr;              // its per-workgroup scratch (lmem_cap u16)
@@ -500,6 +501,7 @@ struct LevelCtx {
     uint32_t q = 0, rb = 0, vb = 0;        // quantized solve: bucket width (units), remainder / vertex bits of an entry
     uint16_t *lmem = nullptr;              // quantized solve: level_scratch_bytes of per-workgroup scratch
     bool idn = false;                      // nodes[j] = j, n = V, n % 4 == 0: the vectorised row output
+    unsigned long long *row_ctr = nullptr; // level solve: {next row, workgroups done}, 0 between launches (nullable: rows dealt statically)
 };
 LevelCtx level_ctx(srt_plan *p);
 // the class CSRs of a level plan at its bound (the run's first step)

@@ -1651,9 +1651,10 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
     const float *__restrict__ sl_loss, uint64_t *__restrict__ out_lat, float *__restrict__ out_loss,
     unsigned long long *stats, const uint32_t *__restrict__ row_list, void *__restrict__ out32,
     float *__restrict__ out32_loss, bool stage16, uint32_t *__restrict__ probe,
-    unsigned long long *__restrict__ visit_cnt, bool idn) {
+    unsigned long long *__restrict__ visit_cnt, bool idn, unsigned long long *row_ctr) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ unsigned long long red_min[16], red_cnt[16], red_vis[16];
+    __shared__ uint32_t dyn_k;
     __shared__ uint32_t red_max[16];
     constexpr uint32_t WCN = CLSN - 1;
     __shared__ uint32_t plan_end[WCN + 1];
@@ -1675,7 +1676,21 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
     uint64_t mn = ~0ull;
     unsigned long long unreach = 0, visits = 0;
     const uint32_t nrows = row_list ? row1 : row1 - row0;
-    for (uint32_t k = blockIdx.x; k < nrows; k += gridDim.x) {
+    // rows dealt by a counter (row_ctr != nullptr; else statically, row k to
+    // workgroup k mod grid): a workgroup takes its next row one row ahead (the
+    // atomic's latency behind the row's work), so a CU whose rows ran long
+    // takes fewer; every workgroup makes exactly one fetch past the last row
+    unsigned long long kn = 0;
+    auto fetch = [&]() -> uint32_t {
+        if (tid == 0) dyn_k = (uint32_t)(kn < nrows ? kn : nrows);
+        __syncthreads();
+        return dyn_k;
+    };
+    if (row_ctr && tid == 0) kn = atomicAdd(&row_ctr[0], 1ull);
+    uint32_t k0 = blockIdx.x;
+    if (row_ctr) k0 = fetch();
+    for (uint32_t k = k0; k < nrows; k = row_ctr ? fetch() : k + gridDim.x) {
+        if (row_ctr && tid == 0) kn = atomicAdd(&row_ctr[0], 1ull);  // the next row
         const uint32_t i = row_list ? row_list[k] : row0 + k;
         const uint32_t s = nodes[i];
 #if LOSS_COUNT
@@ -2155,6 +2170,12 @@ __global__ __launch_bounds__(LOSS_NT) void level_solve_kernel(
             atomicMin(&stats[0], m);
             if (c) atomicAdd(&stats[1], c);
             if (visit_cnt && vz) atomicAdd(visit_cnt, vz);
+        }
+        // the last workgroup done (every fetch made) returns the counter to 0
+        // for the next launch (memory-side atomics; the launch boundary orders it)
+        if (row_ctr && atomicAdd(&row_ctr[1], 1ull) == gridDim.x - 1ull) {
+            atomicExch(&row_ctr[0], 0ull);
+            atomicExch(&row_ctr[1], 0ull);
         }
     }
 }
@@ -3227,6 +3248,17 @@ LevelCtx level_ctx(srt_plan *p) {
     c.vb = p->lvl_vb;
     c.lmem = p->d_lmem;
     c.idn = p->ident_nodes && p->n == p->V && p->n % 4 == 0;
+    // rows dealt by a counter (knob SRT_LVL_DYN=0: statically, A/B)
+    static const bool dyn = !(std::getenv("SRT_LVL_DYN") && std::atoi(std::getenv("SRT_LVL_DYN")) == 0);
+    if (dyn && !p->d_rowctr) {
+        if (hipMalloc(&p->d_rowctr, 2 * sizeof(unsigned long long)) != hipSuccess ||
+            hipMemsetAsync(p->d_rowctr, 0, 2 * sizeof(unsigned long long), p->stream) != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipFree(p->d_rowctr);
+            p->d_rowctr = nullptr;
+        }
+    }
+    c.row_ctr = dyn ? p->d_rowctr : nullptr;
     return c;
 }
 
@@ -3569,7 +3601,7 @@ void launch_solve_ctx(const LevelCtx &c, unsigned long long *d_stats, const uint
     hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), lds, c.stream, V, c.nodes, c.n, list ? 0u : r0, r1, co, ci, eo, ei,
                        lcap, c.g, c.sl_lat, c.sl_loss, c.out_lat, c.out_loss, d_stats, list,
                        stage_mode ? stage : nullptr, stage_mode ? stage_loss : nullptr, stage_mode == 1, probe,
-                       c.visits, c.idn);
+                       c.visits, c.idn, c.row_ctr);
 }
 
 // the per-workgroup scratch of the quantized solve (p->d_lmem): every
